@@ -1,0 +1,255 @@
+#!/usr/bin/env python3
+"""Headline benchmark: queries/sec @ top-1000 over a 10M x 768 bf16 corpus.
+
+BASELINE.json metric: "passages encoded/sec + queries/sec@top-1000, 10M x 768
+corpus, 1/2/4/8 GPU".  `value` is the search half (queries/sec@top-1000, the
+north-star path: brute-force Q.D^T + top-k, BaseFaissIPRetriever.search,
+DRT/evaluator/index.py:31-33); the encode half is reported beside it under
+"encode" when --encode is given (passages/sec of the bf16 BERT-base passage
+tower, DRModel.encode, DRT/model/biencoder.py:127-151).
+
+One step = one query batch (Qb = 128, the reference's eval batch,
+arguments.py:189) searched exactly against the WHOLE corpus (k = 1000):
+every rank scans its contiguous row shard (10M / N rows, resident in HBM),
+the per-shard top-k lists are all-gathered over RCCL and merged on device.
+The corpus is fixed as N grows ("scaling": "strong").
+
+Launch: python bench.py [--gpus N --steps K --warmup W]; for N > 1 under
+torch.distributed.run (one process per GPU, RCCL).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, REPO)
+
+HBM_PEAK_GBS = 8000.0      # MI355X HBM3E spec, MI355X_MICROARCH.md
+BF16_PEAK_TFLOPS = 2500.0  # dense bf16 MFMA spec
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--n-corpus", type=int, default=10_000_000)
+    ap.add_argument("--dim", type=int, default=768)
+    ap.add_argument("--qb", type=int, default=128)
+    ap.add_argument("--k", type=int, default=1000)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-rows", type=int, default=1_000_000)
+    ap.add_argument("--cpu-seconds", type=float, default=12.0)
+    ap.add_argument("--encode", action="store_true", help="also time the bf16 BERT-base passage encoder")
+    return ap.parse_args()
+
+
+def init_dist(n_gpus):
+    import torch
+    import torch.distributed as dist
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    return rank, world, local
+
+
+def gen_shard(n_total, world, rank, d, device):
+    """Seeded N(0,1) bf16 corpus rows of this rank's contiguous shard (generated in HBM)."""
+    import torch
+    per = -(-n_total // world)
+    lo = min(n_total, rank * per)
+    hi = min(n_total, lo + per)
+    g = torch.Generator(device=device)
+    g.manual_seed(1234 + rank)
+    shard = torch.empty((hi - lo, d), dtype=torch.bfloat16, device=device)
+    step = 1 << 20
+    for a in range(0, hi - lo, step):
+        b = min(hi - lo, a + step)
+        shard[a:b] = torch.randn((b - a, d), generator=g, device=device, dtype=torch.float32).to(torch.bfloat16)
+    return shard, lo, hi
+
+
+def cpu_baseline(args):
+    """Oracle (numpy, fp32 like faiss IndexFlatIP) on a bounded sample of the same workload."""
+    import numpy as np
+    from oracle.search_oracle import bf16_round, ip_topk
+    try:
+        from threadpoolctl import threadpool_info
+        cores = max([i.get("num_threads", 1) for i in threadpool_info() if i.get("user_api") == "blas"] or [1])
+    except Exception:
+        cores = os.cpu_count() or 1
+    rng = np.random.default_rng(99)
+    rows = args.cpu_rows
+    p = bf16_round(rng.standard_normal((rows, args.dim), dtype=np.float32))
+    q = bf16_round(rng.standard_normal((args.qb, args.dim), dtype=np.float32))
+    nb = 0
+    t0 = time.perf_counter()
+    while True:
+        ip_topk(q, p, args.k, chunk=rows, dtype=np.float32)
+        nb += 1
+        el = time.perf_counter() - t0
+        if el >= args.cpu_seconds or nb >= 50:
+            break
+    qps_sample = nb * args.qb / el
+    scale = rows / args.n_corpus
+    return {
+        "value": round(qps_sample * scale, 3),
+        "unit": "queries/s",
+        "cores": int(cores),
+        "kind": "port",
+        "sample": (f"oracle/search_oracle.ip_topk fp32 (numpy BLAS) on {nb} batches x {args.qb} queries "
+                   f"against a {rows}-row slice ({qps_sample:.1f} q/s), scaled by {rows}/{args.n_corpus} "
+                   f"to the full corpus; {el:.1f} s"),
+    }
+
+
+def encode_leg(args, device):
+    try:
+        from denseretrievaltoolkits_amd import bench_encode
+    except ImportError:
+        return None
+    return bench_encode.run(device)
+
+
+def main():
+    args = parse()
+    import torch
+    import torch.distributed as dist
+    rank, world, local = init_dist(args.gpus)
+    dev = torch.device("cuda", local)
+    from denseretrievaltoolkits_amd import _native, kernels
+
+    lib = _native.load()
+    d, k, qb = args.dim, args.k, args.qb
+    shard, lo, hi = gen_shard(args.n_corpus, world, rank, d, dev)
+    n_local = hi - lo
+    nsteps = args.warmup + args.steps
+    gq = torch.Generator(device=dev)
+    gq.manual_seed(5678)
+    queries = torch.randn((nsteps, qb, d), generator=gq, device=dev).to(torch.bfloat16)
+
+    s_loc = torch.empty((nsteps, qb, k), dtype=torch.float32, device=dev)
+    i_loc = torch.empty((nsteps, qb, k), dtype=torch.int64, device=dev)
+    st = torch.zeros((nsteps, qb), dtype=torch.int32, device=dev)
+    if world > 1:
+        s_all = torch.empty((world, qb, k), dtype=torch.float32, device=dev)
+        i_all = torch.empty((world, qb, k), dtype=torch.int64, device=dev)
+    results = []
+
+    def step(j):
+        kernels.ip_topk(queries[j], shard, k, id_offset=lo, resolve=False,
+                        out=(s_loc[j], i_loc[j]), status=st[j])
+        if world > 1:
+            dist.all_gather_into_tensor(s_all, s_loc[j])
+            dist.all_gather_into_tensor(i_all, i_loc[j])
+            return kernels.topk_merge(s_all, i_all, k)
+        return s_loc[j], i_loc[j]
+
+    def fix_failures(first, last):
+        """Exact resolve of any uncertified query (counted inside the timed region)."""
+        bad = (st[first:last] != 0).any(dim=1).to(torch.int32)
+        if world > 1:
+            dist.all_reduce(bad, op=dist.ReduceOp.MAX)
+        nb = 0
+        for j in (torch.nonzero(bad).flatten() + first).tolist():
+            nb += kernels.resolve_failed(queries[j], shard, k, lo, s_loc[j], i_loc[j], st[j])
+            step_merge_only = world > 1
+            if step_merge_only:
+                dist.all_gather_into_tensor(s_all, s_loc[j])
+                dist.all_gather_into_tensor(i_all, i_loc[j])
+                kernels.topk_merge(s_all, i_all, k)
+        return nb
+
+    for j in range(args.warmup):
+        step(j)
+    fix_failures(0, args.warmup)
+    torch.cuda.synchronize()
+
+    lib.drt_profile_enable(_native.PROF_SCAN, 1)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for j in range(args.warmup, nsteps):
+        step(j)
+    n_resolved = fix_failures(args.warmup, nsteps)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    t1 = time.perf_counter()
+    lib.drt_profile_enable(_native.PROF_SCAN, 0)
+    tot_ms = _native.ctypes.c_double(0.0)
+    cnt = _native.c_i64(0)
+    _native.check(lib.drt_profile_read(_native.PROF_SCAN, _native.ctypes.byref(tot_ms), _native.ctypes.byref(cnt)),
+                  "drt_profile_read")
+
+    elapsed = torch.tensor([t1 - t0], dtype=torch.float64, device=dev)
+    scan_ms = torch.tensor([tot_ms.value / max(1, cnt.value)], dtype=torch.float64, device=dev)
+    if world > 1:
+        dist.all_reduce(elapsed, op=dist.ReduceOp.MAX)
+        dist.all_reduce(scan_ms, op=dist.ReduceOp.MAX)
+    el = float(elapsed.item())
+    scan_ms_v = float(scan_ms.item())
+
+    out = None
+    if rank == 0:
+        qps = args.steps * qb / el
+        # algorithmic bytes of ONE filter-scan launch on the largest shard:
+        # corpus shard (per-row d*2 B) + query block + result lists
+        per = -(-args.n_corpus // world)
+        alg_bytes = per * d * 2 + qb * d * 2 + qb * k * 12
+        achieved = alg_bytes / (scan_ms_v * 1e-3) / 1e9
+        out = {
+            "metric": "queries/sec@top-1000, 10Mx768 corpus (BASELINE: passages encoded/sec + queries/sec@top-1000, 10Mx768 corpus, 1/2/4/8 GPU)",
+            "value": round(qps, 2),
+            "unit": "queries/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(el / args.steps * 1e3, 4),
+            "higher_is_better": True,
+            "scaling": "strong",
+            "vs_baseline": None,
+            "dtype": "bf16",
+            "data": "synthetic: N(0,1) corpus and queries rounded to bf16, generated in HBM (seeded)",
+            "config": {
+                "workload": f"exact IP top-{k}, {args.n_corpus} x {d} bf16 corpus row-sharded over {world} GPU(s), "
+                            f"query batch {qb}, RCCL all-gather of per-shard top-k + device merge",
+                "n_corpus": args.n_corpus, "dim": d, "query_batch": qb, "k": k,
+                "parallelism": f"row-shard x{world}",
+            },
+            "roofline": {
+                "kernel": "ip_scan_kernel<768,FILTER> (csrc/search.hip)",
+                "bound": "hbm",
+                "achieved": round(achieved, 1),
+                "peak": HBM_PEAK_GBS,
+                "unit": "GB/s",
+                "frac": round(achieved / HBM_PEAK_GBS, 4),
+                "traffic": None,
+                "avg_launch_ms": round(scan_ms_v, 4),
+                "launches": int(cnt.value),
+                "alg_bytes_per_launch": alg_bytes,
+            },
+            "uncertified_queries_resolved": int(n_resolved),
+        }
+        if world == 1 and not args.no_cpu_baseline:
+            out["cpu_baseline"] = cpu_baseline(args)
+        if args.encode:
+            enc = encode_leg(args, dev)
+            if enc is not None:
+                out["encode"] = enc
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,63 @@
+// Shared device/host helpers for the DRT MI355X (gfx950) kernels.
+//
+// Everything here is CDNA4-only: 64-lane waves, MFMA bf16 tiles, LDS-DMA
+// (global_load_lds) staging.  No CUDA shims, no dual paths.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "../../include/drt.h"
+
+namespace drt {
+
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+
+typedef __attribute__((address_space(3))) void lds_void;
+
+// ---------------------------------------------------------------------------
+// Order-preserving key for (score desc, row asc).
+//
+// faiss IndexFlatIP returns hits by descending inner product
+// (DRT/evaluator/index.py:31-33 re-sorts them with np.argsort(-scores)); the
+// reference leaves the order of equal scores unspecified, the build pins it to
+// ascending row/doc id.  `desc_key(s)` is a uint32 whose ASCENDING order is the
+// DESCENDING order of s; (desc_key << 32 | row) then sorts ascending exactly in
+// (score desc, row asc) order.  -0.0 is folded onto +0.0 first (numpy treats
+// them as equal).
+// ---------------------------------------------------------------------------
+__host__ __device__ __forceinline__ uint32_t desc_key(float s) {
+  s = s + 0.0f;
+  uint32_t u = __builtin_bit_cast(uint32_t, s);
+  uint32_t ord = (u & 0x80000000u) ? ~u : (u | 0x80000000u);  // ascending order
+  return ~ord;                                                 // descending order
+}
+
+__host__ __device__ __forceinline__ float desc_key_to_score(uint32_t k) {
+  uint32_t ord = ~k;
+  uint32_t u = (ord & 0x80000000u) ? (ord & 0x7FFFFFFFu) : ~ord;
+  return __builtin_bit_cast(float, u);
+}
+
+// faiss pads rows that have fewer than k results with label -1 and the
+// lowest float (CMin<float>::neutral() == numeric_limits<float>::lowest()).
+constexpr float kPadScore = -3.402823466e+38f;
+
+inline int hip_status(hipError_t e) { return e == hipSuccess ? DRT_OK : (int)e; }
+
+#define DRT_CHECK_HIP(expr)                  \
+  do {                                       \
+    hipError_t _e = (expr);                  \
+    if (_e != hipSuccess) return (int)_e;    \
+  } while (0)
+
+#define DRT_REQUIRE(cond)                    \
+  do {                                       \
+    if (!(cond)) return DRT_EINVAL;          \
+  } while (0)
+
+}  // namespace drt

@@ -1,0 +1,214 @@
+// NT GEMM on CDNA4 MFMA:  C[m, n] = sum_k A[m, k] * B[n, k]  (+ epilogue)
+//
+// Both operands are K-contiguous ("x @ W^T" with an nn.Linear weight [out, in],
+// and q_reps @ p_reps^T for the in-batch score matrix,
+// DRT/model/biencoder.py:107 / DRT/trainer/losses.py:16), so one kernel shape
+// serves the encoder projections and the training scores.
+//
+// Tile 128 x 128 x 64, 4 waves (2 x 2), each wave 64 x 64 = 2 x 2 tiles of
+// v_mfma_f32_32x32x16_bf16.  A and B tiles are staged global -> LDS with
+// global_load_lds_dwordx4 (inline asm, counted vmcnt), 2-slot ring, in the
+// same XOR-swizzled [row][8 x 16 B] image as the search scan so the
+// ds_read_b128 fragment reads are bank-conflict free.
+#include "drt_common.h"
+#include "profile.h"
+
+namespace drt {
+
+constexpr int kGemmThreads = 256;
+constexpr int kBM = 128, kBN = 128, kBK = 64;
+constexpr int kTileA = kBM * kBK * 2;  // 16 KiB
+constexpr int kTileB = kBN * kBK * 2;  // 16 KiB
+constexpr int kStage = kTileA + kTileB;
+constexpr int kGemmLds = 2 * kStage;   // 64 KiB -> 2 work-groups per CU
+
+struct GemmArgs {
+  const __bf16* A;   // [m][lda]
+  const __bf16* B;   // [n][ldb]
+  void* C;           // [m][ldc]  fp32 or bf16
+  const float* bias; // [n] or null
+  const __bf16* R;   // residual [m][ldr] or null
+  int64_t m, n, k;
+  int64_t lda, ldb, ldc, ldr;
+  float alpha;
+};
+
+__device__ __forceinline__ void g_glds16(const void* gsrc, uint32_t lds_addr) {
+  uint32_t keep;
+  asm volatile(
+      "s_mov_b32 %0, m0\n\t"
+      "s_mov_b32 m0, %2\n\t"
+      "s_nop 0\n\t"
+      "global_load_lds_dwordx4 %1, off\n\t"
+      "s_mov_b32 m0, %0"
+      : "=&s"(keep)
+      : "v"(gsrc), "s"(lds_addr)
+      : "memory");
+}
+
+__device__ __forceinline__ uint32_t g_lds_addr(const void* p) {
+  return (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) char*)p;
+}
+
+// Stage a 128-row x 64-col bf16 panel: 16 wave-instructions of 8 rows x 128 B,
+// 4 per wave.  Rows past `rows` are clamped (masked in the epilogue).
+__device__ __forceinline__ void stage_panel(const __bf16* base, int64_t ld, int64_t row0, int64_t rows,
+                                            int64_t k0, uint32_t lds, int wave, int lane) {
+  const int rsub = lane >> 3, pos = lane & 7;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int J = j * 4 + wave;           // 0..15
+    const int row = J * 8 + rsub;         // 0..127
+    int64_t gr = row0 + row;
+    gr = gr < rows ? gr : rows - 1;
+    const int c = pos ^ ((row >> 1) & 7);
+    g_glds16(base + gr * ld + k0 + c * 8, __builtin_amdgcn_readfirstlane(lds + J * 1024));
+  }
+}
+
+__device__ __forceinline__ float gelu_erf(float x) {
+  // transformers ACT2FN["gelu"] = GELUActivation: x * 0.5 * (1 + erf(x / sqrt(2)))
+  return 0.5f * x * (1.0f + erff(x * 0.70710678118654752f));
+}
+
+enum { EPI_NONE = 0, EPI_BIAS = 1, EPI_GELU = 2, EPI_RESID = 4 };
+
+template <bool OUT_BF16, int EPI>
+__global__ __launch_bounds__(kGemmThreads, 2) void gemm_nt_kernel(GemmArgs a) {
+  __shared__ __attribute__((aligned(16))) char smem[kGemmLds];
+  const int tid = threadIdx.x;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int lane = tid & 63;
+  const int r = lane & 31, h = lane >> 5;
+  const int wm = wave >> 1, wn = wave & 1;
+
+  // XCD-aware bijective remap: blocks b and b+8 share an XCD (and its L2),
+  // so give each XCD a contiguous run of tiles along n (shared A panel).
+  const int nwg = gridDim.x;
+  const int bid = blockIdx.x;
+  const int xcd = bid & 7, q8 = nwg >> 3, r8 = nwg & 7;
+  const int wg = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (bid >> 3);
+  const int tiles_n = (int)((a.n + kBN - 1) / kBN);
+  const int64_t m0 = (int64_t)(wg / tiles_n) * kBM;
+  const int64_t n0 = (int64_t)(wg % tiles_n) * kBN;
+
+  const uint32_t lds0 = g_lds_addr(smem);
+  const int ksteps = (int)(a.k / kBK);
+
+  f32x16 acc[2][2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int e = 0; e < 16; ++e) acc[i][j][e] = 0.0f;
+
+  const int sw = (r >> 1) & 7;
+  int aoff[4];
+#pragma unroll
+  for (int s = 0; s < 4; ++s) aoff[s] = r * 128 + ((((2 * s) | h) ^ sw) << 4);
+
+  stage_panel(a.A, a.lda, m0, a.m, 0, lds0, wave, lane);
+  stage_panel(a.B, a.ldb, n0, a.n, 0, lds0 + kTileA, wave, lane);
+
+  for (int kt = 0; kt < ksteps; ++kt) {
+    const int slot = kt & 1;
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    if (kt + 1 < ksteps) {
+      const uint32_t nb = lds0 + (slot ^ 1) * kStage;
+      stage_panel(a.A, a.lda, m0, a.m, (int64_t)(kt + 1) * kBK, nb, wave, lane);
+      stage_panel(a.B, a.ldb, n0, a.n, (int64_t)(kt + 1) * kBK, nb + kTileA, wave, lane);
+    }
+    const char* As = smem + slot * kStage + wm * 64 * 128;
+    const char* Bs = smem + slot * kStage + kTileA + wn * 64 * 128;
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+      bf16x8 af[2], bfr[2];
+#pragma unroll
+      for (int i = 0; i < 2; ++i) af[i] = *(const bf16x8*)(As + i * 32 * 128 + aoff[s]);
+#pragma unroll
+      for (int j = 0; j < 2; ++j) bfr[j] = *(const bf16x8*)(Bs + j * 32 * 128 + aoff[s]);
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+    }
+  }
+
+  // Epilogue.  acc[i][j][e]: row m0 + wm*64 + i*32 + (e&3) + 8*(e>>2) + 4*h,
+  //                          col n0 + wn*64 + j*32 + r.
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    const int64_t col = n0 + wn * 64 + j * 32 + r;
+    if (col >= a.n) continue;
+    float bv = 0.0f;
+    if (EPI & EPI_BIAS) bv = a.bias[col];
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+#pragma unroll
+      for (int e = 0; e < 16; ++e) {
+        const int64_t row = m0 + wm * 64 + i * 32 + (e & 3) + 8 * (e >> 2) + 4 * h;
+        if (row >= a.m) continue;
+        float v = acc[i][j][e] * a.alpha + bv;
+        if (EPI & EPI_GELU) v = gelu_erf(v);
+        if (EPI & EPI_RESID) v += (float)a.R[row * a.ldr + col];
+        if (OUT_BF16) ((__bf16*)a.C)[row * a.ldc + col] = (__bf16)v;
+        else ((float*)a.C)[row * a.ldc + col] = v;
+      }
+    }
+  }
+}
+
+template <bool OUT_BF16, int EPI>
+static int launch_gemm_t(const GemmArgs& a, hipStream_t s) {
+  const int64_t tiles = ((a.m + kBM - 1) / kBM) * ((a.n + kBN - 1) / kBN);
+  const ProfPair pp = prof_begin(PROF_GEMM, s);
+  hipLaunchKernelGGL((gemm_nt_kernel<OUT_BF16, EPI>), dim3((unsigned)tiles), dim3(kGemmThreads), 0, s, a);
+  prof_end(pp, s);
+  return hip_status(hipGetLastError());
+}
+
+int launch_gemm(const GemmArgs& a, bool out_bf16, int epi, hipStream_t s) {
+  if (a.m == 0 || a.n == 0) return DRT_OK;
+  if (a.k <= 0 || a.k % kBK != 0) return DRT_EINVAL;
+  if (!out_bf16) {
+    switch (epi) {
+      case EPI_NONE: return launch_gemm_t<false, EPI_NONE>(a, s);
+      case EPI_BIAS: return launch_gemm_t<false, EPI_BIAS>(a, s);
+      default: return DRT_EINVAL;
+    }
+  }
+  switch (epi) {
+    case EPI_NONE: return launch_gemm_t<true, EPI_NONE>(a, s);
+    case EPI_BIAS: return launch_gemm_t<true, EPI_BIAS>(a, s);
+    case EPI_BIAS | EPI_GELU: return launch_gemm_t<true, EPI_BIAS | EPI_GELU>(a, s);
+    case EPI_BIAS | EPI_RESID: return launch_gemm_t<true, EPI_BIAS | EPI_RESID>(a, s);
+    default: return DRT_EINVAL;
+  }
+}
+
+}  // namespace drt
+
+using namespace drt;
+
+extern "C" int drt_gemm_nt_bf16_f32(const void* A, const void* B, float* C, int64_t m, int64_t n, int32_t d,
+                                    int64_t ldc, void* stream) {
+  DRT_REQUIRE(m >= 0 && n >= 0 && d > 0 && d % 64 == 0 && ldc >= n);
+  if (m == 0 || n == 0) return DRT_OK;
+  DRT_REQUIRE(A && B && C);
+  GemmArgs a{};
+  a.A = (const __bf16*)A;
+  a.B = (const __bf16*)B;
+  a.C = C;
+  a.m = m;
+  a.n = n;
+  a.k = d;
+  a.lda = d;
+  a.ldb = d;
+  a.ldc = ldc;
+  a.alpha = 1.0f;
+  return launch_gemm(a, false, EPI_NONE, (hipStream_t)stream);
+}

@@ -1,0 +1,907 @@
+// Brute-force inner-product top-k over a device-resident corpus shard.
+//
+// Replaces faiss.IndexFlatIP.search as called by
+// BaseFaissIPRetriever.search (DRT/evaluator/index.py:31-33) and the
+// filesystem shard exchange of Trainer._index_corpus/_load_index
+// (DRT/trainer/trainer.py:220-262).  Algorithm:
+//
+//   1. sample pass   ip_scan<DENSE> over a strided sample of M shard rows,
+//                    select<DENSE32,KTH> -> per-query threshold tau_q = r-th
+//                    largest sampled score (a lower bound of the k-th score
+//                    with probability 1 - 1e-9; certified in step 4).
+//   2. filter pass   ip_scan<FILTER> streams every shard row once from HBM
+//                    through LDS (global_load_lds, 3-deep ring), computes the
+//                    128-query x 32-row score tile with v_mfma_f32_32x32x16_bf16
+//                    (queries resident in VGPRs for the whole launch) and
+//                    appends (score, row) keys >= tau_q to a per-query list.
+//   3. select        select<KEYS64,TOPK> per query: MSD radix select on the
+//                    64-bit key (score desc, row asc) + LDS bitonic sort.
+//   4. certify       count_q >= k (or == n) and count_q <= cap  <=> exact.
+//                    Otherwise status[q] = 1 and drt_ip_topk_resolve rescans
+//                    that query densely (exact by construction).
+#include <algorithm>
+#include <cmath>
+#include <vector>
+
+#include "drt_common.h"
+#include "profile.h"
+
+namespace drt {
+
+constexpr int kTileRows = 32;   // corpus rows per MFMA tile (32x32x16)
+constexpr int kScanThreads = 256;  // 4 waves, one per SIMD
+constexpr int kQueriesPerWG = 128;  // 4 waves x 32 query columns
+constexpr int kHitCap = 1024;       // LDS hit list entries per work-group
+
+enum { SCAN_FILTER = 0, SCAN_DENSE = 1 };
+
+struct ScanArgs {
+  const __bf16* Q;
+  int64_t nq;
+  int64_t ldq;
+  const __bf16* P;
+  int64_t ldp;      // elements between consecutive corpus rows
+  int64_t row0;     // logical row i lives at P row (row0 + i * rstride)
+  int64_t nrows;
+  int64_t rstride;
+  const float* tau;   // FILTER: [nq] thresholds (NaN = inactive query)
+  uint32_t* counts;   // FILTER: [nq] hit counters (zeroed by the caller)
+  void* out;          // FILTER: u64 [nq][cap] keys; DENSE: u32 [nq][cap] desc keys
+  int64_t cap;
+};
+
+template <int D>
+struct ScanCfg {
+  static_assert(D % 64 == 0 && D <= 1024, "d must be a multiple of 64, <= 1024");
+  static constexpr int KS = D / 16;                         // MFMA k-steps
+  static constexpr int TILE_BYTES = kTileRows * D * 2;      // one 32-row tile
+  static constexpr int GLDS_PER_TILE = TILE_BYTES / 1024;   // 1 KiB per wave-instr
+  static constexpr int GLDS_PER_WAVE = GLDS_PER_TILE / 4;
+  static constexpr int NBUF = (3 * TILE_BYTES + 16 * 1024 <= 160 * 1024) ? 3 : 2;
+  static constexpr int PD = NBUF - 1;  // prefetch distance in tiles
+  static constexpr int RING_BYTES = NBUF * TILE_BYTES;
+  static constexpr int HIT_KEY_OFF = RING_BYTES;
+  static constexpr int HIT_Q_OFF = HIT_KEY_OFF + kHitCap * 8;
+  static constexpr int HIT_N_OFF = HIT_Q_OFF + kHitCap * 2;
+  static constexpr int LDS_BYTES = HIT_N_OFF + 16;
+  static_assert(LDS_BYTES <= 160 * 1024, "LDS budget");
+};
+
+// LDS-DMA of 16 B per lane.  Issued through inline asm on purpose: with the
+// builtin, hipcc cannot prove the ring slots disjoint and waits vmcnt(0)
+// before the first ds_read of every tile, which drains the prefetch ring.
+// The asm form is invisible to hipcc's counters, so the kernel counts its
+// own LDS-DMA with s_waitcnt vmcnt(N) (cdna_hip_programming.md §5.7 item 1).
+__device__ __forceinline__ void glds16(const void* gsrc, uint32_t lds_addr) {
+  uint32_t keep;
+  asm volatile(
+      "s_mov_b32 %0, m0\n\t"
+      "s_mov_b32 m0, %2\n\t"
+      "s_nop 0\n\t"
+      "global_load_lds_dwordx4 %1, off\n\t"
+      "s_mov_b32 m0, %0"
+      : "=&s"(keep)
+      : "v"(gsrc), "s"(lds_addr)
+      : "memory");
+}
+
+__device__ __forceinline__ uint32_t lds_addr_of(const void* p) {
+  return (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) char*)p;
+}
+
+// LDS image of one tile: [chunk-group g (128 B of every row)][row 0..31][8 x 16 B]
+// with the 16-B chunk position XOR-swizzled by (row >> 1) & 7 so that the
+// MFMA A-fragment reads (ds_read_b128, 32 rows x same chunk) are
+// bank-conflict free.  One global_load_lds_dwordx4 wave-instruction fills
+// 8 rows x 128 B (coalesced 128-B row segments).
+template <int D>
+__device__ __forceinline__ void issue_tile(const ScanArgs& a, uint32_t buf_lds, int64_t tile, int wave,
+                                           int lane) {
+  using C = ScanCfg<D>;
+  const int rsub = lane >> 3;    // row within the 8-row group
+  const int pos = lane & 7;      // LDS chunk slot
+#pragma unroll
+  for (int j = 0; j < C::GLDS_PER_WAVE; ++j) {
+    const int J = j * 4 + wave;            // wave-instruction index in the tile
+    const int g = J >> 2;                  // chunk group
+    const int row = ((J & 3) << 3) + rsub;  // tile row 0..31
+    int64_t li = tile * kTileRows + row;
+    li = li < a.nrows ? li : a.nrows - 1;  // clamp: tail rows are masked later
+    const int c = pos ^ ((row >> 1) & 7);
+    const __bf16* src = a.P + (a.row0 + li * a.rstride) * a.ldp + g * 64 + c * 8;
+    glds16(src, __builtin_amdgcn_readfirstlane(buf_lds + J * 1024));  // wave-uniform base
+  }
+}
+
+template <int N>
+__device__ __forceinline__ void wait_vmcnt() {
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+
+__device__ __forceinline__ void lds_barrier() {
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+}
+
+// Push one filtered hit: LDS list first, direct global append when full.
+__device__ __forceinline__ void push_hit(const ScanArgs& a, int q_local,
+                                         int64_t q, uint64_t key, uint32_t* hit_n,
+                                         uint64_t* hk, uint16_t* hq) {
+  const uint32_t p = atomicAdd(hit_n, 1u);
+  if (p < (uint32_t)kHitCap) {
+    hk[p] = key;
+    hq[p] = (uint16_t)q_local;
+  } else {
+    const uint32_t g = atomicAdd(a.counts + q, 1u);
+    if (g < (uint64_t)a.cap) ((uint64_t*)a.out)[q * a.cap + g] = key;
+  }
+}
+
+__device__ __forceinline__ void flush_hits(const ScanArgs& a, int64_t qbase, uint32_t n,
+                                           const uint64_t* hk, const uint16_t* hq) {
+  n = n < (uint32_t)kHitCap ? n : (uint32_t)kHitCap;
+  for (uint32_t i = threadIdx.x; i < n; i += kScanThreads) {
+    const int64_t q = qbase + hq[i];
+    const uint32_t g = atomicAdd(a.counts + q, 1u);
+    if (g < (uint64_t)a.cap) ((uint64_t*)a.out)[q * a.cap + g] = hk[i];
+  }
+}
+
+template <int D, int MODE>
+__global__ __launch_bounds__(kScanThreads, 1) void ip_scan_kernel(ScanArgs a) {
+  using C = ScanCfg<D>;
+  __shared__ __attribute__((aligned(16))) char smem[C::LDS_BYTES];
+  uint64_t* hk = (uint64_t*)(smem + C::HIT_KEY_OFF);
+  uint16_t* hq = (uint16_t*)(smem + C::HIT_Q_OFF);
+  uint32_t* hit_n = (uint32_t*)(smem + C::HIT_N_OFF);
+
+  const int tid = threadIdx.x;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int lane = tid & 63;
+  const int r = lane & 31;   // MFMA column (query) / A-row (corpus row)
+  const int h = lane >> 5;   // k-half
+
+  const int64_t qbase = (int64_t)blockIdx.y * kQueriesPerWG;
+  const int q_local = wave * 32 + r;
+  const int64_t q = qbase + q_local;
+  const bool q_ok = q < a.nq;
+
+  const int64_t ntiles = (a.nrows + kTileRows - 1) / kTileRows;
+  const int64_t t0 = blockIdx.x;
+  const int64_t tstep = gridDim.x;
+  const int64_t my_tiles = t0 < ntiles ? (ntiles - 1 - t0) / tstep + 1 : 0;
+  if (my_tiles == 0) return;  // uniform per work-group
+
+  if (MODE == SCAN_FILTER && tid == 0) *hit_n = 0;
+
+  const uint32_t ring = lds_addr_of(smem);
+
+  // Query fragments stay in VGPRs for the whole launch: B[k][col] = Q[col][k].
+  // Loaded before the ring is primed so hipcc's own vmcnt waits for them do
+  // not drain LDS-DMA.  Out-of-range query columns load row 0 and are zeroed.
+  const int64_t qs = q_ok ? q : 0;
+  bf16x8 qf[C::KS];
+#pragma unroll
+  for (int s = 0; s < C::KS; ++s) qf[s] = *(const bf16x8*)(a.Q + qs * a.ldq + s * 16 + h * 8);
+  float tau = __builtin_nanf("");
+  if (MODE == SCAN_FILTER) {
+    const float tv = a.tau[qs];
+    tau = q_ok ? tv : tau;
+  }
+  if (!q_ok) {
+#pragma unroll
+    for (int s = 0; s < C::KS; ++s) qf[s] = (bf16x8){};
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+
+  // Prologue: PD tiles in flight.
+  issue_tile<D>(a, ring, t0, wave, lane);
+  if (C::PD > 1 && my_tiles > 1) issue_tile<D>(a, ring + C::TILE_BYTES, t0 + tstep, wave, lane);
+
+  // Per-lane swizzled A-fragment offsets inside one chunk group (4 distinct
+  // even chunk ids per group; chunk = 2s + h).
+  const int sw = (r >> 1) & 7;
+  int aoff[4];
+#pragma unroll
+  for (int m = 0; m < 4; ++m) aoff[m] = r * 128 + ((((2 * m) | h) ^ sw) << 4);
+
+  int buf = 0;                    // ring slot of tile `it`
+  int nbuf2 = C::PD;               // ring slot of tile `it + PD` (== slot of it - 1)
+  for (int64_t it = 0; it < my_tiles; ++it) {
+    const int64_t tile = t0 + it * tstep;
+    // Tile `it` landed (this wave's share); with PD = 2 tile it+1 may stay
+    // in flight.  Only LDS-DMA is outstanding here in FILTER mode; DENSE
+    // stores are younger and only make the wait stricter.
+    if (C::PD > 1 && it + 1 < my_tiles) wait_vmcnt<C::GLDS_PER_WAVE>();
+    else wait_vmcnt<0>();
+    lds_barrier();  // every wave's share landed; tile it-1 fully consumed
+
+    if (MODE == SCAN_FILTER) {
+      const uint32_t n = *hit_n;
+      if (n >= (uint32_t)(kHitCap / 2)) {
+        flush_hits(a, qbase, n, hk, hq);
+        lds_barrier();
+        if (tid == 0) *hit_n = 0;
+        lds_barrier();
+      }
+    }
+
+    if (it + C::PD < my_tiles)
+      issue_tile<D>(a, ring + nbuf2 * C::TILE_BYTES, tile + C::PD * tstep, wave, lane);
+
+    const char* tb = smem + buf * C::TILE_BYTES;
+    f32x16 acc;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) acc[i] = 0.0f;
+#pragma unroll
+    for (int s = 0; s < C::KS; ++s) {
+      const bf16x8 af = *(const bf16x8*)(tb + (s >> 2) * (kTileRows * 128) + aoff[s & 3]);
+      acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af, qf[s], acc, 0, 0, 0);
+    }
+
+    // acc[i]: query column r, corpus row (i&3) + 8*(i>>2) + 4*h of the tile.
+    const int64_t rowbase = tile * kTileRows + 4 * h;
+    if (MODE == SCAN_FILTER) {
+      float mx = acc[0];
+#pragma unroll
+      for (int i = 1; i < 16; ++i) mx = fmaxf(mx, acc[i]);
+      if (__ballot(mx >= tau) != 0ull) {
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+          const int64_t row = rowbase + (i & 3) + 8 * (i >> 2);
+          if (acc[i] >= tau && row < a.nrows) {
+            const uint64_t key = ((uint64_t)desc_key(acc[i]) << 32) | (uint64_t)(uint32_t)row;
+            push_hit(a, q_local, q, key, hit_n, hk, hq);
+          }
+        }
+      }
+    } else {
+      if (q_ok) {
+        uint32_t* o = (uint32_t*)a.out + q * a.cap;
+#pragma unroll
+        for (int m = 0; m < 4; ++m) {
+          const int64_t row = rowbase + 8 * m;
+          u32x4 v;
+          v[0] = desc_key(acc[4 * m + 0]);
+          v[1] = desc_key(acc[4 * m + 1]);
+          v[2] = desc_key(acc[4 * m + 2]);
+          v[3] = desc_key(acc[4 * m + 3]);
+          if (row + 3 < a.nrows) {
+            *(u32x4*)(o + row) = v;
+          } else {
+#pragma unroll
+            for (int j = 0; j < 4; ++j)
+              if (row + j < a.nrows) o[row + j] = v[j];
+          }
+        }
+      }
+    }
+    buf = (buf + 1 == C::NBUF) ? 0 : buf + 1;
+    nbuf2 = (nbuf2 + 1 == C::NBUF) ? 0 : nbuf2 + 1;
+  }
+
+  if (MODE == SCAN_FILTER) {
+    lds_barrier();
+    flush_hits(a, qbase, *hit_n, hk, hq);
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Per-query selection: MSD radix select on 64-bit keys + LDS bitonic sort.
+// ---------------------------------------------------------------------------
+enum { SEL_KEYS64 = 0, SEL_DENSE32 = 1 };
+enum { SEL_TOPK = 0, SEL_KTH = 1 };
+constexpr int kSelThreads = 512;
+constexpr int kSelMaxK = 2048;
+
+struct SelectArgs {
+  const void* in;
+  int64_t in_stride;        // elements per query row of `in`
+  const uint32_t* counts;   // KEYS64: [nq] hit counts; DENSE32: nullptr
+  int64_t n_in;             // DENSE32: valid entries per query
+  int64_t cap;              // KEYS64: capacity per query
+  int64_t n_total;          // rows the counts were taken over (certification)
+  int k;
+  int64_t nq;
+  // TOPK output
+  float* out_scores;
+  int64_t* out_ids;
+  int64_t ldo;
+  int64_t id_offset;
+  int32_t* status;          // may be null
+  const int32_t* qmap;      // optional: output row for block q (resolve path)
+  // KTH output
+  float* tau;
+};
+
+template <int INPUT>
+__device__ __forceinline__ uint64_t sel_load(const SelectArgs& a, int64_t q, int64_t j) {
+  if (INPUT == SEL_KEYS64) return ((const uint64_t*)a.in)[q * a.in_stride + j];
+  const uint32_t v = ((const uint32_t*)a.in)[q * a.in_stride + j];
+  return ((uint64_t)v << 32) | (uint64_t)(uint32_t)j;
+}
+
+template <int INPUT, int OUTPUT>
+__global__ __launch_bounds__(kSelThreads) void select_kernel(SelectArgs a) {
+  __shared__ uint32_t hist[256];
+  __shared__ uint64_t sh_prefix, sh_mask;
+  __shared__ int64_t sh_kk;
+  __shared__ int sh_done;
+  __shared__ uint32_t sh_nsel;
+  __shared__ __attribute__((aligned(16))) uint64_t buf[kSelMaxK];
+
+  const int tid = threadIdx.x;
+  const int64_t q = blockIdx.x;
+  int64_t c_raw, c;
+  if (INPUT == SEL_KEYS64) {
+    c_raw = a.counts[q];
+    c = c_raw < a.cap ? c_raw : a.cap;
+  } else {
+    c_raw = a.n_in;
+    c = a.n_in;
+  }
+  const int64_t kk_total = (int64_t)a.k < c ? (int64_t)a.k : c;
+
+  if (tid == 0) {
+    sh_prefix = 0;
+    sh_mask = 0;
+    sh_kk = kk_total;
+    sh_done = (c <= (int64_t)a.k) ? 1 : 0;  // everything selected
+    if (c <= (int64_t)a.k) {
+      sh_prefix = ~0ull;
+      sh_mask = ~0ull;
+    }
+  }
+  __syncthreads();
+
+  const int last_shift = (OUTPUT == SEL_KTH) ? 32 : 0;
+  for (int shift = 56; shift >= last_shift && !sh_done; shift -= 8) {
+    for (int i = tid; i < 256; i += kSelThreads) hist[i] = 0;
+    __syncthreads();
+    const uint64_t prefix = sh_prefix, mask = sh_mask;
+    for (int64_t j = tid; j < c; j += kSelThreads) {
+      const uint64_t x = sel_load<INPUT>(a, q, j);
+      if ((x & mask) == prefix) atomicAdd(&hist[(x >> shift) & 255], 1u);
+    }
+    __syncthreads();
+    if (tid < 64) {
+      // lane owns bins 4*lane .. 4*lane+3
+      const uint32_t b0 = hist[4 * tid], b1 = hist[4 * tid + 1], b2 = hist[4 * tid + 2],
+                     b3 = hist[4 * tid + 3];
+      const uint32_t s4 = b0 + b1 + b2 + b3;
+      uint32_t incl = s4;
+#pragma unroll
+      for (int o = 1; o < 64; o <<= 1) {
+        const uint32_t v = __shfl_up(incl, o, 64);
+        if (tid >= o) incl += v;
+      }
+      const uint32_t excl = incl - s4;
+      const int64_t kk = sh_kk;
+      // the lane whose range [excl, incl) contains rank kk-1
+      if ((int64_t)excl < kk && kk <= (int64_t)incl) {
+        uint32_t run = excl;
+        const uint32_t bb[4] = {b0, b1, b2, b3};
+        int d = 0;
+        uint32_t cnt = 0;
+#pragma unroll
+        for (int t = 0; t < 4; ++t) {
+          if ((int64_t)(run + bb[t]) >= kk) {
+            d = 4 * tid + t;
+            cnt = bb[t];
+            break;
+          }
+          run += bb[t];
+        }
+        const int64_t rem = kk - run;
+        sh_prefix = prefix | ((uint64_t)d << shift);
+        sh_mask = mask | (255ull << shift);
+        sh_kk = rem;
+        if ((int64_t)cnt == rem && OUTPUT == SEL_TOPK) sh_done = 1;  // whole bucket selected
+      }
+    }
+    __syncthreads();
+  }
+
+  if (OUTPUT == SEL_KTH) {
+    if (tid == 0) {
+      float t;
+      if (c < (int64_t)a.k || c == 0) t = -__builtin_inff();  // too few samples: keep all
+      else t = desc_key_to_score((uint32_t)(sh_prefix >> 32));
+      a.tau[q] = t;
+    }
+    return;
+  }
+
+  // threshold: select every key whose masked value <= prefix
+  const uint64_t thr = sh_prefix | ~sh_mask;
+  if (tid == 0) sh_nsel = 0;
+  __syncthreads();
+  for (int64_t j = tid; j < c; j += kSelThreads) {
+    const uint64_t x = sel_load<INPUT>(a, q, j);
+    if (x <= thr) {
+      const uint32_t p = atomicAdd(&sh_nsel, 1u);
+      if (p < (uint32_t)kSelMaxK) buf[p] = x;
+    }
+  }
+  __syncthreads();
+  int n2 = 1;
+  while (n2 < (int)kk_total) n2 <<= 1;
+  const int nsel = (int)(sh_nsel < (uint32_t)kSelMaxK ? sh_nsel : kSelMaxK);
+  for (int i = nsel + tid; i < n2; i += kSelThreads) buf[i] = ~0ull;
+  __syncthreads();
+  // bitonic sort ascending of buf[0..n2)
+  for (int size = 2; size <= n2; size <<= 1) {
+    for (int stride = size >> 1; stride > 0; stride >>= 1) {
+      for (int i = tid; i < n2 / 2; i += kSelThreads) {
+        const int lo = 2 * i - (i & (stride - 1));
+        const int hi = lo + stride;
+        const bool up = ((lo & size) == 0);
+        const uint64_t x = buf[lo], y = buf[hi];
+        if ((x > y) == up) {
+          buf[lo] = y;
+          buf[hi] = x;
+        }
+      }
+      __syncthreads();
+    }
+  }
+  const int64_t orow = a.qmap ? (int64_t)a.qmap[q] : q;
+  float* os = a.out_scores + orow * a.ldo;
+  int64_t* oi = a.out_ids + orow * a.ldo;
+  for (int j = tid; j < a.k; j += kSelThreads) {
+    if (j < kk_total) {
+      const uint64_t x = buf[j];
+      os[j] = desc_key_to_score((uint32_t)(x >> 32));
+      oi[j] = a.id_offset + (int64_t)(x & 0xFFFFFFFFull);
+    } else {
+      os[j] = kPadScore;
+      oi[j] = -1;
+    }
+  }
+  if (a.status && tid == 0) {
+    int st = 0;
+    if (INPUT == SEL_KEYS64) {
+      if (c_raw > a.cap) st = 1;                                     // overflow
+      if (c_raw < (int64_t)a.k && c_raw < a.n_total) st = 1;          // threshold too high
+    }
+    a.status[orow] = st;
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Merge of per-shard sorted top-k lists (RCCL all-gather output).
+// Pairwise merge by rank: element i of A lands at i + #{B < A[i]},
+// element j of B at j + #{A <= B[j]} (total order: score desc, id asc).
+// ---------------------------------------------------------------------------
+struct MergeEnt {
+  uint32_t key;  // desc_key(score)
+  int64_t id;
+};
+
+__device__ __forceinline__ bool ent_less(uint32_t ka, int64_t ia, uint32_t kb, int64_t ib) {
+  return ka < kb || (ka == kb && ia < ib);
+}
+
+constexpr int kMergeThreads = 512;
+
+__global__ __launch_bounds__(kMergeThreads) void merge_kernel(const float* scores, const int64_t* ids,
+                                                              int64_t nq, int nparts, int k_in,
+                                                              int k_out, float* out_s, int64_t* out_i) {
+  __shared__ uint32_t ka[kSelMaxK], kb[kSelMaxK], kc[kSelMaxK];
+  __shared__ int64_t ia[kSelMaxK], ib[kSelMaxK], ic[kSelMaxK];
+  const int tid = threadIdx.x;
+  const int64_t q = blockIdx.x;
+  // running list A holds up to min(k_out, seen) entries
+  int na = k_in < k_out ? k_in : k_out;
+  for (int i = tid; i < na; i += kMergeThreads) {
+    const int64_t o = (0 * nq + q) * k_in + i;
+    ka[i] = desc_key(scores[o]);
+    ia[i] = ids[o];
+  }
+  __syncthreads();
+  for (int p = 1; p < nparts; ++p) {
+    const int nb = k_in < k_out ? k_in : k_out;
+    for (int i = tid; i < nb; i += kMergeThreads) {
+      const int64_t o = ((int64_t)p * nq + q) * k_in + i;
+      kb[i] = desc_key(scores[o]);
+      ib[i] = ids[o];
+    }
+    __syncthreads();
+    const int nc = (na + nb) < k_out ? (na + nb) : k_out;
+    for (int i = tid; i < na; i += kMergeThreads) {
+      // #B strictly less than A[i]
+      int lo = 0, hi = nb;
+      while (lo < hi) {
+        const int mid = (lo + hi) >> 1;
+        if (ent_less(kb[mid], ib[mid], ka[i], ia[i])) lo = mid + 1;
+        else hi = mid;
+      }
+      const int rk = i + lo;
+      if (rk < nc) {
+        kc[rk] = ka[i];
+        ic[rk] = ia[i];
+      }
+    }
+    for (int j = tid; j < nb; j += kMergeThreads) {
+      // #A less than or equal to B[j]
+      int lo = 0, hi = na;
+      while (lo < hi) {
+        const int mid = (lo + hi) >> 1;
+        if (!ent_less(kb[j], ib[j], ka[mid], ia[mid])) lo = mid + 1;
+        else hi = mid;
+      }
+      const int rk = j + lo;
+      if (rk < nc) {
+        kc[rk] = kb[j];
+        ic[rk] = ib[j];
+      }
+    }
+    __syncthreads();
+    for (int i = tid; i < nc; i += kMergeThreads) {
+      ka[i] = kc[i];
+      ia[i] = ic[i];
+    }
+    na = nc;
+    __syncthreads();
+  }
+  for (int i = tid; i < k_out; i += kMergeThreads) {
+    const int64_t o = q * k_out + i;
+    if (i < na) {
+      out_s[o] = desc_key_to_score(ka[i]);
+      out_i[o] = ia[i];
+    } else {
+      out_s[o] = kPadScore;
+      out_i[o] = -1;
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Host-side planning and launch helpers.
+// ---------------------------------------------------------------------------
+struct TopkPlan {
+  int64_t n, k, nq, nq_pad;
+  bool sample;        // false: n <= cap, dense scan of everything
+  int64_t cap;        // FILTER capacity per query (or dense width when !sample)
+  int64_t m;          // sampled rows
+  int64_t stride;     // sample stride
+  int64_t r;          // rank of the sampled score used as tau
+  // workspace offsets (bytes)
+  size_t off_tau, off_cnt, off_keys, off_sample, total;
+};
+
+static double poisson_tail_ge(double lam, int64_t r) {
+  // P[X >= r], X ~ Poisson(lam), by summing the pmf from r upward.
+  double logp = -lam + r * std::log(lam) - std::lgamma((double)r + 1.0);
+  double p = std::exp(logp), s = 0.0;
+  for (int64_t i = r; i < r + 2000; ++i) {
+    s += p;
+    p *= lam / (double)(i + 1);
+    if (p < 1e-30 * s) break;
+  }
+  return s;
+}
+
+static size_t align_up(size_t x, size_t a) { return (x + a - 1) / a * a; }
+
+static TopkPlan make_plan(int64_t nq, int64_t n, int64_t k) {
+  TopkPlan p{};
+  p.n = n;
+  p.k = k;
+  p.nq = nq;
+  p.nq_pad = (nq + kQueriesPerWG - 1) / kQueriesPerWG * kQueriesPerWG;
+  const int64_t target = std::max<int64_t>(4096, 4 * k);  // expected hits per query
+  p.cap = 4 * target;
+  if (n <= p.cap) {
+    p.sample = false;
+    p.cap = align_up(std::max<int64_t>(n, 4), 4);
+    p.m = 0;
+    p.stride = 1;
+    p.r = 0;
+  } else {
+    p.sample = true;
+    // smallest r with P[miss] = P[Poisson(k r / target) >= r] < 1e-9
+    int64_t r = 1;
+    while (poisson_tail_ge((double)k * r / (double)target, r) > 1e-9 && r < 100000) ++r;
+    p.r = r;
+    int64_t m = (r * n + target - 1) / target;
+    if (m > n) m = n;
+    p.stride = std::max<int64_t>(1, n / m);
+    p.m = (n - p.stride / 2 + p.stride - 1) / p.stride;  // rows stride/2 + i*stride < n
+    if (p.m < r) p.m = std::min<int64_t>(n, r);
+  }
+  size_t o = 0;
+  p.off_tau = o;
+  o = align_up(o + p.nq_pad * 4, 256);
+  p.off_cnt = o;
+  o = align_up(o + p.nq_pad * 4, 256);
+  p.off_keys = o;
+  if (p.sample) o = align_up(o + (size_t)p.nq_pad * p.cap * 8, 256);
+  else o = align_up(o + (size_t)p.nq_pad * p.cap * 4, 256);
+  p.off_sample = o;
+  if (p.sample) o = align_up(o + (size_t)p.nq_pad * align_up(p.m, 4) * 4, 256);
+  p.total = o;
+  return p;
+}
+
+static int scan_grid_x(int64_t ntiles) {
+  int dev = 0, cus = 256;
+  if (hipGetDevice(&dev) == hipSuccess) {
+    int v = 0;
+    if (hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess && v > 0)
+      cus = v;
+  }
+  const int64_t g = std::min<int64_t>(ntiles, (int64_t)cus);
+  return (int)std::max<int64_t>(g, 1);
+}
+
+template <int D>
+static int launch_scan_d(const ScanArgs& a, int mode, hipStream_t s) {
+  const int64_t ntiles = (a.nrows + kTileRows - 1) / kTileRows;
+  if (ntiles == 0 || a.nq == 0) return DRT_OK;
+  dim3 grid(scan_grid_x(ntiles), (unsigned)((a.nq + kQueriesPerWG - 1) / kQueriesPerWG));
+  if (mode == SCAN_FILTER) hipLaunchKernelGGL((ip_scan_kernel<D, SCAN_FILTER>), grid, dim3(kScanThreads), 0, s, a);
+  else hipLaunchKernelGGL((ip_scan_kernel<D, SCAN_DENSE>), grid, dim3(kScanThreads), 0, s, a);
+  return hip_status(hipGetLastError());
+}
+
+static int launch_scan_impl(const ScanArgs& a, int d, int mode, hipStream_t s) {
+  switch (d) {
+    case 64: return launch_scan_d<64>(a, mode, s);
+    case 128: return launch_scan_d<128>(a, mode, s);
+    case 192: return launch_scan_d<192>(a, mode, s);
+    case 256: return launch_scan_d<256>(a, mode, s);
+    case 320: return launch_scan_d<320>(a, mode, s);
+    case 384: return launch_scan_d<384>(a, mode, s);
+    case 448: return launch_scan_d<448>(a, mode, s);
+    case 512: return launch_scan_d<512>(a, mode, s);
+    case 576: return launch_scan_d<576>(a, mode, s);
+    case 640: return launch_scan_d<640>(a, mode, s);
+    case 704: return launch_scan_d<704>(a, mode, s);
+    case 768: return launch_scan_d<768>(a, mode, s);
+    case 832: return launch_scan_d<832>(a, mode, s);
+    case 896: return launch_scan_d<896>(a, mode, s);
+    case 960: return launch_scan_d<960>(a, mode, s);
+    case 1024: return launch_scan_d<1024>(a, mode, s);
+    default: return DRT_EINVAL;
+  }
+}
+
+static int launch_scan(const ScanArgs& a, int d, int mode, hipStream_t s, int family) {
+  const ProfPair pp = prof_begin(family, s);
+  const int rc = launch_scan_impl(a, d, mode, s);
+  prof_end(pp, s);
+  return rc;
+}
+
+static int launch_select(const SelectArgs& a, int input, int output, hipStream_t s) {
+  if (a.nq == 0) return DRT_OK;
+  dim3 grid((unsigned)a.nq);
+  const ProfPair pp = prof_begin(PROF_SELECT, s);
+  struct End { const ProfPair& p; hipStream_t s; ~End() { prof_end(p, s); } } end_{pp, s};
+  if (input == SEL_KEYS64 && output == SEL_TOPK)
+    hipLaunchKernelGGL((select_kernel<SEL_KEYS64, SEL_TOPK>), grid, dim3(kSelThreads), 0, s, a);
+  else if (input == SEL_DENSE32 && output == SEL_TOPK)
+    hipLaunchKernelGGL((select_kernel<SEL_DENSE32, SEL_TOPK>), grid, dim3(kSelThreads), 0, s, a);
+  else if (input == SEL_DENSE32 && output == SEL_KTH)
+    hipLaunchKernelGGL((select_kernel<SEL_DENSE32, SEL_KTH>), grid, dim3(kSelThreads), 0, s, a);
+  else
+    return DRT_EINVAL;
+  return hip_status(hipGetLastError());
+}
+
+static bool valid_dims(int64_t nq, int64_t n, int32_t d, int32_t k) {
+  return nq >= 0 && n >= 0 && d > 0 && d % 64 == 0 && d <= 1024 && k >= 1 && k <= kSelMaxK &&
+         n < (int64_t)0xFFFFFFFFll;
+}
+
+}  // namespace drt
+
+using namespace drt;
+
+extern "C" {
+
+const char* drt_version(void) { return "drt-mi355x 0.1 (gfx950)"; }
+
+size_t drt_ip_topk_workspace(int64_t nq, int64_t n, int32_t d, int32_t k) {
+  if (!valid_dims(nq, n, d, k)) return 0;
+  return make_plan(nq, n, k).total;
+}
+
+int drt_ip_topk_bf16(const void* Q, int64_t nq, const void* P, int64_t n, int32_t d, int32_t k,
+                     int64_t id_offset, float* out_scores, int64_t* out_ids, int32_t* status,
+                     void* ws, size_t ws_bytes, void* stream) {
+  DRT_REQUIRE(valid_dims(nq, n, d, k));
+  if (nq == 0) return DRT_OK;
+  DRT_REQUIRE(Q && out_scores && out_ids && ws);
+  const TopkPlan p = make_plan(nq, n, k);
+  DRT_REQUIRE(ws_bytes >= p.total);
+  hipStream_t s = (hipStream_t)stream;
+  char* w = (char*)ws;
+  float* tau = (float*)(w + p.off_tau);
+  uint32_t* cnt = (uint32_t*)(w + p.off_cnt);
+
+  if (n == 0) {
+    SelectArgs sa{};
+    sa.in = w + p.off_keys;
+    sa.in_stride = p.cap;
+    sa.n_in = 0;
+    sa.n_total = 0;
+    sa.k = k;
+    sa.nq = nq;
+    sa.out_scores = out_scores;
+    sa.out_ids = out_ids;
+    sa.ldo = k;
+    sa.id_offset = id_offset;
+    sa.status = status;
+    return launch_select(sa, SEL_DENSE32, SEL_TOPK, s);
+  }
+  DRT_REQUIRE(P != nullptr);
+
+  ScanArgs a{};
+  a.Q = (const __bf16*)Q;
+  a.nq = nq;
+  a.ldq = d;
+  a.P = (const __bf16*)P;
+  a.ldp = d;
+
+  if (!p.sample) {
+    // Small shard: score every row densely, select directly.
+    a.row0 = 0;
+    a.nrows = n;
+    a.rstride = 1;
+    a.out = w + p.off_keys;
+    a.cap = p.cap;
+    int rc = launch_scan(a, d, SCAN_DENSE, s, PROF_SCAN);
+    if (rc) return rc;
+    SelectArgs sa{};
+    sa.in = w + p.off_keys;
+    sa.in_stride = p.cap;
+    sa.n_in = n;
+    sa.n_total = n;
+    sa.k = k;
+    sa.nq = nq;
+    sa.out_scores = out_scores;
+    sa.out_ids = out_ids;
+    sa.ldo = k;
+    sa.id_offset = id_offset;
+    sa.status = status;
+    return launch_select(sa, SEL_DENSE32, SEL_TOPK, s);
+  }
+
+  // 1. sample pass -> tau
+  a.row0 = p.stride / 2;
+  a.nrows = p.m;
+  a.rstride = p.stride;
+  a.out = w + p.off_sample;
+  a.cap = align_up(p.m, 4);
+  int rc = launch_scan(a, d, SCAN_DENSE, s, PROF_SAMPLE);
+  if (rc) return rc;
+  SelectArgs ka{};
+  ka.in = w + p.off_sample;
+  ka.in_stride = align_up(p.m, 4);
+  ka.n_in = p.m;
+  ka.k = (int)p.r;
+  ka.nq = nq;
+  ka.tau = tau;
+  rc = launch_select(ka, SEL_DENSE32, SEL_KTH, s);
+  if (rc) return rc;
+
+  // 2. filter pass
+  DRT_CHECK_HIP(hipMemsetAsync(cnt, 0, p.nq_pad * 4, s));
+  a.row0 = 0;
+  a.nrows = n;
+  a.rstride = 1;
+  a.tau = tau;
+  a.counts = cnt;
+  a.out = w + p.off_keys;
+  a.cap = p.cap;
+  rc = launch_scan(a, d, SCAN_FILTER, s, PROF_SCAN);
+  if (rc) return rc;
+
+  // 3. select + certify
+  SelectArgs sa{};
+  sa.in = w + p.off_keys;
+  sa.in_stride = p.cap;
+  sa.counts = cnt;
+  sa.cap = p.cap;
+  sa.n_total = n;
+  sa.k = k;
+  sa.nq = nq;
+  sa.out_scores = out_scores;
+  sa.out_ids = out_ids;
+  sa.ldo = k;
+  sa.id_offset = id_offset;
+  sa.status = status;
+  return launch_select(sa, SEL_KEYS64, SEL_TOPK, s);
+}
+
+int drt_ip_topk_resolve(const void* Q, int64_t nq, const void* P, int64_t n, int32_t d, int32_t k,
+                        int64_t id_offset, float* out_scores, int64_t* out_ids, int32_t* status,
+                        int64_t* n_resolved, void* stream) {
+  DRT_REQUIRE(valid_dims(nq, n, d, k));
+  if (n_resolved) *n_resolved = 0;
+  if (nq == 0 || status == nullptr) return DRT_OK;
+  hipStream_t s = (hipStream_t)stream;
+  std::vector<int32_t> st(nq);
+  DRT_CHECK_HIP(hipMemcpyAsync(st.data(), status, nq * 4, hipMemcpyDeviceToHost, s));
+  DRT_CHECK_HIP(hipStreamSynchronize(s));
+  std::vector<int32_t> bad;
+  for (int64_t i = 0; i < nq; ++i)
+    if (st[i] != 0) bad.push_back((int32_t)i);
+  if (bad.empty()) return DRT_OK;
+  if (n_resolved) *n_resolved = (int64_t)bad.size();
+
+  // Dense exact rescan, chunked so the score buffer stays <= ~2 GB.
+  const int64_t width = align_up(std::max<int64_t>(n, 4), 4);
+  int64_t chunk = std::max<int64_t>(1, std::min<int64_t>((int64_t)bad.size(), (2ll << 30) / (width * 4)));
+  chunk = std::min<int64_t>(chunk, kQueriesPerWG);
+  void *qbuf = nullptr, *sbuf = nullptr, *mbuf = nullptr;
+  int rc = DRT_OK;
+  hipError_t e;
+  if ((e = hipMalloc(&qbuf, chunk * (int64_t)d * 2)) != hipSuccess) return (int)e;
+  if ((e = hipMalloc(&sbuf, chunk * width * 4)) != hipSuccess) { hipFree(qbuf); return (int)e; }
+  if ((e = hipMalloc(&mbuf, chunk * 4)) != hipSuccess) { hipFree(qbuf); hipFree(sbuf); return (int)e; }
+  for (size_t b0 = 0; b0 < bad.size() && rc == DRT_OK; b0 += chunk) {
+    const int64_t nb = std::min<int64_t>(chunk, (int64_t)bad.size() - (int64_t)b0);
+    for (int64_t i = 0; i < nb; ++i) {
+      e = hipMemcpyAsync((char*)qbuf + i * d * 2, (const char*)Q + (int64_t)bad[b0 + i] * d * 2, d * 2,
+                         hipMemcpyDeviceToDevice, s);
+      if (e != hipSuccess) { rc = (int)e; break; }
+    }
+    if (rc) break;
+    if ((e = hipMemcpyAsync(mbuf, bad.data() + b0, nb * 4, hipMemcpyHostToDevice, s)) != hipSuccess) {
+      rc = (int)e;
+      break;
+    }
+    ScanArgs a{};
+    a.Q = (const __bf16*)qbuf;
+    a.nq = nb;
+    a.ldq = d;
+    a.P = (const __bf16*)P;
+    a.ldp = d;
+    a.row0 = 0;
+    a.nrows = n;
+    a.rstride = 1;
+    a.out = sbuf;
+    a.cap = width;
+    rc = launch_scan(a, d, SCAN_DENSE, s, -1);
+    if (rc) break;
+    SelectArgs sa{};
+    sa.in = sbuf;
+    sa.in_stride = width;
+    sa.n_in = n;
+    sa.n_total = n;
+    sa.k = k;
+    sa.nq = nb;
+    sa.out_scores = out_scores;
+    sa.out_ids = out_ids;
+    sa.ldo = k;
+    sa.id_offset = id_offset;
+    sa.status = status;
+    sa.qmap = (const int32_t*)mbuf;
+    rc = launch_select(sa, SEL_DENSE32, SEL_TOPK, s);
+    if (rc) break;
+    if ((e = hipStreamSynchronize(s)) != hipSuccess) { rc = (int)e; break; }
+  }
+  hipStreamSynchronize(s);
+  hipFree(qbuf);
+  hipFree(sbuf);
+  hipFree(mbuf);
+  return rc;
+}
+
+int drt_topk_merge(const float* scores, const int64_t* ids, int64_t nq, int32_t nparts, int32_t k_in,
+                   int32_t k_out, float* out_scores, int64_t* out_ids, void* stream) {
+  DRT_REQUIRE(nq >= 0 && nparts >= 1 && nparts <= 64 && k_in >= 1 && k_in <= kSelMaxK && k_out >= 1 &&
+              k_out <= kSelMaxK && (int64_t)k_out <= (int64_t)k_in * nparts);
+  if (nq == 0) return DRT_OK;
+  DRT_REQUIRE(scores && ids && out_scores && out_ids);
+  const ProfPair pp = prof_begin(PROF_MERGE, (hipStream_t)stream);
+  hipLaunchKernelGGL(merge_kernel, dim3((unsigned)nq), dim3(kMergeThreads), 0, (hipStream_t)stream, scores,
+                     ids, nq, (int)nparts, (int)k_in, (int)k_out, out_scores, out_ids);
+  prof_end(pp, (hipStream_t)stream);
+  return hip_status(hipGetLastError());
+}
+
+}  // extern "C"

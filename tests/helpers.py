@@ -1,0 +1,49 @@
+"""Shared test helpers: seeded synthetic data in the BASELINE layout."""
+import numpy as np
+
+
+def int_bf16(rng, shape, lo=-8, hi=8):
+    """Small-integer values: exactly representable in bf16, dot products exact in fp32."""
+    return rng.integers(lo, hi + 1, size=shape).astype(np.float32)
+
+
+def gauss_bf16(rng, shape):
+    from oracle.search_oracle import bf16_round
+    return bf16_round(rng.standard_normal(shape).astype(np.float32))
+
+
+def to_dev_bf16(x, device):
+    import torch
+    from oracle.search_oracle import bf16_bits
+    t = torch.from_numpy(bf16_bits(x).view(np.int16).copy()).view(torch.bfloat16)
+    return t.to(device)
+
+
+def sample_plan(n, k):
+    """Mirror of make_plan() in csrc/search.hip (used only to build adversarial inputs)."""
+    import math
+    target = max(4096, 4 * k)
+    cap = 4 * target
+    if n <= cap:
+        return None
+
+    def tail(lam, r):
+        logp = -lam + r * math.log(lam) - math.lgamma(r + 1.0)
+        p = math.exp(logp)
+        s = 0.0
+        i = r
+        while True:
+            s += p
+            p *= lam / (i + 1)
+            i += 1
+            if p < 1e-30 * s or i > r + 2000:
+                break
+        return s
+
+    r = 1
+    while tail(k * r / target, r) > 1e-9:
+        r += 1
+    m = min(n, (r * n + target - 1) // target)
+    stride = max(1, n // m)
+    m = (n - stride // 2 + stride - 1) // stride
+    return dict(r=r, m=m, stride=stride, cap=cap, rows=np.arange(m) * stride + stride // 2)

@@ -1,0 +1,41 @@
+#!/bin/bash
+# One GPU-box session: parity tests -> smoke -> bench -> rocprof stats.
+# Stops at the first crash / abort / timeout (exit status other than 0/1 from
+# pytest, non-zero elsewhere); plain test failures (exit 1) still let the
+# measurement steps run.
+set -u
+cd "$(dirname "$0")/.."
+OUT=gpurun_out
+mkdir -p $OUT
+export TMPDIR=/tmp
+STEPS=${STEPS:-20}
+TAG=${TAG:-r01}
+
+run() {  # run <name> <timeout> cmd...
+  local name=$1 to=$2; shift 2
+  echo "=== $name: $*" | tee -a $OUT/session.log
+  timeout -k 10 "$to" "$@" > $OUT/$name.log 2>&1
+  local rc=$?
+  echo "=== $name rc=$rc" | tee -a $OUT/session.log
+  tail -n 30 $OUT/$name.log
+  return $rc
+}
+
+if [ "${SKIP_TESTS:-0}" != "1" ]; then
+  run pytest_gpu ${TEST_TIMEOUT:-900} python -m pytest tests -m gpu -q -rfE --timeout 600 ${PYTEST_ARGS:-}
+  rc=$?
+  if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then echo "STOP: pytest rc=$rc"; exit $rc; fi
+fi
+run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" || exit $?
+run bench 600 python bench.py --steps $STEPS --warmup 3 ${BENCH_ARGS:-} || exit $?
+grep '^{' $OUT/bench.log | tail -1 > $OUT/bench_$TAG.json
+if [ "${SKIP_PROF:-0}" != "1" ]; then
+  cd /tmp
+  run_prof() {
+    timeout -k 10 600 rocprofv3 --kernel-trace --stats -d $GRAFT_REPO_ROOT/$OUT/prof_$TAG -o run --output-format csv \
+      -- python3 $GRAFT_REPO_ROOT/bench.py --steps $STEPS --warmup 3 --no-cpu-baseline > $GRAFT_REPO_ROOT/$OUT/prof_$TAG.log 2>&1
+  }
+  run_prof; rc=$?
+  echo "=== rocprof rc=$rc" | tee -a $GRAFT_REPO_ROOT/$OUT/session.log
+  find $GRAFT_REPO_ROOT/$OUT/prof_$TAG -name "*stats*" | head
+fi
