@@ -139,8 +139,8 @@ def main():
     i_loc = torch.empty((nsteps, qb, k), dtype=torch.int64, device=dev)
     st = torch.zeros((nsteps, qb), dtype=torch.int32, device=dev)
     if world > 1:
-        s_all = torch.empty((world, qb, k), dtype=torch.float32, device=dev)
-        i_all = torch.empty((world, qb, k), dtype=torch.int64, device=dev)
+        s_all = torch.empty((world * qb, k), dtype=torch.float32, device=dev)
+        i_all = torch.empty((world * qb, k), dtype=torch.int64, device=dev)
     results = []
 
     def step(j):
@@ -149,7 +149,7 @@ def main():
         if world > 1:
             dist.all_gather_into_tensor(s_all, s_loc[j])
             dist.all_gather_into_tensor(i_all, i_loc[j])
-            return kernels.topk_merge(s_all, i_all, k)
+            return kernels.topk_merge(s_all.view(world, qb, k), i_all.view(world, qb, k), k)
         return s_loc[j], i_loc[j]
 
     def fix_failures(first, last):
@@ -164,7 +164,7 @@ def main():
             if step_merge_only:
                 dist.all_gather_into_tensor(s_all, s_loc[j])
                 dist.all_gather_into_tensor(i_all, i_loc[j])
-                kernels.topk_merge(s_all, i_all, k)
+                kernels.topk_merge(s_all.view(world, qb, k), i_all.view(world, qb, k), k)
         return nb
 
     for j in range(args.warmup):

@@ -1,0 +1,70 @@
+"""Encode leg of bench.py: passages encoded/sec of the bf16 BERT-base passage tower.
+
+Config C2 (BASELINE.json configs[1]): DPR bert-base, 128-token passages.
+Random-init BERT-base weights (no checkpoint offline), synthetic token ids in
+the collator format; one step = DRModel.encode_passage of one batch
+(embeddings -> 12 layers -> [CLS] pooling), all on the HIP kernels.
+"""
+from __future__ import annotations
+
+import time
+
+import torch
+
+FLOP_PER_PASSAGE_L128 = 22.347e9   # linear 169.87 MFLOP/token + attention 4*L^2*768*12
+
+
+def flops_per_seq(L, H=768, layers=12, inter=3072):
+    lin = 2 * L * (H * 3 * H + H * H + 2 * H * inter) * layers
+    att = 4 * L * L * H * layers
+    return lin + att
+
+
+def run(device, batch=512, L=128, steps=5, warmup=2):
+    from transformers import BertConfig, BertModel
+    from .model.encoder import HipBertEncoder
+    from . import _native
+    torch.manual_seed(0)
+    m = BertModel(BertConfig(), add_pooling_layer=False).eval()
+    enc = HipBertEncoder.from_hf(m, device)
+    del m
+    g = torch.Generator(device=device)
+    g.manual_seed(1)
+    ids = torch.randint(1000, 30522, (batch, L), generator=g, device=device, dtype=torch.int64)
+    ids[:, 0] = 101
+    ids[:, -1] = 102
+    mask = torch.ones((batch, L), dtype=torch.int64, device=device)
+    lib = _native.load()
+    for _ in range(warmup):
+        enc.pool(enc(ids, mask), mask, "first")
+    torch.cuda.synchronize()
+    lib.drt_profile_enable(_native.PROF_GEMM, 1)
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        enc.pool(enc(ids, mask), mask, "first")
+    torch.cuda.synchronize()
+    el = time.perf_counter() - t0
+    lib.drt_profile_enable(_native.PROF_GEMM, 0)
+    tot = _native.ctypes.c_double(0)
+    cnt = _native.c_i64(0)
+    lib.drt_profile_read(_native.PROF_GEMM, _native.ctypes.byref(tot), _native.ctypes.byref(cnt))
+    pps = steps * batch / el
+    fl = flops_per_seq(L)
+    gemm_flops = 2 * L * batch * (768 * 3 * 768 + 768 * 768 + 2 * 768 * 3072) * 12 * steps
+    gemm_tf = gemm_flops / (tot.value * 1e-3) / 1e12 if tot.value > 0 else None
+    return {
+        "metric": "passages encoded/sec (bf16 BERT-base, 128-token passages)",
+        "value": round(pps, 1),
+        "unit": "passages/s",
+        "batch": batch, "seq_len": L, "steps": steps,
+        "ms_per_step": round(el / steps * 1e3, 3),
+        "roofline": {
+            "bound": "mfma",
+            "achieved": round(fl * pps / 1e12, 1),
+            "peak": 2500.0,
+            "unit": "TFLOP/s",
+            "frac": round(fl * pps / 1e12 / 2500.0, 4),
+            "flop_per_passage": fl,
+            "gemm_only_tflops": round(gemm_tf, 1) if gemm_tf else None,
+        },
+    }

@@ -1,0 +1,381 @@
+// BERT bi-encoder forward kernels (DRModel.encode, DRT/model/biencoder.py:127-151,
+// over HF BertModel: transformers/models/bert/modeling_bert.py embeddings :53-107,
+// self-attention :139-204, sublayer outputs :282-352).
+//
+//   embed_ln        word + position + token-type embedding, LayerNorm (fp32 math)
+//   layernorm       LayerNorm of an fp32 [M, H] row (GEMM epilogue already added
+//                   bias + residual), bf16 out
+//   attention       per (sequence, head): softmax(Q K^T / sqrt(dh) + key mask) V
+//                   with v_mfma_f32_32x32x16_bf16, online softmax over 32-key
+//                   tiles; S^T = K Q^T keeps each query's scores lane-local and
+//                   the S^T accumulator feeds the P.V MFMA directly as its B
+//                   operand (no LDS round trip for P)
+//   pool            first / masked-mean / masked-max pooling (utils.py:233-240)
+//   l2norm          F.normalize(reps, dim=1) (biencoder.py:149-150)
+#include "drt_common.h"
+
+namespace drt {
+
+// ---------------------------------------------------------------------------
+// Row LayerNorm helpers: one wave per row, H = 64 * EPL (EPL <= 16).
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+
+template <int EPL>
+__device__ __forceinline__ void ln_row(float (&x)[EPL], const float* gamma, const float* beta, float eps, int lane,
+                                       int H, __bf16* out_row) {
+  float s = 0.f;
+#pragma unroll
+  for (int e = 0; e < EPL; ++e) s += x[e];
+  const float mean = wave_sum(s) / (float)H;
+  float v = 0.f;
+#pragma unroll
+  for (int e = 0; e < EPL; ++e) {
+    const float d = x[e] - mean;
+    v += d * d;
+  }
+  const float var = wave_sum(v) / (float)H;
+  const float rstd = rsqrtf(var + eps);
+  // element e of lane: column c = (e / 4) * 256 + lane * 4 + (e % 4)   (4-wide chunks)
+#pragma unroll
+  for (int e4 = 0; e4 < EPL / 4; ++e4) {
+    const int c = e4 * 256 + lane * 4;
+    bf16x4 o;
+#pragma unroll
+    for (int u = 0; u < 4; ++u) o[u] = (__bf16)((x[e4 * 4 + u] - mean) * rstd * gamma[c + u] + beta[c + u]);
+    *(bf16x4*)(out_row + c) = o;
+  }
+}
+
+template <int EPL>
+__global__ __launch_bounds__(256) void embed_ln_kernel(const int64_t* ids, const int64_t* type_ids, int64_t T,
+                                                       int64_t L, const float* wemb, const float* pemb,
+                                                       const float* temb, const float* gamma, const float* beta,
+                                                       float eps, int H, __bf16* out) {
+  const int lane = threadIdx.x & 63;
+  const int64_t t = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (t >= T) return;
+  const int64_t id = ids[t];
+  const int64_t pos = t % L;
+  const int64_t tt = type_ids ? type_ids[t] : 0;
+  const float* w = wemb + id * H;
+  const float* p = pemb + pos * H;
+  const float* y = temb + tt * H;
+  float x[EPL];
+#pragma unroll
+  for (int e4 = 0; e4 < EPL / 4; ++e4) {
+    const int c = e4 * 256 + lane * 4;
+    const f32x4 a = *(const f32x4*)(w + c);
+    const f32x4 b = *(const f32x4*)(p + c);
+    const f32x4 d = *(const f32x4*)(y + c);
+#pragma unroll
+    for (int u = 0; u < 4; ++u) x[e4 * 4 + u] = (a[u] + d[u]) + b[u];  // (word + type) + position, as HF
+  }
+  ln_row<EPL>(x, gamma, beta, eps, lane, H, out + t * H);
+}
+
+template <int EPL>
+__global__ __launch_bounds__(256) void layernorm_f32_kernel(const float* X, int64_t M, int H, const float* gamma,
+                                                            const float* beta, float eps, __bf16* out) {
+  const int lane = threadIdx.x & 63;
+  const int64_t t = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (t >= M) return;
+  const float* xr = X + t * H;
+  float x[EPL];
+#pragma unroll
+  for (int e4 = 0; e4 < EPL / 4; ++e4) {
+    const f32x4 a = *(const f32x4*)(xr + e4 * 256 + lane * 4);
+#pragma unroll
+    for (int u = 0; u < 4; ++u) x[e4 * 4 + u] = a[u];
+  }
+  ln_row<EPL>(x, gamma, beta, eps, lane, H, out + t * H);
+}
+
+// ---------------------------------------------------------------------------
+// Attention.  One work-group (4 waves) per (sequence b, head hd); wave w owns
+// query blocks w, w+4, ... of 32 rows.  K is staged in LDS as swizzled
+// [key][8 x 16 B] rows (A operand of S^T = K Q^T), V transposed as Vt[d][key]
+// with a padded row stride (A operand of O^T = V^T P^T).
+// ---------------------------------------------------------------------------
+constexpr int kAttnThreads = 256;
+constexpr int kHeadDim = 64;
+constexpr int kMaxSeq = 512;
+
+struct AttnArgs {
+  const __bf16* qkv;      // [B*L][3*H]  (Q | K | V, head-major inside each)
+  const int64_t* mask;    // [B][L] attention_mask (1 = token, 0 = pad) or null
+  __bf16* ctx;            // [B*L][H]
+  int64_t B, L;
+  int heads, H;
+  float scale;            // 1/sqrt(dh): applied to Q (exact for dh = 64)
+};
+
+__global__ __launch_bounds__(kAttnThreads) void attention_kernel(AttnArgs a) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int L = (int)a.L;
+  const int Lp = (L + 31) & ~31;           // keys padded to the 32-key tile
+  const int vts = Lp * 2 + 8;              // Vt row stride (bytes): conflict-free ds_read_b64
+  char* Ks = smem;                          // Lp * 128 B
+  char* Vt = smem + Lp * 128;               // 64 * vts B
+  float* kbias = (float*)(Vt + 64 * vts);   // Lp floats
+
+  const int tid = threadIdx.x;
+  const int wave = tid >> 6, lane = tid & 63;
+  const int r = lane & 31, h = lane >> 5;
+  const int64_t b = blockIdx.x / a.heads;
+  const int hd = blockIdx.x % a.heads;
+  const int64_t row0 = b * a.L;
+  const int64_t ld = 3 * (int64_t)a.H;
+  const __bf16* Qg = a.qkv + row0 * ld + hd * kHeadDim;
+  const __bf16* Kg = Qg + a.H;
+  const __bf16* Vg = Qg + 2 * a.H;
+
+  // ---- stage K (swizzled rows) and V^T, key bias
+  for (int i = tid; i < Lp * 8; i += kAttnThreads) {
+    const int key = i >> 3, c = i & 7;
+    u32x4 kv = {0u, 0u, 0u, 0u}, vv = {0u, 0u, 0u, 0u};
+    if (key < L) {
+      kv = *(const u32x4*)(Kg + (int64_t)key * ld + c * 8);
+      vv = *(const u32x4*)(Vg + (int64_t)key * ld + c * 8);
+    }
+    *(u32x4*)(Ks + key * 128 + ((c ^ ((key >> 1) & 7)) << 4)) = kv;
+    const uint16_t* ve = (const uint16_t*)&vv;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) *(uint16_t*)(Vt + (c * 8 + j) * vts + key * 2) = ve[j];
+  }
+  for (int i = tid; i < Lp; i += kAttnThreads) {
+    float bv = 0.0f;
+    if (i >= L) bv = -3.402823466e+38f;
+    else if (a.mask && a.mask[b * a.L + i] == 0) bv = -3.402823466e+38f;  // (1 - mask) * finfo.min
+    kbias[i] = bv;
+  }
+  __syncthreads();
+
+  const int sw = (r >> 1) & 7;
+  const int nqb = Lp / 32;
+  for (int qb = wave; qb < nqb; qb += 4) {
+    // Q fragment (B operand, B[k=d][col=q] = Q[q][d]) scaled by 1/sqrt(dh)
+    int qrow = qb * 32 + r;
+    qrow = qrow < L ? qrow : L - 1;
+    bf16x8 qf[4];
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+      bf16x8 v = *(const bf16x8*)(Qg + (int64_t)qrow * ld + s * 16 + h * 8);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) v[j] = (__bf16)((float)v[j] * a.scale);
+      qf[s] = v;
+    }
+    f32x16 o[2];
+#pragma unroll
+    for (int t = 0; t < 2; ++t)
+#pragma unroll
+      for (int e = 0; e < 16; ++e) o[t][e] = 0.0f;
+    float m = -__builtin_inff(), l = 0.0f;
+
+    for (int kt = 0; kt < Lp; kt += 32) {
+      // S^T tile: rows = keys kt.., cols = queries
+      f32x16 s;
+#pragma unroll
+      for (int e = 0; e < 16; ++e) s[e] = 0.0f;
+#pragma unroll
+      for (int st = 0; st < 4; ++st) {
+        const int key = kt + r;
+        const bf16x8 kf = *(const bf16x8*)(Ks + key * 128 + ((((2 * st) | h) ^ sw) << 4));
+        s = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kf, qf[st], s, 0, 0, 0);
+      }
+      float mt = -__builtin_inff();
+#pragma unroll
+      for (int e = 0; e < 16; ++e) {
+        s[e] += kbias[kt + (e & 3) + 8 * (e >> 2) + 4 * h];
+        mt = fmaxf(mt, s[e]);
+      }
+      mt = fmaxf(mt, __shfl_xor(mt, 32, 64));
+      const float mn = fmaxf(m, mt);
+      const float alpha = __expf(m - mn);
+      float ps = 0.0f;
+#pragma unroll
+      for (int e = 0; e < 16; ++e) {
+        s[e] = __expf(s[e] - mn);
+        ps += s[e];
+      }
+      ps += __shfl_xor(ps, 32, 64);
+      l = l * alpha + ps;
+      m = mn;
+#pragma unroll
+      for (int t = 0; t < 2; ++t)
+#pragma unroll
+        for (int e = 0; e < 16; ++e) o[t][e] *= alpha;
+      // O^T += V^T P^T over the 32 keys (2 k-steps of 16)
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks) {
+        bf16x8 pf;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) pf[j] = (__bf16)s[8 * ks + j];
+#pragma unroll
+        for (int t = 0; t < 2; ++t) {
+          const char* vrow = Vt + (32 * t + r) * vts + (kt + 16 * ks + 4 * h) * 2;
+          const bf16x4 v0 = *(const bf16x4*)(vrow);
+          const bf16x4 v1 = *(const bf16x4*)(vrow + 16);
+          bf16x8 vf;
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            vf[j] = v0[j];
+            vf[4 + j] = v1[j];
+          }
+          o[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vf, pf, o[t], 0, 0, 0);
+        }
+      }
+    }
+    // O^T[d][q]: lane holds query r; d = 32t + (e&3) + 8(e>>2) + 4h
+    const int q = qb * 32 + r;
+    if (q < L) {
+      const float inv = 1.0f / l;
+      __bf16* orow = a.ctx + (row0 + q) * a.H + hd * kHeadDim;
+#pragma unroll
+      for (int t = 0; t < 2; ++t)
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+          bf16x4 v;
+#pragma unroll
+          for (int u = 0; u < 4; ++u) v[u] = (__bf16)(o[t][4 * g + u] * inv);
+          *(bf16x4*)(orow + 32 * t + 8 * g + 4 * h) = v;
+        }
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Pooling (utils.py:233-240, biencoder.py:139-146) and L2 normalisation.
+// mode 0 = first ([CLS]), 1 = mean over mask, 2 = max of hidden*mask.
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void pool_kernel(const __bf16* hidden, const int64_t* mask, int64_t B, int64_t L,
+                                                   int H, int mode, float* out, __bf16* out_bf16) {
+  const int64_t b = blockIdx.x;
+  for (int c = threadIdx.x; c < H; c += 256) {
+    float v;
+    if (mode == 0) {
+      v = (float)hidden[(b * L) * H + c];
+    } else if (mode == 1) {
+      float s = 0.f, cnt = 0.f;
+      for (int64_t l = 0; l < L; ++l) {
+        const float mk = mask ? (float)mask[b * L + l] : 1.0f;
+        s += (float)hidden[(b * L + l) * H + c] * mk;
+        cnt += mk;
+      }
+      v = s / fmaxf(cnt, 1e-9f);
+    } else {
+      float mx = -__builtin_inff();
+      for (int64_t l = 0; l < L; ++l) {
+        const float mk = mask ? (float)mask[b * L + l] : 1.0f;
+        mx = fmaxf(mx, (float)hidden[(b * L + l) * H + c] * mk);
+      }
+      v = mx;
+    }
+    out[b * H + c] = v;
+    if (out_bf16) out_bf16[b * H + c] = (__bf16)v;
+  }
+}
+
+__global__ __launch_bounds__(256) void l2norm_kernel(float* x, int64_t B, int H, __bf16* out_bf16) {
+  __shared__ float red[4];
+  const int64_t b = blockIdx.x;
+  float s = 0.f;
+  for (int c = threadIdx.x; c < H; c += 256) {
+    const float v = x[b * H + c];
+    s += v * v;
+  }
+  s = wave_sum(s);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = s;
+  __syncthreads();
+  const float tot = red[0] + red[1] + red[2] + red[3];
+  const float den = fmaxf(sqrtf(tot), 1e-12f);  // F.normalize eps
+  for (int c = threadIdx.x; c < H; c += 256) {
+    const float v = x[b * H + c] / den;
+    x[b * H + c] = v;
+    if (out_bf16) out_bf16[b * H + c] = (__bf16)v;
+  }
+}
+
+}  // namespace drt
+
+using namespace drt;
+
+extern "C" {
+
+int drt_embed_ln(const int64_t* ids, const int64_t* type_ids, int64_t B, int64_t L, const float* word_emb,
+                 const float* pos_emb, const float* type_emb, const float* gamma, const float* beta, float eps,
+                 int32_t H, void* out, void* stream) {
+  DRT_REQUIRE(B >= 0 && L > 0 && H > 0 && H % 256 == 0 && H <= 1024);
+  const int64_t T = B * L;
+  if (T == 0) return DRT_OK;
+  DRT_REQUIRE(ids && word_emb && pos_emb && type_emb && gamma && beta && out);
+  hipStream_t s = (hipStream_t)stream;
+  dim3 grid((unsigned)((T + 3) / 4));
+  switch (H / 64) {
+    case 4: hipLaunchKernelGGL(embed_ln_kernel<4>, grid, dim3(256), 0, s, ids, type_ids, T, L, word_emb, pos_emb, type_emb, gamma, beta, eps, H, (__bf16*)out); break;
+    case 8: hipLaunchKernelGGL(embed_ln_kernel<8>, grid, dim3(256), 0, s, ids, type_ids, T, L, word_emb, pos_emb, type_emb, gamma, beta, eps, H, (__bf16*)out); break;
+    case 12: hipLaunchKernelGGL(embed_ln_kernel<12>, grid, dim3(256), 0, s, ids, type_ids, T, L, word_emb, pos_emb, type_emb, gamma, beta, eps, H, (__bf16*)out); break;
+    case 16: hipLaunchKernelGGL(embed_ln_kernel<16>, grid, dim3(256), 0, s, ids, type_ids, T, L, word_emb, pos_emb, type_emb, gamma, beta, eps, H, (__bf16*)out); break;
+    default: return DRT_EINVAL;
+  }
+  return hip_status(hipGetLastError());
+}
+
+int drt_layernorm_f32_bf16(const float* X, int64_t M, int32_t H, const float* gamma, const float* beta, float eps,
+                           void* out, void* stream) {
+  DRT_REQUIRE(M >= 0 && H > 0 && H % 256 == 0 && H <= 1024);
+  if (M == 0) return DRT_OK;
+  DRT_REQUIRE(X && gamma && beta && out);
+  hipStream_t s = (hipStream_t)stream;
+  dim3 grid((unsigned)((M + 3) / 4));
+  switch (H / 64) {
+    case 4: hipLaunchKernelGGL(layernorm_f32_kernel<4>, grid, dim3(256), 0, s, X, M, H, gamma, beta, eps, (__bf16*)out); break;
+    case 8: hipLaunchKernelGGL(layernorm_f32_kernel<8>, grid, dim3(256), 0, s, X, M, H, gamma, beta, eps, (__bf16*)out); break;
+    case 12: hipLaunchKernelGGL(layernorm_f32_kernel<12>, grid, dim3(256), 0, s, X, M, H, gamma, beta, eps, (__bf16*)out); break;
+    case 16: hipLaunchKernelGGL(layernorm_f32_kernel<16>, grid, dim3(256), 0, s, X, M, H, gamma, beta, eps, (__bf16*)out); break;
+    default: return DRT_EINVAL;
+  }
+  return hip_status(hipGetLastError());
+}
+
+int drt_attention_bf16(const void* qkv, const int64_t* mask, void* ctx, int64_t B, int64_t L, int32_t heads,
+                       int32_t head_dim, float scale, void* stream) {
+  DRT_REQUIRE(B >= 0 && L > 0 && L <= kMaxSeq && heads > 0 && head_dim == kHeadDim);
+  if (B == 0) return DRT_OK;
+  DRT_REQUIRE(qkv && ctx);
+  AttnArgs a{(const __bf16*)qkv, mask, (__bf16*)ctx, B, L, heads, heads * head_dim, scale};
+  const int Lp = ((int)L + 31) & ~31;
+  const size_t lds = (size_t)Lp * 128 + (size_t)64 * (Lp * 2 + 8) + (size_t)Lp * 4;
+  static bool attr_set = false;
+  if (!attr_set) {
+    DRT_CHECK_HIP(hipFuncSetAttribute((const void*)attention_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                      160 * 1024));
+    attr_set = true;
+  }
+  hipLaunchKernelGGL(attention_kernel, dim3((unsigned)(B * heads)), dim3(kAttnThreads), lds, (hipStream_t)stream, a);
+  return hip_status(hipGetLastError());
+}
+
+int drt_pool_bf16(const void* hidden, const int64_t* mask, int64_t B, int64_t L, int32_t H, int32_t mode,
+                  float* out, void* out_bf16, void* stream) {
+  DRT_REQUIRE(B >= 0 && L > 0 && H > 0 && mode >= 0 && mode <= 2);
+  if (B == 0) return DRT_OK;
+  DRT_REQUIRE(hidden && out);
+  hipLaunchKernelGGL(pool_kernel, dim3((unsigned)B), dim3(256), 0, (hipStream_t)stream, (const __bf16*)hidden, mask,
+                     B, L, H, mode, out, (__bf16*)out_bf16);
+  return hip_status(hipGetLastError());
+}
+
+int drt_l2_normalize_f32(float* x, int64_t B, int32_t H, void* out_bf16, void* stream) {
+  DRT_REQUIRE(B >= 0 && H > 0);
+  if (B == 0) return DRT_OK;
+  DRT_REQUIRE(x);
+  hipLaunchKernelGGL(l2norm_kernel, dim3((unsigned)B), dim3(256), 0, (hipStream_t)stream, x, B, H, (__bf16*)out_bf16);
+  return hip_status(hipGetLastError());
+}
+
+}  // extern "C"

@@ -178,6 +178,8 @@ int launch_gemm(const GemmArgs& a, bool out_bf16, int epi, hipStream_t s) {
     switch (epi) {
       case EPI_NONE: return launch_gemm_t<false, EPI_NONE>(a, s);
       case EPI_BIAS: return launch_gemm_t<false, EPI_BIAS>(a, s);
+      case EPI_BIAS | EPI_RESID: return launch_gemm_t<false, EPI_BIAS | EPI_RESID>(a, s);
+      case EPI_RESID: return launch_gemm_t<false, EPI_RESID>(a, s);
       default: return DRT_EINVAL;
     }
   }
@@ -186,6 +188,7 @@ int launch_gemm(const GemmArgs& a, bool out_bf16, int epi, hipStream_t s) {
     case EPI_BIAS: return launch_gemm_t<true, EPI_BIAS>(a, s);
     case EPI_BIAS | EPI_GELU: return launch_gemm_t<true, EPI_BIAS | EPI_GELU>(a, s);
     case EPI_BIAS | EPI_RESID: return launch_gemm_t<true, EPI_BIAS | EPI_RESID>(a, s);
+    case EPI_GELU: return launch_gemm_t<true, EPI_GELU>(a, s);
     default: return DRT_EINVAL;
   }
 }
@@ -211,4 +214,31 @@ extern "C" int drt_gemm_nt_bf16_f32(const void* A, const void* B, float* C, int6
   a.ldc = ldc;
   a.alpha = 1.0f;
   return launch_gemm(a, false, EPI_NONE, (hipStream_t)stream);
+}
+
+// nn.Linear: Y[M, N] = X[M, K] . W[N, K]^T (+ bias) (GELU) (+ residual [M, N] bf16)
+// flags: DRT_LIN_GELU = 1, DRT_LIN_OUT_F32 = 2.
+extern "C" int drt_linear_bf16(const void* X, const void* W, const float* bias, const void* residual, void* Y,
+                               int64_t M, int64_t N, int64_t K, int32_t flags, void* stream) {
+  DRT_REQUIRE(M >= 0 && N > 0 && K > 0 && K % 64 == 0);
+  if (M == 0) return DRT_OK;
+  DRT_REQUIRE(X && W && Y);
+  const bool gelu = flags & 1, f32 = flags & 2;
+  DRT_REQUIRE(!(gelu && residual));
+  GemmArgs a{};
+  a.A = (const __bf16*)X;
+  a.B = (const __bf16*)W;
+  a.C = Y;
+  a.bias = bias;
+  a.R = (const __bf16*)residual;
+  a.m = M;
+  a.n = N;
+  a.k = K;
+  a.lda = K;
+  a.ldb = K;
+  a.ldc = N;
+  a.ldr = N;
+  a.alpha = 1.0f;
+  const int epi = (bias ? EPI_BIAS : 0) | (gelu ? EPI_GELU : 0) | (residual ? EPI_RESID : 0);
+  return launch_gemm(a, !f32, epi, (hipStream_t)stream);
 }

@@ -287,12 +287,28 @@ __global__ __launch_bounds__(kScanThreads, 1) void ip_scan_kernel(ScanArgs a) {
 }
 
 // ---------------------------------------------------------------------------
-// Per-query selection: MSD radix select on 64-bit keys + LDS bitonic sort.
+// Per-query selection.
+//
+// Fast path (every realistic input): one block per query,
+//   A  min/max of the scores,
+//   B  1024-bin histogram LINEAR IN THE SCORE VALUE (per-wave sub-histograms,
+//      so a dense score range does not serialise on a few LDS bins),
+//   C  suffix scan -> highest bin b with >= k elements at or above it,
+//   D  TOPK: gather every key in bins >= b into LDS (<= 4096 of them),
+//      bitonic sort on the 64-bit key (score desc, row asc), emit k;
+//      KTH:  tau = min score among bins >= b  (<= the k-th largest: safe).
+// Bin membership is one monotone float formula used by every pass, so the
+// selected set is always an upper set of the scores (ties stay together).
+// Fallback (degenerate data, e.g. >4096 equal scores): MSD radix select on
+// the full 64-bit key, 8 bits per pass, then the same sort.
 // ---------------------------------------------------------------------------
 enum { SEL_KEYS64 = 0, SEL_DENSE32 = 1 };
 enum { SEL_TOPK = 0, SEL_KTH = 1 };
 constexpr int kSelThreads = 512;
+constexpr int kSelWaves = kSelThreads / 64;
 constexpr int kSelMaxK = 2048;
+constexpr int kSelBins = 1024;
+constexpr int kSelBuf = 4096;
 
 struct SelectArgs {
   const void* in;
@@ -321,115 +337,32 @@ __device__ __forceinline__ uint64_t sel_load(const SelectArgs& a, int64_t q, int
   return ((uint64_t)v << 32) | (uint64_t)(uint32_t)j;
 }
 
-template <int INPUT, int OUTPUT>
-__global__ __launch_bounds__(kSelThreads) void select_kernel(SelectArgs a) {
-  __shared__ uint32_t hist[256];
-  __shared__ uint64_t sh_prefix, sh_mask;
-  __shared__ int64_t sh_kk;
-  __shared__ int sh_done;
-  __shared__ uint32_t sh_nsel;
-  __shared__ __attribute__((aligned(16))) uint64_t buf[kSelMaxK];
+__device__ __forceinline__ float key_score(uint64_t x) { return desc_key_to_score((uint32_t)(x >> 32)); }
 
+__device__ __forceinline__ int score_bin(float s, float smin, float scale) {
+  float f = (s - smin) * scale;
+  int b = (int)f;
+  b = b < 0 ? 0 : b;
+  return b > kSelBins - 1 ? kSelBins - 1 : b;
+}
+
+template <typename T, typename Op>
+__device__ __forceinline__ T block_reduce(T v, T* scratch, Op op) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = op(v, __shfl_xor(v, o, 64));
+  const int w = threadIdx.x >> 6;
+  __syncthreads();
+  if ((threadIdx.x & 63) == 0) scratch[w] = v;
+  __syncthreads();
+  T r = scratch[0];
+#pragma unroll
+  for (int i = 1; i < kSelWaves; ++i) r = op(r, scratch[i]);
+  return r;
+}
+
+// Bitonic sort of buf[0..n2) ascending (n2 power of two), whole block.
+__device__ __forceinline__ void block_bitonic(uint64_t* buf, int n2) {
   const int tid = threadIdx.x;
-  const int64_t q = blockIdx.x;
-  int64_t c_raw, c;
-  if (INPUT == SEL_KEYS64) {
-    c_raw = a.counts[q];
-    c = c_raw < a.cap ? c_raw : a.cap;
-  } else {
-    c_raw = a.n_in;
-    c = a.n_in;
-  }
-  const int64_t kk_total = (int64_t)a.k < c ? (int64_t)a.k : c;
-
-  if (tid == 0) {
-    sh_prefix = 0;
-    sh_mask = 0;
-    sh_kk = kk_total;
-    sh_done = (c <= (int64_t)a.k) ? 1 : 0;  // everything selected
-    if (c <= (int64_t)a.k) {
-      sh_prefix = ~0ull;
-      sh_mask = ~0ull;
-    }
-  }
-  __syncthreads();
-
-  const int last_shift = (OUTPUT == SEL_KTH) ? 32 : 0;
-  for (int shift = 56; shift >= last_shift && !sh_done; shift -= 8) {
-    for (int i = tid; i < 256; i += kSelThreads) hist[i] = 0;
-    __syncthreads();
-    const uint64_t prefix = sh_prefix, mask = sh_mask;
-    for (int64_t j = tid; j < c; j += kSelThreads) {
-      const uint64_t x = sel_load<INPUT>(a, q, j);
-      if ((x & mask) == prefix) atomicAdd(&hist[(x >> shift) & 255], 1u);
-    }
-    __syncthreads();
-    if (tid < 64) {
-      // lane owns bins 4*lane .. 4*lane+3
-      const uint32_t b0 = hist[4 * tid], b1 = hist[4 * tid + 1], b2 = hist[4 * tid + 2],
-                     b3 = hist[4 * tid + 3];
-      const uint32_t s4 = b0 + b1 + b2 + b3;
-      uint32_t incl = s4;
-#pragma unroll
-      for (int o = 1; o < 64; o <<= 1) {
-        const uint32_t v = __shfl_up(incl, o, 64);
-        if (tid >= o) incl += v;
-      }
-      const uint32_t excl = incl - s4;
-      const int64_t kk = sh_kk;
-      // the lane whose range [excl, incl) contains rank kk-1
-      if ((int64_t)excl < kk && kk <= (int64_t)incl) {
-        uint32_t run = excl;
-        const uint32_t bb[4] = {b0, b1, b2, b3};
-        int d = 0;
-        uint32_t cnt = 0;
-#pragma unroll
-        for (int t = 0; t < 4; ++t) {
-          if ((int64_t)(run + bb[t]) >= kk) {
-            d = 4 * tid + t;
-            cnt = bb[t];
-            break;
-          }
-          run += bb[t];
-        }
-        const int64_t rem = kk - run;
-        sh_prefix = prefix | ((uint64_t)d << shift);
-        sh_mask = mask | (255ull << shift);
-        sh_kk = rem;
-        if ((int64_t)cnt == rem && OUTPUT == SEL_TOPK) sh_done = 1;  // whole bucket selected
-      }
-    }
-    __syncthreads();
-  }
-
-  if (OUTPUT == SEL_KTH) {
-    if (tid == 0) {
-      float t;
-      if (c < (int64_t)a.k || c == 0) t = -__builtin_inff();  // too few samples: keep all
-      else t = desc_key_to_score((uint32_t)(sh_prefix >> 32));
-      a.tau[q] = t;
-    }
-    return;
-  }
-
-  // threshold: select every key whose masked value <= prefix
-  const uint64_t thr = sh_prefix | ~sh_mask;
-  if (tid == 0) sh_nsel = 0;
-  __syncthreads();
-  for (int64_t j = tid; j < c; j += kSelThreads) {
-    const uint64_t x = sel_load<INPUT>(a, q, j);
-    if (x <= thr) {
-      const uint32_t p = atomicAdd(&sh_nsel, 1u);
-      if (p < (uint32_t)kSelMaxK) buf[p] = x;
-    }
-  }
-  __syncthreads();
-  int n2 = 1;
-  while (n2 < (int)kk_total) n2 <<= 1;
-  const int nsel = (int)(sh_nsel < (uint32_t)kSelMaxK ? sh_nsel : kSelMaxK);
-  for (int i = nsel + tid; i < n2; i += kSelThreads) buf[i] = ~0ull;
-  __syncthreads();
-  // bitonic sort ascending of buf[0..n2)
   for (int size = 2; size <= n2; size <<= 1) {
     for (int stride = size >> 1; stride > 0; stride >>= 1) {
       for (int i = tid; i < n2 / 2; i += kSelThreads) {
@@ -445,13 +378,204 @@ __global__ __launch_bounds__(kSelThreads) void select_kernel(SelectArgs a) {
       __syncthreads();
     }
   }
+}
+
+template <int INPUT, int OUTPUT>
+__global__ __launch_bounds__(kSelThreads) void select_kernel(SelectArgs a) {
+  __shared__ uint32_t hist[kSelWaves][kSelBins];
+  __shared__ uint32_t suffix[kSelBins];
+  __shared__ float fscr[kSelWaves];
+  __shared__ uint64_t uscr[kSelWaves];
+  __shared__ uint64_t sh_prefix, sh_mask;
+  __shared__ int64_t sh_kk;
+  __shared__ int sh_done, sh_bin;
+  __shared__ uint32_t sh_nsel;
+  __shared__ __attribute__((aligned(16))) uint64_t buf[kSelBuf];
+
+  const int tid = threadIdx.x;
+  const int wave = tid >> 6;
+  const int64_t q = blockIdx.x;
+  int64_t c_raw, c;
+  if (INPUT == SEL_KEYS64) {
+    c_raw = a.counts[q];
+    c = c_raw < a.cap ? c_raw : a.cap;
+  } else {
+    c_raw = a.n_in;
+    c = a.n_in;
+  }
+  const int64_t kk_total = (int64_t)a.k < c ? (int64_t)a.k : c;
+
+  if (OUTPUT == SEL_KTH && (c < (int64_t)a.k || c == 0)) {
+    if (tid == 0) a.tau[q] = -__builtin_inff();  // too few samples: keep everything
+    return;
+  }
+
+  bool fast_done = false;   // uniform
+  int nsel = 0;             // TOPK: entries in buf
+  if (c > (int64_t)a.k) {
+    // ---- A: score range
+    float lo = __builtin_inff(), hi = -__builtin_inff();
+    for (int64_t j = tid; j < c; j += kSelThreads) {
+      const float s = key_score(sel_load<INPUT>(a, q, j));
+      lo = fminf(lo, s);
+      hi = fmaxf(hi, s);
+    }
+    lo = block_reduce(lo, fscr, [](float x, float y) { return fminf(x, y); });
+    hi = block_reduce(hi, fscr, [](float x, float y) { return fmaxf(x, y); });
+    const float range = hi - lo;
+    const float scale = (range > 0.0f && range < __builtin_inff()) ? (float)kSelBins / range : 0.0f;
+    // ---- B: per-wave histograms
+    for (int i = tid; i < kSelWaves * kSelBins; i += kSelThreads) (&hist[0][0])[i] = 0;
+    __syncthreads();
+    for (int64_t j = tid; j < c; j += kSelThreads) {
+      const float s = key_score(sel_load<INPUT>(a, q, j));
+      atomicAdd(&hist[wave][score_bin(s, lo, scale)], 1u);
+    }
+    __syncthreads();
+    for (int i = tid; i < kSelBins; i += kSelThreads) {
+      uint32_t t = 0;
+#pragma unroll
+      for (int w = 0; w < kSelWaves; ++w) t += hist[w][i];
+      suffix[i] = t;
+    }
+    __syncthreads();
+    // ---- C: inclusive suffix sum (Hillis-Steele over 1024 bins)
+    for (int off = 1; off < kSelBins; off <<= 1) {
+      uint32_t v[kSelBins / kSelThreads];
+#pragma unroll
+      for (int u = 0; u < kSelBins / kSelThreads; ++u) {
+        const int i = tid + u * kSelThreads;
+        v[u] = suffix[i] + (i + off < kSelBins ? suffix[i + off] : 0u);
+      }
+      __syncthreads();
+#pragma unroll
+      for (int u = 0; u < kSelBins / kSelThreads; ++u) suffix[tid + u * kSelThreads] = v[u];
+      __syncthreads();
+    }
+    // highest bin b with suffix[b] >= kk_total (suffix is non-increasing in b)
+    if (tid == 0) sh_bin = 0;
+    __syncthreads();
+    for (int i = tid; i < kSelBins; i += kSelThreads) {
+      const bool ok = (int64_t)suffix[i] >= kk_total;
+      const bool next_ok = (i + 1 < kSelBins) && (int64_t)suffix[i + 1] >= kk_total;
+      if (ok && !next_ok) sh_bin = i;
+    }
+    __syncthreads();
+    const int b = sh_bin;
+    const uint32_t cnt_sel = suffix[b];
+    if (OUTPUT == SEL_KTH) {
+      // ---- D(KTH): tau = min score in bins >= b  (a lower bound of the k-th largest)
+      float t = __builtin_inff();
+      for (int64_t j = tid; j < c; j += kSelThreads) {
+        const float s = key_score(sel_load<INPUT>(a, q, j));
+        if (score_bin(s, lo, scale) >= b) t = fminf(t, s);
+      }
+      t = block_reduce(t, fscr, [](float x, float y) { return fminf(x, y); });
+      if (tid == 0) a.tau[q] = t;
+      return;
+    }
+    if (cnt_sel <= (uint32_t)kSelBuf) {
+      // ---- D(TOPK): gather the upper set, sort, emit
+      if (tid == 0) sh_nsel = 0;
+      __syncthreads();
+      for (int64_t j = tid; j < c; j += kSelThreads) {
+        const uint64_t x = sel_load<INPUT>(a, q, j);
+        if (score_bin(key_score(x), lo, scale) >= b) {
+          const uint32_t p = atomicAdd(&sh_nsel, 1u);
+          if (p < (uint32_t)kSelBuf) buf[p] = x;
+        }
+      }
+      __syncthreads();
+      nsel = (int)sh_nsel;
+      fast_done = true;
+    }
+  }
+
+  if (!fast_done) {
+    // ---- fallback / small input: MSD radix select on 64-bit keys
+    if (tid == 0) {
+      sh_prefix = 0;
+      sh_mask = 0;
+      sh_kk = kk_total;
+      sh_done = (c <= (int64_t)a.k) ? 1 : 0;  // everything selected
+      if (c <= (int64_t)a.k) {
+        sh_prefix = ~0ull;
+        sh_mask = ~0ull;
+      }
+    }
+    __syncthreads();
+    uint32_t* h0 = &hist[0][0];
+    for (int shift = 56; shift >= 0 && !sh_done; shift -= 8) {
+      for (int i = tid; i < 256; i += kSelThreads) h0[i] = 0;
+      __syncthreads();
+      const uint64_t prefix = sh_prefix, mask = sh_mask;
+      for (int64_t j = tid; j < c; j += kSelThreads) {
+        const uint64_t x = sel_load<INPUT>(a, q, j);
+        if ((x & mask) == prefix) atomicAdd(&h0[(x >> shift) & 255], 1u);
+      }
+      __syncthreads();
+      if (tid < 64) {
+        const uint32_t b0 = h0[4 * tid], b1 = h0[4 * tid + 1], b2 = h0[4 * tid + 2], b3 = h0[4 * tid + 3];
+        const uint32_t s4 = b0 + b1 + b2 + b3;
+        uint32_t incl = s4;
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+          const uint32_t v = __shfl_up(incl, o, 64);
+          if (tid >= o) incl += v;
+        }
+        const uint32_t excl = incl - s4;
+        const int64_t kk = sh_kk;
+        if ((int64_t)excl < kk && kk <= (int64_t)incl) {
+          uint32_t run = excl;
+          const uint32_t bb[4] = {b0, b1, b2, b3};
+          int d = 0;
+          uint32_t cnt = 0;
+#pragma unroll
+          for (int t = 0; t < 4; ++t) {
+            if ((int64_t)(run + bb[t]) >= kk) {
+              d = 4 * tid + t;
+              cnt = bb[t];
+              break;
+            }
+            run += bb[t];
+          }
+          const int64_t rem = kk - run;
+          sh_prefix = prefix | ((uint64_t)d << shift);
+          sh_mask = mask | (255ull << shift);
+          sh_kk = rem;
+          if ((int64_t)cnt == rem) sh_done = 1;  // whole bucket selected
+        }
+      }
+      __syncthreads();
+    }
+    const uint64_t thr = sh_prefix | ~sh_mask;  // every key whose masked value <= prefix
+    if (tid == 0) sh_nsel = 0;
+    __syncthreads();
+    for (int64_t j = tid; j < c; j += kSelThreads) {
+      const uint64_t x = sel_load<INPUT>(a, q, j);
+      if (x <= thr) {
+        const uint32_t p = atomicAdd(&sh_nsel, 1u);
+        if (p < (uint32_t)kSelBuf) buf[p] = x;
+      }
+    }
+    __syncthreads();
+    nsel = (int)sh_nsel;
+  }
+
+  nsel = nsel < kSelBuf ? nsel : kSelBuf;
+  int n2 = 1;
+  while (n2 < nsel) n2 <<= 1;
+  for (int i = nsel + tid; i < n2; i += kSelThreads) buf[i] = ~0ull;
+  __syncthreads();
+  block_bitonic(buf, n2);
+
   const int64_t orow = a.qmap ? (int64_t)a.qmap[q] : q;
   float* os = a.out_scores + orow * a.ldo;
   int64_t* oi = a.out_ids + orow * a.ldo;
   for (int j = tid; j < a.k; j += kSelThreads) {
     if (j < kk_total) {
       const uint64_t x = buf[j];
-      os[j] = desc_key_to_score((uint32_t)(x >> 32));
+      os[j] = key_score(x);
       oi[j] = a.id_offset + (int64_t)(x & 0xFFFFFFFFull);
     } else {
       os[j] = kPadScore;
@@ -465,6 +589,72 @@ __global__ __launch_bounds__(kSelThreads) void select_kernel(SelectArgs a) {
       if (c_raw < (int64_t)a.k && c_raw < a.n_total) st = 1;          // threshold too high
     }
     a.status[orow] = st;
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Sample threshold: tau_q = score of the r-th best sampled key.
+// kth_partial: grid (chunks, nq); each block LDS-sorts one 4096-key chunk of
+//              the dense sample row and keeps its best r keys.
+// kth_final:   grid nq; sorts the chunks' survivors (<= 4096), picks the r-th.
+// Padding keys are 0xFFFFFFFF (sort last, never chosen ahead of real keys).
+// ---------------------------------------------------------------------------
+constexpr int kKthChunk = 4096;
+constexpr int kKthThreads = 512;
+
+__device__ __forceinline__ void block_bitonic_u32(uint32_t* buf, int n2, int nthreads) {
+  const int tid = threadIdx.x;
+  for (int size = 2; size <= n2; size <<= 1) {
+    for (int stride = size >> 1; stride > 0; stride >>= 1) {
+      for (int i = tid; i < n2 / 2; i += nthreads) {
+        const int lo = 2 * i - (i & (stride - 1));
+        const int hi = lo + stride;
+        const bool up = ((lo & size) == 0);
+        const uint32_t x = buf[lo], y = buf[hi];
+        if ((x > y) == up) {
+          buf[lo] = y;
+          buf[hi] = x;
+        }
+      }
+      __syncthreads();
+    }
+  }
+}
+
+__global__ __launch_bounds__(kKthThreads) void kth_partial_kernel(const uint32_t* in, int64_t stride, int64_t n,
+                                                                  int r, uint32_t* part) {
+  __shared__ __attribute__((aligned(16))) uint32_t buf[kKthChunk];
+  const int64_t q = blockIdx.y;
+  const int nchunk = gridDim.x;
+  const int64_t j0 = (int64_t)blockIdx.x * kKthChunk;
+  const int64_t cnt64 = n - j0 < kKthChunk ? n - j0 : kKthChunk;
+  const int cnt = (int)cnt64;
+  const uint32_t* src = in + q * stride + j0;
+  // rows are 16-B aligned (stride % 4 == 0, j0 % 4096 == 0): vector loads, tail scalar
+  const int nv = cnt >> 2;
+  for (int i = threadIdx.x; i < nv; i += kKthThreads) *(u32x4*)(buf + 4 * i) = *(const u32x4*)(src + 4 * i);
+  for (int i = 4 * nv + threadIdx.x; i < kKthChunk; i += kKthThreads) buf[i] = i < cnt ? src[i] : 0xFFFFFFFFu;
+  __syncthreads();
+  int n2 = 1;
+  while (n2 < cnt) n2 <<= 1;
+  block_bitonic_u32(buf, n2, kKthThreads);
+  uint32_t* o = part + (q * nchunk + blockIdx.x) * r;
+  for (int i = threadIdx.x; i < r; i += kKthThreads) o[i] = i < cnt ? buf[i] : 0xFFFFFFFFu;
+}
+
+__global__ __launch_bounds__(kKthThreads) void kth_final_kernel(const uint32_t* part, int nchunk, int r,
+                                                                float* tau) {
+  __shared__ uint32_t buf[kKthChunk];
+  const int64_t q = blockIdx.x;
+  const int tot = nchunk * r;
+  for (int i = threadIdx.x; i < kKthChunk; i += kKthThreads) buf[i] = i < tot ? part[q * tot + i] : 0xFFFFFFFFu;
+  __syncthreads();
+  int n2 = 1;
+  while (n2 < tot) n2 <<= 1;
+  block_bitonic_u32(buf, n2, kKthThreads);
+  if (threadIdx.x == 0) {
+    const uint32_t kr = buf[r - 1];
+    tau[q] = (kr == 0xFFFFFFFFu) ? -__builtin_inff() : desc_key_to_score(kr);
   }
 }
 
@@ -566,8 +756,9 @@ struct TopkPlan {
   int64_t m;          // sampled rows
   int64_t stride;     // sample stride
   int64_t r;          // rank of the sampled score used as tau
+  int64_t nchunk;     // kth_partial chunks per query
   // workspace offsets (bytes)
-  size_t off_tau, off_cnt, off_keys, off_sample, total;
+  size_t off_tau, off_cnt, off_keys, off_sample, off_part, total;
 };
 
 static double poisson_tail_ge(double lam, int64_t r) {
@@ -607,8 +798,14 @@ static TopkPlan make_plan(int64_t nq, int64_t n, int64_t k) {
     int64_t m = (r * n + target - 1) / target;
     if (m > n) m = n;
     p.stride = std::max<int64_t>(1, n / m);
+    // the kth_final pass keeps chunks * r <= 4096 survivors
+    const int64_t m_cap = std::max<int64_t>(1, kKthChunk / r) * kKthChunk;
+    if (m > m_cap) m = m_cap;
+    p.stride = std::max<int64_t>(1, n / m);
     p.m = (n - p.stride / 2 + p.stride - 1) / p.stride;  // rows stride/2 + i*stride < n
+    if (p.m > m_cap) p.m = m_cap;
     if (p.m < r) p.m = std::min<int64_t>(n, r);
+    p.nchunk = (p.m + kKthChunk - 1) / kKthChunk;
   }
   size_t o = 0;
   p.off_tau = o;
@@ -620,6 +817,8 @@ static TopkPlan make_plan(int64_t nq, int64_t n, int64_t k) {
   else o = align_up(o + (size_t)p.nq_pad * p.cap * 4, 256);
   p.off_sample = o;
   if (p.sample) o = align_up(o + (size_t)p.nq_pad * align_up(p.m, 4) * 4, 256);
+  p.off_part = o;
+  if (p.sample) o = align_up(o + (size_t)p.nq_pad * p.nchunk * p.r * 4, 256);
   p.total = o;
   return p;
 }
@@ -777,15 +976,16 @@ int drt_ip_topk_bf16(const void* Q, int64_t nq, const void* P, int64_t n, int32_
   a.cap = align_up(p.m, 4);
   int rc = launch_scan(a, d, SCAN_DENSE, s, PROF_SAMPLE);
   if (rc) return rc;
-  SelectArgs ka{};
-  ka.in = w + p.off_sample;
-  ka.in_stride = align_up(p.m, 4);
-  ka.n_in = p.m;
-  ka.k = (int)p.r;
-  ka.nq = nq;
-  ka.tau = tau;
-  rc = launch_select(ka, SEL_DENSE32, SEL_KTH, s);
-  if (rc) return rc;
+  {
+    const ProfPair pp = prof_begin(PROF_SELECT, s);
+    hipLaunchKernelGGL(kth_partial_kernel, dim3((unsigned)p.nchunk, (unsigned)nq), dim3(kKthThreads), 0, s,
+                       (const uint32_t*)(w + p.off_sample), (int64_t)align_up(p.m, 4), p.m, (int)p.r,
+                       (uint32_t*)(w + p.off_part));
+    hipLaunchKernelGGL(kth_final_kernel, dim3((unsigned)nq), dim3(kKthThreads), 0, s,
+                       (const uint32_t*)(w + p.off_part), (int)p.nchunk, (int)p.r, tau);
+    prof_end(pp, s);
+    DRT_CHECK_HIP(hipGetLastError());
+  }
 
   // 2. filter pass
   DRT_CHECK_HIP(hipMemsetAsync(cnt, 0, p.nq_pad * 4, s));

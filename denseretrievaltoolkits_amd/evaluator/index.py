@@ -1,0 +1,74 @@
+"""Drop-in for DRT/evaluator/index.py on the MI355X search kernels.
+
+``BaseFaissIPRetriever`` keeps the reference constructor / add / search /
+batch_search contract (DRT/evaluator/index.py:16-44) and its public ``index``
+attribute, but the index is a device-resident bf16 ``FlatIPIndex`` searched by
+the fused HIP scan + top-k kernels instead of a CPU faiss.IndexFlatIP.
+
+Behaviour notes (vs the reference):
+* ``search`` returns only the ids, [nq, k] int64, ordered by descending score
+  (index.py:32-33); ties are ordered by ascending id (the reference's
+  ``np.argsort(-scores)`` leaves them unspecified).  The scores of the last
+  search stay available as ``last_scores``.
+* ``batch_search`` returns the concatenated ids (the reference's version
+  unpacks ``search``'s single return value into two names and raises; the
+  intent — batching over queries — is kept).
+* rows are stored as bf16: scores are exact fp32 dot products of the
+  bf16-rounded embeddings.
+"""
+from __future__ import annotations
+
+from typing import List, Optional
+
+import numpy as np
+
+from ..search import FlatIPIndex
+
+
+class BaseFaissIPRetriever:
+    def __init__(self, init_reps, device=None):
+        if isinstance(init_reps, np.ndarray):
+            index = FlatIPIndex(init_reps.shape[1], device=device)
+        elif init_reps is None:
+            index = None
+        else:
+            index = FlatIPIndex(int(init_reps), device=device)
+        self.index = index
+        self.docid: List = []
+        self.last_scores: Optional[np.ndarray] = None
+
+    def add(self, p_reps) -> None:
+        self.index.add(p_reps)
+
+    def search(self, q_reps, k: int = 1000) -> np.ndarray:
+        scores, indices = self.index.search(q_reps, k)
+        self.last_scores = scores
+        return indices
+
+    def search_device(self, q_reps, k: int = 1000):
+        """Device tensors (scores fp32, ids int64) without the host round trip."""
+        return self.index.search_device(q_reps, k)
+
+    def batch_search(self, q_reps, k: int, batch_size: int, quiet: bool = False) -> np.ndarray:
+        out = []
+        for start in range(0, q_reps.shape[0], batch_size):
+            out.append(self.search(q_reps[start: start + batch_size], k))
+        if not out:
+            return np.zeros((0, k), dtype=np.int64)
+        return np.concatenate(out, axis=0)
+
+
+class FaissRetriever(BaseFaissIPRetriever):
+    """index_factory ANN retriever of the reference (index.py:47-54).  Never called by
+    the reference's scripts and out of scope here: importable, but building
+    one raises instead of silently degrading to brute force."""
+
+    def __init__(self, init_reps: np.ndarray, factory_str: str):
+        raise NotImplementedError("FaissRetriever (faiss.index_factory ANN) is not part of the MI355X hot path; "
+                                  "use BaseFaissIPRetriever (exact) instead")
+
+
+def BM25Retriever(*args, **kwargs):  # noqa: N802 - keeps the reference's importable name (sampler.py:5)
+    """Sparse BM25 negative mining is CPU data prep, out of scope; the
+    reference's own implementation should be used for it."""
+    raise NotImplementedError("BM25Retriever is out of scope for the MI355X build (CPU negative mining)")

@@ -1,0 +1,196 @@
+"""BERT encoder forward on the HIP kernels (bf16 storage, fp32 accumulation).
+
+Replaces the third-party HF ``BertModel.forward`` that ``DRModel.encode``
+calls (DRT/model/biencoder.py:137; transformers modeling_bert.py:620-686) for
+inference: embeddings + LayerNorm, then per layer
+
+    qkv  = linear(h, Wqkv)                        (Q | K | V fused, bf16)
+    ctx  = attention(qkv, key-padding mask)       (fused MFMA kernel)
+    x    = linear(ctx, Wo) + bo + h               (fp32)
+    h    = layernorm(x)                           (bf16)
+    f    = gelu(linear(h, W1) + b1)               (bf16)
+    x    = linear(f, W2) + b2 + h                 (fp32)
+    h    = layernorm(x)
+
+Weights are snapshotted from the HF module (bf16 copies of the linears,
+fp32 embeddings / biases / LayerNorm) and re-snapshotted automatically when
+the source parameters change (torch bumps ``Tensor._version`` on in-place
+optimizer updates).
+"""
+from __future__ import annotations
+
+import math
+from dataclasses import dataclass
+from typing import Dict, Optional
+
+import torch
+
+from .. import _native
+
+POOL_MODES = {"first": 0, "mean": 1, "max": 2}
+
+
+@dataclass
+class BertShape:
+    hidden: int
+    layers: int
+    heads: int
+    intermediate: int
+    eps: float
+    act: str
+
+    @classmethod
+    def from_config(cls, cfg) -> "BertShape":
+        return cls(cfg.hidden_size, cfg.num_hidden_layers, cfg.num_attention_heads, cfg.intermediate_size,
+                   float(cfg.layer_norm_eps), str(cfg.hidden_act))
+
+
+def _check_supported(shape: BertShape):
+    if shape.hidden % 256 or shape.hidden > 1024:
+        raise ValueError(f"hidden size {shape.hidden} unsupported (multiple of 256, <= 1024)")
+    if shape.hidden // shape.heads != 64:
+        raise ValueError("head_dim must be 64")
+    if shape.intermediate % 64:
+        raise ValueError("intermediate size must be a multiple of 64")
+    if shape.act not in ("gelu", "gelu_new") and shape.act != "gelu":
+        raise ValueError(f"activation {shape.act} unsupported (erf GELU only)")
+    if shape.act != "gelu":
+        raise ValueError("only erf GELU ('gelu') is implemented")
+
+
+class HipBertEncoder:
+    """Inference forward of a BERT-family encoder on gfx950 kernels."""
+
+    def __init__(self, shape: BertShape, state: Dict[str, torch.Tensor], device: torch.device,
+                 prefix: str = ""):
+        _check_supported(shape)
+        self.shape = shape
+        self.device = device
+        self.lib = _native.load()
+        self._load(state, prefix)
+
+    # -- weights --------------------------------------------------------
+    def _load(self, sd: Dict[str, torch.Tensor], prefix: str):
+        dev = self.device
+
+        def f32(name):
+            return sd[prefix + name].detach().to(dev, torch.float32).contiguous()
+
+        def b16(name):
+            return sd[prefix + name].detach().to(dev, torch.float32).to(torch.bfloat16).contiguous()
+
+        self.word = f32("embeddings.word_embeddings.weight")
+        self.pos = f32("embeddings.position_embeddings.weight")
+        self.type = f32("embeddings.token_type_embeddings.weight")
+        self.emb_g = f32("embeddings.LayerNorm.weight")
+        self.emb_b = f32("embeddings.LayerNorm.bias")
+        self.layers = []
+        for i in range(self.shape.layers):
+            p = f"encoder.layer.{i}."
+            wqkv = torch.cat([sd[prefix + p + f"attention.self.{n}.weight"].detach().float()
+                              for n in ("query", "key", "value")], 0)
+            bqkv = torch.cat([sd[prefix + p + f"attention.self.{n}.bias"].detach().float()
+                              for n in ("query", "key", "value")], 0)
+            self.layers.append(dict(
+                wqkv=wqkv.to(dev).to(torch.bfloat16).contiguous(),
+                bqkv=bqkv.to(dev).contiguous(),
+                wo=b16(p + "attention.output.dense.weight"), bo=f32(p + "attention.output.dense.bias"),
+                g1=f32(p + "attention.output.LayerNorm.weight"), b1=f32(p + "attention.output.LayerNorm.bias"),
+                wi=b16(p + "intermediate.dense.weight"), bi=f32(p + "intermediate.dense.bias"),
+                wf=b16(p + "output.dense.weight"), bf=f32(p + "output.dense.bias"),
+                g2=f32(p + "output.LayerNorm.weight"), b2=f32(p + "output.LayerNorm.bias"),
+            ))
+
+    @classmethod
+    def from_hf(cls, model, device) -> "HipBertEncoder":
+        return cls(BertShape.from_config(model.config), dict(model.state_dict()), torch.device(device))
+
+    # -- forward --------------------------------------------------------
+    def _lin(self, x, w, b, out, resid=None, gelu=False):
+        m, k = x.shape
+        n = w.shape[0]
+        flags = (1 if gelu else 0) | (2 if out.dtype == torch.float32 else 0)
+        _native.check(self.lib.drt_linear_bf16(x.data_ptr(), w.data_ptr(), b.data_ptr() if b is not None else None,
+                                               resid.data_ptr() if resid is not None else None, out.data_ptr(),
+                                               m, n, k, flags, self.stream), "drt_linear_bf16")
+        return out
+
+    def forward(self, input_ids: torch.Tensor, attention_mask: Optional[torch.Tensor] = None,
+                token_type_ids: Optional[torch.Tensor] = None) -> torch.Tensor:
+        """last_hidden_state [B, L, H] bf16."""
+        sh = self.shape
+        dev = self.device
+        ids = input_ids.to(dev, torch.int64).contiguous()
+        B, L = ids.shape
+        if L > self.pos.shape[0]:
+            raise ValueError(f"sequence length {L} exceeds max_position_embeddings {self.pos.shape[0]}")
+        mask = attention_mask.to(dev, torch.int64).contiguous() if attention_mask is not None else None
+        tt = token_type_ids.to(dev, torch.int64).contiguous() if token_type_ids is not None else None
+        H, T = sh.hidden, B * L
+        self.stream = _native.stream_ptr(dev)
+        h = torch.empty((T, H), dtype=torch.bfloat16, device=dev)
+        _native.check(self.lib.drt_embed_ln(ids.data_ptr(), tt.data_ptr() if tt is not None else None, B, L,
+                                            self.word.data_ptr(), self.pos.data_ptr(), self.type.data_ptr(),
+                                            self.emb_g.data_ptr(), self.emb_b.data_ptr(), sh.eps, H, h.data_ptr(),
+                                            self.stream), "drt_embed_ln")
+        qkv = torch.empty((T, 3 * H), dtype=torch.bfloat16, device=dev)
+        ctx = torch.empty((T, H), dtype=torch.bfloat16, device=dev)
+        x32 = torch.empty((T, H), dtype=torch.float32, device=dev)
+        ffn = torch.empty((T, sh.intermediate), dtype=torch.bfloat16, device=dev)
+        scale = 1.0 / math.sqrt(H // sh.heads)
+        for ly in self.layers:
+            self._lin(h, ly["wqkv"], ly["bqkv"], qkv)
+            _native.check(self.lib.drt_attention_bf16(qkv.data_ptr(), mask.data_ptr() if mask is not None else None,
+                                                      ctx.data_ptr(), B, L, sh.heads, H // sh.heads, scale,
+                                                      self.stream), "drt_attention_bf16")
+            self._lin(ctx, ly["wo"], ly["bo"], x32, resid=h)
+            _native.check(self.lib.drt_layernorm_f32_bf16(x32.data_ptr(), T, H, ly["g1"].data_ptr(),
+                                                          ly["b1"].data_ptr(), sh.eps, h.data_ptr(), self.stream),
+                          "drt_layernorm_f32_bf16")
+            self._lin(h, ly["wi"], ly["bi"], ffn, gelu=True)
+            self._lin(ffn, ly["wf"], ly["bf"], x32, resid=h)
+            _native.check(self.lib.drt_layernorm_f32_bf16(x32.data_ptr(), T, H, ly["g2"].data_ptr(),
+                                                          ly["b2"].data_ptr(), sh.eps, h.data_ptr(), self.stream),
+                          "drt_layernorm_f32_bf16")
+        return h.view(B, L, H)
+
+    __call__ = forward
+
+    def pool(self, hidden: torch.Tensor, attention_mask: Optional[torch.Tensor], pooling: str,
+             want_bf16: bool = False):
+        """reps fp32 [B, H] (and optional bf16 copy) with the reference's pooling semantics."""
+        if pooling not in POOL_MODES:
+            raise ValueError("Unknown pooling type: {}".format(pooling))
+        B, L, H = hidden.shape
+        dev = hidden.device
+        mask = attention_mask.to(dev, torch.int64).contiguous() if attention_mask is not None else None
+        reps = torch.empty((B, H), dtype=torch.float32, device=dev)
+        rb = torch.empty((B, H), dtype=torch.bfloat16, device=dev) if want_bf16 else None
+        _native.check(self.lib.drt_pool_bf16(hidden.data_ptr(), mask.data_ptr() if mask is not None else None,
+                                             B, L, H, POOL_MODES[pooling], reps.data_ptr(),
+                                             rb.data_ptr() if rb is not None else None, _native.stream_ptr(dev)),
+                      "drt_pool_bf16")
+        return reps, rb
+
+
+def l2_normalize_(reps: torch.Tensor, want_bf16: bool = False):
+    lib = _native.load()
+    reps = reps.contiguous()
+    B, H = reps.shape
+    rb = torch.empty((B, H), dtype=torch.bfloat16, device=reps.device) if want_bf16 else None
+    _native.check(lib.drt_l2_normalize_f32(reps.data_ptr(), B, H, rb.data_ptr() if rb is not None else None,
+                                           _native.stream_ptr(reps.device)), "drt_l2_normalize_f32")
+    return reps, rb
+
+
+def linear_head(reps_bf16: torch.Tensor, weight_bf16: torch.Tensor) -> torch.Tensor:
+    """LinearHead.forward (DRT/model/linear.py:22-23): reps @ W^T, no bias, fp32 out."""
+    lib = _native.load()
+    B, K = reps_bf16.shape
+    N = weight_bf16.shape[0]
+    out = torch.empty((B, N), dtype=torch.float32, device=reps_bf16.device)
+    if K % 64:
+        raise ValueError("head input dim must be a multiple of 64")
+    _native.check(lib.drt_linear_bf16(reps_bf16.data_ptr(), weight_bf16.data_ptr(), None, None, out.data_ptr(),
+                                      B, N, K, 2, _native.stream_ptr(reps_bf16.device)), "drt_linear_bf16")
+    return out

@@ -1,0 +1,76 @@
+"""Fused in-batch score matrix + cross entropy with autograd, on the HIP kernels.
+
+Forward   S = q @ p^T (exact-f32 MFMA), loss = scale * mean_i CE(S_i, i * stride)
+Backward  dS = scale * g / m * (softmax(S) - onehot);  dq = dS @ p;  dp = dS^T @ q
+Replaces ``torch.matmul(q_reps, p_reps.transpose(0, 1))`` + ``nn.CrossEntropyLoss``
+in DRModel.forward (DRT/model/biencoder.py:107-119) and SimpleContrastiveLoss
+(DRT/trainer/losses.py:11-17).
+"""
+from __future__ import annotations
+
+import torch
+
+from . import _native
+
+
+def _f32(t):
+    return t.detach().to(torch.float32).contiguous()
+
+
+def gemm_nt_f32(a: torch.Tensor, b: torch.Tensor) -> torch.Tensor:
+    lib = _native.load()
+    m, k = a.shape
+    n = b.shape[0]
+    out = torch.empty((m, n), dtype=torch.float32, device=a.device)
+    _native.check(lib.drt_gemm_nt_f32(a.data_ptr(), b.data_ptr(), out.data_ptr(), m, n, k, a.stride(0),
+                                      b.stride(0), out.stride(0), _native.stream_ptr(a.device)), "drt_gemm_nt_f32")
+    return out
+
+
+def transpose_f32(x: torch.Tensor) -> torch.Tensor:
+    lib = _native.load()
+    r, c = x.shape
+    y = torch.empty((c, r), dtype=torch.float32, device=x.device)
+    _native.check(lib.drt_transpose_f32(x.data_ptr(), r, c, y.data_ptr(), _native.stream_ptr(x.device)),
+                  "drt_transpose_f32")
+    return y
+
+
+class ScoreCE(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, q, p, target_stride: int, scale: float):
+        if not (q.is_cuda and p.is_cuda):
+            raise ValueError("ScoreCE runs on the GPU only (no CPU fallback)")
+        lib = _native.load()
+        qf, pf = _f32(q), _f32(p)
+        S = gemm_nt_f32(qf, pf)
+        m, n = S.shape
+        lse = torch.empty(m, dtype=torch.float32, device=S.device)
+        rl = torch.empty(m, dtype=torch.float32, device=S.device)
+        loss = torch.empty((), dtype=torch.float32, device=S.device)
+        _native.check(lib.drt_ce_fwd(S.data_ptr(), m, n, int(target_stride), float(scale), lse.data_ptr(),
+                                     rl.data_ptr(), loss.data_ptr(), _native.stream_ptr(S.device)), "drt_ce_fwd")
+        ctx.save_for_backward(qf, pf, S, lse)
+        ctx.target_stride = int(target_stride)
+        ctx.scale = float(scale)
+        ctx.in_dtypes = (q.dtype, p.dtype)
+        ctx.mark_non_differentiable(S)
+        return loss, S
+
+    @staticmethod
+    def backward(ctx, g_loss, g_scores):
+        qf, pf, S, lse = ctx.saved_tensors
+        lib = _native.load()
+        m, n = S.shape
+        g = g_loss.detach().to(torch.float32).contiguous().reshape(1)
+        dS = torch.empty_like(S)
+        _native.check(lib.drt_ce_bwd(S.data_ptr(), lse.data_ptr(), m, n, ctx.target_stride, g.data_ptr(),
+                                     ctx.scale, dS.data_ptr(), _native.stream_ptr(S.device)), "drt_ce_bwd")
+        dq = gemm_nt_f32(dS, transpose_f32(pf))            # [m, d] = dS [m,n] . p [n,d]
+        dp = gemm_nt_f32(transpose_f32(dS), transpose_f32(qf))  # [n, d] = dS^T [n,m] . q [m,d]
+        return dq.to(ctx.in_dtypes[0]), dp.to(ctx.in_dtypes[1]), None, None
+
+
+def score_ce(q: torch.Tensor, p: torch.Tensor, target_stride: int, scale: float = 1.0):
+    """(loss, scores) for in-batch negatives with target_i = i * target_stride."""
+    return ScoreCE.apply(q, p, target_stride, scale)

@@ -83,6 +83,57 @@ int drt_gemm_nt_bf16_f32(const void* A, const void* B, float* C, int64_t m, int6
                          int32_t d, int64_t ldc, void* stream);
 
 /* ------------------------------------------------------------------------
+ * Bi-encoder forward building blocks (DRModel.encode, biencoder.py:127-151,
+ * over HF BertModel; BERT post-LN layer = linear(QKV) -> attention ->
+ * linear(out, +bias +residual, fp32) -> layernorm -> linear(FFN1, GELU) ->
+ * linear(FFN2, +bias +residual, fp32) -> layernorm).
+ * ------------------------------------------------------------------------
+ * drt_embed_ln: out[B*L, H] bf16 = LN(word_emb[ids] + type_emb[type_ids or 0]
+ *   + pos_emb[l]) (modeling_bert.py:53-107); tables/LN params fp32, H % 256 == 0.
+ * drt_linear_bf16: Y = X . W^T (+bias)(GELU)(+residual); X [M,K], W [N,K] bf16,
+ *   bias fp32 [N] or NULL, residual bf16 [M,N] or NULL; flags bit0 = GELU(erf),
+ *   bit1 = fp32 output (else bf16).  K % 64 == 0.
+ * drt_layernorm_f32_bf16: out bf16 = LN(X fp32 [M,H]).
+ * drt_attention_bf16: ctx[B*L, heads*64] = softmax(Q K^T * scale + mask) V per
+ *   head, from packed qkv [B*L, 3*heads*64]; mask int64 [B,L] (1 token, 0 pad)
+ *   or NULL; L <= 512, head_dim == 64.
+ * drt_pool_bf16: reps fp32 [B,H] (+ optional bf16 copy) from hidden bf16
+ *   [B,L,H]; mode 0 first, 1 masked mean, 2 max(hidden*mask) (utils.py:233-240).
+ * drt_l2_normalize_f32: in place x /= max(||x||_2, 1e-12) per row.          */
+int drt_embed_ln(const int64_t* ids, const int64_t* type_ids, int64_t B, int64_t L,
+                 const float* word_emb, const float* pos_emb, const float* type_emb,
+                 const float* gamma, const float* beta, float eps, int32_t H, void* out,
+                 void* stream);
+int drt_linear_bf16(const void* X, const void* W, const float* bias, const void* residual,
+                    void* Y, int64_t M, int64_t N, int64_t K, int32_t flags, void* stream);
+int drt_layernorm_f32_bf16(const float* X, int64_t M, int32_t H, const float* gamma,
+                           const float* beta, float eps, void* out, void* stream);
+int drt_attention_bf16(const void* qkv, const int64_t* mask, void* ctx, int64_t B, int64_t L,
+                       int32_t heads, int32_t head_dim, float scale, void* stream);
+int drt_pool_bf16(const void* hidden, const int64_t* mask, int64_t B, int64_t L, int32_t H,
+                  int32_t mode, float* out, void* out_bf16, void* stream);
+int drt_l2_normalize_f32(float* x, int64_t B, int32_t H, void* out_bf16, void* stream);
+
+/* ------------------------------------------------------------------------
+ * In-batch-negative training loss (DRModel.forward, biencoder.py:107-119;
+ * SimpleContrastiveLoss, losses.py:11-17), fp32 like the reference.
+ * ------------------------------------------------------------------------
+ * drt_gemm_nt_f32: C[m,n] = A[m,k] . B[n,k]^T on the exact-f32 MFMA.
+ * drt_ce_fwd: per row lse_i = log sum_j exp(S_ij), row_loss_i = lse_i - S_i,t
+ *   with t = i * target_stride; *loss = scale * mean_i row_loss_i
+ *   (deterministic order).  All device pointers.
+ * drt_ce_bwd: dS_ij = grad * scale / m * (softmax(S)_ij - [j == t]); grad is
+ *   a device scalar (NULL = 1).
+ * drt_transpose_f32: Y[cols, rows] = X[rows, cols]^T.                       */
+int drt_gemm_nt_f32(const float* A, const float* B, float* C, int64_t m, int64_t n, int64_t k,
+                    int64_t lda, int64_t ldb, int64_t ldc, void* stream);
+int drt_ce_fwd(const float* S, int64_t m, int64_t n, int64_t target_stride, float scale,
+               float* lse, float* row_loss, float* loss, void* stream);
+int drt_ce_bwd(const float* S, const float* lse, int64_t m, int64_t n, int64_t target_stride,
+               const float* grad, float scale, float* dS, void* stream);
+int drt_transpose_f32(const float* X, int64_t rows, int64_t cols, float* Y, void* stream);
+
+/* ------------------------------------------------------------------------
  * Launch timing (measurement support for bench.py's roofline figure).
  * When enabled, every launch of the named kernel family is bracketed by a
  * pair of hipEvents recorded on the stream it is launched on.

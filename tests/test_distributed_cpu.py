@@ -1,0 +1,94 @@
+"""Multi-rank (gloo, CPU) tests of the sharded-index logic: offsets, all-gather of
+per-shard top-k, merge == single-index result.  The per-rank shard scan and the
+merge are injected with the oracle here (the HIP versions are covered by the GPU
+tests); what is under test is the distributed bookkeeping of ShardedFlatIP."""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+from oracle import search_oracle as orc
+
+
+class _OracleShard:
+    """Test double for FlatIPIndex on CPU (oracle scan)."""
+
+    def __init__(self, d):
+        self.d = d
+        self.rows = np.zeros((0, d), np.float32)
+        self.device = torch.device("cpu")
+
+    @property
+    def ntotal(self):
+        return self.rows.shape[0]
+
+    def add(self, x):
+        self.rows = np.concatenate([self.rows, np.asarray(x, np.float32)], 0)
+
+    def search_device(self, q, k, id_offset=0):
+        s, i = orc.ip_topk(np.asarray(q, np.float32), self.rows, k, id_offset=id_offset)
+        return torch.from_numpy(s), torch.from_numpy(i)
+
+
+def _oracle_merge(s_all, i_all, k):
+    s, i = orc.merge_topk(s_all.numpy(), i_all.numpy(), k)
+    return torch.from_numpy(s), torch.from_numpy(i)
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _worker(rank, world, port, n, d, k, nq, out_q):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from denseretrievaltoolkits_amd.search import ShardedFlatIP
+    rng = np.random.default_rng(0)
+    p = rng.integers(-3, 4, size=(n, d)).astype(np.float32)
+    q = rng.integers(-3, 4, size=(nq, d)).astype(np.float32)
+    lo, hi = orc.shard_bounds(n, world, rank)
+    idx = ShardedFlatIP(d, local=_OracleShard(d), merge=_oracle_merge)
+    idx.add_shard(p[lo:hi])
+    assert idx.offset == lo and idx.ntotal == n
+    s, i = idx.search_device(q, k)
+    es, ei = orc.ip_topk(q, p, k)
+    ok = bool(np.array_equal(i.numpy(), ei) and np.array_equal(s.numpy(), es))
+    out_q.put((rank, ok))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,n", [(2, 1001), (3, 50), (4, 7)])
+def test_sharded_search_equals_single_index(world, n):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, n, 16, 20, 5, q)) for r in range(world)]
+    for pr in procs:
+        pr.start()
+    res = [q.get(timeout=120) for _ in range(world)]
+    for pr in procs:
+        pr.join(timeout=60)
+        assert pr.exitcode == 0
+    assert all(ok for _, ok in res), res
+
+
+def test_overlay_registers_hot_path_modules():
+    import sys
+    from denseretrievaltoolkits_amd import drt_overlay
+    names = drt_overlay.install()
+    import DRT.evaluator.index as idx_mod
+    import DRT.model.biencoder as bi
+    assert idx_mod.BaseFaissIPRetriever.__module__ == "denseretrievaltoolkits_amd.evaluator.index"
+    assert bi.DRModel.__module__ == "denseretrievaltoolkits_amd.model.biencoder"
+    assert set(names) == set(drt_overlay.HOT_PATH_MODULES)
+    for n in list(sys.modules):
+        if n == "DRT" or n.startswith("DRT."):
+            del sys.modules[n]
