@@ -621,25 +621,144 @@ __device__ __forceinline__ void block_bitonic_u32(uint32_t* buf, int n2, int nth
   }
 }
 
+// Best r keys of one 4096-key chunk.  Keys live in registers (8 per thread);
+// a 256-bin histogram linear in the score value (per-wave sub-histograms)
+// finds the bin holding rank r, only the keys in the bins up to it (~r + a
+// few) are gathered and sorted.  Degenerate chunks (> 1024 keys tied around
+// rank r) fall back to sorting the whole chunk.
+constexpr int kKthPer = kKthChunk / kKthThreads;   // 8 keys per thread
+constexpr int kKthBins = 256;
+constexpr int kKthSel = 1024;
+
 __global__ __launch_bounds__(kKthThreads) void kth_partial_kernel(const uint32_t* in, int64_t stride, int64_t n,
                                                                   int r, uint32_t* part) {
   __shared__ __attribute__((aligned(16))) uint32_t buf[kKthChunk];
+  __shared__ uint32_t hist[kKthThreads / 64][kKthBins];
+  __shared__ float red[2][kKthThreads / 64];
+  __shared__ uint32_t sh_n;
+  __shared__ int sh_bin;
+  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
   const int64_t q = blockIdx.y;
   const int nchunk = gridDim.x;
   const int64_t j0 = (int64_t)blockIdx.x * kKthChunk;
-  const int64_t cnt64 = n - j0 < kKthChunk ? n - j0 : kKthChunk;
-  const int cnt = (int)cnt64;
+  const int cnt = (int)(n - j0 < kKthChunk ? n - j0 : kKthChunk);
   const uint32_t* src = in + q * stride + j0;
-  // rows are 16-B aligned (stride % 4 == 0, j0 % 4096 == 0): vector loads, tail scalar
-  const int nv = cnt >> 2;
-  for (int i = threadIdx.x; i < nv; i += kKthThreads) *(u32x4*)(buf + 4 * i) = *(const u32x4*)(src + 4 * i);
-  for (int i = 4 * nv + threadIdx.x; i < kKthChunk; i += kKthThreads) buf[i] = i < cnt ? src[i] : 0xFFFFFFFFu;
+
+  uint32_t key[kKthPer];
+  // thread t holds keys 4t..4t+3 and 2048+4t..2048+4t+3 (two coalesced 16-B loads)
+#pragma unroll
+  for (int v = 0; v < 2; ++v) {
+    const int base = v * (kKthChunk / 2) + 4 * tid;
+    if (base + 3 < cnt) {
+      const u32x4 x = *(const u32x4*)(src + base);
+#pragma unroll
+      for (int u = 0; u < 4; ++u) key[4 * v + u] = x[u];
+    } else {
+#pragma unroll
+      for (int u = 0; u < 4; ++u) key[4 * v + u] = base + u < cnt ? src[base + u] : 0xFFFFFFFFu;
+    }
+  }
+  // score range over real keys
+  float hi = -__builtin_inff(), lo = __builtin_inff();
+#pragma unroll
+  for (int e = 0; e < kKthPer; ++e) {
+    if (key[e] != 0xFFFFFFFFu) {
+      const float sc = desc_key_to_score(key[e]);
+      hi = fmaxf(hi, sc);
+      lo = fminf(lo, sc);
+    }
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    hi = fmaxf(hi, __shfl_xor(hi, o, 64));
+    lo = fminf(lo, __shfl_xor(lo, o, 64));
+  }
+  if (lane == 0) {
+    red[0][wave] = hi;
+    red[1][wave] = lo;
+  }
+  for (int i = tid; i < (kKthThreads / 64) * kKthBins; i += kKthThreads) (&hist[0][0])[i] = 0;
   __syncthreads();
+#pragma unroll
+  for (int w = 0; w < kKthThreads / 64; ++w) {
+    hi = fmaxf(hi, red[0][w]);
+    lo = fminf(lo, red[1][w]);
+  }
+  const float range = hi - lo;
+  const float scale = (range > 0.0f && range < __builtin_inff()) ? (float)kKthBins / range : 0.0f;
+  // bin 0 = best scores
+  int bins[kKthPer];
+#pragma unroll
+  for (int e = 0; e < kKthPer; ++e) {
+    int bb = kKthBins;  // padding
+    if (key[e] != 0xFFFFFFFFu) {
+      const float f = (hi - desc_key_to_score(key[e])) * scale;
+      bb = (int)f;
+      bb = bb < 0 ? 0 : (bb > kKthBins - 1 ? kKthBins - 1 : bb);
+      atomicAdd(&hist[wave][bb], 1u);
+    }
+    bins[e] = bb;
+  }
+  __syncthreads();
+  if (tid < 64) {
+    uint32_t c4[4];
+    uint32_t s4 = 0;
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+      uint32_t v = 0;
+#pragma unroll
+      for (int w = 0; w < kKthThreads / 64; ++w) v += hist[w][4 * tid + t];
+      c4[t] = v;
+      s4 += v;
+    }
+    uint32_t incl = s4;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const uint32_t v = __shfl_up(incl, o, 64);
+      if (tid >= o) incl += v;
+    }
+    uint32_t run = incl - s4;
+    if (tid == 63 && incl < (uint32_t)r) sh_bin = kKthBins - 1;  // fewer than r real keys: take all
+    if (run < (uint32_t)r && (uint32_t)r <= incl) {
+#pragma unroll
+      for (int t = 0; t < 4; ++t) {
+        if (run + c4[t] >= (uint32_t)r) {
+          sh_bin = 4 * tid + t;
+          break;
+        }
+        run += c4[t];
+      }
+    }
+  }
+  if (tid == 0) sh_n = 0;
+  __syncthreads();
+  const int b = sh_bin;
+  // gather keys of bins <= b
+#pragma unroll
+  for (int e = 0; e < kKthPer; ++e) {
+    if (bins[e] <= b) {
+      const uint32_t pos = atomicAdd(&sh_n, 1u);
+      if (pos < (uint32_t)kKthSel) buf[pos] = key[e];
+    }
+  }
+  __syncthreads();
+  int nsel = (int)sh_n;
+  if (nsel > kKthSel) {
+    // degenerate: sort the whole chunk
+    __syncthreads();
+#pragma unroll
+    for (int v = 0; v < 2; ++v)
+#pragma unroll
+      for (int u = 0; u < 4; ++u) buf[v * (kKthChunk / 2) + 4 * tid + u] = key[4 * v + u];
+    nsel = kKthChunk;
+  }
   int n2 = 1;
-  while (n2 < cnt) n2 <<= 1;
+  while (n2 < nsel) n2 <<= 1;
+  for (int i = nsel + tid; i < n2; i += kKthThreads) buf[i] = 0xFFFFFFFFu;
+  __syncthreads();
   block_bitonic_u32(buf, n2, kKthThreads);
   uint32_t* o = part + (q * nchunk + blockIdx.x) * r;
-  for (int i = threadIdx.x; i < r; i += kKthThreads) o[i] = i < cnt ? buf[i] : 0xFFFFFFFFu;
+  for (int i = tid; i < r; i += kKthThreads) o[i] = i < nsel ? buf[i] : 0xFFFFFFFFu;
 }
 
 __global__ __launch_bounds__(kKthThreads) void kth_final_kernel(const uint32_t* part, int nchunk, int r,
