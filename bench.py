@@ -45,6 +45,7 @@ def parse():
     ap.add_argument("--cpu-rows", type=int, default=1_000_000)
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--encode", action="store_true", help="also time the bf16 BERT-base passage encoder")
+    ap.add_argument("--scan-variant", type=int, default=0, help="benchmark-only ablation of the scan kernel")
     return ap.parse_args()
 
 
@@ -127,6 +128,7 @@ def main():
     from denseretrievaltoolkits_amd import _native, kernels
 
     lib = _native.load()
+    lib.drt_scan_variant(args.scan_variant)
     d, k, qb = args.dim, args.k, args.qb
     shard, lo, hi = gen_shard(args.n_corpus, world, rank, d, dev)
     n_local = hi - lo
@@ -226,7 +228,7 @@ def main():
                 "parallelism": f"row-shard x{world}",
             },
             "roofline": {
-                "kernel": "ip_scan_kernel<768,FILTER> (csrc/search.hip)",
+                "kernel": "ip_scan16_kernel<768,FILTER,0,8> (csrc/search.hip)",
                 "bound": "hbm",
                 "achieved": round(achieved, 1),
                 "peak": HBM_PEAK_GBS,

@@ -33,6 +33,7 @@ _SIGNATURES = [
     ("drt_ip_topk_workspace", c_sz, [c_i64, c_i64, c_i32, c_i32]),
     ("drt_ip_topk_bf16", c_i32, [c_vp, c_i64, c_vp, c_i64, c_i32, c_i32, c_i64, c_vp, c_vp, c_vp, c_vp, c_sz, c_vp]),
     ("drt_ip_topk_resolve", c_i32, [c_vp, c_i64, c_vp, c_i64, c_i32, c_i32, c_i64, c_vp, c_vp, c_vp, c_vp, c_vp]),
+    ("drt_scan_variant", c_i32, [c_i32]),
     ("drt_topk_merge", c_i32, [c_vp, c_vp, c_i64, c_i32, c_i32, c_i32, c_vp, c_vp, c_vp]),
     ("drt_gemm_nt_bf16_f32", c_i32, [c_vp, c_vp, c_vp, c_i64, c_i64, c_i32, c_i64, c_vp]),
     ("drt_embed_ln", c_i32, [c_vp, c_vp, c_i64, c_i64, c_vp, c_vp, c_vp, c_vp, c_vp, c_f32, c_i32, c_vp, c_vp]),
@@ -41,6 +42,7 @@ _SIGNATURES = [
     ("drt_attention_bf16", c_i32, [c_vp, c_vp, c_vp, c_i64, c_i64, c_i32, c_i32, c_f32, c_vp]),
     ("drt_pool_bf16", c_i32, [c_vp, c_vp, c_i64, c_i64, c_i32, c_i32, c_vp, c_vp, c_vp]),
     ("drt_l2_normalize_f32", c_i32, [c_vp, c_i64, c_i32, c_vp, c_vp]),
+    ("drt_gemm_force_small", c_i32, [c_i32]),
     ("drt_gemm_nt_f32", c_i32, [c_vp, c_vp, c_vp, c_i64, c_i64, c_i64, c_i64, c_i64, c_i64, c_vp]),
     ("drt_ce_fwd", c_i32, [c_vp, c_i64, c_i64, c_i64, c_f32, c_vp, c_vp, c_vp, c_vp]),
     ("drt_ce_bwd", c_i32, [c_vp, c_vp, c_i64, c_i64, c_i64, c_vp, c_f32, c_vp, c_vp]),

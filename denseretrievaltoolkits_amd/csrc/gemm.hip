@@ -73,6 +73,8 @@ __device__ __forceinline__ float gelu_erf(float x) {
 
 enum { EPI_NONE = 0, EPI_BIAS = 1, EPI_GELU = 2, EPI_RESID = 4 };
 
+static int g_gemm_variant = 0;  // A/B switch: 0 auto (large full-K), 1 small 128^2, 2 large half-K ring
+
 template <bool OUT_BF16, int EPI>
 __global__ __launch_bounds__(kGemmThreads, 2) void gemm_nt_kernel(GemmArgs a) {
   __shared__ __attribute__((aligned(16))) char smem[kGemmLds];
@@ -162,11 +164,268 @@ __global__ __launch_bounds__(kGemmThreads, 2) void gemm_nt_kernel(GemmArgs a) {
   }
 }
 
+// ---------------------------------------------------------------------------
+// Large-tile variant for the encoder projections (M = tokens >> 256).
+//  * 256 x 256 output tile, 8 waves (2 along M x 4 along N), wave tile 128 x 64.
+//  * K streamed in half-tiles of 32: A and B halves (256 rows x 64 B each,
+//    16 KiB) land by LDS-DMA in a 4-slot ring (128 KiB); three half-tiles stay
+//    in flight across the raw s_barrier (counted vmcnt, never 0 in the loop).
+//  * operands swapped (D = W . X^T): each lane owns one token row and four
+//    consecutive output columns per register group, so the epilogue issues
+//    16-B (fp32) / 8-B (bf16) stores and 16-B bias / 8-B residual loads.
+// LDS half-tile image: [row][4 x 16 B], chunk XOR-swizzled by (row >> 2) & 3
+// (conflict-free ds_read_b128 for 32-row fragment reads).
+// ---------------------------------------------------------------------------
+constexpr int kL = 256;                  // tile edge
+constexpr int kLThreads = 512;
+constexpr int kLHalf = kL * 32 * 2;      // 16 KiB: one operand, 32 k
+constexpr int kLSlot = 2 * kLHalf;       // A half + B half
+constexpr int kLSlots = 4;
+constexpr int kLGlds = 2 * kLHalf / 1024 / 8;   // LDS-DMA instructions per wave per slot (4)
+
+// 256 rows x 32 k: 16 wave-instructions of 16 rows x 64 B, 2 per wave.
+__device__ __forceinline__ void stage_half256(const __bf16* base, int64_t ld, int64_t row0, int64_t rows,
+                                              int64_t k0, uint32_t lds, int wave, int lane) {
+  const int rsub = lane >> 2, pos = lane & 3;
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    const int J = j * 8 + wave;           // 0..15
+    const int row = J * 16 + rsub;        // 0..255
+    int64_t gr = row0 + row;
+    gr = gr < rows ? gr : rows - 1;
+    const int c = pos ^ ((row >> 2) & 3);
+    g_glds16(base + gr * ld + k0 + c * 8, __builtin_amdgcn_readfirstlane(lds + J * 1024));
+  }
+}
+
+template <bool OUT_BF16, int EPI>
+__global__ __launch_bounds__(kLThreads, 1) void gemm_nt_lh_kernel(GemmArgs a) {
+  __shared__ __attribute__((aligned(16))) char smem[kLSlots * kLSlot];
+  const int tid = threadIdx.x;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int lane = tid & 63;
+  const int r = lane & 31, h = lane >> 5;
+  const int wm = wave >> 2, wn = wave & 3;   // 2 x 4 waves
+
+  const int nwg = gridDim.x;
+  const int bid = blockIdx.x;
+  const int xcd = bid & 7, q8 = nwg >> 3, r8 = nwg & 7;
+  const int wg = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (bid >> 3);
+  const int tiles_n = (int)((a.n + kL - 1) / kL);
+  const int64_t m0 = (int64_t)(wg / tiles_n) * kL;
+  const int64_t n0 = (int64_t)(wg % tiles_n) * kL;
+
+  const uint32_t lds0 = g_lds_addr(smem);
+  const int nh = (int)(a.k / 32);   // half-tiles
+
+  // acc[j][i]: D rows = W rows (n), cols = X rows (m)
+  f32x16 acc[2][4];
+#pragma unroll
+  for (int j = 0; j < 2; ++j)
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int e = 0; e < 16; ++e) acc[j][i][e] = 0.0f;
+
+  const int sw = (r >> 2) & 3;
+  int aoff[2];
+#pragma unroll
+  for (int s = 0; s < 2; ++s) aoff[s] = r * 64 + ((((2 * s) | h) ^ sw) << 4);
+
+  // prologue: three half-tiles in flight
+#pragma unroll
+  for (int p = 0; p < 3; ++p) {
+    if (p < nh) {
+      const uint32_t sl = lds0 + p * kLSlot;
+      stage_half256(a.A, a.lda, m0, a.m, (int64_t)p * 32, sl, wave, lane);
+      stage_half256(a.B, a.ldb, n0, a.n, (int64_t)p * 32, sl + kLHalf, wave, lane);
+    }
+  }
+
+  for (int hs = 0; hs < nh; ++hs) {
+    const int younger = nh - 1 - hs;   // half-tiles issued after this one (<= 2)
+    if (younger >= 2) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+    else if (younger == 1) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    if (hs + 3 < nh) {
+      const uint32_t sl = lds0 + ((hs + 3) & 3) * kLSlot;
+      stage_half256(a.A, a.lda, m0, a.m, (int64_t)(hs + 3) * 32, sl, wave, lane);
+      stage_half256(a.B, a.ldb, n0, a.n, (int64_t)(hs + 3) * 32, sl + kLHalf, wave, lane);
+    }
+    const char* Xs = smem + (hs & 3) * kLSlot + wm * 128 * 64;            // A panel (tokens)
+    const char* Ws = smem + (hs & 3) * kLSlot + kLHalf + wn * 64 * 64;    // B panel (weights)
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      bf16x8 wf[2], xf[4];
+#pragma unroll
+      for (int j = 0; j < 2; ++j) wf[j] = *(const bf16x8*)(Ws + j * 32 * 64 + aoff[s]);
+#pragma unroll
+      for (int i = 0; i < 4; ++i) xf[i] = *(const bf16x8*)(Xs + i * 32 * 64 + aoff[s]);
+      __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+      for (int j = 0; j < 2; ++j)
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+          acc[j][i] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wf[j], xf[i], acc[j][i], 0, 0, 0);
+      __builtin_amdgcn_s_setprio(0);
+    }
+  }
+
+  l_epilogue<OUT_BF16, EPI>(a, acc, m0, n0, wm, wn, r, h);
+}
+
+// Full-K-tile large kernel: BK = 64, 128-B row image ([row][8 x 16 B], chunk
+// XOR (row >> 1) & 7), 2-slot ring (2 x 64 KiB), one vmcnt(0) + barrier per
+// K-tile, next K-tile staged before the current one's MFMAs; swapped-operand
+// epilogue as above.
+__device__ __forceinline__ void stage_full256(const __bf16* base, int64_t ld, int64_t row0, int64_t rows,
+                                              int64_t k0, uint32_t lds, int wave, int lane) {
+  const int rsub = lane >> 3, pos = lane & 7;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int J = j * 8 + wave;           // 0..31
+    const int row = J * 8 + rsub;         // 0..255
+    int64_t gr = row0 + row;
+    gr = gr < rows ? gr : rows - 1;
+    const int c = pos ^ ((row >> 1) & 7);
+    g_glds16(base + gr * ld + k0 + c * 8, __builtin_amdgcn_readfirstlane(lds + J * 1024));
+  }
+}
+
+template <bool OUT_BF16, int EPI>
+__device__ __forceinline__ void l_epilogue(const GemmArgs& a, f32x16 (&acc)[2][4], int64_t m0, int64_t n0, int wm,
+                                           int wn, int r, int h) {
+  const bool full_n = (n0 + kL <= a.n) && (a.ldc % 4 == 0) && (!(EPI & EPI_RESID) || a.ldr % 4 == 0);
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+      const int64_t col = n0 + wn * 64 + j * 32 + 8 * g + 4 * h;
+      f32x4 bv = {0.f, 0.f, 0.f, 0.f};
+      if (EPI & EPI_BIAS) {
+        if (full_n) bv = *(const f32x4*)(a.bias + col);
+        else
+#pragma unroll
+          for (int u = 0; u < 4; ++u) bv[u] = col + u < a.n ? a.bias[col + u] : 0.f;
+      }
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int64_t row = m0 + wm * 128 + i * 32 + r;
+        if (row >= a.m) continue;
+        f32x4 v;
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          float x = acc[j][i][4 * g + u] * a.alpha + bv[u];
+          if (EPI & EPI_GELU) x = gelu_erf(x);
+          v[u] = x;
+        }
+        if (full_n) {
+          if (EPI & EPI_RESID) {
+            const bf16x4 rv = *(const bf16x4*)(a.R + row * a.ldr + col);
+#pragma unroll
+            for (int u = 0; u < 4; ++u) v[u] += (float)rv[u];
+          }
+          if (OUT_BF16) {
+            bf16x4 o;
+#pragma unroll
+            for (int u = 0; u < 4; ++u) o[u] = (__bf16)v[u];
+            *(bf16x4*)((__bf16*)a.C + row * a.ldc + col) = o;
+          } else {
+            *(f32x4*)((float*)a.C + row * a.ldc + col) = v;
+          }
+        } else {
+#pragma unroll
+          for (int u = 0; u < 4; ++u) {
+            if (col + u >= a.n) continue;
+            float x = v[u];
+            if (EPI & EPI_RESID) x += (float)a.R[row * a.ldr + col + u];
+            if (OUT_BF16) ((__bf16*)a.C)[row * a.ldc + col + u] = (__bf16)x;
+            else ((float*)a.C)[row * a.ldc + col + u] = x;
+          }
+        }
+      }
+    }
+  }
+}
+
+template <bool OUT_BF16, int EPI>
+__global__ __launch_bounds__(kLThreads, 1) void gemm_nt_l_kernel(GemmArgs a) {
+  constexpr int kPanel = kL * kBK * 2;   // 32 KiB
+  constexpr int kStageL = 2 * kPanel;
+  __shared__ __attribute__((aligned(16))) char smem[2 * kStageL];
+  const int tid = threadIdx.x;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int lane = tid & 63;
+  const int r = lane & 31, h = lane >> 5;
+  const int wm = wave >> 2, wn = wave & 3;
+  const int nwg = gridDim.x;
+  const int bid = blockIdx.x;
+  const int xcd = bid & 7, q8 = nwg >> 3, r8 = nwg & 7;
+  const int wg = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (bid >> 3);
+  const int tiles_n = (int)((a.n + kL - 1) / kL);
+  const int64_t m0 = (int64_t)(wg / tiles_n) * kL;
+  const int64_t n0 = (int64_t)(wg % tiles_n) * kL;
+  const uint32_t lds0 = g_lds_addr(smem);
+  const int ksteps = (int)(a.k / kBK);
+  f32x16 acc[2][4];
+#pragma unroll
+  for (int j = 0; j < 2; ++j)
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int e = 0; e < 16; ++e) acc[j][i][e] = 0.0f;
+  const int sw = (r >> 1) & 7;
+  int aoff[4];
+#pragma unroll
+  for (int s = 0; s < 4; ++s) aoff[s] = r * 128 + ((((2 * s) | h) ^ sw) << 4);
+  stage_full256(a.A, a.lda, m0, a.m, 0, lds0, wave, lane);
+  stage_full256(a.B, a.ldb, n0, a.n, 0, lds0 + kPanel, wave, lane);
+  for (int kt = 0; kt < ksteps; ++kt) {
+    const int slot = kt & 1;
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    if (kt + 1 < ksteps) {
+      const uint32_t nb = lds0 + (slot ^ 1) * kStageL;
+      stage_full256(a.A, a.lda, m0, a.m, (int64_t)(kt + 1) * kBK, nb, wave, lane);
+      stage_full256(a.B, a.ldb, n0, a.n, (int64_t)(kt + 1) * kBK, nb + kPanel, wave, lane);
+    }
+    const char* Xs = smem + slot * kStageL + wm * 128 * 128;
+    const char* Ws = smem + slot * kStageL + kPanel + wn * 64 * 128;
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+      bf16x8 wf[2], xf[4];
+#pragma unroll
+      for (int j = 0; j < 2; ++j) wf[j] = *(const bf16x8*)(Ws + j * 32 * 128 + aoff[s]);
+#pragma unroll
+      for (int i = 0; i < 4; ++i) xf[i] = *(const bf16x8*)(Xs + i * 32 * 128 + aoff[s]);
+      __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+      for (int j = 0; j < 2; ++j)
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+          acc[j][i] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wf[j], xf[i], acc[j][i], 0, 0, 0);
+      __builtin_amdgcn_s_setprio(0);
+    }
+  }
+  l_epilogue<OUT_BF16, EPI>(a, acc, m0, n0, wm, wn, r, h);
+}
+
 template <bool OUT_BF16, int EPI>
 static int launch_gemm_t(const GemmArgs& a, hipStream_t s) {
-  const int64_t tiles = ((a.m + kBM - 1) / kBM) * ((a.n + kBN - 1) / kBN);
   const ProfPair pp = prof_begin(PROF_GEMM, s);
-  hipLaunchKernelGGL((gemm_nt_kernel<OUT_BF16, EPI>), dim3((unsigned)tiles), dim3(kGemmThreads), 0, s, a);
+  // large tiles once there are >= 2 tiles per CU of them; small problems keep 128^2
+  const int64_t tiles_l = ((a.m + kL - 1) / kL) * ((a.n + kL - 1) / kL);
+  if (tiles_l >= 512 && g_gemm_variant == 0) {
+    hipLaunchKernelGGL((gemm_nt_l_kernel<OUT_BF16, EPI>), dim3((unsigned)tiles_l), dim3(kLThreads), 0, s, a);
+  } else if (tiles_l >= 512 && g_gemm_variant == 2) {
+    hipLaunchKernelGGL((gemm_nt_lh_kernel<OUT_BF16, EPI>), dim3((unsigned)tiles_l), dim3(kLThreads), 0, s, a);
+  } else {
+    const int64_t tiles = ((a.m + kBM - 1) / kBM) * ((a.n + kBN - 1) / kBN);
+    hipLaunchKernelGGL((gemm_nt_kernel<OUT_BF16, EPI>), dim3((unsigned)tiles), dim3(kGemmThreads), 0, s, a);
+  }
   prof_end(pp, s);
   return hip_status(hipGetLastError());
 }
@@ -241,4 +500,12 @@ extern "C" int drt_linear_bf16(const void* X, const void* W, const float* bias, 
   a.alpha = 1.0f;
   const int epi = (bias ? EPI_BIAS : 0) | (gelu ? EPI_GELU : 0) | (residual ? EPI_RESID : 0);
   return launch_gemm(a, !f32, epi, (hipStream_t)stream);
+}
+
+// Testing / benchmarking switch: 0 = automatic, 1 = 128^2 kernel for every size,
+// 2 = large half-K-ring kernel where the large kernel applies.
+extern "C" int drt_gemm_force_small(int32_t on) {
+  if (on < 0 || on > 2) return DRT_EINVAL;
+  g_gemm_variant = on;
+  return DRT_OK;
 }

@@ -137,17 +137,18 @@ __device__ __forceinline__ void push_hit(const ScanArgs& a, int q_local,
   }
 }
 
+template <int NT = kScanThreads>
 __device__ __forceinline__ void flush_hits(const ScanArgs& a, int64_t qbase, uint32_t n,
                                            const uint64_t* hk, const uint16_t* hq) {
   n = n < (uint32_t)kHitCap ? n : (uint32_t)kHitCap;
-  for (uint32_t i = threadIdx.x; i < n; i += kScanThreads) {
+  for (uint32_t i = threadIdx.x; i < n; i += NT) {
     const int64_t q = qbase + hq[i];
     const uint32_t g = atomicAdd(a.counts + q, 1u);
     if (g < (uint64_t)a.cap) ((uint64_t*)a.out)[q * a.cap + g] = hk[i];
   }
 }
 
-template <int D, int MODE>
+template <int D, int MODE, bool NOMMA = false>
 __global__ __launch_bounds__(kScanThreads, 1) void ip_scan_kernel(ScanArgs a) {
   using C = ScanCfg<D>;
   __shared__ __attribute__((aligned(16))) char smem[C::LDS_BYTES];
@@ -233,10 +234,16 @@ __global__ __launch_bounds__(kScanThreads, 1) void ip_scan_kernel(ScanArgs a) {
     f32x16 acc;
 #pragma unroll
     for (int i = 0; i < 16; ++i) acc[i] = 0.0f;
+    if (NOMMA) {
+      // ablation (memory-pipeline ceiling): touch the tile, no MFMA, no hits
+      const bf16x8 af = *(const bf16x8*)(tb + aoff[0]);
+      acc[0] = -__builtin_inff() + 0.0f * (float)af[0];
+    } else {
 #pragma unroll
-    for (int s = 0; s < C::KS; ++s) {
-      const bf16x8 af = *(const bf16x8*)(tb + (s >> 2) * (kTileRows * 128) + aoff[s & 3]);
-      acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af, qf[s], acc, 0, 0, 0);
+      for (int s = 0; s < C::KS; ++s) {
+        const bf16x8 af = *(const bf16x8*)(tb + (s >> 2) * (kTileRows * 128) + aoff[s & 3]);
+        acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af, qf[s], acc, 0, 0, 0);
+      }
     }
 
     // acc[i]: query column r, corpus row (i&3) + 8*(i>>2) + 4*h of the tile.
@@ -283,6 +290,236 @@ __global__ __launch_bounds__(kScanThreads, 1) void ip_scan_kernel(ScanArgs a) {
   if (MODE == SCAN_FILTER) {
     lds_barrier();
     flush_hits(a, qbase, *hit_n, hk, hq);
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Production scan: 16-row tiles on v_mfma_f32_16x16x32_bf16, 6-slot LDS ring
+// (prefetch distance 5: up to 5 x 24 KiB in flight per CU while the waves
+// compute, vs 2 x 48 KiB for the 32-row ring above).
+//   B operand (queries, VGPR-resident): lane l holds Q[q0 + 16 b + (l&15)]
+//     [32 s + 8 (l>>4) .. +8] for column block b = 0, 1 and k-step s.
+//   A operand (corpus, LDS): lane l reads row (l&15), 16-B chunk 4 s + (l>>4).
+//   D: lane l holds query (l&15) of block b, rows 4 (l>>4) + 0..3.
+// LDS image per tile: [chunk group g][row 0..15][8 x 16 B], chunk position
+// XOR (row >> 1) & 7 -> conflict-free ds_read_b128 (all 4 lane groups).
+// ---------------------------------------------------------------------------
+constexpr int kT16 = 16;
+
+template <int D, int NW = 4>
+struct Scan16Cfg {
+  static constexpr int KS = D / 32;                         // 16x16x32 k-steps
+  static constexpr int TILE_BYTES = kT16 * D * 2;            // 24 KiB at d = 768
+  static constexpr int GLDS_PER_TILE = TILE_BYTES / 1024;
+  // every wave issues the same count (vmcnt bookkeeping); the remainder
+  // instructions are duplicates of earlier ones (same bytes, same LDS address)
+  static constexpr int GLDS_PER_WAVE = (GLDS_PER_TILE + NW - 1) / NW;   // 6 (4 waves) / 3 (8 waves) at d = 768
+  static constexpr int HITS_BYTES = kHitCap * 10 + 16;
+  static constexpr int NBUF_RAW = (160 * 1024 - HITS_BYTES) / TILE_BYTES;
+  static constexpr int NBUF = NBUF_RAW > 8 ? 8 : NBUF_RAW;
+  static constexpr int PD = NBUF - 1;
+  static constexpr int RING_BYTES = NBUF * TILE_BYTES;
+  static constexpr int HIT_KEY_OFF = RING_BYTES;
+  static constexpr int HIT_Q_OFF = HIT_KEY_OFF + kHitCap * 8;
+  static constexpr int HIT_N_OFF = HIT_Q_OFF + kHitCap * 2;
+  static constexpr int LDS_BYTES = HIT_N_OFF + 16;
+  static_assert(D % 64 == 0 && D <= 1024, "d");
+  static_assert(NBUF >= 3, "ring too small");
+  static_assert(LDS_BYTES <= 160 * 1024, "LDS budget");
+};
+
+template <int D, int NW>
+__device__ __forceinline__ void issue_tile16(const ScanArgs& a, uint32_t buf_lds, int64_t tile, int wave, int lane) {
+  using C = Scan16Cfg<D, NW>;
+  const int rsub = lane >> 3, pos = lane & 7;
+#pragma unroll
+  for (int j = 0; j < C::GLDS_PER_WAVE; ++j) {
+    int J = j * NW + wave;                   // wave-instruction index in the tile
+    if (C::GLDS_PER_TILE % NW != 0 && J >= C::GLDS_PER_TILE) J -= C::GLDS_PER_TILE;
+    const int g = J >> 1;                    // chunk group (2 instructions each)
+    const int row = ((J & 1) << 3) + rsub;   // 0..15
+    int64_t li = tile * kT16 + row;
+    li = li < a.nrows ? li : a.nrows - 1;
+    const int c = pos ^ ((row >> 1) & 7);
+    const __bf16* src = a.P + (a.row0 + li * a.rstride) * a.ldp + g * 64 + c * 8;
+    glds16(src, __builtin_amdgcn_readfirstlane(buf_lds + J * 1024));
+  }
+}
+
+template <int N>
+__device__ __forceinline__ void wait_tiles_younger(int younger) {
+  // this wave has `younger` tiles issued after the one it needs; each is N instructions
+  switch (younger) {
+    case 0: asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); break;
+    case 1: asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory"); break;
+    case 2: asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * N) : "memory"); break;
+    case 3: asm volatile("s_waitcnt vmcnt(%0)" ::"n"(3 * N < 63 ? 3 * N : 63) : "memory"); break;
+    case 4: asm volatile("s_waitcnt vmcnt(%0)" ::"n"(4 * N < 63 ? 4 * N : 63) : "memory"); break;
+    case 5: asm volatile("s_waitcnt vmcnt(%0)" ::"n"(5 * N < 63 ? 5 * N : 63) : "memory"); break;
+    default: asm volatile("s_waitcnt vmcnt(%0)" ::"n"(6 * N < 63 ? 6 * N : 63) : "memory"); break;
+  }
+}
+
+// ABL (benchmark ablations, FILTER only): 0 production, 1 no MFMA and no filter,
+// 2 MFMA on register operands (no LDS fragment reads), 3 no filter.
+template <int D, int MODE, int ABL = 0, int NW = 4>
+__global__ __launch_bounds__(NW * 64, 1) void ip_scan16_kernel(ScanArgs a) {
+  using C = Scan16Cfg<D, NW>;
+  constexpr int QB = 128 / (NW * 16);   // 16-query column blocks per wave
+  __shared__ __attribute__((aligned(16))) char smem[C::LDS_BYTES];
+  uint64_t* hk = (uint64_t*)(smem + C::HIT_KEY_OFF);
+  uint16_t* hq = (uint16_t*)(smem + C::HIT_Q_OFF);
+  uint32_t* hit_n = (uint32_t*)(smem + C::HIT_N_OFF);
+
+  const int tid = threadIdx.x;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int lane = tid & 63;
+  const int r = lane & 15;      // A row / D column (query within block)
+  const int kq = lane >> 4;     // k-quarter (A/B) / row quad (D)
+
+  const int64_t qbase = (int64_t)blockIdx.y * kQueriesPerWG;
+  const int64_t ntiles = (a.nrows + kT16 - 1) / kT16;
+  const int64_t t0 = blockIdx.x;
+  const int64_t tstep = gridDim.x;
+  const int64_t my_tiles = t0 < ntiles ? (ntiles - 1 - t0) / tstep + 1 : 0;
+  if (my_tiles == 0) return;
+  if (MODE == SCAN_FILTER && tid == 0) *hit_n = 0;
+  const uint32_t ring = lds_addr_of(smem);
+
+  // queries of this wave: qbase + 16 * QB * wave + 16 * b + r
+  int qloc[QB];
+  int64_t qg[QB];
+  bool qok[QB];
+  bf16x8 qf[C::KS][QB];
+  float tau[QB];
+#pragma unroll
+  for (int b = 0; b < QB; ++b) {
+    qloc[b] = wave * 16 * QB + 16 * b + r;
+    qg[b] = qbase + qloc[b];
+    qok[b] = qg[b] < a.nq;
+    const int64_t qs = qok[b] ? qg[b] : 0;
+#pragma unroll
+    for (int s = 0; s < C::KS; ++s) qf[s][b] = *(const bf16x8*)(a.Q + qs * a.ldq + s * 32 + kq * 8);
+    tau[b] = __builtin_nanf("");
+    if (MODE == SCAN_FILTER) {
+      const float tv = a.tau[qs];
+      tau[b] = qok[b] ? tv : tau[b];
+    }
+    if (!qok[b]) {
+#pragma unroll
+      for (int s = 0; s < C::KS; ++s) qf[s][b] = (bf16x8){};
+    }
+  }
+  // Consume every fragment here so hipcc places its vmcnt waits for these loads
+  // in the prologue; otherwise it waits at their first use INSIDE the loop,
+  // where the counts it computes ignore the asm LDS-DMA and drain the ring.
+#pragma unroll
+  for (int s = 0; s < C::KS; ++s)
+#pragma unroll
+    for (int b = 0; b < QB; ++b) asm volatile("" ::"v"(qf[s][b]));
+#pragma unroll
+  for (int b = 0; b < QB; ++b) asm volatile("" ::"v"(tau[b]));
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+
+  // prologue: PD tiles in flight
+#pragma unroll
+  for (int p = 0; p < C::PD; ++p)
+    if (p < my_tiles) issue_tile16<D, NW>(a, ring + p * C::TILE_BYTES, t0 + p * tstep, wave, lane);
+
+  // A-fragment address: chunk 4s + kq of row r, group s >> 1, position (4(s&1) + kq) ^ sw
+  const int sw = (r >> 1) & 7;
+  int aoff[2];
+#pragma unroll
+  for (int m = 0; m < 2; ++m) aoff[m] = r * 128 + (((4 * m + kq) ^ sw) << 4);
+
+  int buf = 0;
+  int nslot = C::PD;   // slot of tile it + PD (== slot of it - 1)
+  for (int64_t it = 0; it < my_tiles; ++it) {
+    const int64_t tile = t0 + it * tstep;
+    const int64_t younger = my_tiles - 1 - it;
+    wait_tiles_younger<C::GLDS_PER_WAVE>((int)(younger < C::PD - 1 ? younger : C::PD - 1));
+    lds_barrier();
+
+    if (MODE == SCAN_FILTER) {
+      const uint32_t n = *hit_n;
+      if (n >= (uint32_t)(kHitCap / 2)) {
+        flush_hits<NW * 64>(a, qbase, n, hk, hq);
+        lds_barrier();
+        if (tid == 0) *hit_n = 0;
+        lds_barrier();
+      }
+    }
+    if (it + C::PD < my_tiles)
+      issue_tile16<D, NW>(a, ring + nslot * C::TILE_BYTES, tile + C::PD * tstep, wave, lane);
+
+    const char* tb = smem + buf * C::TILE_BYTES;
+    f32x4 acc[QB];
+#pragma unroll
+    for (int b = 0; b < QB; ++b) acc[b] = (f32x4){0.f, 0.f, 0.f, 0.f};
+    if (ABL == 1) {
+      const bf16x8 af = *(const bf16x8*)(tb + aoff[0]);
+      asm volatile("" ::"v"(af));
+    } else if (ABL == 2) {
+      const bf16x8 af = *(const bf16x8*)(tb + aoff[0]);
+#pragma unroll
+      for (int s = 0; s < C::KS; ++s)
+#pragma unroll
+        for (int b = 0; b < QB; ++b) acc[b] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af, qf[s][b], acc[b], 0, 0, 0);
+    } else {
+#pragma unroll
+      for (int s = 0; s < C::KS; ++s) {
+        const bf16x8 af = *(const bf16x8*)(tb + (s >> 1) * (kT16 * 128) + aoff[s & 1]);
+#pragma unroll
+        for (int b = 0; b < QB; ++b) acc[b] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af, qf[s][b], acc[b], 0, 0, 0);
+      }
+    }
+
+    const int64_t rowbase = tile * kT16 + 4 * kq;
+    if (ABL == 1 || ABL == 3) {
+#pragma unroll
+      for (int b = 0; b < QB; ++b) asm volatile("" ::"v"(acc[b]));
+    } else if (MODE == SCAN_FILTER) {
+      float mx = -__builtin_inff();
+#pragma unroll
+      for (int b = 0; b < QB; ++b)
+        mx = fmaxf(mx, fmaxf(fmaxf(acc[b][0], acc[b][1]), fmaxf(acc[b][2], acc[b][3])) - tau[b]);
+      if (__ballot(mx >= 0.0f) != 0ull) {
+#pragma unroll
+        for (int b = 0; b < QB; ++b) {
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            const int64_t row = rowbase + j;
+            if (acc[b][j] >= tau[b] && row < a.nrows) {
+              const uint64_t key = ((uint64_t)desc_key(acc[b][j]) << 32) | (uint64_t)(uint32_t)row;
+              push_hit(a, qloc[b], qg[b], key, hit_n, hk, hq);
+            }
+          }
+        }
+      }
+    } else {
+#pragma unroll
+      for (int b = 0; b < QB; ++b) {
+        if (!qok[b]) continue;
+        uint32_t* o = (uint32_t*)a.out + qg[b] * a.cap;
+        u32x4 v;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) v[j] = desc_key(acc[b][j]);
+        if (rowbase + 3 < a.nrows) {
+          *(u32x4*)(o + rowbase) = v;
+        } else {
+#pragma unroll
+          for (int j = 0; j < 4; ++j)
+            if (rowbase + j < a.nrows) o[rowbase + j] = v[j];
+        }
+      }
+    }
+    buf = (buf + 1 == C::NBUF) ? 0 : buf + 1;
+    nslot = (nslot + 1 == C::NBUF) ? 0 : nslot + 1;
+  }
+
+  if (MODE == SCAN_FILTER) {
+    lds_barrier();
+    flush_hits<NW * 64>(a, qbase, *hit_n, hk, hq);
   }
 }
 
@@ -953,13 +1190,38 @@ static int scan_grid_x(int64_t ntiles) {
   return (int)std::max<int64_t>(g, 1);
 }
 
+static int g_scan_variant = 0;  // testing/benchmark switch (drt_scan_variant)
+
 template <int D>
 static int launch_scan_d(const ScanArgs& a, int mode, hipStream_t s) {
+  if (a.nq == 0 || a.nrows == 0) return DRT_OK;
+  const dim3 block(kScanThreads);
+  const unsigned gy = (unsigned)((a.nq + kQueriesPerWG - 1) / kQueriesPerWG);
+  if (g_scan_variant == 0 || g_scan_variant >= 3) {
+    const int64_t ntiles = (a.nrows + kT16 - 1) / kT16;
+    dim3 grid(scan_grid_x(ntiles), gy);
+    if (mode == SCAN_FILTER && D == 768 && g_scan_variant == 3)
+      hipLaunchKernelGGL((ip_scan16_kernel<D, SCAN_FILTER, 1>), grid, block, 0, s, a);
+    else if (mode == SCAN_FILTER && D == 768 && g_scan_variant == 4)
+      hipLaunchKernelGGL((ip_scan16_kernel<D, SCAN_FILTER, 2>), grid, block, 0, s, a);
+    else if (mode == SCAN_FILTER && D == 768 && g_scan_variant == 5)
+      hipLaunchKernelGGL((ip_scan16_kernel<D, SCAN_FILTER, 3>), grid, block, 0, s, a);
+    else if (mode == SCAN_FILTER && g_scan_variant == 6)
+      hipLaunchKernelGGL((ip_scan16_kernel<D, SCAN_FILTER, 0, 4>), grid, block, 0, s, a);
+    else if (mode == SCAN_DENSE && g_scan_variant == 6)
+      hipLaunchKernelGGL((ip_scan16_kernel<D, SCAN_DENSE, 0, 4>), grid, block, 0, s, a);
+    else if (mode == SCAN_FILTER)  // production: 8 waves (2 per SIMD), 16 queries each
+      hipLaunchKernelGGL((ip_scan16_kernel<D, SCAN_FILTER, 0, 8>), grid, dim3(512), 0, s, a);
+    else
+      hipLaunchKernelGGL((ip_scan16_kernel<D, SCAN_DENSE, 0, 8>), grid, dim3(512), 0, s, a);
+    return hip_status(hipGetLastError());
+  }
   const int64_t ntiles = (a.nrows + kTileRows - 1) / kTileRows;
-  if (ntiles == 0 || a.nq == 0) return DRT_OK;
-  dim3 grid(scan_grid_x(ntiles), (unsigned)((a.nq + kQueriesPerWG - 1) / kQueriesPerWG));
-  if (mode == SCAN_FILTER) hipLaunchKernelGGL((ip_scan_kernel<D, SCAN_FILTER>), grid, dim3(kScanThreads), 0, s, a);
-  else hipLaunchKernelGGL((ip_scan_kernel<D, SCAN_DENSE>), grid, dim3(kScanThreads), 0, s, a);
+  dim3 grid(scan_grid_x(ntiles), gy);
+  if (mode == SCAN_FILTER && g_scan_variant == 1 && D == 768)
+    hipLaunchKernelGGL((ip_scan_kernel<D, SCAN_FILTER, true>), grid, block, 0, s, a);
+  else if (mode == SCAN_FILTER) hipLaunchKernelGGL((ip_scan_kernel<D, SCAN_FILTER>), grid, block, 0, s, a);
+  else hipLaunchKernelGGL((ip_scan_kernel<D, SCAN_DENSE>), grid, block, 0, s, a);
   return hip_status(hipGetLastError());
 }
 
@@ -1020,6 +1282,17 @@ using namespace drt;
 extern "C" {
 
 const char* drt_version(void) { return "drt-mi355x 0.1 (gfx950)"; }
+
+// Testing/benchmark switch: 0 = production (16-row tiles, 6-slot ring, 8 waves),
+// 6 = the same with 4 waves,
+// 1 = 32-row FILTER scan without MFMA (memory-pipeline ceiling; results are
+// meaningless), 2 = previous 32-row / 3-slot kernel; 3/4/5 = 16-row kernel
+// ablations (no MFMA / no LDS fragment reads / no filter; d = 768 only).
+int drt_scan_variant(int32_t v) {
+  if (v < 0 || v > 6) return DRT_EINVAL;
+  g_scan_variant = v;
+  return DRT_OK;
+}
 
 size_t drt_ip_topk_workspace(int64_t nq, int64_t n, int32_t d, int32_t k) {
   if (!valid_dims(nq, n, d, k)) return 0;

@@ -68,6 +68,12 @@ int drt_ip_topk_resolve(const void* Q, int64_t nq, const void* P, int64_t n, int
                         int32_t k, int64_t id_offset, float* out_scores, int64_t* out_ids,
                         int32_t* status, int64_t* n_resolved, void* stream);
 
+/* Benchmark/test switch: 0 = production scan (16-row tiles, 6-slot ring),
+ * 1 = filter scan WITHOUT its MFMA work (memory-pipeline ceiling; results are
+ * meaningless), 2 = the previous 32-row / 3-slot scan kernel, 3/4/5 = 16-row
+ * ablations (no MFMA / no LDS reads / no filter), 6 = 16-row with 4 waves.  */
+int drt_scan_variant(int32_t v);
+
 /* Merge `nparts` per-shard top-k lists into one global top-k.
  * scores/ids: [nparts, nq, k_in] (each part sorted score desc, id asc, as
  * drt_ip_topk_bf16 writes them); out: [nq, k_out], k_out <= k_in*nparts,
@@ -113,6 +119,9 @@ int drt_attention_bf16(const void* qkv, const int64_t* mask, void* ctx, int64_t 
 int drt_pool_bf16(const void* hidden, const int64_t* mask, int64_t B, int64_t L, int32_t H,
                   int32_t mode, float* out, void* out_bf16, void* stream);
 int drt_l2_normalize_f32(float* x, int64_t B, int32_t H, void* out_bf16, void* stream);
+/* A/B switch for tests/bench: 0 automatic, 1 forces the 128x128-tile GEMM,
+ * 2 selects the half-K-ring variant of the 256x256-tile GEMM.               */
+int drt_gemm_force_small(int32_t on);
 
 /* ------------------------------------------------------------------------
  * In-batch-negative training loss (DRModel.forward, biencoder.py:107-119;

@@ -90,3 +90,37 @@ def test_linear_epilogues_vs_torch(dev):
     o32 = torch.empty(M, N, dtype=torch.float32, device=dev)
     _native.check(lib.drt_linear_bf16(xd.data_ptr(), wd.data_ptr(), bd.data_ptr(), rd.data_ptr(), o32.data_ptr(), M, N, K, 2, s), "resid")
     torch.testing.assert_close(o32.cpu(), ref + r.float(), atol=2e-3, rtol=1e-4)
+
+
+@pytest.mark.parametrize("M,N,K,flags", [(16384, 2304, 768, 0), (32768, 768, 3072, 2), (20000, 3072, 768, 1),
+                                          (131072, 768, 768, 2)])
+def test_large_tile_gemm_vs_torch_and_small_kernel(dev, M, N, K, flags):
+    """256x256-tile kernel (>= 512 tiles) against torch fp32 and the 128x128 kernel."""
+    import torch
+    from denseretrievaltoolkits_amd import _native
+    lib = _native.load()
+    g = torch.Generator(device=dev).manual_seed(M + N)
+    x = torch.randn(M, K, generator=g, device=dev).to(torch.bfloat16)
+    w = (0.05 * torch.randn(N, K, generator=g, device=dev)).to(torch.bfloat16)
+    b = torch.randn(N, generator=g, device=dev)
+    r = torch.randn(M, N, generator=g, device=dev).to(torch.bfloat16) if flags == 2 else None
+    ref = x.float() @ w.float().T + b
+    if flags == 1:
+        ref = torch.nn.functional.gelu(ref)
+    if r is not None:
+        ref = ref + r.float()
+    dt = torch.float32 if flags & 2 else torch.bfloat16
+    outs = []
+    for force in (0, 1, 2):
+        lib.drt_gemm_force_small(force)
+        out = torch.empty(M, N, dtype=dt, device=dev)
+        _native.check(lib.drt_linear_bf16(x.data_ptr(), w.data_ptr(), b.data_ptr(),
+                                          r.data_ptr() if r is not None else None, out.data_ptr(), M, N, K, flags,
+                                          _native.stream_ptr(dev)), "linear")
+        outs.append(out.float())
+    lib.drt_gemm_force_small(0)
+    tol = dict(atol=2e-3, rtol=1e-4) if dt == torch.float32 else dict(atol=3e-2, rtol=1e-2)
+    torch.testing.assert_close(outs[0], ref, **tol)
+    # both kernels accumulate each k-step in the same order -> identical fp32 results
+    if dt == torch.float32:
+        assert torch.equal(outs[0], outs[1]) and torch.equal(outs[0], outs[2])

@@ -22,7 +22,7 @@ run() {  # run <name> <timeout> cmd...
 }
 
 if [ "${SKIP_TESTS:-0}" != "1" ]; then
-  run pytest_gpu ${TEST_TIMEOUT:-900} python -m pytest tests -m gpu -q -rfE --timeout 600 ${PYTEST_ARGS:-}
+  run pytest_gpu ${TEST_TIMEOUT:-900} python -m pytest ${TEST_PATHS:-tests} -m gpu -q -rfE --timeout 600 ${PYTEST_ARGS:-}
   rc=$?
   if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then echo "STOP: pytest rc=$rc"; exit $rc; fi
 fi
@@ -38,4 +38,16 @@ if [ "${SKIP_PROF:-0}" != "1" ]; then
   run_prof; rc=$?
   echo "=== rocprof rc=$rc" | tee -a $GRAFT_REPO_ROOT/$OUT/session.log
   find $GRAFT_REPO_ROOT/$OUT/prof_$TAG -name "*stats*" | head
+fi
+if [ "${PMC:-0}" = "1" ]; then
+  cd /tmp
+  for C in FETCH_SIZE WRITE_SIZE; do
+    timeout -k 10 600 rocprofv3 --pmc $C --output-format csv -d $GRAFT_REPO_ROOT/$OUT/pmc_${TAG}_$C -o run \
+      -- python3 $GRAFT_REPO_ROOT/bench.py --steps 3 --warmup 1 --no-cpu-baseline > $GRAFT_REPO_ROOT/$OUT/pmc_${TAG}_$C.log 2>&1
+    rc=$?; echo "=== pmc $C rc=$rc" | tee -a $GRAFT_REPO_ROOT/$OUT/session.log
+    [ $rc -ne 0 ] && exit $rc
+  done
+fi
+if [ "${GEMMB:-0}" = "1" ]; then
+  cd $GRAFT_REPO_ROOT && timeout -k 10 300 python tools/gemm_bench.py > $OUT/gemm_bench.log 2>&1; echo "=== gemm_bench rc=$?"; tail -2 $OUT/gemm_bench.log
 fi
