@@ -10,9 +10,13 @@ tower, DRModel.encode, DRT/model/biencoder.py:127-151).
 
 One step = one query batch (Qb = 128, the reference's eval batch,
 arguments.py:189) searched exactly against the WHOLE corpus (k = 1000):
-every rank scans its contiguous row shard (10M / N rows, resident in HBM),
-the per-shard top-k lists are all-gathered over RCCL and merged on device.
-The corpus is fixed as N grows ("scaling": "strong").
+every rank scans its contiguous row shard (10M / N rows, resident in HBM).
+For N > 1 the shards run the global-threshold protocol (search.py
+ShardedFlatIP): all-gather of the tiny per-shard sample lists -> one corpus
+threshold, filter scan of the shard against it, all-gather of the packed
+per-shard top-k (u64 score-key|id) and a device merge that certifies
+exactness; an uncertified batch is redone with the per-shard exact path
+inside the timed region.  The corpus is fixed as N grows ("scaling": "strong").
 
 Launch: python bench.py [--gpus N --steps K --warmup W]; for N > 1 under
 torch.distributed.run (one process per GPU, RCCL).
@@ -46,6 +50,11 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--encode", action="store_true", help="also time the bf16 BERT-base passage encoder")
     ap.add_argument("--scan-variant", type=int, default=0, help="benchmark-only ablation of the scan kernel")
+    ap.add_argument("--streams", type=int, default=2,
+                    help="HIP streams the query batches rotate over (overlaps one batch's exchange and small "
+                         "kernels with the next batch's scan)")
+    ap.add_argument("--protocol", choices=["global_tau", "per_shard"], default="global_tau",
+                    help="N > 1 exchange protocol (per_shard = exact top-k per shard + merge)")
     return ap.parse_args()
 
 
@@ -55,9 +64,17 @@ def init_dist(n_gpus):
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    # DRT_BENCH_BACKEND=gloo: rehearsal of the N > 1 logic with several ranks
+    # sharing one GPU (collectives staged through host memory; not a measurement)
+    backend = os.environ.get("DRT_BENCH_BACKEND", "nccl")
+    if backend == "gloo":
+        local = local % max(1, torch.cuda.device_count())
     torch.cuda.set_device(local)
     if world > 1:
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if backend == "gloo":
+            dist.init_process_group("gloo")
+        else:
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
     return rank, world, local
 
 
@@ -140,37 +157,66 @@ def main():
     s_loc = torch.empty((nsteps, qb, k), dtype=torch.float32, device=dev)
     i_loc = torch.empty((nsteps, qb, k), dtype=torch.int64, device=dev)
     st = torch.zeros((nsteps, qb), dtype=torch.int32, device=dev)
-    if world > 1:
-        s_all = torch.empty((world * qb, k), dtype=torch.float32, device=dev)
-        i_all = torch.empty((world * qb, k), dtype=torch.int64, device=dev)
-    results = []
+    gloo = world > 1 and dist.get_backend() == "gloo"
 
-    def step(j):
+    def all_gather(t):
+        """[world * rows, ...] concatenated all-gather (RCCL on device; host-staged under gloo)."""
+        src = t.contiguous().cpu() if gloo else t.contiguous()
+        out = torch.empty((world * src.shape[0],) + tuple(src.shape[1:]), dtype=src.dtype, device=src.device)
+        dist.all_gather_into_tensor(out, src)
+        return out.to(dev).view((world,) + tuple(t.shape))
+
+    def step_per_shard(j):
         kernels.ip_topk(queries[j], shard, k, id_offset=lo, resolve=False,
                         out=(s_loc[j], i_loc[j]), status=st[j])
         if world > 1:
-            dist.all_gather_into_tensor(s_all, s_loc[j])
-            dist.all_gather_into_tensor(i_all, i_loc[j])
-            return kernels.topk_merge(s_all.view(world, qb, k), i_all.view(world, qb, k), k)
+            return kernels.topk_merge(all_gather(s_loc[j]), all_gather(i_loc[j]), k)
         return s_loc[j], i_loc[j]
 
+    def step_global_tau(j):
+        best = kernels.dist_sample(queries[j], shard, args.n_corpus, k)
+        tau = kernels.dist_tau(all_gather(best), k)
+        packed = kernels.dist_filter(queries[j], shard, args.n_corpus, k, lo, tau)
+        s, i, stj = kernels.merge_packed(all_gather(packed), k, args.n_corpus)
+        st[j] = stj
+        return s, i
+
+    use_global = world > 1 and args.protocol == "global_tau"
+    step = step_global_tau if use_global else step_per_shard
+
     def fix_failures(first, last):
-        """Exact resolve of any uncertified query (counted inside the timed region)."""
+        """Exact redo of any uncertified query batch (counted inside the timed region).
+        Global-tau statuses come from the merged lists, identical on every rank."""
         bad = (st[first:last] != 0).any(dim=1).to(torch.int32)
-        if world > 1:
-            dist.all_reduce(bad, op=dist.ReduceOp.MAX)
+        if world > 1 and not use_global:
+            bad_c = bad.cpu() if gloo else bad
+            dist.all_reduce(bad_c, op=dist.ReduceOp.MAX)
+            bad = bad_c.to(dev)
         nb = 0
         for j in (torch.nonzero(bad).flatten() + first).tolist():
+            if use_global:
+                kernels.ip_topk(queries[j], shard, k, id_offset=lo, resolve=True, out=(s_loc[j], i_loc[j]))
+                kernels.topk_merge(all_gather(s_loc[j]), all_gather(i_loc[j]), k)
+                nb += qb
+                continue
             nb += kernels.resolve_failed(queries[j], shard, k, lo, s_loc[j], i_loc[j], st[j])
-            step_merge_only = world > 1
-            if step_merge_only:
-                dist.all_gather_into_tensor(s_all, s_loc[j])
-                dist.all_gather_into_tensor(i_all, i_loc[j])
-                kernels.topk_merge(s_all.view(world, qb, k), i_all.view(world, qb, k), k)
+            if world > 1:
+                kernels.topk_merge(all_gather(s_loc[j]), all_gather(i_loc[j]), k)
         return nb
 
-    for j in range(args.warmup):
-        step(j)
+    main_stream = torch.cuda.current_stream(dev)
+    streams = [main_stream] + [torch.cuda.Stream(device=dev) for _ in range(max(1, args.streams) - 1)]
+
+    def run_steps(first, last):
+        for s in streams[1:]:
+            s.wait_stream(main_stream)
+        for j in range(first, last):
+            with torch.cuda.stream(streams[j % len(streams)]):
+                step(j)
+        for s in streams[1:]:
+            main_stream.wait_stream(s)
+
+    run_steps(0, args.warmup)
     fix_failures(0, args.warmup)
     torch.cuda.synchronize()
 
@@ -179,8 +225,7 @@ def main():
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    for j in range(args.warmup, nsteps):
-        step(j)
+    run_steps(args.warmup, nsteps)
     n_resolved = fix_failures(args.warmup, nsteps)
     torch.cuda.synchronize()
     if world > 1:
@@ -206,7 +251,7 @@ def main():
         # algorithmic bytes of ONE filter-scan launch on the largest shard:
         # corpus shard (per-row d*2 B) + query block + result lists
         per = -(-args.n_corpus // world)
-        alg_bytes = per * d * 2 + qb * d * 2 + qb * k * 12
+        alg_bytes = per * d * 2 + qb * d * 2 + (qb * (k + 1) * 8 if use_global else qb * k * 12)
         achieved = alg_bytes / (scan_ms_v * 1e-3) / 1e9
         out = {
             "metric": "queries/sec@top-1000, 10Mx768 corpus (BASELINE: passages encoded/sec + queries/sec@top-1000, 10Mx768 corpus, 1/2/4/8 GPU)",
@@ -223,9 +268,13 @@ def main():
             "data": "synthetic: N(0,1) corpus and queries rounded to bf16, generated in HBM (seeded)",
             "config": {
                 "workload": f"exact IP top-{k}, {args.n_corpus} x {d} bf16 corpus row-sharded over {world} GPU(s), "
-                            f"query batch {qb}, RCCL all-gather of per-shard top-k + device merge",
+                            f"query batch {qb}" + (", global-threshold protocol (RCCL all-gather of sample lists "
+                                                   "and packed per-shard top-k, device merge)" if use_global else
+                                                   (", RCCL all-gather of per-shard top-k + device merge"
+                                                    if world > 1 else "")),
                 "n_corpus": args.n_corpus, "dim": d, "query_batch": qb, "k": k,
                 "parallelism": f"row-shard x{world}",
+                "streams": len(streams),
             },
             "roofline": {
                 "kernel": "ip_scan16_kernel<768,FILTER,0,8> (csrc/search.hip)",

@@ -48,6 +48,7 @@ struct ScanArgs {
   uint32_t* counts;   // FILTER: [nq] hit counters (zeroed by the caller)
   void* out;          // FILTER: u64 [nq][cap] keys; DENSE: u32 [nq][cap] desc keys
   int64_t cap;
+  int64_t exp_hits;   // FILTER: expected hits per query (0: cap / 4); picks the append flavour
 };
 
 template <int D>
@@ -134,6 +135,37 @@ __device__ __forceinline__ void push_hit(const ScanArgs& a, int q_local,
   } else {
     const uint32_t g = atomicAdd(a.counts + q, 1u);
     if (g < (uint64_t)a.cap) ((uint64_t*)a.out)[q * a.cap + g] = key;
+  }
+}
+
+// Flush with one global atomic per (work-group, query): LDS counting by query,
+// then per-query reservation, then scatter.  qcnt/qoff: 128-entry LDS scratch.
+template <int NT>
+__device__ __forceinline__ void flush_hits_agg(const ScanArgs& a, int64_t qbase, uint32_t n, const uint64_t* hk,
+                                               const uint16_t* hq, uint32_t* qcnt, uint32_t* qoff) {
+  n = n < (uint32_t)kHitCap ? n : (uint32_t)kHitCap;
+  for (int i = threadIdx.x; i < kQueriesPerWG; i += NT) qcnt[i] = 0;
+  lds_barrier();
+  uint32_t rank[(kHitCap + NT - 1) / NT];
+#pragma unroll
+  for (int u = 0; u < (kHitCap + NT - 1) / NT; ++u) {
+    const uint32_t i = threadIdx.x + u * NT;
+    if (i < n) rank[u] = atomicAdd(&qcnt[hq[i]], 1u);
+  }
+  lds_barrier();
+  for (int q = threadIdx.x; q < kQueriesPerWG; q += NT) {
+    const uint32_t c = qcnt[q];
+    qoff[q] = (c && qbase + q < a.nq) ? atomicAdd(a.counts + qbase + q, c) : 0u;
+  }
+  lds_barrier();
+#pragma unroll
+  for (int u = 0; u < (kHitCap + NT - 1) / NT; ++u) {
+    const uint32_t i = threadIdx.x + u * NT;
+    if (i < n) {
+      const int ql = hq[i];
+      const uint32_t g = qoff[ql] + rank[u];
+      if (g < (uint64_t)a.cap) ((uint64_t*)a.out)[(qbase + ql) * a.cap + g] = hk[i];
+    }
   }
 }
 
@@ -314,7 +346,7 @@ struct Scan16Cfg {
   // every wave issues the same count (vmcnt bookkeeping); the remainder
   // instructions are duplicates of earlier ones (same bytes, same LDS address)
   static constexpr int GLDS_PER_WAVE = (GLDS_PER_TILE + NW - 1) / NW;   // 6 (4 waves) / 3 (8 waves) at d = 768
-  static constexpr int HITS_BYTES = kHitCap * 10 + 16;
+  static constexpr int HITS_BYTES = kHitCap * 10 + 16 + 2 * kQueriesPerWG * 4;
   static constexpr int NBUF_RAW = (160 * 1024 - HITS_BYTES) / TILE_BYTES;
   static constexpr int NBUF = NBUF_RAW > 8 ? 8 : NBUF_RAW;
   static constexpr int PD = NBUF - 1;
@@ -322,7 +354,8 @@ struct Scan16Cfg {
   static constexpr int HIT_KEY_OFF = RING_BYTES;
   static constexpr int HIT_Q_OFF = HIT_KEY_OFF + kHitCap * 8;
   static constexpr int HIT_N_OFF = HIT_Q_OFF + kHitCap * 2;
-  static constexpr int LDS_BYTES = HIT_N_OFF + 16;
+  static constexpr int QCNT_OFF = HIT_N_OFF + 16;
+  static constexpr int LDS_BYTES = QCNT_OFF + 2 * kQueriesPerWG * 4;
   static_assert(D % 64 == 0 && D <= 1024, "d");
   static_assert(NBUF >= 3, "ring too small");
   static_assert(LDS_BYTES <= 160 * 1024, "LDS budget");
@@ -362,7 +395,7 @@ __device__ __forceinline__ void wait_tiles_younger(int younger) {
 
 // ABL (benchmark ablations, FILTER only): 0 production, 1 no MFMA and no filter,
 // 2 MFMA on register operands (no LDS fragment reads), 3 no filter.
-template <int D, int MODE, int ABL = 0, int NW = 4>
+template <int D, int MODE, int ABL = 0, int NW = 4, bool AGG = true>
 __global__ __launch_bounds__(NW * 64, 1) void ip_scan16_kernel(ScanArgs a) {
   using C = Scan16Cfg<D, NW>;
   constexpr int QB = 128 / (NW * 16);   // 16-query column blocks per wave
@@ -370,6 +403,8 @@ __global__ __launch_bounds__(NW * 64, 1) void ip_scan16_kernel(ScanArgs a) {
   uint64_t* hk = (uint64_t*)(smem + C::HIT_KEY_OFF);
   uint16_t* hq = (uint16_t*)(smem + C::HIT_Q_OFF);
   uint32_t* hit_n = (uint32_t*)(smem + C::HIT_N_OFF);
+  uint32_t* qcnt = (uint32_t*)(smem + C::QCNT_OFF);
+  uint32_t* qoff = qcnt + kQueriesPerWG;
 
   const int tid = threadIdx.x;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -443,7 +478,8 @@ __global__ __launch_bounds__(NW * 64, 1) void ip_scan16_kernel(ScanArgs a) {
     if (MODE == SCAN_FILTER) {
       const uint32_t n = *hit_n;
       if (n >= (uint32_t)(kHitCap / 2)) {
-        flush_hits<NW * 64>(a, qbase, n, hk, hq);
+        if (AGG) flush_hits_agg<NW * 64>(a, qbase, n, hk, hq, qcnt, qoff);
+        else flush_hits<NW * 64>(a, qbase, n, hk, hq);
         lds_barrier();
         if (tid == 0) *hit_n = 0;
         lds_barrier();
@@ -484,14 +520,49 @@ __global__ __launch_bounds__(NW * 64, 1) void ip_scan16_kernel(ScanArgs a) {
       for (int b = 0; b < QB; ++b)
         mx = fmaxf(mx, fmaxf(fmaxf(acc[b][0], acc[b][1]), fmaxf(acc[b][2], acc[b][3])) - tau[b]);
       if (__ballot(mx >= 0.0f) != 0ull) {
+        if (AGG) {
+          // wave-aggregated append: one LDS atomic per wave per tile
+          uint32_t m = 0;
 #pragma unroll
-        for (int b = 0; b < QB; ++b) {
+          for (int b = 0; b < QB; ++b)
 #pragma unroll
-          for (int j = 0; j < 4; ++j) {
-            const int64_t row = rowbase + j;
-            if (acc[b][j] >= tau[b] && row < a.nrows) {
-              const uint64_t key = ((uint64_t)desc_key(acc[b][j]) << 32) | (uint64_t)(uint32_t)row;
-              push_hit(a, qloc[b], qg[b], key, hit_n, hk, hq);
+            for (int j = 0; j < 4; ++j)
+              if (acc[b][j] >= tau[b] && rowbase + j < a.nrows) m |= 1u << (4 * b + j);
+          const uint32_t c = __builtin_popcount(m);
+          uint32_t incl = c;
+#pragma unroll
+          for (int o = 1; o < 64; o <<= 1) {
+            const uint32_t v = __shfl_up(incl, o, 64);
+            if (lane >= o) incl += v;
+          }
+          const uint32_t tot = __shfl(incl, 63, 64);
+          uint32_t base = 0;
+          if (lane == 0) base = atomicAdd(hit_n, tot);
+          base = __shfl(base, 0, 64) + incl - c;
+          while (m) {
+            const int bit = __builtin_ctz(m);
+            m &= m - 1;
+            const int b = bit >> 2, j = bit & 3;
+            const uint64_t key = ((uint64_t)desc_key(acc[b][j]) << 32) | (uint64_t)(uint32_t)(rowbase + j);
+            if (base < (uint32_t)kHitCap) {
+              hk[base] = key;
+              hq[base] = (uint16_t)qloc[b];
+            } else {
+              const uint32_t g = atomicAdd(a.counts + qg[b], 1u);
+              if (g < (uint64_t)a.cap) ((uint64_t*)a.out)[qg[b] * a.cap + g] = key;
+            }
+            ++base;
+          }
+        } else {
+#pragma unroll
+          for (int b = 0; b < QB; ++b) {
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+              const int64_t row = rowbase + j;
+              if (acc[b][j] >= tau[b] && row < a.nrows) {
+                const uint64_t key = ((uint64_t)desc_key(acc[b][j]) << 32) | (uint64_t)(uint32_t)row;
+                push_hit(a, qloc[b], qg[b], key, hit_n, hk, hq);
+              }
             }
           }
         }
@@ -519,7 +590,9 @@ __global__ __launch_bounds__(NW * 64, 1) void ip_scan16_kernel(ScanArgs a) {
 
   if (MODE == SCAN_FILTER) {
     lds_barrier();
-    flush_hits<NW * 64>(a, qbase, *hit_n, hk, hq);
+    const uint32_t nf = *hit_n;
+    if (AGG) flush_hits_agg<NW * 64>(a, qbase, nf, hk, hq, qcnt, qoff);
+    else flush_hits<NW * 64>(a, qbase, nf, hk, hq);
   }
 }
 
@@ -546,6 +619,8 @@ constexpr int kSelWaves = kSelThreads / 64;
 constexpr int kSelMaxK = 2048;
 constexpr int kSelBins = 1024;
 constexpr int kSelBuf = 4096;
+constexpr int kSelKPT = 16;                          // keys per thread held in registers
+constexpr int kSelRegCap = kSelKPT * kSelThreads;    // 8192
 
 struct SelectArgs {
   const void* in;
@@ -565,6 +640,10 @@ struct SelectArgs {
   const int32_t* qmap;      // optional: output row for block q (resolve path)
   // KTH output
   float* tau;
+  // distributed protocol: packed output [nq][k + 1] u64 = (desc score key << 32 | global id),
+  // entry k = flags (bit 0: overflow); with a global tau a short local list is not a failure
+  uint64_t* out_packed;
+  bool global_tau;
 };
 
 template <int INPUT>
@@ -626,7 +705,7 @@ __global__ __launch_bounds__(kSelThreads) void select_kernel(SelectArgs a) {
   __shared__ uint64_t sh_prefix, sh_mask;
   __shared__ int64_t sh_kk;
   __shared__ int sh_done, sh_bin;
-  __shared__ uint32_t sh_nsel;
+  __shared__ uint32_t sh_nsel, sh_nside;
   __shared__ __attribute__((aligned(16))) uint64_t buf[kSelBuf];
 
   const int tid = threadIdx.x;
@@ -649,7 +728,115 @@ __global__ __launch_bounds__(kSelThreads) void select_kernel(SelectArgs a) {
 
   bool fast_done = false;   // uniform
   int nsel = 0;             // TOPK: entries in buf
-  if (c > (int64_t)a.k) {
+  if (c > (int64_t)a.k && c <= kSelRegCap) {
+    // every key loaded once (all loads in flight together), passes run on registers
+    uint64_t kr[kSelKPT];
+    float sc[kSelKPT];
+#pragma unroll
+    for (int u = 0; u < kSelKPT; ++u) {
+      const int64_t j = (int64_t)u * kSelThreads + tid;
+      kr[u] = j < c ? sel_load<INPUT>(a, q, j) : ~0ull;
+    }
+    float lo = __builtin_inff(), hi = -__builtin_inff();
+#pragma unroll
+    for (int u = 0; u < kSelKPT; ++u) {
+      sc[u] = key_score(kr[u]);
+      if ((int64_t)u * kSelThreads + tid < c) {
+        lo = fminf(lo, sc[u]);
+        hi = fmaxf(hi, sc[u]);
+      }
+    }
+    lo = block_reduce(lo, fscr, [](float x, float y) { return fminf(x, y); });
+    hi = block_reduce(hi, fscr, [](float x, float y) { return fmaxf(x, y); });
+    const float range = hi - lo;
+    const float scale = (range > 0.0f && range < __builtin_inff()) ? (float)kSelBins / range : 0.0f;
+    for (int i = tid; i < kSelWaves * kSelBins; i += kSelThreads) (&hist[0][0])[i] = 0;
+    __syncthreads();
+    int bn[kSelKPT];
+#pragma unroll
+    for (int u = 0; u < kSelKPT; ++u) {
+      bn[u] = -1;
+      if ((int64_t)u * kSelThreads + tid < c) {
+        bn[u] = score_bin(sc[u], lo, scale);
+        atomicAdd(&hist[wave][bn[u]], 1u);
+      }
+    }
+    __syncthreads();
+    for (int i = tid; i < kSelBins; i += kSelThreads) {
+      uint32_t t = 0;
+#pragma unroll
+      for (int w = 0; w < kSelWaves; ++w) t += hist[w][i];
+      suffix[i] = t;
+    }
+    __syncthreads();
+    for (int off = 1; off < kSelBins; off <<= 1) {
+      uint32_t v[kSelBins / kSelThreads];
+#pragma unroll
+      for (int u = 0; u < kSelBins / kSelThreads; ++u) {
+        const int i = tid + u * kSelThreads;
+        v[u] = suffix[i] + (i + off < kSelBins ? suffix[i + off] : 0u);
+      }
+      __syncthreads();
+#pragma unroll
+      for (int u = 0; u < kSelBins / kSelThreads; ++u) suffix[tid + u * kSelThreads] = v[u];
+      __syncthreads();
+    }
+    if (tid == 0) sh_bin = 0;
+    __syncthreads();
+    for (int i = tid; i < kSelBins; i += kSelThreads) {
+      const bool ok = (int64_t)suffix[i] >= kk_total;
+      const bool next_ok = (i + 1 < kSelBins) && (int64_t)suffix[i + 1] >= kk_total;
+      if (ok && !next_ok) sh_bin = i;
+    }
+    __syncthreads();
+    const int b = sh_bin;
+    if (OUTPUT == SEL_KTH) {
+      float t = __builtin_inff();
+#pragma unroll
+      for (int u = 0; u < kSelKPT; ++u)
+        if (bn[u] >= b) t = fminf(t, sc[u]);
+      t = block_reduce(t, fscr, [](float x, float y) { return fminf(x, y); });
+      if (tid == 0) a.tau[q] = t;
+      return;
+    }
+    const uint32_t cnt_sel = suffix[b];
+    const uint32_t c_above = (b + 1 < kSelBins) ? suffix[b + 1] : 0u;
+    const uint32_t cnt_b = cnt_sel - c_above;
+    if (cnt_b <= (uint32_t)(kSelBuf / 2) && kk_total <= kSelBuf / 2) {
+      uint64_t* side = buf + kSelBuf / 2;
+      if (tid == 0) {
+        sh_nsel = 0;
+        sh_nside = 0;
+      }
+      __syncthreads();
+#pragma unroll
+      for (int u = 0; u < kSelKPT; ++u) {
+        if (bn[u] > b) buf[atomicAdd(&sh_nsel, 1u)] = kr[u];
+        else if (bn[u] == b) side[atomicAdd(&sh_nside, 1u)] = kr[u];
+      }
+      __syncthreads();
+      const int ns = (int)sh_nside;
+      int m2 = 1;
+      while (m2 < ns) m2 <<= 1;
+      for (int i = ns + tid; i < m2; i += kSelThreads) side[i] = ~0ull;
+      __syncthreads();
+      block_bitonic(side, m2);
+      const int need = (int)kk_total - (int)c_above;
+      for (int i = tid; i < need; i += kSelThreads) buf[c_above + i] = side[i];
+      __syncthreads();
+      nsel = (int)kk_total;
+      fast_done = true;
+    } else if (cnt_sel <= (uint32_t)kSelBuf) {
+      if (tid == 0) sh_nsel = 0;
+      __syncthreads();
+#pragma unroll
+      for (int u = 0; u < kSelKPT; ++u)
+        if (bn[u] >= b) buf[atomicAdd(&sh_nsel, 1u)] = kr[u];
+      __syncthreads();
+      nsel = (int)sh_nsel;
+      fast_done = true;
+    }
+  } else if (c > (int64_t)a.k) {
     // ---- A: score range
     float lo = __builtin_inff(), hi = -__builtin_inff();
     for (int64_t j = tid; j < c; j += kSelThreads) {
@@ -711,8 +898,38 @@ __global__ __launch_bounds__(kSelThreads) void select_kernel(SelectArgs a) {
       if (tid == 0) a.tau[q] = t;
       return;
     }
-    if (cnt_sel <= (uint32_t)kSelBuf) {
-      // ---- D(TOPK): gather the upper set, sort, emit
+    const uint32_t c_above = (b + 1 < kSelBins) ? suffix[b + 1] : 0u;   // bins above b: all selected
+    const uint32_t cnt_b = cnt_sel - c_above;                             // boundary bin
+    if (cnt_b <= (uint32_t)(kSelBuf / 2) && kk_total <= kSelBuf / 2) {
+      // ---- D(TOPK): bins > b straight into buf[0, c_above); the boundary bin
+      // into buf[kSelBuf/2, ...), sorted alone, its best (kk - c_above) appended:
+      // exactly kk keys reach the final sort.
+      uint64_t* side = buf + kSelBuf / 2;
+      if (tid == 0) {
+        sh_nsel = 0;
+        sh_nside = 0;
+      }
+      __syncthreads();
+      for (int64_t j = tid; j < c; j += kSelThreads) {
+        const uint64_t x = sel_load<INPUT>(a, q, j);
+        const int bx = score_bin(key_score(x), lo, scale);
+        if (bx > b) buf[atomicAdd(&sh_nsel, 1u)] = x;
+        else if (bx == b) side[atomicAdd(&sh_nside, 1u)] = x;
+      }
+      __syncthreads();
+      const int ns = (int)sh_nside;
+      int m2 = 1;
+      while (m2 < ns) m2 <<= 1;
+      for (int i = ns + tid; i < m2; i += kSelThreads) side[i] = ~0ull;
+      __syncthreads();
+      block_bitonic(side, m2);
+      const int need = (int)kk_total - (int)c_above;
+      for (int i = tid; i < need; i += kSelThreads) buf[c_above + i] = side[i];
+      __syncthreads();
+      nsel = (int)kk_total;
+      fast_done = true;
+    } else if (cnt_sel <= (uint32_t)kSelBuf) {
+      // ---- D(TOPK): gather the whole upper set, sort, emit
       if (tid == 0) sh_nsel = 0;
       __syncthreads();
       for (int64_t j = tid; j < c; j += kSelThreads) {
@@ -807,6 +1024,19 @@ __global__ __launch_bounds__(kSelThreads) void select_kernel(SelectArgs a) {
   block_bitonic(buf, n2);
 
   const int64_t orow = a.qmap ? (int64_t)a.qmap[q] : q;
+  if (a.out_packed) {
+    uint64_t* op = a.out_packed + orow * (int64_t)(a.k + 1);
+    for (int j = tid; j < a.k; j += kSelThreads) {
+      if (j < kk_total) {
+        const uint64_t x = buf[j];
+        op[j] = (x & 0xFFFFFFFF00000000ull) | (uint64_t)(uint32_t)(a.id_offset + (int64_t)(x & 0xFFFFFFFFull));
+      } else {
+        op[j] = ~0ull;
+      }
+    }
+    if (tid == 0) op[a.k] = (INPUT == SEL_KEYS64 && c_raw > a.cap) ? 1ull : 0ull;
+    return;
+  }
   float* os = a.out_scores + orow * a.ldo;
   int64_t* oi = a.out_ids + orow * a.ldo;
   for (int j = tid; j < a.k; j += kSelThreads) {
@@ -822,8 +1052,8 @@ __global__ __launch_bounds__(kSelThreads) void select_kernel(SelectArgs a) {
   if (a.status && tid == 0) {
     int st = 0;
     if (INPUT == SEL_KEYS64) {
-      if (c_raw > a.cap) st = 1;                                     // overflow
-      if (c_raw < (int64_t)a.k && c_raw < a.n_total) st = 1;          // threshold too high
+      if (c_raw > a.cap) st = 1;                                                       // overflow
+      if (!a.global_tau && c_raw < (int64_t)a.k && c_raw < a.n_total) st = 1;          // threshold too high
     }
     a.status[orow] = st;
   }
@@ -998,20 +1228,155 @@ __global__ __launch_bounds__(kKthThreads) void kth_partial_kernel(const uint32_t
   for (int i = tid; i < r; i += kKthThreads) o[i] = i < nsel ? buf[i] : 0xFFFFFFFFu;
 }
 
-__global__ __launch_bounds__(kKthThreads) void kth_final_kernel(const uint32_t* part, int nchunk, int r,
-                                                                float* tau) {
+// Element i of list l for query q lives at part[l * lstride + q * qstride + i], i < r.
+// Writes tau[q] (r-th best score; -inf if fewer than r real keys) and/or the
+// sorted best r keys best[q * r + i].
+__global__ __launch_bounds__(kKthThreads) void kth_final_kernel(const uint32_t* part, int nlists, int r,
+                                                                int64_t lstride, int64_t qstride, float* tau,
+                                                                uint32_t* best) {
   __shared__ uint32_t buf[kKthChunk];
   const int64_t q = blockIdx.x;
-  const int tot = nchunk * r;
-  for (int i = threadIdx.x; i < kKthChunk; i += kKthThreads) buf[i] = i < tot ? part[q * tot + i] : 0xFFFFFFFFu;
+  const int tot = nlists * r;
+  for (int i = threadIdx.x; i < kKthChunk; i += kKthThreads)
+    buf[i] = i < tot ? part[(int64_t)(i / r) * lstride + q * qstride + (i % r)] : 0xFFFFFFFFu;
   __syncthreads();
   int n2 = 1;
   while (n2 < tot) n2 <<= 1;
   block_bitonic_u32(buf, n2, kKthThreads);
-  if (threadIdx.x == 0) {
+  if (tau && threadIdx.x == 0) {
     const uint32_t kr = buf[r - 1];
     tau[q] = (kr == 0xFFFFFFFFu) ? -__builtin_inff() : desc_key_to_score(kr);
   }
+  if (best)
+    for (int i = threadIdx.x; i < r; i += kKthThreads) best[q * r + i] = buf[i];
+}
+
+// Tree merge of packed per-shard lists: all P2 = pow2ceil(nparts) lists of k
+// sorted keys sit in LDS (missing lists = pads); log2(P2) rounds merge pairs
+// in place (every element computes its rank in the merged pair with one
+// binary search, all reads finish before the barrier, survivors (rank < k) are
+// written after it).  EPT = elements per thread in round 0 (P2 * k / 512).
+constexpr int kTreeThreads = 512;
+
+template <int EPT>
+__global__ __launch_bounds__(kTreeThreads) void merge_packed_tree_kernel(const uint64_t* parts, int64_t nq,
+                                                                         int nparts, int p2, int k,
+                                                                         int64_t n_global, float* out_s,
+                                                                         int64_t* out_i, int32_t* status) {
+  extern __shared__ __attribute__((aligned(16))) uint64_t L[];  // [p2][k]
+  __shared__ int bad;
+  const int tid = threadIdx.x;
+  const int64_t q = blockIdx.x;
+  const int64_t ps = (int64_t)(k + 1);
+  if (tid == 0) bad = 0;
+  __syncthreads();
+  for (int e = tid; e < p2 * k; e += kTreeThreads) {
+    const int l = e / k, i = e - l * k;
+    L[e] = l < nparts ? parts[((int64_t)l * nq + q) * ps + i] : ~0ull;
+  }
+  if (tid < nparts && (parts[((int64_t)tid * nq + q) * ps + k] & 1ull)) bad = 1;
+  __syncthreads();
+  for (int half = 1; half < p2; half <<= 1) {
+    // pair g merges slot 2g*half (A) with slot (2g+1)*half (B) into slot 2g*half
+    const int npairs = p2 / (2 * half);
+    const int nel = npairs * 2 * k;
+    uint64_t key[EPT];
+    int pos[EPT];
+#pragma unroll
+    for (int t = 0; t < EPT; ++t) {
+      const int e = tid + t * kTreeThreads;
+      pos[t] = -1;
+      if (e < nel) {
+        const int g = e / (2 * k), w = e - g * 2 * k;
+        const int side = w >= k, i = w - side * k;
+        const uint64_t* A = L + (int64_t)(2 * g) * half * k;
+        const uint64_t* B = A + (int64_t)half * k;
+        const uint64_t* other = side ? A : B;
+        const uint64_t x = (side ? B : A)[i];
+        int lo = 0, hi = k;
+        if (!side) {       // #B < x
+          while (lo < hi) { const int mid = (lo + hi) >> 1; if (other[mid] < x) lo = mid + 1; else hi = mid; }
+        } else {           // #A <= x
+          while (lo < hi) { const int mid = (lo + hi) >> 1; if (other[mid] <= x) lo = mid + 1; else hi = mid; }
+        }
+        const int r = i + lo;
+        if (r < k) {
+          key[t] = x;
+          pos[t] = (2 * g) * half * k + r;
+        }
+      }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int t = 0; t < EPT; ++t)
+      if (pos[t] >= 0) L[pos[t]] = key[t];
+    __syncthreads();
+  }
+  for (int i = tid; i < k; i += kTreeThreads) {
+    const uint64_t x = L[i];
+    if (x == ~0ull) {
+      out_s[q * k + i] = kPadScore;
+      out_i[q * k + i] = -1;
+    } else {
+      out_s[q * k + i] = desc_key_to_score((uint32_t)(x >> 32));
+      out_i[q * k + i] = (int64_t)(x & 0xFFFFFFFFull);
+    }
+  }
+  if (status && tid == 0) status[q] = (bad || (L[k - 1] == ~0ull && n_global >= (int64_t)k)) ? 1 : 0;
+}
+
+// Merge of packed per-shard lists [nparts][nq][k + 1] (sorted u64 keys, entry k =
+// flags) into (score, id) [nq][k]; status[q] = 1 unless exact: the k-th merged
+// entry is real (>= k candidates over all shards, so the global tau was <= the
+// k-th score) and no shard overflowed.
+__global__ __launch_bounds__(512) void merge_packed_kernel(const uint64_t* parts, int64_t nq, int nparts, int k,
+                                                           int64_t n_global, float* out_s, int64_t* out_i,
+                                                           int32_t* status) {
+  __shared__ uint64_t A[kSelMaxK], B[kSelMaxK], Cb[kSelMaxK];
+  __shared__ int bad;
+  const int tid = threadIdx.x;
+  const int64_t q = blockIdx.x;
+  const int64_t ps = (int64_t)(k + 1);
+  if (tid == 0) bad = 0;
+  for (int i = tid; i < k; i += 512) A[i] = parts[q * ps + i];
+  __syncthreads();
+  if (tid == 0 && (parts[q * ps + k] & 1ull)) bad = 1;
+  for (int p = 1; p < nparts; ++p) {
+    const uint64_t* src = parts + ((int64_t)p * nq + q) * ps;
+    for (int i = tid; i < k; i += 512) B[i] = src[i];
+    if (tid == 0 && (src[k] & 1ull)) bad = 1;
+    __syncthreads();
+    for (int i = tid; i < k; i += 512) {
+      int lo = 0, hi = k;   // #B < A[i]
+      while (lo < hi) {
+        const int mid = (lo + hi) >> 1;
+        if (B[mid] < A[i]) lo = mid + 1;
+        else hi = mid;
+      }
+      if (i + lo < k) Cb[i + lo] = A[i];
+      int lo2 = 0, hi2 = k;  // #A <= B[i]
+      while (lo2 < hi2) {
+        const int mid = (lo2 + hi2) >> 1;
+        if (A[mid] <= B[i]) lo2 = mid + 1;
+        else hi2 = mid;
+      }
+      if (i + lo2 < k) Cb[i + lo2] = B[i];
+    }
+    __syncthreads();
+    for (int i = tid; i < k; i += 512) A[i] = Cb[i];
+    __syncthreads();
+  }
+  for (int i = tid; i < k; i += 512) {
+    const uint64_t x = A[i];
+    if (x == ~0ull) {
+      out_s[q * k + i] = kPadScore;
+      out_i[q * k + i] = -1;
+    } else {
+      out_s[q * k + i] = desc_key_to_score((uint32_t)(x >> 32));
+      out_i[q * k + i] = (int64_t)(x & 0xFFFFFFFFull);
+    }
+  }
+  if (status && tid == 0) status[q] = (bad || (A[k - 1] == ~0ull && n_global >= (int64_t)k)) ? 1 : 0;
 }
 
 // ---------------------------------------------------------------------------
@@ -1179,6 +1544,49 @@ static TopkPlan make_plan(int64_t nq, int64_t n, int64_t k) {
   return p;
 }
 
+// Distributed plan: shard of n_local rows out of n_global.  target / cap / r
+// come from the GLOBAL plan, so the union of the shards' samples has the same
+// sampling fraction r / target as a single-index search; each shard expects
+// target * n_local / n_global filter hits.
+static TopkPlan make_dist_plan(int64_t nq, int64_t n_local, int64_t n_global, int64_t k) {
+  const TopkPlan g = make_plan(nq, n_global, k);
+  TopkPlan p{};
+  p.n = n_local;
+  p.k = k;
+  p.nq = nq;
+  p.nq_pad = g.nq_pad;
+  const int64_t target = std::max<int64_t>(4096, 4 * k);
+  p.cap = std::max<int64_t>(g.cap, 4 * target);
+  p.sample = g.sample;
+  p.r = g.sample ? g.r : 0;
+  p.stride = 1;
+  p.m = 0;
+  p.nchunk = 0;
+  if (p.sample && n_local > 0) {
+    int64_t m = (p.r * n_local + target - 1) / target;
+    if (m > n_local) m = n_local;
+    const int64_t m_cap = std::max<int64_t>(1, kKthChunk / p.r) * kKthChunk;
+    if (m > m_cap) m = m_cap;
+    p.stride = std::max<int64_t>(1, n_local / m);
+    p.m = (n_local - p.stride / 2 + p.stride - 1) / p.stride;
+    if (p.m > m_cap) p.m = m_cap;
+    p.nchunk = (p.m + kKthChunk - 1) / kKthChunk;
+  }
+  size_t o = 0;
+  p.off_tau = o;
+  o = align_up(o + p.nq_pad * 4, 256);
+  p.off_cnt = o;
+  o = align_up(o + p.nq_pad * 4, 256);
+  p.off_keys = o;
+  o = align_up(o + (size_t)p.nq_pad * p.cap * 8, 256);
+  p.off_sample = o;
+  o = align_up(o + (size_t)p.nq_pad * align_up(p.m, 4) * 4, 256);
+  p.off_part = o;
+  o = align_up(o + (size_t)p.nq_pad * p.nchunk * p.r * 4, 256);
+  p.total = o;
+  return p;
+}
+
 static int scan_grid_x(int64_t ntiles) {
   int dev = 0, cus = 256;
   if (hipGetDevice(&dev) == hipSuccess) {
@@ -1210,8 +1618,18 @@ static int launch_scan_d(const ScanArgs& a, int mode, hipStream_t s) {
       hipLaunchKernelGGL((ip_scan16_kernel<D, SCAN_FILTER, 0, 4>), grid, block, 0, s, a);
     else if (mode == SCAN_DENSE && g_scan_variant == 6)
       hipLaunchKernelGGL((ip_scan16_kernel<D, SCAN_DENSE, 0, 4>), grid, block, 0, s, a);
-    else if (mode == SCAN_FILTER)  // production: 8 waves (2 per SIMD), 16 queries each
-      hipLaunchKernelGGL((ip_scan16_kernel<D, SCAN_FILTER, 0, 8>), grid, dim3(512), 0, s, a);
+    else if (mode == SCAN_FILTER && g_scan_variant == 7)
+      hipLaunchKernelGGL((ip_scan16_kernel<D, SCAN_FILTER, 0, 8, false>), grid, dim3(512), 0, s, a);
+    else if (mode == SCAN_FILTER) {
+      // production: 8 waves (2 per SIMD), 16 queries each.  Hit append: one LDS
+      // atomic per hit when hits are rare, one per wave-tile (popcount + wave scan)
+      // when they are dense.  Expected hits per 16x16 wave-tile = 256 * (cap/4) / n;
+      // measured crossover (profiles/r01_*): dense below ~3M rows at cap 16384.
+      const double eh = a.exp_hits > 0 ? (double)a.exp_hits : (double)a.cap / 4.0;
+      const bool dense_hits = eh * 256.0 / (double)a.nrows >= 0.35;
+      if (dense_hits) hipLaunchKernelGGL((ip_scan16_kernel<D, SCAN_FILTER, 0, 8, true>), grid, dim3(512), 0, s, a);
+      else hipLaunchKernelGGL((ip_scan16_kernel<D, SCAN_FILTER, 0, 8, false>), grid, dim3(512), 0, s, a);
+    }
     else
       hipLaunchKernelGGL((ip_scan16_kernel<D, SCAN_DENSE, 0, 8>), grid, dim3(512), 0, s, a);
     return hip_status(hipGetLastError());
@@ -1270,6 +1688,11 @@ static int launch_select(const SelectArgs& a, int input, int output, hipStream_t
   return hip_status(hipGetLastError());
 }
 
+static bool valid_dist_dims(int64_t nq, int64_t n_local, int64_t n_global, int32_t d, int32_t k) {
+  return nq >= 0 && n_local >= 0 && n_global >= n_local && d > 0 && d % 64 == 0 && d <= 1024 && k >= 1 &&
+         k <= kSelMaxK && n_global < (int64_t)0xFFFFFFFFll;
+}
+
 static bool valid_dims(int64_t nq, int64_t n, int32_t d, int32_t k) {
   return nq >= 0 && n >= 0 && d > 0 && d % 64 == 0 && d <= 1024 && k >= 1 && k <= kSelMaxK &&
          n < (int64_t)0xFFFFFFFFll;
@@ -1289,7 +1712,7 @@ const char* drt_version(void) { return "drt-mi355x 0.1 (gfx950)"; }
 // meaningless), 2 = previous 32-row / 3-slot kernel; 3/4/5 = 16-row kernel
 // ablations (no MFMA / no LDS fragment reads / no filter; d = 768 only).
 int drt_scan_variant(int32_t v) {
-  if (v < 0 || v > 6) return DRT_EINVAL;
+  if (v < 0 || v > 7) return DRT_EINVAL;
   g_scan_variant = v;
   return DRT_OK;
 }
@@ -1374,7 +1797,8 @@ int drt_ip_topk_bf16(const void* Q, int64_t nq, const void* P, int64_t n, int32_
                        (const uint32_t*)(w + p.off_sample), (int64_t)align_up(p.m, 4), p.m, (int)p.r,
                        (uint32_t*)(w + p.off_part));
     hipLaunchKernelGGL(kth_final_kernel, dim3((unsigned)nq), dim3(kKthThreads), 0, s,
-                       (const uint32_t*)(w + p.off_part), (int)p.nchunk, (int)p.r, tau);
+                       (const uint32_t*)(w + p.off_part), (int)p.nchunk, (int)p.r, (int64_t)p.r,
+                       (int64_t)(p.nchunk * p.r), tau, (uint32_t*)nullptr);
     prof_end(pp, s);
     DRT_CHECK_HIP(hipGetLastError());
   }
@@ -1494,6 +1918,158 @@ int drt_topk_merge(const float* scores, const int64_t* ids, int64_t nq, int32_t 
                      ids, nq, (int)nparts, (int)k_in, (int)k_out, out_scores, out_ids);
   prof_end(pp, (hipStream_t)stream);
   return hip_status(hipGetLastError());
+}
+
+// ---------------------------------------------------------------------------
+// Distributed exact top-k with ONE global threshold (see include/drt.h).
+// ---------------------------------------------------------------------------
+int32_t drt_ip_topk_sample_rank(int32_t k) {
+  if (k < 1 || k > kSelMaxK) return -1;
+  const TopkPlan p = make_plan(1, (int64_t)0xFFFFFFFEll, k);
+  return (int32_t)p.r;
+}
+
+size_t drt_ip_topk_dist_workspace(int64_t nq, int64_t n_local, int64_t n_global, int32_t d, int32_t k) {
+  if (!valid_dist_dims(nq, n_local, n_global, d, k)) return 0;
+  return make_dist_plan(nq, n_local, n_global, k).total;
+}
+
+int drt_ip_topk_dist_sample(const void* Q, int64_t nq, const void* P, int64_t n_local, int64_t n_global, int32_t d,
+                            int32_t k, uint32_t* best, void* ws, size_t ws_bytes, void* stream) {
+  DRT_REQUIRE(valid_dist_dims(nq, n_local, n_global, d, k));
+  if (nq == 0) return DRT_OK;
+  DRT_REQUIRE(Q && best && ws);
+  const TopkPlan p = make_dist_plan(nq, n_local, n_global, k);
+  DRT_REQUIRE(ws_bytes >= p.total);
+  const int64_t r = drt_ip_topk_sample_rank(k);
+  hipStream_t s = (hipStream_t)stream;
+  if (!p.sample || n_local == 0) {
+    // global corpus fits one filter pass (or this shard is empty): contribute no sample
+    DRT_CHECK_HIP(hipMemsetAsync(best, 0xFF, (size_t)nq * r * 4, s));
+    return DRT_OK;
+  }
+  DRT_REQUIRE(P != nullptr);
+  char* w = (char*)ws;
+  ScanArgs a{};
+  a.Q = (const __bf16*)Q;
+  a.nq = nq;
+  a.ldq = d;
+  a.P = (const __bf16*)P;
+  a.ldp = d;
+  a.row0 = p.stride / 2;
+  a.nrows = p.m;
+  a.rstride = p.stride;
+  a.out = w + p.off_sample;
+  a.cap = align_up(p.m, 4);
+  int rc = launch_scan(a, d, SCAN_DENSE, s, PROF_SAMPLE);
+  if (rc) return rc;
+  const ProfPair pp = prof_begin(PROF_SELECT, s);
+  // fewer than r sampled rows: kth_partial pads its list with 0xFFFFFFFF
+  hipLaunchKernelGGL(kth_partial_kernel, dim3((unsigned)p.nchunk, (unsigned)nq), dim3(kKthThreads), 0, s,
+                     (const uint32_t*)(w + p.off_sample), (int64_t)align_up(p.m, 4), p.m, (int)r,
+                     (uint32_t*)(w + p.off_part));
+  hipLaunchKernelGGL(kth_final_kernel, dim3((unsigned)nq), dim3(kKthThreads), 0, s,
+                     (const uint32_t*)(w + p.off_part), (int)p.nchunk, (int)r, (int64_t)r, (int64_t)(p.nchunk * r),
+                     (float*)nullptr, best);
+  prof_end(pp, s);
+  return hip_status(hipGetLastError());
+}
+
+int drt_ip_topk_dist_tau(const uint32_t* lists, int64_t nq, int32_t nlists, int32_t k, float* tau, void* stream) {
+  const int32_t r = drt_ip_topk_sample_rank(k);
+  DRT_REQUIRE(r > 0 && nq >= 0 && nlists >= 1 && (int64_t)nlists * r <= kKthChunk);
+  if (nq == 0) return DRT_OK;
+  DRT_REQUIRE(lists && tau);
+  hipLaunchKernelGGL(kth_final_kernel, dim3((unsigned)nq), dim3(kKthThreads), 0, (hipStream_t)stream, lists,
+                     (int)nlists, (int)r, (int64_t)nq * r, (int64_t)r, tau, (uint32_t*)nullptr);
+  return hip_status(hipGetLastError());
+}
+
+int drt_ip_topk_dist_filter(const void* Q, int64_t nq, const void* P, int64_t n_local, int64_t n_global, int32_t d,
+                            int32_t k, int64_t id_offset, const float* tau, uint64_t* packed, void* ws,
+                            size_t ws_bytes, void* stream) {
+  DRT_REQUIRE(valid_dist_dims(nq, n_local, n_global, d, k));
+  DRT_REQUIRE(id_offset >= 0 && id_offset + n_local <= n_global);
+  if (nq == 0) return DRT_OK;
+  DRT_REQUIRE(Q && tau && packed && ws);
+  const TopkPlan p = make_dist_plan(nq, n_local, n_global, k);
+  DRT_REQUIRE(ws_bytes >= p.total);
+  hipStream_t s = (hipStream_t)stream;
+  char* w = (char*)ws;
+  uint32_t* cnt = (uint32_t*)(w + p.off_cnt);
+  SelectArgs sa{};
+  sa.in = w + p.off_keys;
+  sa.in_stride = p.cap;
+  sa.k = k;
+  sa.nq = nq;
+  sa.id_offset = id_offset;
+  sa.out_packed = packed;
+  sa.global_tau = true;
+  if (n_local == 0) {
+    sa.n_in = 0;
+    sa.n_total = 0;
+    return launch_select(sa, SEL_DENSE32, SEL_TOPK, s);
+  }
+  DRT_REQUIRE(P != nullptr);
+  DRT_CHECK_HIP(hipMemsetAsync(cnt, 0, p.nq_pad * 4, s));
+  ScanArgs a{};
+  a.Q = (const __bf16*)Q;
+  a.nq = nq;
+  a.ldq = d;
+  a.P = (const __bf16*)P;
+  a.ldp = d;
+  a.row0 = 0;
+  a.nrows = n_local;
+  a.rstride = 1;
+  a.tau = tau;
+  a.counts = cnt;
+  a.out = w + p.off_keys;
+  a.cap = p.cap;
+  const int64_t target = std::max<int64_t>(4096, 4 * (int64_t)k);
+  a.exp_hits = p.sample ? std::max<int64_t>(1, target * n_local / std::max<int64_t>(1, n_global)) : n_local;
+  int rc = launch_scan(a, d, SCAN_FILTER, s, PROF_SCAN);
+  if (rc) return rc;
+  sa.counts = cnt;
+  sa.cap = p.cap;
+  sa.n_total = n_local;
+  return launch_select(sa, SEL_KEYS64, SEL_TOPK, s);
+}
+
+int drt_topk_merge_packed(const uint64_t* parts, int64_t nq, int32_t nparts, int32_t k, int64_t n_global,
+                          float* out_scores, int64_t* out_ids, int32_t* status, void* stream) {
+  DRT_REQUIRE(nq >= 0 && nparts >= 1 && nparts <= 4096 && k >= 1 && k <= kSelMaxK && n_global >= 0);
+  if (nq == 0) return DRT_OK;
+  DRT_REQUIRE(parts && out_scores && out_ids);
+  hipStream_t s = (hipStream_t)stream;
+  const ProfPair pp = prof_begin(PROF_MERGE, s);
+  int p2 = 1;
+  while (p2 < nparts) p2 <<= 1;
+  const size_t lds = (size_t)p2 * k * 8;
+  const int ept = (p2 * k + kTreeThreads - 1) / kTreeThreads;
+  int rc = DRT_OK;
+  if (nparts > 1 && lds <= 128 * 1024 && ept <= 32) {
+#define DRT_TREE(E)                                                                                          \
+  {                                                                                                          \
+    static bool attr_set = false;                                                                            \
+    if (!attr_set) {                                                                                         \
+      DRT_CHECK_HIP(hipFuncSetAttribute((const void*)merge_packed_tree_kernel<E>,                            \
+                                        hipFuncAttributeMaxDynamicSharedMemorySize, 128 * 1024));            \
+      attr_set = true;                                                                                       \
+    }                                                                                                        \
+    hipLaunchKernelGGL(merge_packed_tree_kernel<E>, dim3((unsigned)nq), dim3(kTreeThreads), lds, s, parts, nq, \
+                       (int)nparts, p2, (int)k, n_global, out_scores, out_ids, status);                      \
+  }
+    if (ept <= 8) DRT_TREE(8)
+    else if (ept <= 16) DRT_TREE(16)
+    else DRT_TREE(32)
+#undef DRT_TREE
+  } else {
+    hipLaunchKernelGGL(merge_packed_kernel, dim3((unsigned)nq), dim3(512), 0, s, parts, nq, (int)nparts, (int)k,
+                       n_global, out_scores, out_ids, status);
+  }
+  prof_end(pp, s);
+  rc = hip_status(hipGetLastError());
+  return rc;
 }
 
 }  // extern "C"

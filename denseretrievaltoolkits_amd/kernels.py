@@ -23,7 +23,8 @@ def _require_device(*ts: torch.Tensor) -> None:
 
 
 def _workspace(device: torch.device, nbytes: int) -> torch.Tensor:
-    key = (device.type, device.index)
+    """Scratch buffer per (device, current stream): launches on different streams never share one."""
+    key = (device.type, device.index, _native.stream_ptr(device))
     buf = _ws_cache.get(key)
     if buf is None or buf.numel() < nbytes:
         buf = torch.empty(max(nbytes, 1), dtype=torch.uint8, device=device)
@@ -104,6 +105,87 @@ def topk_merge(scores: torch.Tensor, ids: torch.Tensor, k_out: int) -> Tuple[tor
                                      out_s.data_ptr(), out_i.data_ptr(), _native.stream_ptr(scores.device)),
                   "drt_topk_merge")
     return out_s, out_i
+
+
+# ---------------------------------------------------------------------------
+# Global-threshold distributed search (include/drt.h, drt_ip_topk_dist_*)
+# ---------------------------------------------------------------------------
+def sample_rank(k: int) -> int:
+    r = int(_native.load().drt_ip_topk_sample_rank(k))
+    if r <= 0:
+        raise ValueError(f"unsupported k={k}")
+    return r
+
+
+def _dist_ws(q, n_local, n_global, k):
+    lib = _native.load()
+    nq, d = q.shape
+    wsb = lib.drt_ip_topk_dist_workspace(nq, n_local, n_global, d, k)
+    if wsb == 0 and nq > 0:
+        raise ValueError(f"unsupported dist shape nq={nq} n_local={n_local} n_global={n_global} d={d} k={k}")
+    return _workspace(q.device, wsb), wsb
+
+
+def dist_sample(q: torch.Tensor, p: torch.Tensor, n_global: int, k: int) -> torch.Tensor:
+    """Best r sampled score keys of this shard, [nq, r] int32 (uint32 bit patterns, ascending)."""
+    lib = _native.load()
+    _require_device(q, p)
+    q = q.contiguous()
+    p = p.contiguous()
+    nq, d = q.shape
+    best = torch.empty((nq, sample_rank(k)), dtype=torch.int32, device=q.device)
+    ws, wsb = _dist_ws(q, p.shape[0], n_global, k)
+    _native.check(lib.drt_ip_topk_dist_sample(q.data_ptr(), nq, p.data_ptr() if p.shape[0] else None, p.shape[0],
+                                              n_global, d, k, best.data_ptr(), ws.data_ptr(), wsb,
+                                              _native.stream_ptr(q.device)), "drt_ip_topk_dist_sample")
+    return best
+
+
+def dist_tau(lists: torch.Tensor, k: int) -> torch.Tensor:
+    """Global threshold from all shards' lists [nlists, nq, r] -> tau [nq] fp32."""
+    lib = _native.load()
+    _require_device(lists)
+    lists = lists.contiguous()
+    nlists, nq, _ = lists.shape
+    tau = torch.empty((nq,), dtype=torch.float32, device=lists.device)
+    _native.check(lib.drt_ip_topk_dist_tau(lists.data_ptr(), nq, nlists, k, tau.data_ptr(),
+                                           _native.stream_ptr(lists.device)), "drt_ip_topk_dist_tau")
+    return tau
+
+
+def dist_filter(q: torch.Tensor, p: torch.Tensor, n_global: int, k: int, id_offset: int,
+                tau: torch.Tensor, out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """This shard's packed top-k of rows scoring >= tau: [nq, k + 1] int64 (uint64 bit patterns)."""
+    lib = _native.load()
+    _require_device(q, p, tau)
+    q = q.contiguous()
+    p = p.contiguous()
+    nq, d = q.shape
+    if out is None:
+        out = torch.empty((nq, k + 1), dtype=torch.int64, device=q.device)
+    ws, wsb = _dist_ws(q, p.shape[0], n_global, k)
+    _native.check(lib.drt_ip_topk_dist_filter(q.data_ptr(), nq, p.data_ptr() if p.shape[0] else None, p.shape[0],
+                                              n_global, d, k, id_offset, tau.data_ptr(), out.data_ptr(),
+                                              ws.data_ptr(), wsb, _native.stream_ptr(q.device)),
+                  "drt_ip_topk_dist_filter")
+    return out
+
+
+def merge_packed(parts: torch.Tensor, k: int, n_global: int):
+    """[nparts, nq, k + 1] packed lists -> (scores [nq,k], ids [nq,k], status [nq] int32; 0 = exact)."""
+    lib = _native.load()
+    _require_device(parts)
+    parts = parts.contiguous()
+    nparts, nq, kp1 = parts.shape
+    if kp1 != k + 1:
+        raise ValueError("merge_packed expects [nparts, nq, k + 1]")
+    dev = parts.device
+    s = torch.empty((nq, k), dtype=torch.float32, device=dev)
+    i = torch.empty((nq, k), dtype=torch.int64, device=dev)
+    st = torch.empty((nq,), dtype=torch.int32, device=dev)
+    _native.check(lib.drt_topk_merge_packed(parts.data_ptr(), nq, nparts, k, n_global, s.data_ptr(), i.data_ptr(),
+                                            st.data_ptr(), _native.stream_ptr(dev)), "drt_topk_merge_packed")
+    return s, i, st
 
 
 def gemm_nt_f32(a: torch.Tensor, b: torch.Tensor, out: Optional[torch.Tensor] = None) -> torch.Tensor:

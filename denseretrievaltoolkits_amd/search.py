@@ -85,6 +85,22 @@ class FlatIPIndex:
         s, i = self.search_device(q, k)
         return s.cpu().numpy(), i.cpu().numpy()
 
+    # global-threshold protocol steps (ShardedFlatIP) ---------------------
+    def _queries(self, q):
+        qd = _as_device_bf16(q, self.device)
+        if qd.dim() != 2 or qd.shape[1] != self.d:
+            raise ValueError(f"search: expected [nq, {self.d}] queries, got {tuple(qd.shape)}")
+        return qd
+
+    def dist_sample(self, q, n_global: int, k: int) -> torch.Tensor:
+        return kernels.dist_sample(self._queries(q), self.rows, n_global, k)
+
+    def dist_tau(self, lists: torch.Tensor, k: int) -> torch.Tensor:
+        return kernels.dist_tau(lists, k)
+
+    def dist_filter(self, q, n_global: int, k: int, id_offset: int, tau: torch.Tensor) -> torch.Tensor:
+        return kernels.dist_filter(self._queries(q), self.rows, n_global, k, id_offset, tau)
+
     # persistence (replaces faiss.write_index / read_index, trainer.py:245,257)
     def save(self, path: str) -> None:
         rows = self.rows.view(torch.int16).cpu().numpy()
@@ -101,12 +117,25 @@ class FlatIPIndex:
 class ShardedFlatIP:
     """Row-sharded exact IP index: one shard per rank, RCCL all-gather + device merge.
 
-    ``local`` (the per-rank shard index) and ``merge`` default to the HIP
-    implementations; they are injectable only so the distributed logic can be
-    exercised with the gloo backend on CPU in tests.
+    ``local`` (the per-rank shard index), ``merge`` and ``merge_packed``
+    default to the HIP implementations; they are injectable only so the
+    distributed logic can be exercised with the gloo backend on CPU in tests.
+
+    Two exchange protocols (``protocol``):
+
+    ``"global_tau"`` (default)  every shard samples its rows, the tiny best-r
+        sample lists are all-gathered so all shards agree on ONE threshold for
+        the whole corpus, each shard then filters against it (collecting ~1/world
+        of the candidates a standalone search would) and emits a packed top-k
+        ((score key << 32) | global id, u64); one all-gather + a device merge
+        gives the exact answer, certified on device (>= k candidates overall,
+        no shard overflow).  An uncertified batch falls back to:
+    ``"per_shard"``  exact top-k per shard (own threshold, own resolve), then
+        all-gather of (scores, ids) and merge.
     """
 
-    def __init__(self, d: int, group=None, device=None, local=None, merge=None):
+    def __init__(self, d: int, group=None, device=None, local=None, merge=None, merge_packed=None,
+                 protocol: str = "global_tau"):
         import torch.distributed as dist
         self.dist = dist
         self.group = group
@@ -114,6 +143,11 @@ class ShardedFlatIP:
         self.rank = dist.get_rank(group) if dist.is_initialized() else 0
         self.local = local if local is not None else FlatIPIndex(d, device=device)
         self.merge = merge if merge is not None else kernels.topk_merge
+        self.merge_packed = merge_packed if merge_packed is not None else kernels.merge_packed
+        if protocol not in ("global_tau", "per_shard"):
+            raise ValueError(f"unknown protocol {protocol!r}")
+        self.protocol = protocol
+        self.fallbacks = 0   # batches the global-tau protocol could not certify
         self.d = d
         self.offset = 0      # global id of this shard's first row
         self.ntotal = 0      # rows over all shards
@@ -142,16 +176,34 @@ class ShardedFlatIP:
 
     def search_device(self, q, k: int) -> Tuple[torch.Tensor, torch.Tensor]:
         """Every rank passes the SAME queries; every rank gets the global top-k."""
-        s, i = self.local.search_device(q, k, id_offset=self.offset)
         if self.world == 1:
-            return s, i
-        nq = s.shape[0]
-        # concatenated [world * nq, k] output (the layout every backend accepts)
-        s_all = torch.empty((self.world * nq, k), dtype=torch.float32, device=s.device)
-        i_all = torch.empty((self.world * nq, k), dtype=torch.int64, device=s.device)
-        self.dist.all_gather_into_tensor(s_all, s.contiguous(), group=self.group)
-        self.dist.all_gather_into_tensor(i_all, i.contiguous(), group=self.group)
-        return self.merge(s_all.view(self.world, nq, k), i_all.view(self.world, nq, k), k)
+            return self.local.search_device(q, k, id_offset=self.offset)
+        if self.protocol == "global_tau" and self.ntotal < 0xFFFFFFFF:
+            res = self._search_global_tau(q, k)
+            if res is not None:
+                return res
+            self.fallbacks += 1
+        return self._search_per_shard(q, k)
+
+    def _all_gather(self, t: torch.Tensor) -> torch.Tensor:
+        """Concatenated [world * rows, ...] all-gather (the layout every backend accepts)."""
+        out = torch.empty((self.world * t.shape[0],) + tuple(t.shape[1:]), dtype=t.dtype, device=t.device)
+        self.dist.all_gather_into_tensor(out, t.contiguous(), group=self.group)
+        return out.view((self.world,) + tuple(t.shape))
+
+    def _search_global_tau(self, q, k: int):
+        best = self.local.dist_sample(q, self.ntotal, k)                 # [nq, r] u32 keys
+        tau = self.local.dist_tau(self._all_gather(best), k)             # [nq]
+        packed = self.local.dist_filter(q, self.ntotal, k, self.offset, tau)   # [nq, k + 1] u64
+        s, i, status = self.merge_packed(self._all_gather(packed), k, self.ntotal)
+        # every rank merged the same gathered lists, so every rank takes the same branch
+        if bool((status != 0).any()):
+            return None
+        return s, i
+
+    def _search_per_shard(self, q, k: int):
+        s, i = self.local.search_device(q, k, id_offset=self.offset)
+        return self.merge(self._all_gather(s), self._all_gather(i), k)
 
     def search(self, q, k: int) -> Tuple[np.ndarray, np.ndarray]:
         s, i = self.search_device(q, k)

@@ -281,3 +281,74 @@ class Trainer:
             self.start_epoch = checkpoint["epoch"] + 1
             self.module.load(checkpoint["state_dict"])
             self.optimizer.load_state_dict(checkpoint["optimizer"])
+
+
+class RRTrainer(Trainer):
+    """Drop-in for RRTrainer (DRT/trainer/trainer.py:392-484): pair scores on the HIP
+    reranker; per-rank result files as the reference, merged on rank 0 through an
+    object all-gather instead of re-reading every rank's file."""
+
+    def train_step(self, inputs):
+        return self.model(pos_pairs=inputs[0], neg_pairs=inputs[1]).loss
+
+    def evaluate(self, pair_loader, ep):
+        self.model.eval()
+        a = self.training_args
+        topk = a.topk if not isinstance(a.topk, str) else [int(x) for x in a.topk.split(",")]
+        if self.world > 1 and hasattr(pair_loader.sampler, "set_epoch"):
+            pair_loader.sampler.set_epoch(0)
+        result = {}
+        m = self.module
+        for batch in pair_loader:
+            data = {k: v.to(self.device) if v is not None else None for k, v in batch[1].items()}
+            with torch.no_grad():
+                scores = m(pos_pairs=data, neg_pairs=None).detach().cpu().numpy()
+            for q, ans, d, s, did in zip(batch[0], batch[2], batch[3], scores, batch[4]):
+                r = result.setdefault(q, ([], [], [], []))
+                r[0].append(float(s[0]))
+                r[1].append(int(has_answers(d, ans)))
+                r[2].append(d)
+                r[3].append(did)
+        rdir = getattr(a, "rr_result_dir", "")
+        if rdir:
+            os.makedirs(rdir, exist_ok=True)
+            with open(os.path.join(rdir, f"{ep}.{self.local_rank}.json"), "w", encoding="utf-8") as f:
+                for qid, (scs, js, ds, dids) in result.items():
+                    for s, j, d, did in zip(scs, js, ds, dids):
+                        json.dump({"qid": qid, "did": did, "score": s, "match": j, "document": d}, f,
+                                  ensure_ascii=False)
+                        f.write("\n")
+        local = {q: (r[0], r[1]) for q, r in result.items()}
+        if self.world > 1:
+            parts = [None] * self.world
+            dist.all_gather_object(parts, local)
+        else:
+            parts = [local]
+        m_all = None
+        if self.rank == 0:
+            merged = {}
+            for part in parts:
+                for q, (scs, js) in part.items():
+                    mm = merged.setdefault(q, ([], []))
+                    mm[0].extend(scs)
+                    mm[1].extend(js)
+            m_all = {f"{mt}@{k}": 0.0 for mt in ["MRR", "NDCG", "Recall"] for k in topk}
+            n = 0
+            for q, (scs, js) in merged.items():
+                n += 1
+                order = np.argsort(-np.asarray(scs), kind="stable")
+                metrics = get_metrics([np.asarray(js)[order]], topk)
+                for key in m_all:
+                    m_all[key] += metrics[key]
+            m_all["query_num"] = n
+            for key in m_all:
+                m_all[key] = m_all[key] / max(n, 1)
+            cdir = getattr(a, "cache_train_dir", "")
+            if cdir:
+                os.makedirs(cdir, exist_ok=True)
+                with open(os.path.join(cdir, f"{ep}.{self.local_rank}_RR_metrics"), "w", encoding="utf-8") as f:
+                    json.dump(m_all, f, ensure_ascii=False)
+        if dist.is_initialized():
+            dist.barrier()
+        self.last_metrics = m_all
+        return m_all

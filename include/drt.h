@@ -82,6 +82,39 @@ int drt_topk_merge(const float* scores, const int64_t* ids, int64_t nq, int32_t 
                    int32_t k_in, int32_t k_out, float* out_scores, int64_t* out_ids,
                    void* stream);
 
+/* ------------------------------------------------------------------------
+ * Distributed exact top-k with ONE global threshold (row shards, one process
+ * per GPU).  Replaces the same boundary as drt_ip_topk_bf16 + drt_topk_merge
+ * (faiss search per partition + merge_retrieval_results_by_score,
+ * DRT/evaluator/index.py:31-33, DRT/model/utils.py:215-229) with a protocol
+ * that makes every shard filter against the threshold of the WHOLE corpus,
+ * so each shard collects ~1/world of the candidates:
+ *   1. drt_ip_topk_dist_sample   per shard: best r sampled keys  [nq][r] u32
+ *   2. caller all-gathers the lists -> [world][nq][r]  (r = sample_rank(k))
+ *   3. drt_ip_topk_dist_tau      tau[q] = r-th best over all lists
+ *   4. drt_ip_topk_dist_filter   per shard: packed top-k [nq][k + 1] u64
+ *        entry j < k: (desc score key << 32) | global id  (ascending = score
+ *        desc, id asc; ~0 = empty), entry k: flags (bit 0 = shard overflow)
+ *   5. caller all-gathers packed -> [world][nq][k + 1]
+ *   6. drt_topk_merge_packed     exact merged top-k + status[q] (1 = not
+ *        certified: fall back to the per-shard exact path for that batch)
+ * Requires n_global < 2^32 (ids travel in 32 bits).                         */
+int32_t drt_ip_topk_sample_rank(int32_t k);
+size_t drt_ip_topk_dist_workspace(int64_t nq, int64_t n_local, int64_t n_global, int32_t d,
+                                  int32_t k);
+int drt_ip_topk_dist_sample(const void* Q, int64_t nq, const void* P, int64_t n_local,
+                            int64_t n_global, int32_t d, int32_t k, uint32_t* best, void* ws,
+                            size_t ws_bytes, void* stream);
+int drt_ip_topk_dist_tau(const uint32_t* lists, int64_t nq, int32_t nlists, int32_t k, float* tau,
+                         void* stream);
+int drt_ip_topk_dist_filter(const void* Q, int64_t nq, const void* P, int64_t n_local,
+                            int64_t n_global, int32_t d, int32_t k, int64_t id_offset,
+                            const float* tau, uint64_t* packed, void* ws, size_t ws_bytes,
+                            void* stream);
+int drt_topk_merge_packed(const uint64_t* parts, int64_t nq, int32_t nparts, int32_t k,
+                          int64_t n_global, float* out_scores, int64_t* out_ids, int32_t* status,
+                          void* stream);
+
 /* Dense score matrix C[m, n] = A[m, d] . B[n, d]^T with fp32 accumulation
  * (torch.matmul(q_reps, p_reps.T), biencoder.py:107).  A, B bf16; C fp32 with
  * leading dimension ldc.                                                     */

@@ -138,3 +138,131 @@ def shard_bounds(n: int, world: int, rank: int):
     lo = min(n, rank * per)
     hi = min(n, lo + per)
     return lo, hi
+
+
+# ---------------------------------------------------------------------------
+# Global-threshold distributed protocol (csrc/search.hip drt_ip_topk_dist_*).
+# Not a reference algorithm: the reference concatenates shards into ONE faiss
+# index (trainer.py:220-262); the protocol must reproduce exactly that
+# single-index result, which is what the tests check, so this restatement
+# only has to agree with the GPU kernels on the exchanged intermediate data.
+# ---------------------------------------------------------------------------
+PAD_KEY32 = np.uint32(0xFFFFFFFF)
+PAD_KEY64 = np.uint64(0xFFFFFFFFFFFFFFFF)
+
+
+def desc_key(scores: np.ndarray) -> np.ndarray:
+    """uint32 whose ascending order is descending score (drt_common.h desc_key)."""
+    s = np.asarray(scores, dtype=np.float32) + np.float32(0.0)
+    u = s.view(np.uint32)
+    ordk = np.where(u & np.uint32(0x80000000), ~u, u | np.uint32(0x80000000)).astype(np.uint32)
+    return (~ordk).astype(np.uint32)
+
+
+def desc_key_to_score(k: np.ndarray) -> np.ndarray:
+    ordk = ~np.asarray(k, dtype=np.uint32)
+    u = np.where(ordk & np.uint32(0x80000000), ordk & np.uint32(0x7FFFFFFF), ~ordk).astype(np.uint32)
+    return u.view(np.float32)
+
+
+def _poisson_tail_ge(lam, r):
+    import math
+    p = math.exp(-lam + r * math.log(lam) - math.lgamma(r + 1.0))
+    s = 0.0
+    i = r
+    while i < r + 2000:
+        s += p
+        p *= lam / (i + 1)
+        i += 1
+        if p < 1e-30 * s:
+            break
+    return s
+
+
+def sample_rank(k: int) -> int:
+    """drt_ip_topk_sample_rank: smallest r with P[Poisson(k r / target) >= r] < 1e-9."""
+    target = max(4096, 4 * k)
+    r = 1
+    while _poisson_tail_ge(k * r / target, r) > 1e-9 and r < 100000:
+        r += 1
+    return r
+
+
+def dist_plan(n_local: int, n_global: int, k: int):
+    """make_dist_plan: (sample?, r, sampled row indices of this shard, cap)."""
+    target = max(4096, 4 * k)
+    cap = 4 * target
+    sample = n_global > cap
+    r = sample_rank(k) if sample else 0
+    rows = np.zeros(0, np.int64)
+    if sample and n_local > 0:
+        m = min(n_local, (r * n_local + target - 1) // target)
+        m_cap = max(1, 4096 // r) * 4096
+        m = min(m, m_cap)
+        stride = max(1, n_local // m)
+        m = min((n_local - stride // 2 + stride - 1) // stride, m_cap)
+        rows = np.arange(m, dtype=np.int64) * stride + stride // 2
+    return dict(sample=sample, r=sample_rank(k), rows=rows, cap=cap, target=target)
+
+
+def _scores_f32(q, p):
+    return (np.asarray(q, np.float64) @ np.asarray(p, np.float64).T).astype(np.float32)
+
+
+def dist_sample(q, p_local, n_global, k):
+    """Best r sampled desc-keys per query, ascending, padded with 0xFFFFFFFF -> uint32 [nq, r]."""
+    plan = dist_plan(p_local.shape[0], n_global, k)
+    r = plan["r"]
+    nq = np.asarray(q).shape[0]
+    out = np.full((nq, r), PAD_KEY32, dtype=np.uint32)
+    if not plan["sample"] or len(plan["rows"]) == 0:
+        return out
+    keys = np.sort(desc_key(_scores_f32(q, p_local[plan["rows"]])), axis=1)[:, :r]
+    out[:, :keys.shape[1]] = keys
+    return out
+
+
+def dist_tau(lists, k):
+    """tau[q] = score of the r-th smallest key over [nlists, nq, r] (-inf if fewer than r real keys)."""
+    lists = np.asarray(lists, dtype=np.uint32)
+    r = sample_rank(k)
+    allk = np.sort(np.transpose(lists, (1, 0, 2)).reshape(lists.shape[1], -1), axis=1)
+    kr = allk[:, r - 1]
+    tau = desc_key_to_score(kr).copy()
+    tau[kr == PAD_KEY32] = -np.inf
+    return tau.astype(np.float32)
+
+
+def dist_filter(q, p_local, n_global, k, id_offset, tau):
+    """Packed uint64 [nq, k + 1]: sorted (desc_key << 32 | global id) of rows with score >= tau;
+    entry k = flags (bit 0: more than cap candidates, i.e. the GPU buffer overflowed)."""
+    plan = dist_plan(p_local.shape[0], n_global, k)
+    nq = np.asarray(q).shape[0]
+    out = np.full((nq, k + 1), PAD_KEY64, dtype=np.uint64)
+    out[:, k] = 0
+    if p_local.shape[0] == 0:
+        return out
+    s = _scores_f32(q, p_local)
+    for i in range(nq):
+        sel = np.nonzero(s[i] >= tau[i])[0]
+        if len(sel) > plan["cap"]:
+            out[i, k] = 1
+        keys = (desc_key(s[i, sel]).astype(np.uint64) << np.uint64(32)) | (sel + id_offset).astype(np.uint64)
+        keys = np.sort(keys)[:k]
+        out[i, :len(keys)] = keys
+    return out
+
+
+def merge_packed(parts, k, n_global):
+    """[nparts, nq, k + 1] packed lists -> (scores f32 [nq,k], ids i64 [nq,k], status i32 [nq])."""
+    parts = np.asarray(parts, dtype=np.uint64)
+    nparts, nq, _ = parts.shape
+    keys = np.sort(np.transpose(parts[:, :, :k], (1, 0, 2)).reshape(nq, -1), axis=1)[:, :k]
+    pad = keys == PAD_KEY64
+    s = desc_key_to_score((keys >> np.uint64(32)).astype(np.uint32)).copy()
+    ids = (keys & np.uint64(0xFFFFFFFF)).astype(np.int64)
+    s[pad] = PAD_SCORE
+    ids[pad] = PAD_ID
+    over = (parts[:, :, k] & np.uint64(1)).any(axis=0)
+    status = (over | (pad[:, k - 1] & (n_global >= k))).astype(np.int32)
+    return s.astype(np.float32), ids, status

@@ -1,0 +1,124 @@
+"""GPU parity of the global-threshold distributed protocol (drt_ip_topk_dist_*,
+drt_topk_merge_packed), shards simulated on one GPU.
+
+Reference behaviour: the reference concatenates every rank's shard into one
+faiss IndexFlatIP (DRT/trainer/trainer.py:220-262) and searches it
+(DRT/evaluator/index.py:31-33); the protocol must return exactly that
+single-index top-k.  Integer-valued inputs make every score exact, so the
+exchanged intermediates (sample keys, tau, packed lists) are compared with the
+oracle restatement bit for bit as well as the final (scores, ids).
+"""
+import numpy as np
+import pytest
+
+from helpers import int_bf16, gauss_bf16, to_dev_bf16
+from oracle import search_oracle as orc
+
+pytestmark = pytest.mark.gpu
+
+
+def _gpu_protocol(dev, q, p, k, world, check_intermediates=True):
+    import torch
+    from denseretrievaltoolkits_amd import kernels
+    n = p.shape[0]
+    d = q.shape[1]
+    qt = to_dev_bf16(q, dev)
+    bounds = [orc.shard_bounds(n, world, r) for r in range(world)]
+    shards = [to_dev_bf16(p[lo:hi], dev) if hi > lo else torch.empty((0, d), dtype=torch.bfloat16, device=dev)
+              for lo, hi in bounds]
+    lists = torch.stack([kernels.dist_sample(qt, sh, n, k) for sh in shards])
+    tau = kernels.dist_tau(lists, k)
+    parts = torch.stack([kernels.dist_filter(qt, sh, n, k, lo, tau) for sh, (lo, _) in zip(shards, bounds)])
+    s, i, st = kernels.merge_packed(parts, k, n)
+    torch.cuda.synchronize()
+    if check_intermediates:
+        e_lists = np.stack([orc.dist_sample(q, p[lo:hi], n, k) for lo, hi in bounds])
+        np.testing.assert_array_equal(lists.cpu().numpy().view(np.uint32), e_lists)
+        e_tau = orc.dist_tau(e_lists, k)
+        np.testing.assert_array_equal(tau.cpu().numpy(), e_tau)
+        e_parts = np.stack([orc.dist_filter(q, p[lo:hi], n, k, lo, e_tau) for lo, hi in bounds])
+        np.testing.assert_array_equal(parts.cpu().numpy().view(np.uint64), e_parts)
+    return s.cpu().numpy(), i.cpu().numpy(), st.cpu().numpy()
+
+
+@pytest.mark.parametrize("world,nq,n,d,k", [
+    (8, 128, 400000, 768, 1000),   # N=8 shape of the bench (sampled global tau)
+    (2, 16, 50000, 768, 1000),
+    (3, 33, 100003, 128, 100),     # ragged shards
+    (4, 5, 12000, 64, 10),         # n_global <= cap: tau = -inf, everything filtered
+    (5, 4, 3, 128, 10),            # fewer rows than k, empty shards
+    (2, 7, 60000, 1024, 2048),     # k at its maximum
+])
+def test_dist_protocol_integer_bit_exact(dev, world, nq, n, d, k):
+    rng = np.random.default_rng(world * 7 + n + d + k)
+    q = int_bf16(rng, (nq, d), -4, 4)
+    p = int_bf16(rng, (n, d), -4, 4)
+    s, i, st = _gpu_protocol(dev, q, p, k, world)
+    es, ei = orc.ip_topk(q, p, k)
+    assert (st == 0).all()
+    np.testing.assert_array_equal(i, ei)
+    np.testing.assert_array_equal(s, es)
+
+
+def test_dist_protocol_gaussian(dev):
+    rng = np.random.default_rng(11)
+    world, nq, n, d, k = 8, 64, 240000, 768, 1000
+    q = gauss_bf16(rng, (nq, d))
+    p = gauss_bf16(rng, (n, d))
+    s, i, st = _gpu_protocol(dev, q, p, k, world, check_intermediates=False)
+    assert (st == 0).all()
+    es, ei = orc.ip_topk(q, p, k)
+    np.testing.assert_allclose(s, es, atol=1e-3, rtol=0)
+    assert (i == ei).mean() > 0.999
+
+
+def test_dist_protocol_equals_single_gpu_search(dev):
+    """Gaussian data: global-tau result == single-index HIP result bit for bit (same kernels' fp32 scores)."""
+    import torch
+    from denseretrievaltoolkits_amd import kernels
+    rng = np.random.default_rng(12)
+    world, nq, n, d, k = 4, 32, 200000, 768, 1000
+    q = gauss_bf16(rng, (nq, d))
+    p = gauss_bf16(rng, (n, d))
+    s, i, st = _gpu_protocol(dev, q, p, k, world, check_intermediates=False)
+    s1, i1, _ = kernels.ip_topk(to_dev_bf16(q, dev), to_dev_bf16(p, dev), k)
+    assert (st == 0).all()
+    np.testing.assert_array_equal(i, i1.cpu().numpy())
+    np.testing.assert_array_equal(s, s1.cpu().numpy())
+
+
+def test_dist_overflow_and_short_lists_are_flagged(dev):
+    import torch
+    from denseretrievaltoolkits_amd import kernels
+    rng = np.random.default_rng(5)
+    nq, n, d, k = 3, 80000, 128, 50
+    q = int_bf16(rng, (nq, d), -4, 4)
+    p = int_bf16(rng, (n, d), -4, 4)
+    qt, pt = to_dev_bf16(q, dev), to_dev_bf16(p, dev)
+    # tau = -inf on a shard bigger than cap: overflow flag, status 1
+    tau = torch.full((nq,), float("-inf"), device=dev)
+    parts = kernels.dist_filter(qt, pt, n, k, 0, tau)[None]
+    assert (parts[0, :, k].cpu().numpy() & 1).all()
+    _, _, st = kernels.merge_packed(parts, k, n)
+    assert (st.cpu().numpy() == 1).all()
+    # tau above every score: no candidates, status 1
+    tau = torch.full((nq,), 1e9, device=dev)
+    parts = kernels.dist_filter(qt, pt, n, k, 0, tau)[None]
+    s, i, st = kernels.merge_packed(parts, k, n)
+    assert (st.cpu().numpy() == 1).all()
+    assert (i.cpu().numpy() == -1).all()
+
+
+def test_dist_shape_errors(dev):
+    import torch
+    from denseretrievaltoolkits_amd import _native, kernels
+    qt = torch.zeros((2, 128), dtype=torch.bfloat16, device=dev)
+    pt = torch.zeros((10, 128), dtype=torch.bfloat16, device=dev)
+    tau = torch.zeros((2,), device=dev)
+    with pytest.raises(ValueError):
+        kernels.dist_filter(qt, pt, 5, 10, 0, tau)                 # n_global < n_local
+    with pytest.raises(ValueError):
+        kernels.dist_filter(qt, pt, 12, 10, 5, tau)                # id_offset + n_local > n_global
+    with pytest.raises(ValueError):
+        kernels.dist_tau(torch.zeros((400, 2, kernels.sample_rank(1000)), dtype=torch.int32, device=dev), 1000)
+    assert kernels.sample_rank(1000) == orc.sample_rank(1000)

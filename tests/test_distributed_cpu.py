@@ -33,6 +33,22 @@ class _OracleShard:
         s, i = orc.ip_topk(np.asarray(q, np.float32), self.rows, k, id_offset=id_offset)
         return torch.from_numpy(s), torch.from_numpy(i)
 
+    # global-threshold protocol steps (uint32 / uint64 keys travel as int32 / int64 tensors)
+    def dist_sample(self, q, n_global, k):
+        return torch.from_numpy(orc.dist_sample(np.asarray(q, np.float32), self.rows, n_global, k).view(np.int32))
+
+    def dist_tau(self, lists, k):
+        return torch.from_numpy(orc.dist_tau(lists.numpy().view(np.uint32), k))
+
+    def dist_filter(self, q, n_global, k, id_offset, tau):
+        pk = orc.dist_filter(np.asarray(q, np.float32), self.rows, n_global, k, id_offset, tau.numpy())
+        return torch.from_numpy(pk.view(np.int64))
+
+
+def _oracle_merge_packed(parts, k, n_global):
+    s, i, st = orc.merge_packed(parts.numpy().view(np.uint64), k, n_global)
+    return torch.from_numpy(s), torch.from_numpy(i), torch.from_numpy(st)
+
 
 def _oracle_merge(s_all, i_all, k):
     s, i = orc.merge_topk(s_all.numpy(), i_all.numpy(), k)
@@ -45,39 +61,58 @@ def _free_port():
         return s.getsockname()[1]
 
 
-def _worker(rank, world, port, n, d, k, nq, out_q):
+def _worker(rank, world, port, n, d, k, nq, out_q, protocol="global_tau", vals=3):
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world)
     from denseretrievaltoolkits_amd.search import ShardedFlatIP
     rng = np.random.default_rng(0)
-    p = rng.integers(-3, 4, size=(n, d)).astype(np.float32)
-    q = rng.integers(-3, 4, size=(nq, d)).astype(np.float32)
+    p = rng.integers(-vals, vals + 1, size=(n, d)).astype(np.float32)
+    q = rng.integers(-vals, vals + 1, size=(nq, d)).astype(np.float32)
     lo, hi = orc.shard_bounds(n, world, rank)
-    idx = ShardedFlatIP(d, local=_OracleShard(d), merge=_oracle_merge)
+    idx = ShardedFlatIP(d, local=_OracleShard(d), merge=_oracle_merge, merge_packed=_oracle_merge_packed,
+                        protocol=protocol)
     idx.add_shard(p[lo:hi])
     assert idx.offset == lo and idx.ntotal == n
     s, i = idx.search_device(q, k)
     es, ei = orc.ip_topk(q, p, k)
     ok = bool(np.array_equal(i.numpy(), ei) and np.array_equal(s.numpy(), es))
-    out_q.put((rank, ok))
+    out_q.put((rank, ok, idx.fallbacks))
     dist.barrier()
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world,n", [(2, 1001), (3, 50), (4, 7)])
-def test_sharded_search_equals_single_index(world, n):
+def _run(world, n, k=20, nq=5, protocol="global_tau", d=16, vals=3):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, n, 16, 20, 5, q)) for r in range(world)]
+    procs = [ctx.Process(target=_worker, args=(r, world, port, n, d, k, nq, q, protocol, vals))
+             for r in range(world)]
     for pr in procs:
         pr.start()
-    res = [q.get(timeout=120) for _ in range(world)]
+    res = [q.get(timeout=180) for _ in range(world)]
     for pr in procs:
         pr.join(timeout=60)
         assert pr.exitcode == 0
-    assert all(ok for _, ok in res), res
+    assert all(r[1] for r in res), res
+    return res
+
+
+@pytest.mark.parametrize("protocol", ["global_tau", "per_shard"])
+@pytest.mark.parametrize("world,n", [(2, 1001), (3, 50), (4, 7)])
+def test_sharded_search_equals_single_index(world, n, protocol):
+    _run(world, n, protocol=protocol)
+
+
+def test_global_tau_sampled_corpus():
+    """n_global > cap: the shards sample, agree on one tau, filter, certify; no fallback expected."""
+    res = _run(2, 40000, k=20, nq=4, vals=8)
+    assert all(r[2] == 0 for r in res), res
+
+
+def test_global_tau_uneven_and_empty_shards():
+    # ceil-sharding of 20001 rows over 4 ranks; rank shards differ in size
+    _run(4, 20001, k=10, nq=3, vals=8)
 
 
 def test_overlay_registers_hot_path_modules():

@@ -87,3 +87,19 @@ def test_drmodel_mirror_torch_path_matches_reference_golden(tag):
         m = DRModelForInference(lm_q=lm, lm_p=lm, pooling=pooling, head_q=h, head_p=h, normalize=norm == "1").eval()
         out = m(passage={"input_ids": ids, "attention_mask": mask})
         np.testing.assert_allclose(out.p_reps.numpy(), z[key], rtol=1e-4, atol=1e-5)
+
+
+def test_rrmodel_mirror_torch_path_matches_reference_golden():
+    import torch
+    from denseretrievaltoolkits_amd.model.linear import LinearHead
+    from denseretrievaltoolkits_amd.model.reranker import RRModel
+    z = np.load(os.path.join(G, "rerank.npz"))
+    lm = _hf(2, 2)
+    head = LinearHead(768, 1)
+    with torch.no_grad():
+        head.linear.weight.copy_(torch.from_numpy(bw.param_value(2, "rr_head.linear.weight", (1, 768))))
+    for pooling in ("first", "mean"):
+        m = RRModel(lm=lm, head=head, pooling=pooling).eval()
+        s = m(pos_pairs={"input_ids": torch.from_numpy(z["input_ids"]),
+                         "attention_mask": torch.from_numpy(z["attention_mask"])})
+        np.testing.assert_allclose(s.detach().numpy(), z[f"scores_{pooling}"], rtol=1e-4, atol=1e-5)

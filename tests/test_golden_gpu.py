@@ -94,3 +94,25 @@ def test_merge_kernel_matches_reference_merge(dev):
         for r, q in enumerate(qids):
             want = [int(d[1:]) for d, _ in case["merged"][q]]
             assert list(mi[r, :len(want)]) == want
+
+
+def test_hip_rerank_matches_reference_scores(dev):
+    """RRModel.encode (reranker.py:111-130) at L = 160 on the HIP encoder + 768->1 head."""
+    import torch
+    from denseretrievaltoolkits_amd.model.linear import LinearHead
+    from denseretrievaltoolkits_amd.model.reranker import RRModel
+    z = np.load(os.path.join(G, "rerank.npz"))
+    lm = _hf(2, 2, dev)
+    head = LinearHead(768, 1)
+    with torch.no_grad():
+        head.linear.weight.copy_(torch.from_numpy(bw.param_value(2, "rr_head.linear.weight", (1, 768))))
+    head = head.to(dev)
+    for pooling in ("first", "mean"):
+        m = RRModel(lm=lm, head=head, pooling=pooling).eval()
+        s = m(pos_pairs={"input_ids": torch.from_numpy(z["input_ids"]).to(dev),
+                         "attention_mask": torch.from_numpy(z["attention_mask"]).to(dev)})
+        ref = z[f"scores_{pooling}"]
+        got = s.float().cpu().numpy()
+        err = np.abs(got - ref).max() / (np.abs(ref).max() + 1e-6)
+        print(f"rerank {pooling}: max rel err {err:.4f}")
+        assert err < 0.02

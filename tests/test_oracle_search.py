@@ -65,3 +65,48 @@ def test_bf16_round_matches_torch():
     x = np.random.default_rng(2).standard_normal(10000).astype(np.float32) * 100
     ref = torch.from_numpy(x).to(torch.bfloat16).float().numpy()
     np.testing.assert_array_equal(orc.bf16_round(x), ref)
+
+
+# ---------------------------------------------------------------------------
+# global-threshold protocol restatement == single-index oracle
+# ---------------------------------------------------------------------------
+def _protocol(q, p, k, world):
+    n = p.shape[0]
+    bounds = [orc.shard_bounds(n, world, r) for r in range(world)]
+    lists = np.stack([orc.dist_sample(q, p[lo:hi], n, k) for lo, hi in bounds])
+    tau = orc.dist_tau(lists, k)
+    parts = np.stack([orc.dist_filter(q, p[lo:hi], n, k, lo, tau) for lo, hi in bounds])
+    return orc.merge_packed(parts, k, n), tau
+
+
+@pytest.mark.parametrize("world,n,k", [(2, 40000, 20), (3, 17000, 50), (4, 1000, 30), (2, 10, 30)])
+def test_global_tau_protocol_matches_single_index(world, n, k):
+    rng = np.random.default_rng(n + k)
+    p = rng.integers(-8, 9, size=(n, 16)).astype(np.float32)
+    q = rng.integers(-8, 9, size=(4, 16)).astype(np.float32)
+    (s, i, st), tau = _protocol(q, p, k, world)
+    es, ei = orc.ip_topk(q, p, k)
+    assert (st == 0).all()
+    assert np.array_equal(i, ei) and np.array_equal(s, es)
+    if n <= 4 * max(4096, 4 * k):
+        assert np.isneginf(tau).all()
+
+
+def test_global_tau_protocol_flags_too_high_threshold():
+    rng = np.random.default_rng(3)
+    p = rng.integers(-8, 9, size=(40000, 16)).astype(np.float32)
+    q = rng.integers(-8, 9, size=(2, 16)).astype(np.float32)
+    k = 20
+    n = p.shape[0]
+    tau = np.full(2, 1e9, np.float32)          # nothing passes: fewer than k candidates
+    parts = np.stack([orc.dist_filter(q, p[lo:hi], n, k, lo, tau)
+                      for lo, hi in (orc.shard_bounds(n, 2, r) for r in range(2))])
+    _, _, st = orc.merge_packed(parts, k, n)
+    assert (st == 1).all()
+
+
+def test_desc_key_roundtrip_and_order():
+    x = np.array([3.5, -0.0, 0.0, -2.25, np.float32(np.finfo(np.float32).min), 1e30], np.float32)
+    k = orc.desc_key(x)
+    assert np.array_equal(orc.desc_key_to_score(k), x + np.float32(0.0))
+    assert np.array_equal(np.argsort(k, kind="stable"), np.argsort(-(x + 0.0), kind="stable"))

@@ -92,6 +92,26 @@ def gen_loss(ref_bi, ref_losses):
     np.savez_compressed(os.path.join(OUT, "loss.npz"), **cases)
 
 
+def gen_rerank():
+    import DRT.model.linear as ref_linear
+    import DRT.model.reranker as ref_rr
+    from transformers import BertModel
+    torch.manual_seed(0)
+    lm = BertModel(bw.bert_config(layers=2), add_pooling_layer=False).eval()
+    bw.init_model_(lm, 2)
+    head = ref_linear.LinearHead(768, 1)
+    with torch.no_grad():
+        head.linear.weight.copy_(torch.from_numpy(bw.param_value(2, "rr_head.linear.weight", (1, 768))))
+    out = {}
+    ids, mask = bw.token_batch(6, 160, seed=33)
+    for pooling in ("first", "mean"):
+        m = ref_rr.RRModel(lm=lm, head=head, pooling=pooling).eval()
+        with torch.no_grad():
+            s = m(pos_pairs={"input_ids": torch.from_numpy(ids), "attention_mask": torch.from_numpy(mask)})
+        out[f"scores_{pooling}"] = s.numpy()
+    np.savez_compressed(os.path.join(OUT, "rerank.npz"), input_ids=ids, attention_mask=mask, **out)
+
+
 def gen_metrics(ref_metrics):
     rng = np.random.default_rng(7)
     cases = []
@@ -134,6 +154,7 @@ def main():
     gen_loss(ref_bi, ref_losses)
     gen_metrics(ref_metrics)
     gen_merge(ref_utils)
+    gen_rerank()
     for f in sorted(os.listdir(OUT)):
         print(f, os.path.getsize(os.path.join(OUT, f)))
 
