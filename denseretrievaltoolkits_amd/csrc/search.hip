@@ -676,25 +676,91 @@ __device__ __forceinline__ T block_reduce(T v, T* scratch, Op op) {
   return r;
 }
 
-// Bitonic sort of buf[0..n2) ascending (n2 power of two), whole block.
-__device__ __forceinline__ void block_bitonic(uint64_t* buf, int n2) {
-  const int tid = threadIdx.x;
-  for (int size = 2; size <= n2; size <<= 1) {
-    for (int stride = size >> 1; stride > 0; stride >>= 1) {
-      for (int i = tid; i < n2 / 2; i += kSelThreads) {
-        const int lo = 2 * i - (i & (stride - 1));
-        const int hi = lo + stride;
-        const bool up = ((lo & size) == 0);
-        const uint64_t x = buf[lo], y = buf[hi];
-        if ((x > y) == up) {
-          buf[lo] = y;
-          buf[hi] = x;
-        }
-      }
-      __syncthreads();
+// Block-wide bitonic sort of buf[0..n) ascending (n a power of two, n <= 8 * NT).
+// The keys live in registers (element u * NT + tid in v[u]); a compare-exchange
+// at stride s runs in-thread (s >= NT), through LDS (64 <= s < NT: two
+// barriers) or as a cross-lane shuffle (s < 64, no barrier), so most of the
+// log2(n) * (log2(n) + 1) / 2 stages cost no block synchronisation.  Slots past
+// n hold the maximum key (they sort last and are never written back).
+template <typename T, int NT, int E, int US>
+__device__ __forceinline__ void sort_inthread(T (&v)[E], int size, int tid) {
+#pragma unroll
+  for (int u = 0; u < E; ++u) {
+    if ((u & US) == 0 && (u | US) < E) {
+      const int i = u * NT + tid;
+      const bool up = (i & size) == 0;
+      const T a = v[u], b = v[u | US];
+      v[u] = up ? (a < b ? a : b) : (a < b ? b : a);
+      v[u | US] = up ? (a < b ? b : a) : (a < b ? a : b);
     }
   }
 }
+
+template <typename T, int NT, int N>
+__device__ __forceinline__ void block_sort_fixed(T* buf, int n) {
+  constexpr int E = N / NT;
+  const int tid = threadIdx.x;
+  const T kMax = ~(T)0;
+  T v[E];
+#pragma unroll
+  for (int u = 0; u < E; ++u) {
+    const int i = u * NT + tid;
+    v[u] = i < n ? buf[i] : kMax;
+  }
+  __syncthreads();
+#pragma unroll
+  for (int size = 2; size <= N; size <<= 1) {
+#pragma unroll
+    for (int stride = size >> 1; stride > 0; stride >>= 1) {
+      if (stride >= NT) {
+        if (E >= 2 && stride == NT) sort_inthread<T, NT, E, 1>(v, size, tid);
+        else if (E >= 4 && stride == 2 * NT) sort_inthread<T, NT, E, 2>(v, size, tid);
+        else if (E >= 8) sort_inthread<T, NT, E, 4>(v, size, tid);
+      } else {
+        T p[E];
+        if (stride >= 64) {
+#pragma unroll
+          for (int u = 0; u < E; ++u) buf[u * NT + tid] = v[u];
+          __syncthreads();
+#pragma unroll
+          for (int u = 0; u < E; ++u) p[u] = buf[(u * NT + tid) ^ stride];
+          __syncthreads();
+        } else {
+#pragma unroll
+          for (int u = 0; u < E; ++u) p[u] = __shfl_xor(v[u], stride, 64);
+        }
+#pragma unroll
+        for (int u = 0; u < E; ++u) {
+          const int i = u * NT + tid;
+          const bool keep_min = ((i & stride) == 0) == ((i & size) == 0);
+          const T a = v[u], b = p[u];
+          v[u] = keep_min ? (a < b ? a : b) : (a < b ? b : a);
+        }
+      }
+    }
+  }
+#pragma unroll
+  for (int u = 0; u < E; ++u) {
+    const int i = u * NT + tid;
+    if (i < n) buf[i] = v[u];
+  }
+  __syncthreads();
+}
+
+template <typename T, int NT>
+__device__ __forceinline__ void block_sort(T* buf, int n) {
+  if (n <= 1) {
+    __syncthreads();
+    return;
+  }
+  if (n <= NT) block_sort_fixed<T, NT, NT>(buf, n);
+  else if (n <= 2 * NT) block_sort_fixed<T, NT, 2 * NT>(buf, n);
+  else if (n <= 4 * NT) block_sort_fixed<T, NT, 4 * NT>(buf, n);
+  else block_sort_fixed<T, NT, 8 * NT>(buf, n);
+}
+
+// Bitonic sort of buf[0..n2) ascending (n2 power of two, <= kSelBuf), whole block.
+__device__ __forceinline__ void block_bitonic(uint64_t* buf, int n2) { block_sort<uint64_t, kSelThreads>(buf, n2); }
 
 template <int INPUT, int OUTPUT>
 __global__ __launch_bounds__(kSelThreads) void select_kernel(SelectArgs a) {
@@ -735,7 +801,8 @@ __global__ __launch_bounds__(kSelThreads) void select_kernel(SelectArgs a) {
 #pragma unroll
     for (int u = 0; u < kSelKPT; ++u) {
       const int64_t j = (int64_t)u * kSelThreads + tid;
-      kr[u] = j < c ? sel_load<INPUT>(a, q, j) : ~0ull;
+      const uint64_t x = sel_load<INPUT>(a, q, j < c ? j : 0);   // clamped: loads issue back to back
+      kr[u] = j < c ? x : ~0ull;
     }
     float lo = __builtin_inff(), hi = -__builtin_inff();
 #pragma unroll
@@ -1069,24 +1136,7 @@ __global__ __launch_bounds__(kSelThreads) void select_kernel(SelectArgs a) {
 constexpr int kKthChunk = 4096;
 constexpr int kKthThreads = 512;
 
-__device__ __forceinline__ void block_bitonic_u32(uint32_t* buf, int n2, int nthreads) {
-  const int tid = threadIdx.x;
-  for (int size = 2; size <= n2; size <<= 1) {
-    for (int stride = size >> 1; stride > 0; stride >>= 1) {
-      for (int i = tid; i < n2 / 2; i += nthreads) {
-        const int lo = 2 * i - (i & (stride - 1));
-        const int hi = lo + stride;
-        const bool up = ((lo & size) == 0);
-        const uint32_t x = buf[lo], y = buf[hi];
-        if ((x > y) == up) {
-          buf[lo] = y;
-          buf[hi] = x;
-        }
-      }
-      __syncthreads();
-    }
-  }
-}
+__device__ __forceinline__ void block_bitonic_u32(uint32_t* buf, int n2) { block_sort<uint32_t, kKthThreads>(buf, n2); }
 
 // Best r keys of one 4096-key chunk.  Keys live in registers (8 per thread);
 // a 256-bin histogram linear in the score value (per-wave sub-histograms)
@@ -1223,7 +1273,7 @@ __global__ __launch_bounds__(kKthThreads) void kth_partial_kernel(const uint32_t
   while (n2 < nsel) n2 <<= 1;
   for (int i = nsel + tid; i < n2; i += kKthThreads) buf[i] = 0xFFFFFFFFu;
   __syncthreads();
-  block_bitonic_u32(buf, n2, kKthThreads);
+  block_bitonic_u32(buf, n2);
   uint32_t* o = part + (q * nchunk + blockIdx.x) * r;
   for (int i = tid; i < r; i += kKthThreads) o[i] = i < nsel ? buf[i] : 0xFFFFFFFFu;
 }
@@ -1237,12 +1287,22 @@ __global__ __launch_bounds__(kKthThreads) void kth_final_kernel(const uint32_t* 
   __shared__ uint32_t buf[kKthChunk];
   const int64_t q = blockIdx.x;
   const int tot = nlists * r;
-  for (int i = threadIdx.x; i < kKthChunk; i += kKthThreads)
-    buf[i] = i < tot ? part[(int64_t)(i / r) * lstride + q * qstride + (i % r)] : 0xFFFFFFFFu;
+  {
+    uint32_t tmp[kKthChunk / kKthThreads];
+#pragma unroll
+    for (int u = 0; u < kKthChunk / kKthThreads; ++u) {
+      const int i = threadIdx.x + u * kKthThreads;
+      const int ic = i < tot ? i : 0;
+      const uint32_t x = part[(int64_t)(ic / r) * lstride + q * qstride + (ic % r)];
+      tmp[u] = i < tot ? x : 0xFFFFFFFFu;
+    }
+#pragma unroll
+    for (int u = 0; u < kKthChunk / kKthThreads; ++u) buf[threadIdx.x + u * kKthThreads] = tmp[u];
+  }
   __syncthreads();
   int n2 = 1;
   while (n2 < tot) n2 <<= 1;
-  block_bitonic_u32(buf, n2, kKthThreads);
+  block_bitonic_u32(buf, n2);
   if (tau && threadIdx.x == 0) {
     const uint32_t kr = buf[r - 1];
     tau[q] = (kr == 0xFFFFFFFFu) ? -__builtin_inff() : desc_key_to_score(kr);
@@ -1251,68 +1311,129 @@ __global__ __launch_bounds__(kKthThreads) void kth_final_kernel(const uint32_t* 
     for (int i = threadIdx.x; i < r; i += kKthThreads) best[q * r + i] = buf[i];
 }
 
-// Tree merge of packed per-shard lists: all P2 = pow2ceil(nparts) lists of k
-// sorted keys sit in LDS (missing lists = pads); log2(P2) rounds merge pairs
-// in place (every element computes its rank in the merged pair with one
-// binary search, all reads finish before the barrier, survivors (rank < k) are
-// written after it).  EPT = elements per thread in round 0 (P2 * k / 512).
+// Tree merge of packed per-shard lists by bitonic networks: all P2 =
+// pow2ceil(nparts) lists, padded to KP = pow2ceil(k) keys, sit in LDS.  Each
+// round merges list pairs (A, B): the half-cleaner min(A[i], B[KP-1-i]) keeps
+// exactly the KP smallest keys of A u B as a bitonic sequence, which a bitonic
+// merge (strides KP/2 .. 1) sorts.  Keys are held in registers; strides < 64
+// are cross-lane shuffles, strides >= NT are in-thread, the rest go through
+// the pair's own LDS slot (consecutive addresses, conflict-free) -- unlike a
+// binary-search merge, whose scattered 64-bit LDS reads serialise on banks.
 constexpr int kTreeThreads = 512;
+constexpr int kTreeMaxE = 16;   // keys per thread in round 0: P2 / 2 * KP <= 16 * 512
 
-template <int EPT>
+template <int US>
+__device__ __forceinline__ void tree_inthread(uint64_t (&v)[kTreeMaxE]) {
+#pragma unroll
+  for (int t = 0; t < kTreeMaxE; ++t) {
+    if ((t & US) == 0) {
+      const uint64_t a = v[t], b = v[t | US];
+      v[t] = a < b ? a : b;
+      v[t | US] = a < b ? b : a;
+    }
+  }
+}
+
+template <int KP>
 __global__ __launch_bounds__(kTreeThreads) void merge_packed_tree_kernel(const uint64_t* parts, int64_t nq,
                                                                          int nparts, int p2, int k,
                                                                          int64_t n_global, float* out_s,
                                                                          int64_t* out_i, int32_t* status) {
-  extern __shared__ __attribute__((aligned(16))) uint64_t L[];  // [p2][k]
+  extern __shared__ __attribute__((aligned(16))) uint64_t L[];  // [p2][KP]
+  constexpr int NT = kTreeThreads;
   __shared__ int bad;
   const int tid = threadIdx.x;
+  const int lane = tid & 63;
   const int64_t q = blockIdx.x;
   const int64_t ps = (int64_t)(k + 1);
   if (tid == 0) bad = 0;
   __syncthreads();
-  for (int e = tid; e < p2 * k; e += kTreeThreads) {
-    const int l = e / k, i = e - l * k;
-    L[e] = l < nparts ? parts[((int64_t)l * nq + q) * ps + i] : ~0ull;
+  {
+    uint64_t tmp[2 * kTreeMaxE];
+#pragma unroll
+    for (int t = 0; t < 2 * kTreeMaxE; ++t) {
+      const int e = tid + t * NT;
+      const int l = e / KP, i = e & (KP - 1);
+      const bool ok = e < p2 * KP && l < nparts && i < k;
+      // unconditional load from a clamped address, then select: a guarded load
+      // makes hipcc branch around it and drain vmcnt(0) per element
+      const uint64_t x = parts[((int64_t)(ok ? l : 0) * nq + q) * ps + (ok ? i : 0)];
+      tmp[t] = ok ? x : ~0ull;
+    }
+#pragma unroll
+    for (int t = 0; t < 2 * kTreeMaxE; ++t) {
+      const int e = tid + t * NT;
+      if (e < p2 * KP) L[e] = tmp[t];
+    }
   }
   if (tid < nparts && (parts[((int64_t)tid * nq + q) * ps + k] & 1ull)) bad = 1;
   __syncthreads();
   for (int half = 1; half < p2; half <<= 1) {
-    // pair g merges slot 2g*half (A) with slot (2g+1)*half (B) into slot 2g*half
     const int npairs = p2 / (2 * half);
-    const int nel = npairs * 2 * k;
-    uint64_t key[EPT];
-    int pos[EPT];
+    const int total = npairs * KP;             // keys this round (outputs)
+    uint64_t v[kTreeMaxE];
+    // half-cleaner: pair g, index i -> min(A[i], B[KP - 1 - i])
 #pragma unroll
-    for (int t = 0; t < EPT; ++t) {
-      const int e = tid + t * kTreeThreads;
-      pos[t] = -1;
-      if (e < nel) {
-        const int g = e / (2 * k), w = e - g * 2 * k;
-        const int side = w >= k, i = w - side * k;
-        const uint64_t* A = L + (int64_t)(2 * g) * half * k;
-        const uint64_t* B = A + (int64_t)half * k;
-        const uint64_t* other = side ? A : B;
-        const uint64_t x = (side ? B : A)[i];
-        int lo = 0, hi = k;
-        if (!side) {       // #B < x
-          while (lo < hi) { const int mid = (lo + hi) >> 1; if (other[mid] < x) lo = mid + 1; else hi = mid; }
-        } else {           // #A <= x
-          while (lo < hi) { const int mid = (lo + hi) >> 1; if (other[mid] <= x) lo = mid + 1; else hi = mid; }
-        }
-        const int r = i + lo;
-        if (r < k) {
-          key[t] = x;
-          pos[t] = (2 * g) * half * k + r;
-        }
+    for (int t = 0; t < kTreeMaxE; ++t) {
+      const int e = tid + t * NT;
+      const int g = e / KP, i = e & (KP - 1);
+      v[t] = ~0ull;
+      if (e < total) {
+        const uint64_t a = L[(2 * g) * half * KP + i];
+        const uint64_t b = L[(2 * g + 1) * half * KP + (KP - 1 - i)];
+        v[t] = a < b ? a : b;
       }
     }
     __syncthreads();
+    // bitonic merge of each pair's KP keys (ascending).  Stage loop kept rolled:
+    // a fully unrolled network is tens of KB of straight-line code that every
+    // (single-pass) wave fetches cold, which costs more than the loop overhead.
+#pragma unroll 1
+    for (int stride = KP / 2; stride > 0; stride >>= 1) {
+      if (stride >= NT) {
+        switch (stride / NT) {
+          case 1: tree_inthread<1>(v); break;
+          case 2: tree_inthread<2>(v); break;
+          default: tree_inthread<4>(v); break;
+        }
+      } else if (stride >= 64) {
 #pragma unroll
-    for (int t = 0; t < EPT; ++t)
-      if (pos[t] >= 0) L[pos[t]] = key[t];
+        for (int t = 0; t < kTreeMaxE; ++t) {
+          const int e = tid + t * NT;
+          if (e < total) L[(2 * (e / KP)) * half * KP + (e & (KP - 1))] = v[t];
+        }
+        __syncthreads();
+#pragma unroll
+        for (int t = 0; t < kTreeMaxE; ++t) {
+          const int e = tid + t * NT;
+          if (e < total) {
+            const int pe = e ^ stride;
+            const uint64_t b = L[(2 * (pe / KP)) * half * KP + (pe & (KP - 1))];
+            const bool lower = (e & stride) == 0;
+            v[t] = lower ? (v[t] < b ? v[t] : b) : (v[t] < b ? b : v[t]);
+          }
+        }
+        __syncthreads();
+      } else {
+#pragma unroll
+        for (int t = 0; t < kTreeMaxE; ++t) {
+          if ((tid & ~63) + t * NT < total) {   // wave-uniform: total is a multiple of 64
+            const uint64_t b = __shfl_xor(v[t], stride, 64);
+            const bool lower = (lane & stride) == 0;
+            v[t] = lower ? (v[t] < b ? v[t] : b) : (v[t] < b ? b : v[t]);
+          }
+        }
+      }
+    }
+    // sorted pair result -> slot 2g * half
+#pragma unroll
+    for (int t = 0; t < kTreeMaxE; ++t) {
+      const int e = tid + t * NT;
+      if (e < total) L[(2 * (e / KP)) * half * KP + (e & (KP - 1))] = v[t];
+    }
     __syncthreads();
   }
-  for (int i = tid; i < k; i += kTreeThreads) {
+  for (int i = tid; i < k; i += NT) {
     const uint64_t x = L[i];
     if (x == ~0ull) {
       out_s[q * k + i] = kPadScore;
@@ -1412,10 +1533,24 @@ __global__ __launch_bounds__(kMergeThreads) void merge_kernel(const float* score
   __syncthreads();
   for (int p = 1; p < nparts; ++p) {
     const int nb = k_in < k_out ? k_in : k_out;
-    for (int i = tid; i < nb; i += kMergeThreads) {
-      const int64_t o = ((int64_t)p * nq + q) * k_in + i;
-      kb[i] = desc_key(scores[o]);
-      ib[i] = ids[o];
+    {
+      float sv[kSelMaxK / kMergeThreads];
+      int64_t iv[kSelMaxK / kMergeThreads];
+#pragma unroll
+      for (int u = 0; u < kSelMaxK / kMergeThreads; ++u) {   // clamped loads, issued back to back
+        const int i = tid + u * kMergeThreads;
+        const int64_t o = ((int64_t)p * nq + q) * k_in + (i < nb ? i : 0);
+        sv[u] = scores[o];
+        iv[u] = ids[o];
+      }
+#pragma unroll
+      for (int u = 0; u < kSelMaxK / kMergeThreads; ++u) {
+        const int i = tid + u * kMergeThreads;
+        if (i < nb) {
+          kb[i] = desc_key(sv[u]);
+          ib[i] = iv[u];
+        }
+      }
     }
     __syncthreads();
     const int nc = (na + nb) < k_out ? (na + nb) : k_out;
@@ -2044,24 +2179,30 @@ int drt_topk_merge_packed(const uint64_t* parts, int64_t nq, int32_t nparts, int
   const ProfPair pp = prof_begin(PROF_MERGE, s);
   int p2 = 1;
   while (p2 < nparts) p2 <<= 1;
-  const size_t lds = (size_t)p2 * k * 8;
-  const int ept = (p2 * k + kTreeThreads - 1) / kTreeThreads;
+  int kp = 64;
+  while (kp < k) kp <<= 1;
+  const size_t lds = (size_t)p2 * kp * 8;
   int rc = DRT_OK;
-  if (nparts > 1 && lds <= 128 * 1024 && ept <= 32) {
-#define DRT_TREE(E)                                                                                          \
+  if (nparts > 1 && (p2 / 2) * kp <= kTreeMaxE * kTreeThreads && lds <= 128 * 1024) {
+#define DRT_TREE(KPV)                                                                                        \
   {                                                                                                          \
     static bool attr_set = false;                                                                            \
     if (!attr_set) {                                                                                         \
-      DRT_CHECK_HIP(hipFuncSetAttribute((const void*)merge_packed_tree_kernel<E>,                            \
+      DRT_CHECK_HIP(hipFuncSetAttribute((const void*)merge_packed_tree_kernel<KPV>,                          \
                                         hipFuncAttributeMaxDynamicSharedMemorySize, 128 * 1024));            \
       attr_set = true;                                                                                       \
     }                                                                                                        \
-    hipLaunchKernelGGL(merge_packed_tree_kernel<E>, dim3((unsigned)nq), dim3(kTreeThreads), lds, s, parts, nq, \
-                       (int)nparts, p2, (int)k, n_global, out_scores, out_ids, status);                      \
+    hipLaunchKernelGGL(merge_packed_tree_kernel<KPV>, dim3((unsigned)nq), dim3(kTreeThreads), lds, s, parts,   \
+                       nq, (int)nparts, p2, (int)k, n_global, out_scores, out_ids, status);                  \
   }
-    if (ept <= 8) DRT_TREE(8)
-    else if (ept <= 16) DRT_TREE(16)
-    else DRT_TREE(32)
+    switch (kp) {
+      case 64: DRT_TREE(64) break;
+      case 128: DRT_TREE(128) break;
+      case 256: DRT_TREE(256) break;
+      case 512: DRT_TREE(512) break;
+      case 1024: DRT_TREE(1024) break;
+      default: DRT_TREE(2048) break;
+    }
 #undef DRT_TREE
   } else {
     hipLaunchKernelGGL(merge_packed_kernel, dim3((unsigned)nq), dim3(512), 0, s, parts, nq, (int)nparts, (int)k,
