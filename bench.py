@@ -50,7 +50,7 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--encode", action="store_true", help="also time the bf16 BERT-base passage encoder")
     ap.add_argument("--scan-variant", type=int, default=0, help="benchmark-only ablation of the scan kernel")
-    ap.add_argument("--streams", type=int, default=2,
+    ap.add_argument("--streams", type=int, default=1,
                     help="HIP streams the query batches rotate over (overlaps one batch's exchange and small "
                          "kernels with the next batch's scan)")
     ap.add_argument("--protocol", choices=["global_tau", "per_shard"], default="global_tau",
@@ -126,6 +126,23 @@ def cpu_baseline(args):
                    f"against a {rows}-row slice ({qps_sample:.1f} q/s), scaled by {rows}/{args.n_corpus} "
                    f"to the full corpus; {el:.1f} s"),
     }
+
+
+def pmc_traffic(args, world):
+    """HBM bytes per launch of the dominant kernel from a committed rocprofv3 PMC pass
+    (tools/pmc_traffic.py -> profiles/*_pmc_traffic.json) measured on this exact
+    configuration; None when no such measurement exists."""
+    import glob
+    want = {"n_corpus": args.n_corpus, "world": world, "qb": args.qb, "k": args.k, "dim": args.dim}
+    for f in sorted(glob.glob(os.path.join(REPO, "profiles", "*_pmc_traffic.json")), reverse=True):
+        try:
+            with open(f) as fh:
+                rec = json.load(fh)
+        except (OSError, ValueError):
+            continue
+        if rec.get("config") == want:
+            return int(rec["traffic_bytes_per_launch"]), os.path.basename(f)
+    return None, None
 
 
 def encode_leg(args, device):
@@ -253,6 +270,7 @@ def main():
         per = -(-args.n_corpus // world)
         alg_bytes = per * d * 2 + qb * d * 2 + (qb * (k + 1) * 8 if use_global else qb * k * 12)
         achieved = alg_bytes / (scan_ms_v * 1e-3) / 1e9
+        traffic, traffic_src = pmc_traffic(args, world)
         out = {
             "metric": "queries/sec@top-1000, 10Mx768 corpus (BASELINE: passages encoded/sec + queries/sec@top-1000, 10Mx768 corpus, 1/2/4/8 GPU)",
             "value": round(qps, 2),
@@ -283,7 +301,8 @@ def main():
                 "peak": HBM_PEAK_GBS,
                 "unit": "GB/s",
                 "frac": round(achieved / HBM_PEAK_GBS, 4),
-                "traffic": None,
+                "traffic": traffic,
+                "traffic_source": traffic_src,
                 "avg_launch_ms": round(scan_ms_v, 4),
                 "launches": int(cnt.value),
                 "alg_bytes_per_launch": alg_bytes,

@@ -43,10 +43,13 @@ if [ "${PMC:-0}" = "1" ]; then
   cd /tmp
   for C in FETCH_SIZE WRITE_SIZE; do
     timeout -k 10 600 rocprofv3 --pmc $C --output-format csv -d $GRAFT_REPO_ROOT/$OUT/pmc_${TAG}_$C -o run \
-      -- python3 $GRAFT_REPO_ROOT/bench.py --steps 3 --warmup 1 --no-cpu-baseline > $GRAFT_REPO_ROOT/$OUT/pmc_${TAG}_$C.log 2>&1
+      -- python3 $GRAFT_REPO_ROOT/bench.py --steps 3 --warmup 1 --no-cpu-baseline ${BENCH_ARGS:-} > $GRAFT_REPO_ROOT/$OUT/pmc_${TAG}_$C.log 2>&1
     rc=$?; echo "=== pmc $C rc=$rc" | tee -a $GRAFT_REPO_ROOT/$OUT/session.log
     [ $rc -ne 0 ] && exit $rc
   done
+  python3 $GRAFT_REPO_ROOT/tools/pmc_traffic.py $GRAFT_REPO_ROOT/$OUT/pmc_${TAG}_FETCH_SIZE $GRAFT_REPO_ROOT/$OUT/pmc_${TAG}_WRITE_SIZE \
+    $GRAFT_REPO_ROOT/$OUT/${TAG}_pmc_traffic.json --n-corpus ${NCORPUS:-10000000}
+  cd $GRAFT_REPO_ROOT
 fi
 if [ "${GEMMB:-0}" = "1" ]; then
   cd $GRAFT_REPO_ROOT && timeout -k 10 300 python tools/gemm_bench.py > $OUT/gemm_bench.log 2>&1; echo "=== gemm_bench rc=$?"; tail -2 $OUT/gemm_bench.log
