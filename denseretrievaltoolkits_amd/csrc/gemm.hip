@@ -31,7 +31,9 @@ struct GemmArgs {
   int64_t m, n, k;
   int64_t lda, ldb, ldc, ldr;
   float alpha;
+  unsigned long long* dbg;  // diagnostic builds only (segment stamps)
 };
+static unsigned long long* g_gemm_dbg = nullptr;
 
 __device__ __forceinline__ void g_glds16(const void* gsrc, uint32_t lds_addr) {
   uint32_t keep;
@@ -69,6 +71,22 @@ __device__ __forceinline__ void stage_panel(const __bf16* base, int64_t ld, int6
 __device__ __forceinline__ float gelu_erf(float x) {
   // transformers ACT2FN["gelu"] = GELUActivation: x * 0.5 * (1 + erf(x / sqrt(2)))
   return 0.5f * x * (1.0f + erff(x * 0.70710678118654752f));
+}
+
+// GELU(erf) with erf from Abramowitz & Stegun 7.1.26 (|error| <= 1.5e-7, far below
+// the bf16 rounding of the stored activation): one rcp, one exp, 6 FMA.
+__device__ __forceinline__ float gelu_fast(float x) {
+  const float z = fabsf(x) * 0.70710678118654752f;
+  const float t = __builtin_amdgcn_rcpf(fmaf(0.3275911f, z, 1.0f));
+  float p = fmaf(1.061405429f, t, -1.453152027f);
+  p = fmaf(p, t, 1.421413741f);
+  p = fmaf(p, t, -0.284496736f);
+  p = fmaf(p, t, 0.254829592f);
+  p *= t;
+  const float e = __builtin_amdgcn_exp2f(-z * z * 1.4426950408889634f);
+  const float erf_abs = fmaf(-p, e, 1.0f);
+  const float erf_v = x < 0.f ? -erf_abs : erf_abs;
+  return 0.5f * x * (1.0f + erf_v);
 }
 
 enum { EPI_NONE = 0, EPI_BIAS = 1, EPI_GELU = 2, EPI_RESID = 4 };
@@ -413,15 +431,493 @@ __global__ __launch_bounds__(kLThreads, 1) void gemm_nt_l_kernel(GemmArgs a) {
   l_epilogue<OUT_BF16, EPI>(a, acc, m0, n0, wm, wn, r, h);
 }
 
+// ---------------------------------------------------------------------------
+// Ping-pong 256 x 256 kernel (the encoder projections' main path).
+//
+//  * 8 waves = two groups of 4 (waves 0-3: token rows 0-127 of the tile,
+//    waves 4-7: rows 128-255), one wave of each group per SIMD.  Group 1 runs
+//    one s_barrier behind group 0, so on every SIMD one wave issues its MFMA
+//    cluster while its partner issues the LDS fragment reads and LDS-DMA of the
+//    next phase (matrix beside memory, MI355X_MICROARCH.md "Two waves per SIMD").
+//  * K is streamed in slabs of 32: one slab = X panel [256 tok][64 B] + W panel
+//    [256 out][64 B] = 32 KiB, landed by global_load_lds_dwordx4 into a 4-slot
+//    ring (128 KiB), two slabs in flight (counted vmcnt, never 0 in the loop,
+//    raw s_barrier).  Each phase issues one panel (2 DMA per wave) of slab s+2.
+//  * slab = 2 phases per wave: phase a reads W frags j 0-3 + X frags i 0-3 and
+//    issues 16 v_mfma_f32_16x16x32_bf16; phase b reads X frags i 4-7 and issues
+//    16 more.  Wave tile = 128 tokens x 64 outputs = 8 x 4 tiles of 16 x 16.
+//  * operands swapped (D = W . X^T): lane owns one token row and 4 consecutive
+//    output columns per tile -> 8-B bf16 / 16-B fp32 stores.
+// Panel image: [row][4 x 16 B], 16-B chunk XOR ((row >> 1) & 2): conflict-free
+// ds_read_b128 for the 16x16x32 lane map (row = lane & 15, chunk = lane >> 4).
+// WAR/RAW of the ring (group 1 lags one barrier): slab s+2 is waited for in
+// phase b of slab s by every wave before the barrier both groups pass before
+// reading it; slot (s+2)&3 last held slab s-2, whose final reads retired
+// (lgkmcnt(0)) two barriers before the first DMA into it.
+// ---------------------------------------------------------------------------
+constexpr int kPPanel = kL * 32 * 2;     // 16 KiB
+constexpr int kPSlab = 2 * kPPanel;      // 32 KiB
+constexpr int kPRing = 4;
+
+// 256 rows x 32 k into a [row][4 x 16 B] panel: 16 wave-instructions of 16 rows, 2 per wave.
+__device__ __forceinline__ void stage_panel32(const __bf16* base, int64_t ld, int64_t row0, int64_t rows,
+                                              int64_t k0, uint32_t lds, int wave, int lane) {
+  const int rsub = lane >> 2, pos = lane & 3;
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    const int J = j * 8 + wave;
+    const int row = J * 16 + rsub;
+    int64_t gr = row0 + row;
+    gr = gr < rows ? gr : rows - 1;
+    const int c = pos ^ ((row >> 1) & 2);
+    g_glds16(base + gr * ld + k0 + c * 8, __builtin_amdgcn_readfirstlane(lds + J * 1024));
+  }
+}
+
+// s_waitcnt vmcnt(4 * n): all but the n youngest slabs (4 LDS-DMA per wave each) landed.
+__device__ __forceinline__ void vmcnt_slabs_after(int n) {
+  switch (n) {
+    case 0: asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); break;
+    case 1: asm volatile("s_waitcnt vmcnt(4)" ::: "memory"); break;
+    case 2: asm volatile("s_waitcnt vmcnt(8)" ::: "memory"); break;
+    case 3: asm volatile("s_waitcnt vmcnt(12)" ::: "memory"); break;
+    default: asm volatile("s_waitcnt vmcnt(16)" ::: "memory"); break;
+  }
+}
+
+template <bool OUT_BF16, int EPI>
+__device__ __forceinline__ void pp_epilogue(const GemmArgs& a, f32x4 (&acc)[8][4], int64_t m0, int64_t n0, int grp,
+                                            int wn, int fr, int fc) {
+  // Epilogue. acc[i][j][u]: token row m0 + grp*128 + i*16 + fr,
+  //                         output col n0 + wn*64 + j*16 + 4*fc + u.
+  const bool full_n = (n0 + kL <= a.n) && (a.ldc % 4 == 0) && (!(EPI & EPI_RESID) || a.ldr % 4 == 0);
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int64_t col = n0 + wn * 64 + j * 16 + 4 * fc;
+    f32x4 bv = {0.f, 0.f, 0.f, 0.f};
+    if (EPI & EPI_BIAS) {
+      if (full_n) bv = *(const f32x4*)(a.bias + col);
+      else
+#pragma unroll
+        for (int u = 0; u < 4; ++u) bv[u] = col + u < a.n ? a.bias[col + u] : 0.f;
+    }
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const int64_t row = m0 + grp * 128 + i * 16 + fr;
+      if (row >= a.m) continue;
+      f32x4 v;
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        float x = acc[i][j][u] * a.alpha + bv[u];
+        if (EPI & EPI_GELU) x = gelu_erf(x);
+        v[u] = x;
+      }
+      if (full_n) {
+        if (EPI & EPI_RESID) {
+          const bf16x4 rv = *(const bf16x4*)(a.R + row * a.ldr + col);
+#pragma unroll
+          for (int u = 0; u < 4; ++u) v[u] += (float)rv[u];
+        }
+        if (OUT_BF16) {
+          bf16x4 o;
+#pragma unroll
+          for (int u = 0; u < 4; ++u) o[u] = (__bf16)v[u];
+          *(bf16x4*)((__bf16*)a.C + row * a.ldc + col) = o;
+        } else {
+          *(f32x4*)((float*)a.C + row * a.ldc + col) = v;
+        }
+      } else {
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          if (col + u >= a.n) continue;
+          float x = v[u];
+          if (EPI & EPI_RESID) x += (float)a.R[row * a.ldr + col + u];
+          if (OUT_BF16) ((__bf16*)a.C)[row * a.ldc + col + u] = (__bf16)x;
+          else ((float*)a.C)[row * a.ldc + col + u] = x;
+        }
+      }
+    }
+  }
+}
+
+// Epilogue through LDS (T21-style widening): each wave stages its 128 x 64 output
+// slice in a private LDS region (row-per-lane 8-B pieces in, 16-B row-contiguous
+// pieces out, 16-B chunks XOR-swizzled by row), then writes whole 128-B (bf16) /
+// 256-B (fp32) row segments.  Needs a full tile in n; rows are masked.
+template <bool OUT_BF16, int EPI>
+__device__ __forceinline__ void pp_epilogue_lds(const GemmArgs& a, f32x4 (&acc)[8][4], int64_t m0, int64_t n0,
+                                                int grp, int wn, int fr, int fc, char* lds_wave, int lane) {
+  const int64_t colw = n0 + wn * 64;   // first column of this wave's slice
+  f32x4 bv[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    bv[j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    if (EPI & EPI_BIAS) bv[j] = *(const f32x4*)(a.bias + colw + j * 16 + 4 * fc);
+  }
+  if (OUT_BF16) {
+    // [128 rows][8 x 16 B], chunk ^= row & 7
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const int r = i * 16 + fr;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        bf16x4 o;
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          float x = acc[i][j][u] * a.alpha + bv[j][u];
+          if (EPI & EPI_GELU) x = gelu_fast(x);
+          o[u] = (__bf16)x;
+        }
+        const int chunk = (2 * j + (fc >> 1)) ^ (r & 7);
+        *(bf16x4*)(lds_wave + r * 128 + chunk * 16 + (fc & 1) * 8) = o;
+      }
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    const int c = lane & 7;
+#pragma unroll
+    for (int p = 0; p < 16; ++p) {
+      const int r = p * 8 + (lane >> 3);
+      const bf16x8 v = *(const bf16x8*)(lds_wave + r * 128 + ((c ^ (r & 7)) << 4));
+      const int64_t row = m0 + grp * 128 + r;
+      if (row < a.m) *(bf16x8*)((__bf16*)a.C + row * a.ldc + colw + c * 8) = v;
+    }
+  } else {
+    // two passes of 64 rows: [64 rows][16 x 16 B] fp32, chunk ^= row & 7
+    const int c = lane & 15;
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      bf16x4 rv[16];
+      if (EPI & EPI_RESID) {
+#pragma unroll
+        for (int p = 0; p < 16; ++p) {
+          int64_t row = m0 + grp * 128 + h * 64 + p * 4 + (lane >> 4);
+          row = row < a.m ? row : a.m - 1;
+          rv[p] = *(const bf16x4*)(a.R + row * a.ldr + colw + c * 4);
+        }
+      }
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int r = i * 16 + fr;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          f32x4 v;
+#pragma unroll
+          for (int u = 0; u < 4; ++u) {
+            float x = acc[h * 4 + i][j][u] * a.alpha + bv[j][u];
+            if (EPI & EPI_GELU) x = gelu_fast(x);
+            v[u] = x;
+          }
+          const int chunk = (j * 4 + fc) ^ (r & 7);
+          *(f32x4*)(lds_wave + r * 256 + chunk * 16) = v;
+        }
+      }
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+#pragma unroll
+      for (int p = 0; p < 16; ++p) {
+        const int r = p * 4 + (lane >> 4);
+        f32x4 v = *(const f32x4*)(lds_wave + r * 256 + ((c ^ (r & 7)) << 4));
+        const int64_t row = m0 + grp * 128 + h * 64 + r;
+        if (row < a.m) {
+          if (EPI & EPI_RESID) {
+#pragma unroll
+            for (int u = 0; u < 4; ++u) v[u] += (float)rv[p][u];
+          }
+          *(f32x4*)((float*)a.C + row * a.ldc + colw + c * 4) = v;
+        }
+      }
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    }
+  }
+}
+
+#define PP_STAMP(idx)                                                                         \
+  if (ABL == 3 && s >= 8 && s < 12 && lane == 0 && blockIdx.x < 16)                              \
+    a.dbg[((blockIdx.x * 8 + wave) * 4 + (s - 8)) * 10 + (idx)] = __builtin_amdgcn_s_memtime();
+
+template <bool OUT_BF16, int EPI, int ABL = 0>
+__global__ __launch_bounds__(kLThreads, 1) void gemm_nt_pp_kernel(GemmArgs a) {
+  __shared__ __attribute__((aligned(16))) char smem[kPRing * kPSlab];
+  const int tid = threadIdx.x;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int lane = tid & 63;
+  const int grp = wave >> 2;              // ping-pong group = token half
+  const int wn = wave & 3;                // 64-column slice of the tile
+
+  const int nwg = gridDim.x;
+  const int bid = blockIdx.x;
+  const int xcd = bid & 7, q8 = nwg >> 3, r8 = nwg & 7;
+  const int wg = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (bid >> 3);
+  const int tiles_n = (int)((a.n + kL - 1) / kL);
+  const int64_t m0 = (int64_t)(wg / tiles_n) * kL;
+  const int64_t n0 = (int64_t)(wg % tiles_n) * kL;
+
+  const uint32_t lds0 = g_lds_addr(smem);
+  const int ns = (int)(a.k / 32);
+
+  f32x4 acc[8][4];
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  const int fr = lane & 15, fc = lane >> 4;
+  const int foff = fr * 64 + ((fc ^ ((fr >> 1) & 2)) << 4);
+  const int xoff = grp * 128 * 64 + foff;            // X panel: this group's 128 token rows
+  const int woff = kPPanel + wn * 64 * 64 + foff;    // W panel: this wave's 64 output rows
+
+  // prologue: slabs 0 and 1 in flight, slab 0 landed
+  stage_panel32(a.A, a.lda, m0, a.m, 0, lds0, wave, lane);
+  stage_panel32(a.B, a.ldb, n0, a.n, 0, lds0 + kPPanel, wave, lane);
+  if (ns > 1) {
+    stage_panel32(a.A, a.lda, m0, a.m, 32, lds0 + kPSlab, wave, lane);
+    stage_panel32(a.B, a.ldb, n0, a.n, 32, lds0 + kPSlab + kPPanel, wave, lane);
+    asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+  } else {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  }
+  __builtin_amdgcn_s_barrier();
+  if (grp == 1) __builtin_amdgcn_s_barrier();
+  __builtin_amdgcn_sched_barrier(0);
+
+  for (int s = 0; s < ns; ++s) {
+    const char* slab = smem + (s & (kPRing - 1)) * kPSlab;
+    const bool pre = (ABL != 1) && s + 2 < ns;
+    const uint32_t nslab = lds0 + ((s + 2) & (kPRing - 1)) * kPSlab;
+    // ---- phase a: memory
+    PP_STAMP(8)
+    bf16x8 wf[4], xf[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) wf[j] = *(const bf16x8*)(slab + woff + j * 1024);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) xf[i] = *(const bf16x8*)(slab + xoff + i * 1024);
+    if (pre) stage_panel32(a.A, a.lda, m0, a.m, (int64_t)(s + 2) * 32, nslab, wave, lane);
+    __builtin_amdgcn_sched_barrier(0);
+    PP_STAMP(9)
+    __builtin_amdgcn_s_barrier();
+    PP_STAMP(0)
+    // ---- phase a: matrix
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_sched_barrier(0);
+    PP_STAMP(1)
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        if (ABL == 2) { asm volatile("" :: "v"(wf[j]), "v"(xf[i])); continue; }
+        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[j], xf[i], acc[i][j], 0, 0, 0);
+      }
+    __builtin_amdgcn_s_setprio(0);
+    __builtin_amdgcn_sched_barrier(0);
+    PP_STAMP(2)
+    __builtin_amdgcn_s_barrier();
+    PP_STAMP(3)
+    // ---- phase b: memory
+#pragma unroll
+    for (int i = 0; i < 4; ++i) xf[i] = *(const bf16x8*)(slab + xoff + (i + 4) * 1024);
+    if (pre) {
+      stage_panel32(a.B, a.ldb, n0, a.n, (int64_t)(s + 2) * 32, nslab + kPPanel, wave, lane);
+      asm volatile("s_waitcnt vmcnt(4)" ::: "memory");   // slab s+1 landed, s+2 in flight
+    } else {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    __builtin_amdgcn_sched_barrier(0);
+    PP_STAMP(4)
+    __builtin_amdgcn_s_barrier();
+    PP_STAMP(5)
+    // ---- phase b: matrix
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_sched_barrier(0);
+    PP_STAMP(6)
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        if (ABL == 2) { asm volatile("" :: "v"(wf[j]), "v"(xf[i])); continue; }
+        acc[i + 4][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[j], xf[i], acc[i + 4][j], 0, 0, 0);
+      }
+    __builtin_amdgcn_s_setprio(0);
+    __builtin_amdgcn_sched_barrier(0);
+    PP_STAMP(7)
+    __builtin_amdgcn_s_barrier();
+  }
+  if (grp == 0) __builtin_amdgcn_s_barrier();
+
+  pp_epilogue<OUT_BF16, EPI>(a, acc, m0, n0, grp, wn, fr, fc);
+}
+
+// One phase per slab: per wave, a memory segment (12 fragment reads of slab s,
+// LDS-DMA of slab s+3, vmcnt for slab s+1, lgkmcnt(0)) and a 32-MFMA segment,
+// ping-ponged with the partner wave of the other group.  Because the reading
+// wave drains its own fragment reads before the barrier that ends its memory
+// segment, the ring slot of slab s is free one barrier later: 4 slots carry
+// 3 slabs in flight (96 KiB per CU).
+// RAW: slab s+1 is waited for (vmcnt) in the memory segment of slab s by every
+// wave, before the barrier after which group 0 reads it.  WAR: slot (s+3)&3
+// held slab s-1, whose reads both groups drained before the barrier that
+// precedes group 0's memory segment of slab s.
+template <bool OUT_BF16, int EPI, int ABL = 0, int RING = 4>
+__global__ __launch_bounds__(kLThreads, 1) void gemm_nt_pp1_kernel(GemmArgs a) {
+  constexpr int D = RING - 1;   // slabs in flight
+  __shared__ __attribute__((aligned(16))) char smem[RING * kPSlab];
+  const int tid = threadIdx.x;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int lane = tid & 63;
+  const int grp = wave >> 2;
+  const int wn = wave & 3;
+
+  const int nwg = gridDim.x;
+  const int bid = blockIdx.x;
+  const int xcd = bid & 7, q8 = nwg >> 3, r8 = nwg & 7;
+  const int wg = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (bid >> 3);
+  const int tiles_n = (int)((a.n + kL - 1) / kL);
+  const int64_t m0 = (int64_t)(wg / tiles_n) * kL;
+  const int64_t n0 = (int64_t)(wg % tiles_n) * kL;
+
+  const uint32_t lds0 = g_lds_addr(smem);
+  const int ns = (int)(a.k / 32);
+  unsigned long long st0 = 0, st1 = 0, st2 = 0;
+  if (ABL & 32) st0 = __builtin_amdgcn_s_memtime();
+
+  f32x4 acc[8][4];
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  const int fr = lane & 15, fc = lane >> 4;
+  const int foff = fr * 64 + ((fc ^ ((fr >> 1) & 2)) << 4);
+  const int xoff = grp * 128 * 64 + foff;
+  const int woff = kPPanel + wn * 64 * 64 + foff;
+
+  // prologue: slabs 0..D-1 in flight, slab 0 landed
+#pragma unroll
+  for (int p = 0; p < D; ++p) {
+    if (p < ns) {
+      stage_panel32(a.A, a.lda, m0, a.m, p * 32, lds0 + p * kPSlab, wave, lane);
+      stage_panel32(a.B, a.ldb, n0, a.n, p * 32, lds0 + p * kPSlab + kPPanel, wave, lane);
+    }
+  }
+  vmcnt_slabs_after(ns - 1 < D - 1 ? ns - 1 : D - 1);
+  __builtin_amdgcn_s_barrier();
+  if (grp == 1 && !(ABL & 4)) __builtin_amdgcn_s_barrier();
+  __builtin_amdgcn_sched_barrier(0);
+
+  if (ABL & 32) st1 = __builtin_amdgcn_s_memtime();
+  unsigned long long t_start = 0;
+  if (ABL & 16) t_start = __builtin_amdgcn_s_memtime();
+  int slot = 0, fill = D % RING;
+  for (int s = 0; s < ns; ++s) {
+    const char* slab = smem + slot * kPSlab;
+    // ---- memory segment
+    bf16x8 wf[4], xf[8];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) wf[j] = (ABL & 8) ? bf16x8{} : *(const bf16x8*)(slab + woff + j * 1024);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) xf[i] = (ABL & 8) ? bf16x8{} : *(const bf16x8*)(slab + xoff + i * 1024);
+    if (ABL & 8) {
+#pragma unroll
+      for (int i = 0; i < 8; ++i) asm volatile("" : "+v"(xf[i]));
+#pragma unroll
+      for (int j = 0; j < 4; ++j) asm volatile("" : "+v"(wf[j]));
+    }
+    const int left = (ABL & 1) ? 0 : ns - 1 - s;   // slabs after s
+    if (left >= D) {
+      const uint32_t nslab = lds0 + fill * kPSlab;
+      stage_panel32(a.A, a.lda, m0, a.m, (int64_t)(s + D) * 32, nslab, wave, lane);
+      stage_panel32(a.B, a.ldb, n0, a.n, (int64_t)(s + D) * 32, nslab + kPPanel, wave, lane);
+      vmcnt_slabs_after(D - 1);
+    } else {
+      vmcnt_slabs_after(left > 0 ? left - 1 : 0);
+    }
+    slot = slot + 1 == RING ? 0 : slot + 1;
+    fill = fill + 1 == RING ? 0 : fill + 1;
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_sched_barrier(0);
+    if (!(ABL & 4)) __builtin_amdgcn_s_barrier();
+    // ---- matrix segment
+    __builtin_amdgcn_sched_barrier(0);
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        if (ABL & 2) { asm volatile("" :: "v"(wf[j]), "v"(xf[i])); continue; }
+        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[j], xf[i], acc[i][j], 0, 0, 0);
+      }
+    __builtin_amdgcn_s_setprio(0);
+    __builtin_amdgcn_sched_barrier(0);
+    if (!(ABL & 4)) __builtin_amdgcn_s_barrier();
+  }
+  if (ABL & 16) {
+    const unsigned long long t_end = __builtin_amdgcn_s_memtime();
+    if (lane == 0 && blockIdx.x < 64) {
+      a.dbg[(blockIdx.x * 8 + wave) * 2] = t_start;
+      a.dbg[(blockIdx.x * 8 + wave) * 2 + 1] = t_end;
+    }
+  }
+  if (grp == 0 && !(ABL & 4)) __builtin_amdgcn_s_barrier();
+  if (ABL & 32) st2 = __builtin_amdgcn_s_memtime();
+  const bool full = (n0 + kL <= a.n) && (a.ldc % 8 == 0) && (!(EPI & EPI_RESID) || a.ldr % 4 == 0);
+  if (full) pp_epilogue_lds<OUT_BF16, EPI>(a, acc, m0, n0, grp, wn, fr, fc, smem + wave * 16384, lane);
+  else pp_epilogue<OUT_BF16, EPI>(a, acc, m0, n0, grp, wn, fr, fc);
+  if (ABL & 32) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    const unsigned long long st3 = __builtin_amdgcn_s_memtime();
+    unsigned xcc;
+    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
+    unsigned hw;
+    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hw));
+    if (lane == 0 && wave == 0) {
+      unsigned long long* d = a.dbg + blockIdx.x * 6;
+      d[0] = st0; d[1] = st1; d[2] = st2; d[3] = st3; d[4] = xcc; d[5] = hw;
+    }
+  }
+}
+
 template <bool OUT_BF16, int EPI>
 static int launch_gemm_t(const GemmArgs& a, hipStream_t s) {
   const ProfPair pp = prof_begin(PROF_GEMM, s);
   // large tiles once there are >= 2 tiles per CU of them; small problems keep 128^2
   const int64_t tiles_l = ((a.m + kL - 1) / kL) * ((a.n + kL - 1) / kL);
   if (tiles_l >= 512 && g_gemm_variant == 0) {
+    hipLaunchKernelGGL((gemm_nt_pp1_kernel<OUT_BF16, EPI, 0, 5>), dim3((unsigned)tiles_l), dim3(kLThreads), 0, s, a);
+  } else if (tiles_l >= 512 && g_gemm_variant == 9) {
     hipLaunchKernelGGL((gemm_nt_l_kernel<OUT_BF16, EPI>), dim3((unsigned)tiles_l), dim3(kLThreads), 0, s, a);
   } else if (tiles_l >= 512 && g_gemm_variant == 2) {
     hipLaunchKernelGGL((gemm_nt_lh_kernel<OUT_BF16, EPI>), dim3((unsigned)tiles_l), dim3(kLThreads), 0, s, a);
+  } else if (tiles_l >= 512 && g_gemm_variant == 3) {
+    hipLaunchKernelGGL((gemm_nt_pp_kernel<OUT_BF16, EPI>), dim3((unsigned)tiles_l), dim3(kLThreads), 0, s, a);
+  } else if (tiles_l >= 512 && g_gemm_variant == 4) {
+    hipLaunchKernelGGL((gemm_nt_pp_kernel<OUT_BF16, EPI, 1>), dim3((unsigned)tiles_l), dim3(kLThreads), 0, s, a);
+  } else if (tiles_l >= 512 && g_gemm_variant == 6 && g_gemm_dbg) {
+    GemmArgs b = a;
+    b.dbg = g_gemm_dbg;
+    hipLaunchKernelGGL((gemm_nt_pp_kernel<OUT_BF16, EPI, 3>), dim3((unsigned)tiles_l), dim3(kLThreads), 0, s, b);
+  } else if (tiles_l >= 512 && g_gemm_variant >= 16 && g_gemm_dbg) {
+    GemmArgs b = a;
+    b.dbg = g_gemm_dbg;
+    dim3 G((unsigned)tiles_l), T(kLThreads);
+    switch (g_gemm_variant - 16) {
+      case 0: hipLaunchKernelGGL((gemm_nt_pp1_kernel<OUT_BF16, EPI, 16>), G, T, 0, s, b); break;
+      case 1: hipLaunchKernelGGL((gemm_nt_pp1_kernel<OUT_BF16, EPI, 17>), G, T, 0, s, b); break;
+      case 2: hipLaunchKernelGGL((gemm_nt_pp1_kernel<OUT_BF16, EPI, 18>), G, T, 0, s, b); break;
+      case 4: hipLaunchKernelGGL((gemm_nt_pp1_kernel<OUT_BF16, EPI, 20>), G, T, 0, s, b); break;
+      case 5: hipLaunchKernelGGL((gemm_nt_pp1_kernel<OUT_BF16, EPI, 21>), G, T, 0, s, b); break;
+      case 8: hipLaunchKernelGGL((gemm_nt_pp1_kernel<OUT_BF16, EPI, 24>), G, T, 0, s, b); break;
+      case 9: hipLaunchKernelGGL((gemm_nt_pp1_kernel<OUT_BF16, EPI, 25>), G, T, 0, s, b); break;
+      case 12: hipLaunchKernelGGL((gemm_nt_pp1_kernel<OUT_BF16, EPI, 28>), G, T, 0, s, b); break;
+      case 13: hipLaunchKernelGGL((gemm_nt_pp1_kernel<OUT_BF16, EPI, 29>), G, T, 0, s, b); break;
+      case 15: hipLaunchKernelGGL((gemm_nt_pp1_kernel<OUT_BF16, EPI, 32>), G, T, 0, s, b); break;
+      default: return DRT_EINVAL;
+    }
+  } else if (tiles_l >= 512 && g_gemm_variant == 7) {
+    hipLaunchKernelGGL((gemm_nt_pp1_kernel<OUT_BF16, EPI>), dim3((unsigned)tiles_l), dim3(kLThreads), 0, s, a);
+  } else if (tiles_l >= 512 && g_gemm_variant == 8) {
+    hipLaunchKernelGGL((gemm_nt_pp1_kernel<OUT_BF16, EPI, 0, 5>), dim3((unsigned)tiles_l), dim3(kLThreads), 0, s, a);
+  } else if (tiles_l >= 512 && g_gemm_variant == 5) {
+    hipLaunchKernelGGL((gemm_nt_pp_kernel<OUT_BF16, EPI, 2>), dim3((unsigned)tiles_l), dim3(kLThreads), 0, s, a);
   } else {
     const int64_t tiles = ((a.m + kBM - 1) / kBM) * ((a.n + kBN - 1) / kBN);
     hipLaunchKernelGGL((gemm_nt_kernel<OUT_BF16, EPI>), dim3((unsigned)tiles), dim3(kGemmThreads), 0, s, a);
@@ -503,9 +999,15 @@ extern "C" int drt_linear_bf16(const void* X, const void* W, const float* bias, 
 }
 
 // Testing / benchmarking switch: 0 = automatic, 1 = 128^2 kernel for every size,
-// 2 = large half-K-ring kernel where the large kernel applies.
+// 2 = large half-K-ring kernel where the large kernel applies, 3 = ping-pong 256^2 kernel.
 extern "C" int drt_gemm_force_small(int32_t on) {
-  if (on < 0 || on > 2) return DRT_EINVAL;
+  if (on < 0 || on > 31) return DRT_EINVAL;
   g_gemm_variant = on;
+  return DRT_OK;
+}
+
+// Diagnostic: device buffer for the variant-6 segment stamps (16 blocks x 8 waves x 4 slabs x 4 u64).
+extern "C" int drt_gemm_debug_buffer(void* buf) {
+  g_gemm_dbg = (unsigned long long*)buf;
   return DRT_OK;
 }

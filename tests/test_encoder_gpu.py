@@ -95,7 +95,9 @@ def test_linear_epilogues_vs_torch(dev):
 @pytest.mark.parametrize("M,N,K,flags", [(16384, 2304, 768, 0), (32768, 768, 3072, 2), (20000, 3072, 768, 1),
                                           (131072, 768, 768, 2)])
 def test_large_tile_gemm_vs_torch_and_small_kernel(dev, M, N, K, flags):
-    """256x256-tile kernel (>= 512 tiles) against torch fp32 and the 128x128 kernel."""
+    """256x256-tile kernels (>= 512 tiles) against torch fp32 and the 128x128 kernel.
+    Variants: 0 auto (ping-pong, 5-slot ring), 1 128x128, 2 half-K ring, 3 ping-pong 2-phase,
+    7 ping-pong 4-slot ring, 8 ping-pong 5-slot ring, 9 full-K 32x32x16 kernel."""
     import torch
     from denseretrievaltoolkits_amd import _native
     lib = _native.load()
@@ -111,7 +113,8 @@ def test_large_tile_gemm_vs_torch_and_small_kernel(dev, M, N, K, flags):
         ref = ref + r.float()
     dt = torch.float32 if flags & 2 else torch.bfloat16
     outs = []
-    for force in (0, 1, 2):
+    variants = (0, 1, 2, 3, 7, 8, 9)
+    for force in variants:
         lib.drt_gemm_force_small(force)
         out = torch.empty(M, N, dtype=dt, device=dev)
         _native.check(lib.drt_linear_bf16(x.data_ptr(), w.data_ptr(), b.data_ptr(),
@@ -120,7 +123,10 @@ def test_large_tile_gemm_vs_torch_and_small_kernel(dev, M, N, K, flags):
         outs.append(out.float())
     lib.drt_gemm_force_small(0)
     tol = dict(atol=2e-3, rtol=1e-4) if dt == torch.float32 else dict(atol=3e-2, rtol=1e-2)
-    torch.testing.assert_close(outs[0], ref, **tol)
-    # both kernels accumulate each k-step in the same order -> identical fp32 results
+    for v, o in zip(variants, outs):
+        torch.testing.assert_close(o, ref, **tol, msg=lambda m: f"variant {v}: {m}")
+    # kernels on the same MFMA shape accumulate each k-step in the same order -> identical fp32 results
     if dt == torch.float32:
-        assert torch.equal(outs[0], outs[1]) and torch.equal(outs[0], outs[2])
+        by = dict(zip(variants, outs))
+        assert torch.equal(by[1], by[2]) and torch.equal(by[1], by[9])
+        assert torch.equal(by[0], by[3]) and torch.equal(by[0], by[7]) and torch.equal(by[0], by[8])
