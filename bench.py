@@ -5,8 +5,9 @@ BASELINE.json metric: "passages encoded/sec + queries/sec@top-1000, 10M x 768
 corpus, 1/2/4/8 GPU".  `value` is the search half (queries/sec@top-1000, the
 north-star path: brute-force Q.D^T + top-k, BaseFaissIPRetriever.search,
 DRT/evaluator/index.py:31-33); the encode half is reported beside it under
-"encode" when --encode is given (passages/sec of the bf16 BERT-base passage
-tower, DRModel.encode, DRT/model/biencoder.py:127-151).
+"encode" (passages/sec of the bf16 BERT-base passage
+tower, DRModel.encode, DRT/model/biencoder.py:127-151), timed on every rank
+after the search leg (weak scaling: each rank encodes its own batches).
 
 One step = one query batch (Qb = 128, the reference's eval batch,
 arguments.py:189) searched exactly against the WHOLE corpus (k = 1000):
@@ -48,7 +49,8 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-rows", type=int, default=1_000_000)
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
-    ap.add_argument("--encode", action="store_true", help="also time the bf16 BERT-base passage encoder")
+    ap.add_argument("--no-encode", action="store_true",
+                    help="skip the encode leg (passages/sec of the bf16 BERT-base passage tower, every rank)")
     ap.add_argument("--scan-variant", type=int, default=0, help="benchmark-only ablation of the scan kernel")
     ap.add_argument("--streams", type=int, default=1,
                     help="HIP streams the query batches rotate over (overlaps one batch's exchange and small "
@@ -311,10 +313,21 @@ def main():
         }
         if world == 1 and not args.no_cpu_baseline:
             out["cpu_baseline"] = cpu_baseline(args)
-        if args.encode:
-            enc = encode_leg(args, dev)
-            if enc is not None:
-                out["encode"] = enc
+    enc = None if args.no_encode else encode_leg(args, dev)
+    if enc is not None:
+        if world > 1:
+            # aggregate over ranks: every rank encodes its own batches; slowest rank sets the rate
+            pps = torch.tensor([enc["value"]], dtype=torch.float64, device="cpu" if gloo else dev)
+            dist.all_reduce(pps, op=dist.ReduceOp.MIN)
+            enc["per_gpu_min"] = float(pps.item())
+            enc["value"] = round(float(pps.item()) * world, 1)
+            enc["scaling"] = "weak"
+            rf = enc["roofline"]
+            rf["achieved"] = round(rf["flop_per_passage"] * enc["per_gpu_min"] / 1e12, 1)
+            rf["frac"] = round(rf["achieved"] / rf["peak"], 4)
+        if out is not None:
+            out["encode"] = enc
+    if rank == 0:
         print(json.dumps(out), flush=True)
     if world > 1:
         dist.barrier()

@@ -20,7 +20,7 @@ def flops_per_seq(L, H=768, layers=12, inter=3072):
     return lin + att
 
 
-def run(device, batch=512, L=128, steps=5, warmup=2):
+def run(device, batch=512, L=128, steps=10, warmup=2):
     from transformers import BertConfig, BertModel
     from .model.encoder import HipBertEncoder
     from . import _native

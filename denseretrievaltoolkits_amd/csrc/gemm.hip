@@ -630,123 +630,6 @@ __device__ __forceinline__ void pp_epilogue_lds(const GemmArgs& a, f32x4 (&acc)[
   }
 }
 
-#define PP_STAMP(idx)                                                                         \
-  if (ABL == 3 && s >= 8 && s < 12 && lane == 0 && blockIdx.x < 16)                              \
-    a.dbg[((blockIdx.x * 8 + wave) * 4 + (s - 8)) * 10 + (idx)] = __builtin_amdgcn_s_memtime();
-
-template <bool OUT_BF16, int EPI, int ABL = 0>
-__global__ __launch_bounds__(kLThreads, 1) void gemm_nt_pp_kernel(GemmArgs a) {
-  __shared__ __attribute__((aligned(16))) char smem[kPRing * kPSlab];
-  const int tid = threadIdx.x;
-  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int lane = tid & 63;
-  const int grp = wave >> 2;              // ping-pong group = token half
-  const int wn = wave & 3;                // 64-column slice of the tile
-
-  const int nwg = gridDim.x;
-  const int bid = blockIdx.x;
-  const int xcd = bid & 7, q8 = nwg >> 3, r8 = nwg & 7;
-  const int wg = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (bid >> 3);
-  const int tiles_n = (int)((a.n + kL - 1) / kL);
-  const int64_t m0 = (int64_t)(wg / tiles_n) * kL;
-  const int64_t n0 = (int64_t)(wg % tiles_n) * kL;
-
-  const uint32_t lds0 = g_lds_addr(smem);
-  const int ns = (int)(a.k / 32);
-
-  f32x4 acc[8][4];
-#pragma unroll
-  for (int i = 0; i < 8; ++i)
-#pragma unroll
-    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-
-  const int fr = lane & 15, fc = lane >> 4;
-  const int foff = fr * 64 + ((fc ^ ((fr >> 1) & 2)) << 4);
-  const int xoff = grp * 128 * 64 + foff;            // X panel: this group's 128 token rows
-  const int woff = kPPanel + wn * 64 * 64 + foff;    // W panel: this wave's 64 output rows
-
-  // prologue: slabs 0 and 1 in flight, slab 0 landed
-  stage_panel32(a.A, a.lda, m0, a.m, 0, lds0, wave, lane);
-  stage_panel32(a.B, a.ldb, n0, a.n, 0, lds0 + kPPanel, wave, lane);
-  if (ns > 1) {
-    stage_panel32(a.A, a.lda, m0, a.m, 32, lds0 + kPSlab, wave, lane);
-    stage_panel32(a.B, a.ldb, n0, a.n, 32, lds0 + kPSlab + kPPanel, wave, lane);
-    asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
-  } else {
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  }
-  __builtin_amdgcn_s_barrier();
-  if (grp == 1) __builtin_amdgcn_s_barrier();
-  __builtin_amdgcn_sched_barrier(0);
-
-  for (int s = 0; s < ns; ++s) {
-    const char* slab = smem + (s & (kPRing - 1)) * kPSlab;
-    const bool pre = (ABL != 1) && s + 2 < ns;
-    const uint32_t nslab = lds0 + ((s + 2) & (kPRing - 1)) * kPSlab;
-    // ---- phase a: memory
-    PP_STAMP(8)
-    bf16x8 wf[4], xf[4];
-#pragma unroll
-    for (int j = 0; j < 4; ++j) wf[j] = *(const bf16x8*)(slab + woff + j * 1024);
-#pragma unroll
-    for (int i = 0; i < 4; ++i) xf[i] = *(const bf16x8*)(slab + xoff + i * 1024);
-    if (pre) stage_panel32(a.A, a.lda, m0, a.m, (int64_t)(s + 2) * 32, nslab, wave, lane);
-    __builtin_amdgcn_sched_barrier(0);
-    PP_STAMP(9)
-    __builtin_amdgcn_s_barrier();
-    PP_STAMP(0)
-    // ---- phase a: matrix
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    __builtin_amdgcn_sched_barrier(0);
-    PP_STAMP(1)
-    __builtin_amdgcn_s_setprio(1);
-#pragma unroll
-    for (int i = 0; i < 4; ++i)
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        if (ABL == 2) { asm volatile("" :: "v"(wf[j]), "v"(xf[i])); continue; }
-        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[j], xf[i], acc[i][j], 0, 0, 0);
-      }
-    __builtin_amdgcn_s_setprio(0);
-    __builtin_amdgcn_sched_barrier(0);
-    PP_STAMP(2)
-    __builtin_amdgcn_s_barrier();
-    PP_STAMP(3)
-    // ---- phase b: memory
-#pragma unroll
-    for (int i = 0; i < 4; ++i) xf[i] = *(const bf16x8*)(slab + xoff + (i + 4) * 1024);
-    if (pre) {
-      stage_panel32(a.B, a.ldb, n0, a.n, (int64_t)(s + 2) * 32, nslab + kPPanel, wave, lane);
-      asm volatile("s_waitcnt vmcnt(4)" ::: "memory");   // slab s+1 landed, s+2 in flight
-    } else {
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    }
-    __builtin_amdgcn_sched_barrier(0);
-    PP_STAMP(4)
-    __builtin_amdgcn_s_barrier();
-    PP_STAMP(5)
-    // ---- phase b: matrix
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    __builtin_amdgcn_sched_barrier(0);
-    PP_STAMP(6)
-    __builtin_amdgcn_s_setprio(1);
-#pragma unroll
-    for (int i = 0; i < 4; ++i)
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        if (ABL == 2) { asm volatile("" :: "v"(wf[j]), "v"(xf[i])); continue; }
-        acc[i + 4][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[j], xf[i], acc[i + 4][j], 0, 0, 0);
-      }
-    __builtin_amdgcn_s_setprio(0);
-    __builtin_amdgcn_sched_barrier(0);
-    PP_STAMP(7)
-    __builtin_amdgcn_s_barrier();
-  }
-  if (grp == 0) __builtin_amdgcn_s_barrier();
-
-  pp_epilogue<OUT_BF16, EPI>(a, acc, m0, n0, grp, wn, fr, fc);
-}
-
 // One phase per slab: per wave, a memory segment (12 fragment reads of slab s,
 // LDS-DMA of slab s+3, vmcnt for slab s+1, lgkmcnt(0)) and a 32-MFMA segment,
 // ping-ponged with the partner wave of the other group.  Because the reading
@@ -887,14 +770,6 @@ static int launch_gemm_t(const GemmArgs& a, hipStream_t s) {
     hipLaunchKernelGGL((gemm_nt_l_kernel<OUT_BF16, EPI>), dim3((unsigned)tiles_l), dim3(kLThreads), 0, s, a);
   } else if (tiles_l >= 512 && g_gemm_variant == 2) {
     hipLaunchKernelGGL((gemm_nt_lh_kernel<OUT_BF16, EPI>), dim3((unsigned)tiles_l), dim3(kLThreads), 0, s, a);
-  } else if (tiles_l >= 512 && g_gemm_variant == 3) {
-    hipLaunchKernelGGL((gemm_nt_pp_kernel<OUT_BF16, EPI>), dim3((unsigned)tiles_l), dim3(kLThreads), 0, s, a);
-  } else if (tiles_l >= 512 && g_gemm_variant == 4) {
-    hipLaunchKernelGGL((gemm_nt_pp_kernel<OUT_BF16, EPI, 1>), dim3((unsigned)tiles_l), dim3(kLThreads), 0, s, a);
-  } else if (tiles_l >= 512 && g_gemm_variant == 6 && g_gemm_dbg) {
-    GemmArgs b = a;
-    b.dbg = g_gemm_dbg;
-    hipLaunchKernelGGL((gemm_nt_pp_kernel<OUT_BF16, EPI, 3>), dim3((unsigned)tiles_l), dim3(kLThreads), 0, s, b);
   } else if (tiles_l >= 512 && g_gemm_variant >= 16 && g_gemm_dbg) {
     GemmArgs b = a;
     b.dbg = g_gemm_dbg;
@@ -902,12 +777,6 @@ static int launch_gemm_t(const GemmArgs& a, hipStream_t s) {
     switch (g_gemm_variant - 16) {
       case 0: hipLaunchKernelGGL((gemm_nt_pp1_kernel<OUT_BF16, EPI, 16>), G, T, 0, s, b); break;
       case 1: hipLaunchKernelGGL((gemm_nt_pp1_kernel<OUT_BF16, EPI, 17>), G, T, 0, s, b); break;
-      case 2: hipLaunchKernelGGL((gemm_nt_pp1_kernel<OUT_BF16, EPI, 18>), G, T, 0, s, b); break;
-      case 4: hipLaunchKernelGGL((gemm_nt_pp1_kernel<OUT_BF16, EPI, 20>), G, T, 0, s, b); break;
-      case 5: hipLaunchKernelGGL((gemm_nt_pp1_kernel<OUT_BF16, EPI, 21>), G, T, 0, s, b); break;
-      case 8: hipLaunchKernelGGL((gemm_nt_pp1_kernel<OUT_BF16, EPI, 24>), G, T, 0, s, b); break;
-      case 9: hipLaunchKernelGGL((gemm_nt_pp1_kernel<OUT_BF16, EPI, 25>), G, T, 0, s, b); break;
-      case 12: hipLaunchKernelGGL((gemm_nt_pp1_kernel<OUT_BF16, EPI, 28>), G, T, 0, s, b); break;
       case 13: hipLaunchKernelGGL((gemm_nt_pp1_kernel<OUT_BF16, EPI, 29>), G, T, 0, s, b); break;
       case 15: hipLaunchKernelGGL((gemm_nt_pp1_kernel<OUT_BF16, EPI, 32>), G, T, 0, s, b); break;
       default: return DRT_EINVAL;
@@ -916,8 +785,6 @@ static int launch_gemm_t(const GemmArgs& a, hipStream_t s) {
     hipLaunchKernelGGL((gemm_nt_pp1_kernel<OUT_BF16, EPI>), dim3((unsigned)tiles_l), dim3(kLThreads), 0, s, a);
   } else if (tiles_l >= 512 && g_gemm_variant == 8) {
     hipLaunchKernelGGL((gemm_nt_pp1_kernel<OUT_BF16, EPI, 0, 5>), dim3((unsigned)tiles_l), dim3(kLThreads), 0, s, a);
-  } else if (tiles_l >= 512 && g_gemm_variant == 5) {
-    hipLaunchKernelGGL((gemm_nt_pp_kernel<OUT_BF16, EPI, 2>), dim3((unsigned)tiles_l), dim3(kLThreads), 0, s, a);
   } else {
     const int64_t tiles = ((a.m + kBM - 1) / kBM) * ((a.n + kBN - 1) / kBN);
     hipLaunchKernelGGL((gemm_nt_kernel<OUT_BF16, EPI>), dim3((unsigned)tiles), dim3(kGemmThreads), 0, s, a);

@@ -153,11 +153,11 @@ int drt_pool_bf16(const void* hidden, const int64_t* mask, int64_t B, int64_t L,
                   int32_t mode, float* out, void* out_bf16, void* stream);
 int drt_l2_normalize_f32(float* x, int64_t B, int32_t H, void* out_bf16, void* stream);
 /* A/B switch for tests/bench: 0 automatic (ping-pong 256x256, 5-slot ring),
- * 1 forces the 128x128-tile GEMM, 2 half-K-ring 256x256, 3 ping-pong 2-phase,
+ * 1 forces the 128x128-tile GEMM, 2 half-K-ring 256x256,
  * 7/8 ping-pong 4/5-slot ring, 9 full-K 32x32x16 256x256; >= 16 diagnostic
  * builds (ablations / cycle stamps, need drt_gemm_debug_buffer).            */
 int drt_gemm_force_small(int32_t on);
-/* Diagnostic only: device buffer for the GEMM cycle-stamp variants (drt_gemm_force_small(6, >= 16)). */
+/* Diagnostic only: device buffer for the GEMM cycle-stamp variants (drt_gemm_force_small >= 16). */
 int drt_gemm_debug_buffer(void* buf);
 
 /* ------------------------------------------------------------------------

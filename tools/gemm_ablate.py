@@ -1,5 +1,5 @@
 """Loop-only cycle stamps of the pp1 GEMM under ablations (diagnostic variants 16+bits:
-1 no LDS-DMA in the loop, 2 no MFMA, 4 no barriers, 8 no fragment reads).  Prints
+1 no LDS-DMA in the loop, 13 = no DMA, no barriers, no fragment reads: the bare MFMA loop).  Prints
 median cycles per slab (first tile of blocks 0-63) and the kernel's TFLOP/s."""
 import os
 import sys
@@ -22,8 +22,7 @@ out = torch.empty(M, N, dtype=torch.float32 if flags & 2 else torch.bfloat16, de
 dbg = torch.zeros(64 * 8 * 2, dtype=torch.int64, device=dev)
 lib.drt_gemm_debug_buffer(dbg.data_ptr())
 s = _native.stream_ptr(dev)
-names = {0: "base", 1: "nodma", 2: "nomfma", 4: "nobar", 5: "nobar+nodma", 8: "nods", 9: "nods+nodma",
-         12: "nods+nobar", 13: "nods+nobar+nodma"}
+names = {0: "base", 1: "nodma", 13: "nods+nobar+nodma"}
 for abl, nm in names.items():
     lib.drt_gemm_force_small(16 + abl)
     call = lambda: _native.check(lib.drt_linear_bf16(x.data_ptr(), w.data_ptr(), b.data_ptr(),

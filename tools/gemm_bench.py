@@ -1,7 +1,7 @@
 """GEMM throughput of the encoder projection shapes per kernel variant (HIP events),
 plus a correctness check of every variant against torch fp32 and torch's hipBLASLt
-bf16 GEMM as a reference point.  Variants: 0 auto, 1 128^2, 2 large half-K ring,
-3 ping-pong 256^2."""
+bf16 GEMM as a reference point.  Variants: 0 auto (= 8), 1 128^2, 2 large half-K ring,
+7/8 ping-pong 256^2 with a 4/5-slot ring, 9 full-K 32x32x16 256^2."""
 import json
 import sys
 
@@ -10,7 +10,7 @@ import torch
 sys.path.insert(0, __import__("os").path.dirname(__import__("os").path.dirname(__import__("os").path.abspath(__file__))))
 from denseretrievaltoolkits_amd import _native  # noqa: E402
 
-VARIANTS = {0: "auto", 1: "small", 2: "half", 3: "pp", 4: "pp_nodma", 5: "pp_nomfma", 7: "pp1", 8: "pp1r5"}
+VARIANTS = {0: "auto", 1: "small", 2: "half", 7: "pp1", 8: "pp1r5", 9: "large32"}
 
 
 def run(M=65536, reps=20, variants=(0, 1, 2, 3)):
@@ -65,5 +65,5 @@ def run(M=65536, reps=20, variants=(0, 1, 2, 3)):
 
 
 if __name__ == "__main__":
-    vs = tuple(int(v) for v in sys.argv[1].split(",")) if len(sys.argv) > 1 else (0, 1, 2, 3)
+    vs = tuple(int(v) for v in sys.argv[1].split(",")) if len(sys.argv) > 1 else (0, 1, 9)
     run(variants=vs)
