@@ -327,6 +327,9 @@ def main():
             rf["frac"] = round(rf["achieved"] / rf["peak"], 4)
         if out is not None:
             out["encode"] = enc
+    if rank == 0 and not args.no_encode and world == 1:
+        from denseretrievaltoolkits_amd import bench_encode
+        out["rerank"] = bench_encode.run_rerank(dev)
     if rank == 0:
         print(json.dumps(out), flush=True)
     if world > 1:

@@ -68,3 +68,47 @@ def run(device, batch=512, L=128, steps=10, warmup=2):
             "gemm_only_tflops": round(gemm_tf, 1) if gemm_tf else None,
         },
     }
+
+
+def run_rerank(device, pairs=1000, q_len=32, p_len=128, steps=3, warmup=1):
+    """Config C5 (BASELINE.json configs[4]): cross-encoder rerank of the top-1000
+    candidates of one query per step (RRModel.encode, DRT/model/reranker.py:111-130):
+    1000 pairs [CLS] q [SEP] p [SEP] of L = q_len + p_len = 160 tokens through the bf16
+    BERT-base tower, [CLS] pooling, LinearHead(768 -> 1)."""
+    from transformers import BertConfig, BertModel
+    from .model.encoder import HipBertEncoder, linear_head
+    torch.manual_seed(0)
+    m = BertModel(BertConfig(), add_pooling_layer=False).eval()
+    enc = HipBertEncoder.from_hf(m, device)
+    del m
+    L = q_len + p_len
+    g = torch.Generator(device=device)
+    g.manual_seed(2)
+    ids = torch.randint(1000, 30522, (pairs, L), generator=g, device=device, dtype=torch.int64)
+    ids[:, 0] = 101
+    ids[:, q_len - 1] = 102
+    ids[:, -1] = 102
+    mask = torch.ones((pairs, L), dtype=torch.int64, device=device)
+    head_w = (0.02 * torch.randn((1, 768), generator=g, device=device)).to(torch.bfloat16)
+
+    def step():
+        _, rb = enc.pool(enc(ids, mask), mask, "first", want_bf16=True)
+        return linear_head(rb, head_w)
+
+    for _ in range(warmup):
+        step()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        step()
+    torch.cuda.synchronize()
+    el = time.perf_counter() - t0
+    qps = steps / el
+    fl = flops_per_seq(L) * pairs
+    return {
+        "metric": f"queries/sec reranked (top-{pairs} pairs per query, L={L}, bf16 BERT-base cross-encoder)",
+        "value": round(qps, 2), "unit": "queries/s", "pairs_per_query": pairs, "seq_len": L, "steps": steps,
+        "ms_per_step": round(el / steps * 1e3, 3),
+        "roofline": {"bound": "mfma", "achieved": round(fl * qps / 1e12, 1), "peak": 2500.0, "unit": "TFLOP/s",
+                     "frac": round(fl * qps / 1e12 / 2500.0, 4), "flop_per_pair": flops_per_seq(L)},
+    }

@@ -64,14 +64,21 @@ def main():
     fams = {"scan": _native.PROF_SCAN, "sample": _native.PROF_SAMPLE, "select": _native.PROF_SELECT,
             "merge": _native.PROF_MERGE}
 
-    def timed(fn, label):
+    def timed(fn, label, nstreams=1):
         fn(0)
         torch.cuda.synchronize()
+        main_s = torch.cuda.current_stream(dev)
+        streams = [main_s] + [torch.cuda.Stream(device=dev) for _ in range(nstreams - 1)]
         for f in fams.values():
             lib.drt_profile_enable(f, 1)
         t0 = time.perf_counter()
+        for st in streams[1:]:
+            st.wait_stream(main_s)
         for j in range(a.steps):
-            fn(j)
+            with torch.cuda.stream(streams[j % len(streams)]):
+                fn(j)
+        for st in streams[1:]:
+            main_s.wait_stream(st)
         torch.cuda.synchronize()
         el = time.perf_counter() - t0
         res = {"ms_per_step": round(el / a.steps * 1e3, 4)}
@@ -103,6 +110,8 @@ def main():
         kernels.topk_merge(S, I, k)
 
     timed(gt, "global_tau")
+    timed(gt, "global_tau_2streams", 2)
+    timed(gt, "global_tau_3streams", 3)
     timed(psh, "per_shard")
     print(json.dumps(out), flush=True)
 
