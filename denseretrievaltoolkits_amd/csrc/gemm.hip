@@ -32,6 +32,7 @@ struct GemmArgs {
   int64_t lda, ldb, ldc, ldr;
   float alpha;
   unsigned long long* dbg;  // diagnostic builds only (segment stamps)
+  int order;                // tile order within an XCD's range (tile_order)
 };
 static unsigned long long* g_gemm_dbg = nullptr;
 
@@ -91,7 +92,8 @@ __device__ __forceinline__ float gelu_fast(float x) {
 
 enum { EPI_NONE = 0, EPI_BIAS = 1, EPI_GELU = 2, EPI_RESID = 4 };
 
-static int g_gemm_variant = 0;  // A/B switch: 0 auto (large full-K), 1 small 128^2, 2 large half-K ring
+static int g_gemm_variant = 0;
+static int g_gemm_order = -1;   // -1 auto: grouped-8 for K <= 1024 (small panels), row-major otherwise  // A/B switch: 0 auto (large full-K), 1 small 128^2, 2 large half-K ring
 
 template <bool OUT_BF16, int EPI>
 __global__ __launch_bounds__(kGemmThreads, 2) void gemm_nt_kernel(GemmArgs a) {
@@ -474,6 +476,37 @@ __device__ __forceinline__ void stage_panel32(const __bf16* base, int64_t ld, in
   }
 }
 
+// Tile order inside the contiguous range of tiles an XCD owns (wg = rank in the
+// XCD-remapped grid): 0 row-major (consecutive tiles share the X panel),
+// 1 grouped by 8 m-panels (a round of 32 concurrent tiles = 8 m x 4 n panels),
+// 2 column-major inside the XCD's m-range (a round shares one W panel),
+// 3 / 4 grouped by 4 / 16 m-panels.
+__device__ __forceinline__ void tile_order(int order, int wg, int nwg, int tiles_n, int& tm, int& tn) {
+  if (order == 0) {
+    tm = wg / tiles_n;
+    tn = wg % tiles_n;
+    return;
+  }
+  const int tiles_m = nwg / tiles_n;
+  if (order == 1 || order >= 3) {
+    const int G = order == 1 ? 8 : (order == 3 ? 4 : 16);
+    const int grp = wg / (G * tiles_n), first = grp * G;
+    const int gm = tiles_m - first < G ? tiles_m - first : G;
+    const int l = wg - grp * G * tiles_n;
+    tm = first + l % gm;
+    tn = l / gm;
+    return;
+  }
+  // order 2: the XCD's m-range is [x*mpx, ...); walk it column by column
+  const int mpx = (tiles_m + 7) / 8;
+  const int x = wg / (mpx * tiles_n);
+  const int first = x * mpx;
+  const int gm = tiles_m - first < mpx ? tiles_m - first : mpx;
+  const int l = wg - x * mpx * tiles_n;
+  tm = first + l % gm;
+  tn = l / gm;
+}
+
 // s_waitcnt vmcnt(4 * n): all but the n youngest slabs (4 LDS-DMA per wave each) landed.
 __device__ __forceinline__ void vmcnt_slabs_after(int n) {
   switch (n) {
@@ -655,8 +688,10 @@ __global__ __launch_bounds__(kLThreads, 1) void gemm_nt_pp1_kernel(GemmArgs a) {
   const int xcd = bid & 7, q8 = nwg >> 3, r8 = nwg & 7;
   const int wg = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (bid >> 3);
   const int tiles_n = (int)((a.n + kL - 1) / kL);
-  const int64_t m0 = (int64_t)(wg / tiles_n) * kL;
-  const int64_t n0 = (int64_t)(wg % tiles_n) * kL;
+  int tm, tn;
+  tile_order(a.order, wg, nwg, tiles_n, tm, tn);
+  const int64_t m0 = (int64_t)tm * kL;
+  const int64_t n0 = (int64_t)tn * kL;
 
   const uint32_t lds0 = g_lds_addr(smem);
   const int ns = (int)(a.k / 32);
@@ -760,7 +795,9 @@ __global__ __launch_bounds__(kLThreads, 1) void gemm_nt_pp1_kernel(GemmArgs a) {
 }
 
 template <bool OUT_BF16, int EPI>
-static int launch_gemm_t(const GemmArgs& a, hipStream_t s) {
+static int launch_gemm_t(const GemmArgs& a0, hipStream_t s) {
+  GemmArgs a = a0;
+  a.order = g_gemm_order >= 0 ? g_gemm_order : (a.k <= 1024 ? 1 : 0);
   const ProfPair pp = prof_begin(PROF_GEMM, s);
   // large tiles once there are >= 2 tiles per CU of them; small problems keep 128^2
   const int64_t tiles_l = ((a.m + kL - 1) / kL) * ((a.n + kL - 1) / kL);
@@ -876,5 +913,12 @@ extern "C" int drt_gemm_force_small(int32_t on) {
 // Diagnostic: device buffer for the variant-6 segment stamps (16 blocks x 8 waves x 4 slabs x 4 u64).
 extern "C" int drt_gemm_debug_buffer(void* buf) {
   g_gemm_dbg = (unsigned long long*)buf;
+  return DRT_OK;
+}
+
+// Benchmark switch: tile order of the ping-pong kernel (0 row-major, 1 grouped-8, 2 column-major per XCD).
+extern "C" int drt_gemm_tile_order(int32_t order) {
+  if (order < -1 || order > 4) return DRT_EINVAL;
+  g_gemm_order = order;
   return DRT_OK;
 }

@@ -159,6 +159,10 @@ int drt_l2_normalize_f32(float* x, int64_t B, int32_t H, void* out_bf16, void* s
 int drt_gemm_force_small(int32_t on);
 /* Diagnostic only: device buffer for the GEMM cycle-stamp variants (drt_gemm_force_small >= 16). */
 int drt_gemm_debug_buffer(void* buf);
+/* Benchmark switch: tile order of the 256x256 ping-pong GEMM inside each XCD's tile range
+ * (-1 automatic, 0 row-major, 1 grouped by 8 m-panels, 2 column-major,
+ * 3/4 grouped by 4/16).                                                     */
+int drt_gemm_tile_order(int32_t order);
 
 /* ------------------------------------------------------------------------
  * In-batch-negative training loss (DRModel.forward, biencoder.py:107-119;

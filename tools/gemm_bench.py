@@ -66,4 +66,8 @@ def run(M=65536, reps=20, variants=(0, 1, 2, 3)):
 
 if __name__ == "__main__":
     vs = tuple(int(v) for v in sys.argv[1].split(",")) if len(sys.argv) > 1 else (0, 1, 9)
-    run(variants=vs)
+    orders = tuple(int(v) for v in sys.argv[2].split(",")) if len(sys.argv) > 2 else (-1,)
+    for o in orders:
+        _native.load().drt_gemm_tile_order(o)
+        print("tile order", o)
+        run(variants=vs)
