@@ -53,6 +53,7 @@ _SIGNATURES = [
     ("drt_gemm_debug_buffer", c_i32, [c_vp]),
     ("drt_gemm_tile_order", c_i32, [c_i32]),
     ("drt_gemm_nt_f32", c_i32, [c_vp, c_vp, c_vp, c_i64, c_i64, c_i64, c_i64, c_i64, c_i64, c_vp]),
+    ("drt_gemm_f32", c_i32, [c_vp, c_vp, c_vp, c_i64, c_i64, c_i64, c_i64, c_i64, c_i64, c_i32, c_i32, c_i32, c_vp, c_vp]),
     ("drt_ce_fwd", c_i32, [c_vp, c_i64, c_i64, c_i64, c_f32, c_vp, c_vp, c_vp, c_vp]),
     ("drt_ce_bwd", c_i32, [c_vp, c_vp, c_i64, c_i64, c_i64, c_vp, c_f32, c_vp, c_vp]),
     ("drt_transpose_f32", c_i32, [c_vp, c_i64, c_i64, c_vp, c_vp]),

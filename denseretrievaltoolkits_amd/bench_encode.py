@@ -112,3 +112,43 @@ def run_rerank(device, pairs=1000, q_len=32, p_len=128, steps=3, warmup=1):
         "roofline": {"bound": "mfma", "achieved": round(fl * qps / 1e12, 1), "peak": 2500.0, "unit": "TFLOP/s",
                      "frac": round(fl * qps / 1e12 / 2500.0, 4), "flop_per_pair": flops_per_seq(L)},
     }
+
+
+def run_train_scores(device, bq=512, d=768, n_passages=(2, 8), steps=20, warmup=3):
+    """Config C3 (BASELINE.json configs[2]): the in-batch-negative score matrix of
+    DRModel.forward (DRT/model/biencoder.py:107-119) at batch 512: scores = q . p^T
+    [512, 512 n], CrossEntropy(mean) with target i * n, and its backward (dq, dp),
+    fp32 end to end on the HIP op (score_ce.ScoreCE), next to torch's fp32
+    matmul + cross_entropy + autograd on the same device."""
+    from .score_ce import score_ce
+    g = torch.Generator(device=device)
+    g.manual_seed(3)
+    res = {"metric": "in-batch-negative score+CE forward+backward, ms per step (fp32)", "batch": bq, "dim": d}
+    for n in n_passages:
+        q = torch.randn((bq, d), generator=g, device=device).requires_grad_(True)
+        p = torch.randn((bq * n, d), generator=g, device=device).requires_grad_(True)
+        tgt = torch.arange(bq, device=device) * n
+
+        def ours():
+            loss, _ = score_ce(q, p, n, 1.0)
+            loss.backward()
+
+        def ref():
+            s = q @ p.T
+            torch.nn.functional.cross_entropy(s, tgt).backward()
+
+        out = {}
+        for name, fn in (("hip", ours), ("torch", ref)):
+            for _ in range(warmup):
+                fn()
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            for _ in range(steps):
+                fn()
+            torch.cuda.synchronize()
+            out[name + "_ms"] = round((time.perf_counter() - t0) / steps * 1e3, 4)
+        fl = 6 * bq * bq * n * d
+        out["flop"] = fl
+        out["hip_tflops"] = round(fl / (out["hip_ms"] * 1e-3) / 1e12, 2)
+        res[f"n{n}"] = out
+    return res

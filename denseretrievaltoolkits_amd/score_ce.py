@@ -36,6 +36,22 @@ def transpose_f32(x: torch.Tensor) -> torch.Tensor:
     return y
 
 
+def gemm_f32(a: torch.Tensor, b: torch.Tensor, a_kc: bool, b_kc: bool, m: int, n: int, k: int) -> torch.Tensor:
+    """C[m, n] = sum_k A(m, k) B(k, n) on the exact-f32 MFMA; A is a [m][k] (a_kc) or [k][m]
+    row-major tensor, B is [n][k] (b_kc) or [k][n].  Split-K (deterministic) when the
+    64 x 64 output tiles alone cannot fill the chip."""
+    lib = _native.load()
+    out = torch.empty((m, n), dtype=torch.float32, device=a.device)
+    tiles = -(-m // 64) * -(-n // 64)
+    splits = max(1, min(-(-320 // tiles), k // 128))
+    ws = torch.empty((splits, m, n), dtype=torch.float32, device=a.device) if splits > 1 else None
+    _native.check(lib.drt_gemm_f32(a.data_ptr(), b.data_ptr(), out.data_ptr(), m, n, k, a.stride(0), b.stride(0),
+                                   out.stride(0), int(a_kc), int(b_kc), splits,
+                                   ws.data_ptr() if ws is not None else None, _native.stream_ptr(a.device)),
+                  "drt_gemm_f32")
+    return out
+
+
 class ScoreCE(torch.autograd.Function):
     @staticmethod
     def forward(ctx, q, p, target_stride: int, scale: float):
@@ -43,7 +59,7 @@ class ScoreCE(torch.autograd.Function):
             raise ValueError("ScoreCE runs on the GPU only (no CPU fallback)")
         lib = _native.load()
         qf, pf = _f32(q), _f32(p)
-        S = gemm_nt_f32(qf, pf)
+        S = gemm_f32(qf, pf, True, True, qf.shape[0], pf.shape[0], qf.shape[1])
         m, n = S.shape
         lse = torch.empty(m, dtype=torch.float32, device=S.device)
         rl = torch.empty(m, dtype=torch.float32, device=S.device)
@@ -66,8 +82,9 @@ class ScoreCE(torch.autograd.Function):
         dS = torch.empty_like(S)
         _native.check(lib.drt_ce_bwd(S.data_ptr(), lse.data_ptr(), m, n, ctx.target_stride, g.data_ptr(),
                                      ctx.scale, dS.data_ptr(), _native.stream_ptr(S.device)), "drt_ce_bwd")
-        dq = gemm_nt_f32(dS, transpose_f32(pf))            # [m, d] = dS [m,n] . p [n,d]
-        dp = gemm_nt_f32(transpose_f32(dS), transpose_f32(qf))  # [n, d] = dS^T [n,m] . q [m,d]
+        d = qf.shape[1]
+        dq = gemm_f32(dS, pf, True, False, m, d, n)     # [m, d] = dS [m, n] . p [n, d]
+        dp = gemm_f32(dS, qf, False, False, n, d, m)    # [n, d] = dS^T [n, m] . q [m, d]
         return dq.to(ctx.in_dtypes[0]), dp.to(ctx.in_dtypes[1]), None, None
 
 

@@ -177,6 +177,13 @@ int drt_gemm_tile_order(int32_t order);
  * drt_transpose_f32: Y[cols, rows] = X[rows, cols]^T.                       */
 int drt_gemm_nt_f32(const float* A, const float* B, float* C, int64_t m, int64_t n, int64_t k,
                     int64_t lda, int64_t ldb, int64_t ldc, void* stream);
+/* drt_gemm_f32: C[m,n] = sum_k A(m,k) B(k,n), exact-f32 MFMA, for the score matrix and its
+ * backward without transposes (replaces torch.matmul in DRModel.forward, biencoder.py:107, and
+ * the autograd of it).  a_kc: A stored [m][lda>=k] (else [k][lda>=m]); b_kc: B stored
+ * [n][ldb>=k] (else [k][ldb>=n]).  splits > 1: deterministic split-K through ws
+ * (splits * m * n floats, partial sums added in a fixed order).                        */
+int drt_gemm_f32(const float* A, const float* B, float* C, int64_t m, int64_t n, int64_t k, int64_t lda,
+                 int64_t ldb, int64_t ldc, int32_t a_kc, int32_t b_kc, int32_t splits, float* ws, void* stream);
 int drt_ce_fwd(const float* S, int64_t m, int64_t n, int64_t target_stride, float scale,
                float* lse, float* row_loss, float* loss, void* stream);
 int drt_ce_bwd(const float* S, const float* lse, int64_t m, int64_t n, int64_t target_stride,

@@ -116,3 +116,18 @@ def test_hip_rerank_matches_reference_scores(dev):
         err = np.abs(got - ref).max() / (np.abs(ref).max() + 1e-6)
         print(f"rerank {pooling}: max rel err {err:.4f}")
         assert err < 0.02
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("m,n,k", [(512, 1024, 768), (7, 13, 5), (130, 70, 333), (512, 768, 4096)])
+@pytest.mark.parametrize("a_kc,b_kc", [(True, True), (True, False), (False, True), (False, False)])
+def test_gemm_f32_layouts_vs_fp64(dev, m, n, k, a_kc, b_kc):
+    """drt_gemm_f32 (exact-f32 MFMA, all operand layouts, ragged shapes, split-K) vs fp64."""
+    import torch
+    from denseretrievaltoolkits_amd.score_ce import gemm_f32
+    g = torch.Generator(device=dev).manual_seed(m * 7 + n)
+    A = torch.randn((m, k) if a_kc else (k, m), generator=g, device=dev)
+    B = torch.randn((n, k) if b_kc else (k, n), generator=g, device=dev)
+    ref = (A.double() if a_kc else A.double().T) @ (B.double().T if b_kc else B.double())
+    out = gemm_f32(A, B, a_kc, b_kc, m, n, k)
+    torch.testing.assert_close(out.double(), ref, atol=1e-3 * max(1.0, k ** 0.5 / 8), rtol=1e-5)
