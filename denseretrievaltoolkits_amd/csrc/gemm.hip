@@ -507,6 +507,28 @@ __device__ __forceinline__ void tile_order(int order, int wg, int nwg, int tiles
   tn = l / gm;
 }
 
+// s_waitcnt vmcnt(4 * n + extra), extra in {0, 16}: the n youngest slabs plus `extra`
+// younger non-DMA loads may stay in flight.
+__device__ __forceinline__ void vmcnt_slabs_after_plus(int n, int extra) {
+  if (extra == 0) {
+    switch (n) {
+      case 0: asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); break;
+      case 1: asm volatile("s_waitcnt vmcnt(4)" ::: "memory"); break;
+      case 2: asm volatile("s_waitcnt vmcnt(8)" ::: "memory"); break;
+      case 3: asm volatile("s_waitcnt vmcnt(12)" ::: "memory"); break;
+      default: asm volatile("s_waitcnt vmcnt(16)" ::: "memory"); break;
+    }
+    return;
+  }
+  switch (n) {
+    case 0: asm volatile("s_waitcnt vmcnt(16)" ::: "memory"); break;
+    case 1: asm volatile("s_waitcnt vmcnt(20)" ::: "memory"); break;
+    case 2: asm volatile("s_waitcnt vmcnt(24)" ::: "memory"); break;
+    case 3: asm volatile("s_waitcnt vmcnt(28)" ::: "memory"); break;
+    default: asm volatile("s_waitcnt vmcnt(32)" ::: "memory"); break;
+  }
+}
+
 // s_waitcnt vmcnt(4 * n): all but the n youngest slabs (4 LDS-DMA per wave each) landed.
 __device__ __forceinline__ void vmcnt_slabs_after(int n) {
   switch (n) {
@@ -577,9 +599,24 @@ __device__ __forceinline__ void pp_epilogue(const GemmArgs& a, f32x4 (&acc)[8][4
 // slice in a private LDS region (row-per-lane 8-B pieces in, 16-B row-contiguous
 // pieces out, 16-B chunks XOR-swizzled by row), then writes whole 128-B (bf16) /
 // 256-B (fp32) row segments.  Needs a full tile in n; rows are masked.
-template <bool OUT_BF16, int EPI>
+// Residual rows of one 64-row half of a wave's slice, in the read-back lane map of the
+// fp32 LDS epilogue (row p * 4 + lane / 16, 4 columns at (lane & 15) * 4).
+__device__ __forceinline__ void load_resid_half(const GemmArgs& a, int64_t m0, int64_t n0, int grp, int wn, int h,
+                                                int lane, bf16x4 (&rv)[16]) {
+  const int64_t colw = n0 + wn * 64;
+  const int c = lane & 15;
+#pragma unroll
+  for (int p = 0; p < 16; ++p) {
+    int64_t row = m0 + grp * 128 + h * 64 + p * 4 + (lane >> 4);
+    row = row < a.m ? row : a.m - 1;
+    rv[p] = *(const bf16x4*)(a.R + row * a.ldr + colw + c * 4);
+  }
+}
+
+template <bool OUT_BF16, int EPI, bool PRE = false>
 __device__ __forceinline__ void pp_epilogue_lds(const GemmArgs& a, f32x4 (&acc)[8][4], int64_t m0, int64_t n0,
-                                                int grp, int wn, int fr, int fc, char* lds_wave, int lane) {
+                                                int grp, int wn, int fr, int fc, char* lds_wave, int lane,
+                                                bf16x4 (&rv0)[16]) {
   const int64_t colw = n0 + wn * 64;   // first column of this wave's slice
   f32x4 bv[4];
 #pragma unroll
@@ -615,19 +652,17 @@ __device__ __forceinline__ void pp_epilogue_lds(const GemmArgs& a, f32x4 (&acc)[
       if (row < a.m) *(bf16x8*)((__bf16*)a.C + row * a.ldc + colw + c * 8) = v;
     }
   } else {
-    // two passes of 64 rows: [64 rows][16 x 16 B] fp32, chunk ^= row & 7
+    // two passes of 64 rows: [64 rows][16 x 16 B] fp32, chunk ^= row & 7.  Residual rows
+    // of both passes are requested before any staging (pass 0's possibly in the K loop).
     const int c = lane & 15;
+    bf16x4 rv1[16];
+    if (EPI & EPI_RESID) {
+      if (!PRE) load_resid_half(a, m0, n0, grp, wn, 0, lane, rv0);
+      load_resid_half(a, m0, n0, grp, wn, 1, lane, rv1);
+    }
 #pragma unroll
     for (int h = 0; h < 2; ++h) {
-      bf16x4 rv[16];
-      if (EPI & EPI_RESID) {
-#pragma unroll
-        for (int p = 0; p < 16; ++p) {
-          int64_t row = m0 + grp * 128 + h * 64 + p * 4 + (lane >> 4);
-          row = row < a.m ? row : a.m - 1;
-          rv[p] = *(const bf16x4*)(a.R + row * a.ldr + colw + c * 4);
-        }
-      }
+      const bf16x4 (&rv)[16] = h == 0 ? rv0 : rv1;
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
         const int r = i * 16 + fr;
@@ -695,6 +730,8 @@ __global__ __launch_bounds__(kLThreads, 1) void gemm_nt_pp1_kernel(GemmArgs a) {
 
   const uint32_t lds0 = g_lds_addr(smem);
   const int ns = (int)(a.k / 32);
+  // ABL & 64 (diagnostic): every tile streams the panels of tile (0, 0) -> all L2 hits
+  const int64_t dm0 = (ABL & 64) ? 0 : m0, dn0 = (ABL & 64) ? 0 : n0;
   unsigned long long st0 = 0, st1 = 0, st2 = 0;
   if (ABL & 32) st0 = __builtin_amdgcn_s_memtime();
 
@@ -713,8 +750,8 @@ __global__ __launch_bounds__(kLThreads, 1) void gemm_nt_pp1_kernel(GemmArgs a) {
 #pragma unroll
   for (int p = 0; p < D; ++p) {
     if (p < ns) {
-      stage_panel32(a.A, a.lda, m0, a.m, p * 32, lds0 + p * kPSlab, wave, lane);
-      stage_panel32(a.B, a.ldb, n0, a.n, p * 32, lds0 + p * kPSlab + kPPanel, wave, lane);
+      stage_panel32(a.A, a.lda, dm0, a.m, p * 32, lds0 + p * kPSlab, wave, lane);
+      stage_panel32(a.B, a.ldb, dn0, a.n, p * 32, lds0 + p * kPSlab + kPPanel, wave, lane);
     }
   }
   vmcnt_slabs_after(ns - 1 < D - 1 ? ns - 1 : D - 1);
@@ -725,6 +762,13 @@ __global__ __launch_bounds__(kLThreads, 1) void gemm_nt_pp1_kernel(GemmArgs a) {
   if (ABL & 32) st1 = __builtin_amdgcn_s_memtime();
   unsigned long long t_start = 0;
   if (ABL & 16) t_start = __builtin_amdgcn_s_memtime();
+  // fp32 + residual epilogue: the residual rows of pass 0 are requested right after the
+  // tile's last LDS-DMA, so their latency hides behind the last D slabs of the K loop
+  // (measured: prefetching here costs 32 VGPRs in the loop -> spills; kept off)
+  constexpr bool PRE = false;
+  constexpr int RP = PRE ? 16 : 0;   // vector-memory ops of that prefetch (younger than every DMA)
+  const bool pre_on = PRE && ns > D;
+  bf16x4 rv0[16];
   int slot = 0, fill = D % RING;
   for (int s = 0; s < ns; ++s) {
     const char* slab = smem + slot * kPSlab;
@@ -743,9 +787,16 @@ __global__ __launch_bounds__(kLThreads, 1) void gemm_nt_pp1_kernel(GemmArgs a) {
     const int left = (ABL & 1) ? 0 : ns - 1 - s;   // slabs after s
     if (left >= D) {
       const uint32_t nslab = lds0 + fill * kPSlab;
-      stage_panel32(a.A, a.lda, m0, a.m, (int64_t)(s + D) * 32, nslab, wave, lane);
-      stage_panel32(a.B, a.ldb, n0, a.n, (int64_t)(s + D) * 32, nslab + kPPanel, wave, lane);
-      vmcnt_slabs_after(D - 1);
+      stage_panel32(a.A, a.lda, dm0, a.m, (int64_t)(s + D) * 32, nslab, wave, lane);
+      stage_panel32(a.B, a.ldb, dn0, a.n, (int64_t)(s + D) * 32, nslab + kPPanel, wave, lane);
+      if (PRE && left == D && pre_on) {
+        load_resid_half(a, m0, n0, grp, wn, 0, lane, rv0);
+        vmcnt_slabs_after_plus(D - 1, RP);
+      } else {
+        vmcnt_slabs_after(D - 1);
+      }
+    } else if (PRE && pre_on) {
+      vmcnt_slabs_after_plus(left > 0 ? left - 1 : 0, RP);
     } else {
       vmcnt_slabs_after(left > 0 ? left - 1 : 0);
     }
@@ -778,7 +829,10 @@ __global__ __launch_bounds__(kLThreads, 1) void gemm_nt_pp1_kernel(GemmArgs a) {
   if (grp == 0 && !(ABL & 4)) __builtin_amdgcn_s_barrier();
   if (ABL & 32) st2 = __builtin_amdgcn_s_memtime();
   const bool full = (n0 + kL <= a.n) && (a.ldc % 8 == 0) && (!(EPI & EPI_RESID) || a.ldr % 4 == 0);
-  if (full) pp_epilogue_lds<OUT_BF16, EPI>(a, acc, m0, n0, grp, wn, fr, fc, smem + wave * 16384, lane);
+  if (full) {
+    if (pre_on) pp_epilogue_lds<OUT_BF16, EPI, true>(a, acc, m0, n0, grp, wn, fr, fc, smem + wave * 16384, lane, rv0);
+    else pp_epilogue_lds<OUT_BF16, EPI, false>(a, acc, m0, n0, grp, wn, fr, fc, smem + wave * 16384, lane, rv0);
+  }
   else pp_epilogue<OUT_BF16, EPI>(a, acc, m0, n0, grp, wn, fr, fc);
   if (ABL & 32) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -816,6 +870,8 @@ static int launch_gemm_t(const GemmArgs& a0, hipStream_t s) {
       case 1: hipLaunchKernelGGL((gemm_nt_pp1_kernel<OUT_BF16, EPI, 17>), G, T, 0, s, b); break;
       case 13: hipLaunchKernelGGL((gemm_nt_pp1_kernel<OUT_BF16, EPI, 29>), G, T, 0, s, b); break;
       case 15: hipLaunchKernelGGL((gemm_nt_pp1_kernel<OUT_BF16, EPI, 32>), G, T, 0, s, b); break;
+      case 7: hipLaunchKernelGGL((gemm_nt_pp1_kernel<OUT_BF16, EPI, 16, 5>), G, T, 0, s, b); break;
+      case 10: hipLaunchKernelGGL((gemm_nt_pp1_kernel<OUT_BF16, EPI, 16 | 2 | 8, 5>), G, T, 0, s, b); break;
       default: return DRT_EINVAL;
     }
   } else if (tiles_l >= 512 && g_gemm_variant == 7) {

@@ -1,5 +1,6 @@
 """Loop-only cycle stamps of the pp1 GEMM under ablations (diagnostic variants 16+bits:
-1 no LDS-DMA in the loop, 13 = no DMA, no barriers, no fragment reads: the bare MFMA loop).  Prints
+1 no LDS-DMA in the loop, 13 = no DMA, no barriers, no fragment reads: the bare MFMA loop,
+7 the 5-slot ring with stamps, 10 = LDS-DMA only (no MFMA, no fragment reads)).  Prints
 median cycles per slab (first tile of blocks 0-63) and the kernel's TFLOP/s."""
 import os
 import sys
@@ -22,7 +23,7 @@ out = torch.empty(M, N, dtype=torch.float32 if flags & 2 else torch.bfloat16, de
 dbg = torch.zeros(64 * 8 * 2, dtype=torch.int64, device=dev)
 lib.drt_gemm_debug_buffer(dbg.data_ptr())
 s = _native.stream_ptr(dev)
-names = {0: "base", 1: "nodma", 13: "nods+nobar+nodma"}
+names = {0: "base", 1: "nodma", 13: "nods+nobar+nodma", 7: "ring5", 10: "ring5 dma-only"}
 for abl, nm in names.items():
     lib.drt_gemm_force_small(16 + abl)
     call = lambda: _native.check(lib.drt_linear_bf16(x.data_ptr(), w.data_ptr(), b.data_ptr(),
