@@ -95,6 +95,25 @@ __global__ __launch_bounds__(256) void layernorm_f32_kernel(const float* X, int6
   ln_row<EPL>(x, gamma, beta, eps, lane, H, out + t * H);
 }
 
+// Same LayerNorm over bf16 pre-LN sums (the encoder's default: the GEMM epilogue
+// adds bias + residual in fp32 and rounds once, halving the bytes of both sides).
+template <int EPL>
+__global__ __launch_bounds__(256) void layernorm_bf16_kernel(const __bf16* X, int64_t M, int H, const float* gamma,
+                                                             const float* beta, float eps, __bf16* out) {
+  const int lane = threadIdx.x & 63;
+  const int64_t t = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (t >= M) return;
+  const __bf16* xr = X + t * H;
+  float x[EPL];
+#pragma unroll
+  for (int e4 = 0; e4 < EPL / 4; ++e4) {
+    const bf16x4 a = *(const bf16x4*)(xr + e4 * 256 + lane * 4);
+#pragma unroll
+    for (int u = 0; u < 4; ++u) x[e4 * 4 + u] = (float)a[u];
+  }
+  ln_row<EPL>(x, gamma, beta, eps, lane, H, out + t * H);
+}
+
 // ---------------------------------------------------------------------------
 // Attention.  One work-group (4 waves) per (sequence b, head hd); wave w owns
 // query blocks w, w+4, ... of 32 rows.  K is staged in LDS as swizzled
@@ -337,6 +356,25 @@ int drt_layernorm_f32_bf16(const float* X, int64_t M, int32_t H, const float* ga
     case 8: hipLaunchKernelGGL(layernorm_f32_kernel<8>, grid, dim3(256), 0, s, X, M, H, gamma, beta, eps, (__bf16*)out); break;
     case 12: hipLaunchKernelGGL(layernorm_f32_kernel<12>, grid, dim3(256), 0, s, X, M, H, gamma, beta, eps, (__bf16*)out); break;
     case 16: hipLaunchKernelGGL(layernorm_f32_kernel<16>, grid, dim3(256), 0, s, X, M, H, gamma, beta, eps, (__bf16*)out); break;
+    default: return DRT_EINVAL;
+  }
+  return hip_status(hipGetLastError());
+}
+
+int drt_layernorm_bf16(const void* X, int64_t M, int32_t H, const float* gamma, const float* beta, float eps,
+                       void* out, void* stream) {
+  DRT_REQUIRE(M >= 0 && H > 0 && H % 256 == 0 && H <= 1024);
+  if (M == 0) return DRT_OK;
+  DRT_REQUIRE(X && gamma && beta && out);
+  hipStream_t s = (hipStream_t)stream;
+  const __bf16* x = (const __bf16*)X;
+  __bf16* o = (__bf16*)out;
+  dim3 grid((unsigned)((M + 3) / 4));
+  switch (H / 64) {
+    case 4: hipLaunchKernelGGL(layernorm_bf16_kernel<4>, grid, dim3(256), 0, s, x, M, H, gamma, beta, eps, o); break;
+    case 8: hipLaunchKernelGGL(layernorm_bf16_kernel<8>, grid, dim3(256), 0, s, x, M, H, gamma, beta, eps, o); break;
+    case 12: hipLaunchKernelGGL(layernorm_bf16_kernel<12>, grid, dim3(256), 0, s, x, M, H, gamma, beta, eps, o); break;
+    case 16: hipLaunchKernelGGL(layernorm_bf16_kernel<16>, grid, dim3(256), 0, s, x, M, H, gamma, beta, eps, o); break;
     default: return DRT_EINVAL;
   }
   return hip_status(hipGetLastError());

@@ -624,7 +624,7 @@ __device__ __forceinline__ void pp_epilogue_lds(const GemmArgs& a, f32x4 (&acc)[
     bv[j] = f32x4{0.f, 0.f, 0.f, 0.f};
     if (EPI & EPI_BIAS) bv[j] = *(const f32x4*)(a.bias + colw + j * 16 + 4 * fc);
   }
-  if (OUT_BF16) {
+  if (OUT_BF16 && !(EPI & EPI_RESID)) {
     // [128 rows][8 x 16 B], chunk ^= row & 7
 #pragma unroll
     for (int i = 0; i < 8; ++i) {
@@ -654,6 +654,8 @@ __device__ __forceinline__ void pp_epilogue_lds(const GemmArgs& a, f32x4 (&acc)[
   } else {
     // two passes of 64 rows: [64 rows][16 x 16 B] fp32, chunk ^= row & 7.  Residual rows
     // of both passes are requested before any staging (pass 0's possibly in the K loop).
+    // bf16 output with a residual (pre-LayerNorm sums) also stages fp32, so the sum is
+    // rounded once, at the store (8-B pieces, 128-B row segments).
     const int c = lane & 15;
     bf16x4 rv1[16];
     if (EPI & EPI_RESID) {
@@ -690,7 +692,14 @@ __device__ __forceinline__ void pp_epilogue_lds(const GemmArgs& a, f32x4 (&acc)[
 #pragma unroll
             for (int u = 0; u < 4; ++u) v[u] += (float)rv[p][u];
           }
-          *(f32x4*)((float*)a.C + row * a.ldc + colw + c * 4) = v;
+          if (OUT_BF16) {
+            bf16x4 o;
+#pragma unroll
+            for (int u = 0; u < 4; ++u) o[u] = (__bf16)v[u];
+            *(bf16x4*)((__bf16*)a.C + row * a.ldc + colw + c * 4) = o;
+          } else {
+            *(f32x4*)((float*)a.C + row * a.ldc + colw + c * 4) = v;
+          }
         }
       }
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");

@@ -133,6 +133,8 @@ int drt_gemm_nt_bf16_f32(const void* A, const void* B, float* C, int64_t m, int6
  *   bias fp32 [N] or NULL, residual bf16 [M,N] or NULL; flags bit0 = GELU(erf),
  *   bit1 = fp32 output (else bf16).  K % 64 == 0.
  * drt_layernorm_f32_bf16: out bf16 = LN(X fp32 [M,H]).
+ * drt_layernorm_bf16: out bf16 = LN(X bf16 [M,H]) (fp32 statistics); the
+ *   encoder's default, fed by a bf16 +bias +residual epilogue (one rounding).
  * drt_attention_bf16: ctx[B*L, heads*64] = softmax(Q K^T * scale + mask) V per
  *   head, from packed qkv [B*L, 3*heads*64]; mask int64 [B,L] (1 token, 0 pad)
  *   or NULL; L <= 512, head_dim == 64.
@@ -147,6 +149,8 @@ int drt_linear_bf16(const void* X, const void* W, const float* bias, const void*
                     void* Y, int64_t M, int64_t N, int64_t K, int32_t flags, void* stream);
 int drt_layernorm_f32_bf16(const float* X, int64_t M, int32_t H, const float* gamma,
                            const float* beta, float eps, void* out, void* stream);
+int drt_layernorm_bf16(const void* X, int64_t M, int32_t H, const float* gamma,
+                       const float* beta, float eps, void* out, void* stream);
 int drt_attention_bf16(const void* qkv, const int64_t* mask, void* ctx, int64_t B, int64_t L,
                        int32_t heads, int32_t head_dim, float scale, void* stream);
 int drt_pool_bf16(const void* hidden, const int64_t* mask, int64_t B, int64_t L, int32_t H,

@@ -31,20 +31,22 @@ def _cos(a, b):
     return (a * b).sum(1) / (np.linalg.norm(a, axis=1) * np.linalg.norm(b, axis=1) + 1e-30)
 
 
-@pytest.mark.parametrize("layers,B,L", [(2, 8, 128), (12, 4, 128), (2, 5, 32), (2, 3, 160), (1, 2, 512), (2, 3, 50)])
-def test_hidden_states_vs_hf_fp32(dev, layers, B, L):
+@pytest.mark.parametrize("layers,B,L,presum", [(2, 8, 128, "bf16"), (12, 4, 128, "bf16"), (12, 4, 128, "fp32"),
+                                                (2, 5, 32, "bf16"), (2, 3, 160, "bf16"), (1, 2, 512, "bf16"),
+                                                (2, 3, 50, "fp32")])
+def test_hidden_states_vs_hf_fp32(dev, layers, B, L, presum):
     import torch
     from denseretrievaltoolkits_amd.model.encoder import HipBertEncoder
     m = _models(layers)
     ids, mask = bw.token_batch(B, L, seed=L + B)
     with torch.no_grad():
         ref = m(input_ids=torch.from_numpy(ids), attention_mask=torch.from_numpy(mask)).last_hidden_state.numpy()
-    enc = HipBertEncoder.from_hf(m, dev)
+    enc = HipBertEncoder.from_hf(m, dev, presum=presum)
     out = enc(torch.from_numpy(ids).to(dev), torch.from_numpy(mask).to(dev)).float().cpu().numpy()
     valid = mask.astype(bool)
     cos = _cos(out[valid], ref[valid])
     err = np.abs(out[valid] - ref[valid]).max()
-    print(f"layers={layers} B={B} L={L}: min cos {cos.min():.6f}, max abs err {err:.4f}")
+    print(f"layers={layers} B={B} L={L} presum={presum}: min cos {cos.min():.6f}, max abs err {err:.4f}")
     assert cos.min() >= COS_MIN
     assert np.isfinite(out).all()
 
@@ -93,7 +95,7 @@ def test_linear_epilogues_vs_torch(dev):
 
 
 @pytest.mark.parametrize("M,N,K,flags", [(16384, 2304, 768, 0), (32768, 768, 3072, 2), (20000, 3072, 768, 1),
-                                          (131072, 768, 768, 2)])
+                                          (131072, 768, 768, 2), (65536, 768, 768, 4), (30000, 768, 3072, 4)])
 def test_large_tile_gemm_vs_torch_and_small_kernel(dev, M, N, K, flags):
     """256x256-tile kernels (>= 512 tiles) against torch fp32 and the 128x128 kernel.
     Variants: 0 auto (ping-pong, 5-slot ring), 1 128x128, 2 half-K ring,
@@ -105,7 +107,8 @@ def test_large_tile_gemm_vs_torch_and_small_kernel(dev, M, N, K, flags):
     x = torch.randn(M, K, generator=g, device=dev).to(torch.bfloat16)
     w = (0.05 * torch.randn(N, K, generator=g, device=dev)).to(torch.bfloat16)
     b = torch.randn(N, generator=g, device=dev)
-    r = torch.randn(M, N, generator=g, device=dev).to(torch.bfloat16) if flags == 2 else None
+    # flags 4 (test-local): bf16 output + residual, the encoder's pre-LayerNorm sums
+    r = torch.randn(M, N, generator=g, device=dev).to(torch.bfloat16) if flags in (2, 4) else None
     ref = x.float() @ w.float().T + b
     if flags == 1:
         ref = torch.nn.functional.gelu(ref)
@@ -118,7 +121,8 @@ def test_large_tile_gemm_vs_torch_and_small_kernel(dev, M, N, K, flags):
         lib.drt_gemm_force_small(force)
         out = torch.empty(M, N, dtype=dt, device=dev)
         _native.check(lib.drt_linear_bf16(x.data_ptr(), w.data_ptr(), b.data_ptr(),
-                                          r.data_ptr() if r is not None else None, out.data_ptr(), M, N, K, flags,
+                                          r.data_ptr() if r is not None else None, out.data_ptr(), M, N, K,
+                                          flags & 3,
                                           _native.stream_ptr(dev)), "linear")
         outs.append(out.float())
     lib.drt_gemm_force_small(0)
@@ -130,3 +134,21 @@ def test_large_tile_gemm_vs_torch_and_small_kernel(dev, M, N, K, flags):
         by = dict(zip(variants, outs))
         assert torch.equal(by[1], by[2]) and torch.equal(by[1], by[9])
         assert torch.equal(by[0], by[7]) and torch.equal(by[0], by[8])
+
+
+@pytest.mark.parametrize("M,H", [(1, 768), (1003, 768), (64, 256), (37, 1024)])
+def test_layernorm_bf16_and_f32_inputs_vs_torch(dev, M, H):
+    """drt_layernorm_bf16 (the encoder's default pre-LN sums) and drt_layernorm_f32_bf16 vs torch fp32 LN."""
+    import torch
+    from denseretrievaltoolkits_amd import _native
+    lib = _native.load()
+    g = torch.Generator(device=dev).manual_seed(M * 7 + H)
+    x = (3.0 * torch.randn(M, H, generator=g, device=dev) + 0.5)
+    gam = torch.randn(H, generator=g, device=dev)
+    bet = torch.randn(H, generator=g, device=dev)
+    s = _native.stream_ptr(dev)
+    for fn, xin in ((lib.drt_layernorm_bf16, x.to(torch.bfloat16)), (lib.drt_layernorm_f32_bf16, x)):
+        out = torch.empty(M, H, dtype=torch.bfloat16, device=dev)
+        _native.check(fn(xin.data_ptr(), M, H, gam.data_ptr(), bet.data_ptr(), 1e-12, out.data_ptr(), s), "ln")
+        ref = torch.nn.functional.layer_norm(xin.float(), (H,), gam, bet, 1e-12)
+        torch.testing.assert_close(out.float(), ref, atol=3e-2, rtol=1e-2)
