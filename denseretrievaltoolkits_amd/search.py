@@ -22,7 +22,7 @@ from typing import Optional, Tuple
 import numpy as np
 import torch
 
-from . import kernels
+from . import kernels, shards
 
 
 def _as_device_bf16(x, device) -> torch.Tensor:
@@ -101,16 +101,24 @@ class FlatIPIndex:
     def dist_filter(self, q, n_global: int, k: int, id_offset: int, tau: torch.Tensor) -> torch.Tensor:
         return kernels.dist_filter(self._queries(q), self.rows, n_global, k, id_offset, tau)
 
-    # persistence (replaces faiss.write_index / read_index, trainer.py:245,257)
+    # persistence (replaces faiss.write_index / read_index, trainer.py:245,257): a
+    # memory-mapped bf16 shard file streamed chunk by chunk (shards.py)
     def save(self, path: str) -> None:
-        rows = self.rows.view(torch.int16).cpu().numpy()
-        np.save(path, rows, allow_pickle=False)
+        shards.save_rows(self.rows, path)
 
     @classmethod
     def load(cls, path: str, device=None) -> "FlatIPIndex":
-        rows = np.load(path, allow_pickle=False)
-        idx = cls(rows.shape[1], device=device, capacity=rows.shape[0])
-        idx.add(torch.from_numpy(rows).view(torch.bfloat16))
+        return cls.load_rows([path], None, None, device=device)
+
+    @classmethod
+    def load_rows(cls, paths, start=None, stop=None, device=None) -> "FlatIPIndex":
+        """Rows [start, stop) of the concatenated shard files (default: all) on one device."""
+        sizes, d = shards.shard_sizes(paths)
+        start = 0 if start is None else int(start)
+        stop = sum(sizes) if stop is None else int(stop)
+        idx = cls(d, device=device, capacity=0)
+        idx._buf = shards.load_rows(paths, start, stop, idx.device)
+        idx.ntotal = stop - start
         return idx
 
 
@@ -208,3 +216,28 @@ class ShardedFlatIP:
     def search(self, q, k: int) -> Tuple[np.ndarray, np.ndarray]:
         s, i = self.search_device(q, k)
         return s.cpu().numpy(), i.cpu().numpy()
+
+    # persistence: every rank writes its own shard file; any world size reads them back
+    def save_shard(self, directory: str, ep) -> str:
+        """Write THIS rank's rows to ``{ep}.{rank}.bf16.npy`` (replaces trainer.py:210-216)."""
+        import os
+        os.makedirs(directory, exist_ok=True)
+        path = shards.shard_path(directory, ep, self.rank)
+        self.local.save(path)
+        return path
+
+    @classmethod
+    def load_shards(cls, directory: str, ep, group=None, device=None, **kw) -> "ShardedFlatIP":
+        """Each rank maps the shard files of ``ep`` (in rank order) and streams its contiguous
+        global row range into HBM; the files may come from a different world size.
+        Replaces the rank-0 index build + every-rank index read (trainer.py:220-262)."""
+        paths = shards.list_shards(directory, ep)
+        sizes, d = shards.shard_sizes(paths)
+        self = cls(d, group=group, device=device, **kw)
+        a, b = shards.split_rows(sum(sizes), self.world, self.rank)
+        if kw.get("local") is None:
+            self.local = FlatIPIndex.load_rows(paths, a, b, device=self.local.device)
+        else:
+            self.local.add(shards.load_rows(paths, a, b, torch.device("cpu")).float())
+        self.sync_offsets()
+        return self

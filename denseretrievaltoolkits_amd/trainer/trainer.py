@@ -33,7 +33,7 @@ from torch import optim
 from torch.nn.parallel import DistributedDataParallel as DDP
 
 from ..evaluator.metrics import get_metrics
-from ..evaluator.nq_eval import has_answers
+from ..evaluator.nq_eval import AnswerMatcher, has_answers
 from ..search import ShardedFlatIP
 from .losses import get_loss_function
 from .scheduler import ConstantScheduler, CosineScheduler, InverseSquareRootScheduler, LinearScheduler
@@ -157,8 +157,8 @@ class Trainer:
         d = getattr(self.training_args, "encode_corpus_dir", "")
         if d:
             os.makedirs(d, exist_ok=True)
-            self.index.local.save(os.path.join(d, f"{ep}.{self.local_rank}.bf16.npy"))
-            with open(os.path.join(d, f"{ep}.{self.local_rank}.json"), "w", encoding="utf-8") as f:
+            self.index.save_shard(d, ep)   # {ep}.{rank}.bf16.npy, memory-mappable (shards.py)
+            with open(os.path.join(d, f"{ep}.{self.rank}.json"), "w", encoding="utf-8") as f:
                 json.dump({"id": ids_local}, f, ensure_ascii=False)
         if dist.is_initialized():
             dist.barrier()
@@ -200,6 +200,12 @@ class Trainer:
         mine = ids[self.rank * mx: self.rank * mx + sizes[self.rank]]
         return mine.cpu().numpy()
 
+    def _doc_text(self, did_):
+        t = self._doc_cache.get(did_)
+        if t is None:
+            t = self._doc_cache[did_] = self.corpus_dataloader.dataset[did_]["original"]
+        return t
+
     def evaluate(self, query_loader, ep):
         self.model.eval()
         self._encoding_corpus(ep)
@@ -213,6 +219,8 @@ class Trainer:
             query_loader.sampler.set_epoch(0)
         documents, queries, answers, qid, did = [], [], [], [], []
         k = a.retrieve_num
+        matcher = AnswerMatcher()
+        self._doc_cache = {}
         for batch in query_loader:
             data = {kk: v.to(self.device) if v is not None else None for kk, v in batch[1].items()}
             q_reps = self._encode(query=data).q_reps
@@ -221,16 +229,12 @@ class Trainer:
             docs, doc_ids = [], []
             for i, indice in enumerate(indices):
                 eval_num += 1
-                doc, doc_id = [], []
-                for j, row in enumerate(indice):
-                    if row < 0:
-                        continue
-                    did_ = self.idx[row]
-                    d = self.corpus_dataloader.dataset[did_]["original"]
-                    doc_id.append(did_)
-                    doc.append(d)
-                    if has_answers(d, batch[2][i]):
-                        pos_index[i][j] = 1
+                cols = np.flatnonzero(indice >= 0)
+                doc_id = [self.idx[row] for row in indice[cols]]
+                doc = [self._doc_text(did_) for did_ in doc_id]
+                # has_answers over the whole list at once (nq_eval.AnswerMatcher: each passage
+                # tokenised once per evaluation, not once per retrieving query)
+                pos_index[i, cols] = matcher.match(doc_id, doc, batch[2][i])
                 docs.append(doc)
                 doc_ids.append(doc_id)
             documents.extend(docs)
@@ -299,6 +303,7 @@ class RRTrainer(Trainer):
             pair_loader.sampler.set_epoch(0)
         result = {}
         m = self.module
+        matcher = AnswerMatcher()
         for batch in pair_loader:
             data = {k: v.to(self.device) if v is not None else None for k, v in batch[1].items()}
             with torch.no_grad():
@@ -306,7 +311,7 @@ class RRTrainer(Trainer):
             for q, ans, d, s, did in zip(batch[0], batch[2], batch[3], scores, batch[4]):
                 r = result.setdefault(q, ([], [], [], []))
                 r[0].append(float(s[0]))
-                r[1].append(int(has_answers(d, ans)))
+                r[1].append(int(matcher.match([did], [d], ans)[0]))
                 r[2].append(d)
                 r[3].append(did)
         rdir = getattr(a, "rr_result_dir", "")

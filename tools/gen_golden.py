@@ -144,6 +144,36 @@ def gen_merge(ref_utils):
         json.dump(cases, f)
 
 
+def answer_cases(seed=21, n_docs=60, n_queries=40):
+    """Synthetic passages / answer lists for has_answers (uncased, NFD, punctuation,
+    accents, multi-token answers, answers absent from every passage, empty answers)."""
+    rng = np.random.default_rng(seed)
+    words = ["Paris", "paris", "the", "Eiffel", "Tower", "tower", "1889", "Caf\u00e9", "cafe\u0301", "New",
+             "York", "new-york", "U.S.", "u.s", "\u00c9cole", "ecole", "x", "42", "forty-two", "\u6771\u4eac",
+             "na\u00efve", "ma\u00f1ana", "O'Neil", "it's", "(1)", "rock", "and", "roll", "rock'n'roll", ","]
+    docs = [" ".join(rng.choice(words, size=int(rng.integers(0, 40)))) for _ in range(n_docs)]
+    cases = []
+    for _ in range(n_queries):
+        na = int(rng.integers(0, 4))
+        ans = [" ".join(rng.choice(words, size=int(rng.integers(1, 4)))) for _ in range(na)]
+        if rng.random() < 0.1:
+            ans.append("")
+        if rng.random() < 0.2:
+            ans.append("zzz not present")
+        sel = rng.choice(n_docs, size=int(rng.integers(1, 25)), replace=True).tolist()
+        cases.append({"answers": ans, "docs": sel})
+    return docs, cases
+
+
+def gen_answers():
+    import DRT.evaluator.nq_eval as ref_nq
+    docs, cases = answer_cases()
+    for c in cases:
+        c["has"] = [int(ref_nq.has_answers(docs[j], c["answers"])) for j in c["docs"]]
+    with open(os.path.join(OUT, "answers.json"), "w", encoding="utf-8") as f:
+        json.dump({"docs": docs, "cases": cases}, f, ensure_ascii=False)
+
+
 def main():
     os.makedirs(OUT, exist_ok=True)
     ref_bi, ref_linear, ref_utils, ref_losses, ref_metrics = _ref()
@@ -155,6 +185,7 @@ def main():
     gen_metrics(ref_metrics)
     gen_merge(ref_utils)
     gen_rerank()
+    gen_answers()
     for f in sorted(os.listdir(OUT)):
         print(f, os.path.getsize(os.path.join(OUT, f)))
 
