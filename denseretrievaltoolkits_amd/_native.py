@@ -57,6 +57,10 @@ _SIGNATURES = [
     ("drt_gemm_f32", c_i32, [c_vp, c_vp, c_vp, c_i64, c_i64, c_i64, c_i64, c_i64, c_i64, c_i32, c_i32, c_i32, c_vp, c_vp]),
     ("drt_ce_fwd", c_i32, [c_vp, c_i64, c_i64, c_i64, c_f32, c_vp, c_vp, c_vp, c_vp]),
     ("drt_ce_bwd", c_i32, [c_vp, c_vp, c_i64, c_i64, c_i64, c_vp, c_f32, c_vp, c_vp]),
+    ("drt_score_ce_workspace", c_sz, [c_i64, c_i64, c_i32]),
+    ("drt_score_ce_fwd", c_i32, [c_vp, c_vp, c_i64, c_i64, c_i32, c_i64, c_f32, c_vp, c_vp, c_vp, c_vp, c_sz, c_vp]),
+    ("drt_score_ce_bwd", c_i32, [c_vp, c_vp, c_vp, c_vp, c_i64, c_i64, c_i32, c_i64, c_vp, c_f32, c_vp, c_vp, c_vp,
+                                 c_sz, c_vp]),
     ("drt_transpose_f32", c_i32, [c_vp, c_i64, c_i64, c_vp, c_vp]),
     ("drt_profile_enable", c_i32, [c_i32, c_i32]),
     ("drt_profile_read", c_i32, [c_i32, c_vp, c_vp]),

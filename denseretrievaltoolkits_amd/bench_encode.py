@@ -147,8 +147,33 @@ def run_train_scores(device, bq=512, d=768, n_passages=(2, 8), steps=20, warmup=
                 fn()
             torch.cuda.synchronize()
             out[name + "_ms"] = round((time.perf_counter() - t0) / steps * 1e3, 4)
+        # device time of the same step: captured once in a hipGraph (torch.cuda.graph) and replayed,
+        # so host-side autograd / Python overhead (which dominates both eager timings) drops out
+        for name, fn in (("hip", ours), ("torch", ref)):
+            try:
+                side = torch.cuda.Stream(device)
+                side.wait_stream(torch.cuda.current_stream(device))
+                with torch.cuda.stream(side):
+                    for _ in range(warmup):
+                        fn()
+                torch.cuda.current_stream(device).wait_stream(side)
+                graph = torch.cuda.CUDAGraph()
+                with torch.cuda.graph(graph):
+                    fn()
+                graph.replay()
+                torch.cuda.synchronize()
+                t0 = time.perf_counter()
+                for _ in range(steps * 5):
+                    graph.replay()
+                torch.cuda.synchronize()
+                out[name + "_graph_ms"] = round((time.perf_counter() - t0) / (steps * 5) * 1e3, 4)
+                del graph
+            except Exception as e:  # report, keep the bench line
+                out[name + "_graph_error"] = f"{type(e).__name__}: {e}"[:200]
         fl = 6 * bq * bq * n * d
         out["flop"] = fl
         out["hip_tflops"] = round(fl / (out["hip_ms"] * 1e-3) / 1e12, 2)
+        if "hip_graph_ms" in out:
+            out["hip_graph_tflops"] = round(fl / (out["hip_graph_ms"] * 1e-3) / 1e12, 2)
         res[f"n{n}"] = out
     return res

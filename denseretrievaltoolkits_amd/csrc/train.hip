@@ -114,18 +114,18 @@ __device__ __forceinline__ void store_op(float (*S)[kGLd], int tid, const float 
   }
 }
 
+// One 64 x 64 output tile (tile_m, tile_n) over k in [kz * kchunk, ...) into C + kz * m * ldc.
 template <bool A_KC, bool B_KC, bool VEC>
-__global__ __launch_bounds__(256) void gemm_f32_kernel(const float* A, const float* B, float* C, int64_t m,
-                                                       int64_t n, int64_t k, int64_t lda, int64_t ldb, int64_t ldc,
-                                                       int64_t kchunk) {
-  __shared__ __attribute__((aligned(16))) float As[kGBK][kGLd];
-  __shared__ __attribute__((aligned(16))) float Bs[kGBK][kGLd];
+__device__ __forceinline__ void gemm_f32_tile(const float* A, const float* B, float* C, int64_t m, int64_t n,
+                                              int64_t k, int64_t lda, int64_t ldb, int64_t ldc, int64_t kchunk,
+                                              int64_t tile_m, int64_t tile_n, int64_t kz,
+                                              float (*As)[kGLd], float (*Bs)[kGLd]) {
   const int tid = threadIdx.x;
   const int wave = tid >> 6, lane = tid & 63;
   const int r = lane & 31, h = lane >> 5;
   const int wm = wave >> 1, wn = wave & 1;
-  const int64_t m0 = (int64_t)blockIdx.y * kGT, n0 = (int64_t)blockIdx.x * kGT;
-  const int64_t kb = (int64_t)blockIdx.z * kchunk;
+  const int64_t m0 = tile_m * kGT, n0 = tile_n * kGT;
+  const int64_t kb = kz * kchunk;
   const int64_t ke = kb + kchunk < k ? kb + kchunk : k;
   f32x16 acc;
 #pragma unroll
@@ -151,12 +151,66 @@ __global__ __launch_bounds__(256) void gemm_f32_kernel(const float* A, const flo
       acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a, b, acc, 0, 0, 0);
     }
   }
-  float* Cz = C + (int64_t)blockIdx.z * m * ldc;
+  float* Cz = C + kz * m * ldc;
 #pragma unroll
   for (int e = 0; e < 16; ++e) {
     const int64_t row = m0 + wm * 32 + (e & 3) + 8 * (e >> 2) + 4 * h;
     const int64_t col = n0 + wn * 32 + r;
     if (row < m && col < n) Cz[row * ldc + col] = acc[e];
+  }
+}
+
+template <bool A_KC, bool B_KC, bool VEC>
+__global__ __launch_bounds__(256) void gemm_f32_kernel(const float* A, const float* B, float* C, int64_t m,
+                                                       int64_t n, int64_t k, int64_t lda, int64_t ldb, int64_t ldc,
+                                                       int64_t kchunk) {
+  __shared__ __attribute__((aligned(16))) float As[kGBK][kGLd];
+  __shared__ __attribute__((aligned(16))) float Bs[kGBK][kGLd];
+  gemm_f32_tile<A_KC, B_KC, VEC>(A, B, C, m, n, k, lda, ldb, ldc, kchunk, blockIdx.y, blockIdx.x, blockIdx.z, As, Bs);
+}
+
+// Score-matrix backward, both GEMMs in ONE launch (split-K partials into ws):
+//   problem 0: dq [m][d] = dS [m][n] . p [n][d]       (A k-contiguous, B [k][n])
+//   problem 1: dp [n][d] = dS^T   . q [m][d]          (A = dS read as [k][m], B [k][n])
+// block b < t0 * z0 -> problem 0, else problem 1; z = split index.
+struct DualGemm {
+  const float* dS; const float* p; const float* q;
+  float* ws0; float* ws1;
+  int64_t m, n, d;
+  int64_t kchunk0, kchunk1, z0, z1, tn;   // tn = d tiles
+};
+
+template <bool VEC>
+__global__ __launch_bounds__(256) void gemm_f32_dual_kernel(DualGemm g) {
+  __shared__ __attribute__((aligned(16))) float As[kGBK][kGLd];
+  __shared__ __attribute__((aligned(16))) float Bs[kGBK][kGLd];
+  int64_t b = blockIdx.x;
+  const int64_t tm0 = (g.m + kGT - 1) / kGT;
+  const int64_t nb0 = tm0 * g.tn * g.z0;
+  if (b < nb0) {
+    const int64_t kz = b / (tm0 * g.tn), t = b % (tm0 * g.tn);
+    gemm_f32_tile<true, false, VEC>(g.dS, g.p, g.ws0, g.m, g.d, g.n, g.n, g.d, g.d, g.kchunk0, t / g.tn, t % g.tn,
+                                     kz, As, Bs);
+  } else {
+    b -= nb0;
+    const int64_t tm1 = (g.n + kGT - 1) / kGT;
+    const int64_t kz = b / (tm1 * g.tn), t = b % (tm1 * g.tn);
+    gemm_f32_tile<false, false, VEC>(g.dS, g.q, g.ws1, g.n, g.d, g.m, g.n, g.d, g.d, g.kchunk1, t / g.tn,
+                                      t % g.tn, kz, As, Bs);
+  }
+}
+
+// Fixed-order split-K sums of both problems: out0 [m0 x d] from z0 partials, out1 [m1 x d] from z1.
+__global__ __launch_bounds__(256) void dual_reduce_kernel(const float* ws0, int64_t z0, int64_t e0, float* out0,
+                                                          const float* ws1, int64_t z1, int64_t e1, float* out1) {
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < e0 + e1; i += (int64_t)gridDim.x * 256) {
+    const bool first = i < e0;
+    const int64_t j = first ? i : i - e0;
+    const float* w = first ? ws0 : ws1;
+    const int64_t z = first ? z0 : z1, e = first ? e0 : e1;
+    float s = w[j];
+    for (int64_t u = 1; u < z; ++u) s += w[u * e + j];
+    (first ? out0 : out1)[j] = s;
   }
 }
 
@@ -205,6 +259,40 @@ __global__ __launch_bounds__(256) void ce_fwd_kernel(const float* S, int64_t m, 
     lse[i] = l;
     const int64_t t = i * tstride;
     row_loss[i] = l - row[t];
+  }
+}
+
+// Forward row pass fused with the split-K reduction: row i of S = sum of the z partials
+// (fixed order), written out, then lse_i and loss_i as ce_fwd_kernel.
+__global__ __launch_bounds__(256) void ce_fwd_reduce_kernel(const float* ws, int64_t z, float* S, int64_t m,
+                                                            int64_t n, int64_t tstride, float* lse, float* row_loss) {
+  __shared__ float red[4];
+  __shared__ float target_score;
+  const int64_t i = blockIdx.x;
+  float* row = S + i * n;
+  const int64_t e = m * n, t = i * tstride;
+  float mx = -__builtin_inff();
+  for (int64_t j = threadIdx.x; j < n; j += 256) {
+    float v = ws[i * n + j];
+    for (int64_t u = 1; u < z; ++u) v += ws[u * e + i * n + j];
+    row[j] = v;
+    if (j == t) target_score = v;
+    mx = fmaxf(mx, v);
+  }
+  mx = warp_max(mx);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = mx;
+  __syncthreads();
+  mx = fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]));
+  __syncthreads();
+  float sum = 0.f;
+  for (int64_t j = threadIdx.x; j < n; j += 256) sum += expf(row[j] - mx);   // own writes: same thread
+  sum = warp_add(sum);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = sum;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const float l = mx + logf(red[0] + red[1] + red[2] + red[3]);
+    lse[i] = l;
+    row_loss[i] = l - target_score;
   }
 }
 
@@ -317,6 +405,89 @@ int drt_ce_bwd(const float* S, const float* lse, int64_t m, int64_t n, int64_t t
   DRT_REQUIRE(S && lse && dS);
   hipLaunchKernelGGL(ce_bwd_kernel, dim3((unsigned)m), dim3(256), 0, (hipStream_t)stream, S, lse, m, n,
                      target_stride, grad, scale, dS);
+  return hip_status(hipGetLastError());
+}
+
+// ---- fused score + CE (one host call per direction; workspace from drt_score_ce_workspace)
+static void split_plan(int64_t m, int64_t n, int64_t k, int64_t& kchunk, int64_t& nz) {
+  // split K until ~320 blocks of 64 x 64 tiles are in flight (>= 128 k per split)
+  const int64_t tiles = ((m + kGT - 1) / kGT) * ((n + kGT - 1) / kGT);
+  int64_t splits = (320 + tiles - 1) / tiles;
+  if (splits > k / 128) splits = k / 128;
+  if (splits < 1) splits = 1;
+  kchunk = (k + splits - 1) / splits;
+  kchunk = (kchunk + kGBK - 1) / kGBK * kGBK;
+  nz = k > 0 ? (k + kchunk - 1) / kchunk : 1;
+}
+
+static size_t score_ce_ws_floats(int64_t m, int64_t n, int64_t d, size_t* fwd, size_t* bwd) {
+  int64_t kc, z, kc0, z0, kc1, z1;
+  split_plan(m, n, d, kc, z);
+  split_plan(m, d, n, kc0, z0);
+  split_plan(n, d, m, kc1, z1);
+  const size_t f = (size_t)z * m * n + (size_t)m;
+  const size_t b = (size_t)m * n + (size_t)z0 * m * d + (size_t)z1 * n * d;
+  if (fwd) *fwd = f;
+  if (bwd) *bwd = b;
+  return f > b ? f : b;
+}
+
+size_t drt_score_ce_workspace(int64_t m, int64_t n, int32_t d) {
+  if (m <= 0 || n <= 0 || d <= 0) return 0;
+  return score_ce_ws_floats(m, n, d, nullptr, nullptr) * sizeof(float);
+}
+
+// S = q . p^T (exact f32), lse, loss = scale * mean_i (lse_i - S[i][i * target_stride]).
+// 3 launches: split-K GEMM -> per-row (split reduce + LSE + row loss) -> fixed-order mean.
+int drt_score_ce_fwd(const float* q, const float* p, int64_t m, int64_t n, int32_t d, int64_t target_stride,
+                     float scale, float* S, float* lse, float* loss, void* ws, size_t ws_bytes, void* stream) {
+  DRT_REQUIRE(m > 0 && n > 0 && d > 0 && target_stride >= 0 && (m - 1) * target_stride < n);
+  DRT_REQUIRE(q && p && S && lse && loss && ws && ws_bytes >= drt_score_ce_workspace(m, n, d));
+  hipStream_t s = (hipStream_t)stream;
+  int64_t kc, z;
+  split_plan(m, n, d, kc, z);
+  float* part = (float*)ws;
+  float* row_loss = part + (size_t)z * m * n;
+  const bool vec = ((uintptr_t)q % 16 == 0) && ((uintptr_t)p % 16 == 0) && d % 4 == 0;
+  dim3 grid((unsigned)((n + kGT - 1) / kGT), (unsigned)((m + kGT - 1) / kGT), (unsigned)z);
+  if (vec) hipLaunchKernelGGL((gemm_f32_kernel<true, true, true>), grid, dim3(256), 0, s, q, p, part, m, n,
+                              (int64_t)d, (int64_t)d, (int64_t)d, n, kc);
+  else hipLaunchKernelGGL((gemm_f32_kernel<true, true, false>), grid, dim3(256), 0, s, q, p, part, m, n,
+                          (int64_t)d, (int64_t)d, (int64_t)d, n, kc);
+  hipLaunchKernelGGL(ce_fwd_reduce_kernel, dim3((unsigned)m), dim3(256), 0, s, (const float*)part, z, S, m, n,
+                     target_stride, lse, row_loss);
+  hipLaunchKernelGGL(mean_kernel, dim3(1), dim3(256), 0, s, (const float*)row_loss, m, scale, loss);
+  return hip_status(hipGetLastError());
+}
+
+// dS = scale * g / m * (softmax(S) - onehot); dq = dS . p; dp = dS^T . q.
+// 3 launches: dS -> both GEMMs in one grid (split-K partials) -> both fixed-order reductions.
+int drt_score_ce_bwd(const float* q, const float* p, const float* S, const float* lse, int64_t m, int64_t n,
+                     int32_t d, int64_t target_stride, const float* grad, float scale, float* dq, float* dp,
+                     void* ws, size_t ws_bytes, void* stream) {
+  DRT_REQUIRE(m > 0 && n > 0 && d > 0 && target_stride >= 0 && (m - 1) * target_stride < n);
+  DRT_REQUIRE(q && p && S && lse && dq && dp && ws && ws_bytes >= drt_score_ce_workspace(m, n, d));
+  hipStream_t s = (hipStream_t)stream;
+  DualGemm g{};
+  float* dS = (float*)ws;
+  int64_t kc0, z0, kc1, z1;
+  split_plan(m, d, n, kc0, z0);
+  split_plan(n, d, m, kc1, z1);
+  g.dS = dS; g.p = p; g.q = q;
+  g.ws0 = dS + (size_t)m * n;
+  g.ws1 = g.ws0 + (size_t)z0 * m * d;
+  g.m = m; g.n = n; g.d = d;
+  g.kchunk0 = kc0; g.kchunk1 = kc1; g.z0 = z0; g.z1 = z1;
+  g.tn = (d + kGT - 1) / kGT;
+  hipLaunchKernelGGL(ce_bwd_kernel, dim3((unsigned)m), dim3(256), 0, s, S, lse, m, n, target_stride, grad, scale, dS);
+  const int64_t blocks = ((m + kGT - 1) / kGT) * g.tn * z0 + ((n + kGT - 1) / kGT) * g.tn * z1;
+  const bool vec = ((uintptr_t)q % 16 == 0) && ((uintptr_t)p % 16 == 0) && d % 4 == 0 && n % 4 == 0;
+  if (vec) hipLaunchKernelGGL(gemm_f32_dual_kernel<true>, dim3((unsigned)blocks), dim3(256), 0, s, g);
+  else hipLaunchKernelGGL(gemm_f32_dual_kernel<false>, dim3((unsigned)blocks), dim3(256), 0, s, g);
+  const int64_t e0 = m * d, e1 = n * d;
+  const int64_t rb = (e0 + e1 + 255) / 256 < 2048 ? (e0 + e1 + 255) / 256 : 2048;
+  hipLaunchKernelGGL(dual_reduce_kernel, dim3((unsigned)rb), dim3(256), 0, s, (const float*)g.ws0, z0, e0, dq,
+                     (const float*)g.ws1, z1, e1, dp);
   return hip_status(hipGetLastError());
 }
 

@@ -193,6 +193,21 @@ int drt_ce_fwd(const float* S, int64_t m, int64_t n, int64_t target_stride, floa
 int drt_ce_bwd(const float* S, const float* lse, int64_t m, int64_t n, int64_t target_stride,
                const float* grad, float scale, float* dS, void* stream);
 int drt_transpose_f32(const float* X, int64_t rows, int64_t cols, float* Y, void* stream);
+/* Fused score + CE, one host call per direction (the path score_ce.ScoreCE uses;
+ * replaces the matmul + CrossEntropyLoss of DRModel.forward, biencoder.py:107-119,
+ * and their autograd).  q [m,d], p [n,d] fp32 row-major; target t_i = i * target_stride.
+ * drt_score_ce_fwd: S [m,n], lse [m], *loss (3 launches: split-K GEMM, per-row split
+ *   reduction + LSE + row loss, fixed-order mean).
+ * drt_score_ce_bwd: dq [m,d] = dS . p, dp [n,d] = dS^T . q with dS as drt_ce_bwd
+ *   (3 launches: dS, both GEMMs in one grid, both fixed-order split reductions).
+ * Both need ws of drt_score_ce_workspace(m, n, d) bytes (scratch only; results are
+ * bit-identical to drt_gemm_f32 + drt_ce_fwd / drt_ce_bwd).                  */
+size_t drt_score_ce_workspace(int64_t m, int64_t n, int32_t d);
+int drt_score_ce_fwd(const float* q, const float* p, int64_t m, int64_t n, int32_t d, int64_t target_stride,
+                     float scale, float* S, float* lse, float* loss, void* ws, size_t ws_bytes, void* stream);
+int drt_score_ce_bwd(const float* q, const float* p, const float* S, const float* lse, int64_t m, int64_t n,
+                     int32_t d, int64_t target_stride, const float* grad, float scale, float* dq, float* dp,
+                     void* ws, size_t ws_bytes, void* stream);
 
 /* ------------------------------------------------------------------------
  * Launch timing (measurement support for bench.py's roofline figure).
