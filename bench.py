@@ -330,6 +330,7 @@ def main():
     if rank == 0 and not args.no_encode and world == 1:
         from denseretrievaltoolkits_amd import bench_encode
         out["rerank"] = bench_encode.run_rerank(dev)
+        out["query_encode"] = bench_encode.run_query_encode(dev)
         out["train_scores"] = bench_encode.run_train_scores(dev)
     if rank == 0:
         print(json.dumps(out), flush=True)

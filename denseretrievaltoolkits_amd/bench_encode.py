@@ -70,6 +70,45 @@ def run(device, batch=512, L=128, steps=10, warmup=2):
     }
 
 
+def run_query_encode(device, batches=(8, 128), L=32, steps=50, warmup=3):
+    """Query tower (C4: queries of 32 tokens, searched in batches of 128): DRModel.encode_query's
+    HIP forward + [CLS] pooling, eager launches vs hipGraph replay (HipBertEncoder._replay), at a
+    small interactive batch (8: host-bound when eager) and the search batch (128: GPU-bound)."""
+    from transformers import BertConfig, BertModel
+    from .model.encoder import HipBertEncoder
+    torch.manual_seed(0)
+    m = BertModel(BertConfig(), add_pooling_layer=False).eval()
+    enc = HipBertEncoder.from_hf(m, device)
+    del m
+    g = torch.Generator(device=device)
+    g.manual_seed(4)
+    fl = flops_per_seq(L)
+    res = {"metric": f"queries encoded/sec (bf16 BERT-base query tower, {L} tokens)", "unit": "queries/s",
+           "seq_len": L, "steps": steps}
+    for batch in batches:
+        ids = torch.randint(1000, 30522, (batch, L), generator=g, device=device, dtype=torch.int64)
+        ids[:, 0] = 101
+        ids[:, -1] = 102
+        mask = torch.ones((batch, L), dtype=torch.int64, device=device)
+        r = {}
+        for name, graphs in (("eager", False), ("graph", True)):
+            enc.graphs = graphs
+            for _ in range(warmup):
+                enc.pool(enc(ids, mask), mask, "first")
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            for _ in range(steps):
+                enc.pool(enc(ids, mask), mask, "first")
+            torch.cuda.synchronize()
+            el = time.perf_counter() - t0
+            r[name] = round(steps * batch / el, 1)
+            r[name + "_ms_per_batch"] = round(el / steps * 1e3, 4)
+        r["mfma_frac"] = round(fl * r["graph"] / 1e12 / 2500.0, 4)
+        res[f"b{batch}"] = r
+    res["value"] = res[f"b{batches[-1]}"]["graph"]
+    return res
+
+
 def run_rerank(device, pairs=1000, q_len=32, p_len=128, steps=3, warmup=1):
     """Config C5 (BASELINE.json configs[4]): cross-encoder rerank of the top-1000
     candidates of one query per step (RRModel.encode, DRT/model/reranker.py:111-130):

@@ -153,18 +153,45 @@ __global__ __launch_bounds__(kAttnThreads) void attention_kernel(AttnArgs a) {
   const __bf16* Kg = Qg + a.H;
   const __bf16* Vg = Qg + 2 * a.H;
 
-  // ---- stage K (swizzled rows) and V^T, key bias
-  for (int i = tid; i < Lp * 8; i += kAttnThreads) {
-    const int key = i >> 3, c = i & 7;
-    u32x4 kv = {0u, 0u, 0u, 0u}, vv = {0u, 0u, 0u, 0u};
-    if (key < L) {
-      kv = *(const u32x4*)(Kg + (int64_t)key * ld + c * 8);
-      vv = *(const u32x4*)(Vg + (int64_t)key * ld + c * 8);
-    }
-    *(u32x4*)(Ks + key * 128 + ((c ^ ((key >> 1) & 7)) << 4)) = kv;
-    const uint16_t* ve = (const uint16_t*)&vv;
+  // ---- stage K (swizzled rows) and V^T, key bias.  Passes of 128 keys: thread (key group
+  // kg = tid >> 3, 16-B chunk c = tid & 7) owns keys 4 kg .. 4 kg + 3 of chunk c, issues all 8
+  // global loads of the pass before any LDS store, and writes V^T as 8 ds_write_b64 (4 keys
+  // of one d per store) instead of 32 ds_write_b16.  The first Q block's fragments are
+  // requested before the pass so their latency overlaps the staging.
+  const int c8 = tid & 7, kg = tid >> 3;
+  int qrow0 = wave * 32 + (lane & 31);
+  qrow0 = qrow0 < L ? qrow0 : L - 1;
+  bf16x8 q0[4];
 #pragma unroll
-    for (int j = 0; j < 8; ++j) *(uint16_t*)(Vt + (c * 8 + j) * vts + key * 2) = ve[j];
+  for (int st = 0; st < 4; ++st) q0[st] = *(const bf16x8*)(Qg + (int64_t)qrow0 * ld + st * 16 + (lane >> 5) * 8);
+  for (int kp = 0; kp < Lp; kp += 128) {
+    u32x4 kv[4], vv[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int key = kp + kg * 4 + u;
+      kv[u] = u32x4{0u, 0u, 0u, 0u};
+      vv[u] = u32x4{0u, 0u, 0u, 0u};
+      if (key < L) {
+        kv[u] = *(const u32x4*)(Kg + (int64_t)key * ld + c8 * 8);
+        vv[u] = *(const u32x4*)(Vg + (int64_t)key * ld + c8 * 8);
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int key = kp + kg * 4 + u;
+      if (key < Lp) *(u32x4*)(Ks + key * 128 + ((c8 ^ ((key >> 1) & 7)) << 4)) = kv[u];
+    }
+    const int key0 = kp + kg * 4;
+    if (key0 < Lp) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        uint16_t e[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) e[u] = ((const uint16_t*)&vv[u])[j];
+        const uint32_t lo = (uint32_t)e[0] | ((uint32_t)e[1] << 16), hi = (uint32_t)e[2] | ((uint32_t)e[3] << 16);
+        *(uint2*)(Vt + (c8 * 8 + j) * vts + key0 * 2) = make_uint2(lo, hi);
+      }
+    }
   }
   for (int i = tid; i < Lp; i += kAttnThreads) {
     float bv = 0.0f;
@@ -183,7 +210,7 @@ __global__ __launch_bounds__(kAttnThreads) void attention_kernel(AttnArgs a) {
     bf16x8 qf[4];
 #pragma unroll
     for (int s = 0; s < 4; ++s) {
-      bf16x8 v = *(const bf16x8*)(Qg + (int64_t)qrow * ld + s * 16 + h * 8);
+      bf16x8 v = qb == wave ? q0[s] : *(const bf16x8*)(Qg + (int64_t)qrow * ld + s * 16 + h * 8);
 #pragma unroll
       for (int j = 0; j < 8; ++j) v[j] = (__bf16)((float)v[j] * a.scale);
       qf[s] = v;

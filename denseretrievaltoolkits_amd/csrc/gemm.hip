@@ -33,6 +33,8 @@ struct GemmArgs {
   float alpha;
   unsigned long long* dbg;  // diagnostic builds only (segment stamps)
   int order;                // tile order within an XCD's range (tile_order)
+  int64_t kchunk;           // split-K (128^2 kernel, PART): k per split; ws [splits][m][n] fp32
+  float* ws;
 };
 static unsigned long long* g_gemm_dbg = nullptr;
 
@@ -95,7 +97,7 @@ enum { EPI_NONE = 0, EPI_BIAS = 1, EPI_GELU = 2, EPI_RESID = 4 };
 static int g_gemm_variant = 0;
 static int g_gemm_order = -1;   // -1 auto: grouped-8 for K <= 1024 (small panels), row-major otherwise  // A/B switch: 0 auto (large full-K), 1 small 128^2, 2 large half-K ring
 
-template <bool OUT_BF16, int EPI>
+template <bool OUT_BF16, int EPI, bool PART = false>
 __global__ __launch_bounds__(kGemmThreads, 2) void gemm_nt_kernel(GemmArgs a) {
   __shared__ __attribute__((aligned(16))) char smem[kGemmLds];
   const int tid = threadIdx.x;
@@ -115,7 +117,10 @@ __global__ __launch_bounds__(kGemmThreads, 2) void gemm_nt_kernel(GemmArgs a) {
   const int64_t n0 = (int64_t)(wg % tiles_n) * kBN;
 
   const uint32_t lds0 = g_lds_addr(smem);
-  const int ksteps = (int)(a.k / kBK);
+  // PART: this block sums k in [kbeg, kend) of split blockIdx.z (kchunk % kBK == 0)
+  const int64_t kbeg = PART ? (int64_t)blockIdx.z * a.kchunk : 0;
+  const int64_t kend = PART ? (kbeg + a.kchunk < a.k ? kbeg + a.kchunk : a.k) : a.k;
+  const int ksteps = (int)((kend - kbeg) / kBK);
 
   f32x16 acc[2][2];
 #pragma unroll
@@ -130,8 +135,8 @@ __global__ __launch_bounds__(kGemmThreads, 2) void gemm_nt_kernel(GemmArgs a) {
 #pragma unroll
   for (int s = 0; s < 4; ++s) aoff[s] = r * 128 + ((((2 * s) | h) ^ sw) << 4);
 
-  stage_panel(a.A, a.lda, m0, a.m, 0, lds0, wave, lane);
-  stage_panel(a.B, a.ldb, n0, a.n, 0, lds0 + kTileA, wave, lane);
+  stage_panel(a.A, a.lda, m0, a.m, kbeg, lds0, wave, lane);
+  stage_panel(a.B, a.ldb, n0, a.n, kbeg, lds0 + kTileA, wave, lane);
 
   for (int kt = 0; kt < ksteps; ++kt) {
     const int slot = kt & 1;
@@ -140,8 +145,8 @@ __global__ __launch_bounds__(kGemmThreads, 2) void gemm_nt_kernel(GemmArgs a) {
     __builtin_amdgcn_s_barrier();
     if (kt + 1 < ksteps) {
       const uint32_t nb = lds0 + (slot ^ 1) * kStage;
-      stage_panel(a.A, a.lda, m0, a.m, (int64_t)(kt + 1) * kBK, nb, wave, lane);
-      stage_panel(a.B, a.ldb, n0, a.n, (int64_t)(kt + 1) * kBK, nb + kTileA, wave, lane);
+      stage_panel(a.A, a.lda, m0, a.m, kbeg + (int64_t)(kt + 1) * kBK, nb, wave, lane);
+      stage_panel(a.B, a.ldb, n0, a.n, kbeg + (int64_t)(kt + 1) * kBK, nb + kTileA, wave, lane);
     }
     const char* As = smem + slot * kStage + wm * 64 * 128;
     const char* Bs = smem + slot * kStage + kTileA + wn * 64 * 128;
@@ -162,6 +167,22 @@ __global__ __launch_bounds__(kGemmThreads, 2) void gemm_nt_kernel(GemmArgs a) {
 
   // Epilogue.  acc[i][j][e]: row m0 + wm*64 + i*32 + (e&3) + 8*(e>>2) + 4*h,
   //                          col n0 + wn*64 + j*32 + r.
+  if (PART) {   // raw fp32 partial sums of this split; splitk_epi_kernel finishes
+    float* wz = a.ws + (int64_t)blockIdx.z * a.m * a.n;
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const int64_t col = n0 + wn * 64 + j * 32 + r;
+      if (col >= a.n) continue;
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int e = 0; e < 16; ++e) {
+          const int64_t row = m0 + wm * 64 + i * 32 + (e & 3) + 8 * (e >> 2) + 4 * h;
+          if (row < a.m) wz[row * a.n + col] = acc[i][j][e];
+        }
+    }
+    return;
+  }
 #pragma unroll
   for (int j = 0; j < 2; ++j) {
     const int64_t col = n0 + wn * 64 + j * 32 + r;
@@ -182,6 +203,62 @@ __global__ __launch_bounds__(kGemmThreads, 2) void gemm_nt_kernel(GemmArgs a) {
       }
     }
   }
+}
+
+// Split-K finish: out = epilogue(sum_z ws[z]) in a fixed z order (deterministic), 4 columns
+// per thread when n % 4 == 0.
+template <bool OUT_BF16, int EPI>
+__global__ __launch_bounds__(256) void splitk_epi_kernel(GemmArgs a, int splits) {
+  const int64_t mn = a.m * a.n;
+  const bool v4 = (a.n % 4 == 0) && (a.ldc % 4 == 0) && (!(EPI & EPI_RESID) || a.ldr % 4 == 0);
+  const int64_t units = v4 ? mn / 4 : mn;
+  for (int64_t u = (int64_t)blockIdx.x * 256 + threadIdx.x; u < units; u += (int64_t)gridDim.x * 256) {
+    const int64_t e0 = v4 ? u * 4 : u;
+    const int64_t row = e0 / a.n, col = e0 % a.n;
+    const int w = v4 ? 4 : 1;
+    float v[4];
+    if (v4) {
+      f32x4 s4 = *(const f32x4*)(a.ws + e0);
+      for (int z = 1; z < splits; ++z) {
+        const f32x4 t = *(const f32x4*)(a.ws + (int64_t)z * mn + e0);
+        s4 += t;
+      }
+#pragma unroll
+      for (int q = 0; q < 4; ++q) v[q] = s4[q];
+    } else {
+      float s1 = a.ws[e0];
+      for (int z = 1; z < splits; ++z) s1 += a.ws[(int64_t)z * mn + e0];
+      v[0] = s1;
+    }
+    for (int q = 0; q < w; ++q) {
+      float x = v[q] * a.alpha;
+      if (EPI & EPI_BIAS) x += a.bias[col + q];
+      if (EPI & EPI_GELU) x = gelu_erf(x);
+      if (EPI & EPI_RESID) x += (float)a.R[row * a.ldr + col + q];
+      if (OUT_BF16) ((__bf16*)a.C)[row * a.ldc + col + q] = (__bf16)x;
+      else ((float*)a.C)[row * a.ldc + col + q] = x;
+    }
+  }
+}
+
+// Split plan of the 128^2 kernel for problems too small to fill the chip (query-sized
+// batches): enough splits for ~2 blocks per CU, >= 128 k per split.  0 = no split.
+static int small_splits(int64_t m, int64_t n, int64_t k, int64_t* kchunk) {
+  const int64_t tiles = ((m + kBM - 1) / kBM) * ((n + kBN - 1) / kBN);
+  if (tiles >= 384 || k < 256) return 0;
+  int64_t splits = (512 + tiles - 1) / tiles;
+  if (splits > k / 128) splits = k / 128;
+  // partials must stay small enough to be re-read from the caches: at 4096 x 768 (a 128-query
+  // batch) 3 splits = 38 MB of partials measured slower than the unsplit kernel
+  const int64_t cap = (int64_t)(16 << 20) / (m * n * 4);
+  if (splits > cap) splits = cap;
+  if (splits < 2) return 0;
+  int64_t kc = (k + splits - 1) / splits;
+  kc = (kc + kBK - 1) / kBK * kBK;
+  splits = (k + kc - 1) / kc;
+  if (splits < 2) return 0;
+  *kchunk = kc;
+  return (int)splits;
 }
 
 // ---------------------------------------------------------------------------
@@ -889,7 +966,19 @@ static int launch_gemm_t(const GemmArgs& a0, hipStream_t s) {
     hipLaunchKernelGGL((gemm_nt_pp1_kernel<OUT_BF16, EPI, 0, 5>), dim3((unsigned)tiles_l), dim3(kLThreads), 0, s, a);
   } else {
     const int64_t tiles = ((a.m + kBM - 1) / kBM) * ((a.n + kBN - 1) / kBN);
-    hipLaunchKernelGGL((gemm_nt_kernel<OUT_BF16, EPI>), dim3((unsigned)tiles), dim3(kGemmThreads), 0, s, a);
+    int64_t kc = 0;
+    const int splits = a.ws ? small_splits(a.m, a.n, a.k, &kc) : 0;
+    if (splits > 1) {
+      GemmArgs b = a;
+      b.kchunk = kc;
+      hipLaunchKernelGGL((gemm_nt_kernel<OUT_BF16, EPI, true>), dim3((unsigned)tiles, 1, (unsigned)splits),
+                         dim3(kGemmThreads), 0, s, b);
+      const int64_t units = (a.n % 4 == 0) ? a.m * a.n / 4 : a.m * a.n;
+      const int64_t blocks = (units + 255) / 256 < 4096 ? (units + 255) / 256 : 4096;
+      hipLaunchKernelGGL((splitk_epi_kernel<OUT_BF16, EPI>), dim3((unsigned)blocks), dim3(256), 0, s, b, splits);
+    } else {
+      hipLaunchKernelGGL((gemm_nt_kernel<OUT_BF16, EPI>), dim3((unsigned)tiles), dim3(kGemmThreads), 0, s, a);
+    }
   }
   prof_end(pp, s);
   return hip_status(hipGetLastError());
@@ -940,10 +1029,31 @@ extern "C" int drt_gemm_nt_bf16_f32(const void* A, const void* B, float* C, int6
   return launch_gemm(a, false, EPI_NONE, (hipStream_t)stream);
 }
 
+// Workspace that lets drt_linear_bf16_ws split K on problems too small to fill the chip
+// (0 when no split is planned for this shape).
+extern "C" size_t drt_linear_workspace(int64_t M, int64_t N, int64_t K) {
+  if (M <= 0 || N <= 0 || K <= 0 || K % 64) return 0;
+  const int64_t tiles_l = ((M + kL - 1) / kL) * ((N + kL - 1) / kL);
+  if (tiles_l >= 512) return 0;   // the 256^2 path does not split
+  int64_t kc = 0;
+  const int splits = small_splits(M, N, K, &kc);
+  return splits > 1 ? (size_t)splits * (size_t)M * (size_t)N * sizeof(float) : 0;
+}
+
+extern "C" int drt_linear_bf16_ws(const void* X, const void* W, const float* bias, const void* residual, void* Y,
+                                  int64_t M, int64_t N, int64_t K, int32_t flags, void* ws, size_t ws_bytes,
+                                  void* stream);
+
 // nn.Linear: Y[M, N] = X[M, K] . W[N, K]^T (+ bias) (GELU) (+ residual [M, N] bf16)
 // flags: DRT_LIN_GELU = 1, DRT_LIN_OUT_F32 = 2.
 extern "C" int drt_linear_bf16(const void* X, const void* W, const float* bias, const void* residual, void* Y,
                                int64_t M, int64_t N, int64_t K, int32_t flags, void* stream) {
+  return drt_linear_bf16_ws(X, W, bias, residual, Y, M, N, K, flags, nullptr, 0, stream);
+}
+
+extern "C" int drt_linear_bf16_ws(const void* X, const void* W, const float* bias, const void* residual, void* Y,
+                                  int64_t M, int64_t N, int64_t K, int32_t flags, void* ws, size_t ws_bytes,
+                                  void* stream) {
   DRT_REQUIRE(M >= 0 && N > 0 && K > 0 && K % 64 == 0);
   if (M == 0) return DRT_OK;
   DRT_REQUIRE(X && W && Y);
@@ -963,6 +1073,8 @@ extern "C" int drt_linear_bf16(const void* X, const void* W, const float* bias, 
   a.ldc = N;
   a.ldr = N;
   a.alpha = 1.0f;
+  // split-K only with a large-enough caller workspace (else the unsplit kernel)
+  if (ws && ws_bytes >= drt_linear_workspace(M, N, K) && drt_linear_workspace(M, N, K) > 0) a.ws = (float*)ws;
   const int epi = (bias ? EPI_BIAS : 0) | (gelu ? EPI_GELU : 0) | (residual ? EPI_RESID : 0);
   return launch_gemm(a, !f32, epi, (hipStream_t)stream);
 }

@@ -71,6 +71,12 @@ class HipBertEncoder:
         if presum not in ("bf16", "fp32"):
             raise ValueError(f"presum must be 'bf16' or 'fp32', got {presum!r}")
         self.presum = presum
+        self.graphs = True              # hipGraph replay for B * L <= graph_max_tokens
+        self.graph_max_tokens = 16384
+        self.graph_cache_size = 8
+        self._graph_cache = {}
+        self._ws_plan = {}
+        self._ws = None
         self.shape = shape
         self.device = device
         self.lib = _native.load()
@@ -118,15 +124,26 @@ class HipBertEncoder:
         m, k = x.shape
         n = w.shape[0]
         flags = (1 if gelu else 0) | (2 if out.dtype == torch.float32 else 0)
-        _native.check(self.lib.drt_linear_bf16(x.data_ptr(), w.data_ptr(), b.data_ptr() if b is not None else None,
-                                               resid.data_ptr() if resid is not None else None, out.data_ptr(),
-                                               m, n, k, flags, self.stream), "drt_linear_bf16")
+        ws = self._ws
+        _native.check(self.lib.drt_linear_bf16_ws(x.data_ptr(), w.data_ptr(), b.data_ptr() if b is not None else None,
+                                                  resid.data_ptr() if resid is not None else None, out.data_ptr(),
+                                                  m, n, k, flags, ws.data_ptr() if ws is not None else None,
+                                                  ws.numel() * 4 if ws is not None else 0, self.stream),
+                      "drt_linear_bf16_ws")
         return out
+
+    def _ws_bytes(self, T: int) -> int:
+        """Split-K scratch for this token count (small batches only; 0 at encode sizes)."""
+        nb = self._ws_plan.get(T)
+        if nb is None:
+            H, I = self.shape.hidden, self.shape.intermediate
+            nb = max(int(self.lib.drt_linear_workspace(T, n, k)) for n, k in ((3 * H, H), (H, H), (I, H), (H, I)))
+            self._ws_plan[T] = nb
+        return nb
 
     def forward(self, input_ids: torch.Tensor, attention_mask: Optional[torch.Tensor] = None,
                 token_type_ids: Optional[torch.Tensor] = None) -> torch.Tensor:
         """last_hidden_state [B, L, H] bf16."""
-        sh = self.shape
         dev = self.device
         ids = input_ids.to(dev, torch.int64).contiguous()
         B, L = ids.shape
@@ -134,6 +151,50 @@ class HipBertEncoder:
             raise ValueError(f"sequence length {L} exceeds max_position_embeddings {self.pos.shape[0]}")
         mask = attention_mask.to(dev, torch.int64).contiguous() if attention_mask is not None else None
         tt = token_type_ids.to(dev, torch.int64).contiguous() if token_type_ids is not None else None
+        if (self.graphs and 0 < B * L <= self.graph_max_tokens
+                and not torch.cuda.is_current_stream_capturing()):
+            return self._replay(ids, mask, tt)
+        return self._run(ids, mask, tt)
+
+    # -- hipGraph replay ------------------------------------------------
+    # Small batches (queries: 128 x 32 tokens) are host-bound: 1 + 7 x layers launches through
+    # ctypes cost more host time than the GPU needs.  Each (B, L, mask?, types?) shape is
+    # captured once into a hipGraph (torch.cuda.graph on the launch stream) and replayed: one
+    # host call per forward.  Inputs are copied into the graph's static buffers; the output is
+    # a copy of the graph's static output (the next replay overwrites it).  A new encoder is
+    # built whenever the weights change (biencoder._hip_encoder), which drops its graphs.
+    def _replay(self, ids, mask, tt):
+        key = (tuple(ids.shape), mask is not None, tt is not None)
+        ent = self._graph_cache.get(key)
+        if ent is None:
+            dev = self.device
+            si = ids.clone()
+            sm = mask.clone() if mask is not None else None
+            st = tt.clone() if tt is not None else None
+            side = torch.cuda.Stream(dev)
+            side.wait_stream(torch.cuda.current_stream(dev))
+            with torch.cuda.stream(side):     # eager warm-up: one-time kernel attributes, allocator
+                self._run(si, sm, st)
+            torch.cuda.current_stream(dev).wait_stream(side)
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g):
+                out = self._run(si, sm, st)
+            if len(self._graph_cache) >= self.graph_cache_size:
+                self._graph_cache.pop(next(iter(self._graph_cache)))
+            ent = self._graph_cache[key] = (g, si, sm, st, out)
+        g, si, sm, st, out = ent
+        si.copy_(ids)
+        if sm is not None:
+            sm.copy_(mask)
+        if st is not None:
+            st.copy_(tt)
+        g.replay()
+        return out.clone()
+
+    def _run(self, ids, mask, tt):
+        sh = self.shape
+        dev = self.device
+        B, L = ids.shape
         H, T = sh.hidden, B * L
         self.stream = _native.stream_ptr(dev)
         h = torch.empty((T, H), dtype=torch.bfloat16, device=dev)
@@ -147,6 +208,8 @@ class HipBertEncoder:
         x32 = torch.empty((T, H), dtype=torch.float32 if f32 else torch.bfloat16, device=dev)
         ln = self.lib.drt_layernorm_f32_bf16 if f32 else self.lib.drt_layernorm_bf16
         ffn = torch.empty((T, sh.intermediate), dtype=torch.bfloat16, device=dev)
+        nb = self._ws_bytes(T)
+        self._ws = torch.empty((nb + 3) // 4, dtype=torch.float32, device=dev) if nb else None
         scale = 1.0 / math.sqrt(H // sh.heads)
         for ly in self.layers:
             self._lin(h, ly["wqkv"], ly["bqkv"], qkv)

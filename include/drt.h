@@ -147,6 +147,15 @@ int drt_embed_ln(const int64_t* ids, const int64_t* type_ids, int64_t B, int64_t
                  void* stream);
 int drt_linear_bf16(const void* X, const void* W, const float* bias, const void* residual,
                     void* Y, int64_t M, int64_t N, int64_t K, int32_t flags, void* stream);
+/* drt_linear_bf16_ws: the same with a caller workspace; shapes too small to fill the chip
+ * (query-sized batches: < 384 tiles of 128^2, partials <= 16 MiB) split K over ~2 blocks
+ * per CU into ws (fp32 partials) and finish with one fixed-order reduction + epilogue
+ * (deterministic).
+ * drt_linear_workspace(M, N, K) = the bytes it needs (0: no split for this shape).      */
+size_t drt_linear_workspace(int64_t M, int64_t N, int64_t K);
+int drt_linear_bf16_ws(const void* X, const void* W, const float* bias, const void* residual,
+                       void* Y, int64_t M, int64_t N, int64_t K, int32_t flags, void* ws,
+                       size_t ws_bytes, void* stream);
 int drt_layernorm_f32_bf16(const float* X, int64_t M, int32_t H, const float* gamma,
                            const float* beta, float eps, void* out, void* stream);
 int drt_layernorm_bf16(const void* X, int64_t M, int32_t H, const float* gamma,

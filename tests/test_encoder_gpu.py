@@ -152,3 +152,66 @@ def test_layernorm_bf16_and_f32_inputs_vs_torch(dev, M, H):
         _native.check(fn(xin.data_ptr(), M, H, gam.data_ptr(), bet.data_ptr(), 1e-12, out.data_ptr(), s), "ln")
         ref = torch.nn.functional.layer_norm(xin.float(), (H,), gam, bet, 1e-12)
         torch.testing.assert_close(out.float(), ref, atol=3e-2, rtol=1e-2)
+
+
+def test_graph_replay_bit_identical_to_eager(dev):
+    """hipGraph replay (B * L <= graph_max_tokens) == the eager launch sequence, bit for bit, across
+    new inputs of a captured shape, several shapes, and cache eviction."""
+    import torch
+    from denseretrievaltoolkits_amd.model.encoder import HipBertEncoder
+    m = _models(2, seed=4)
+    enc = HipBertEncoder.from_hf(m, dev)
+    enc.graph_cache_size = 2
+    shapes = [(16, 32), (3, 50), (16, 32), (7, 128), (3, 50)]
+    for i, (B, L) in enumerate(shapes):
+        ids, mask = bw.token_batch(B, L, seed=100 + i)
+        ids_d, mask_d = torch.from_numpy(ids).to(dev), torch.from_numpy(mask).to(dev)
+        enc.graphs = True
+        a = enc(ids_d, mask_d)
+        b2 = enc(ids_d, None)
+        enc.graphs = False
+        e = enc(ids_d, mask_d)
+        e2 = enc(ids_d, None)
+        assert torch.equal(a, e) and torch.equal(b2, e2), (B, L)
+    assert len(enc._graph_cache) <= 2
+
+
+@pytest.mark.parametrize("M,N,K,flags,resid", [(256, 2304, 768, 0, False), (256, 768, 3072, 0, True),
+                                               (1024, 768, 768, 2, True), (100, 3072, 768, 1, False),
+                                               (37, 98, 512, 2, True), (8, 768, 3072, 2, False)])
+def test_split_k_linear_vs_unsplit_and_torch(dev, M, N, K, flags, resid):
+    """drt_linear_bf16_ws (split K for query-sized batches, fixed-order reduction + epilogue) against the
+    unsplit drt_linear_bf16 and torch fp32; the split is planned for every shape here."""
+    import torch
+    from denseretrievaltoolkits_amd import _native
+    lib = _native.load()
+    nb = int(lib.drt_linear_workspace(M, N, K))
+    assert nb > 0
+    g = torch.Generator(device=dev).manual_seed(M + N + K)
+    x = torch.randn(M, K, generator=g, device=dev).to(torch.bfloat16)
+    w = (0.05 * torch.randn(N, K, generator=g, device=dev)).to(torch.bfloat16)
+    b = torch.randn(N, generator=g, device=dev)
+    r = torch.randn(M, N, generator=g, device=dev).to(torch.bfloat16) if resid else None
+    ref = x.float() @ w.float().T + b
+    if flags & 1:
+        ref = torch.nn.functional.gelu(ref)
+    if r is not None:
+        ref = ref + r.float()
+    dt = torch.float32 if flags & 2 else torch.bfloat16
+    ws = torch.empty((nb + 3) // 4, dtype=torch.float32, device=dev)
+    s = _native.stream_ptr(dev)
+    o1 = torch.empty(M, N, dtype=dt, device=dev)
+    o0 = torch.empty(M, N, dtype=dt, device=dev)
+    rp = r.data_ptr() if r is not None else None
+    _native.check(lib.drt_linear_bf16_ws(x.data_ptr(), w.data_ptr(), b.data_ptr(), rp, o1.data_ptr(), M, N, K, flags,
+                                         ws.data_ptr(), nb, s), "split")
+    _native.check(lib.drt_linear_bf16(x.data_ptr(), w.data_ptr(), b.data_ptr(), rp, o0.data_ptr(), M, N, K, flags, s),
+                  "unsplit")
+    # too-small workspace: silently the unsplit kernel, same result as o0
+    o2 = torch.empty(M, N, dtype=dt, device=dev)
+    _native.check(lib.drt_linear_bf16_ws(x.data_ptr(), w.data_ptr(), b.data_ptr(), rp, o2.data_ptr(), M, N, K, flags,
+                                         ws.data_ptr(), nb - 4, s), "small ws")
+    assert torch.equal(o2, o0)
+    tol = dict(atol=2e-3, rtol=1e-4) if dt == torch.float32 else dict(atol=3e-2, rtol=1e-2)
+    torch.testing.assert_close(o1.float(), ref, **tol)
+    torch.testing.assert_close(o0.float(), ref, **tol)
