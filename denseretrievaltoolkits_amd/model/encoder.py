@@ -71,7 +71,9 @@ class HipBertEncoder:
         if presum not in ("bf16", "fp32"):
             raise ValueError(f"presum must be 'bf16' or 'fp32', got {presum!r}")
         self.presum = presum
-        self.graphs = True              # hipGraph replay for B * L <= graph_max_tokens
+        # hipGraph replay for B * L <= graph_max_tokens: off by default -- measured no gain
+        # (bench query_encode: batch 8 and 128 are GPU-bound, the replay adds input/output copies)
+        self.graphs = False
         self.graph_max_tokens = 16384
         self.graph_cache_size = 8
         self._graph_cache = {}

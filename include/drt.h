@@ -170,6 +170,8 @@ int drt_l2_normalize_f32(float* x, int64_t B, int32_t H, void* out_bf16, void* s
  * 7/8 ping-pong 4/5-slot ring, 9 full-K 32x32x16 256x256; >= 16 diagnostic
  * builds (ablations / cycle stamps, need drt_gemm_debug_buffer).            */
 int drt_gemm_force_small(int32_t on);
+/* Benchmark switch: smallest grid, in 256x256 tiles, that takes the 256x256 kernel. */
+int drt_gemm_large_min_tiles(int64_t tiles);
 /* Diagnostic only: device buffer for the GEMM cycle-stamp variants (drt_gemm_force_small >= 16). */
 int drt_gemm_debug_buffer(void* buf);
 /* Benchmark switch: tile order of the 256x256 ping-pong GEMM inside each XCD's tile range
