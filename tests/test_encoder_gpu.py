@@ -215,3 +215,28 @@ def test_split_k_linear_vs_unsplit_and_torch(dev, M, N, K, flags, resid):
     tol = dict(atol=2e-3, rtol=1e-4) if dt == torch.float32 else dict(atol=3e-2, rtol=1e-2)
     torch.testing.assert_close(o1.float(), ref, **tol)
     torch.testing.assert_close(o0.float(), ref, **tol)
+
+
+def test_gemm_gelu_epilogue_value_sweep(dev):
+    """The 256^2 kernel's GELU epilogue (packed, one exp per element) on exact pre-activations:
+    X rows are unit vectors, so every output is exactly W[n, m % 64] + bias; 16384 distinct values in
+    [-9, 9] against torch's erf GELU, both rounded to bf16: at most 1 bf16 ulp apart."""
+    import torch
+    from denseretrievaltoolkits_amd import _native
+    lib = _native.load()
+    M, N, K = 32768, 256, 64
+    x = torch.zeros(M, K, device=dev)
+    x[torch.arange(M), torch.arange(M) % K] = 1.0
+    x = x.to(torch.bfloat16)
+    v = torch.linspace(-9.0, 9.0, N * K, device=dev).reshape(N, K).to(torch.bfloat16)
+    b = torch.zeros(N, device=dev)
+    out = torch.empty(M, N, dtype=torch.bfloat16, device=dev)
+    _native.check(lib.drt_linear_bf16(x.data_ptr(), v.data_ptr(), b.data_ptr(), None, out.data_ptr(), M, N, K, 1,
+                                      _native.stream_ptr(dev)), "gelu")
+    pre = v.float().T[torch.arange(M) % K]                       # [M, N] exact pre-activations
+    ref = torch.nn.functional.gelu(pre.double()).float().to(torch.bfloat16)
+    # one bf16 ulp (2^-7 relative) except in the far negative tail (GELU(x < -5.7) ~ 0: absolute 1e-6)
+    err = (out.float() - ref.float()).abs()
+    assert bool((err <= ref.float().abs() * 2.0 ** -7 + 1e-6).all()), float(err.max())
+    big = ref.float().abs() > 1e-3
+    assert float((out != ref)[big].float().mean()) < 0.02
