@@ -133,7 +133,7 @@ struct AttnArgs {
   float scale;            // 1/sqrt(dh): applied to Q (exact for dh = 64)
 };
 
-__global__ __launch_bounds__(kAttnThreads) void attention_kernel(AttnArgs a) {
+__global__ __launch_bounds__(kAttnThreads, 4) void attention_kernel(AttnArgs a) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int L = (int)a.L;
   const int Lp = (L + 31) & ~31;           // keys padded to the 32-key tile
