@@ -1446,6 +1446,105 @@ __global__ __launch_bounds__(kTreeThreads) void merge_packed_tree_kernel(const u
   if (status && tid == 0) status[q] = (bad || (L[k - 1] == ~0ull && n_global >= (int64_t)k)) ? 1 : 0;
 }
 
+// Rank merge of packed per-shard lists (the N > 1 step's merge for nparts * k * 8 B <= 64 KiB):
+// one work-group per (query, part) instead of one per query (128 work-groups on 256 CUs in the
+// bench), every part of the query staged in LDS, and each key of the block's own part placed
+// directly at its merged rank = own index + #keys below it in every other part (binary
+// searches in LDS; keys are unique: (score key << 32) | global id).  Same output and status as
+// merge_packed_tree_kernel.  Padding keys (~0) are skipped; part 0's block writes the pad tail
+// (merged count T < k) and the status.
+constexpr int kRankThreads = 1024;
+constexpr int kRankMaxParts = 8;
+constexpr int kRankLds = 64 * 1024;
+__global__ __launch_bounds__(kRankThreads) void merge_packed_rank_kernel(const uint64_t* parts, int64_t nq,
+                                                                         int nparts, int k, int64_t n_global,
+                                                                         float* out_s, int64_t* out_i,
+                                                                         int32_t* status) {
+  extern __shared__ __attribute__((aligned(16))) uint64_t P[];   // [nparts][k]
+  __shared__ int cnt[kRankMaxParts];
+  __shared__ int bad;
+  const int tid = threadIdx.x;
+  const int64_t q = blockIdx.x / nparts;
+  const int me = (int)(blockIdx.x % nparts);
+  const int64_t ps = (int64_t)(k + 1);
+  if (tid == 0) bad = 0;
+  {
+    // all loads of the fill in flight at once (clamped addresses, then select; nparts * k <= 8192)
+    constexpr int E = kRankLds / 8 / kRankThreads;
+    uint64_t tmp[E];
+#pragma unroll
+    for (int t = 0; t < E; ++t) {
+      const int e = tid + t * kRankThreads;
+      const bool ok = e < nparts * k;
+      const int l = ok ? e / k : 0, i = ok ? e - l * k : 0;
+      tmp[t] = parts[((int64_t)l * nq + q) * ps + i];
+    }
+#pragma unroll
+    for (int t = 0; t < E; ++t) {
+      const int e = tid + t * kRankThreads;
+      if (e < nparts * k) P[e] = tmp[t];
+    }
+  }
+  __syncthreads();
+  // valid (non-pad) count of every part: first ~0 key (lists are sorted ascending)
+  if (tid < nparts) {
+    const uint64_t* L = P + tid * k;
+    int lo = 0, hi = k;
+    while (lo < hi) {
+      const int mid = (lo + hi) >> 1;
+      if (L[mid] != ~0ull) lo = mid + 1;
+      else hi = mid;
+    }
+    cnt[tid] = lo;
+    if (parts[((int64_t)tid * nq + q) * ps + k] & 1ull) atomicOr(&bad, 1);
+  }
+  __syncthreads();
+  int c[kRankMaxParts];
+#pragma unroll
+  for (int l = 0; l < kRankMaxParts; ++l) c[l] = (l < nparts && l != me) ? cnt[l] : 0;
+  const uint64_t* mine = P + me * k;
+  for (int i = tid; i < cnt[me]; i += kRankThreads) {
+    const uint64_t x = mine[i];
+    // branch-free lower bounds in all other parts at once: the kRankMaxParts searches
+    // advance in lock step, so their LDS reads overlap instead of forming one long chain
+    int base[kRankMaxParts], len[kRankMaxParts];
+#pragma unroll
+    for (int l = 0; l < kRankMaxParts; ++l) {
+      base[l] = 0;
+      len[l] = c[l];
+    }
+    for (int step = 0; step < 12; ++step) {
+#pragma unroll
+      for (int l = 0; l < kRankMaxParts; ++l) {
+        if (len[l] > 1) {
+          const int half = len[l] >> 1;
+          base[l] = P[l * k + base[l] + half - 1] < x ? base[l] + half : base[l];
+          len[l] -= half;
+        }
+      }
+    }
+    int rank = i;
+#pragma unroll
+    for (int l = 0; l < kRankMaxParts; ++l)
+      rank += base[l] + ((len[l] == 1 && P[l * k + base[l]] < x) ? 1 : 0);
+    if (rank < k) {
+      out_s[q * k + rank] = desc_key_to_score((uint32_t)(x >> 32));
+      out_i[q * k + rank] = (int64_t)(x & 0xFFFFFFFFull);
+    }
+  }
+  if (me == 0) {
+    int tot = 0;
+    for (int l = 0; l < nparts; ++l) tot += cnt[l];
+    for (int i = tot + tid; i < k; i += kRankThreads) {
+      out_s[q * k + i] = kPadScore;
+      out_i[q * k + i] = -1;
+    }
+    if (status && tid == 0) status[q] = (bad || (tot < k && n_global >= (int64_t)k)) ? 1 : 0;
+  }
+}
+
+static int g_merge_variant = 0;   // 0 auto, 1 tree, 2 rank (tests / benchmarks)
+
 // Merge of packed per-shard lists [nparts][nq][k + 1] (sorted u64 keys, entry k =
 // flags) into (score, id) [nq][k]; status[q] = 1 unless exact: the k-th merged
 // entry is real (>= k candidates over all shards, so the global tau was <= the
@@ -2170,6 +2269,13 @@ int drt_ip_topk_dist_filter(const void* Q, int64_t nq, const void* P, int64_t n_
   return launch_select(sa, SEL_KEYS64, SEL_TOPK, s);
 }
 
+// Test / benchmark switch of drt_topk_merge_packed: 0 automatic, 1 tree merge, 2 rank merge (where it fits).
+int drt_topk_merge_packed_variant(int32_t v) {
+  if (v < 0 || v > 2) return DRT_EINVAL;
+  g_merge_variant = v;
+  return DRT_OK;
+}
+
 int drt_topk_merge_packed(const uint64_t* parts, int64_t nq, int32_t nparts, int32_t k, int64_t n_global,
                           float* out_scores, int64_t* out_ids, int32_t* status, void* stream) {
   DRT_REQUIRE(nq >= 0 && nparts >= 1 && nparts <= 4096 && k >= 1 && k <= kSelMaxK && n_global >= 0);
@@ -2183,7 +2289,18 @@ int drt_topk_merge_packed(const uint64_t* parts, int64_t nq, int32_t nparts, int
   while (kp < k) kp <<= 1;
   const size_t lds = (size_t)p2 * kp * 8;
   int rc = DRT_OK;
-  if (nparts > 1 && (p2 / 2) * kp <= kTreeMaxE * kTreeThreads && lds <= 128 * 1024) {
+  const size_t rank_lds = (size_t)nparts * k * 8;
+  const bool rank_ok = nparts <= kRankMaxParts && rank_lds <= (size_t)kRankLds;
+  if (rank_ok && g_merge_variant != 1 && (g_merge_variant == 2 || nparts > 1)) {
+    static bool attr_set = false;
+    if (!attr_set) {
+      DRT_CHECK_HIP(hipFuncSetAttribute((const void*)merge_packed_rank_kernel,
+                                        hipFuncAttributeMaxDynamicSharedMemorySize, kRankLds));
+      attr_set = true;
+    }
+    hipLaunchKernelGGL(merge_packed_rank_kernel, dim3((unsigned)(nq * nparts)), dim3(kRankThreads), rank_lds, s,
+                       parts, nq, (int)nparts, (int)k, n_global, out_scores, out_ids, status);
+  } else if (nparts > 1 && (p2 / 2) * kp <= kTreeMaxE * kTreeThreads && lds <= 128 * 1024) {
 #define DRT_TREE(KPV)                                                                                        \
   {                                                                                                          \
     static bool attr_set = false;                                                                            \

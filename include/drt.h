@@ -114,6 +114,10 @@ int drt_ip_topk_dist_filter(const void* Q, int64_t nq, const void* P, int64_t n_
 int drt_topk_merge_packed(const uint64_t* parts, int64_t nq, int32_t nparts, int32_t k,
                           int64_t n_global, float* out_scores, int64_t* out_ids, int32_t* status,
                           void* stream);
+/* Test / benchmark switch of drt_topk_merge_packed's kernel: 0 automatic (rank merge, one
+ * work-group per (query, part), when nparts * k * 8 B <= 64 KiB; else the per-query bitonic tree
+ * merge), 1 tree merge, 2 rank merge wherever it fits.  Same results for every setting.     */
+int drt_topk_merge_packed_variant(int32_t v);
 
 /* Dense score matrix C[m, n] = A[m, d] . B[n, d]^T with fp32 accumulation
  * (torch.matmul(q_reps, p_reps.T), biencoder.py:107).  A, B bf16; C fp32 with

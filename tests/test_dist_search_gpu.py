@@ -122,3 +122,34 @@ def test_dist_shape_errors(dev):
     with pytest.raises(ValueError):
         kernels.dist_tau(torch.zeros((400, 2, kernels.sample_rank(1000)), dtype=torch.int32, device=dev), 1000)
     assert kernels.sample_rank(1000) == orc.sample_rank(1000)
+
+
+@pytest.mark.parametrize("nparts,nq,k,fill", [(8, 128, 1000, 0.5), (2, 5, 2048, 1.0), (3, 7, 100, 0.0),
+                                              (5, 9, 10, 0.3), (9, 4, 1000, 0.4), (16, 3, 1000, 0.2),
+                                              (8, 2, 1000, 0.05), (1, 6, 64, 0.7)])
+def test_merge_packed_variants_vs_oracle(dev, nparts, nq, k, fill):
+    """drt_topk_merge_packed's rank merge (one work-group per (query, part)) and tree merge against
+    the oracle on random packed lists: unique keys, ragged fills, empty parts, overflow flags."""
+    import torch
+    from denseretrievaltoolkits_amd import _native, kernels
+    lib = _native.load()
+    rng = np.random.default_rng(nparts * 1000 + k)
+    parts = np.full((nparts, nq, k + 1), np.iinfo(np.uint64).max, dtype=np.uint64)
+    n_global = nparts * k * 4
+    for q in range(nq):
+        ids = rng.permutation(n_global)[: nparts * k].astype(np.uint64)
+        sc = rng.integers(0, 1 << 20, size=nparts * k).astype(np.uint64)   # ties across parts, ids break them
+        keys = (sc << np.uint64(32)) | ids
+        for l in range(nparts):
+            cnt = int(rng.binomial(k, fill)) if fill < 1.0 else k
+            parts[l, q, :cnt] = np.sort(keys[l * k: l * k + cnt])
+            parts[l, q, k] = np.uint64(rng.random() < 0.1)            # overflow flag
+    es, ei, est = orc.merge_packed(parts, k, n_global)
+    pt = torch.from_numpy(parts.view(np.int64)).to(dev)
+    for v in (0, 1, 2):
+        _native.check(lib.drt_topk_merge_packed_variant(v), "variant")
+        s, i, st = kernels.merge_packed(pt, k, n_global)
+        np.testing.assert_array_equal(i.cpu().numpy(), ei, err_msg=f"variant {v}")
+        np.testing.assert_array_equal(s.cpu().numpy(), es, err_msg=f"variant {v}")
+        np.testing.assert_array_equal(st.cpu().numpy(), est, err_msg=f"variant {v}")
+    lib.drt_topk_merge_packed_variant(0)
