@@ -131,6 +131,8 @@ struct AttnArgs {
   int64_t B, L;
   int heads, H;
   float scale;            // 1/sqrt(dh): applied to Q (exact for dh = 64)
+  float* lse;             // optional [B][heads][L]: log-sum-exp of each query's scaled, masked
+                          // scores (what the attention backward needs to rebuild P)
 };
 
 __global__ __launch_bounds__(kAttnThreads, 4) void attention_kernel(AttnArgs a) {
@@ -278,6 +280,7 @@ __global__ __launch_bounds__(kAttnThreads, 4) void attention_kernel(AttnArgs a) 
     }
     // O^T[d][q]: lane holds query r; d = 32t + (e&3) + 8(e>>2) + 4h
     const int q = qb * 32 + r;
+    if (q < L && a.lse && h == 0) a.lse[((int64_t)b * a.heads + hd) * L + q] = m + __logf(l);
     if (q < L) {
       const float inv = 1.0f / l;
       __bf16* orow = a.ctx + (row0 + q) * a.H + hd * kHeadDim;
@@ -407,12 +410,20 @@ int drt_layernorm_bf16(const void* X, int64_t M, int32_t H, const float* gamma, 
   return hip_status(hipGetLastError());
 }
 
+int drt_attention_fwd_lse_bf16(const void* qkv, const int64_t* mask, void* ctx, float* lse, int64_t B, int64_t L,
+                               int32_t heads, int32_t head_dim, float scale, void* stream);
+
 int drt_attention_bf16(const void* qkv, const int64_t* mask, void* ctx, int64_t B, int64_t L, int32_t heads,
                        int32_t head_dim, float scale, void* stream) {
+  return drt_attention_fwd_lse_bf16(qkv, mask, ctx, nullptr, B, L, heads, head_dim, scale, stream);
+}
+
+int drt_attention_fwd_lse_bf16(const void* qkv, const int64_t* mask, void* ctx, float* lse, int64_t B, int64_t L,
+                               int32_t heads, int32_t head_dim, float scale, void* stream) {
   DRT_REQUIRE(B >= 0 && L > 0 && L <= kMaxSeq && heads > 0 && head_dim == kHeadDim);
   if (B == 0) return DRT_OK;
   DRT_REQUIRE(qkv && ctx);
-  AttnArgs a{(const __bf16*)qkv, mask, (__bf16*)ctx, B, L, heads, heads * head_dim, scale};
+  AttnArgs a{(const __bf16*)qkv, mask, (__bf16*)ctx, B, L, heads, heads * head_dim, scale, lse};
   const int Lp = ((int)L + 31) & ~31;
   const size_t lds = (size_t)Lp * 128 + (size_t)64 * (Lp * 2 + 8) + (size_t)Lp * 4;
   static bool attr_set = false;

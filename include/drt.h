@@ -166,6 +166,34 @@ int drt_layernorm_bf16(const void* X, int64_t M, int32_t H, const float* gamma,
                        const float* beta, float eps, void* out, void* stream);
 int drt_attention_bf16(const void* qkv, const int64_t* mask, void* ctx, int64_t B, int64_t L,
                        int32_t heads, int32_t head_dim, float scale, void* stream);
+/* drt_attention_fwd_lse_bf16: the same forward, also writing lse [B][heads][L] fp32 = the
+ * log-sum-exp of each query's scaled, masked scores (input of the attention backward).  */
+int drt_attention_fwd_lse_bf16(const void* qkv, const int64_t* mask, void* ctx, float* lse, int64_t B,
+                               int64_t L, int32_t heads, int32_t head_dim, float scale, void* stream);
+
+/* ------------------------------------------------------------------------
+ * Encoder backward building blocks (the gradient of HF BertModel's
+ * ops as the training step of run_random_sampling.py takes it under autograd,
+ * DRT/trainer/trainer.py:113-133; transformers modeling_bert.py:282-352).
+ * ------------------------------------------------------------------------
+ * drt_layernorm_bwd_bf16: dx [M,H] bf16 = LN backward of dy through LN(x) with gamma (x = the
+ *   bf16 pre-LN sums the forward stored; statistics recomputed) + dres (residual gradient or
+ *   NULL); dgamma / dbeta fp32 [H], deterministic (fixed-order partial sums in ws of
+ *   drt_layernorm_bwd_workspace(M, H) bytes).  H % 256 == 0, H <= 1024.
+ * drt_colsum_bf16: out[n] fp32 = sum_rows x[row][n] (bias gradients), fixed order, ws of
+ *   drt_colsum_workspace(M, N) bytes (0 for M < 256).
+ * drt_gelu_bwd_bf16: dx = dy * (Phi(x) + x phi(x)) for the erf GELU (pre = the FFN1
+ *   pre-activation), n elements.
+ * drt_transpose_bf16: y [C,R] = x [R,C]^T (operand layout for the weight gradients).      */
+size_t drt_layernorm_bwd_workspace(int64_t M, int32_t H);
+int drt_layernorm_bwd_bf16(const void* dy, const void* x, const float* gamma, float eps, int64_t M,
+                           int32_t H, const void* dres, void* dx, float* dgamma, float* dbeta,
+                           void* ws, size_t ws_bytes, void* stream);
+size_t drt_colsum_workspace(int64_t M, int64_t N);
+int drt_colsum_bf16(const void* x, int64_t M, int64_t N, float* out, void* ws, size_t ws_bytes,
+                    void* stream);
+int drt_gelu_bwd_bf16(const void* dy, const void* pre, int64_t n, void* dx, void* stream);
+int drt_transpose_bf16(const void* x, int64_t R, int64_t C, void* y, void* stream);
 int drt_pool_bf16(const void* hidden, const int64_t* mask, int64_t B, int64_t L, int32_t H,
                   int32_t mode, float* out, void* out_bf16, void* stream);
 int drt_l2_normalize_f32(float* x, int64_t B, int32_t H, void* out_bf16, void* stream);

@@ -1,0 +1,114 @@
+"""GPU: encoder backward building blocks against torch fp32 autograd of the
+same forward ops (HF BertModel's LayerNorm / GELU / Linear bias / attention softmax,
+transformers modeling_bert.py:164-204, 282-352) on the same bf16 inputs."""
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.mark.parametrize("M,H,resid", [(1000, 768, True), (37, 256, False), (4096, 1024, True), (3, 512, False)])
+def test_layernorm_bwd_vs_torch(dev, M, H, resid):
+    import torch
+    from denseretrievaltoolkits_amd import _native
+    lib = _native.load()
+    g = torch.Generator(device=dev).manual_seed(M + H)
+    x = (2.0 * torch.randn(M, H, generator=g, device=dev) + 0.3).to(torch.bfloat16)
+    gamma = 1.0 + 0.2 * torch.randn(H, generator=g, device=dev)
+    beta = 0.1 * torch.randn(H, generator=g, device=dev)
+    dy = torch.randn(M, H, generator=g, device=dev).to(torch.bfloat16)
+    dres = torch.randn(M, H, generator=g, device=dev).to(torch.bfloat16) if resid else None
+    xf = x.float().requires_grad_(True)
+    gf = gamma.clone().requires_grad_(True)
+    bf = beta.clone().requires_grad_(True)
+    torch.nn.functional.layer_norm(xf, (H,), gf, bf, 1e-12).backward(dy.float())
+    ref_dx = xf.grad + (dres.float() if resid else 0.0)
+    nb = int(lib.drt_layernorm_bwd_workspace(M, H))
+    ws = torch.empty((nb + 3) // 4, dtype=torch.float32, device=dev)
+    dx = torch.empty(M, H, dtype=torch.bfloat16, device=dev)
+    dgam = torch.empty(H, device=dev)
+    dbet = torch.empty(H, device=dev)
+    _native.check(lib.drt_layernorm_bwd_bf16(dy.data_ptr(), x.data_ptr(), gamma.data_ptr(), 1e-12, M, H,
+                                             dres.data_ptr() if resid else None, dx.data_ptr(), dgam.data_ptr(),
+                                             dbet.data_ptr(), ws.data_ptr(), nb, _native.stream_ptr(dev)), "ln bwd")
+    torch.testing.assert_close(dx.float(), ref_dx, atol=3e-2, rtol=1e-2)
+    torch.testing.assert_close(dgam, gf.grad, atol=1e-3 * max(1.0, M ** 0.5), rtol=1e-4)
+    torch.testing.assert_close(dbet, bf.grad, atol=1e-3 * max(1.0, M ** 0.5), rtol=1e-4)
+    # deterministic: a second run gives identical bits
+    dgam2 = torch.empty(H, device=dev)
+    _native.check(lib.drt_layernorm_bwd_bf16(dy.data_ptr(), x.data_ptr(), gamma.data_ptr(), 1e-12, M, H,
+                                             dres.data_ptr() if resid else None, dx.data_ptr(), dgam2.data_ptr(),
+                                             dbet.data_ptr(), ws.data_ptr(), nb, _native.stream_ptr(dev)), "ln bwd")
+    assert torch.equal(dgam, dgam2)
+
+
+@pytest.mark.parametrize("M,N", [(65536, 768), (300, 3072), (1, 64), (255, 100), (5000, 2304)])
+def test_colsum_bias_grad_vs_torch(dev, M, N):
+    import torch
+    from denseretrievaltoolkits_amd import _native
+    lib = _native.load()
+    x = torch.randn(M, N, generator=torch.Generator(device=dev).manual_seed(M), device=dev).to(torch.bfloat16)
+    nb = int(lib.drt_colsum_workspace(M, N))
+    ws = torch.empty(max(1, (nb + 3) // 4), dtype=torch.float32, device=dev)
+    out = torch.empty(N, device=dev)
+    _native.check(lib.drt_colsum_bf16(x.data_ptr(), M, N, out.data_ptr(), ws.data_ptr(), nb,
+                                      _native.stream_ptr(dev)), "colsum")
+    torch.testing.assert_close(out, x.float().sum(0), atol=1e-3 * M ** 0.5, rtol=1e-5)
+
+
+@pytest.mark.parametrize("n", [65536 * 3072 // 64, 1001, 7])
+def test_gelu_bwd_vs_torch(dev, n):
+    import torch
+    from denseretrievaltoolkits_amd import _native
+    lib = _native.load()
+    g = torch.Generator(device=dev).manual_seed(n)
+    pre = (3.0 * torch.randn(n, generator=g, device=dev)).to(torch.bfloat16)
+    dy = torch.randn(n, generator=g, device=dev).to(torch.bfloat16)
+    xf = pre.float().requires_grad_(True)
+    torch.nn.functional.gelu(xf).backward(dy.float())
+    dx = torch.empty(n, dtype=torch.bfloat16, device=dev)
+    _native.check(lib.drt_gelu_bwd_bf16(dy.data_ptr(), pre.data_ptr(), n, dx.data_ptr(), _native.stream_ptr(dev)),
+                  "gelu bwd")
+    torch.testing.assert_close(dx.float(), xf.grad, atol=1e-2, rtol=1e-2)
+
+
+@pytest.mark.parametrize("R,C", [(65536, 768), (100, 3072), (1, 1), (129, 65)])
+def test_transpose_bf16(dev, R, C):
+    import torch
+    from denseretrievaltoolkits_amd import _native
+    lib = _native.load()
+    x = torch.randn(R, C, device=dev).to(torch.bfloat16)
+    y = torch.empty(C, R, dtype=torch.bfloat16, device=dev)
+    _native.check(lib.drt_transpose_bf16(x.data_ptr(), R, C, y.data_ptr(), _native.stream_ptr(dev)), "transpose")
+    assert torch.equal(y, x.t().contiguous())
+
+
+@pytest.mark.parametrize("B,L", [(4, 128), (3, 50), (2, 512), (5, 32)])
+def test_attention_lse_vs_torch(dev, B, L):
+    """drt_attention_fwd_lse_bf16: ctx unchanged vs drt_attention_bf16, and the per-query
+    log-sum-exp of the scaled, key-masked scores against torch fp32 on the same bf16 q/k."""
+    import torch
+    from denseretrievaltoolkits_amd import _native
+    lib = _native.load()
+    heads, dh = 12, 64
+    H = heads * dh
+    g = torch.Generator(device=dev).manual_seed(B * L)
+    qkv = torch.randn(B * L, 3 * H, generator=g, device=dev).to(torch.bfloat16)
+    lens = torch.randint(1, L + 1, (B,), generator=g, device=dev)
+    mask = (torch.arange(L, device=dev)[None, :] < lens[:, None]).to(torch.int64)
+    ctx0 = torch.empty(B * L, H, dtype=torch.bfloat16, device=dev)
+    ctx1 = torch.empty_like(ctx0)
+    lse = torch.empty(B, heads, L, device=dev)
+    s = _native.stream_ptr(dev)
+    scale = 1.0 / dh ** 0.5
+    _native.check(lib.drt_attention_bf16(qkv.data_ptr(), mask.data_ptr(), ctx0.data_ptr(), B, L, heads, dh, scale, s), "a")
+    _native.check(lib.drt_attention_fwd_lse_bf16(qkv.data_ptr(), mask.data_ptr(), ctx1.data_ptr(), lse.data_ptr(), B, L,
+                                                 heads, dh, scale, s), "lse")
+    assert torch.equal(ctx0, ctx1)
+    q = qkv[:, :H].float().view(B, L, heads, dh).transpose(1, 2)
+    k = qkv[:, H:2 * H].float().view(B, L, heads, dh).transpose(1, 2)
+    qs = (q * scale).to(torch.bfloat16).float()          # the kernel scales Q in bf16 (exact for dh = 64)
+    sc = qs @ k.transpose(-1, -2)
+    sc = sc + ((1 - mask[:, None, None, :].float()) * torch.finfo(torch.float32).min)
+    ref = torch.logsumexp(sc, -1)
+    torch.testing.assert_close(lse, ref, atol=1e-3, rtol=1e-4)
