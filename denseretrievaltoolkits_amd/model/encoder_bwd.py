@@ -1,0 +1,113 @@
+"""Backward building blocks of the HIP encoder tower (in progress).
+
+The training step of run_random_sampling.py (DRT/trainer/trainer.py:113-133) differentiates
+HF ``BertModel`` under autograd; these functions restate the gradients of its ops on the HIP
+kernels for the bf16 activations the HIP forward stores:
+
+* ``linear_backward``   nn.Linear: dX = dY W (the NT GEMM against a transposed weight copy),
+                        dW = dY^T X (both operands transposed to k-contiguous rows, then the
+                        split-K NT GEMM with fp32 output), db = column sums of dY;
+* ``layernorm_backward`` / ``gelu_backward`` / ``attention_forward_lse``: thin wrappers of the
+                        C-ABI entries (include/drt.h).
+
+Assembling the tower backward (with attention backward and dropout masks) is the next step;
+until then training keeps the HF module under torch-ROCm autograd (biencoder.py).
+"""
+from __future__ import annotations
+
+from typing import Optional, Tuple
+
+import torch
+
+from .. import _native
+
+
+def _ws(nbytes: int, dev) -> Optional[torch.Tensor]:
+    return torch.empty((nbytes + 3) // 4, dtype=torch.float32, device=dev) if nbytes else None
+
+
+def _ptr(t: Optional[torch.Tensor]):
+    return t.data_ptr() if t is not None else None
+
+
+def transpose_bf16(x: torch.Tensor, cols_pad: int = 0) -> torch.Tensor:
+    """x [R, C] bf16 -> x^T [C, R + pad] with zero padding columns (k-contiguous GEMM operand)."""
+    lib = _native.load()
+    R, C = x.shape
+    y = torch.empty((C, R + cols_pad), dtype=torch.bfloat16, device=x.device)
+    if cols_pad:
+        y[:, R:].zero_()
+        tmp = torch.empty((C, R), dtype=torch.bfloat16, device=x.device)
+        _native.check(lib.drt_transpose_bf16(x.data_ptr(), R, C, tmp.data_ptr(), _native.stream_ptr(x.device)),
+                      "drt_transpose_bf16")
+        y[:, :R] = tmp
+        return y
+    _native.check(lib.drt_transpose_bf16(x.data_ptr(), R, C, y.data_ptr(), _native.stream_ptr(x.device)),
+                  "drt_transpose_bf16")
+    return y
+
+
+def colsum(x: torch.Tensor) -> torch.Tensor:
+    lib = _native.load()
+    M, N = x.shape
+    out = torch.empty(N, dtype=torch.float32, device=x.device)
+    nb = int(lib.drt_colsum_workspace(M, N))
+    ws = _ws(nb, x.device)
+    _native.check(lib.drt_colsum_bf16(x.data_ptr(), M, N, out.data_ptr(), _ptr(ws), nb,
+                                      _native.stream_ptr(x.device)), "drt_colsum_bf16")
+    return out
+
+
+def linear_backward(dy: torch.Tensor, x: torch.Tensor, w_t: torch.Tensor, want_dx: bool = True
+                    ) -> Tuple[Optional[torch.Tensor], torch.Tensor, torch.Tensor]:
+    """Gradients of y = x W^T + b (nn.Linear, W [N, K]) for dy [T, N], x [T, K] (bf16 CUDA),
+    given w_t = W^T [K, N] bf16.  Returns (dx bf16 [T, K] or None, dW fp32 [N, K], db fp32 [N])."""
+    lib = _native.load()
+    dev = dy.device
+    s = _native.stream_ptr(dev)
+    T, N = dy.shape
+    K = x.shape[1]
+    if N % 64 or K % 64:
+        raise ValueError("linear_backward: feature sizes must be multiples of 64")
+    dx = None
+    if want_dx:
+        dx = torch.empty((T, K), dtype=torch.bfloat16, device=dev)
+        nb = int(lib.drt_linear_workspace(T, K, N))
+        ws = _ws(nb, dev)
+        _native.check(lib.drt_linear_bf16_ws(dy.data_ptr(), w_t.data_ptr(), None, None, dx.data_ptr(), T, K, N, 0,
+                                             _ptr(ws), nb, s), "dgrad")
+    pad = (-T) % 64
+    dyT = transpose_bf16(dy, pad)        # [N, T64]
+    xT = transpose_bf16(x, pad)          # [K, T64]
+    T64 = T + pad
+    dW = torch.empty((N, K), dtype=torch.float32, device=dev)
+    nb = int(lib.drt_linear_workspace(N, K, T64))
+    ws = _ws(nb, dev)
+    _native.check(lib.drt_linear_bf16_ws(dyT.data_ptr(), xT.data_ptr(), None, None, dW.data_ptr(), N, K, T64, 2,
+                                         _ptr(ws), nb, s), "wgrad")
+    return dx, dW, colsum(dy)
+
+
+def layernorm_backward(dy: torch.Tensor, x: torch.Tensor, gamma: torch.Tensor, eps: float,
+                       dres: Optional[torch.Tensor] = None):
+    """(dx bf16 [M, H], dgamma fp32 [H], dbeta fp32 [H]) of out = LN(x) (x = the bf16 pre-LN sums)."""
+    lib = _native.load()
+    M, H = x.shape
+    dev = x.device
+    dx = torch.empty((M, H), dtype=torch.bfloat16, device=dev)
+    dg = torch.empty(H, dtype=torch.float32, device=dev)
+    db = torch.empty(H, dtype=torch.float32, device=dev)
+    nb = int(lib.drt_layernorm_bwd_workspace(M, H))
+    ws = _ws(nb, dev)
+    _native.check(lib.drt_layernorm_bwd_bf16(dy.data_ptr(), x.data_ptr(), gamma.data_ptr(), float(eps), M, H,
+                                             _ptr(dres), dx.data_ptr(), dg.data_ptr(), db.data_ptr(), _ptr(ws), nb,
+                                             _native.stream_ptr(dev)), "drt_layernorm_bwd_bf16")
+    return dx, dg, db
+
+
+def gelu_backward(dy: torch.Tensor, pre: torch.Tensor) -> torch.Tensor:
+    lib = _native.load()
+    dx = torch.empty_like(dy)
+    _native.check(lib.drt_gelu_bwd_bf16(dy.data_ptr(), pre.data_ptr(), dy.numel(), dx.data_ptr(),
+                                        _native.stream_ptr(dy.device)), "drt_gelu_bwd_bf16")
+    return dx

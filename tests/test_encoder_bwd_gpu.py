@@ -1,7 +1,6 @@
 """GPU: encoder backward building blocks against torch fp32 autograd of the
 same forward ops (HF BertModel's LayerNorm / GELU / Linear bias / attention softmax,
 transformers modeling_bert.py:164-204, 282-352) on the same bf16 inputs."""
-import numpy as np
 import pytest
 
 pytestmark = pytest.mark.gpu
@@ -112,3 +111,25 @@ def test_attention_lse_vs_torch(dev, B, L):
     sc = sc + ((1 - mask[:, None, None, :].float()) * torch.finfo(torch.float32).min)
     ref = torch.logsumexp(sc, -1)
     torch.testing.assert_close(lse, ref, atol=1e-3, rtol=1e-4)
+
+
+@pytest.mark.parametrize("T,N,K", [(16384, 768, 768), (4096, 3072, 768), (1000, 768, 3072), (130, 2304, 768)])
+def test_linear_backward_vs_torch(dev, T, N, K):
+    """nn.Linear backward on the HIP kernels (dgrad NT GEMM vs the transposed weight, wgrad =
+    transposes + split-K NT GEMM with fp32 output, bias = column sums) vs torch fp32 autograd."""
+    import torch
+    from denseretrievaltoolkits_amd.model.encoder_bwd import linear_backward
+    g = torch.Generator(device=dev).manual_seed(T + N + K)
+    x = torch.randn(T, K, generator=g, device=dev).to(torch.bfloat16)
+    w = (0.05 * torch.randn(N, K, generator=g, device=dev)).to(torch.bfloat16)
+    b = torch.randn(N, generator=g, device=dev)
+    dy = torch.randn(T, N, generator=g, device=dev).to(torch.bfloat16)
+    xf = x.float().requires_grad_(True)
+    wf = w.float().requires_grad_(True)
+    bf = b.clone().requires_grad_(True)
+    torch.nn.functional.linear(xf, wf, bf).backward(dy.float())
+    dx, dW, db = linear_backward(dy, x, w.t().contiguous())
+    torch.testing.assert_close(dx.float(), xf.grad, atol=3e-2, rtol=1e-2)
+    tol = 2e-3 * T ** 0.5
+    torch.testing.assert_close(dW, wf.grad, atol=tol, rtol=1e-3)
+    torch.testing.assert_close(db, bf.grad, atol=tol, rtol=1e-4)
