@@ -3,13 +3,14 @@
 // under autograd).  Each kernel restates the gradient of one forward op of
 // transformers modeling_bert.py (BertSelfOutput / BertOutput LayerNorm :282-352,
 // BertIntermediate GELU :325-337, nn.Linear bias) for the bf16 activations the HIP forward
-// stores; the tower-level assembly (and attention backward) is the next step.
+// stores; the tower-level assembly (with dropout masks) is the next step.
 //
 //   layernorm_bwd   dx = rstd (g - mean(g) - xhat mean(g xhat)),  g = dy * gamma,
 //                   (+ a residual gradient), per-block dgamma / dbeta partials
 //   colsum          out[n] = sum_rows x[row][n] in a fixed order (bias / LN parameter grads)
 //   gelu_bwd        dx = dy (Phi(x) + x phi(x))      (erf GELU, activations.py:70-90)
 //   transpose_bf16  y[c][r] = x[r][c]                 (operand layout for weight gradients)
+//   attention_bwd   dQ, dK, dV of softmax(Q K^T / sqrt(dh) + mask) V  (L <= 128)
 #include "drt_common.h"
 
 namespace drt {
@@ -158,6 +159,250 @@ __global__ __launch_bounds__(256) void transpose_bf16_kernel(const __bf16* x, in
   }
 }
 
+// ---------------------------------------------------------------------------
+// Attention backward (BertSelfAttention, modeling_bert.py:164-204, under autograd), one
+// work-group (4 waves) per (sequence, head), L <= 128, head_dim 64.  With Qs = scale * Q
+// (rounded to bf16 as the forward does), S = Qs K^T + key bias, P = exp(S - lse):
+//   Dv_q = sum_d dO[q][d] O[q][d];   dP = dO V^T;   dS = P (dP - Dv)
+//   dV = P^T dO;   dK = dS^T Qs;   dQ = scale * dS K.
+// LDS: Qs, K, V, dO row-major [Lp][64] (16-B chunk XOR (row >> 1) & 7, as the forward's
+// K image) and Qs^T, K^T, dO^T as [64][128] (chunk XOR (d & 15)), so every MFMA operand is
+// one conflict-free ds_read_b128 of a row; per-wave 32 x 32 scratch tiles (80-B rows) turn
+// the P / dS accumulators (rows in registers) into A operands.  Phase 1: wave w owns key
+// block w (dK, dV over all query blocks); phase 2: wave w owns query block w (dQ over all
+// key blocks, S and dP recomputed).  v_mfma_f32_32x32x16_bf16 throughout.
+// ---------------------------------------------------------------------------
+constexpr int kAbThreads = 256;
+constexpr int kAbMaxSeq = 128;
+constexpr int kAbRow = 128;               // bytes per [.][64] bf16 row
+constexpr int kAbTRow = 256;              // bytes per [64][128] transposed row
+constexpr int kAbScr = 80;                // bytes per scratch row (32 bf16 + 16 B pad)
+
+struct AttnBwdArgs {
+  const __bf16* qkv;     // [B*L][3H]
+  const __bf16* ctx;     // [B*L][H]  forward output O
+  const __bf16* dctx;    // [B*L][H]  dO
+  const float* lse;      // [B][heads][L]
+  const int64_t* mask;   // [B][L] or null
+  __bf16* dqkv;          // [B*L][3H]
+  int64_t B, L;
+  int heads, H;
+  float scale;
+};
+
+__device__ __forceinline__ int ab_rc(int row, int chunk) { return row * kAbRow + ((chunk ^ ((row >> 1) & 7)) << 4); }
+__device__ __forceinline__ int ab_tc(int d, int chunk) { return d * kAbTRow + ((chunk ^ (d & 15)) << 4); }
+
+__global__ __launch_bounds__(kAbThreads) void attention_bwd_kernel(AttnBwdArgs a) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int L = (int)a.L;
+  const int Lp = (L + 31) & ~31;
+  char* Qs = smem;                                   // [Lp][64]
+  char* Ks = Qs + Lp * kAbRow;
+  char* Vs = Ks + Lp * kAbRow;
+  char* Os = Vs + Lp * kAbRow;                       // dO
+  char* QT = Os + Lp * kAbRow;                       // [64][128]
+  char* KT = QT + 64 * kAbTRow;
+  char* OT = KT + 64 * kAbTRow;                      // dO^T
+  char* scr = OT + 64 * kAbTRow;                     // [4 waves][2][32][80 B]
+  float* lse = (float*)(scr + 4 * 2 * 32 * kAbScr);  // [Lp]
+  float* dv = lse + Lp;                              // [Lp]  Dv
+  float* kb = dv + Lp;                               // [Lp]  key bias
+
+  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+  const int r = lane & 31, h = lane >> 5;
+  const int64_t b = blockIdx.x / a.heads;
+  const int hd = blockIdx.x % a.heads;
+  const int64_t row0 = b * a.L;
+  const int64_t ld = 3 * (int64_t)a.H;
+  const __bf16* Qg = a.qkv + row0 * ld + hd * 64;
+  const __bf16* Kg = Qg + a.H;
+  const __bf16* Vg = Qg + 2 * a.H;
+  const __bf16* Og = a.ctx + row0 * a.H + hd * 64;
+  const __bf16* dOg = a.dctx + row0 * a.H + hd * 64;
+
+  // ---- staging: rows (row-major images) and the transposed images, element by element
+  for (int i = tid; i < Lp * 8; i += kAbThreads) {
+    const int row = i >> 3, c = i & 7;
+    bf16x8 q = {}, k = {}, v = {}, o = {}, oo = {};
+    if (row < L) {
+      q = *(const bf16x8*)(Qg + (int64_t)row * ld + c * 8);
+      k = *(const bf16x8*)(Kg + (int64_t)row * ld + c * 8);
+      v = *(const bf16x8*)(Vg + (int64_t)row * ld + c * 8);
+      o = *(const bf16x8*)(dOg + (int64_t)row * a.H + c * 8);
+      oo = *(const bf16x8*)(Og + (int64_t)row * a.H + c * 8);
+    }
+    float part = 0.f;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      q[j] = (__bf16)((float)q[j] * a.scale);
+      part += (float)o[j] * (float)oo[j];
+    }
+    *(bf16x8*)(Qs + ab_rc(row, c)) = q;
+    *(bf16x8*)(Ks + ab_rc(row, c)) = k;
+    *(bf16x8*)(Vs + ab_rc(row, c)) = v;
+    *(bf16x8*)(Os + ab_rc(row, c)) = o;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int d = c * 8 + j;
+      const int off = ab_tc(d, row >> 3) + (row & 7) * 2;
+      *(__bf16*)(QT + off) = q[j];
+      *(__bf16*)(KT + off) = k[j];
+      *(__bf16*)(OT + off) = o[j];
+    }
+    // Dv: the 8 chunk-partials of one row sit in 8 consecutive lanes
+    part += __shfl_xor(part, 1, 64);
+    part += __shfl_xor(part, 2, 64);
+    part += __shfl_xor(part, 4, 64);
+    if (c == 0) dv[row] = part;
+  }
+  for (int i = tid; i < Lp; i += kAbThreads) {
+    float bv = 0.0f;
+    if (i >= L) bv = -3.402823466e+38f;
+    else if (a.mask && a.mask[b * a.L + i] == 0) bv = -3.402823466e+38f;
+    kb[i] = bv;
+    lse[i] = i < L ? a.lse[((int64_t)b * a.heads + hd) * a.L + i] : 0.0f;
+  }
+  __syncthreads();
+
+  const int nblk = Lp / 32;
+  char* sP = scr + (wave * 2 + 0) * 32 * kAbScr;
+  char* sS = scr + (wave * 2 + 1) * 32 * kAbScr;
+
+  // ---- phase 1: dK, dV for key block kbk (rows = keys in the D layout, cols = q / d)
+  for (int kbk = wave; kbk < nblk; kbk += 4) {
+    f32x16 dK[2], dV[2];
+#pragma unroll
+    for (int t = 0; t < 2; ++t)
+#pragma unroll
+      for (int e = 0; e < 16; ++e) {
+        dK[t][e] = 0.f;
+        dV[t][e] = 0.f;
+      }
+    const int key = kbk * 32 + r;   // A-operand row of this lane
+    for (int qb = 0; qb < nblk; ++qb) {
+      const int qcol = qb * 32 + r; // B-operand column of this lane
+      f32x16 st = {}, dpt = {};
+#pragma unroll
+      for (int e = 0; e < 16; ++e) {
+        st[e] = 0.f;
+        dpt[e] = 0.f;
+      }
+#pragma unroll
+      for (int k4 = 0; k4 < 4; ++k4) {
+        const int c = 2 * k4 + h;
+        const bf16x8 ka = *(const bf16x8*)(Ks + ab_rc(key, c));
+        const bf16x8 qbv = *(const bf16x8*)(Qs + ab_rc(qcol, c));
+        st = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ka, qbv, st, 0, 0, 0);
+        const bf16x8 va = *(const bf16x8*)(Vs + ab_rc(key, c));
+        const bf16x8 ob = *(const bf16x8*)(Os + ab_rc(qcol, c));
+        dpt = __builtin_amdgcn_mfma_f32_32x32x16_bf16(va, ob, dpt, 0, 0, 0);
+      }
+      // P^T, dS^T: row = key kbk*32 + (e&3) + 8(e>>2) + 4h, column = query qcol
+      const float lq = lse[qcol], dq = dv[qcol];
+#pragma unroll
+      for (int e = 0; e < 16; ++e) {
+        const int kr = (e & 3) + 8 * (e >> 2) + 4 * h;
+        const float p = __expf(st[e] + kb[kbk * 32 + kr] - lq);
+        const float ds = p * (dpt[e] - dq);
+        *(__bf16*)(sP + kr * kAbScr + r * 2) = (__bf16)p;
+        *(__bf16*)(sS + kr * kAbScr + r * 2) = (__bf16)ds;
+      }
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks) {
+        const bf16x8 pa = *(const bf16x8*)(sP + r * kAbScr + (2 * ks + h) * 16);
+        const bf16x8 sa = *(const bf16x8*)(sS + r * kAbScr + (2 * ks + h) * 16);
+        const int qc = (qb * 32 + 16 * ks + 8 * h) >> 3;
+#pragma unroll
+        for (int t = 0; t < 2; ++t) {
+          const int d = 32 * t + r;
+          const bf16x8 ob = *(const bf16x8*)(OT + ab_tc(d, qc));
+          const bf16x8 qbt = *(const bf16x8*)(QT + ab_tc(d, qc));
+          dV[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(pa, ob, dV[t], 0, 0, 0);
+          dK[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(sa, qbt, dK[t], 0, 0, 0);
+        }
+      }
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+    }
+    // dK / dV [key][d]: row = key (regs), column d = 32 t + r (lanes)
+#pragma unroll
+    for (int e = 0; e < 16; ++e) {
+      const int kr = kbk * 32 + (e & 3) + 8 * (e >> 2) + 4 * h;
+      if (kr < L) {
+        __bf16* dst = a.dqkv + (row0 + kr) * ld + hd * 64;
+#pragma unroll
+        for (int t = 0; t < 2; ++t) {
+          dst[a.H + 32 * t + r] = (__bf16)dK[t][e];
+          dst[2 * a.H + 32 * t + r] = (__bf16)dV[t][e];
+        }
+      }
+    }
+  }
+
+  // ---- phase 2: dQ for query block qbq (rows = queries, cols = keys / d)
+  for (int qbq = wave; qbq < nblk; qbq += 4) {
+    f32x16 dQ[2];
+#pragma unroll
+    for (int t = 0; t < 2; ++t)
+#pragma unroll
+      for (int e = 0; e < 16; ++e) dQ[t][e] = 0.f;
+    const int qrow = qbq * 32 + r;
+    for (int kbk = 0; kbk < nblk; ++kbk) {
+      const int kcol = kbk * 32 + r;
+      f32x16 sv = {}, dp = {};
+#pragma unroll
+      for (int e = 0; e < 16; ++e) {
+        sv[e] = 0.f;
+        dp[e] = 0.f;
+      }
+#pragma unroll
+      for (int k4 = 0; k4 < 4; ++k4) {
+        const int c = 2 * k4 + h;
+        const bf16x8 qa = *(const bf16x8*)(Qs + ab_rc(qrow, c));
+        const bf16x8 kbv = *(const bf16x8*)(Ks + ab_rc(kcol, c));
+        sv = __builtin_amdgcn_mfma_f32_32x32x16_bf16(qa, kbv, sv, 0, 0, 0);
+        const bf16x8 oa = *(const bf16x8*)(Os + ab_rc(qrow, c));
+        const bf16x8 vb = *(const bf16x8*)(Vs + ab_rc(kcol, c));
+        dp = __builtin_amdgcn_mfma_f32_32x32x16_bf16(oa, vb, dp, 0, 0, 0);
+      }
+      const float kbias = kb[kcol];
+#pragma unroll
+      for (int e = 0; e < 16; ++e) {
+        const int qr = (e & 3) + 8 * (e >> 2) + 4 * h;
+        const int q = qbq * 32 + qr;
+        const float p = __expf(sv[e] + kbias - lse[q]);
+        *(__bf16*)(sS + qr * kAbScr + r * 2) = (__bf16)(p * (dp[e] - dv[q]));
+      }
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks) {
+        const bf16x8 sa = *(const bf16x8*)(sS + r * kAbScr + (2 * ks + h) * 16);
+        const int kc = (kbk * 32 + 16 * ks + 8 * h) >> 3;
+#pragma unroll
+        for (int t = 0; t < 2; ++t) {
+          const bf16x8 kt = *(const bf16x8*)(KT + ab_tc(32 * t + r, kc));
+          dQ[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(sa, kt, dQ[t], 0, 0, 0);
+        }
+      }
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+    }
+#pragma unroll
+    for (int e = 0; e < 16; ++e) {
+      const int qr = qbq * 32 + (e & 3) + 8 * (e >> 2) + 4 * h;
+      if (qr < L) {
+        __bf16* dst = a.dqkv + (row0 + qr) * ld + hd * 64;
+#pragma unroll
+        for (int t = 0; t < 2; ++t) dst[32 * t + r] = (__bf16)(dQ[t][e] * a.scale);
+      }
+    }
+  }
+}
+
 static int64_t colsum_slabs(int64_t M) { return M < 256 ? 1 : (M + 255) / 256 < 512 ? (M + 255) / 256 : 512; }
 
 template <typename T>
@@ -234,6 +479,29 @@ int drt_gelu_bwd_bf16(const void* dy, const void* pre, int64_t n, void* dx, void
   const int64_t blocks = (n + 2047) / 2048;
   hipLaunchKernelGGL(gelu_bwd_kernel, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream, (const __bf16*)dy,
                      (const __bf16*)pre, n, (__bf16*)dx);
+  return hip_status(hipGetLastError());
+}
+
+// dqkv [B*L][3H] (dQ | dK | dV, head-major like qkv) of the attention forward
+// (drt_attention_fwd_lse_bf16) given dctx = dO, the forward's ctx = O and lse.  L <= 128.
+int drt_attention_bwd_bf16(const void* qkv, const void* ctx, const void* dctx, const float* lse,
+                           const int64_t* mask, void* dqkv, int64_t B, int64_t L, int32_t heads, int32_t head_dim,
+                           float scale, void* stream) {
+  DRT_REQUIRE(B >= 0 && L > 0 && L <= kAbMaxSeq && heads > 0 && head_dim == 64);
+  if (B == 0) return DRT_OK;
+  DRT_REQUIRE(qkv && ctx && dctx && lse && dqkv);
+  AttnBwdArgs a{(const __bf16*)qkv, (const __bf16*)ctx, (const __bf16*)dctx, lse, mask, (__bf16*)dqkv, B, L,
+                heads, heads * 64, scale};
+  const int Lp = ((int)L + 31) & ~31;
+  const size_t lds = (size_t)4 * Lp * kAbRow + (size_t)3 * 64 * kAbTRow + (size_t)8 * 32 * kAbScr +
+                     (size_t)3 * Lp * 4;
+  static bool attr_set = false;
+  if (!attr_set) {
+    DRT_CHECK_HIP(hipFuncSetAttribute((const void*)attention_bwd_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                      160 * 1024));
+    attr_set = true;
+  }
+  hipLaunchKernelGGL(attention_bwd_kernel, dim3((unsigned)(B * heads)), dim3(kAbThreads), lds, (hipStream_t)stream, a);
   return hip_status(hipGetLastError());
 }
 

@@ -194,6 +194,12 @@ int drt_colsum_bf16(const void* x, int64_t M, int64_t N, float* out, void* ws, s
                     void* stream);
 int drt_gelu_bwd_bf16(const void* dy, const void* pre, int64_t n, void* dx, void* stream);
 int drt_transpose_bf16(const void* x, int64_t R, int64_t C, void* y, void* stream);
+/* drt_attention_bwd_bf16: dqkv [B*L, 3H] (dQ | dK | dV in qkv's packed layout) of the
+ * attention forward, from qkv, its ctx = O, dctx = dO, the forward's lse and the key mask;
+ * L <= 128, head_dim 64 (BertSelfAttention under autograd, modeling_bert.py:164-204).   */
+int drt_attention_bwd_bf16(const void* qkv, const void* ctx, const void* dctx, const float* lse,
+                           const int64_t* mask, void* dqkv, int64_t B, int64_t L, int32_t heads,
+                           int32_t head_dim, float scale, void* stream);
 int drt_pool_bf16(const void* hidden, const int64_t* mask, int64_t B, int64_t L, int32_t H,
                   int32_t mode, float* out, void* out_bf16, void* stream);
 int drt_l2_normalize_f32(float* x, int64_t B, int32_t H, void* out_bf16, void* stream);
