@@ -55,7 +55,7 @@ template <int EPL>
 __global__ __launch_bounds__(256) void embed_ln_kernel(const int64_t* ids, const int64_t* type_ids, int64_t T,
                                                        int64_t L, const float* wemb, const float* pemb,
                                                        const float* temb, const float* gamma, const float* beta,
-                                                       float eps, int H, __bf16* out) {
+                                                       float eps, int H, __bf16* out, __bf16* pre = nullptr) {
   const int lane = threadIdx.x & 63;
   const int64_t t = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
   if (t >= T) return;
@@ -74,8 +74,39 @@ __global__ __launch_bounds__(256) void embed_ln_kernel(const int64_t* ids, const
     const f32x4 d = *(const f32x4*)(y + c);
 #pragma unroll
     for (int u = 0; u < 4; ++u) x[e4 * 4 + u] = (a[u] + d[u]) + b[u];  // (word + type) + position, as HF
+    if (pre) {   // training forward: the pre-LN sum, input of the LayerNorm backward
+      bf16x4 o;
+#pragma unroll
+      for (int u = 0; u < 4; ++u) o[u] = (__bf16)x[e4 * 4 + u];
+      *(bf16x4*)(pre + t * H + c) = o;
+    }
   }
   ln_row<EPL>(x, gamma, beta, eps, lane, H, out + t * H);
+}
+
+// erf GELU, elementwise (the training forward keeps FFN1's pre-activation for the backward)
+__global__ __launch_bounds__(256) void gelu_kernel(const __bf16* x, int64_t n, __bf16* y) {
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i < n) {
+    const float v = (float)x[i];
+    y[i] = (__bf16)(0.5f * v * (1.0f + erff(v * 0.70710678118654752f)));
+  }
+}
+
+// Embedding backward (BertEmbeddings, modeling_bert.py:68-108): scatter-add of the gradient of
+// the pre-LN sum into the word / position / token-type tables (fp32 atomics; caller zeroes).
+__global__ __launch_bounds__(256) void embedding_bwd_kernel(const int64_t* ids, const int64_t* type_ids,
+                                                            const __bf16* d, int64_t T, int64_t L, int H,
+                                                            int64_t padding_idx, float* dword, float* dpos,
+                                                            float* dtype) {
+  const int64_t t = (int64_t)blockIdx.x;
+  const int64_t id = ids[t], pos = t % L, tt = type_ids ? type_ids[t] : 0;
+  for (int c = threadIdx.x; c < H; c += 256) {
+    const float g = (float)d[t * H + c];
+    if (id != padding_idx) atomicAdd(dword + id * H + c, g);   // nn.Embedding(padding_idx): row stays 0
+    atomicAdd(dpos + pos * H + c, g);
+    atomicAdd(dtype + tt * H + c, g);
+  }
 }
 
 template <int EPL>
@@ -355,22 +386,56 @@ using namespace drt;
 
 extern "C" {
 
+int drt_embed_ln_pre(const int64_t* ids, const int64_t* type_ids, int64_t B, int64_t L, const float* word_emb,
+                     const float* pos_emb, const float* type_emb, const float* gamma, const float* beta, float eps,
+                     int32_t H, void* out, void* pre, void* stream);
+
+int drt_gelu_bf16(const void* x, int64_t n, void* y, void* stream) {
+  DRT_REQUIRE(n >= 0);
+  if (n == 0) return DRT_OK;
+  DRT_REQUIRE(x && y);
+  hipLaunchKernelGGL(gelu_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, (hipStream_t)stream,
+                     (const __bf16*)x, n, (__bf16*)y);
+  return hip_status(hipGetLastError());
+}
+
+int drt_embedding_bwd(const int64_t* ids, const int64_t* type_ids, const void* d, int64_t B, int64_t L, int32_t H,
+                      int64_t padding_idx, float* dword, float* dpos, float* dtype, void* stream) {
+  DRT_REQUIRE(B >= 0 && L > 0 && H > 0);
+  if (B == 0) return DRT_OK;
+  DRT_REQUIRE(ids && d && dword && dpos && dtype);
+  hipLaunchKernelGGL(embedding_bwd_kernel, dim3((unsigned)(B * L)), dim3(256), 0, (hipStream_t)stream, ids, type_ids,
+                     (const __bf16*)d, B * L, L, (int)H, padding_idx, dword, dpos, dtype);
+  return hip_status(hipGetLastError());
+}
+
 int drt_embed_ln(const int64_t* ids, const int64_t* type_ids, int64_t B, int64_t L, const float* word_emb,
                  const float* pos_emb, const float* type_emb, const float* gamma, const float* beta, float eps,
                  int32_t H, void* out, void* stream) {
+  return drt_embed_ln_pre(ids, type_ids, B, L, word_emb, pos_emb, type_emb, gamma, beta, eps, H, out, nullptr, stream);
+}
+
+int drt_embed_ln_pre(const int64_t* ids, const int64_t* type_ids, int64_t B, int64_t L, const float* word_emb,
+                     const float* pos_emb, const float* type_emb, const float* gamma, const float* beta, float eps,
+                     int32_t H, void* out, void* pre, void* stream) {
   DRT_REQUIRE(B >= 0 && L > 0 && H > 0 && H % 256 == 0 && H <= 1024);
   const int64_t T = B * L;
   if (T == 0) return DRT_OK;
   DRT_REQUIRE(ids && word_emb && pos_emb && type_emb && gamma && beta && out);
   hipStream_t s = (hipStream_t)stream;
   dim3 grid((unsigned)((T + 3) / 4));
+  __bf16* o = (__bf16*)out;
+  __bf16* p = (__bf16*)pre;
+#define EMB(E) hipLaunchKernelGGL(embed_ln_kernel<E>, grid, dim3(256), 0, s, ids, type_ids, T, L, word_emb, pos_emb, \
+                                  type_emb, gamma, beta, eps, (int)H, o, p)
   switch (H / 64) {
-    case 4: hipLaunchKernelGGL(embed_ln_kernel<4>, grid, dim3(256), 0, s, ids, type_ids, T, L, word_emb, pos_emb, type_emb, gamma, beta, eps, H, (__bf16*)out); break;
-    case 8: hipLaunchKernelGGL(embed_ln_kernel<8>, grid, dim3(256), 0, s, ids, type_ids, T, L, word_emb, pos_emb, type_emb, gamma, beta, eps, H, (__bf16*)out); break;
-    case 12: hipLaunchKernelGGL(embed_ln_kernel<12>, grid, dim3(256), 0, s, ids, type_ids, T, L, word_emb, pos_emb, type_emb, gamma, beta, eps, H, (__bf16*)out); break;
-    case 16: hipLaunchKernelGGL(embed_ln_kernel<16>, grid, dim3(256), 0, s, ids, type_ids, T, L, word_emb, pos_emb, type_emb, gamma, beta, eps, H, (__bf16*)out); break;
+    case 4: EMB(4); break;
+    case 8: EMB(8); break;
+    case 12: EMB(12); break;
+    case 16: EMB(16); break;
     default: return DRT_EINVAL;
   }
+#undef EMB
   return hip_status(hipGetLastError());
 }
 

@@ -1002,6 +1002,7 @@ int launch_gemm(const GemmArgs& a, bool out_bf16, int epi, hipStream_t s) {
     case EPI_BIAS: return launch_gemm_t<true, EPI_BIAS>(a, s);
     case EPI_BIAS | EPI_GELU: return launch_gemm_t<true, EPI_BIAS | EPI_GELU>(a, s);
     case EPI_BIAS | EPI_RESID: return launch_gemm_t<true, EPI_BIAS | EPI_RESID>(a, s);
+    case EPI_RESID: return launch_gemm_t<true, EPI_RESID>(a, s);   // backward dgrad + residual branch
     case EPI_GELU: return launch_gemm_t<true, EPI_GELU>(a, s);
     default: return DRT_EINVAL;
   }

@@ -58,10 +58,12 @@ def colsum(x: torch.Tensor) -> torch.Tensor:
     return out
 
 
-def linear_backward(dy: torch.Tensor, x: torch.Tensor, w_t: torch.Tensor, want_dx: bool = True
+def linear_backward(dy: torch.Tensor, x: torch.Tensor, w_t: torch.Tensor, want_dx: bool = True,
+                    resid: Optional[torch.Tensor] = None
                     ) -> Tuple[Optional[torch.Tensor], torch.Tensor, torch.Tensor]:
     """Gradients of y = x W^T + b (nn.Linear, W [N, K]) for dy [T, N], x [T, K] (bf16 CUDA),
-    given w_t = W^T [K, N] bf16.  Returns (dx bf16 [T, K] or None, dW fp32 [N, K], db fp32 [N])."""
+    given w_t = W^T [K, N] bf16.  Returns (dx bf16 [T, K] or None, dW fp32 [N, K], db fp32 [N]);
+    ``resid`` [T, K] bf16 is added to dx in the dgrad GEMM's epilogue (a residual branch)."""
     lib = _native.load()
     dev = dy.device
     s = _native.stream_ptr(dev)
@@ -74,8 +76,8 @@ def linear_backward(dy: torch.Tensor, x: torch.Tensor, w_t: torch.Tensor, want_d
         dx = torch.empty((T, K), dtype=torch.bfloat16, device=dev)
         nb = int(lib.drt_linear_workspace(T, K, N))
         ws = _ws(nb, dev)
-        _native.check(lib.drt_linear_bf16_ws(dy.data_ptr(), w_t.data_ptr(), None, None, dx.data_ptr(), T, K, N, 0,
-                                             _ptr(ws), nb, s), "dgrad")
+        _native.check(lib.drt_linear_bf16_ws(dy.data_ptr(), w_t.data_ptr(), None, _ptr(resid), dx.data_ptr(), T, K, N,
+                                             0, _ptr(ws), nb, s), "dgrad")
     pad = (-T) % 64
     dyT = transpose_bf16(dy, pad)        # [N, T64]
     xT = transpose_bf16(x, pad)          # [K, T64]

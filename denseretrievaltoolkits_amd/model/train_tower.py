@@ -1,0 +1,227 @@
+"""Training forward + backward of a BERT tower on the HIP kernels.
+
+The reference differentiates HF ``BertModel`` under autograd in every training step
+(DRT/trainer/trainer.py:113-133 -> DRModel.forward, DRT/model/biencoder.py:88-125).  Here one
+``torch.autograd.Function`` runs the whole tower: the forward on the inference kernels plus the
+activations the backward needs (bf16: layer input, qkv, ctx, attention LSE, pre-LN sums,
+post-LN1, FFN pre-/post-activation), and the backward entirely on HIP kernels:
+
+    LN2 bwd -> FFN2 linear bwd -> GELU bwd -> FFN1 linear bwd (+ dx2 residual in the dgrad
+    epilogue) -> LN1 bwd -> O-proj linear bwd -> attention bwd -> QKV linear bwd (+ dx1)
+    ... -> embedding LN bwd -> word / position / type scatter-add
+
+producing fp32 gradients for every HF parameter (QKV split back into query/key/value).
+Scope: dropout-free configurations (hidden_dropout_prob = attention_probs_dropout_prob = 0),
+L <= 128, erf GELU, head_dim 64; anything else raises (the HF module under autograd remains the
+path for configs with dropout: in-kernel dropout masks are the next step).
+"""
+from __future__ import annotations
+
+from typing import Dict, List, Optional, Tuple
+
+import torch
+
+from .. import _native
+from .encoder import BertShape, _check_supported
+from .encoder_bwd import _ptr, gelu_backward, layernorm_backward, linear_backward
+
+MAX_TRAIN_SEQ = 128
+
+
+def tower_supported(model) -> Optional[str]:
+    """None if the HIP training tower can run this HF BertModel, else the reason."""
+    cfg = model.config
+    if type(model).__name__ != "BertModel":
+        return f"{type(model).__name__} is not a BertModel"
+    if float(cfg.hidden_dropout_prob) != 0.0 or float(cfg.attention_probs_dropout_prob) != 0.0:
+        return "dropout > 0 (in-kernel dropout masks are not implemented yet)"
+    try:
+        _check_supported(BertShape.from_config(cfg))
+    except ValueError as e:
+        return str(e)
+    return None
+
+
+class _Weights:
+    """bf16 copies (and transposes) of the tower's linears for one step; fp32 LN / bias / tables."""
+
+    def __init__(self, model, dev):
+        lib = _native.load()
+        sd = dict(model.named_parameters())
+        self.names = list(sd.keys())
+        self.sd = sd
+        self.layers = []
+        s = _native.stream_ptr(dev)
+
+        def b16(t):
+            return t.detach().to(torch.bfloat16).contiguous()
+
+        def tr(w):   # [N, K] bf16 -> [K, N]
+            n, k = w.shape
+            y = torch.empty((k, n), dtype=torch.bfloat16, device=dev)
+            _native.check(lib.drt_transpose_bf16(w.data_ptr(), n, k, y.data_ptr(), s), "drt_transpose_bf16")
+            return y
+
+        nl = model.config.num_hidden_layers
+        for i in range(nl):
+            p = f"encoder.layer.{i}."
+            wqkv = b16(torch.cat([sd[p + f"attention.self.{n}.weight"].detach() for n in ("query", "key", "value")]))
+            bqkv = torch.cat([sd[p + f"attention.self.{n}.bias"].detach() for n in ("query", "key", "value")]).float()
+            wo = b16(sd[p + "attention.output.dense.weight"])
+            wi = b16(sd[p + "intermediate.dense.weight"])
+            wf = b16(sd[p + "output.dense.weight"])
+            self.layers.append(dict(
+                wqkv=wqkv, wqkv_t=tr(wqkv), bqkv=bqkv.contiguous(),
+                wo=wo, wo_t=tr(wo), bo=sd[p + "attention.output.dense.bias"].detach().float().contiguous(),
+                g1=sd[p + "attention.output.LayerNorm.weight"].detach().float().contiguous(),
+                b1=sd[p + "attention.output.LayerNorm.bias"].detach().float().contiguous(),
+                wi=wi, wi_t=tr(wi), bi=sd[p + "intermediate.dense.bias"].detach().float().contiguous(),
+                wf=wf, wf_t=tr(wf), bf=sd[p + "output.dense.bias"].detach().float().contiguous(),
+                g2=sd[p + "output.LayerNorm.weight"].detach().float().contiguous(),
+                b2=sd[p + "output.LayerNorm.bias"].detach().float().contiguous(),
+            ))
+        e = "embeddings."
+        self.word = sd[e + "word_embeddings.weight"].detach().float().contiguous()
+        self.pos = sd[e + "position_embeddings.weight"].detach().float().contiguous()
+        self.type = sd[e + "token_type_embeddings.weight"].detach().float().contiguous()
+        self.emb_g = sd[e + "LayerNorm.weight"].detach().float().contiguous()
+        self.emb_b = sd[e + "LayerNorm.bias"].detach().float().contiguous()
+
+
+def _lin(lib, x, w, b, out, resid=None, gelu=False, stream=None):
+    m, k = x.shape
+    n = w.shape[0]
+    flags = (1 if gelu else 0) | (2 if out.dtype == torch.float32 else 0)
+    nb = int(lib.drt_linear_workspace(m, n, k))
+    ws = torch.empty((nb + 3) // 4, dtype=torch.float32, device=x.device) if nb else None
+    _native.check(lib.drt_linear_bf16_ws(x.data_ptr(), w.data_ptr(), _ptr(b), _ptr(resid), out.data_ptr(), m, n, k,
+                                         flags, _ptr(ws), nb, stream), "drt_linear_bf16_ws")
+    return out
+
+
+def _layernorm(lib, x, g, b, eps, stream):
+    out = torch.empty_like(x)
+    _native.check(lib.drt_layernorm_bf16(x.data_ptr(), x.shape[0], x.shape[1], g.data_ptr(), b.data_ptr(), eps,
+                                         out.data_ptr(), stream), "drt_layernorm_bf16")
+    return out
+
+
+def tower_forward(model, W: _Weights, ids: torch.Tensor, mask: Optional[torch.Tensor]):
+    """last_hidden_state bf16 [B, L, H] and the saved activations."""
+    lib = _native.load()
+    dev = ids.device
+    s = _native.stream_ptr(dev)
+    cfg = model.config
+    B, L = ids.shape
+    if L > MAX_TRAIN_SEQ:
+        raise ValueError(f"HIP training tower: sequence length {L} > {MAX_TRAIN_SEQ}")
+    H, heads, eps = cfg.hidden_size, cfg.num_attention_heads, float(cfg.layer_norm_eps)
+    T = B * L
+    h = torch.empty((T, H), dtype=torch.bfloat16, device=dev)
+    emb_pre = torch.empty_like(h)
+    _native.check(lib.drt_embed_ln_pre(ids.data_ptr(), None, B, L, W.word.data_ptr(), W.pos.data_ptr(),
+                                       W.type.data_ptr(), W.emb_g.data_ptr(), W.emb_b.data_ptr(), eps, H,
+                                       h.data_ptr(), emb_pre.data_ptr(), s), "drt_embed_ln_pre")
+    saved = []
+    scale = 1.0 / (H // heads) ** 0.5
+    for ly in W.layers:
+        qkv = _lin(lib, h, ly["wqkv"], ly["bqkv"], torch.empty((T, 3 * H), dtype=torch.bfloat16, device=dev),
+                   stream=s)
+        ctx = torch.empty((T, H), dtype=torch.bfloat16, device=dev)
+        lse = torch.empty((B, heads, L), dtype=torch.float32, device=dev)
+        _native.check(lib.drt_attention_fwd_lse_bf16(qkv.data_ptr(), _ptr(mask), ctx.data_ptr(), lse.data_ptr(), B,
+                                                     L, heads, H // heads, scale, s), "drt_attention_fwd_lse_bf16")
+        x1 = _lin(lib, ctx, ly["wo"], ly["bo"], torch.empty_like(h), resid=h, stream=s)
+        h1 = _layernorm(lib, x1, ly["g1"], ly["b1"], eps, s)
+        fpre = _lin(lib, h1, ly["wi"], ly["bi"],
+                    torch.empty((T, ly["wi"].shape[0]), dtype=torch.bfloat16, device=dev), stream=s)
+        f = torch.empty_like(fpre)
+        _native.check(lib.drt_gelu_bf16(fpre.data_ptr(), fpre.numel(), f.data_ptr(), s), "drt_gelu_bf16")
+        x2 = _lin(lib, f, ly["wf"], ly["bf"], torch.empty_like(h), resid=h1, stream=s)
+        saved.append((h, qkv, ctx, lse, x1, h1, fpre, f, x2))
+        h = _layernorm(lib, x2, ly["g2"], ly["b2"], eps, s)
+    return h.view(B, L, H), (emb_pre, saved)
+
+
+def tower_backward(model, W: _Weights, ids, mask, saved, d_hidden: torch.Tensor) -> Dict[str, torch.Tensor]:
+    """fp32 gradients of every tower parameter (HF names) for d last_hidden_state."""
+    lib = _native.load()
+    dev = ids.device
+    s = _native.stream_ptr(dev)
+    cfg = model.config
+    B, L = ids.shape
+    H, heads, eps = cfg.hidden_size, cfg.num_attention_heads, float(cfg.layer_norm_eps)
+    scale = 1.0 / (H // heads) ** 0.5
+    emb_pre, layers = saved
+    d = d_hidden.reshape(B * L, H).to(torch.bfloat16).contiguous()
+    grads: Dict[str, torch.Tensor] = {}
+    for i in reversed(range(len(layers))):
+        h, qkv, ctx, lse, x1, h1, fpre, f, x2 = layers[i]
+        ly = W.layers[i]
+        p = f"encoder.layer.{i}."
+        dx2, dg2, db2 = layernorm_backward(d, x2, ly["g2"], eps)
+        df, dwf, dbf = linear_backward(dx2, f, ly["wf_t"])
+        dfpre = gelu_backward(df, fpre)
+        dh1, dwi, dbi = linear_backward(dfpre, h1, ly["wi_t"], resid=dx2)
+        dx1, dg1, db1 = layernorm_backward(dh1, x1, ly["g1"], eps)
+        dctx, dwo, dbo = linear_backward(dx1, ctx, ly["wo_t"])
+        dqkv = torch.empty_like(qkv)
+        _native.check(lib.drt_attention_bwd_bf16(qkv.data_ptr(), ctx.data_ptr(), dctx.data_ptr(), lse.data_ptr(),
+                                                 _ptr(mask), dqkv.data_ptr(), B, L, heads, H // heads, scale, s),
+                      "drt_attention_bwd_bf16")
+        d, dwqkv, dbqkv = linear_backward(dqkv, h, ly["wqkv_t"], resid=dx1)
+        grads[p + "output.LayerNorm.weight"], grads[p + "output.LayerNorm.bias"] = dg2, db2
+        grads[p + "output.dense.weight"], grads[p + "output.dense.bias"] = dwf, dbf
+        grads[p + "intermediate.dense.weight"], grads[p + "intermediate.dense.bias"] = dwi, dbi
+        grads[p + "attention.output.LayerNorm.weight"], grads[p + "attention.output.LayerNorm.bias"] = dg1, db1
+        grads[p + "attention.output.dense.weight"], grads[p + "attention.output.dense.bias"] = dwo, dbo
+        for j, n in enumerate(("query", "key", "value")):
+            grads[p + f"attention.self.{n}.weight"] = dwqkv[j * H:(j + 1) * H]
+            grads[p + f"attention.self.{n}.bias"] = dbqkv[j * H:(j + 1) * H]
+    demb, dge, dbe = layernorm_backward(d, emb_pre, W.emb_g, eps)
+    e = "embeddings."
+    dword = torch.zeros_like(W.word)
+    dpos = torch.zeros_like(W.pos)
+    dtype = torch.zeros_like(W.type)
+    pad = model.embeddings.word_embeddings.padding_idx
+    _native.check(lib.drt_embedding_bwd(ids.data_ptr(), None, demb.data_ptr(), B, L, H,
+                                        -1 if pad is None else int(pad), dword.data_ptr(), dpos.data_ptr(),
+                                        dtype.data_ptr(), s), "drt_embedding_bwd")
+    grads[e + "word_embeddings.weight"] = dword
+    grads[e + "position_embeddings.weight"] = dpos
+    grads[e + "token_type_embeddings.weight"] = dtype
+    grads[e + "LayerNorm.weight"], grads[e + "LayerNorm.bias"] = dge, dbe
+    return grads
+
+
+class _TowerFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, ids, mask, model, *params):
+        W = _Weights(model, ids.device)
+        hidden, saved = tower_forward(model, W, ids, mask)
+        ctx.model, ctx.W, ctx.saved_acts = model, W, saved
+        ctx.ids, ctx.mask = ids, mask
+        ctx.param_names = [n for n, _ in model.named_parameters()]
+        return hidden.float()
+
+    @staticmethod
+    def backward(ctx, d_hidden):
+        grads = tower_backward(ctx.model, ctx.W, ctx.ids, ctx.mask, ctx.saved_acts, d_hidden.contiguous())
+        out: List[Optional[torch.Tensor]] = [None, None, None]
+        for n in ctx.param_names:
+            g = grads.get(n)
+            out.append(g.to(torch.float32) if g is not None else None)
+        ctx.saved_acts = None
+        return tuple(out)
+
+
+def train_hidden(model, input_ids: torch.Tensor, attention_mask: Optional[torch.Tensor]) -> torch.Tensor:
+    """last_hidden_state fp32 [B, L, H] of ``model`` with the HIP tower backward attached."""
+    why = tower_supported(model)
+    if why is not None:
+        raise NotImplementedError(f"HIP training tower: {why}")
+    dev = next(model.parameters()).device
+    ids = input_ids.to(dev, torch.int64).contiguous()
+    mask = attention_mask.to(dev, torch.int64).contiguous() if attention_mask is not None else None
+    params = [p for _, p in model.named_parameters()]
+    return _TowerFn.apply(ids, mask, model, *params)

@@ -197,6 +197,19 @@ int drt_transpose_bf16(const void* x, int64_t R, int64_t C, void* y, void* strea
 /* drt_attention_bwd_bf16: dqkv [B*L, 3H] (dQ | dK | dV in qkv's packed layout) of the
  * attention forward, from qkv, its ctx = O, dctx = dO, the forward's lse and the key mask;
  * L <= 128, head_dim 64 (BertSelfAttention under autograd, modeling_bert.py:164-204).   */
+/* drt_embed_ln_pre: drt_embed_ln that also writes the bf16 pre-LN sum (word + type + pos).
+ * drt_gelu_bf16: y = GELU(x) elementwise (erf form).
+ * drt_embedding_bwd: scatter-add of d [B*L, H] (gradient of the pre-LN embedding sum) into
+ *   dword [V,H], dpos [P,H], dtype [types,H] fp32 (atomics; caller zeroes them); tokens
+ *   equal to padding_idx (nn.Embedding(padding_idx), -1 = none) add nothing to dword.      */
+int drt_embed_ln_pre(const int64_t* ids, const int64_t* type_ids, int64_t B, int64_t L,
+                     const float* word_emb, const float* pos_emb, const float* type_emb,
+                     const float* gamma, const float* beta, float eps, int32_t H, void* out, void* pre,
+                     void* stream);
+int drt_gelu_bf16(const void* x, int64_t n, void* y, void* stream);
+int drt_embedding_bwd(const int64_t* ids, const int64_t* type_ids, const void* d, int64_t B, int64_t L,
+                      int32_t H, int64_t padding_idx, float* dword, float* dpos, float* dtype,
+                      void* stream);
 int drt_attention_bwd_bf16(const void* qkv, const void* ctx, const void* dctx, const float* lse,
                            const int64_t* mask, void* dqkv, int64_t B, int64_t L, int32_t heads,
                            int32_t head_dim, float scale, void* stream);
