@@ -332,6 +332,7 @@ def main():
         out["rerank"] = bench_encode.run_rerank(dev)
         out["query_encode"] = bench_encode.run_query_encode(dev)
         out["train_scores"] = bench_encode.run_train_scores(dev)
+        out["train_step"] = bench_encode.run_train_step(dev)
     if rank == 0:
         print(json.dumps(out), flush=True)
     if world > 1:

@@ -216,3 +216,51 @@ def run_train_scores(device, bq=512, d=768, n_passages=(2, 8), steps=20, warmup=
             out["hip_graph_tflops"] = round(fl / (out["hip_graph_ms"] * 1e-3) / 1e12, 2)
         res[f"n{n}"] = out
     return res
+
+
+def run_train_step(device, bq=512, n=2, q_len=32, p_len=128, steps=3, warmup=1):
+    """Config C3 end to end: one in-batch-negative training step of DRModel.forward (query tower on
+    512 x 32 tokens, passage tower on 1024 x 128 tokens, score matrix + CE, backward into every
+    tower parameter; DRT/trainer/trainer.py:113-133) on a dropout-free BERT-base (random init):
+    the HIP training tower (bf16 activations, model/train_tower.py) vs the HF module under torch
+    fp32 autograd on the same device.  Optimizer update excluded (identical for both)."""
+    from types import SimpleNamespace
+    from transformers import BertConfig, BertModel
+    from .model.biencoder import DRModel
+    torch.manual_seed(0)
+    lm = BertModel(BertConfig(hidden_dropout_prob=0.0, attention_probs_dropout_prob=0.0),
+                   add_pooling_layer=False).to(device).train()
+    m = DRModel(lm_q=lm, lm_p=lm, pooling="first", data_args=SimpleNamespace(train_n_passages=n),
+                train_args=SimpleNamespace(negatives_x_device=False)).train()
+    g = torch.Generator(device=device)
+    g.manual_seed(6)
+
+    def batch(b, L):
+        ids = torch.randint(1000, 30522, (b, L), generator=g, device=device, dtype=torch.int64)
+        ids[:, 0] = 101
+        ids[:, -1] = 102
+        return {"input_ids": ids, "attention_mask": torch.ones((b, L), dtype=torch.int64, device=device)}
+
+    qry, psg = batch(bq, q_len), batch(bq * n, p_len)
+    fl = 3 * (bq * flops_per_seq(q_len) + bq * n * flops_per_seq(p_len))
+    res = {"metric": "in-batch-negative training step (fwd + bwd of both towers + score/CE), ms",
+           "batch": bq, "train_n_passages": n, "q_len": q_len, "p_len": p_len, "flop_per_step": fl}
+    for name, hip in (("hip", True), ("torch_fp32", False)):
+        m.hip_train = hip
+
+        def step():
+            lm.zero_grad(set_to_none=True)
+            m(query=qry, passage=psg).loss.backward()
+
+        for _ in range(warmup):
+            step()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(steps):
+            step()
+        torch.cuda.synchronize()
+        ms = (time.perf_counter() - t0) / steps * 1e3
+        res[name + "_ms"] = round(ms, 2)
+        res[name + "_tflops"] = round(fl / (ms * 1e-3) / 1e12, 1)
+    res["speedup"] = round(res["torch_fp32_ms"] / res["hip_ms"], 2)
+    return res

@@ -32,6 +32,7 @@ from transformers import AutoModel, BatchEncoding, PreTrainedModel
 from transformers.modeling_outputs import ModelOutput
 
 from .encoder import HipBertEncoder, l2_normalize_, linear_head
+from .train_tower import MAX_TRAIN_SEQ, tower_supported, train_hidden
 from .linear import LinearHead
 
 logger = logging.getLogger(__name__)
@@ -69,6 +70,7 @@ class DRModel(nn.Module):
         self.loss_fn = nn.CrossEntropyLoss(reduction="mean")
         self.feature = feature
         self.pooling = pooling
+        self.hip_train = True   # HIP training tower for dropout-free BERT towers (set False: HF autograd)
         self.normalize = normalize
         self.model_args = model_args
         self.train_args = train_args
@@ -157,9 +159,16 @@ class DRModel(nn.Module):
             if self.normalize:
                 reps, _ = l2_normalize_(reps)
             return hidden, reps
-        # training forward: HF module under autograd (encoder backward kernels are §8f next)
-        out = model(**items, return_dict=True)
-        hidden = getattr(out, self.feature)
+        # training forward.  Dropout-free BERT towers run the HIP training tower (forward with
+        # saved bf16 activations + backward on HIP kernels, model/train_tower.py); towers with
+        # dropout keep the HF module under autograd until in-kernel dropout masks exist.
+        if (self.hip_train and self.feature == "last_hidden_state" and next(model.parameters()).is_cuda
+                and "token_type_ids" not in items and tower_supported(model) is None
+                and items["input_ids"].shape[1] <= MAX_TRAIN_SEQ):
+            hidden = train_hidden(model, items["input_ids"], items.get("attention_mask"))
+        else:
+            out = model(**items, return_dict=True)
+            hidden = getattr(out, self.feature)
         if self.pooling == "first":
             reps = hidden[:, 0, :]
         elif self.pooling == "mean":
