@@ -221,15 +221,15 @@ def run_train_scores(device, bq=512, d=768, n_passages=(2, 8), steps=20, warmup=
 def run_train_step(device, bq=512, n=2, q_len=32, p_len=128, steps=3, warmup=1):
     """Config C3 end to end: one in-batch-negative training step of DRModel.forward (query tower on
     512 x 32 tokens, passage tower on 1024 x 128 tokens, score matrix + CE, backward into every
-    tower parameter; DRT/trainer/trainer.py:113-133) on a dropout-free BERT-base (random init):
+    tower parameter; DRT/trainer/trainer.py:113-133) on BERT-base (random init):
     the HIP training tower (bf16 activations, model/train_tower.py) vs the HF module under torch
-    fp32 autograd on the same device.  Optimizer update excluded (identical for both)."""
+    fp32 autograd on the same device, both with HF's default dropout (0.1 hidden / 0.1 attention:
+    HF's own masks vs the tower's hash masks).  Optimizer update excluded (identical for both)."""
     from types import SimpleNamespace
     from transformers import BertConfig, BertModel
     from .model.biencoder import DRModel
     torch.manual_seed(0)
-    lm = BertModel(BertConfig(hidden_dropout_prob=0.0, attention_probs_dropout_prob=0.0),
-                   add_pooling_layer=False).to(device).train()
+    lm = BertModel(BertConfig(), add_pooling_layer=False).to(device).train()
     m = DRModel(lm_q=lm, lm_p=lm, pooling="first", data_args=SimpleNamespace(train_n_passages=n),
                 train_args=SimpleNamespace(negatives_x_device=False)).train()
     g = torch.Generator(device=device)

@@ -43,6 +43,20 @@ __host__ __device__ __forceinline__ float desc_key_to_score(uint32_t k) {
   return __builtin_bit_cast(float, u);
 }
 
+// Training dropout (HF BertModel in train mode: embeddings, attention probabilities, and the
+// two sublayer outputs, modeling_bert.py:107,195,296,348): a counter-based hash of (seed, site,
+// element index) decides each keep, so forward and backward regenerate the same mask without
+// storing it; keep iff the top 24 hash bits >= p * 2^24.  model/train_tower.py restates it in
+// torch for the tests.
+__host__ __device__ __forceinline__ uint32_t drop_hash24(uint64_t seed, uint64_t site, uint64_t idx) {
+  uint64_t x = idx * 0x9E3779B97F4A7C15ull + seed + site * 0xBF58476D1CE4E5B9ull;
+  x ^= x >> 31;
+  x *= 0x94D049BB133111EBull;
+  x ^= x >> 29;
+  return (uint32_t)(x >> 40);
+}
+__host__ __device__ __forceinline__ uint32_t drop_threshold(float p) { return (uint32_t)(p * 16777216.0f); }
+
 // faiss pads rows that have fewer than k results with label -1 and the
 // lowest float (CMin<float>::neutral() == numeric_limits<float>::lowest()).
 constexpr float kPadScore = -3.402823466e+38f;

@@ -164,8 +164,11 @@ struct AttnArgs {
   float scale;            // 1/sqrt(dh): applied to Q (exact for dh = 64)
   float* lse;             // optional [B][heads][L]: log-sum-exp of each query's scaled, masked
                           // scores (what the attention backward needs to rebuild P)
+  float drop_p;           // training: dropout of the attention probabilities (DROP kernels)
+  uint64_t seed, site;    //   mask = drop_hash24(seed, site, ((b * heads + head) * L + q) * L + key)
 };
 
+template <bool DROP>
 __global__ __launch_bounds__(kAttnThreads, 4) void attention_kernel(AttnArgs a) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int L = (int)a.L;
@@ -284,6 +287,18 @@ __global__ __launch_bounds__(kAttnThreads, 4) void attention_kernel(AttnArgs a) 
       ps += __shfl_xor(ps, 32, 64);
       l = l * alpha + ps;
       m = mn;
+      if (DROP) {   // dropout of P after its normaliser: O = dropout(softmax) V
+        const float inv = 1.0f / (1.0f - a.drop_p);
+        const uint32_t thr = drop_threshold(a.drop_p);
+        const int qq = qb * 32 + r;
+        const uint64_t base = (((uint64_t)b * a.heads + hd) * L + qq) * (uint64_t)L;
+#pragma unroll
+        for (int e = 0; e < 16; ++e) {
+          const int key = kt + (e & 3) + 8 * (e >> 2) + 4 * h;
+          const bool keep = key < L && drop_hash24(a.seed, a.site, base + key) >= thr;
+          s[e] = keep ? s[e] * inv : 0.0f;
+        }
+      }
 #pragma unroll
       for (int t = 0; t < 2; ++t)
 #pragma unroll
@@ -483,21 +498,39 @@ int drt_attention_bf16(const void* qkv, const int64_t* mask, void* ctx, int64_t 
   return drt_attention_fwd_lse_bf16(qkv, mask, ctx, nullptr, B, L, heads, head_dim, scale, stream);
 }
 
+int drt_attention_train_fwd_bf16(const void* qkv, const int64_t* mask, void* ctx, float* lse, int64_t B, int64_t L,
+                                 int32_t heads, int32_t head_dim, float scale, float drop_p, uint64_t seed,
+                                 uint64_t site, void* stream);
+
 int drt_attention_fwd_lse_bf16(const void* qkv, const int64_t* mask, void* ctx, float* lse, int64_t B, int64_t L,
                                int32_t heads, int32_t head_dim, float scale, void* stream) {
+  return drt_attention_train_fwd_bf16(qkv, mask, ctx, lse, B, L, heads, head_dim, scale, 0.0f, 0, 0, stream);
+}
+
+int drt_attention_train_fwd_bf16(const void* qkv, const int64_t* mask, void* ctx, float* lse, int64_t B, int64_t L,
+                                 int32_t heads, int32_t head_dim, float scale, float drop_p, uint64_t seed,
+                                 uint64_t site, void* stream) {
   DRT_REQUIRE(B >= 0 && L > 0 && L <= kMaxSeq && heads > 0 && head_dim == kHeadDim);
+  DRT_REQUIRE(drop_p >= 0.0f && drop_p < 1.0f);
   if (B == 0) return DRT_OK;
   DRT_REQUIRE(qkv && ctx);
-  AttnArgs a{(const __bf16*)qkv, mask, (__bf16*)ctx, B, L, heads, heads * head_dim, scale, lse};
+  AttnArgs a{(const __bf16*)qkv, mask, (__bf16*)ctx, B, L, heads, heads * head_dim, scale, lse, drop_p, seed, site};
   const int Lp = ((int)L + 31) & ~31;
   const size_t lds = (size_t)Lp * 128 + (size_t)64 * (Lp * 2 + 8) + (size_t)Lp * 4;
   static bool attr_set = false;
   if (!attr_set) {
-    DRT_CHECK_HIP(hipFuncSetAttribute((const void*)attention_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                      160 * 1024));
+    DRT_CHECK_HIP(hipFuncSetAttribute((const void*)attention_kernel<false>,
+                                      hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
+    DRT_CHECK_HIP(hipFuncSetAttribute((const void*)attention_kernel<true>,
+                                      hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
     attr_set = true;
   }
-  hipLaunchKernelGGL(attention_kernel, dim3((unsigned)(B * heads)), dim3(kAttnThreads), lds, (hipStream_t)stream, a);
+  if (drop_p > 0.0f)
+    hipLaunchKernelGGL(attention_kernel<true>, dim3((unsigned)(B * heads)), dim3(kAttnThreads), lds,
+                       (hipStream_t)stream, a);
+  else
+    hipLaunchKernelGGL(attention_kernel<false>, dim3((unsigned)(B * heads)), dim3(kAttnThreads), lds,
+                       (hipStream_t)stream, a);
   return hip_status(hipGetLastError());
 }
 

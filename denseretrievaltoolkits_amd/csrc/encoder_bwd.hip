@@ -188,6 +188,8 @@ struct AttnBwdArgs {
   int64_t B, L;
   int heads, H;
   float scale;
+  float drop_p;           // attention-probability dropout of the forward (0: none)
+  uint64_t seed, site;
 };
 
 __device__ __forceinline__ int ab_rc(int row, int chunk) { return row * kAbRow + ((chunk ^ ((row >> 1) & 7)) << 4); }
@@ -266,6 +268,9 @@ __global__ __launch_bounds__(kAbThreads) void attention_bwd_kernel(AttnBwdArgs a
   __syncthreads();
 
   const int nblk = Lp / 32;
+  const bool drop = a.drop_p > 0.0f;
+  const float inv = drop ? 1.0f / (1.0f - a.drop_p) : 1.0f;
+  const uint32_t thr = drop_threshold(a.drop_p);
   char* sP = scr + (wave * 2 + 0) * 32 * kAbScr;
   char* sS = scr + (wave * 2 + 1) * 32 * kAbScr;
 
@@ -298,14 +303,23 @@ __global__ __launch_bounds__(kAbThreads) void attention_bwd_kernel(AttnBwdArgs a
         const bf16x8 ob = *(const bf16x8*)(Os + ab_rc(qcol, c));
         dpt = __builtin_amdgcn_mfma_f32_32x32x16_bf16(va, ob, dpt, 0, 0, 0);
       }
-      // P^T, dS^T: row = key kbk*32 + (e&3) + 8(e>>2) + 4h, column = query qcol
+      // P^T, dS^T: row = key kbk*32 + (e&3) + 8(e>>2) + 4h, column = query qcol.  With dropout,
+      // O = Pd V where Pd = mask P / (1 - p): dV takes Pd, and dS = P (mask dPd / (1 - p) - Dv)
       const float lq = lse[qcol], dq = dv[qcol];
+      const uint64_t dbase = (((uint64_t)b * a.heads + hd) * L + qcol) * (uint64_t)L;
 #pragma unroll
       for (int e = 0; e < 16; ++e) {
         const int kr = (e & 3) + 8 * (e >> 2) + 4 * h;
         const float p = __expf(st[e] + kb[kbk * 32 + kr] - lq);
-        const float ds = p * (dpt[e] - dq);
-        *(__bf16*)(sP + kr * kAbScr + r * 2) = (__bf16)p;
+        float pd = p, dpe = dpt[e];
+        if (drop) {
+          const int key = kbk * 32 + kr;
+          const bool keep = key < L && qcol < L && drop_hash24(a.seed, a.site, dbase + key) >= thr;
+          pd = keep ? p * inv : 0.f;
+          dpe = keep ? dpe * inv : 0.f;
+        }
+        const float ds = p * (dpe - dq);
+        *(__bf16*)(sP + kr * kAbScr + r * 2) = (__bf16)pd;
         *(__bf16*)(sS + kr * kAbScr + r * 2) = (__bf16)ds;
       }
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
@@ -374,7 +388,13 @@ __global__ __launch_bounds__(kAbThreads) void attention_bwd_kernel(AttnBwdArgs a
         const int qr = (e & 3) + 8 * (e >> 2) + 4 * h;
         const int q = qbq * 32 + qr;
         const float p = __expf(sv[e] + kbias - lse[q]);
-        *(__bf16*)(sS + qr * kAbScr + r * 2) = (__bf16)(p * (dp[e] - dv[q]));
+        float dpe = dp[e];
+        if (drop) {
+          const uint64_t idx = (((uint64_t)b * a.heads + hd) * L + q) * (uint64_t)L + kcol;
+          const bool keep = kcol < L && q < L && drop_hash24(a.seed, a.site, idx) >= thr;
+          dpe = keep ? dpe * inv : 0.f;
+        }
+        *(__bf16*)(sS + qr * kAbScr + r * 2) = (__bf16)(p * (dpe - dv[q]));
       }
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
       __builtin_amdgcn_wave_barrier();
@@ -401,6 +421,18 @@ __global__ __launch_bounds__(kAbThreads) void attention_bwd_kernel(AttnBwdArgs a
       }
     }
   }
+}
+
+// out = dropout(y) (+ resid): keep iff drop_hash24(seed, site, i) >= p 2^24, kept values scaled
+// by 1 / (1 - p).  The same call on a gradient (resid = NULL) is the dropout backward.
+__global__ __launch_bounds__(256) void dropout_add_kernel(const __bf16* y, const __bf16* resid, int64_t n, float p,
+                                                          uint64_t seed, uint64_t site, __bf16* out) {
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i >= n) return;
+  const bool keep = drop_hash24(seed, site, (uint64_t)i) >= drop_threshold(p);
+  float v = keep ? (float)y[i] / (1.0f - p) : 0.0f;
+  if (resid) v += (float)resid[i];
+  out[i] = (__bf16)v;
 }
 
 static int64_t colsum_slabs(int64_t M) { return M < 256 ? 1 : (M + 255) / 256 < 512 ? (M + 255) / 256 : 512; }
@@ -484,14 +516,30 @@ int drt_gelu_bwd_bf16(const void* dy, const void* pre, int64_t n, void* dx, void
 
 // dqkv [B*L][3H] (dQ | dK | dV, head-major like qkv) of the attention forward
 // (drt_attention_fwd_lse_bf16) given dctx = dO, the forward's ctx = O and lse.  L <= 128.
+int drt_attention_train_bwd_bf16(const void* qkv, const void* ctx, const void* dctx, const float* lse,
+                                 const int64_t* mask, void* dqkv, int64_t B, int64_t L, int32_t heads,
+                                 int32_t head_dim, float scale, float drop_p, uint64_t seed, uint64_t site,
+                                 void* stream);
+
 int drt_attention_bwd_bf16(const void* qkv, const void* ctx, const void* dctx, const float* lse,
                            const int64_t* mask, void* dqkv, int64_t B, int64_t L, int32_t heads, int32_t head_dim,
                            float scale, void* stream) {
+  return drt_attention_train_bwd_bf16(qkv, ctx, dctx, lse, mask, dqkv, B, L, heads, head_dim, scale, 0.0f, 0, 0,
+                                      stream);
+}
+
+// The same with the forward's attention-probability dropout (drop_p, seed, site as passed to
+// drt_attention_train_fwd_bf16).
+int drt_attention_train_bwd_bf16(const void* qkv, const void* ctx, const void* dctx, const float* lse,
+                                 const int64_t* mask, void* dqkv, int64_t B, int64_t L, int32_t heads,
+                                 int32_t head_dim, float scale, float drop_p, uint64_t seed, uint64_t site,
+                                 void* stream) {
   DRT_REQUIRE(B >= 0 && L > 0 && L <= kAbMaxSeq && heads > 0 && head_dim == 64);
+  DRT_REQUIRE(drop_p >= 0.0f && drop_p < 1.0f);
   if (B == 0) return DRT_OK;
   DRT_REQUIRE(qkv && ctx && dctx && lse && dqkv);
   AttnBwdArgs a{(const __bf16*)qkv, (const __bf16*)ctx, (const __bf16*)dctx, lse, mask, (__bf16*)dqkv, B, L,
-                heads, heads * 64, scale};
+                heads, heads * 64, scale, drop_p, seed, site};
   const int Lp = ((int)L + 31) & ~31;
   const size_t lds = (size_t)4 * Lp * kAbRow + (size_t)3 * 64 * kAbTRow + (size_t)8 * 32 * kAbScr +
                      (size_t)3 * Lp * 4;
@@ -502,6 +550,16 @@ int drt_attention_bwd_bf16(const void* qkv, const void* ctx, const void* dctx, c
     attr_set = true;
   }
   hipLaunchKernelGGL(attention_bwd_kernel, dim3((unsigned)(B * heads)), dim3(kAbThreads), lds, (hipStream_t)stream, a);
+  return hip_status(hipGetLastError());
+}
+
+int drt_dropout_add_bf16(const void* y, const void* resid, int64_t n, float p, uint64_t seed, uint64_t site,
+                         void* out, void* stream) {
+  DRT_REQUIRE(n >= 0 && p >= 0.0f && p < 1.0f);
+  if (n == 0) return DRT_OK;
+  DRT_REQUIRE(y && out);
+  hipLaunchKernelGGL(dropout_add_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, (hipStream_t)stream,
+                     (const __bf16*)y, (const __bf16*)resid, n, p, seed, site, (__bf16*)out);
   return hip_status(hipGetLastError());
 }
 

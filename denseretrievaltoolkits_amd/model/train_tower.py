@@ -11,9 +11,13 @@ post-LN1, FFN pre-/post-activation), and the backward entirely on HIP kernels:
     ... -> embedding LN bwd -> word / position / type scatter-add
 
 producing fp32 gradients for every HF parameter (QKV split back into query/key/value).
-Scope: dropout-free configurations (hidden_dropout_prob = attention_probs_dropout_prob = 0),
-L <= 128, erf GELU, head_dim 64; anything else raises (the HF module under autograd remains the
-path for configs with dropout: in-kernel dropout masks are the next step).
+Dropout as HF applies it in train mode (embeddings output, attention probabilities, both
+sublayer outputs before their residual add; hidden_dropout_prob / attention_probs_dropout_prob):
+each keep is a counter-based hash of (per-call seed, site, element index) (csrc/drt_common.h
+drop_hash24), so the backward regenerates the forward's masks instead of storing them; the
+seed comes from torch's CPU generator (``torch.manual_seed`` makes a step reproducible).  The
+masks are not HF's Philox stream: same distribution and semantics, different draws.
+Scope: L <= 128, erf GELU, head_dim 64; anything else raises.
 """
 from __future__ import annotations
 
@@ -33,8 +37,6 @@ def tower_supported(model) -> Optional[str]:
     cfg = model.config
     if type(model).__name__ != "BertModel":
         return f"{type(model).__name__} is not a BertModel"
-    if float(cfg.hidden_dropout_prob) != 0.0 or float(cfg.attention_probs_dropout_prob) != 0.0:
-        return "dropout > 0 (in-kernel dropout masks are not implemented yet)"
     try:
         _check_supported(BertShape.from_config(cfg))
     except ValueError as e:
@@ -106,8 +108,20 @@ def _layernorm(lib, x, g, b, eps, stream):
     return out
 
 
-def tower_forward(model, W: _Weights, ids: torch.Tensor, mask: Optional[torch.Tensor]):
-    """last_hidden_state bf16 [B, L, H] and the saved activations."""
+def _dropout(lib, y, p, seed, site, stream, resid=None):
+    out = torch.empty_like(y)
+    _native.check(lib.drt_dropout_add_bf16(y.data_ptr(), _ptr(resid), y.numel(), float(p), seed, site,
+                                           out.data_ptr(), stream), "drt_dropout_add_bf16")
+    return out
+
+
+def dropout_sites(layer: int):
+    """(attention probabilities, attention output, FFN output) site ids of a layer; 0 = embeddings."""
+    return 4 * layer + 1, 4 * layer + 2, 4 * layer + 3
+
+
+def tower_forward(model, W: _Weights, ids: torch.Tensor, mask: Optional[torch.Tensor], drop=(0.0, 0.0, 0)):
+    """last_hidden_state bf16 [B, L, H] and the saved activations; drop = (hidden p, attention p, seed)."""
     lib = _native.load()
     dev = ids.device
     s = _native.stream_ptr(dev)
@@ -122,28 +136,42 @@ def tower_forward(model, W: _Weights, ids: torch.Tensor, mask: Optional[torch.Te
     _native.check(lib.drt_embed_ln_pre(ids.data_ptr(), None, B, L, W.word.data_ptr(), W.pos.data_ptr(),
                                        W.type.data_ptr(), W.emb_g.data_ptr(), W.emb_b.data_ptr(), eps, H,
                                        h.data_ptr(), emb_pre.data_ptr(), s), "drt_embed_ln_pre")
+    ph, pa, seed = drop
+    if ph > 0:
+        h = _dropout(lib, h, ph, seed, 0, s)
     saved = []
     scale = 1.0 / (H // heads) ** 0.5
-    for ly in W.layers:
+    for i, ly in enumerate(W.layers):
+        s_att, s_out1, s_out2 = dropout_sites(i)
         qkv = _lin(lib, h, ly["wqkv"], ly["bqkv"], torch.empty((T, 3 * H), dtype=torch.bfloat16, device=dev),
                    stream=s)
         ctx = torch.empty((T, H), dtype=torch.bfloat16, device=dev)
         lse = torch.empty((B, heads, L), dtype=torch.float32, device=dev)
-        _native.check(lib.drt_attention_fwd_lse_bf16(qkv.data_ptr(), _ptr(mask), ctx.data_ptr(), lse.data_ptr(), B,
-                                                     L, heads, H // heads, scale, s), "drt_attention_fwd_lse_bf16")
-        x1 = _lin(lib, ctx, ly["wo"], ly["bo"], torch.empty_like(h), resid=h, stream=s)
+        _native.check(lib.drt_attention_train_fwd_bf16(qkv.data_ptr(), _ptr(mask), ctx.data_ptr(), lse.data_ptr(),
+                                                       B, L, heads, H // heads, scale, float(pa), seed, s_att, s),
+                      "drt_attention_train_fwd_bf16")
+        if ph > 0:   # x1 = dropout(ctx Wo^T + bo) + h
+            x1 = _dropout(lib, _lin(lib, ctx, ly["wo"], ly["bo"], torch.empty_like(h), stream=s), ph, seed, s_out1, s,
+                          resid=h)
+        else:
+            x1 = _lin(lib, ctx, ly["wo"], ly["bo"], torch.empty_like(h), resid=h, stream=s)
         h1 = _layernorm(lib, x1, ly["g1"], ly["b1"], eps, s)
         fpre = _lin(lib, h1, ly["wi"], ly["bi"],
                     torch.empty((T, ly["wi"].shape[0]), dtype=torch.bfloat16, device=dev), stream=s)
         f = torch.empty_like(fpre)
         _native.check(lib.drt_gelu_bf16(fpre.data_ptr(), fpre.numel(), f.data_ptr(), s), "drt_gelu_bf16")
-        x2 = _lin(lib, f, ly["wf"], ly["bf"], torch.empty_like(h), resid=h1, stream=s)
+        if ph > 0:   # x2 = dropout(f Wf^T + bf) + h1
+            x2 = _dropout(lib, _lin(lib, f, ly["wf"], ly["bf"], torch.empty_like(h), stream=s), ph, seed, s_out2, s,
+                          resid=h1)
+        else:
+            x2 = _lin(lib, f, ly["wf"], ly["bf"], torch.empty_like(h), resid=h1, stream=s)
         saved.append((h, qkv, ctx, lse, x1, h1, fpre, f, x2))
         h = _layernorm(lib, x2, ly["g2"], ly["b2"], eps, s)
     return h.view(B, L, H), (emb_pre, saved)
 
 
-def tower_backward(model, W: _Weights, ids, mask, saved, d_hidden: torch.Tensor) -> Dict[str, torch.Tensor]:
+def tower_backward(model, W: _Weights, ids, mask, saved, d_hidden: torch.Tensor, drop=(0.0, 0.0, 0)
+                   ) -> Dict[str, torch.Tensor]:
     """fp32 gradients of every tower parameter (HF names) for d last_hidden_state."""
     lib = _native.load()
     dev = ids.device
@@ -153,22 +181,26 @@ def tower_backward(model, W: _Weights, ids, mask, saved, d_hidden: torch.Tensor)
     H, heads, eps = cfg.hidden_size, cfg.num_attention_heads, float(cfg.layer_norm_eps)
     scale = 1.0 / (H // heads) ** 0.5
     emb_pre, layers = saved
+    ph, pa, seed = drop
     d = d_hidden.reshape(B * L, H).to(torch.bfloat16).contiguous()
     grads: Dict[str, torch.Tensor] = {}
     for i in reversed(range(len(layers))):
         h, qkv, ctx, lse, x1, h1, fpre, f, x2 = layers[i]
         ly = W.layers[i]
         p = f"encoder.layer.{i}."
+        s_att, s_out1, s_out2 = dropout_sites(i)
         dx2, dg2, db2 = layernorm_backward(d, x2, ly["g2"], eps)
-        df, dwf, dbf = linear_backward(dx2, f, ly["wf_t"])
+        df, dwf, dbf = linear_backward(_dropout(lib, dx2, ph, seed, s_out2, s) if ph > 0 else dx2, f, ly["wf_t"])
         dfpre = gelu_backward(df, fpre)
         dh1, dwi, dbi = linear_backward(dfpre, h1, ly["wi_t"], resid=dx2)
         dx1, dg1, db1 = layernorm_backward(dh1, x1, ly["g1"], eps)
-        dctx, dwo, dbo = linear_backward(dx1, ctx, ly["wo_t"])
+        dctx, dwo, dbo = linear_backward(_dropout(lib, dx1, ph, seed, s_out1, s) if ph > 0 else dx1, ctx,
+                                         ly["wo_t"])
         dqkv = torch.empty_like(qkv)
-        _native.check(lib.drt_attention_bwd_bf16(qkv.data_ptr(), ctx.data_ptr(), dctx.data_ptr(), lse.data_ptr(),
-                                                 _ptr(mask), dqkv.data_ptr(), B, L, heads, H // heads, scale, s),
-                      "drt_attention_bwd_bf16")
+        _native.check(lib.drt_attention_train_bwd_bf16(qkv.data_ptr(), ctx.data_ptr(), dctx.data_ptr(),
+                                                       lse.data_ptr(), _ptr(mask), dqkv.data_ptr(), B, L, heads,
+                                                       H // heads, scale, float(pa), seed, s_att, s),
+                      "drt_attention_train_bwd_bf16")
         d, dwqkv, dbqkv = linear_backward(dqkv, h, ly["wqkv_t"], resid=dx1)
         grads[p + "output.LayerNorm.weight"], grads[p + "output.LayerNorm.bias"] = dg2, db2
         grads[p + "output.dense.weight"], grads[p + "output.dense.bias"] = dwf, dbf
@@ -178,6 +210,8 @@ def tower_backward(model, W: _Weights, ids, mask, saved, d_hidden: torch.Tensor)
         for j, n in enumerate(("query", "key", "value")):
             grads[p + f"attention.self.{n}.weight"] = dwqkv[j * H:(j + 1) * H]
             grads[p + f"attention.self.{n}.bias"] = dbqkv[j * H:(j + 1) * H]
+    if ph > 0:
+        d = _dropout(lib, d, ph, seed, 0, s)
     demb, dge, dbe = layernorm_backward(d, emb_pre, W.emb_g, eps)
     e = "embeddings."
     dword = torch.zeros_like(W.word)
@@ -196,18 +230,18 @@ def tower_backward(model, W: _Weights, ids, mask, saved, d_hidden: torch.Tensor)
 
 class _TowerFn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, ids, mask, model, *params):
+    def forward(ctx, ids, mask, model, drop, *params):
         W = _Weights(model, ids.device)
-        hidden, saved = tower_forward(model, W, ids, mask)
-        ctx.model, ctx.W, ctx.saved_acts = model, W, saved
+        hidden, saved = tower_forward(model, W, ids, mask, drop)
+        ctx.model, ctx.W, ctx.saved_acts, ctx.drop = model, W, saved, drop
         ctx.ids, ctx.mask = ids, mask
         ctx.param_names = [n for n, _ in model.named_parameters()]
         return hidden.float()
 
     @staticmethod
     def backward(ctx, d_hidden):
-        grads = tower_backward(ctx.model, ctx.W, ctx.ids, ctx.mask, ctx.saved_acts, d_hidden.contiguous())
-        out: List[Optional[torch.Tensor]] = [None, None, None]
+        grads = tower_backward(ctx.model, ctx.W, ctx.ids, ctx.mask, ctx.saved_acts, d_hidden.contiguous(), ctx.drop)
+        out: List[Optional[torch.Tensor]] = [None, None, None, None]
         for n in ctx.param_names:
             g = grads.get(n)
             out.append(g.to(torch.float32) if g is not None else None)
@@ -215,8 +249,10 @@ class _TowerFn(torch.autograd.Function):
         return tuple(out)
 
 
-def train_hidden(model, input_ids: torch.Tensor, attention_mask: Optional[torch.Tensor]) -> torch.Tensor:
-    """last_hidden_state fp32 [B, L, H] of ``model`` with the HIP tower backward attached."""
+def train_hidden(model, input_ids: torch.Tensor, attention_mask: Optional[torch.Tensor],
+                 seed: Optional[int] = None) -> torch.Tensor:
+    """last_hidden_state fp32 [B, L, H] of ``model`` with the HIP tower backward attached.
+    Dropout follows ``model.training`` and the config's probabilities (seed: torch CPU RNG)."""
     why = tower_supported(model)
     if why is not None:
         raise NotImplementedError(f"HIP training tower: {why}")
@@ -224,4 +260,9 @@ def train_hidden(model, input_ids: torch.Tensor, attention_mask: Optional[torch.
     ids = input_ids.to(dev, torch.int64).contiguous()
     mask = attention_mask.to(dev, torch.int64).contiguous() if attention_mask is not None else None
     params = [p for _, p in model.named_parameters()]
-    return _TowerFn.apply(ids, mask, model, *params)
+    cfg = model.config
+    ph = float(cfg.hidden_dropout_prob) if model.training else 0.0
+    pa = float(cfg.attention_probs_dropout_prob) if model.training else 0.0
+    if seed is None:
+        seed = int(torch.randint(0, 2 ** 62, (1,)).item()) if (ph > 0 or pa > 0) else 0
+    return _TowerFn.apply(ids, mask, model, (ph, pa, seed), *params)

@@ -213,6 +213,21 @@ int drt_embedding_bwd(const int64_t* ids, const int64_t* type_ids, const void* d
 int drt_attention_bwd_bf16(const void* qkv, const void* ctx, const void* dctx, const float* lse,
                            const int64_t* mask, void* dqkv, int64_t B, int64_t L, int32_t heads,
                            int32_t head_dim, float scale, void* stream);
+/* Training dropout (HF train mode, modeling_bert.py:107,195,296,348): keep element i of a
+ * site iff drop_hash24(seed, site, i) >= p 2^24 (csrc/drt_common.h), kept values / (1 - p).
+ * drt_attention_train_fwd_bf16 / _bwd_bf16: attention with dropout of the probabilities
+ *   (element index ((b*heads + head)*L + q)*L + key); p = 0 is the plain forward / backward.
+ * drt_dropout_add_bf16: out = dropout(y) + resid (resid may be NULL) over n elements; the
+ *   same call on a gradient with resid = NULL is the dropout backward.                      */
+int drt_attention_train_fwd_bf16(const void* qkv, const int64_t* mask, void* ctx, float* lse, int64_t B,
+                                 int64_t L, int32_t heads, int32_t head_dim, float scale, float drop_p,
+                                 uint64_t seed, uint64_t site, void* stream);
+int drt_attention_train_bwd_bf16(const void* qkv, const void* ctx, const void* dctx, const float* lse,
+                                 const int64_t* mask, void* dqkv, int64_t B, int64_t L, int32_t heads,
+                                 int32_t head_dim, float scale, float drop_p, uint64_t seed, uint64_t site,
+                                 void* stream);
+int drt_dropout_add_bf16(const void* y, const void* resid, int64_t n, float p, uint64_t seed, uint64_t site,
+                         void* out, void* stream);
 int drt_pool_bf16(const void* hidden, const int64_t* mask, int64_t B, int64_t L, int32_t H,
                   int32_t mode, float* out, void* out_bf16, void* stream);
 int drt_l2_normalize_f32(float* x, int64_t B, int32_t H, void* out_bf16, void* stream);
