@@ -143,11 +143,33 @@ __global__ __launch_bounds__(256) void gelu_bwd_kernel(const __bf16* dy, const _
   }
 }
 
-// 64 x 64 tiles through LDS (padded rows: conflict-free column reads).
-__global__ __launch_bounds__(256) void transpose_bf16_kernel(const __bf16* x, int64_t R, int64_t C, __bf16* y) {
-  __shared__ __bf16 t[64][66];
+// 64 x 64 tiles through LDS.  Full tiles (R, C multiples of 8): 16-B global loads of input
+// rows and 16-B stores of output rows (8 lanes per 128-B output segment), LDS rows padded to
+// 144 B (16-B aligned); edge tiles take the element-wise path.  y has row stride ldy >= R.
+__global__ __launch_bounds__(256) void transpose_bf16_kernel(const __bf16* x, int64_t R, int64_t C, __bf16* y,
+                                                             int64_t ldy) {
+  __shared__ __attribute__((aligned(16))) __bf16 t[64][72];
   const int64_t r0 = (int64_t)blockIdx.y * 64, c0 = (int64_t)blockIdx.x * 64;
-  const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
+  const int tid = threadIdx.x;
+  const bool full = r0 + 64 <= R && c0 + 64 <= C && (C & 7) == 0 && (ldy & 7) == 0;
+  if (full) {
+#pragma unroll
+    for (int it = 0; it < 2; ++it) {
+      const int idx = tid + it * 256, row = idx >> 3, ch = idx & 7;
+      *(bf16x8*)&t[row][ch * 8] = *(const bf16x8*)(x + (r0 + row) * C + c0 + ch * 8);
+    }
+    __syncthreads();
+#pragma unroll
+    for (int it = 0; it < 2; ++it) {
+      const int idx = tid + it * 256, j = idx & 7, c = idx >> 3;   // output row c0 + c, rows r0 + 8j..+7
+      bf16x8 v;
+#pragma unroll
+      for (int u = 0; u < 8; ++u) v[u] = t[8 * j + u][c];
+      *(bf16x8*)(y + (c0 + c) * ldy + r0 + 8 * j) = v;
+    }
+    return;
+  }
+  const int tx = tid & 63, ty = tid >> 6;
   for (int i = ty; i < 64; i += 4) {
     const int64_t r = r0 + i, c = c0 + tx;
     t[i][tx] = (r < R && c < C) ? x[r * C + c] : (__bf16)0.0f;
@@ -155,7 +177,7 @@ __global__ __launch_bounds__(256) void transpose_bf16_kernel(const __bf16* x, in
   __syncthreads();
   for (int i = ty; i < 64; i += 4) {
     const int64_t c = c0 + i, r = r0 + tx;
-    if (c < C && r < R) y[c * R + r] = t[tx][i];
+    if (c < C && r < R) y[c * ldy + r] = t[tx][i];
   }
 }
 
@@ -563,14 +585,18 @@ int drt_dropout_add_bf16(const void* y, const void* resid, int64_t n, float p, u
   return hip_status(hipGetLastError());
 }
 
-int drt_transpose_bf16(const void* x, int64_t R, int64_t C, void* y, void* stream) {
-  DRT_REQUIRE(R >= 0 && C >= 0);
+int drt_transpose_bf16_ld(const void* x, int64_t R, int64_t C, void* y, int64_t ldy, void* stream) {
+  DRT_REQUIRE(R >= 0 && C >= 0 && ldy >= R);
   if (R == 0 || C == 0) return DRT_OK;
-  DRT_REQUIRE(x && y);
+  DRT_REQUIRE(x && y && ((uintptr_t)x % 16 == 0) && ((uintptr_t)y % 16 == 0));
   dim3 grid((unsigned)((C + 63) / 64), (unsigned)((R + 63) / 64));
   hipLaunchKernelGGL(transpose_bf16_kernel, grid, dim3(256), 0, (hipStream_t)stream, (const __bf16*)x, R, C,
-                     (__bf16*)y);
+                     (__bf16*)y, ldy);
   return hip_status(hipGetLastError());
+}
+
+int drt_transpose_bf16(const void* x, int64_t R, int64_t C, void* y, void* stream) {
+  return drt_transpose_bf16_ld(x, R, C, y, R, stream);
 }
 
 }  // extern "C"

@@ -262,6 +262,25 @@ static int small_splits(int64_t m, int64_t n, int64_t k, int64_t* kchunk) {
   return (int)splits;
 }
 
+// Split plan of the 256^2 kernel for long-K problems whose 256^2 grid is small (weight
+// gradients dW = dY^T X: K = tokens, M x N = a weight matrix): ~256 blocks, >= 16 slabs per
+// split, fp32 partials <= 256 MiB.  0 = no split.
+static int large_splits(int64_t m, int64_t n, int64_t k, int64_t min_tiles, int64_t* kchunk) {
+  const int64_t tiles = ((m + 255) / 256) * ((n + 255) / 256);
+  if (tiles >= min_tiles || k < 8192 || k % 32) return 0;
+  int64_t splits = (256 + tiles - 1) / tiles;
+  if (splits > k / 512) splits = k / 512;
+  const int64_t cap = (int64_t)(256ll << 20) / (m * n * 4);
+  if (splits > cap) splits = cap;
+  if (splits < 2) return 0;
+  int64_t kc = (k + splits - 1) / splits;
+  kc = (kc + 63) / 64 * 64;
+  splits = (k + kc - 1) / kc;
+  if (splits < 2) return 0;
+  *kchunk = kc;
+  return (int)splits;
+}
+
 // ---------------------------------------------------------------------------
 // Large-tile variant for the encoder projections (M = tokens >> 256).
 //  * 256 x 256 output tile, 8 waves (2 along M x 4 along N), wave tile 128 x 64.
@@ -816,7 +835,11 @@ __global__ __launch_bounds__(kLThreads, 1) void gemm_nt_pp1_kernel(GemmArgs a) {
   const int64_t n0 = (int64_t)tn * kL;
 
   const uint32_t lds0 = g_lds_addr(smem);
-  const int ns = (int)(a.k / 32);
+  // split-K (kchunk > 0, weight gradients: K = tokens): this block sums k in [kb, kb + kchunk) of
+  // split blockIdx.y and stores raw fp32 partials at C + blockIdx.y * m * ldc (splitk_epi_kernel finishes)
+  const int64_t kb = a.kchunk ? (int64_t)blockIdx.y * a.kchunk : 0;
+  const int64_t ke = a.kchunk ? (kb + a.kchunk < a.k ? kb + a.kchunk : a.k) : a.k;
+  const int ns = (int)((ke - kb) / 32);
   // ABL & 64 (diagnostic): every tile streams the panels of tile (0, 0) -> all L2 hits
   const int64_t dm0 = (ABL & 64) ? 0 : m0, dn0 = (ABL & 64) ? 0 : n0;
   unsigned long long st0 = 0, st1 = 0, st2 = 0;
@@ -837,8 +860,8 @@ __global__ __launch_bounds__(kLThreads, 1) void gemm_nt_pp1_kernel(GemmArgs a) {
 #pragma unroll
   for (int p = 0; p < D; ++p) {
     if (p < ns) {
-      stage_panel32(a.A, a.lda, dm0, a.m, p * 32, lds0 + p * kPSlab, wave, lane);
-      stage_panel32(a.B, a.ldb, dn0, a.n, p * 32, lds0 + p * kPSlab + kPPanel, wave, lane);
+      stage_panel32(a.A, a.lda, dm0, a.m, kb + p * 32, lds0 + p * kPSlab, wave, lane);
+      stage_panel32(a.B, a.ldb, dn0, a.n, kb + p * 32, lds0 + p * kPSlab + kPPanel, wave, lane);
     }
   }
   vmcnt_slabs_after(ns - 1 < D - 1 ? ns - 1 : D - 1);
@@ -874,8 +897,8 @@ __global__ __launch_bounds__(kLThreads, 1) void gemm_nt_pp1_kernel(GemmArgs a) {
     const int left = (ABL & 1) ? 0 : ns - 1 - s;   // slabs after s
     if (left >= D) {
       const uint32_t nslab = lds0 + fill * kPSlab;
-      stage_panel32(a.A, a.lda, dm0, a.m, (int64_t)(s + D) * 32, nslab, wave, lane);
-      stage_panel32(a.B, a.ldb, dn0, a.n, (int64_t)(s + D) * 32, nslab + kPPanel, wave, lane);
+      stage_panel32(a.A, a.lda, dm0, a.m, kb + (int64_t)(s + D) * 32, nslab, wave, lane);
+      stage_panel32(a.B, a.ldb, dn0, a.n, kb + (int64_t)(s + D) * 32, nslab + kPPanel, wave, lane);
       if (PRE && left == D && pre_on) {
         load_resid_half(a, m0, n0, grp, wn, 0, lane, rv0);
         vmcnt_slabs_after_plus(D - 1, RP);
@@ -917,10 +940,16 @@ __global__ __launch_bounds__(kLThreads, 1) void gemm_nt_pp1_kernel(GemmArgs a) {
   if (ABL & 32) st2 = __builtin_amdgcn_s_memtime();
   const bool full = (n0 + kL <= a.n) && (a.ldc % 8 == 0) && (!(EPI & EPI_RESID) || a.ldr % 4 == 0);
   if (full) {
-    if (pre_on) pp_epilogue_lds<OUT_BF16, EPI, true>(a, acc, m0, n0, grp, wn, fr, fc, smem + wave * 16384, lane, rv0);
-    else pp_epilogue_lds<OUT_BF16, EPI, false>(a, acc, m0, n0, grp, wn, fr, fc, smem + wave * 16384, lane, rv0);
+    GemmArgs ae = a;
+    if (a.kchunk) ae.C = (float*)a.C + (int64_t)blockIdx.y * a.m * a.ldc;
+    if (pre_on) pp_epilogue_lds<OUT_BF16, EPI, true>(ae, acc, m0, n0, grp, wn, fr, fc, smem + wave * 16384, lane, rv0);
+    else pp_epilogue_lds<OUT_BF16, EPI, false>(ae, acc, m0, n0, grp, wn, fr, fc, smem + wave * 16384, lane, rv0);
   }
-  else pp_epilogue<OUT_BF16, EPI>(a, acc, m0, n0, grp, wn, fr, fc);
+  else {
+    GemmArgs ae = a;
+    if (a.kchunk) ae.C = (float*)a.C + (int64_t)blockIdx.y * a.m * a.ldc;
+    pp_epilogue<OUT_BF16, EPI>(ae, acc, m0, n0, grp, wn, fr, fc);
+  }
   if (ABL & 32) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     const unsigned long long st3 = __builtin_amdgcn_s_memtime();
@@ -942,6 +971,7 @@ static int launch_gemm_t(const GemmArgs& a0, hipStream_t s) {
   const ProfPair pp = prof_begin(PROF_GEMM, s);
   // large tiles once there are >= 2 tiles per CU of them; small problems keep 128^2
   const int64_t tiles_l = ((a.m + kL - 1) / kL) * ((a.n + kL - 1) / kL);
+  int64_t kc_l = 0;
   if (tiles_l >= g_large_min_tiles && g_gemm_variant == 0) {
     hipLaunchKernelGGL((gemm_nt_pp1_kernel<OUT_BF16, EPI, 0, 5>), dim3((unsigned)tiles_l), dim3(kLThreads), 0, s, a);
   } else if (tiles_l >= 512 && g_gemm_variant == 9) {
@@ -965,6 +995,23 @@ static int launch_gemm_t(const GemmArgs& a0, hipStream_t s) {
     hipLaunchKernelGGL((gemm_nt_pp1_kernel<OUT_BF16, EPI>), dim3((unsigned)tiles_l), dim3(kLThreads), 0, s, a);
   } else if (tiles_l >= 512 && g_gemm_variant == 8) {
     hipLaunchKernelGGL((gemm_nt_pp1_kernel<OUT_BF16, EPI, 0, 5>), dim3((unsigned)tiles_l), dim3(kLThreads), 0, s, a);
+  } else if (g_gemm_variant == 0 && a.ws && large_splits(a.m, a.n, a.k, g_large_min_tiles, &kc_l) > 1) {
+    // long K, small output (weight gradients): split K over the 256^2 kernel, then one
+    // fixed-order reduction applying the epilogue
+    const int splits = large_splits(a.m, a.n, a.k, g_large_min_tiles, &kc_l);
+    GemmArgs b = a;
+    b.kchunk = kc_l;
+    b.C = a.ws;
+    b.ldc = a.n;
+    b.bias = nullptr;
+    b.R = nullptr;
+    b.alpha = 1.0f;
+    hipLaunchKernelGGL((gemm_nt_pp1_kernel<false, EPI_NONE, 0, 5>), dim3((unsigned)tiles_l, (unsigned)splits),
+                       dim3(kLThreads), 0, s, b);
+    GemmArgs e = a;
+    const int64_t units = (a.n % 4 == 0) ? a.m * a.n / 4 : a.m * a.n;
+    const int64_t blocks = (units + 255) / 256 < 4096 ? (units + 255) / 256 : 4096;
+    hipLaunchKernelGGL((splitk_epi_kernel<OUT_BF16, EPI>), dim3((unsigned)blocks), dim3(256), 0, s, e, splits);
   } else {
     const int64_t tiles = ((a.m + kBM - 1) / kBM) * ((a.n + kBN - 1) / kBN);
     int64_t kc = 0;
@@ -1038,6 +1085,8 @@ extern "C" size_t drt_linear_workspace(int64_t M, int64_t N, int64_t K) {
   const int64_t tiles_l = ((M + kL - 1) / kL) * ((N + kL - 1) / kL);
   if (tiles_l >= g_large_min_tiles) return 0;   // the 256^2 path does not split
   int64_t kc = 0;
+  const int ls = large_splits(M, N, K, g_large_min_tiles, &kc);
+  if (ls > 1) return (size_t)ls * (size_t)M * (size_t)N * sizeof(float);
   const int splits = small_splits(M, N, K, &kc);
   return splits > 1 ? (size_t)splits * (size_t)M * (size_t)N * sizeof(float) : 0;
 }

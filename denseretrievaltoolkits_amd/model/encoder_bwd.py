@@ -37,13 +37,8 @@ def transpose_bf16(x: torch.Tensor, cols_pad: int = 0) -> torch.Tensor:
     y = torch.empty((C, R + cols_pad), dtype=torch.bfloat16, device=x.device)
     if cols_pad:
         y[:, R:].zero_()
-        tmp = torch.empty((C, R), dtype=torch.bfloat16, device=x.device)
-        _native.check(lib.drt_transpose_bf16(x.data_ptr(), R, C, tmp.data_ptr(), _native.stream_ptr(x.device)),
-                      "drt_transpose_bf16")
-        y[:, :R] = tmp
-        return y
-    _native.check(lib.drt_transpose_bf16(x.data_ptr(), R, C, y.data_ptr(), _native.stream_ptr(x.device)),
-                  "drt_transpose_bf16")
+    _native.check(lib.drt_transpose_bf16_ld(x.data_ptr(), R, C, y.data_ptr(), R + cols_pad,
+                                            _native.stream_ptr(x.device)), "drt_transpose_bf16_ld")
     return y
 
 

@@ -194,6 +194,8 @@ int drt_colsum_bf16(const void* x, int64_t M, int64_t N, float* out, void* ws, s
                     void* stream);
 int drt_gelu_bwd_bf16(const void* dy, const void* pre, int64_t n, void* dx, void* stream);
 int drt_transpose_bf16(const void* x, int64_t R, int64_t C, void* y, void* stream);
+/* drt_transpose_bf16_ld: the same into y with row stride ldy >= R (padded GEMM operands). */
+int drt_transpose_bf16_ld(const void* x, int64_t R, int64_t C, void* y, int64_t ldy, void* stream);
 /* drt_attention_bwd_bf16: dqkv [B*L, 3H] (dQ | dK | dV in qkv's packed layout) of the
  * attention forward, from qkv, its ctx = O, dctx = dO, the forward's lse and the key mask;
  * L <= 128, head_dim 64 (BertSelfAttention under autograd, modeling_bert.py:164-204).   */

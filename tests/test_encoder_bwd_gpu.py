@@ -173,3 +173,34 @@ def test_attention_bwd_vs_torch(dev, B, L):
         assert err <= 2e-2 * max(1.0, want.abs().max().item()), (name, err, want.abs().max().item())
         cos = torch.nn.functional.cosine_similarity(got.flatten(), want.flatten(), dim=0).item()
         assert cos > 0.999, (name, cos)
+
+
+@pytest.mark.parametrize("R,C,pad", [(1000, 768, 24), (65536, 3072, 0), (77, 130, 3)])
+def test_transpose_bf16_ld(dev, R, C, pad):
+    import torch
+    from denseretrievaltoolkits_amd import _native
+    lib = _native.load()
+    x = torch.randn(R, C, device=dev).to(torch.bfloat16)
+    y = torch.full((C, R + pad), 7.0, dtype=torch.bfloat16, device=dev)
+    _native.check(lib.drt_transpose_bf16_ld(x.data_ptr(), R, C, y.data_ptr(), R + pad, _native.stream_ptr(dev)), "t")
+    assert torch.equal(y[:, :R], x.t())
+    assert bool((y[:, R:] == 7.0).all())
+
+
+@pytest.mark.parametrize("M,N,K", [(2304, 768, 65536), (768, 3072, 16384), (3072, 768, 131072)])
+def test_long_k_split_gemm_vs_torch(dev, M, N, K):
+    """Weight-gradient shapes (K = tokens): the 256^2 kernel split over K + fixed-order reduction."""
+    import torch
+    from denseretrievaltoolkits_amd import _native
+    lib = _native.load()
+    nb = int(lib.drt_linear_workspace(M, N, K))
+    assert nb > 0
+    g = torch.Generator(device=dev).manual_seed(M + K)
+    a = (0.1 * torch.randn(M, K, generator=g, device=dev)).to(torch.bfloat16)
+    b = (0.1 * torch.randn(N, K, generator=g, device=dev)).to(torch.bfloat16)
+    ws = torch.empty((nb + 3) // 4, device=dev)
+    out = torch.empty(M, N, device=dev)
+    _native.check(lib.drt_linear_bf16_ws(a.data_ptr(), b.data_ptr(), None, None, out.data_ptr(), M, N, K, 2,
+                                         ws.data_ptr(), nb, _native.stream_ptr(dev)), "split gemm")
+    ref = a.float() @ b.float().T
+    torch.testing.assert_close(out, ref, atol=2e-3 * (K / 4096) ** 0.5, rtol=1e-3)
