@@ -86,10 +86,22 @@ __global__ __launch_bounds__(256) void embed_ln_kernel(const int64_t* ids, const
 
 // erf GELU, elementwise (the training forward keeps FFN1's pre-activation for the backward)
 __global__ __launch_bounds__(256) void gelu_kernel(const __bf16* x, int64_t n, __bf16* y) {
-  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
-  if (i < n) {
-    const float v = (float)x[i];
-    y[i] = (__bf16)(0.5f * v * (1.0f + erff(v * 0.70710678118654752f)));
+  const int64_t i8 = ((int64_t)blockIdx.x * 256 + threadIdx.x) * 8;
+  if (i8 >= n) return;
+  if (i8 + 8 <= n) {   // 16-B pieces
+    const bf16x8 xv = *(const bf16x8*)(x + i8);
+    bf16x8 o;
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const float v = (float)xv[u];
+      o[u] = (__bf16)(0.5f * v * (1.0f + erff(v * 0.70710678118654752f)));
+    }
+    *(bf16x8*)(y + i8) = o;
+  } else {
+    for (int64_t i = i8; i < n; ++i) {
+      const float v = (float)x[i];
+      y[i] = (__bf16)(0.5f * v * (1.0f + erff(v * 0.70710678118654752f)));
+    }
   }
 }
 
@@ -409,7 +421,8 @@ int drt_gelu_bf16(const void* x, int64_t n, void* y, void* stream) {
   DRT_REQUIRE(n >= 0);
   if (n == 0) return DRT_OK;
   DRT_REQUIRE(x && y);
-  hipLaunchKernelGGL(gelu_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, (hipStream_t)stream,
+  DRT_REQUIRE((uintptr_t)x % 16 == 0 && (uintptr_t)y % 16 == 0);
+  hipLaunchKernelGGL(gelu_kernel, dim3((unsigned)((n + 2047) / 2048)), dim3(256), 0, (hipStream_t)stream,
                      (const __bf16*)x, n, (__bf16*)y);
   return hip_status(hipGetLastError());
 }

@@ -449,19 +449,47 @@ __global__ __launch_bounds__(kAbThreads) void attention_bwd_kernel(AttnBwdArgs a
 // by 1 / (1 - p).  The same call on a gradient (resid = NULL) is the dropout backward.
 __global__ __launch_bounds__(256) void dropout_add_kernel(const __bf16* y, const __bf16* resid, int64_t n, float p,
                                                           uint64_t seed, uint64_t site, __bf16* out) {
-  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
-  if (i >= n) return;
-  const bool keep = drop_hash24(seed, site, (uint64_t)i) >= drop_threshold(p);
-  float v = keep ? (float)y[i] / (1.0f - p) : 0.0f;
-  if (resid) v += (float)resid[i];
-  out[i] = (__bf16)v;
+  const int64_t i8 = ((int64_t)blockIdx.x * 256 + threadIdx.x) * 8;
+  if (i8 >= n) return;
+  const uint32_t thr = drop_threshold(p);
+  const float inv = 1.0f / (1.0f - p);
+  if (i8 + 8 <= n) {   // 16-B pieces
+    const bf16x8 yv = *(const bf16x8*)(y + i8);
+    bf16x8 rv = {};
+    if (resid) rv = *(const bf16x8*)(resid + i8);
+    bf16x8 o;
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const bool keep = drop_hash24(seed, site, (uint64_t)(i8 + u)) >= thr;
+      float v = keep ? (float)yv[u] * inv : 0.0f;
+      if (resid) v += (float)rv[u];
+      o[u] = (__bf16)v;
+    }
+    *(bf16x8*)(out + i8) = o;
+  } else {
+    for (int64_t i = i8; i < n; ++i) {
+      const bool keep = drop_hash24(seed, site, (uint64_t)i) >= thr;
+      float v = keep ? (float)y[i] * inv : 0.0f;
+      if (resid) v += (float)resid[i];
+      out[i] = (__bf16)v;
+    }
+  }
 }
 
-static int64_t colsum_slabs(int64_t M) { return M < 256 ? 1 : (M + 255) / 256 < 512 ? (M + 255) / 256 : 512; }
+// Row slabs of the first colsum pass: enough blocks to fill the chip (~1024 with the
+// column blocks), >= 16 rows per slab, <= 1024 slabs (the second pass sums them in order).
+static int64_t colsum_slabs(int64_t M, int64_t N) {
+  if (M < 256) return 1;
+  const int64_t gx = (N + 255) / 256;
+  int64_t slabs = (1024 + gx - 1) / gx;
+  if (slabs > M / 16) slabs = M / 16;
+  if (slabs > 1024) slabs = 1024;
+  return slabs < 1 ? 1 : slabs;
+}
 
 template <typename T>
 static int colsum_launch(const T* x, int64_t M, int64_t N, float* out, float* ws, hipStream_t s) {
-  const int64_t slabs = colsum_slabs(M);
+  const int64_t slabs = colsum_slabs(M, N);
   const int64_t rows_per = (M + slabs - 1) / slabs;
   const unsigned gx = (unsigned)((N + 255) / 256);
   if (slabs == 1) {
@@ -481,7 +509,7 @@ extern "C" {
 
 size_t drt_colsum_workspace(int64_t M, int64_t N) {
   if (M <= 0 || N <= 0) return 0;
-  const int64_t slabs = colsum_slabs(M);
+  const int64_t slabs = colsum_slabs(M, N);
   return slabs > 1 ? (size_t)slabs * (size_t)N * sizeof(float) : 0;
 }
 
@@ -580,7 +608,8 @@ int drt_dropout_add_bf16(const void* y, const void* resid, int64_t n, float p, u
   DRT_REQUIRE(n >= 0 && p >= 0.0f && p < 1.0f);
   if (n == 0) return DRT_OK;
   DRT_REQUIRE(y && out);
-  hipLaunchKernelGGL(dropout_add_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, (hipStream_t)stream,
+  DRT_REQUIRE((uintptr_t)y % 16 == 0 && (uintptr_t)out % 16 == 0 && (!resid || (uintptr_t)resid % 16 == 0));
+  hipLaunchKernelGGL(dropout_add_kernel, dim3((unsigned)((n + 2047) / 2048)), dim3(256), 0, (hipStream_t)stream,
                      (const __bf16*)y, (const __bf16*)resid, n, p, seed, site, (__bf16*)out);
   return hip_status(hipGetLastError());
 }
