@@ -333,6 +333,8 @@ def main():
         out["query_encode"] = bench_encode.run_query_encode(dev)
         out["train_scores"] = bench_encode.run_train_scores(dev)
         out["train_step"] = bench_encode.run_train_step(dev)
+        # the reference recipe's shapes (run.sh:16-19: train_n_passages 8, p_max_len 156) at batch 128
+        out["train_step_recipe"] = bench_encode.run_train_step(dev, bq=128, n=8, p_len=156)
     if rank == 0:
         print(json.dumps(out), flush=True)
     if world > 1:

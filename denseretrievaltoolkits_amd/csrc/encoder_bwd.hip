@@ -10,7 +10,7 @@
 //   colsum          out[n] = sum_rows x[row][n] in a fixed order (bias / LN parameter grads)
 //   gelu_bwd        dx = dy (Phi(x) + x phi(x))      (erf GELU, activations.py:70-90)
 //   transpose_bf16  y[c][r] = x[r][c]                 (operand layout for weight gradients)
-//   attention_bwd   dQ, dK, dV of softmax(Q K^T / sqrt(dh) + mask) V  (L <= 128)
+//   attention_bwd   dQ, dK, dV of softmax(Q K^T / sqrt(dh) + mask) V  (L <= 160)
 #include "drt_common.h"
 
 namespace drt {
@@ -183,22 +183,26 @@ __global__ __launch_bounds__(256) void transpose_bf16_kernel(const __bf16* x, in
 
 // ---------------------------------------------------------------------------
 // Attention backward (BertSelfAttention, modeling_bert.py:164-204, under autograd), one
-// work-group (4 waves) per (sequence, head), L <= 128, head_dim 64.  With Qs = scale * Q
-// (rounded to bf16 as the forward does), S = Qs K^T + key bias, P = exp(S - lse):
+// work-group (4 waves) per (sequence, head), L <= 160 (the reference recipe's p_max_len 156,
+// run.sh), head_dim 64.  With Qs = scale * Q (rounded to bf16 as the forward does),
+// S = Qs K^T + key bias, P = exp(S - lse):
 //   Dv_q = sum_d dO[q][d] O[q][d];   dP = dO V^T;   dS = P (dP - Dv)
 //   dV = P^T dO;   dK = dS^T Qs;   dQ = scale * dS K.
 // LDS: Qs, K, V, dO row-major [Lp][64] (16-B chunk XOR (row >> 1) & 7, as the forward's
-// K image) and Qs^T, K^T, dO^T as [64][128] (chunk XOR (d & 15)), so every MFMA operand is
-// one conflict-free ds_read_b128 of a row; per-wave 32 x 32 scratch tiles (80-B rows) turn
-// the P / dS accumulators (rows in registers) into A operands.  Phase 1: wave w owns key
-// block w (dK, dV over all query blocks); phase 2: wave w owns query block w (dQ over all
-// key blocks, S and dP recomputed).  v_mfma_f32_32x32x16_bf16 throughout.
+// K image) and Qs^T, K^T, dO^T as [64][Lp] with rows padded by 16 B (an odd number of 16-B
+// chunks per row, so the 16-B pieces of consecutive d land on distinct banks), so every MFMA
+// operand is one conflict-free ds_read_b128; one per-wave 32 x 32 scratch tile (80-B rows)
+// turns the P and then the dS accumulator (rows in registers) into A operands.  Phase 1:
+// wave w owns key blocks w, w + 4 (dK, dV over all query blocks); phase 2: wave w owns query
+// blocks w, w + 4 (dQ over all key blocks, S and dP recomputed).  v_mfma_f32_32x32x16_bf16
+// throughout.  155 KiB of LDS at L = 160.
 // ---------------------------------------------------------------------------
 constexpr int kAbThreads = 256;
-constexpr int kAbMaxSeq = 128;
+constexpr int kAbMaxSeq = 160;
 constexpr int kAbRow = 128;               // bytes per [.][64] bf16 row
-constexpr int kAbTRow = 256;              // bytes per [64][128] transposed row
 constexpr int kAbScr = 80;                // bytes per scratch row (32 bf16 + 16 B pad)
+
+__host__ __device__ constexpr int ab_tstride(int Lp) { return 2 * Lp + 16; }   // bytes per [64][Lp] row
 
 struct AttnBwdArgs {
   const __bf16* qkv;     // [B*L][3H]
@@ -215,7 +219,6 @@ struct AttnBwdArgs {
 };
 
 __device__ __forceinline__ int ab_rc(int row, int chunk) { return row * kAbRow + ((chunk ^ ((row >> 1) & 7)) << 4); }
-__device__ __forceinline__ int ab_tc(int d, int chunk) { return d * kAbTRow + ((chunk ^ (d & 15)) << 4); }
 
 __global__ __launch_bounds__(kAbThreads) void attention_bwd_kernel(AttnBwdArgs a) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -225,11 +228,12 @@ __global__ __launch_bounds__(kAbThreads) void attention_bwd_kernel(AttnBwdArgs a
   char* Ks = Qs + Lp * kAbRow;
   char* Vs = Ks + Lp * kAbRow;
   char* Os = Vs + Lp * kAbRow;                       // dO
-  char* QT = Os + Lp * kAbRow;                       // [64][128]
-  char* KT = QT + 64 * kAbTRow;
-  char* OT = KT + 64 * kAbTRow;                      // dO^T
-  char* scr = OT + 64 * kAbTRow;                     // [4 waves][2][32][80 B]
-  float* lse = (float*)(scr + 4 * 2 * 32 * kAbScr);  // [Lp]
+  const int ts = ab_tstride(Lp);
+  char* QT = Os + Lp * kAbRow;                       // [64][Lp] (+16 B per row)
+  char* KT = QT + 64 * ts;
+  char* OT = KT + 64 * ts;                           // dO^T
+  char* scr = OT + 64 * ts;                          // [4 waves][32][80 B]
+  float* lse = (float*)(scr + 4 * 32 * kAbScr);      // [Lp]
   float* dv = lse + Lp;                              // [Lp]  Dv
   float* kb = dv + Lp;                               // [Lp]  key bias
 
@@ -269,7 +273,7 @@ __global__ __launch_bounds__(kAbThreads) void attention_bwd_kernel(AttnBwdArgs a
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
       const int d = c * 8 + j;
-      const int off = ab_tc(d, row >> 3) + (row & 7) * 2;
+      const int off = d * ts + row * 2;
       *(__bf16*)(QT + off) = q[j];
       *(__bf16*)(KT + off) = k[j];
       *(__bf16*)(OT + off) = o[j];
@@ -293,8 +297,7 @@ __global__ __launch_bounds__(kAbThreads) void attention_bwd_kernel(AttnBwdArgs a
   const bool drop = a.drop_p > 0.0f;
   const float inv = drop ? 1.0f / (1.0f - a.drop_p) : 1.0f;
   const uint32_t thr = drop_threshold(a.drop_p);
-  char* sP = scr + (wave * 2 + 0) * 32 * kAbScr;
-  char* sS = scr + (wave * 2 + 1) * 32 * kAbScr;
+  char* sT = scr + wave * 32 * kAbScr;   // P, then dS (phase 1); dS (phase 2)
 
   // ---- phase 1: dK, dV for key block kbk (rows = keys in the D layout, cols = q / d)
   for (int kbk = wave; kbk < nblk; kbk += 4) {
@@ -329,6 +332,7 @@ __global__ __launch_bounds__(kAbThreads) void attention_bwd_kernel(AttnBwdArgs a
       // O = Pd V where Pd = mask P / (1 - p): dV takes Pd, and dS = P (mask dPd / (1 - p) - Dv)
       const float lq = lse[qcol], dq = dv[qcol];
       const uint64_t dbase = (((uint64_t)b * a.heads + hd) * L + qcol) * (uint64_t)L;
+      float ds[16];
 #pragma unroll
       for (int e = 0; e < 16; ++e) {
         const int kr = (e & 3) + 8 * (e >> 2) + 4 * h;
@@ -340,23 +344,37 @@ __global__ __launch_bounds__(kAbThreads) void attention_bwd_kernel(AttnBwdArgs a
           pd = keep ? p * inv : 0.f;
           dpe = keep ? dpe * inv : 0.f;
         }
-        const float ds = p * (dpe - dq);
-        *(__bf16*)(sP + kr * kAbScr + r * 2) = (__bf16)pd;
-        *(__bf16*)(sS + kr * kAbScr + r * 2) = (__bf16)ds;
+        ds[e] = p * (dpe - dq);
+        *(__bf16*)(sT + kr * kAbScr + r * 2) = (__bf16)pd;
       }
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
       __builtin_amdgcn_wave_barrier();
 #pragma unroll
       for (int ks = 0; ks < 2; ++ks) {
-        const bf16x8 pa = *(const bf16x8*)(sP + r * kAbScr + (2 * ks + h) * 16);
-        const bf16x8 sa = *(const bf16x8*)(sS + r * kAbScr + (2 * ks + h) * 16);
-        const int qc = (qb * 32 + 16 * ks + 8 * h) >> 3;
+        const bf16x8 pa = *(const bf16x8*)(sT + r * kAbScr + (2 * ks + h) * 16);
+        const int qc = qb * 32 + 16 * ks + 8 * h;
 #pragma unroll
         for (int t = 0; t < 2; ++t) {
-          const int d = 32 * t + r;
-          const bf16x8 ob = *(const bf16x8*)(OT + ab_tc(d, qc));
-          const bf16x8 qbt = *(const bf16x8*)(QT + ab_tc(d, qc));
+          const bf16x8 ob = *(const bf16x8*)(OT + (32 * t + r) * ts + qc * 2);
           dV[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(pa, ob, dV[t], 0, 0, 0);
+        }
+      }
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+#pragma unroll
+      for (int e = 0; e < 16; ++e) {
+        const int kr = (e & 3) + 8 * (e >> 2) + 4 * h;
+        *(__bf16*)(sT + kr * kAbScr + r * 2) = (__bf16)ds[e];
+      }
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks) {
+        const bf16x8 sa = *(const bf16x8*)(sT + r * kAbScr + (2 * ks + h) * 16);
+        const int qc = qb * 32 + 16 * ks + 8 * h;
+#pragma unroll
+        for (int t = 0; t < 2; ++t) {
+          const bf16x8 qbt = *(const bf16x8*)(QT + (32 * t + r) * ts + qc * 2);
           dK[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(sa, qbt, dK[t], 0, 0, 0);
         }
       }
@@ -416,17 +434,17 @@ __global__ __launch_bounds__(kAbThreads) void attention_bwd_kernel(AttnBwdArgs a
           const bool keep = kcol < L && q < L && drop_hash24(a.seed, a.site, idx) >= thr;
           dpe = keep ? dpe * inv : 0.f;
         }
-        *(__bf16*)(sS + qr * kAbScr + r * 2) = (__bf16)(p * (dpe - dv[q]));
+        *(__bf16*)(sT + qr * kAbScr + r * 2) = (__bf16)(p * (dpe - dv[q]));
       }
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
       __builtin_amdgcn_wave_barrier();
 #pragma unroll
       for (int ks = 0; ks < 2; ++ks) {
-        const bf16x8 sa = *(const bf16x8*)(sS + r * kAbScr + (2 * ks + h) * 16);
-        const int kc = (kbk * 32 + 16 * ks + 8 * h) >> 3;
+        const bf16x8 sa = *(const bf16x8*)(sT + r * kAbScr + (2 * ks + h) * 16);
+        const int kc = kbk * 32 + 16 * ks + 8 * h;
 #pragma unroll
         for (int t = 0; t < 2; ++t) {
-          const bf16x8 kt = *(const bf16x8*)(KT + ab_tc(32 * t + r, kc));
+          const bf16x8 kt = *(const bf16x8*)(KT + (32 * t + r) * ts + kc * 2);
           dQ[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(sa, kt, dQ[t], 0, 0, 0);
         }
       }
@@ -565,7 +583,7 @@ int drt_gelu_bwd_bf16(const void* dy, const void* pre, int64_t n, void* dx, void
 }
 
 // dqkv [B*L][3H] (dQ | dK | dV, head-major like qkv) of the attention forward
-// (drt_attention_fwd_lse_bf16) given dctx = dO, the forward's ctx = O and lse.  L <= 128.
+// (drt_attention_fwd_lse_bf16) given dctx = dO, the forward's ctx = O and lse.  L <= 160.
 int drt_attention_train_bwd_bf16(const void* qkv, const void* ctx, const void* dctx, const float* lse,
                                  const int64_t* mask, void* dqkv, int64_t B, int64_t L, int32_t heads,
                                  int32_t head_dim, float scale, float drop_p, uint64_t seed, uint64_t site,
@@ -591,8 +609,9 @@ int drt_attention_train_bwd_bf16(const void* qkv, const void* ctx, const void* d
   AttnBwdArgs a{(const __bf16*)qkv, (const __bf16*)ctx, (const __bf16*)dctx, lse, mask, (__bf16*)dqkv, B, L,
                 heads, heads * 64, scale, drop_p, seed, site};
   const int Lp = ((int)L + 31) & ~31;
-  const size_t lds = (size_t)4 * Lp * kAbRow + (size_t)3 * 64 * kAbTRow + (size_t)8 * 32 * kAbScr +
+  const size_t lds = (size_t)4 * Lp * kAbRow + (size_t)3 * 64 * ab_tstride(Lp) + (size_t)4 * 32 * kAbScr +
                      (size_t)3 * Lp * 4;
+  DRT_REQUIRE(lds <= 160 * 1024);
   static bool attr_set = false;
   if (!attr_set) {
     DRT_CHECK_HIP(hipFuncSetAttribute((const void*)attention_bwd_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,

@@ -17,7 +17,8 @@ each keep is a counter-based hash of (per-call seed, site, element index) (csrc/
 drop_hash24), so the backward regenerates the forward's masks instead of storing them; the
 seed comes from torch's CPU generator (``torch.manual_seed`` makes a step reproducible).  The
 masks are not HF's Philox stream: same distribution and semantics, different draws.
-Scope: L <= 128, erf GELU, head_dim 64; anything else raises.
+Scope: L <= 160 (the reference recipe's p_max_len is 156, run.sh), erf GELU, head_dim 64; anything else
+raises.
 """
 from __future__ import annotations
 
@@ -29,7 +30,7 @@ from .. import _native
 from .encoder import BertShape, _check_supported
 from .encoder_bwd import _ptr, gelu_backward, layernorm_backward, linear_backward
 
-MAX_TRAIN_SEQ = 128
+MAX_TRAIN_SEQ = 160
 
 
 def tower_supported(model) -> Optional[str]:

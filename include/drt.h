@@ -198,7 +198,7 @@ int drt_transpose_bf16(const void* x, int64_t R, int64_t C, void* y, void* strea
 int drt_transpose_bf16_ld(const void* x, int64_t R, int64_t C, void* y, int64_t ldy, void* stream);
 /* drt_attention_bwd_bf16: dqkv [B*L, 3H] (dQ | dK | dV in qkv's packed layout) of the
  * attention forward, from qkv, its ctx = O, dctx = dO, the forward's lse and the key mask;
- * L <= 128, head_dim 64 (BertSelfAttention under autograd, modeling_bert.py:164-204).   */
+ * L <= 160, head_dim 64 (BertSelfAttention under autograd, modeling_bert.py:164-204).   */
 /* drt_embed_ln_pre: drt_embed_ln that also writes the bf16 pre-LN sum (word + type + pos).
  * drt_gelu_bf16: y = GELU(x) elementwise (erf form).
  * drt_embedding_bwd: scatter-add of d [B*L, H] (gradient of the pre-LN embedding sum) into

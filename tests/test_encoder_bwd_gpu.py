@@ -135,7 +135,7 @@ def test_linear_backward_vs_torch(dev, T, N, K):
     torch.testing.assert_close(db, bf.grad, atol=tol, rtol=1e-4)
 
 
-@pytest.mark.parametrize("B,L", [(4, 128), (3, 50), (6, 32), (2, 100)])
+@pytest.mark.parametrize("B,L", [(4, 128), (3, 50), (6, 32), (2, 100), (3, 156), (2, 160), (2, 129)])
 def test_attention_bwd_vs_torch(dev, B, L):
     """drt_attention_bwd_bf16 (dQ | dK | dV) against torch fp32 autograd of the same attention
     (scaled scores + HF key mask, softmax, P V) on the same bf16 qkv, with padded sequences."""

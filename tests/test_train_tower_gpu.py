@@ -21,7 +21,7 @@ def _bert(layers, seed, dev):
     return m.to(dev)
 
 
-@pytest.mark.parametrize("layers,B,L", [(2, 4, 64), (1, 8, 128), (2, 6, 32)])
+@pytest.mark.parametrize("layers,B,L", [(2, 4, 64), (1, 8, 128), (2, 6, 32), (1, 4, 156)])
 def test_tower_grads_vs_hf_autograd(dev, layers, B, L):
     import torch
     from denseretrievaltoolkits_amd.model.train_tower import train_hidden
@@ -70,8 +70,8 @@ def test_tower_rejects_unsupported(dev):
     from transformers import BertModel
     from denseretrievaltoolkits_amd.model.train_tower import train_hidden
     m = BertModel(bw.bert_config(layers=1), add_pooling_layer=False).to(dev)
-    with pytest.raises(ValueError):                      # attention backward holds L <= 128 in LDS
-        train_hidden(m, torch.ones((1, 129), dtype=torch.int64, device=dev), None)
+    with pytest.raises(ValueError):                      # attention backward holds L <= 160 in LDS
+        train_hidden(m, torch.ones((1, 161), dtype=torch.int64, device=dev), None)
 
 
 def test_gelu_forward_vs_torch(dev):
@@ -171,7 +171,7 @@ def _ref_forward_with_masks(m, ids, mask, ph, pa, seed):
     return x
 
 
-@pytest.mark.parametrize("layers,B,L", [(2, 4, 64), (1, 6, 128)])
+@pytest.mark.parametrize("layers,B,L", [(2, 4, 64), (1, 6, 128), (1, 3, 156)])
 def test_tower_with_dropout_vs_masked_fp32_reference(dev, layers, B, L):
     """Train-mode tower with HF's default dropout (0.1 / 0.1) against a functional fp32 BERT under
     autograd that applies the SAME hash masks: hidden states and every parameter gradient."""
