@@ -164,7 +164,7 @@ def main():
     from denseretrievaltoolkits_amd import _native, kernels
 
     lib = _native.load()
-    lib.drt_scan_variant(args.scan_variant)
+    _native.check(lib.drt_scan_variant(args.scan_variant), "drt_scan_variant")
     d, k, qb = args.dim, args.k, args.qb
     shard, lo, hi = gen_shard(args.n_corpus, world, rank, d, dev)
     n_local = hi - lo

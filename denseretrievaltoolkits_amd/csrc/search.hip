@@ -394,7 +394,8 @@ __device__ __forceinline__ void wait_tiles_younger(int younger) {
 }
 
 // ABL (benchmark ablations, FILTER only): 0 production, 1 no MFMA and no filter,
-// 2 MFMA on register operands (no LDS fragment reads), 3 no filter.
+// 2 MFMA on register operands (no LDS fragment reads), 3 no filter, 4 LDS fragment reads
+// only (no MFMA, no filter), 5 MFMA on register operands, no filter.
 template <int D, int MODE, int ABL = 0, int NW = 4, bool AGG = true>
 __global__ __launch_bounds__(NW * 64, 1) void ip_scan16_kernel(ScanArgs a) {
   using C = Scan16Cfg<D, NW>;
@@ -467,35 +468,23 @@ __global__ __launch_bounds__(NW * 64, 1) void ip_scan16_kernel(ScanArgs a) {
 #pragma unroll
   for (int m = 0; m < 2; ++m) aoff[m] = r * 128 + (((4 * m + kq) ^ sw) << 4);
 
-  int buf = 0;
-  int nslot = C::PD;   // slot of tile it + PD (== slot of it - 1)
-  for (int64_t it = 0; it < my_tiles; ++it) {
-    const int64_t tile = t0 + it * tstep;
-    const int64_t younger = my_tiles - 1 - it;
-    wait_tiles_younger<C::GLDS_PER_WAVE>((int)(younger < C::PD - 1 ? younger : C::PD - 1));
-    lds_barrier();
-
-    if (MODE == SCAN_FILTER) {
-      const uint32_t n = *hit_n;
-      if (n >= (uint32_t)(kHitCap / 2)) {
-        if (AGG) flush_hits_agg<NW * 64>(a, qbase, n, hk, hq, qcnt, qoff);
-        else flush_hits<NW * 64>(a, qbase, n, hk, hq);
-        lds_barrier();
-        if (tid == 0) *hit_n = 0;
-        lds_barrier();
-      }
-    }
-    if (it + C::PD < my_tiles)
-      issue_tile16<D, NW>(a, ring + nslot * C::TILE_BYTES, tile + C::PD * tstep, wave, lane);
-
-    const char* tb = smem + buf * C::TILE_BYTES;
-    f32x4 acc[QB];
+  // The epilogue (filter / key stores) of tile it runs after the MFMAs of tile it + 1 are
+  // issued (two accumulator sets, alternating): its VALU work and the wait for the last MFMA
+  // result overlap the next tile's matrix work instead of stalling the wave at every tile.
+  auto mma_tile = [&](f32x4 (&acc)[QB], int buf_) {
+    const char* tb = smem + buf_ * C::TILE_BYTES;
 #pragma unroll
     for (int b = 0; b < QB; ++b) acc[b] = (f32x4){0.f, 0.f, 0.f, 0.f};
     if (ABL == 1) {
       const bf16x8 af = *(const bf16x8*)(tb + aoff[0]);
       asm volatile("" ::"v"(af));
-    } else if (ABL == 2) {
+    } else if (ABL == 4) {
+#pragma unroll
+      for (int s = 0; s < C::KS; ++s) {
+        const bf16x8 af = *(const bf16x8*)(tb + (s >> 1) * (kT16 * 128) + aoff[s & 1]);
+        asm volatile("" ::"v"(af));
+      }
+    } else if (ABL == 2 || ABL == 5) {
       const bf16x8 af = *(const bf16x8*)(tb + aoff[0]);
 #pragma unroll
       for (int s = 0; s < C::KS; ++s)
@@ -510,8 +499,9 @@ __global__ __launch_bounds__(NW * 64, 1) void ip_scan16_kernel(ScanArgs a) {
       }
     }
 
-    const int64_t rowbase = tile * kT16 + 4 * kq;
-    if (ABL == 1 || ABL == 3) {
+  };
+  auto epilogue = [&](const f32x4 (&acc)[QB], int64_t rowbase) {
+    if (ABL == 1 || ABL == 3 || ABL == 4 || ABL == 5) {
 #pragma unroll
       for (int b = 0; b < QB; ++b) asm volatile("" ::"v"(acc[b]));
     } else if (MODE == SCAN_FILTER) {
@@ -584,9 +574,47 @@ __global__ __launch_bounds__(NW * 64, 1) void ip_scan16_kernel(ScanArgs a) {
         }
       }
     }
+  };
+
+  f32x4 accA[QB], accB[QB];
+  int64_t rbA = 0, rbB = 0;
+  int buf = 0;
+  int nslot = C::PD;   // slot of tile it + PD (== slot of it - 1)
+  for (int64_t it = 0; it < my_tiles; ++it) {
+    const int64_t tile = t0 + it * tstep;
+    const int64_t younger = my_tiles - 1 - it;
+    wait_tiles_younger<C::GLDS_PER_WAVE>((int)(younger < C::PD - 1 ? younger : C::PD - 1));
+    lds_barrier();
+
+    if (MODE == SCAN_FILTER) {
+      const uint32_t n = *hit_n;
+      if (n >= (uint32_t)(kHitCap / 2)) {
+        if (AGG) flush_hits_agg<NW * 64>(a, qbase, n, hk, hq, qcnt, qoff);
+        else flush_hits<NW * 64>(a, qbase, n, hk, hq);
+        lds_barrier();
+        if (tid == 0) *hit_n = 0;
+        lds_barrier();
+      }
+    }
+    if (it + C::PD < my_tiles)
+      issue_tile16<D, NW>(a, ring + nslot * C::TILE_BYTES, tile + C::PD * tstep, wave, lane);
+
+    const int64_t rowbase = tile * kT16 + 4 * kq;
+    if ((it & 1) == 0) {
+      mma_tile(accA, buf);
+      if (it > 0) epilogue(accB, rbB);
+      rbA = rowbase;
+    } else {
+      mma_tile(accB, buf);
+      epilogue(accA, rbA);
+      rbB = rowbase;
+    }
     buf = (buf + 1 == C::NBUF) ? 0 : buf + 1;
     nslot = (nslot + 1 == C::NBUF) ? 0 : nslot + 1;
   }
+
+  if (my_tiles & 1) epilogue(accA, rbA);
+  else epilogue(accB, rbB);
 
   if (MODE == SCAN_FILTER) {
     lds_barrier();
@@ -1852,6 +1880,14 @@ static int launch_scan_d(const ScanArgs& a, int mode, hipStream_t s) {
       hipLaunchKernelGGL((ip_scan16_kernel<D, SCAN_FILTER, 0, 4>), grid, block, 0, s, a);
     else if (mode == SCAN_DENSE && g_scan_variant == 6)
       hipLaunchKernelGGL((ip_scan16_kernel<D, SCAN_DENSE, 0, 4>), grid, block, 0, s, a);
+    else if (mode == SCAN_FILTER && D == 768 && g_scan_variant == 8)
+      hipLaunchKernelGGL((ip_scan16_kernel<D, SCAN_FILTER, 4, 8>), grid, dim3(512), 0, s, a);
+    else if (mode == SCAN_FILTER && D == 768 && g_scan_variant == 9)
+      hipLaunchKernelGGL((ip_scan16_kernel<D, SCAN_FILTER, 5, 8>), grid, dim3(512), 0, s, a);
+    else if (mode == SCAN_FILTER && D == 768 && g_scan_variant == 10)
+      hipLaunchKernelGGL((ip_scan16_kernel<D, SCAN_FILTER, 3, 8>), grid, dim3(512), 0, s, a);
+    else if (mode == SCAN_FILTER && D == 768 && g_scan_variant == 11)
+      hipLaunchKernelGGL((ip_scan16_kernel<D, SCAN_FILTER, 1, 8>), grid, dim3(512), 0, s, a);
     else if (mode == SCAN_FILTER && g_scan_variant == 7)
       hipLaunchKernelGGL((ip_scan16_kernel<D, SCAN_FILTER, 0, 8, false>), grid, dim3(512), 0, s, a);
     else if (mode == SCAN_FILTER) {
@@ -1944,9 +1980,11 @@ const char* drt_version(void) { return "drt-mi355x 0.1 (gfx950)"; }
 // 6 = the same with 4 waves,
 // 1 = 32-row FILTER scan without MFMA (memory-pipeline ceiling; results are
 // meaningless), 2 = previous 32-row / 3-slot kernel; 3/4/5 = 16-row kernel
-// ablations (no MFMA / no LDS fragment reads / no filter; d = 768 only).
+// ablations (no MFMA / no LDS fragment reads / no filter; d = 768 only); 8-11 = 8-wave
+// ablations (LDS fragment reads only / MFMA on register operands without filter / no filter /
+// no MFMA and no filter).
 int drt_scan_variant(int32_t v) {
-  if (v < 0 || v > 7) return DRT_EINVAL;
+  if (v < 0 || v > 11) return DRT_EINVAL;
   g_scan_variant = v;
   return DRT_OK;
 }
