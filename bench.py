@@ -47,14 +47,9 @@ def parse():
     ap.add_argument("--qb", type=int, default=128)
     ap.add_argument("--k", type=int, default=1000)
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--cpu-rows", type=int, default=1_000_000)
-    ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--no-encode", action="store_true",
                     help="skip the encode leg (passages/sec of the bf16 BERT-base passage tower, every rank)")
     ap.add_argument("--scan-variant", type=int, default=0, help="benchmark-only ablation of the scan kernel")
-    ap.add_argument("--streams", type=int, default=1,
-                    help="HIP streams the query batches rotate over (overlaps one batch's exchange and small "
-                         "kernels with the next batch's scan)")
     ap.add_argument("--protocol", choices=["global_tau", "per_shard"], default="global_tau",
                     help="N > 1 exchange protocol (per_shard = exact top-k per shard + merge)")
     return ap.parse_args()
@@ -96,38 +91,80 @@ def gen_shard(n_total, world, rank, d, device):
     return shard, lo, hi
 
 
-def cpu_baseline(args):
-    """Oracle (numpy, fp32 like faiss IndexFlatIP) on a bounded sample of the same workload."""
-    import numpy as np
-    from oracle.search_oracle import bf16_round, ip_topk
+def _cpu_threads():
+    import torch
+    info = {"host_cpu_count": os.cpu_count(), "torch_threads": torch.get_num_threads()}
     try:
         from threadpoolctl import threadpool_info
-        cores = max([i.get("num_threads", 1) for i in threadpool_info() if i.get("user_api") == "blas"] or [1])
+        blas = [i.get("num_threads", 1) for i in threadpool_info() if i.get("user_api") == "blas"]
+        info["blas_threads"] = max(blas) if blas else None
     except Exception:
-        cores = os.cpu_count() or 1
-    rng = np.random.default_rng(99)
-    rows = args.cpu_rows
-    p = bf16_round(rng.standard_normal((rows, args.dim), dtype=np.float32))
-    q = bf16_round(rng.standard_normal((args.qb, args.dim), dtype=np.float32))
-    nb = 0
-    t0 = time.perf_counter()
-    while True:
-        ip_topk(q, p, args.k, chunk=rows, dtype=np.float32)
-        nb += 1
-        el = time.perf_counter() - t0
-        if el >= args.cpu_seconds or nb >= 50:
-            break
-    qps_sample = nb * args.qb / el
-    scale = rows / args.n_corpus
+        info["blas_threads"] = None
+    return info
+
+
+def cpu_baseline(args, shard, queries, gpu_result):
+    """The oracle (numpy fp32 BLAS, like faiss IndexFlatIP's sgemm + top-k) timed on the host
+    cores against the SAME 10M-row corpus the GPU searched: the shard streams to host in
+    262,144-row chunks (bf16 -> fp32 conversion untimed, as building a faiss index would be),
+    and ONE query batch is scored and selected chunk by chunk (timed).  Also checks the GPU's
+    top-k of that batch against the CPU result at full size."""
+    import numpy as np
+    from oracle.search_oracle import ip_topk, merge_topk
+    thr = _cpu_threads()
+    q = queries.float().cpu().numpy()
+    n = shard.shape[0]
+    chunk = 262144
+    best_s = best_i = None
+    t_comp = 0.0
+    for a in range(0, n, chunk):
+        pc = shard[a: a + chunk].float().cpu().numpy()
+        t0 = time.perf_counter()
+        cs, ci = ip_topk(q, pc, args.k, id_offset=a, chunk=pc.shape[0], dtype=np.float32)
+        if best_s is None:
+            best_s, best_i = cs, ci
+        else:
+            best_s, best_i = merge_topk(np.stack([best_s, cs]), np.stack([best_i, ci]), args.k)
+        t_comp += time.perf_counter() - t0
+    gs, gi = gpu_result
+    gi = gi.cpu().numpy()
+    gs = gs.cpu().numpy()
+    same = float((gi == best_i).mean())
     return {
-        "value": round(qps_sample * scale, 3),
+        "value": round(q.shape[0] / t_comp, 3),
         "unit": "queries/s",
-        "cores": int(cores),
+        "cores": int(thr["blas_threads"] or thr["torch_threads"]),
         "kind": "port",
-        "sample": (f"oracle/search_oracle.ip_topk fp32 (numpy BLAS) on {nb} batches x {args.qb} queries "
-                   f"against a {rows}-row slice ({qps_sample:.1f} q/s), scaled by {rows}/{args.n_corpus} "
-                   f"to the full corpus; {el:.1f} s"),
+        "sample": (f"oracle/search_oracle.ip_topk fp32 (numpy BLAS, {thr['blas_threads']} threads) on one batch of "
+                   f"{q.shape[0]} queries against the full {n}-row bf16 corpus streamed from the GPU in "
+                   f"{chunk}-row chunks (fp32 conversion untimed); {t_comp:.1f} s of compute"),
+        **thr,
+        "parity_vs_gpu": {"ids_equal_frac": round(same, 6),
+                          "max_abs_score_diff": float(np.abs(gs - best_s).max())},
     }
+
+
+def encode_cpu_baseline(batch=32, L=128, steps=2):
+    """torch-CPU fp32 DRModel.encode (the reference's arithmetic: HF BertModel fp32 + [CLS]
+    pooling through this build's DRModelForInference, which is pinned to the reference's
+    golden reps on CPU), BERT-base random init, B = 32, L = 128."""
+    import torch
+    from transformers import BertConfig, BertModel
+    from denseretrievaltoolkits_amd.model.biencoder import DRModelForInference
+    thr = _cpu_threads()
+    torch.manual_seed(0)
+    lm = BertModel(BertConfig(), add_pooling_layer=False).eval()
+    m = DRModelForInference(lm_q=lm, lm_p=lm, pooling="first").eval()
+    ids = torch.randint(1000, 30522, (batch, L), dtype=torch.int64)
+    ids[:, 0], ids[:, -1] = 101, 102
+    item = {"input_ids": ids, "attention_mask": torch.ones((batch, L), dtype=torch.int64)}
+    m(passage=item)
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        m(passage=item)
+    el = time.perf_counter() - t0
+    return {"value": round(steps * batch / el, 2), "unit": "passages/s", "cores": int(thr["torch_threads"]),
+            "kind": "port", "sample": f"{steps} batches of {batch} x {L} tokens, fp32, {el:.1f} s", **thr}
 
 
 def pmc_traffic(args, world):
@@ -173,84 +210,45 @@ def main():
     gq.manual_seed(5678)
     queries = torch.randn((nsteps, qb, d), generator=gq, device=dev).to(torch.bfloat16)
 
-    s_loc = torch.empty((nsteps, qb, k), dtype=torch.float32, device=dev)
-    i_loc = torch.empty((nsteps, qb, k), dtype=torch.int64, device=dev)
-    st = torch.zeros((nsteps, qb), dtype=torch.int32, device=dev)
     gloo = world > 1 and dist.get_backend() == "gloo"
-
-    def all_gather(t):
-        """[world * rows, ...] concatenated all-gather (RCCL on device; host-staged under gloo)."""
-        src = t.contiguous().cpu() if gloo else t.contiguous()
-        out = torch.empty((world * src.shape[0],) + tuple(src.shape[1:]), dtype=src.dtype, device=src.device)
-        dist.all_gather_into_tensor(out, src)
-        return out.to(dev).view((world,) + tuple(t.shape))
-
-    def step_per_shard(j):
-        kernels.ip_topk(queries[j], shard, k, id_offset=lo, resolve=False,
-                        out=(s_loc[j], i_loc[j]), status=st[j])
-        if world > 1:
-            return kernels.topk_merge(all_gather(s_loc[j]), all_gather(i_loc[j]), k)
-        return s_loc[j], i_loc[j]
-
-    def step_global_tau(j):
-        best = kernels.dist_sample(queries[j], shard, args.n_corpus, k)
-        tau = kernels.dist_tau(all_gather(best), k)
-        packed = kernels.dist_filter(queries[j], shard, args.n_corpus, k, lo, tau)
-        s, i, stj = kernels.merge_packed(all_gather(packed), k, args.n_corpus)
-        st[j] = stj
-        return s, i
-
     use_global = world > 1 and args.protocol == "global_tau"
-    step = step_global_tau if use_global else step_per_shard
+    # the product path: the same index objects and certified, pipelined batch search that
+    # BaseFaissIPRetriever.batch_search / Trainer.evaluate use (search.py); every query
+    # certified exact inside the timed region (an uncertified one is rescanned there)
+    from denseretrievaltoolkits_amd.search import FlatIPIndex, ShardedFlatIP
+    if world == 1:
+        index = FlatIPIndex.from_rows(shard)
 
-    def fix_failures(first, last):
-        """Exact redo of any uncertified query batch (counted inside the timed region).
-        Global-tau statuses come from the merged lists, identical on every rank."""
-        bad = (st[first:last] != 0).any(dim=1).to(torch.int32)
-        if world > 1 and not use_global:
-            bad_c = bad.cpu() if gloo else bad
-            dist.all_reduce(bad_c, op=dist.ReduceOp.MAX)
-            bad = bad_c.to(dev)
-        nb = 0
-        for j in (torch.nonzero(bad).flatten() + first).tolist():
-            if use_global:
-                kernels.ip_topk(queries[j], shard, k, id_offset=lo, resolve=True, out=(s_loc[j], i_loc[j]))
-                kernels.topk_merge(all_gather(s_loc[j]), all_gather(i_loc[j]), k)
-                nb += qb
-                continue
-            nb += kernels.resolve_failed(queries[j], shard, k, lo, s_loc[j], i_loc[j], st[j])
-            if world > 1:
-                kernels.topk_merge(all_gather(s_loc[j]), all_gather(i_loc[j]), k)
-        return nb
+        def run(first, last):
+            return index.search_batches([queries[j] for j in range(first, last)], k)
+    else:
+        index = ShardedFlatIP(d, device=dev, protocol=args.protocol)
+        index.local = FlatIPIndex.from_rows(shard)
+        index.sync_offsets()
+        assert index.offset == lo and index.ntotal == args.n_corpus
 
-    main_stream = torch.cuda.current_stream(dev)
-    streams = [main_stream] + [torch.cuda.Stream(device=dev) for _ in range(max(1, args.streams) - 1)]
+        def run(first, last):
+            return index.search_batches([queries[j] for j in range(first, last)], k)
 
-    def run_steps(first, last):
-        for s in streams[1:]:
-            s.wait_stream(main_stream)
-        for j in range(first, last):
-            with torch.cuda.stream(streams[j % len(streams)]):
-                step(j)
-        for s in streams[1:]:
-            main_stream.wait_stream(s)
-
-    run_steps(0, args.warmup)
-    fix_failures(0, args.warmup)
+    run(0, args.warmup)
     torch.cuda.synchronize()
+    local_index = index if world == 1 else index.local
+    res0 = local_index.resolved
+    fb0 = 0 if world == 1 else index.fallbacks
 
     lib.drt_profile_enable(_native.PROF_SCAN, 1)
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    run_steps(args.warmup, nsteps)
-    n_resolved = fix_failures(args.warmup, nsteps)
+    results = run(args.warmup, nsteps)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     t1 = time.perf_counter()
     lib.drt_profile_enable(_native.PROF_SCAN, 0)
+    n_resolved = local_index.resolved - res0
+    n_fallback = (0 if world == 1 else index.fallbacks) - fb0
     tot_ms = _native.ctypes.c_double(0.0)
     cnt = _native.c_i64(0)
     _native.check(lib.drt_profile_read(_native.PROF_SCAN, _native.ctypes.byref(tot_ms), _native.ctypes.byref(cnt)),
@@ -259,6 +257,8 @@ def main():
     elapsed = torch.tensor([t1 - t0], dtype=torch.float64, device=dev)
     scan_ms = torch.tensor([tot_ms.value / max(1, cnt.value)], dtype=torch.float64, device=dev)
     if world > 1:
+        if gloo:
+            elapsed, scan_ms = elapsed.cpu(), scan_ms.cpu()
         dist.all_reduce(elapsed, op=dist.ReduceOp.MAX)
         dist.all_reduce(scan_ms, op=dist.ReduceOp.MAX)
     el = float(elapsed.item())
@@ -294,10 +294,11 @@ def main():
                                                     if world > 1 else "")),
                 "n_corpus": args.n_corpus, "dim": d, "query_batch": qb, "k": k,
                 "parallelism": f"row-shard x{world}",
-                "streams": len(streams),
+                "path": "FlatIPIndex.search_batches (certified, pipelined)" if world == 1 else
+                        f"ShardedFlatIP.search_batches ({args.protocol}, certified, pipelined)",
             },
             "roofline": {
-                "kernel": "ip_scan16_kernel<768,FILTER,0,8> (csrc/search.hip)",
+                "kernel": "ip_scan16_kernel<768,FILTER,0,8,false,6> (csrc/search.hip)",
                 "bound": "hbm",
                 "achieved": round(achieved, 1),
                 "peak": HBM_PEAK_GBS,
@@ -310,9 +311,10 @@ def main():
                 "alg_bytes_per_launch": alg_bytes,
             },
             "uncertified_queries_resolved": int(n_resolved),
+            "global_tau_fallback_batches": int(n_fallback),
         }
         if world == 1 and not args.no_cpu_baseline:
-            out["cpu_baseline"] = cpu_baseline(args)
+            out["cpu_baseline"] = cpu_baseline(args, shard, queries[args.warmup], results[0])
     enc = None if args.no_encode else encode_leg(args, dev)
     if enc is not None:
         if world > 1:
@@ -329,6 +331,8 @@ def main():
             out["encode"] = enc
     if rank == 0 and not args.no_encode and world == 1:
         from denseretrievaltoolkits_amd import bench_encode
+        if not args.no_cpu_baseline:
+            out["encode"]["cpu_baseline"] = encode_cpu_baseline()
         out["rerank"] = bench_encode.run_rerank(dev)
         out["query_encode"] = bench_encode.run_query_encode(dev)
         out["train_scores"] = bench_encode.run_train_scores(dev)

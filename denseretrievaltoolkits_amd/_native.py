@@ -32,7 +32,9 @@ _SIGNATURES = [
     ("drt_version", ctypes.c_char_p, []),
     ("drt_ip_topk_workspace", c_sz, [c_i64, c_i64, c_i32, c_i32]),
     ("drt_ip_topk_bf16", c_i32, [c_vp, c_i64, c_vp, c_i64, c_i32, c_i32, c_i64, c_vp, c_vp, c_vp, c_vp, c_sz, c_vp]),
-    ("drt_ip_topk_resolve", c_i32, [c_vp, c_i64, c_vp, c_i64, c_i32, c_i32, c_i64, c_vp, c_vp, c_vp, c_vp, c_vp]),
+    ("drt_ip_topk_resolve_workspace", c_sz, [c_i64, c_i64, c_i32]),
+    ("drt_ip_topk_resolve", c_i32, [c_vp, c_i64, c_vp, c_i64, c_i32, c_i32, c_i64, c_vp, c_vp, c_vp, c_vp, c_sz,
+                                    c_vp, c_vp]),
     ("drt_scan_variant", c_i32, [c_i32]),
     ("drt_topk_merge", c_i32, [c_vp, c_vp, c_i64, c_i32, c_i32, c_i32, c_vp, c_vp, c_vp]),
     ("drt_ip_topk_sample_rank", c_i32, [c_i32]),

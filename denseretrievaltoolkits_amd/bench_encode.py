@@ -161,7 +161,7 @@ def run_train_scores(device, bq=512, d=768, n_passages=(2, 8), steps=20, warmup=
     """Config C3 (BASELINE.json configs[2]): the in-batch-negative score matrix of
     DRModel.forward (DRT/model/biencoder.py:107-119) at batch 512: scores = q . p^T
     [512, 512 n], CrossEntropy(mean) with target i * n, and its backward (dq, dp),
-    fp32 end to end on the HIP op (score_ce.ScoreCE), next to torch's fp32
+    fp32 end to end on the HIP op (torch.ops.drt.score_ce_fwd, score_ce.py), next to torch's fp32
     matmul + cross_entropy + autograd on the same device."""
     from .score_ce import score_ce
     g = torch.Generator(device=device)

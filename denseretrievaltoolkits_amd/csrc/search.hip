@@ -86,6 +86,20 @@ __device__ __forceinline__ void glds16(const void* gsrc, uint32_t lds_addr) {
       : "memory");
 }
 
+// The same with the non-temporal policy (the corpus stream is read once per launch).
+__device__ __forceinline__ void glds16_nt(const void* gsrc, uint32_t lds_addr) {
+  uint32_t keep;
+  asm volatile(
+      "s_mov_b32 %0, m0\n\t"
+      "s_mov_b32 m0, %2\n\t"
+      "s_nop 0\n\t"
+      "global_load_lds_dwordx4 %1, off nt\n\t"
+      "s_mov_b32 m0, %0"
+      : "=&s"(keep)
+      : "v"(gsrc), "s"(lds_addr)
+      : "memory");
+}
+
 __device__ __forceinline__ uint32_t lds_addr_of(const void* p) {
   return (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) char*)p;
 }
@@ -361,7 +375,7 @@ struct Scan16Cfg {
   static_assert(LDS_BYTES <= 160 * 1024, "LDS budget");
 };
 
-template <int D, int NW>
+template <int D, int NW, bool NTL = false>
 __device__ __forceinline__ void issue_tile16(const ScanArgs& a, uint32_t buf_lds, int64_t tile, int wave, int lane) {
   using C = Scan16Cfg<D, NW>;
   const int rsub = lane >> 3, pos = lane & 7;
@@ -375,7 +389,8 @@ __device__ __forceinline__ void issue_tile16(const ScanArgs& a, uint32_t buf_lds
     li = li < a.nrows ? li : a.nrows - 1;
     const int c = pos ^ ((row >> 1) & 7);
     const __bf16* src = a.P + (a.row0 + li * a.rstride) * a.ldp + g * 64 + c * 8;
-    glds16(src, __builtin_amdgcn_readfirstlane(buf_lds + J * 1024));
+    if (NTL) glds16_nt(src, __builtin_amdgcn_readfirstlane(buf_lds + J * 1024));
+    else glds16(src, __builtin_amdgcn_readfirstlane(buf_lds + J * 1024));
   }
 }
 
@@ -396,7 +411,11 @@ __device__ __forceinline__ void wait_tiles_younger(int younger) {
 // ABL (benchmark ablations, FILTER only): 0 production, 1 no MFMA and no filter,
 // 2 MFMA on register operands (no LDS fragment reads), 3 no filter, 4 LDS fragment reads
 // only (no MFMA, no filter), 5 MFMA on register operands, no filter.
-template <int D, int MODE, int ABL = 0, int NW = 4, bool AGG = true>
+// OPT (A/B switches of the production loop): bit 0 = no deferred epilogue (each tile's filter
+// right after its own MFMAs), bit 1 = non-temporal corpus loads, bit 2 = s_setprio 1 for
+// waves NW/2.. (the second-dispatched half of each SIMD pair).
+enum { SOPT_NOPIPE = 1, SOPT_NT = 2, SOPT_PRIO = 4 };
+template <int D, int MODE, int ABL = 0, int NW = 4, bool AGG = true, int OPT = 0>
 __global__ __launch_bounds__(NW * 64, 1) void ip_scan16_kernel(ScanArgs a) {
   using C = Scan16Cfg<D, NW>;
   constexpr int QB = 128 / (NW * 16);   // 16-query column blocks per wave
@@ -460,7 +479,8 @@ __global__ __launch_bounds__(NW * 64, 1) void ip_scan16_kernel(ScanArgs a) {
   // prologue: PD tiles in flight
 #pragma unroll
   for (int p = 0; p < C::PD; ++p)
-    if (p < my_tiles) issue_tile16<D, NW>(a, ring + p * C::TILE_BYTES, t0 + p * tstep, wave, lane);
+    if (p < my_tiles) issue_tile16<D, NW, (OPT & SOPT_NT) != 0>(a, ring + p * C::TILE_BYTES, t0 + p * tstep, wave, lane);
+  if ((OPT & SOPT_PRIO) && wave >= NW / 2) __builtin_amdgcn_s_setprio(1);
 
   // A-fragment address: chunk 4s + kq of row r, group s >> 1, position (4(s&1) + kq) ^ sw
   const int sw = (r >> 1) & 7;
@@ -597,10 +617,13 @@ __global__ __launch_bounds__(NW * 64, 1) void ip_scan16_kernel(ScanArgs a) {
       }
     }
     if (it + C::PD < my_tiles)
-      issue_tile16<D, NW>(a, ring + nslot * C::TILE_BYTES, tile + C::PD * tstep, wave, lane);
+      issue_tile16<D, NW, (OPT & SOPT_NT) != 0>(a, ring + nslot * C::TILE_BYTES, tile + C::PD * tstep, wave, lane);
 
     const int64_t rowbase = tile * kT16 + 4 * kq;
-    if ((it & 1) == 0) {
+    if (OPT & SOPT_NOPIPE) {
+      mma_tile(accA, buf);
+      epilogue(accA, rowbase);
+    } else if ((it & 1) == 0) {
       mma_tile(accA, buf);
       if (it > 0) epilogue(accB, rbB);
       rbA = rowbase;
@@ -613,8 +636,10 @@ __global__ __launch_bounds__(NW * 64, 1) void ip_scan16_kernel(ScanArgs a) {
     nslot = (nslot + 1 == C::NBUF) ? 0 : nslot + 1;
   }
 
-  if (my_tiles & 1) epilogue(accA, rbA);
-  else epilogue(accB, rbB);
+  if (!(OPT & SOPT_NOPIPE)) {
+    if (my_tiles & 1) epilogue(accA, rbA);
+    else epilogue(accB, rbB);
+  }
 
   if (MODE == SCAN_FILTER) {
     lds_barrier();
@@ -1888,6 +1913,19 @@ static int launch_scan_d(const ScanArgs& a, int mode, hipStream_t s) {
       hipLaunchKernelGGL((ip_scan16_kernel<D, SCAN_FILTER, 3, 8>), grid, dim3(512), 0, s, a);
     else if (mode == SCAN_FILTER && D == 768 && g_scan_variant == 11)
       hipLaunchKernelGGL((ip_scan16_kernel<D, SCAN_FILTER, 1, 8>), grid, dim3(512), 0, s, a);
+    else if (mode == SCAN_FILTER && g_scan_variant >= 12 && g_scan_variant <= 19) {
+      // production kernel with the OPT switches (variant 12 + OPT bits 0..2), sparse append
+      switch (g_scan_variant - 11) {
+        case 1: hipLaunchKernelGGL((ip_scan16_kernel<D, SCAN_FILTER, 0, 8, false, 1>), grid, dim3(512), 0, s, a); break;
+        case 2: hipLaunchKernelGGL((ip_scan16_kernel<D, SCAN_FILTER, 0, 8, false, 2>), grid, dim3(512), 0, s, a); break;
+        case 3: hipLaunchKernelGGL((ip_scan16_kernel<D, SCAN_FILTER, 0, 8, false, 3>), grid, dim3(512), 0, s, a); break;
+        case 4: hipLaunchKernelGGL((ip_scan16_kernel<D, SCAN_FILTER, 0, 8, false, 4>), grid, dim3(512), 0, s, a); break;
+        case 5: hipLaunchKernelGGL((ip_scan16_kernel<D, SCAN_FILTER, 0, 8, false, 5>), grid, dim3(512), 0, s, a); break;
+        case 6: hipLaunchKernelGGL((ip_scan16_kernel<D, SCAN_FILTER, 0, 8, false, 6>), grid, dim3(512), 0, s, a); break;
+        case 7: hipLaunchKernelGGL((ip_scan16_kernel<D, SCAN_FILTER, 0, 8, false, 7>), grid, dim3(512), 0, s, a); break;
+        default: hipLaunchKernelGGL((ip_scan16_kernel<D, SCAN_FILTER, 0, 8, false, 0>), grid, dim3(512), 0, s, a); break;
+      }
+    }
     else if (mode == SCAN_FILTER && g_scan_variant == 7)
       hipLaunchKernelGGL((ip_scan16_kernel<D, SCAN_FILTER, 0, 8, false>), grid, dim3(512), 0, s, a);
     else if (mode == SCAN_FILTER) {
@@ -1897,8 +1935,11 @@ static int launch_scan_d(const ScanArgs& a, int mode, hipStream_t s) {
       // measured crossover (profiles/r01_*): dense below ~3M rows at cap 16384.
       const double eh = a.exp_hits > 0 ? (double)a.exp_hits : (double)a.cap / 4.0;
       const bool dense_hits = eh * 256.0 / (double)a.nrows >= 0.35;
-      if (dense_hits) hipLaunchKernelGGL((ip_scan16_kernel<D, SCAN_FILTER, 0, 8, true>), grid, dim3(512), 0, s, a);
-      else hipLaunchKernelGGL((ip_scan16_kernel<D, SCAN_FILTER, 0, 8, false>), grid, dim3(512), 0, s, a);
+      // OPT: non-temporal corpus loads + s_setprio 1 for waves 4-7 (r02 A/B, tools/scan_ab.py,
+      // profiles/r02a_scan_ab.log: -2.3 % per launch vs OPT 0, ids identical)
+      constexpr int kOpt = SOPT_NT | SOPT_PRIO;
+      if (dense_hits) hipLaunchKernelGGL((ip_scan16_kernel<D, SCAN_FILTER, 0, 8, true, kOpt>), grid, dim3(512), 0, s, a);
+      else hipLaunchKernelGGL((ip_scan16_kernel<D, SCAN_FILTER, 0, 8, false, kOpt>), grid, dim3(512), 0, s, a);
     }
     else
       hipLaunchKernelGGL((ip_scan16_kernel<D, SCAN_DENSE, 0, 8>), grid, dim3(512), 0, s, a);
@@ -1982,9 +2023,10 @@ const char* drt_version(void) { return "drt-mi355x 0.1 (gfx950)"; }
 // meaningless), 2 = previous 32-row / 3-slot kernel; 3/4/5 = 16-row kernel
 // ablations (no MFMA / no LDS fragment reads / no filter; d = 768 only); 8-11 = 8-wave
 // ablations (LDS fragment reads only / MFMA on register operands without filter / no filter /
-// no MFMA and no filter).
+// no MFMA and no filter); 12-19 = the production filter scan (sparse append) with OPT bits
+// v - 12: 1 no deferred epilogue, 2 non-temporal corpus loads, 4 s_setprio for waves 4-7.
 int drt_scan_variant(int32_t v) {
-  if (v < 0 || v > 11) return DRT_EINVAL;
+  if (v < 0 || v > 19) return DRT_EINVAL;
   g_scan_variant = v;
   return DRT_OK;
 }
@@ -2104,9 +2146,28 @@ int drt_ip_topk_bf16(const void* Q, int64_t nq, const void* P, int64_t n, int32_
   return launch_select(sa, SEL_KEYS64, SEL_TOPK, s);
 }
 
+static int64_t resolve_width(int64_t n) { return align_up(std::max<int64_t>(n, 4), 4); }
+
+// Dense exact rescan, chunked so the score buffer stays <= ~2 GB: queries per chunk.
+static int64_t resolve_chunk(int64_t nbad, int64_t n) {
+  const int64_t width = resolve_width(n);
+  int64_t chunk = std::max<int64_t>(1, std::min<int64_t>(nbad, (2ll << 30) / (width * 4)));
+  return std::min<int64_t>(chunk, kQueriesPerWG);
+}
+
+static size_t resolve_ws_bytes(int64_t chunk, int64_t n, int32_t d) {
+  return (size_t)(align_up(chunk * (int64_t)d * 2, 256) + align_up(chunk * resolve_width(n) * 4, 256) +
+                  align_up(chunk * 4, 256));
+}
+
+size_t drt_ip_topk_resolve_workspace(int64_t nbad, int64_t n, int32_t d) {
+  if (nbad <= 0 || n < 0 || d <= 0 || d % 64 || d > 1024) return 0;
+  return resolve_ws_bytes(resolve_chunk(nbad, n), n, d);
+}
+
 int drt_ip_topk_resolve(const void* Q, int64_t nq, const void* P, int64_t n, int32_t d, int32_t k,
                         int64_t id_offset, float* out_scores, int64_t* out_ids, int32_t* status,
-                        int64_t* n_resolved, void* stream) {
+                        void* ws, size_t ws_bytes, int64_t* n_resolved, void* stream) {
   DRT_REQUIRE(valid_dims(nq, n, d, k));
   if (n_resolved) *n_resolved = 0;
   if (nq == 0 || status == nullptr) return DRT_OK;
@@ -2120,16 +2181,18 @@ int drt_ip_topk_resolve(const void* Q, int64_t nq, const void* P, int64_t n, int
   if (bad.empty()) return DRT_OK;
   if (n_resolved) *n_resolved = (int64_t)bad.size();
 
-  // Dense exact rescan, chunked so the score buffer stays <= ~2 GB.
-  const int64_t width = align_up(std::max<int64_t>(n, 4), 4);
-  int64_t chunk = std::max<int64_t>(1, std::min<int64_t>((int64_t)bad.size(), (2ll << 30) / (width * 4)));
-  chunk = std::min<int64_t>(chunk, kQueriesPerWG);
-  void *qbuf = nullptr, *sbuf = nullptr, *mbuf = nullptr;
+  // the caller's workspace decides the chunk (drt_ip_topk_resolve_workspace(#failed, n, d)
+  // bytes holds the whole default chunk); nothing is allocated here
+  const int64_t width = resolve_width(n);
+  int64_t chunk = resolve_chunk((int64_t)bad.size(), n);
+  while (chunk > 1 && resolve_ws_bytes(chunk, n, d) > ws_bytes) chunk >>= 1;
+  DRT_REQUIRE(ws != nullptr && resolve_ws_bytes(chunk, n, d) <= ws_bytes);
+  char* wp = (char*)ws;
+  void* qbuf = wp;
+  void* sbuf = wp + align_up(chunk * (int64_t)d * 2, 256);
+  void* mbuf = (char*)sbuf + align_up(chunk * width * 4, 256);
   int rc = DRT_OK;
   hipError_t e;
-  if ((e = hipMalloc(&qbuf, chunk * (int64_t)d * 2)) != hipSuccess) return (int)e;
-  if ((e = hipMalloc(&sbuf, chunk * width * 4)) != hipSuccess) { hipFree(qbuf); return (int)e; }
-  if ((e = hipMalloc(&mbuf, chunk * 4)) != hipSuccess) { hipFree(qbuf); hipFree(sbuf); return (int)e; }
   for (size_t b0 = 0; b0 < bad.size() && rc == DRT_OK; b0 += chunk) {
     const int64_t nb = std::min<int64_t>(chunk, (int64_t)bad.size() - (int64_t)b0);
     for (int64_t i = 0; i < nb; ++i) {
@@ -2172,11 +2235,8 @@ int drt_ip_topk_resolve(const void* Q, int64_t nq, const void* P, int64_t n, int
     if (rc) break;
     if ((e = hipStreamSynchronize(s)) != hipSuccess) { rc = (int)e; break; }
   }
-  hipStreamSynchronize(s);
-  hipFree(qbuf);
-  hipFree(sbuf);
-  hipFree(mbuf);
-  return rc;
+  const hipError_t se = hipStreamSynchronize(s);
+  return rc != DRT_OK ? rc : (se == hipSuccess ? DRT_OK : (int)se);
 }
 
 int drt_topk_merge(const float* scores, const int64_t* ids, int64_t nq, int32_t nparts, int32_t k_in,

@@ -1,0 +1,380 @@
+// torch_ops.cpp — PyTorch-ROCm custom operators (torch.ops.drt.*) over the C ABI of drt.h.
+//
+// Thin host-side adapters: shape/dtype checks (TORCH_CHECK -> Python RuntimeError), output and
+// workspace tensors from torch's caching allocator, work enqueued on the current HIP stream of
+// the inputs' device, then one call into libdrt_hip.so.  No arithmetic lives here.
+//
+// Reference sites these ops stand in for (see include/drt.h for the per-function mapping):
+//   faiss.IndexFlatIP.search           DRT/evaluator/index.py:31-33        drt::ip_topk(+_resolve)
+//   per-partition merge                DRT/model/utils.py:215-229          drt::topk_merge, merge_packed
+//   corpus sharding (file exchange)    DRT/trainer/trainer.py:191-262      drt::dist_sample/_tau/_filter
+//   score matrix + CE (+ autograd)     DRT/model/biencoder.py:107-119      drt::score_ce_fwd/_bwd
+//   HF BertModel forward pieces        transformers modeling_bert.py       drt::embed_ln, linear,
+//                                                                          attention, layernorm, pool,
+//                                                                          l2_normalize
+// Fake (meta) kernels and the autograd formula of score_ce_fwd are registered from Python
+// (denseretrievaltoolkits_amd/ops.py).
+#include <torch/library.h>
+#include <ATen/ATen.h>
+#include <c10/hip/HIPStream.h>
+#include <c10/hip/HIPGuard.h>
+
+#include "drt.h"
+
+namespace {
+
+using at::Tensor;
+
+void* stream_of(const Tensor& t) {
+  return (void*)c10::hip::getCurrentHIPStream(t.device().index()).stream();
+}
+
+void check_rc(int rc, const char* what) {
+  TORCH_CHECK(rc != DRT_EINVAL, what, ": invalid argument (DRT_EINVAL)");
+  TORCH_CHECK(rc == DRT_OK, what, ": HIP error ", rc);
+}
+
+void need_gpu(const Tensor& t, const char* name) {
+  TORCH_CHECK(t.is_cuda(), "drt ops run on the GPU only (", name, " is on ", t.device(),
+              "; no CPU fallback exists)");
+}
+
+void need(const Tensor& t, const char* name, at::ScalarType dt, int64_t dim) {
+  need_gpu(t, name);
+  TORCH_CHECK(t.scalar_type() == dt, name, ": expected ", dt, ", got ", t.scalar_type());
+  TORCH_CHECK(t.dim() == dim, name, ": expected a ", dim, "-d tensor, got ", t.dim(), "-d");
+}
+
+const void* ptr_or_null(const c10::optional<Tensor>& t) { return t.has_value() ? t->data_ptr() : nullptr; }
+
+Tensor workspace(const Tensor& like, size_t bytes) {
+  return at::empty({(int64_t)std::max<size_t>(bytes, 1)}, like.options().dtype(at::kByte));
+}
+
+// ---------------------------------------------------------------------------- search
+void ip_topk_out(const Tensor& q_, const Tensor& p_, int64_t k, int64_t id_offset, Tensor& scores, Tensor& ids,
+                 Tensor& status) {
+  need(q_, "q", at::kBFloat16, 2);
+  need(p_, "p", at::kBFloat16, 2);
+  TORCH_CHECK(q_.size(1) == p_.size(1), "q and p differ in dimension: ", q_.sizes(), " vs ", p_.sizes());
+  const c10::hip::HIPGuard g(q_.device());
+  const Tensor q = q_.contiguous(), p = p_.contiguous();
+  const int64_t nq = q.size(0), n = p.size(0), d = q.size(1);
+  TORCH_CHECK(scores.is_contiguous() && scores.scalar_type() == at::kFloat && scores.numel() == nq * k,
+              "scores: expected a contiguous float [", nq, ", ", k, "] tensor");
+  TORCH_CHECK(ids.is_contiguous() && ids.scalar_type() == at::kLong && ids.numel() == nq * k,
+              "ids: expected a contiguous int64 [", nq, ", ", k, "] tensor");
+  TORCH_CHECK(status.is_contiguous() && status.scalar_type() == at::kInt && status.numel() == nq,
+              "status: expected a contiguous int32 [", nq, "] tensor");
+  const size_t wsb = drt_ip_topk_workspace(nq, n, (int32_t)d, (int32_t)k);
+  TORCH_CHECK(wsb > 0 || nq == 0, "unsupported ip_topk shape nq=", nq, " n=", n, " d=", d, " k=", k,
+              " (d % 64 == 0, d <= 1024, 1 <= k <= 2048)");
+  Tensor ws = workspace(q, wsb);
+  check_rc(drt_ip_topk_bf16(q.data_ptr(), nq, n ? p.data_ptr() : nullptr, n, (int32_t)d, (int32_t)k, id_offset,
+                            scores.data_ptr<float>(), ids.data_ptr<int64_t>(), status.data_ptr<int32_t>(),
+                            ws.data_ptr(), wsb, stream_of(q)),
+           "drt_ip_topk_bf16");
+}
+
+std::tuple<Tensor, Tensor, Tensor> ip_topk(const Tensor& q, const Tensor& p, int64_t k, int64_t id_offset) {
+  need_gpu(q, "q");
+  const int64_t nq = q.size(0);
+  Tensor s = at::empty({nq, k}, q.options().dtype(at::kFloat));
+  Tensor i = at::empty({nq, k}, q.options().dtype(at::kLong));
+  Tensor st = at::empty({nq}, q.options().dtype(at::kInt));
+  ip_topk_out(q, p, k, id_offset, s, i, st);
+  return {s, i, st};
+}
+
+int64_t ip_topk_resolve(const Tensor& q_, const Tensor& p_, int64_t k, int64_t id_offset, Tensor& scores,
+                        Tensor& ids, Tensor& status) {
+  need(q_, "q", at::kBFloat16, 2);
+  need(p_, "p", at::kBFloat16, 2);
+  const c10::hip::HIPGuard g(q_.device());
+  const Tensor q = q_.contiguous(), p = p_.contiguous();
+  const int64_t nq = q.size(0), n = p.size(0), d = q.size(1);
+  if (nq == 0) return 0;
+  const int64_t nbad = status.ne(0).sum().item<int64_t>();   // synchronises, like the C entry
+  if (nbad == 0) return 0;
+  const size_t wsb = drt_ip_topk_resolve_workspace(nbad, n, (int32_t)d);
+  Tensor ws = workspace(q, wsb);
+  int64_t nres = 0;
+  check_rc(drt_ip_topk_resolve(q.data_ptr(), nq, n ? p.data_ptr() : nullptr, n, (int32_t)d, (int32_t)k, id_offset,
+                               scores.data_ptr<float>(), ids.data_ptr<int64_t>(), status.data_ptr<int32_t>(),
+                               ws.data_ptr(), wsb, &nres, stream_of(q)),
+           "drt_ip_topk_resolve");
+  return nres;
+}
+
+std::tuple<Tensor, Tensor> topk_merge(const Tensor& scores_, const Tensor& ids_, int64_t k_out) {
+  need(scores_, "scores", at::kFloat, 3);
+  need(ids_, "ids", at::kLong, 3);
+  TORCH_CHECK(scores_.sizes() == ids_.sizes(), "topk_merge: scores and ids differ in shape");
+  const c10::hip::HIPGuard g(scores_.device());
+  const Tensor s = scores_.contiguous(), i = ids_.contiguous();
+  const int64_t nparts = s.size(0), nq = s.size(1), k_in = s.size(2);
+  Tensor os = at::empty({nq, k_out}, s.options());
+  Tensor oi = at::empty({nq, k_out}, i.options());
+  check_rc(drt_topk_merge(s.data_ptr<float>(), i.data_ptr<int64_t>(), nq, (int32_t)nparts, (int32_t)k_in,
+                          (int32_t)k_out, os.data_ptr<float>(), oi.data_ptr<int64_t>(), stream_of(s)),
+           "drt_topk_merge");
+  return {os, oi};
+}
+
+Tensor dist_ws(const Tensor& q, int64_t n_local, int64_t n_global, int64_t k, size_t* wsb) {
+  *wsb = drt_ip_topk_dist_workspace(q.size(0), n_local, n_global, (int32_t)q.size(1), (int32_t)k);
+  TORCH_CHECK(*wsb > 0 || q.size(0) == 0, "unsupported dist shape nq=", q.size(0), " n_local=", n_local,
+              " n_global=", n_global, " d=", q.size(1), " k=", k);
+  return workspace(q, *wsb);
+}
+
+Tensor dist_sample(const Tensor& q_, const Tensor& p_, int64_t n_global, int64_t k) {
+  need(q_, "q", at::kBFloat16, 2);
+  need(p_, "p", at::kBFloat16, 2);
+  const c10::hip::HIPGuard g(q_.device());
+  const Tensor q = q_.contiguous(), p = p_.contiguous();
+  const int32_t r = drt_ip_topk_sample_rank((int32_t)k);
+  TORCH_CHECK(r > 0, "unsupported k=", k);
+  Tensor best = at::empty({q.size(0), r}, q.options().dtype(at::kInt));
+  size_t wsb = 0;
+  Tensor ws = dist_ws(q, p.size(0), n_global, k, &wsb);
+  check_rc(drt_ip_topk_dist_sample(q.data_ptr(), q.size(0), p.size(0) ? p.data_ptr() : nullptr, p.size(0), n_global,
+                                   (int32_t)q.size(1), (int32_t)k, (uint32_t*)best.data_ptr<int32_t>(), ws.data_ptr(),
+                                   wsb, stream_of(q)),
+           "drt_ip_topk_dist_sample");
+  return best;
+}
+
+Tensor dist_tau(const Tensor& lists_, int64_t k) {
+  need(lists_, "lists", at::kInt, 3);
+  const c10::hip::HIPGuard g(lists_.device());
+  const Tensor lists = lists_.contiguous();
+  Tensor tau = at::empty({lists.size(1)}, lists.options().dtype(at::kFloat));
+  check_rc(drt_ip_topk_dist_tau((const uint32_t*)lists.data_ptr<int32_t>(), lists.size(1), (int32_t)lists.size(0),
+                                (int32_t)k, tau.data_ptr<float>(), stream_of(lists)),
+           "drt_ip_topk_dist_tau");
+  return tau;
+}
+
+Tensor dist_filter(const Tensor& q_, const Tensor& p_, int64_t n_global, int64_t k, int64_t id_offset,
+                   const Tensor& tau_) {
+  need(q_, "q", at::kBFloat16, 2);
+  need(p_, "p", at::kBFloat16, 2);
+  need(tau_, "tau", at::kFloat, 1);
+  const c10::hip::HIPGuard g(q_.device());
+  const Tensor q = q_.contiguous(), p = p_.contiguous(), tau = tau_.contiguous();
+  Tensor packed = at::empty({q.size(0), k + 1}, q.options().dtype(at::kLong));
+  size_t wsb = 0;
+  Tensor ws = dist_ws(q, p.size(0), n_global, k, &wsb);
+  check_rc(drt_ip_topk_dist_filter(q.data_ptr(), q.size(0), p.size(0) ? p.data_ptr() : nullptr, p.size(0), n_global,
+                                   (int32_t)q.size(1), (int32_t)k, id_offset, tau.data_ptr<float>(),
+                                   (uint64_t*)packed.data_ptr<int64_t>(), ws.data_ptr(), wsb, stream_of(q)),
+           "drt_ip_topk_dist_filter");
+  return packed;
+}
+
+std::tuple<Tensor, Tensor, Tensor> merge_packed(const Tensor& parts_, int64_t k, int64_t n_global) {
+  need(parts_, "parts", at::kLong, 3);
+  TORCH_CHECK(parts_.size(2) == k + 1, "merge_packed expects [nparts, nq, k + 1]");
+  const c10::hip::HIPGuard g(parts_.device());
+  const Tensor parts = parts_.contiguous();
+  const int64_t nq = parts.size(1);
+  Tensor s = at::empty({nq, k}, parts.options().dtype(at::kFloat));
+  Tensor i = at::empty({nq, k}, parts.options().dtype(at::kLong));
+  Tensor st = at::empty({nq}, parts.options().dtype(at::kInt));
+  check_rc(drt_topk_merge_packed((const uint64_t*)parts.data_ptr<int64_t>(), nq, (int32_t)parts.size(0), (int32_t)k,
+                                 n_global, s.data_ptr<float>(), i.data_ptr<int64_t>(), st.data_ptr<int32_t>(),
+                                 stream_of(parts)),
+           "drt_topk_merge_packed");
+  return {s, i, st};
+}
+
+// ---------------------------------------------------------------------------- training loss
+std::tuple<Tensor, Tensor, Tensor> score_ce_fwd(const Tensor& q_, const Tensor& p_, int64_t target_stride,
+                                                double scale) {
+  need(q_, "q", at::kFloat, 2);
+  need(p_, "p", at::kFloat, 2);
+  TORCH_CHECK(q_.size(1) == p_.size(1), "q ", q_.sizes(), " and p ", p_.sizes(), " differ in dimension");
+  const c10::hip::HIPGuard g(q_.device());
+  const Tensor q = q_.contiguous(), p = p_.contiguous();
+  const int64_t m = q.size(0), n = p.size(0), d = q.size(1);
+  Tensor S = at::empty({m, n}, q.options());
+  Tensor lse = at::empty({m}, q.options());
+  Tensor loss = at::empty({}, q.options());
+  const size_t wsb = drt_score_ce_workspace(m, n, (int32_t)d);
+  Tensor ws = workspace(q, wsb);
+  check_rc(drt_score_ce_fwd(q.data_ptr<float>(), p.data_ptr<float>(), m, n, (int32_t)d, target_stride, (float)scale,
+                            S.data_ptr<float>(), lse.data_ptr<float>(), loss.data_ptr<float>(), ws.data_ptr(), wsb,
+                            stream_of(q)),
+           "drt_score_ce_fwd");
+  return {loss, S, lse};
+}
+
+std::tuple<Tensor, Tensor> score_ce_bwd(const Tensor& grad_, const Tensor& q_, const Tensor& p_, const Tensor& S_,
+                                        const Tensor& lse_, int64_t target_stride, double scale) {
+  need(q_, "q", at::kFloat, 2);
+  need(p_, "p", at::kFloat, 2);
+  need(S_, "scores", at::kFloat, 2);
+  need(lse_, "lse", at::kFloat, 1);
+  const c10::hip::HIPGuard g(q_.device());
+  const Tensor q = q_.contiguous(), p = p_.contiguous(), S = S_.contiguous(), lse = lse_.contiguous();
+  const Tensor grad = grad_.to(at::kFloat).contiguous().reshape({1});
+  const int64_t m = q.size(0), n = p.size(0), d = q.size(1);
+  Tensor dq = at::empty({m, d}, q.options());
+  Tensor dp = at::empty({n, d}, q.options());
+  const size_t wsb = drt_score_ce_workspace(m, n, (int32_t)d);
+  Tensor ws = workspace(q, wsb);
+  check_rc(drt_score_ce_bwd(q.data_ptr<float>(), p.data_ptr<float>(), S.data_ptr<float>(), lse.data_ptr<float>(), m,
+                            n, (int32_t)d, target_stride, grad.data_ptr<float>(), (float)scale, dq.data_ptr<float>(),
+                            dp.data_ptr<float>(), ws.data_ptr(), wsb, stream_of(q)),
+           "drt_score_ce_bwd");
+  return {dq, dp};
+}
+
+// ---------------------------------------------------------------------------- encoder pieces
+Tensor embed_ln(const Tensor& ids_, const c10::optional<Tensor>& type_ids, const Tensor& word, const Tensor& pos,
+                const Tensor& type, const Tensor& gamma, const Tensor& beta, double eps) {
+  need(ids_, "input_ids", at::kLong, 2);
+  const c10::hip::HIPGuard g(ids_.device());
+  const Tensor ids = ids_.contiguous();
+  const int64_t B = ids.size(0), L = ids.size(1), H = word.size(1);
+  TORCH_CHECK(L <= pos.size(0), "sequence length ", L, " exceeds max_position_embeddings ", pos.size(0));
+  c10::optional<Tensor> tt;
+  if (type_ids.has_value()) tt = type_ids->contiguous();
+  Tensor out = at::empty({B, L, H}, ids.options().dtype(at::kBFloat16));
+  check_rc(drt_embed_ln(ids.data_ptr<int64_t>(), tt.has_value() ? tt->data_ptr<int64_t>() : nullptr, B, L,
+                        word.data_ptr<float>(), pos.data_ptr<float>(), type.data_ptr<float>(), gamma.data_ptr<float>(),
+                        beta.data_ptr<float>(), (float)eps, (int32_t)H, out.data_ptr(), stream_of(ids)),
+           "drt_embed_ln");
+  return out;
+}
+
+Tensor linear(const Tensor& x_, const Tensor& w_, const c10::optional<Tensor>& bias,
+              const c10::optional<Tensor>& residual, bool gelu, bool fp32_out) {
+  need(x_, "x", at::kBFloat16, 2);
+  need(w_, "w", at::kBFloat16, 2);
+  TORCH_CHECK(x_.size(1) == w_.size(1), "linear: x ", x_.sizes(), " and w ", w_.sizes(), " differ in K");
+  const c10::hip::HIPGuard g(x_.device());
+  const Tensor x = x_.contiguous(), w = w_.contiguous();
+  const int64_t M = x.size(0), K = x.size(1), N = w.size(0);
+  if (bias.has_value()) TORCH_CHECK(bias->scalar_type() == at::kFloat && bias->numel() == N, "bias: float [N]");
+  c10::optional<Tensor> res;
+  if (residual.has_value()) {
+    TORCH_CHECK(residual->scalar_type() == at::kBFloat16 && residual->numel() == M * N, "residual: bf16 [M, N]");
+    res = residual->contiguous();
+  }
+  Tensor y = at::empty({M, N}, x.options().dtype(fp32_out ? at::kFloat : at::kBFloat16));
+  const int32_t flags = (gelu ? 1 : 0) | (fp32_out ? 2 : 0);
+  const size_t wsb = drt_linear_workspace(M, N, K);
+  Tensor ws = workspace(x, wsb);
+  check_rc(drt_linear_bf16_ws(x.data_ptr(), w.data_ptr(), bias.has_value() ? bias->data_ptr<float>() : nullptr,
+                              res.has_value() ? res->data_ptr() : nullptr, y.data_ptr(), M, N, K, flags,
+                              wsb ? ws.data_ptr() : nullptr, wsb, stream_of(x)),
+           "drt_linear_bf16_ws");
+  return y;
+}
+
+Tensor attention(const Tensor& qkv_, const c10::optional<Tensor>& mask, int64_t B, int64_t heads, double scale) {
+  need(qkv_, "qkv", at::kBFloat16, 2);
+  const c10::hip::HIPGuard g(qkv_.device());
+  const Tensor qkv = qkv_.contiguous();
+  const int64_t T = qkv.size(0), H3 = qkv.size(1);
+  TORCH_CHECK(B > 0 && T % B == 0 && H3 % (3 * heads) == 0, "attention: qkv must be [B*L, 3*heads*64]");
+  const int64_t L = T / B, hd = H3 / (3 * heads);
+  c10::optional<Tensor> m;
+  if (mask.has_value()) {
+    TORCH_CHECK(mask->numel() == B * L, "attention: mask must be [B, L]");
+    m = mask->to(at::kLong).contiguous();
+  }
+  Tensor ctx = at::empty({T, heads * hd}, qkv.options());
+  check_rc(drt_attention_bf16(qkv.data_ptr(), m.has_value() ? m->data_ptr<int64_t>() : nullptr, ctx.data_ptr(), B, L,
+                              (int32_t)heads, (int32_t)hd, (float)scale, stream_of(qkv)),
+           "drt_attention_bf16");
+  return ctx;
+}
+
+Tensor layernorm(const Tensor& x_, const Tensor& gamma, const Tensor& beta, double eps) {
+  need_gpu(x_, "x");
+  const c10::hip::HIPGuard g(x_.device());
+  const Tensor x = x_.contiguous();
+  const int64_t H = x.size(-1), M = x.numel() / H;
+  Tensor out = at::empty(x.sizes(), x.options().dtype(at::kBFloat16));
+  int rc;
+  if (x.scalar_type() == at::kFloat)
+    rc = drt_layernorm_f32_bf16(x.data_ptr<float>(), M, (int32_t)H, gamma.data_ptr<float>(), beta.data_ptr<float>(),
+                                (float)eps, out.data_ptr(), stream_of(x));
+  else {
+    TORCH_CHECK(x.scalar_type() == at::kBFloat16, "layernorm: x must be float or bfloat16");
+    rc = drt_layernorm_bf16(x.data_ptr(), M, (int32_t)H, gamma.data_ptr<float>(), beta.data_ptr<float>(), (float)eps,
+                            out.data_ptr(), stream_of(x));
+  }
+  check_rc(rc, "drt_layernorm");
+  return out;
+}
+
+Tensor pool(const Tensor& hidden_, const c10::optional<Tensor>& mask, int64_t mode) {
+  need(hidden_, "hidden", at::kBFloat16, 3);
+  const c10::hip::HIPGuard g(hidden_.device());
+  const Tensor hidden = hidden_.contiguous();
+  const int64_t B = hidden.size(0), L = hidden.size(1), H = hidden.size(2);
+  c10::optional<Tensor> m;
+  if (mask.has_value()) m = mask->to(at::kLong).contiguous();
+  Tensor reps = at::empty({B, H}, hidden.options().dtype(at::kFloat));
+  check_rc(drt_pool_bf16(hidden.data_ptr(), m.has_value() ? m->data_ptr<int64_t>() : nullptr, B, L, (int32_t)H,
+                         (int32_t)mode, reps.data_ptr<float>(), nullptr, stream_of(hidden)),
+           "drt_pool_bf16");
+  return reps;
+}
+
+Tensor l2_normalize(const Tensor& x_) {
+  need(x_, "x", at::kFloat, 2);
+  const c10::hip::HIPGuard g(x_.device());
+  Tensor x = x_.clone(at::MemoryFormat::Contiguous);
+  check_rc(drt_l2_normalize_f32(x.data_ptr<float>(), x.size(0), (int32_t)x.size(1), nullptr, stream_of(x)),
+           "drt_l2_normalize_f32");
+  return x;
+}
+
+}  // namespace
+
+TORCH_LIBRARY(drt, m) {
+  m.def("ip_topk(Tensor q, Tensor p, int k, int id_offset=0) -> (Tensor, Tensor, Tensor)");
+  m.def("ip_topk.out(Tensor q, Tensor p, int k, int id_offset, *, Tensor(a!) scores, Tensor(b!) ids, "
+        "Tensor(c!) status) -> ()");
+  m.def("ip_topk_resolve(Tensor q, Tensor p, int k, int id_offset, Tensor(a!) scores, Tensor(b!) ids, "
+        "Tensor(c!) status) -> int");
+  m.def("topk_merge(Tensor scores, Tensor ids, int k_out) -> (Tensor, Tensor)");
+  m.def("dist_sample(Tensor q, Tensor p, int n_global, int k) -> Tensor");
+  m.def("dist_tau(Tensor lists, int k) -> Tensor");
+  m.def("dist_filter(Tensor q, Tensor p, int n_global, int k, int id_offset, Tensor tau) -> Tensor");
+  m.def("merge_packed(Tensor parts, int k, int n_global) -> (Tensor, Tensor, Tensor)");
+  m.def("score_ce_fwd(Tensor q, Tensor p, int target_stride, float scale) -> (Tensor, Tensor, Tensor)");
+  m.def("score_ce_bwd(Tensor grad, Tensor q, Tensor p, Tensor scores, Tensor lse, int target_stride, "
+        "float scale) -> (Tensor, Tensor)");
+  m.def("embed_ln(Tensor input_ids, Tensor? token_type_ids, Tensor word, Tensor pos, Tensor type, Tensor gamma, "
+        "Tensor beta, float eps) -> Tensor");
+  m.def("linear(Tensor x, Tensor w, Tensor? bias, Tensor? residual, bool gelu=False, bool fp32_out=False) -> Tensor");
+  m.def("attention(Tensor qkv, Tensor? mask, int batch, int heads, float scale) -> Tensor");
+  m.def("layernorm(Tensor x, Tensor gamma, Tensor beta, float eps) -> Tensor");
+  m.def("pool(Tensor hidden, Tensor? mask, int mode) -> Tensor");
+  m.def("l2_normalize(Tensor x) -> Tensor");
+}
+
+TORCH_LIBRARY_IMPL(drt, CUDA, m) {   // the GPU dispatch key of torch-ROCm
+  m.impl("ip_topk", &ip_topk);
+  m.impl("ip_topk.out", &ip_topk_out);
+  m.impl("ip_topk_resolve", &ip_topk_resolve);
+  m.impl("topk_merge", &topk_merge);
+  m.impl("dist_sample", &dist_sample);
+  m.impl("dist_tau", &dist_tau);
+  m.impl("dist_filter", &dist_filter);
+  m.impl("merge_packed", &merge_packed);
+  m.impl("score_ce_fwd", &score_ce_fwd);
+  m.impl("score_ce_bwd", &score_ce_bwd);
+  m.impl("embed_ln", &embed_ln);
+  m.impl("linear", &linear);
+  m.impl("attention", &attention);
+  m.impl("layernorm", &layernorm);
+  m.impl("pool", &pool);
+  m.impl("l2_normalize", &l2_normalize);
+}

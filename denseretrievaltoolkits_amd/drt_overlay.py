@@ -10,7 +10,9 @@ DRT.evaluator.nq_eval, ...) keeps resolving to the user's own DRT package.
 """
 from __future__ import annotations
 
+import builtins
 import importlib
+import importlib.util
 import sys
 import types
 
@@ -40,6 +42,53 @@ def _ensure_package(name: str):
         return mod
 
 
+# Names the overlay module re-exports from the user's own module when it exists: they are off the
+# hot path but other reference modules import them from there (DRT/trainer/sampler.py:5 imports
+# BM25Retriever from DRT.evaluator.index; BM25Negatives builds one, sampler.py:55).
+USER_REEXPORTS = {"DRT.evaluator.index": ("BM25Retriever", "FaissRetriever")}
+
+
+class _MissingModule(types.ModuleType):
+    """Stands in for an optional dependency of the user's module that is not installed; any use
+    raises (e.g. faiss for FaissRetriever, which the overlay does not serve)."""
+
+    def __getattr__(self, attr):
+        raise ImportError(f"{self.__name__} is not installed (needed for {self.__name__}.{attr})")
+
+
+def _user_module(name: str, optional=("faiss",)):
+    """The user's own module `name` before the overlay replaces it, or None.  If it only fails
+    to import because an optional third-party dependency is absent (the reference's index.py
+    imports faiss at module level, index.py:2), it is executed with that import bound to a
+    placeholder that raises on use, so its other classes (BM25Retriever) stay reachable."""
+    cur = sys.modules.get(name)
+    if cur is not None and not getattr(cur, "__drt_overlay__", False):
+        return cur
+    try:
+        spec = importlib.util.find_spec(name)
+    except (ImportError, ValueError):
+        return None
+    if spec is None or spec.origin is None or spec.loader is None:
+        return None
+    mod = importlib.util.module_from_spec(spec)
+    real_import = builtins.__import__
+
+    def _import(nm, globals=None, locals=None, fromlist=(), level=0):
+        if level == 0 and nm.split(".")[0] in optional:
+            try:
+                return real_import(nm, globals, locals, fromlist, level)
+            except ImportError:
+                return _MissingModule(nm)
+        return real_import(nm, globals, locals, fromlist, level)
+
+    mod.__dict__["__builtins__"] = dict(builtins.__dict__, __import__=_import)
+    try:
+        spec.loader.exec_module(mod)
+    except Exception:
+        return None
+    return mod
+
+
 def install(modules=None):
     """Register the MI355X implementations under the reference's module names."""
     from . import _native
@@ -48,6 +97,13 @@ def install(modules=None):
         mod = importlib.import_module(ours)
         parent, _, child = ref_name.rpartition(".")
         pkg = _ensure_package(parent)
+        names = USER_REEXPORTS.get(ref_name, ())
+        user = _user_module(ref_name) if names else None
+        if user is not None:
+            for n in names:
+                if hasattr(user, n):
+                    setattr(mod, n, getattr(user, n))
+        mod.__drt_overlay__ = True
         sys.modules[ref_name] = mod
         setattr(pkg, child, mod)
     return sorted(HOT_PATH_MODULES)

@@ -21,6 +21,7 @@ from __future__ import annotations
 from typing import List, Optional
 
 import numpy as np
+import torch
 
 from ..search import FlatIPIndex
 
@@ -50,12 +51,15 @@ class BaseFaissIPRetriever:
         return self.index.search_device(q_reps, k)
 
     def batch_search(self, q_reps, k: int, batch_size: int, quiet: bool = False) -> np.ndarray:
-        out = []
-        for start in range(0, q_reps.shape[0], batch_size):
-            out.append(self.search(q_reps[start: start + batch_size], k))
-        if not out:
+        """All query batches enqueued back to back (FlatIPIndex.search_batches: batch j + 1 is
+        on the GPU while batch j is certified), one host copy of the ids at the end."""
+        n = q_reps.shape[0]
+        if n == 0:
             return np.zeros((0, k), dtype=np.int64)
-        return np.concatenate(out, axis=0)
+        qd = self.index._queries(q_reps)
+        res = self.index.search_batches([qd[a: a + batch_size] for a in range(0, n, batch_size)], k)
+        self.last_scores = torch.cat([r[0] for r in res]).cpu().numpy()
+        return torch.cat([r[1] for r in res]).cpu().numpy()
 
 
 class FaissRetriever(BaseFaissIPRetriever):

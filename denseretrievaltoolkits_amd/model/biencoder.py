@@ -10,7 +10,7 @@ biencoder.py:159-241).  What changes is where the arithmetic runs:
   LayerNorm, pooling / head / L2-normalise kernels.  ``hidden`` is returned
   in bf16, ``reps`` in fp32.
 * the training score matrix + cross entropy (forward :107-119) runs on the
-  fused fp32 kernels with autograd (score_ce.ScoreCE).
+  fused fp32 kernels with autograd (torch.ops.drt.score_ce_fwd, score_ce.py).
 * the training encoder forward/backward stays on the HF module under
   torch-ROCm autograd (encoder backward kernels: SURVEY §8f, next).
 """
@@ -137,8 +137,13 @@ class DRModel(nn.Module):
         return hit[1]
 
     def _use_hip(self, model) -> bool:
+        """Inference kernels (no autograd) when no gradient can be asked for: grad mode off, or
+        a frozen tower.  Eval mode with grad on (the reference returns differentiable reps
+        there) takes the training tower, which drops dropout when the module is in eval."""
         dev = next(model.parameters()).device
-        return dev.type == "cuda" and (not self.training or not torch.is_grad_enabled())
+        if dev.type != "cuda":
+            return False
+        return not torch.is_grad_enabled() or not any(p.requires_grad for p in model.parameters())
 
     def encode(self, items, model, head):
         if items is None:
@@ -248,9 +253,11 @@ class DRModel(nn.Module):
     def dist_gather_tensor(self, t: Optional[torch.Tensor]):
         if t is None:
             return None
+        # same semantics as the reference (biencoder.py:243-254): the other ranks' slices are
+        # detached copies, this rank's slice is `t` itself so its gradient flows back
+        from .. import comm
         t = t.contiguous()
-        all_tensors = [torch.empty_like(t) for _ in range(self.world_size)]
-        dist.all_gather(all_tensors, t)
+        all_tensors = comm.all_gather_list(t)
         all_tensors[self.process_rank] = t
         return torch.cat(all_tensors, dim=0)
 

@@ -24,6 +24,7 @@ from transformers.modeling_outputs import ModelOutput
 from ..trainer.losses import CrossEntropyLoss, rr_loss_functions
 from .encoder import HipBertEncoder, linear_head
 from .linear import LinearHead
+from .train_tower import MAX_TRAIN_SEQ, tower_supported, train_hidden
 
 logger = logging.getLogger(__name__)
 
@@ -94,14 +95,22 @@ class RRModel(nn.Module):
         if self.pooling not in ("first", "mean"):
             raise ValueError("Unknown pooling type: {}".format(self.pooling))
         dev = next(self.lm.parameters()).device
-        if dev.type == "cuda" and (not self.training or not torch.is_grad_enabled()):
+        # inference kernels only when no gradient can be asked for (grad mode off or a frozen
+        # tower); eval mode with grad on returns differentiable scores as the reference does
+        frozen = not any(p.requires_grad for p in self.lm.parameters())
+        if dev.type == "cuda" and (not torch.is_grad_enabled() or frozen):
             enc, w = self._hip_state()
             mask = items.get("attention_mask")
             hidden = enc(items["input_ids"], mask, items.get("token_type_ids"))
             _, rb = enc.pool(hidden, mask, self.pooling, want_bf16=True)
             return linear_head(rb, w)  # [B, 1] fp32
-        out = self.lm(**items, return_dict=True)
-        hidden = getattr(out, self.feature)
+        if (dev.type == "cuda" and self.feature == "last_hidden_state" and "token_type_ids" not in items
+                and tower_supported(self.lm) is None and items["input_ids"].shape[1] <= MAX_TRAIN_SEQ):
+            # pair forward + backward on the HIP training tower (model/train_tower.py)
+            hidden = train_hidden(self.lm, items["input_ids"], items.get("attention_mask"))
+        else:
+            out = self.lm(**items, return_dict=True)
+            hidden = getattr(out, self.feature)
         if self.pooling == "first":
             reps = hidden[:, 0, :]
         else:

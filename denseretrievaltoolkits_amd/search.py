@@ -22,7 +22,7 @@ from typing import Optional, Tuple
 import numpy as np
 import torch
 
-from . import kernels, shards
+from . import comm, kernels, shards
 
 
 def _as_device_bf16(x, device) -> torch.Tensor:
@@ -31,6 +31,39 @@ def _as_device_bf16(x, device) -> torch.Tensor:
     if not isinstance(x, torch.Tensor):
         raise TypeError(f"expected np.ndarray or torch.Tensor, got {type(x)}")
     return x.detach().to(device=device, dtype=torch.bfloat16).contiguous()
+
+
+def _stage_status(st: torch.Tensor):
+    """Host copy of a device status vector, staged without waiting: a pinned non-blocking D2H
+    plus an event behind it.  The host looks at it only when the batch is finished, after the
+    next batch has been enqueued (search_batches), so the check never drains the stream."""
+    if not st.is_cuda:
+        return st, None
+    h = torch.empty(st.shape, dtype=st.dtype, pin_memory=True)
+    h.copy_(st, non_blocking=True)
+    ev = torch.cuda.Event()
+    ev.record()
+    return h, ev
+
+
+def _status_failed(h: torch.Tensor, ev) -> int:
+    if ev is not None:
+        ev.synchronize()
+    return int((h != 0).sum().item())
+
+
+def _pipeline(batches, enqueue, finish):
+    """Enqueue batch j + 1 before finishing (certifying) batch j."""
+    res = []
+    pend = None
+    for j, q in enumerate(batches):
+        cur = enqueue(j, q)
+        if pend is not None:
+            res.append(finish(pend))
+        pend = cur
+    if pend is not None:
+        res.append(finish(pend))
+    return res
 
 
 class FlatIPIndex:
@@ -74,12 +107,48 @@ class FlatIPIndex:
     def rows(self) -> torch.Tensor:
         return self._buf[: self.ntotal]
 
-    def search_device(self, q, k: int, id_offset: int = 0) -> Tuple[torch.Tensor, torch.Tensor]:
-        qd = _as_device_bf16(q, self.device)
-        if qd.dim() != 2 or qd.shape[1] != self.d:
-            raise ValueError(f"search: expected [nq, {self.d}] queries, got {tuple(qd.shape)}")
-        s, i, _ = kernels.ip_topk(qd, self.rows, k, id_offset=id_offset, resolve=True)
+    @classmethod
+    def from_rows(cls, rows: torch.Tensor) -> "FlatIPIndex":
+        """Wrap an existing bf16 [n, d] device tensor as the index rows (no copy)."""
+        if rows.dtype != torch.bfloat16 or rows.dim() != 2 or not rows.is_cuda:
+            raise ValueError("from_rows expects a [n, d] bf16 device tensor")
+        idx = cls(rows.shape[1], device=rows.device, capacity=0)
+        idx._buf = rows.contiguous()
+        idx.ntotal = rows.shape[0]
+        return idx
+
+    # search: the fast threshold path + certification.  A query the threshold path cannot
+    # certify (status != 0, ~1e-9 per query on real data) is redone by the exact dense rescan.
+    resolved = 0   # queries redone by the exact rescan over this index's lifetime
+
+    def _enqueue(self, q, k: int, id_offset: int = 0, out=None):
+        qd = self._queries(q)
+        s, i, st = kernels.ip_topk(qd, self.rows, k, id_offset=id_offset, resolve=False, out=out)
+        h, ev = _stage_status(st)
+        return qd, s, i, st, h, ev, id_offset, k
+
+    def _finish(self, pend):
+        qd, s, i, st, h, ev, off, k = pend
+        nbad = _status_failed(h, ev)
+        if nbad:
+            self.resolved += kernels.resolve_failed(qd, self.rows, k, off, s, i, st, n_failed=nbad)
         return s, i
+
+    def search_unresolved(self, q, k: int, id_offset: int = 0):
+        """(scores, ids, status) with status still on device (the per-shard protocol gathers it)."""
+        return kernels.ip_topk(self._queries(q), self.rows, k, id_offset=id_offset, resolve=False)
+
+    def search_device(self, q, k: int, id_offset: int = 0) -> Tuple[torch.Tensor, torch.Tensor]:
+        return self._finish(self._enqueue(q, k, id_offset))
+
+    def search_batches(self, batches, k: int, id_offset: int = 0, outs=None):
+        """Certified top-k of every query batch (device tensors), pipelined: batch j + 1 is
+        enqueued before the host checks batch j's status, so the per-batch certification
+        costs an event wait on finished work, not a drained stream.  ``outs[j]`` = optional
+        (scores, ids) output buffers of batch j.  This is the path BaseFaissIPRetriever
+        .batch_search, Trainer.evaluate and bench.py time."""
+        return _pipeline(batches, lambda j, q: self._enqueue(q, k, id_offset, outs[j] if outs else None),
+                         self._finish)
 
     def search(self, q, k: int) -> Tuple[np.ndarray, np.ndarray]:
         s, i = self.search_device(q, k)
@@ -160,57 +229,75 @@ class ShardedFlatIP:
         self.offset = 0      # global id of this shard's first row
         self.ntotal = 0      # rows over all shards
 
-    def _comm_device(self):
-        if self.world > 1 and self.dist.get_backend(self.group) == "gloo":
-            return torch.device("cpu")
-        return self.local.device
-
     def add_shard(self, x) -> None:
         """Append rows to THIS rank's shard, then agree on the global id offsets (collective)."""
         self.local.add(x)
         self.sync_offsets()
 
     def sync_offsets(self):
-        n = torch.tensor([self.local.ntotal], dtype=torch.int64, device=self._comm_device())
-        if self.world > 1:
-            allv = [torch.zeros_like(n) for _ in range(self.world)]
-            self.dist.all_gather(allv, n, group=self.group)
-            counts = [int(v.item()) for v in allv]
-        else:
-            counts = [int(n.item())]
+        counts = comm.all_gather_sizes(self.local.ntotal, self.local.device, self.group) if self.world > 1 \
+            else [int(self.local.ntotal)]
         self.offset = sum(counts[: self.rank])
         self.ntotal = sum(counts)
         return counts
 
     def search_device(self, q, k: int) -> Tuple[torch.Tensor, torch.Tensor]:
         """Every rank passes the SAME queries; every rank gets the global top-k."""
-        if self.world == 1:
-            return self.local.search_device(q, k, id_offset=self.offset)
-        if self.protocol == "global_tau" and self.ntotal < 0xFFFFFFFF:
-            res = self._search_global_tau(q, k)
-            if res is not None:
-                return res
-            self.fallbacks += 1
-        return self._search_per_shard(q, k)
+        return self._finish(self._enqueue(q, k))
+
+    def search_batches(self, batches, k: int):
+        """search_device over a sequence of query batches, batch j + 1 enqueued (scan, exchange,
+        merge) before the host checks batch j's certificate (see FlatIPIndex.search_batches)."""
+        return _pipeline(batches, lambda j, q: self._enqueue(q, k), self._finish)
 
     def _all_gather(self, t: torch.Tensor) -> torch.Tensor:
-        """Concatenated [world * rows, ...] all-gather (the layout every backend accepts)."""
-        out = torch.empty((self.world * t.shape[0],) + tuple(t.shape[1:]), dtype=t.dtype, device=t.device)
-        self.dist.all_gather_into_tensor(out, t.contiguous(), group=self.group)
-        return out.view((self.world,) + tuple(t.shape))
+        """[world, *t.shape] all-gather (RCCL on device; host-staged under gloo, comm.py)."""
+        return comm.all_gather_stacked(t, self.group)
 
-    def _search_global_tau(self, q, k: int):
-        best = self.local.dist_sample(q, self.ntotal, k)                 # [nq, r] u32 keys
-        tau = self.local.dist_tau(self._all_gather(best), k)             # [nq]
-        packed = self.local.dist_filter(q, self.ntotal, k, self.offset, tau)   # [nq, k + 1] u64
-        s, i, status = self.merge_packed(self._all_gather(packed), k, self.ntotal)
-        # every rank merged the same gathered lists, so every rank takes the same branch
-        if bool((status != 0).any()):
-            return None
-        return s, i
+    def _enqueue(self, q, k: int):
+        if self.world == 1:
+            if hasattr(self.local, "_enqueue"):
+                return ("local", self.local._enqueue(q, k, self.offset))
+            return ("done", self.local.search_device(q, k, id_offset=self.offset))
+        if self.protocol == "global_tau" and self.ntotal < 0xFFFFFFFF:
+            best = self.local.dist_sample(q, self.ntotal, k)                 # [nq, r] u32 keys
+            tau = self.local.dist_tau(self._all_gather(best), k)             # [nq]
+            packed = self.local.dist_filter(q, self.ntotal, k, self.offset, tau)   # [nq, k + 1] u64
+            s, i, status = self.merge_packed(self._all_gather(packed), k, self.ntotal)
+            # every rank merged the same gathered lists: the same status, the same branch
+            return ("gtau", q, k, s, i) + _stage_status(status)
+        return ("pshard", q, k) + self._per_shard_enqueue(q, k)
 
-    def _search_per_shard(self, q, k: int):
-        s, i = self.local.search_device(q, k, id_offset=self.offset)
+    def _per_shard_enqueue(self, q, k: int):
+        if hasattr(self.local, "search_unresolved"):
+            s, i, st = self.local.search_unresolved(q, k, id_offset=self.offset)
+        else:   # injected test doubles return exact results
+            s, i = self.local.search_device(q, k, id_offset=self.offset)
+            st = torch.zeros((s.shape[0],), dtype=torch.int32, device=s.device)
+        gst = self._all_gather(st)
+        ms, mi = self.merge(self._all_gather(s), self._all_gather(i), k)
+        # a query any rank could not certify is redone on every rank (same gathered status)
+        h, ev = _stage_status(gst.amax(0))
+        return ms, mi, h, ev, s, i, st
+
+    def _finish(self, pend):
+        kind = pend[0]
+        if kind == "done":
+            return pend[1]
+        if kind == "local":
+            return self.local._finish(pend[1])
+        if kind == "gtau":
+            _, q, k, s, i, h, ev = pend
+            if _status_failed(h, ev) == 0:
+                return s, i
+            self.fallbacks += 1
+            pend = ("pshard", q, k) + self._per_shard_enqueue(q, k)
+        _, q, k, ms, mi, h, ev, s, i, st = pend
+        if _status_failed(h, ev) == 0:
+            return ms, mi
+        # some rank has uncertified queries: each rank redoes its own exactly, then re-merge
+        nres = kernels.resolve_failed(self.local._queries(q), self.local.rows, k, self.offset, s, i, st)
+        self.local.resolved += nres
         return self.merge(self._all_gather(s), self._all_gather(i), k)
 
     def search(self, q, k: int) -> Tuple[np.ndarray, np.ndarray]:

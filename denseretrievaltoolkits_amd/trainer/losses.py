@@ -1,5 +1,5 @@
 """Contrastive losses with the reference's API (DRT/trainer/losses.py:7-45); the
-score matrix + cross entropy runs on the fused fp32 HIP op (score_ce.ScoreCE).
+score matrix + cross entropy runs on the fused fp32 HIP op (torch.ops.drt.score_ce_fwd, score_ce.py).
 The reranker losses (:48-88) are elementwise torch and kept as is in spirit."""
 from __future__ import annotations
 
@@ -38,8 +38,8 @@ class DistributedContrastiveLoss(SimpleContrastiveLoss):
         return loss * self.word_size if self.scale_loss else loss
 
     def gather_tensor(self, t):
-        gathered = [torch.empty_like(t) for _ in range(self.word_size)]
-        dist.all_gather(gathered, t)
+        from .. import comm
+        gathered = comm.all_gather_list(t.contiguous())
         gathered[self.rank] = t
         return torch.cat(gathered, dim=0)
 

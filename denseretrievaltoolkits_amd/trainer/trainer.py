@@ -32,6 +32,7 @@ import torch.distributed as dist
 from torch import optim
 from torch.nn.parallel import DistributedDataParallel as DDP
 
+from .. import comm
 from ..evaluator.metrics import get_metrics
 from ..evaluator.nq_eval import AnswerMatcher, has_answers
 from ..search import ShardedFlatIP
@@ -68,13 +69,16 @@ class Trainer:
     def _wrapper_model(self):
         self.world, self.rank = _world()
         self.local_rank = int(os.environ.get("LOCAL_RANK", "0"))
-        torch.cuda.set_device(self.local_rank)
-        self.device = torch.device("cuda", self.local_rank)
+        # one process per GPU (run.sh: torch.distributed.launch); ranks beyond the visible
+        # devices share them (the multi-rank tests run several gloo ranks on one GPU)
+        dev_index = self.local_rank % max(1, torch.cuda.device_count())
+        torch.cuda.set_device(dev_index)
+        self.device = torch.device("cuda", dev_index)
         if dist.is_initialized():
             dist.barrier()
         self.model = self.model.to(self.device)
         if self.world > 1:
-            self.model = DDP(self.model, device_ids=[self.local_rank], output_device=self.local_rank,
+            self.model = DDP(self.model, device_ids=[dev_index], output_device=dev_index,
                              find_unused_parameters=True)
 
     @property
@@ -183,22 +187,19 @@ class Trainer:
             dist.barrier()
 
     def _search(self, q_reps: torch.Tensor, k: int) -> np.ndarray:
-        """Global top-k ids for THIS rank's query batch (all ranks call it together)."""
+        """Global top-k ids for THIS rank's query batch (all ranks call it together).
+
+        The reference searches each rank's own queries against a full host index on every
+        rank (trainer.py:296-297).  Here the corpus is row-sharded, so the ranks' query
+        batches (ragged: the last batch may differ per rank) are all-gathered, every rank
+        scans its shard for all of them, and each keeps its own rows of the merged result."""
         if self.world == 1:
             _, i = self.index.search_device(q_reps, k)
             return i.cpu().numpy()
-        n_local = torch.tensor([q_reps.shape[0]], device=self.device)
-        sizes = [torch.zeros_like(n_local) for _ in range(self.world)]
-        dist.all_gather(sizes, n_local)
-        sizes = [int(s.item()) for s in sizes]
-        mx = max(sizes)
-        pad = torch.zeros((mx, q_reps.shape[1]), dtype=q_reps.dtype, device=self.device)
-        pad[: q_reps.shape[0]] = q_reps
-        allq = torch.empty((self.world * mx, q_reps.shape[1]), dtype=q_reps.dtype, device=self.device)
-        dist.all_gather_into_tensor(allq, pad.contiguous())
+        allq, sizes = comm.all_gather_rows(q_reps.contiguous())
         _, ids = self.index.search_device(allq, k)
-        mine = ids[self.rank * mx: self.rank * mx + sizes[self.rank]]
-        return mine.cpu().numpy()
+        lo = sum(sizes[: self.rank])
+        return ids[lo: lo + sizes[self.rank]].cpu().numpy()
 
     def _doc_text(self, did_):
         t = self._doc_cache.get(did_)

@@ -61,12 +61,17 @@ int drt_ip_topk_bf16(const void* Q, int64_t nq, const void* P, int64_t n, int32_
                      void* stream);
 
 /* Exact slow path for every query whose status (device array from
- * drt_ip_topk_bf16) is non-zero.  SYNCHRONOUS: reads status back, allocates
- * scratch, rescans the shard for those queries only, and clears their status.
- * Returns the number of resolved queries in *n_resolved (may be NULL).      */
+ * drt_ip_topk_bf16) is non-zero.  SYNCHRONOUS: reads status back, rescans the
+ * shard for those queries only (dense scores of up to ~2 GB per chunk in the
+ * caller's workspace: drt_ip_topk_resolve_workspace(#failed queries, n, d)
+ * bytes; a smaller workspace means smaller chunks, too small = DRT_EINVAL),
+ * and clears their status.  Returns the number of resolved queries in
+ * *n_resolved (may be NULL).  Nothing is allocated inside.                  */
+size_t drt_ip_topk_resolve_workspace(int64_t n_failed, int64_t n, int32_t d);
 int drt_ip_topk_resolve(const void* Q, int64_t nq, const void* P, int64_t n, int32_t d,
                         int32_t k, int64_t id_offset, float* out_scores, int64_t* out_ids,
-                        int32_t* status, int64_t* n_resolved, void* stream);
+                        int32_t* status, void* workspace, size_t workspace_bytes,
+                        int64_t* n_resolved, void* stream);
 
 /* Benchmark/test switch: 0 = production scan (16-row tiles, 6-slot ring),
  * 1 = filter scan WITHOUT its MFMA work (memory-pipeline ceiling; results are

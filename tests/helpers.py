@@ -47,3 +47,15 @@ def sample_plan(n, k):
     stride = max(1, n // m)
     m = (n - stride // 2 + stride - 1) // stride
     return dict(r=r, m=m, stride=stride, cap=cap, rows=np.arange(m) * stride + stride // 2)
+
+
+def corpus_topk_golden():
+    """tests/golden/corpus_topk.npz (reference merge_retrieval_results_by_score top-k) plus its
+    inputs regenerated from the stored spec (tools/gen_golden.corpus_topk_inputs)."""
+    import os
+    z = np.load(os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "corpus_topk.npz"))
+    rng = np.random.default_rng(int(z["seed"]))
+    lim = int(z["lim"])
+    q = rng.integers(-lim, lim + 1, size=(int(z["nq"]), int(z["d"]))).astype(np.float32)
+    p = rng.integers(-lim, lim + 1, size=(int(z["n"]), int(z["d"]))).astype(np.float32)
+    return q, p, int(z["k"]), int(z["parts"]), z["ids"].astype(np.int64), z["scores"]

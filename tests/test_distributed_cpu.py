@@ -115,6 +115,59 @@ def test_global_tau_uneven_and_empty_shards():
     _run(4, 20001, k=10, nq=3, vals=8)
 
 
+def _trainer_worker(rank, world, port, out_q):
+    """Trainer._index_corpus / _search bookkeeping (trainer.py:220-262, 289-297 replaced): doc-id
+    all-gather in rank order, ragged query batches all-gathered, each rank gets its own rows."""
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from denseretrievaltoolkits_amd.search import ShardedFlatIP
+        from denseretrievaltoolkits_amd.trainer.trainer import Trainer
+        d, k, n = 16, 7, 301
+        rng = np.random.default_rng(2)
+        p = rng.integers(-3, 4, size=(n, d)).astype(np.float32)
+        docs = [f"doc{j}" for j in range(n)]
+        order = list(range(n)) + list(range((-n) % world))      # DistributedSampler padding
+        mine = order[rank::world]
+        tr = object.__new__(Trainer)
+        tr.world, tr.rank, tr.local_rank, tr.device = world, rank, rank, torch.device("cpu")
+        tr.training_args = None
+        tr.index = ShardedFlatIP(d, local=_OracleShard(d), merge=_oracle_merge, merge_packed=_oracle_merge_packed)
+        tr.index.local.add(p[mine])
+        tr._ids_local = [docs[j] for j in mine]
+        tr._index_corpus(0)
+        assert tr.idx == [docs[j] for r in range(world) for j in order[r::world]]
+        glob_rows = np.concatenate([p[order[r::world]] for r in range(world)])
+        ok = True
+        for nq_rank in ([5, 3, 4][:world], [2, 0, 1][:world]):    # ragged, and one empty rank
+            qall = rng.integers(-3, 4, size=(sum(nq_rank), d)).astype(np.float32)
+            lo = sum(nq_rank[:rank])
+            q = torch.from_numpy(qall[lo: lo + nq_rank[rank]])
+            ids = tr._search(q, k)
+            _, ei = orc.ip_topk(qall[lo: lo + nq_rank[rank]], glob_rows, k)
+            ok &= ids.shape == (nq_rank[rank], k) and bool(np.array_equal(ids, ei))
+        out_q.put((rank, ok, 0))
+    except Exception as e:  # pragma: no cover - reported to the parent
+        out_q.put((rank, False, repr(e)))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_trainer_index_and_search_bookkeeping(world):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_trainer_worker, args=(r, world, port, q)) for r in range(world)]
+    for pr in procs:
+        pr.start()
+    res = [q.get(timeout=180) for _ in range(world)]
+    for pr in procs:
+        pr.join(timeout=60)
+    assert all(r[1] for r in res), res
+
+
 def test_overlay_registers_hot_path_modules():
     import sys
     from denseretrievaltoolkits_amd import drt_overlay
@@ -127,3 +180,72 @@ def test_overlay_registers_hot_path_modules():
     for n in list(sys.modules):
         if n == "DRT" or n.startswith("DRT."):
             del sys.modules[n]
+
+
+USER_INDEX = '''
+import numpy as np
+import faiss
+
+
+class BaseFaissIPRetriever:
+    def __init__(self, init_reps):
+        self.index = faiss.IndexFlatIP(init_reps)
+
+
+class FaissRetriever(BaseFaissIPRetriever):
+    def __init__(self, init_reps, factory_str):
+        self.index = faiss.index_factory(init_reps.shape[1], factory_str)
+
+
+class BM25Retriever(BaseFaissIPRetriever):
+    def __init__(self, topK, vocab_size):
+        self.topK = topK
+        self.vocab_size = vocab_size
+'''
+
+USER_SAMPLER = '''
+from ..evaluator.index import BM25Retriever
+
+
+class BM25Negatives:
+    def __init__(self, data_args, vocab_size):
+        self.num_negative = data_args.train_n_passages - 1
+        self.retriever = BM25Retriever(self.num_negative, vocab_size)
+'''
+
+
+def test_overlay_keeps_users_bm25_reachable(tmp_path, monkeypatch):
+    """run_BM25_negative.py under the overlay: the user's sampler imports BM25Retriever from
+    DRT.evaluator.index (reference sampler.py:5,55); install() re-exports the user's class even
+    when faiss (imported at module level by the user's index.py:2) is absent."""
+    import sys
+    from types import SimpleNamespace
+    from denseretrievaltoolkits_amd import drt_overlay
+    from denseretrievaltoolkits_amd.evaluator import index as ours
+    saved = {n: getattr(ours, n) for n in ("BM25Retriever", "FaissRetriever")}
+    root = tmp_path / "user"
+    for pkg in ("DRT", "DRT/evaluator", "DRT/trainer"):
+        (root / pkg).mkdir(parents=True)
+        (root / pkg / "__init__.py").write_text("")
+    (root / "DRT/evaluator/index.py").write_text(USER_INDEX)
+    (root / "DRT/trainer/sampler.py").write_text(USER_SAMPLER)
+    for n in list(sys.modules):
+        if n == "DRT" or n.startswith("DRT."):
+            del sys.modules[n]
+    monkeypatch.syspath_prepend(str(root))
+    try:
+        drt_overlay.install()
+        import DRT.evaluator.index as idx_mod
+        from DRT.trainer.sampler import BM25Negatives
+        assert idx_mod.BaseFaissIPRetriever.__module__ == "denseretrievaltoolkits_amd.evaluator.index"
+        neg = BM25Negatives(SimpleNamespace(train_n_passages=8), vocab_size=30522)
+        assert type(neg.retriever).__name__ == "BM25Retriever" and neg.retriever.topK == 7
+        assert type(neg.retriever).__module__ == "DRT.evaluator.index"
+        with pytest.raises(ImportError, match="faiss"):
+            idx_mod.FaissRetriever(np.zeros((2, 4), np.float32), "Flat")
+    finally:
+        for n, v in saved.items():
+            setattr(ours, n, v)
+        for n in list(sys.modules):
+            if n == "DRT" or n.startswith("DRT."):
+                del sys.modules[n]

@@ -60,6 +60,25 @@ def test_oracle_scores_are_reference_score_matrix():
             assert np.all(np.diff(s[r]) <= 0)
 
 
+def test_oracle_corpus_topk_matches_reference_merge():
+    """oracle.ip_topk over a 20k-row corpus at k = 1000 == the reference's own top-k
+    (merge_retrieval_results_by_score over 3 row partitions, utils.py:215-229), ids and scores."""
+    from helpers import corpus_topk_golden
+    q, p, k, parts, ids, scores = corpus_topk_golden()
+    s, i = orc.ip_topk(q, p, k)
+    np.testing.assert_array_equal(i, ids)
+    np.testing.assert_array_equal(s, scores)
+    # and the oracle's partition merge of per-partition top-k lists
+    bounds = np.linspace(0, p.shape[0], parts + 1).astype(int)
+    ss, ii = [], []
+    for a, b in zip(bounds[:-1], bounds[1:]):
+        ps, pi = orc.ip_topk(q, p[a:b], k)
+        ss.append(ps)
+        ii.append(pi + a)
+    ms, mi = orc.merge_topk(np.stack(ss), np.stack(ii), k)
+    np.testing.assert_array_equal(mi, ids)
+
+
 def _hf(layers, seed):
     import torch
     from transformers import BertModel

@@ -1,0 +1,397 @@
+"""GPU, several ranks: the distributed hot paths as real processes on the HIP kernels.
+
+World 2 / 3 gloo process groups whose ranks share the one GPU of the test box
+(collectives staged through host memory, comm.py; RCCL replaces gloo on a real
+multi-GPU node, nothing else changes).  Every rank runs the real FlatIPIndex
+scan kernels, the real packed / plain merges and the real encoder kernels:
+
+* ShardedFlatIP, both protocols and the forced global-tau fallback, vs the
+  oracle bit for bit; at world 3 against the reference's own top-k
+  (tests/golden/corpus_topk.npz, merge_retrieval_results_by_score).
+  Reference: trainer.py:220-262 (rank-0 index of every rank's rows),
+  index.py:31-33 (search), utils.py:215-229 (partition merge).
+* Trainer.evaluate at world 2 (query all-gather, object all-gather of doc ids,
+  per-rank retrieve / metrics files) vs the oracle over the concatenated
+  shard rows.  Reference: trainer.py:191-346.
+* DRModel.forward and DistributedContrastiveLoss with negatives_x_device:
+  the two ranks hold the two halves of the reference's golden batch
+  (tests/golden/loss.npz), so loss = world x the golden loss and the local
+  gradients = world x the golden gradient rows.  Reference:
+  biencoder.py:103-119,243-254; losses.py:20-40.
+* RRTrainer.evaluate at world 2: per-rank result files, rank-0 metrics ==
+  the reference's file merge + argsort + get_metrics flow restated over the
+  written files.  Reference: trainer.py:403-484.
+"""
+import json
+import os
+import socket
+import traceback
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+TIMEOUT = 240
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _init(rank, world, port):
+    import torch
+    import torch.distributed as dist
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
+                      LOCAL_RANK=str(rank))
+    torch.cuda.set_device(0)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    return torch.device("cuda", 0)
+
+
+def _entry(fn, rank, world, port, out_q, args):
+    import torch.distributed as dist
+    try:
+        dev = _init(rank, world, port)
+        res = fn(rank, world, dev, *args)
+        out_q.put((rank, True, res))
+    except Exception:  # report, never hang the parent
+        out_q.put((rank, False, traceback.format_exc()))
+    finally:
+        if dist.is_initialized():
+            dist.destroy_process_group()
+
+
+def _spawn(fn, world, *args):
+    import torch.multiprocessing as mp
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_entry, args=(fn, r, world, port, q, args)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = {}
+    try:
+        for _ in range(world):
+            r, ok, v = q.get(timeout=TIMEOUT)
+            res[r] = (ok, v)
+    finally:
+        for p in procs:
+            p.join(timeout=60)
+            if p.is_alive():
+                p.kill()
+    bad = {r: v for r, (ok, v) in res.items() if not ok}
+    assert not bad, "\n".join(f"rank {r}:\n{v}" for r, v in bad.items())
+    return {r: v for r, (_, v) in res.items()}
+
+
+# ---------------------------------------------------------------------------
+# sharded search
+# ---------------------------------------------------------------------------
+def _w_sharded(rank, world, dev, case):
+    import torch
+    from helpers import corpus_topk_golden, int_bf16, to_dev_bf16
+    from oracle import search_oracle as orc
+    from denseretrievaltoolkits_amd.search import ShardedFlatIP
+    out = {}
+    if case == "golden":
+        q, p, k, _, gids, gscores = corpus_topk_golden()
+        protocols = ["global_tau", "per_shard"]
+    elif case == "ties":
+        # every row identical: all scores tie, far more than k candidates per shard pass tau,
+        # so the global-tau lists overflow and the batch must take the per-shard fallback
+        rng = np.random.default_rng(5)
+        q = int_bf16(rng, (9, 256), -3, 3)
+        p = np.repeat(int_bf16(rng, (1, 256), -3, 3), 50000, axis=0)
+        k = 100
+        protocols = ["global_tau"]
+    else:
+        rng = np.random.default_rng(41)
+        q = int_bf16(rng, (37, 768), -4, 4)
+        p = int_bf16(rng, (90001, 768), -4, 4)
+        k = 1000
+        protocols = ["global_tau", "per_shard"]
+    es, ei = orc.ip_topk(q, p, k)
+    lo, hi = orc.shard_bounds(p.shape[0], world, rank)
+    for proto in protocols:
+        idx = ShardedFlatIP(p.shape[1], device=dev, protocol=proto)
+        idx.add_shard(to_dev_bf16(p[lo:hi], dev))
+        assert idx.offset == lo and idx.ntotal == p.shape[0], (idx.offset, lo, idx.ntotal)
+        s, i = idx.search_device(to_dev_bf16(q, dev), k)
+        torch.cuda.synchronize()
+        s, i = s.cpu().numpy(), i.cpu().numpy()
+        np.testing.assert_array_equal(i, ei)
+        np.testing.assert_array_equal(s, es)
+        if case == "golden":
+            np.testing.assert_array_equal(i, gids)
+            np.testing.assert_array_equal(s, gscores)
+        out[proto] = idx.fallbacks
+    return out
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_sharded_search_multiprocess_integer(world):
+    res = _spawn(_w_sharded, world, "int")
+    assert all(v["global_tau"] == 0 for v in res.values()), res
+
+
+def test_sharded_search_multiprocess_reference_golden():
+    """World 3 over the reference's golden corpus: ids and scores == merge_retrieval_results_by_score."""
+    _spawn(_w_sharded, 3, "golden")
+
+
+def test_sharded_search_multiprocess_fallback():
+    res = _spawn(_w_sharded, 2, "ties")
+    assert all(v["global_tau"] == 1 for v in res.values()), res
+
+
+# ---------------------------------------------------------------------------
+# Trainer.evaluate at world 2
+# ---------------------------------------------------------------------------
+WORDS = ["paris", "tower", "river", "york", "music", "rock", "roll", "river bank", "tokyo", "alps"]
+
+
+def _w_trainer(rank, world, dev, tmp):
+    from types import SimpleNamespace
+    import torch
+    from transformers import BertModel
+    from oracle import bert_weights as bw
+    from oracle import search_oracle as orc
+    from denseretrievaltoolkits_amd import shards
+    from denseretrievaltoolkits_amd.evaluator.metrics import get_metrics
+    from denseretrievaltoolkits_amd.evaluator.nq_eval import has_answers
+    from denseretrievaltoolkits_amd.model.biencoder import DRModel
+    from denseretrievaltoolkits_amd.trainer.trainer import Trainer
+
+    n_docs, n_q, k, bs = 2001, 41, 50, 128
+    rng = np.random.default_rng(3)
+    corpus = [{"original": " ".join(rng.choice(WORDS, size=int(rng.integers(3, 12))))} for _ in range(n_docs)]
+    answers = [[str(rng.choice(WORDS))] for _ in range(n_q)]
+    p_ids, p_mask = bw.token_batch(n_docs, 64, seed=11)
+    q_ids, q_mask = bw.token_batch(n_q, 16, seed=12)
+    # the reference's DistributedSampler(shuffle=False) split: pad to a multiple of world with
+    # repeats, rank r takes indices r::world (corpus_dataloader.py:17-25); queries likewise but
+    # left ragged here (the last rank has one query fewer) to exercise uneven batches
+    pad = (-n_docs) % world
+    order = list(range(n_docs)) + list(range(pad))
+    mine = order[rank::world]
+    qmine = list(range(n_q))[rank::world]
+
+    class _L:
+        def __init__(self, batches, dataset=None):
+            self.batches, self.dataset, self.sampler = batches, dataset, None
+
+        def __iter__(self):
+            return iter(self.batches)
+
+    def tb(a, idx):
+        return torch.from_numpy(a[idx])
+
+    cb = [(mine[a:a + bs], {"input_ids": tb(p_ids, mine[a:a + bs]), "attention_mask": tb(p_mask, mine[a:a + bs])})
+          for a in range(0, len(mine), bs)]
+    qb = [(qmine[a:a + 16], {"input_ids": tb(q_ids, qmine[a:a + 16]), "attention_mask": tb(q_mask, qmine[a:a + 16])},
+           [answers[i] for i in qmine[a:a + 16]], [f"q{i}" for i in qmine[a:a + 16]])
+          for a in range(0, len(qmine), 16)]
+    torch.manual_seed(0)
+    lm = BertModel(bw.bert_config(layers=1), add_pooling_layer=False).eval()
+    bw.init_model_(lm, 5)
+    model = DRModel(lm_q=lm, lm_p=lm, pooling="first", normalize=True)
+    args = SimpleNamespace(loss_fn="SimpleContrastiveLoss", learning_rate=1e-5, optimizer="adamw", topk="1,5,20,50",
+                           retrieve_num=k, retrieve_dir=os.path.join(tmp, "ret"), cache_train_dir=os.path.join(tmp, "cache"),
+                           encode_corpus_dir=os.path.join(tmp, "emb"), index_order_dir=os.path.join(tmp, "idx"),
+                           max_epochs=0, save_per_train=1, eval_per_train=1)
+    tr = Trainer(args, model, corpus_dataloader=_L(cb, corpus), eval_loader=_L(qb))
+    m = tr.evaluate(_L(qb), 0)
+    assert m["query_num"] == len(qmine)
+
+    # independent restatement: every rank's shard file in rank order = the global row order,
+    # the gathered doc-id list maps rows to docs (trainer.py:307-308)
+    rows = shards.load_rows(shards.list_shards(os.path.join(tmp, "emb"), 0), 0, len(order), "cpu").float().numpy()
+    assert rows.shape == (len(order), 768)
+    with open(os.path.join(tmp, "idx", "0.docid.txt"), encoding="utf-8") as f:
+        row_doc = json.load(f)["id"]
+    assert row_doc == [d for r in range(world) for d in order[r::world]]
+    mod = tr.module
+    with torch.no_grad():
+        qr = torch.cat([mod(query={kk: v.to(dev) for kk, v in b[1].items()}).q_reps for b in qb]).float().cpu()
+    q = qr.to(torch.bfloat16).float().numpy()
+    es, ei = orc.ip_topk(q, rows, k)
+    got = {}
+    with open(os.path.join(tmp, "ret", f"0.{rank}.json"), encoding="utf-8") as f:
+        for line in f:
+            r = json.loads(line)
+            got.setdefault(r["query_id"], []).append(r["doc_id"])
+    pos = np.zeros((len(qmine), k), np.int8)
+    for qi, qid in enumerate(qmine):
+        g = got[qid]
+        assert len(g) == k
+        for j in range(k):
+            want = row_doc[ei[qi, j]]
+            if g[j] != want:
+                # only exact-score ties in the oracle may reorder (duplicated padding rows tie exactly)
+                assert es[qi, j] == es[qi, max(0, j - 1)] or es[qi, j] == es[qi, min(k - 1, j + 1)], (qid, j)
+            pos[qi, j] = has_answers(corpus[g[j]]["original"], answers[qid])
+    ref = get_metrics(pos, [1, 5, 20, 50])
+    for key, v in ref.items():
+        assert abs(m[key] - v / len(qmine)) < 1e-9, (key, m[key], v / len(qmine))
+    with open(os.path.join(tmp, "cache", f"0.{rank}_metrics"), encoding="utf-8") as f:
+        assert json.load(f)["query_num"] == len(qmine)
+    return tr.index.fallbacks
+
+
+def test_trainer_evaluate_world2(tmp_path):
+    res = _spawn(_w_trainer, 2, str(tmp_path))
+    assert set(res) == {0, 1}
+
+
+# ---------------------------------------------------------------------------
+# negatives_x_device: DRModel.forward / DistributedContrastiveLoss at world 2
+# ---------------------------------------------------------------------------
+def _w_xdev(rank, world, dev, golden_path):
+    import torch
+    from types import SimpleNamespace
+    from transformers import BertModel
+    from oracle import bert_weights as bw
+    from denseretrievaltoolkits_amd.model.biencoder import DRModel
+    from denseretrievaltoolkits_amd.trainer.losses import DistributedContrastiveLoss
+
+    z = np.load(golden_path)
+    q, p, n = z["n2_q"], z["n2_p"], int(z["n2_n"])
+    bq = q.shape[0] // world
+    ql = torch.from_numpy(q[rank * bq:(rank + 1) * bq]).to(dev).requires_grad_(True)
+    pl = torch.from_numpy(p[rank * bq * n:(rank + 1) * bq * n]).to(dev).requires_grad_(True)
+    loss = DistributedContrastiveLoss()(ql, pl)
+    loss.backward()
+    out = {}
+    np.testing.assert_allclose(loss.item(), world * float(z["n2_loss"]), rtol=1e-5)
+    np.testing.assert_allclose(ql.grad.cpu().numpy(), world * z["n2_dq"][rank * bq:(rank + 1) * bq], rtol=1e-4,
+                               atol=1e-6)
+    np.testing.assert_allclose(pl.grad.cpu().numpy(), world * z["n2_dp"][rank * bq * n:(rank + 1) * bq * n],
+                               rtol=1e-4, atol=1e-6)
+
+    # DRModel.forward with negatives_x_device on the HIP training tower (dropout off)
+    cfg = bw.bert_config(layers=1)
+    cfg.hidden_dropout_prob = 0.0
+    cfg.attention_probs_dropout_prob = 0.0
+    torch.manual_seed(0)
+    lm = BertModel(cfg, add_pooling_layer=False)
+    bw.init_model_(lm, 5)
+    lm = lm.to(dev).train()
+    model = DRModel(lm_q=lm, lm_p=lm, pooling="first", data_args=SimpleNamespace(train_n_passages=2),
+                    train_args=SimpleNamespace(negatives_x_device=True)).train()
+    qi, qm = bw.token_batch(3, 16, seed=100 + rank)
+    pi, pm = bw.token_batch(6, 32, seed=200 + rank)
+    o = model(query={"input_ids": torch.from_numpy(qi).to(dev), "attention_mask": torch.from_numpy(qm).to(dev)},
+              passage={"input_ids": torch.from_numpy(pi).to(dev), "attention_mask": torch.from_numpy(pm).to(dev)})
+    assert o.q_reps.shape == (3 * world, 768) and o.p_reps.shape == (6 * world, 768)
+    o.q_reps.retain_grad()
+    o.p_reps.retain_grad()
+    o.loss.backward()
+    qa = o.q_reps.detach().double().cpu()
+    pa = o.p_reps.detach().double().cpu()
+    qa.requires_grad_(True)
+    pa.requires_grad_(True)
+    tgt = torch.arange(qa.shape[0]) * 2
+    ref = world * torch.nn.functional.cross_entropy(qa @ pa.T, tgt)
+    ref.backward()
+    np.testing.assert_allclose(o.loss.item(), ref.item(), rtol=1e-5)
+    np.testing.assert_allclose(o.q_reps.grad.double().cpu().numpy(), qa.grad.numpy(), rtol=1e-4, atol=1e-7)
+    np.testing.assert_allclose(o.p_reps.grad.double().cpu().numpy(), pa.grad.numpy(), rtol=1e-4, atol=1e-7)
+    # the tower receives gradient only through its own (local) rows
+    g = lm.embeddings.word_embeddings.weight.grad
+    assert g is not None and torch.isfinite(g).all() and g.abs().sum() > 0
+    out["loss"] = o.loss.item()
+    return out
+
+
+def test_negatives_x_device_world2():
+    from conftest import REPO
+    res = _spawn(_w_xdev, 2, os.path.join(REPO, "tests", "golden", "loss.npz"))
+    # the x-device loss is the same global quantity on every rank
+    assert abs(res[0]["loss"] - res[1]["loss"]) <= 1e-5 * abs(res[0]["loss"])
+
+
+# ---------------------------------------------------------------------------
+# RRTrainer.evaluate at world 2
+# ---------------------------------------------------------------------------
+def _w_rrtrainer(rank, world, dev, tmp):
+    from types import SimpleNamespace
+    import torch
+    from transformers import BertModel
+    from oracle import bert_weights as bw
+    from denseretrievaltoolkits_amd.evaluator.metrics import get_metrics
+    from denseretrievaltoolkits_amd.evaluator.nq_eval import has_answers
+    from denseretrievaltoolkits_amd.model.linear import LinearHead
+    from denseretrievaltoolkits_amd.model.reranker import RRModel
+    from denseretrievaltoolkits_amd.trainer.trainer import RRTrainer
+
+    n_q, per_q, L = 6, 20, 48
+    rng = np.random.default_rng(9)
+    docs = [" ".join(rng.choice(WORDS, size=int(rng.integers(2, 9)))) for _ in range(n_q * per_q)]
+    answers = [[str(rng.choice(WORDS))] for _ in range(n_q)]
+    ids, mask = bw.token_batch(n_q * per_q, L, seed=21)
+    pairs = [(f"q{j // per_q}", j) for j in range(n_q * per_q)]
+    mine = pairs[rank::world]                  # DistributedSampler(shuffle=False) split of the pairs
+    batches = []
+    for a in range(0, len(mine), 16):
+        sel = [j for _, j in mine[a:a + 16]]
+        batches.append(([q for q, _ in mine[a:a + 16]],
+                         {"input_ids": torch.from_numpy(ids[sel]), "attention_mask": torch.from_numpy(mask[sel])},
+                         [answers[j // per_q] for j in sel], [docs[j] for j in sel], [f"d{j}" for j in sel]))
+
+    class _L:
+        def __init__(self, b):
+            self.b, self.sampler = b, None
+
+        def __iter__(self):
+            return iter(self.b)
+
+    torch.manual_seed(0)
+    lm = BertModel(bw.bert_config(layers=1), add_pooling_layer=False).eval()
+    bw.init_model_(lm, 2)
+    head = LinearHead(768, 1)
+    with torch.no_grad():
+        head.linear.weight.copy_(torch.from_numpy(bw.param_value(2, "rr_head.linear.weight", (1, 768))))
+    model = RRModel(lm=lm, head=head, pooling="first")
+    args = SimpleNamespace(loss_fn="none", learning_rate=1e-5, optimizer="adamw", topk=[1, 5, 10],
+                           rr_result_dir=os.path.join(tmp, "rr"), cache_train_dir=os.path.join(tmp, "cache"))
+    tr = RRTrainer(args, model)
+    m = tr.evaluate(_L(batches), 3)
+    import torch.distributed as dist
+    dist.barrier()
+    if rank != 0:
+        assert m is None
+        return None
+    # the reference's rank-0 merge (trainer.py:449-482) restated over the per-rank files
+    res = {}
+    for fn in sorted(os.listdir(os.path.join(tmp, "rr"))):
+        if fn.startswith("3."):
+            with open(os.path.join(tmp, "rr", fn), encoding="utf-8") as f:
+                for line in f:
+                    dct = json.loads(line)
+                    assert dct["match"] == int(has_answers(dct["document"], answers[int(dct["qid"][1:])]))
+                    r = res.setdefault(dct["qid"], ([], []))
+                    r[0].append(dct["score"])
+                    r[1].append(dct["match"])
+    assert len(res) == n_q and all(len(v[0]) == per_q for v in res.values())
+    want = {f"{mt}@{k}": 0.0 for mt in ["MRR", "NDCG", "Recall"] for k in [1, 5, 10]}
+    for _, (scores, is_true) in res.items():
+        scores = np.array(scores)
+        met = get_metrics([np.array(is_true)[np.argsort(-scores, kind="stable")]], [1, 5, 10])
+        for key in want:
+            want[key] += met[key]
+    want["query_num"] = n_q
+    for key in want:
+        want[key] /= n_q           # the reference divides query_num too (trainer.py:476-478)
+    for key, v in want.items():
+        assert abs(m[key] - v) < 1e-12, (key, m[key], v)
+    with open(os.path.join(tmp, "cache", "3.0_RR_metrics"), encoding="utf-8") as f:
+        assert json.load(f) == pytest.approx(m)
+    return {"n_q": len(res)}
+
+
+def test_rrtrainer_evaluate_world2(tmp_path):
+    res = _spawn(_w_rrtrainer, 2, str(tmp_path))
+    assert res[1] is None and res[0] is not None

@@ -144,6 +144,35 @@ def gen_merge(ref_utils):
         json.dump(cases, f)
 
 
+def corpus_topk_inputs(seed=31, n=20000, nq=16, d=768, lim=16):
+    """Integer-valued embeddings (exact in bf16 and in every fp32 dot product), regenerated
+    from this spec on the GPU box."""
+    rng = np.random.default_rng(seed)
+    q = rng.integers(-lim, lim + 1, size=(nq, d)).astype(np.float32)
+    p = rng.integers(-lim, lim + 1, size=(n, d)).astype(np.float32)
+    return q, p
+
+
+def gen_corpus_topk(ref_utils, k=1000, parts=3):
+    """Corpus-level top-k from the reference's own partition merge
+    (merge_retrieval_results_by_score, DRT/model/utils.py:215-229): the corpus is cut into
+    `parts` contiguous row partitions (as the sharded search cuts it), each partition's
+    {doc: score} is q . p^T (biencoder.py:107), and the reference keeps the top k.  Python's
+    sort is stable, so equal scores keep insertion (= ascending doc id) order."""
+    q, p = corpus_topk_inputs()
+    scores = q.astype(np.float64) @ p.astype(np.float64).T
+    n = p.shape[0]
+    bounds = np.linspace(0, n, parts + 1).astype(int)
+    results = []
+    for a, b in zip(bounds[:-1], bounds[1:]):
+        results.append({f"q{r}": {j: float(scores[r, j]) for j in range(a, b)} for r in range(q.shape[0])})
+    merged = ref_utils.merge_retrieval_results_by_score(results, topk=k)
+    ids = np.array([list(merged[f"q{r}"].keys()) for r in range(q.shape[0])], dtype=np.int32)
+    sc = np.array([list(merged[f"q{r}"].values()) for r in range(q.shape[0])], dtype=np.float32)
+    np.savez_compressed(os.path.join(OUT, "corpus_topk.npz"), seed=31, n=n, nq=q.shape[0], d=q.shape[1], lim=16,
+                        k=k, parts=parts, ids=ids, scores=sc)
+
+
 def answer_cases(seed=21, n_docs=60, n_queries=40):
     """Synthetic passages / answer lists for has_answers (uncased, NFD, punctuation,
     accents, multi-token answers, answers absent from every passage, empty answers)."""
@@ -184,6 +213,7 @@ def main():
     gen_loss(ref_bi, ref_losses)
     gen_metrics(ref_metrics)
     gen_merge(ref_utils)
+    gen_corpus_topk(ref_utils)
     gen_rerank()
     gen_answers()
     for f in sorted(os.listdir(OUT)):
