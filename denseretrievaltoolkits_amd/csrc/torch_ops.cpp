@@ -16,8 +16,10 @@
 // (denseretrievaltoolkits_amd/ops.py).
 #include <torch/library.h>
 #include <ATen/ATen.h>
-#include <c10/hip/HIPStream.h>
-#include <c10/hip/HIPGuard.h>
+#include <c10/core/DeviceGuard.h>
+// torch-ROCm exposes GPU tensors under the "cuda" device type; its HIP streams are reached
+// through the MasqueradingAsCUDA view of c10_hip (the HIP stream itself, no CUDA API)
+#include <ATen/hip/impl/HIPStreamMasqueradingAsCUDA.h>
 
 #include "drt.h"
 
@@ -26,11 +28,12 @@ namespace {
 using at::Tensor;
 
 void* stream_of(const Tensor& t) {
-  return (void*)c10::hip::getCurrentHIPStream(t.device().index()).stream();
+  return (void*)at::hip::getCurrentHIPStreamMasqueradingAsCUDA(t.device().index()).stream();
 }
 
+// argument errors surface as Python ValueError (TORCH_CHECK_VALUE), HIP failures as RuntimeError
 void check_rc(int rc, const char* what) {
-  TORCH_CHECK(rc != DRT_EINVAL, what, ": invalid argument (DRT_EINVAL)");
+  TORCH_CHECK_VALUE(rc != DRT_EINVAL, what, ": invalid argument (DRT_EINVAL)");
   TORCH_CHECK(rc == DRT_OK, what, ": HIP error ", rc);
 }
 
@@ -41,8 +44,8 @@ void need_gpu(const Tensor& t, const char* name) {
 
 void need(const Tensor& t, const char* name, at::ScalarType dt, int64_t dim) {
   need_gpu(t, name);
-  TORCH_CHECK(t.scalar_type() == dt, name, ": expected ", dt, ", got ", t.scalar_type());
-  TORCH_CHECK(t.dim() == dim, name, ": expected a ", dim, "-d tensor, got ", t.dim(), "-d");
+  TORCH_CHECK_VALUE(t.scalar_type() == dt, name, ": expected ", dt, ", got ", t.scalar_type());
+  TORCH_CHECK_VALUE(t.dim() == dim, name, ": expected a ", dim, "-d tensor, got ", t.dim(), "-d");
 }
 
 const void* ptr_or_null(const c10::optional<Tensor>& t) { return t.has_value() ? t->data_ptr() : nullptr; }
@@ -56,8 +59,8 @@ void ip_topk_out(const Tensor& q_, const Tensor& p_, int64_t k, int64_t id_offse
                  Tensor& status) {
   need(q_, "q", at::kBFloat16, 2);
   need(p_, "p", at::kBFloat16, 2);
-  TORCH_CHECK(q_.size(1) == p_.size(1), "q and p differ in dimension: ", q_.sizes(), " vs ", p_.sizes());
-  const c10::hip::HIPGuard g(q_.device());
+  TORCH_CHECK_VALUE(q_.size(1) == p_.size(1), "q and p differ in dimension: ", q_.sizes(), " vs ", p_.sizes());
+  const c10::DeviceGuard g(q_.device());
   const Tensor q = q_.contiguous(), p = p_.contiguous();
   const int64_t nq = q.size(0), n = p.size(0), d = q.size(1);
   TORCH_CHECK(scores.is_contiguous() && scores.scalar_type() == at::kFloat && scores.numel() == nq * k,
@@ -67,7 +70,7 @@ void ip_topk_out(const Tensor& q_, const Tensor& p_, int64_t k, int64_t id_offse
   TORCH_CHECK(status.is_contiguous() && status.scalar_type() == at::kInt && status.numel() == nq,
               "status: expected a contiguous int32 [", nq, "] tensor");
   const size_t wsb = drt_ip_topk_workspace(nq, n, (int32_t)d, (int32_t)k);
-  TORCH_CHECK(wsb > 0 || nq == 0, "unsupported ip_topk shape nq=", nq, " n=", n, " d=", d, " k=", k,
+  TORCH_CHECK_VALUE(wsb > 0 || nq == 0, "unsupported ip_topk shape nq=", nq, " n=", n, " d=", d, " k=", k,
               " (d % 64 == 0, d <= 1024, 1 <= k <= 2048)");
   Tensor ws = workspace(q, wsb);
   check_rc(drt_ip_topk_bf16(q.data_ptr(), nq, n ? p.data_ptr() : nullptr, n, (int32_t)d, (int32_t)k, id_offset,
@@ -90,7 +93,7 @@ int64_t ip_topk_resolve(const Tensor& q_, const Tensor& p_, int64_t k, int64_t i
                         Tensor& ids, Tensor& status) {
   need(q_, "q", at::kBFloat16, 2);
   need(p_, "p", at::kBFloat16, 2);
-  const c10::hip::HIPGuard g(q_.device());
+  const c10::DeviceGuard g(q_.device());
   const Tensor q = q_.contiguous(), p = p_.contiguous();
   const int64_t nq = q.size(0), n = p.size(0), d = q.size(1);
   if (nq == 0) return 0;
@@ -109,8 +112,8 @@ int64_t ip_topk_resolve(const Tensor& q_, const Tensor& p_, int64_t k, int64_t i
 std::tuple<Tensor, Tensor> topk_merge(const Tensor& scores_, const Tensor& ids_, int64_t k_out) {
   need(scores_, "scores", at::kFloat, 3);
   need(ids_, "ids", at::kLong, 3);
-  TORCH_CHECK(scores_.sizes() == ids_.sizes(), "topk_merge: scores and ids differ in shape");
-  const c10::hip::HIPGuard g(scores_.device());
+  TORCH_CHECK_VALUE(scores_.sizes() == ids_.sizes(), "topk_merge: scores and ids differ in shape");
+  const c10::DeviceGuard g(scores_.device());
   const Tensor s = scores_.contiguous(), i = ids_.contiguous();
   const int64_t nparts = s.size(0), nq = s.size(1), k_in = s.size(2);
   Tensor os = at::empty({nq, k_out}, s.options());
@@ -123,7 +126,7 @@ std::tuple<Tensor, Tensor> topk_merge(const Tensor& scores_, const Tensor& ids_,
 
 Tensor dist_ws(const Tensor& q, int64_t n_local, int64_t n_global, int64_t k, size_t* wsb) {
   *wsb = drt_ip_topk_dist_workspace(q.size(0), n_local, n_global, (int32_t)q.size(1), (int32_t)k);
-  TORCH_CHECK(*wsb > 0 || q.size(0) == 0, "unsupported dist shape nq=", q.size(0), " n_local=", n_local,
+  TORCH_CHECK_VALUE(*wsb > 0 || q.size(0) == 0, "unsupported dist shape nq=", q.size(0), " n_local=", n_local,
               " n_global=", n_global, " d=", q.size(1), " k=", k);
   return workspace(q, *wsb);
 }
@@ -131,10 +134,10 @@ Tensor dist_ws(const Tensor& q, int64_t n_local, int64_t n_global, int64_t k, si
 Tensor dist_sample(const Tensor& q_, const Tensor& p_, int64_t n_global, int64_t k) {
   need(q_, "q", at::kBFloat16, 2);
   need(p_, "p", at::kBFloat16, 2);
-  const c10::hip::HIPGuard g(q_.device());
+  const c10::DeviceGuard g(q_.device());
   const Tensor q = q_.contiguous(), p = p_.contiguous();
   const int32_t r = drt_ip_topk_sample_rank((int32_t)k);
-  TORCH_CHECK(r > 0, "unsupported k=", k);
+  TORCH_CHECK_VALUE(r > 0, "unsupported k=", k);
   Tensor best = at::empty({q.size(0), r}, q.options().dtype(at::kInt));
   size_t wsb = 0;
   Tensor ws = dist_ws(q, p.size(0), n_global, k, &wsb);
@@ -147,7 +150,7 @@ Tensor dist_sample(const Tensor& q_, const Tensor& p_, int64_t n_global, int64_t
 
 Tensor dist_tau(const Tensor& lists_, int64_t k) {
   need(lists_, "lists", at::kInt, 3);
-  const c10::hip::HIPGuard g(lists_.device());
+  const c10::DeviceGuard g(lists_.device());
   const Tensor lists = lists_.contiguous();
   Tensor tau = at::empty({lists.size(1)}, lists.options().dtype(at::kFloat));
   check_rc(drt_ip_topk_dist_tau((const uint32_t*)lists.data_ptr<int32_t>(), lists.size(1), (int32_t)lists.size(0),
@@ -161,7 +164,7 @@ Tensor dist_filter(const Tensor& q_, const Tensor& p_, int64_t n_global, int64_t
   need(q_, "q", at::kBFloat16, 2);
   need(p_, "p", at::kBFloat16, 2);
   need(tau_, "tau", at::kFloat, 1);
-  const c10::hip::HIPGuard g(q_.device());
+  const c10::DeviceGuard g(q_.device());
   const Tensor q = q_.contiguous(), p = p_.contiguous(), tau = tau_.contiguous();
   Tensor packed = at::empty({q.size(0), k + 1}, q.options().dtype(at::kLong));
   size_t wsb = 0;
@@ -175,8 +178,8 @@ Tensor dist_filter(const Tensor& q_, const Tensor& p_, int64_t n_global, int64_t
 
 std::tuple<Tensor, Tensor, Tensor> merge_packed(const Tensor& parts_, int64_t k, int64_t n_global) {
   need(parts_, "parts", at::kLong, 3);
-  TORCH_CHECK(parts_.size(2) == k + 1, "merge_packed expects [nparts, nq, k + 1]");
-  const c10::hip::HIPGuard g(parts_.device());
+  TORCH_CHECK_VALUE(parts_.size(2) == k + 1, "merge_packed expects [nparts, nq, k + 1]");
+  const c10::DeviceGuard g(parts_.device());
   const Tensor parts = parts_.contiguous();
   const int64_t nq = parts.size(1);
   Tensor s = at::empty({nq, k}, parts.options().dtype(at::kFloat));
@@ -194,8 +197,8 @@ std::tuple<Tensor, Tensor, Tensor> score_ce_fwd(const Tensor& q_, const Tensor& 
                                                 double scale) {
   need(q_, "q", at::kFloat, 2);
   need(p_, "p", at::kFloat, 2);
-  TORCH_CHECK(q_.size(1) == p_.size(1), "q ", q_.sizes(), " and p ", p_.sizes(), " differ in dimension");
-  const c10::hip::HIPGuard g(q_.device());
+  TORCH_CHECK_VALUE(q_.size(1) == p_.size(1), "q ", q_.sizes(), " and p ", p_.sizes(), " differ in dimension");
+  const c10::DeviceGuard g(q_.device());
   const Tensor q = q_.contiguous(), p = p_.contiguous();
   const int64_t m = q.size(0), n = p.size(0), d = q.size(1);
   Tensor S = at::empty({m, n}, q.options());
@@ -216,7 +219,7 @@ std::tuple<Tensor, Tensor> score_ce_bwd(const Tensor& grad_, const Tensor& q_, c
   need(p_, "p", at::kFloat, 2);
   need(S_, "scores", at::kFloat, 2);
   need(lse_, "lse", at::kFloat, 1);
-  const c10::hip::HIPGuard g(q_.device());
+  const c10::DeviceGuard g(q_.device());
   const Tensor q = q_.contiguous(), p = p_.contiguous(), S = S_.contiguous(), lse = lse_.contiguous();
   const Tensor grad = grad_.to(at::kFloat).contiguous().reshape({1});
   const int64_t m = q.size(0), n = p.size(0), d = q.size(1);
@@ -235,7 +238,7 @@ std::tuple<Tensor, Tensor> score_ce_bwd(const Tensor& grad_, const Tensor& q_, c
 Tensor embed_ln(const Tensor& ids_, const c10::optional<Tensor>& type_ids, const Tensor& word, const Tensor& pos,
                 const Tensor& type, const Tensor& gamma, const Tensor& beta, double eps) {
   need(ids_, "input_ids", at::kLong, 2);
-  const c10::hip::HIPGuard g(ids_.device());
+  const c10::DeviceGuard g(ids_.device());
   const Tensor ids = ids_.contiguous();
   const int64_t B = ids.size(0), L = ids.size(1), H = word.size(1);
   TORCH_CHECK(L <= pos.size(0), "sequence length ", L, " exceeds max_position_embeddings ", pos.size(0));
@@ -254,7 +257,7 @@ Tensor linear(const Tensor& x_, const Tensor& w_, const c10::optional<Tensor>& b
   need(x_, "x", at::kBFloat16, 2);
   need(w_, "w", at::kBFloat16, 2);
   TORCH_CHECK(x_.size(1) == w_.size(1), "linear: x ", x_.sizes(), " and w ", w_.sizes(), " differ in K");
-  const c10::hip::HIPGuard g(x_.device());
+  const c10::DeviceGuard g(x_.device());
   const Tensor x = x_.contiguous(), w = w_.contiguous();
   const int64_t M = x.size(0), K = x.size(1), N = w.size(0);
   if (bias.has_value()) TORCH_CHECK(bias->scalar_type() == at::kFloat && bias->numel() == N, "bias: float [N]");
@@ -276,7 +279,7 @@ Tensor linear(const Tensor& x_, const Tensor& w_, const c10::optional<Tensor>& b
 
 Tensor attention(const Tensor& qkv_, const c10::optional<Tensor>& mask, int64_t B, int64_t heads, double scale) {
   need(qkv_, "qkv", at::kBFloat16, 2);
-  const c10::hip::HIPGuard g(qkv_.device());
+  const c10::DeviceGuard g(qkv_.device());
   const Tensor qkv = qkv_.contiguous();
   const int64_t T = qkv.size(0), H3 = qkv.size(1);
   TORCH_CHECK(B > 0 && T % B == 0 && H3 % (3 * heads) == 0, "attention: qkv must be [B*L, 3*heads*64]");
@@ -295,7 +298,7 @@ Tensor attention(const Tensor& qkv_, const c10::optional<Tensor>& mask, int64_t 
 
 Tensor layernorm(const Tensor& x_, const Tensor& gamma, const Tensor& beta, double eps) {
   need_gpu(x_, "x");
-  const c10::hip::HIPGuard g(x_.device());
+  const c10::DeviceGuard g(x_.device());
   const Tensor x = x_.contiguous();
   const int64_t H = x.size(-1), M = x.numel() / H;
   Tensor out = at::empty(x.sizes(), x.options().dtype(at::kBFloat16));
@@ -314,7 +317,7 @@ Tensor layernorm(const Tensor& x_, const Tensor& gamma, const Tensor& beta, doub
 
 Tensor pool(const Tensor& hidden_, const c10::optional<Tensor>& mask, int64_t mode) {
   need(hidden_, "hidden", at::kBFloat16, 3);
-  const c10::hip::HIPGuard g(hidden_.device());
+  const c10::DeviceGuard g(hidden_.device());
   const Tensor hidden = hidden_.contiguous();
   const int64_t B = hidden.size(0), L = hidden.size(1), H = hidden.size(2);
   c10::optional<Tensor> m;
@@ -328,7 +331,7 @@ Tensor pool(const Tensor& hidden_, const c10::optional<Tensor>& mask, int64_t mo
 
 Tensor l2_normalize(const Tensor& x_) {
   need(x_, "x", at::kFloat, 2);
-  const c10::hip::HIPGuard g(x_.device());
+  const c10::DeviceGuard g(x_.device());
   Tensor x = x_.clone(at::MemoryFormat::Contiguous);
   check_rc(drt_l2_normalize_f32(x.data_ptr<float>(), x.size(0), (int32_t)x.size(1), nullptr, stream_of(x)),
            "drt_l2_normalize_f32");

@@ -4,15 +4,18 @@ Same constructor, ``build``/``save``/``load``/``encode``/``forward`` contract
 and checkpoint format (HF ``save_pretrained`` per tower + ``openmatch_config.json``,
 biencoder.py:159-241).  What changes is where the arithmetic runs:
 
-* inference encode (eval mode or no-grad — Trainer.evaluate / _encoding_corpus,
-  DRModelForInference) runs the whole tower on the HIP kernels
-  (model/encoder.HipBertEncoder): bf16 MFMA GEMMs, fused attention, fp32
-  LayerNorm, pooling / head / L2-normalise kernels.  ``hidden`` is returned
-  in bf16, ``reps`` in fp32.
+* encode without autograd (grad mode off or a frozen tower — Trainer.evaluate /
+  _encoding_corpus, DRModelForInference) runs the whole tower on the HIP inference
+  kernels (model/encoder.HipBertEncoder): bf16 MFMA GEMMs, fused attention, fp32
+  LayerNorm statistics, pooling / head / L2-normalise kernels.  ``hidden`` is
+  returned in bf16, ``reps`` in fp32.
+* encode with autograd (training, or eval mode with grad on, where the reference
+  returns differentiable reps) runs BERT towers up to L = 160 on the HIP training
+  tower (model/train_tower.py: forward with saved bf16 activations + backward on
+  HIP kernels, HF train-mode dropout regenerated from a counter hash; dropout is
+  off in eval mode); other towers stay on the HF module under autograd.
 * the training score matrix + cross entropy (forward :107-119) runs on the
   fused fp32 kernels with autograd (torch.ops.drt.score_ce_fwd, score_ce.py).
-* the training encoder forward/backward stays on the HF module under
-  torch-ROCm autograd (encoder backward kernels: SURVEY §8f, next).
 """
 from __future__ import annotations
 
@@ -70,7 +73,7 @@ class DRModel(nn.Module):
         self.loss_fn = nn.CrossEntropyLoss(reduction="mean")
         self.feature = feature
         self.pooling = pooling
-        self.hip_train = True   # HIP training tower for dropout-free BERT towers (set False: HF autograd)
+        self.hip_train = True   # HIP training tower for BERT towers with L <= 160 (set False: HF autograd)
         self.normalize = normalize
         self.model_args = model_args
         self.train_args = train_args
@@ -164,9 +167,9 @@ class DRModel(nn.Module):
             if self.normalize:
                 reps, _ = l2_normalize_(reps)
             return hidden, reps
-        # training forward.  Dropout-free BERT towers run the HIP training tower (forward with
-        # saved bf16 activations + backward on HIP kernels, model/train_tower.py); towers with
-        # dropout keep the HF module under autograd until in-kernel dropout masks exist.
+        # forward with autograd: BERT towers up to MAX_TRAIN_SEQ tokens run the HIP training tower
+        # (saved bf16 activations + backward on HIP kernels, HF dropout semantics in train mode,
+        # model/train_tower.py); anything else keeps the HF module under autograd.
         if (self.hip_train and self.feature == "last_hidden_state" and next(model.parameters()).is_cuda
                 and "token_type_ids" not in items and tower_supported(model) is None
                 and items["input_ids"].shape[1] <= MAX_TRAIN_SEQ):

@@ -85,40 +85,56 @@ def test_drmodel_train_forward_matches_reference(dev):
 
 
 def test_drmodel_train_forward_hip_tower_matches_reference(dev):
-    """DRModel.forward in training mode on the HIP training tower (dropout-free config: bf16
-    activations, model/train_tower.py) against the reference's fp32 scores / loss, and its
-    gradients against the HF-autograd path of the same model."""
+    """DRModel.forward in training mode on the HIP training tower (dropout-free config) against
+    (1) the reference's golden fp32 scores / loss (bf16-activation tolerance), (2) its own
+    reps: scores = q . p^T and loss = CE computed in fp64 from the returned reps (tight), and
+    (3) the HF-autograd path of the same model: per-rep cosine of both towers' reps >= 0.9999
+    and, under the SAME upstream gradient on the reps, every parameter gradient at cos >= 0.999
+    -- a miswired tower (layer order, Q/K/V split, pooling, tied-tower gradient sum) fails here.
+    Reference: DRT/model/biencoder.py:88-125."""
     import torch
     from types import SimpleNamespace
     from denseretrievaltoolkits_amd.model.biencoder import DRModel
     z = np.load(os.path.join(G, "loss.npz"))
     t = lambda k: torch.from_numpy(z[k]).to(dev)
-    grads = {}
+    q_in = {"input_ids": t("fwd_qids"), "attention_mask": t("fwd_qmask")}
+    p_in = {"input_ids": t("fwd_pids"), "attention_mask": t("fwd_pmask")}
+    gen = torch.Generator(device=dev)
+    gen.manual_seed(3)
+    g_q = g_p = None
+    reps, grads = {}, {}
     for hip in (True, False):
         lm = _hf(1, 5, dev).train()
         m = DRModel(lm_q=lm, lm_p=lm, pooling="first", data_args=SimpleNamespace(train_n_passages=2),
                     train_args=SimpleNamespace(negatives_x_device=False)).train()
         m.hip_train = hip
-        out = m(query={"input_ids": t("fwd_qids"), "attention_mask": t("fwd_qmask")},
-                passage={"input_ids": t("fwd_pids"), "attention_mask": t("fwd_pmask")})
+        out = m(query=q_in, passage=p_in)
         if hip:
-            np.testing.assert_allclose(out.scores.detach().cpu().numpy(), z["fwd_scores"], rtol=3e-2,
+            sc = out.scores.detach().double().cpu()
+            qd, pd = out.q_reps.detach().double().cpu(), out.p_reps.detach().double().cpu()
+            np.testing.assert_allclose(sc.numpy(), (qd @ pd.T).numpy(), rtol=1e-5, atol=1e-4)
+            ref_loss = torch.nn.functional.cross_entropy(qd @ pd.T, torch.arange(qd.shape[0]) * 2).item()
+            np.testing.assert_allclose(out.loss.item(), ref_loss, rtol=1e-5)
+            np.testing.assert_allclose(sc.numpy(), z["fwd_scores"], rtol=3e-2,
                                        atol=3e-2 * float(np.abs(z["fwd_scores"]).max()))
             np.testing.assert_allclose(out.loss.item(), float(z["fwd_loss"]), rtol=3e-2)
-        out.loss.backward()
+            g_q = torch.randn(out.q_reps.shape, device=dev, generator=gen)
+            g_p = torch.randn(out.p_reps.shape, device=dev, generator=gen)
+        reps[hip] = (out.q_reps.detach().double(), out.p_reps.detach().double())
+        ((out.q_reps * g_q).sum() + (out.p_reps * g_p).sum()).backward()
         grads[hip] = {n: p.grad.detach().clone() for n, p in lm.named_parameters() if p.grad is not None}
+    for a_, b_ in zip(reps[True], reps[False]):
+        cos = torch.nn.functional.cosine_similarity(a_, b_, dim=1)
+        assert float(cos.min()) >= 0.9999, float(cos.min())
     bad, cosines = [], []
+    assert set(grads[True]) == set(grads[False])
     for n, g_ref in grads[False].items():
         if n.endswith("key.bias") or float(g_ref.norm()) == 0.0:
-            continue
+            continue   # key bias: mathematically zero gradient (softmax shift invariance)
         cos = float(torch.nn.functional.cosine_similarity(grads[True][n].flatten().double(),
                                                           g_ref.flatten().double(), dim=0))
         cosines.append((cos, n))
-        # the two paths differ in their FORWARD (bf16 vs fp32 activations) and the CE softmax over
-        # these large random-init scores amplifies that into the upstream gradient, so this end-to-end
-        # check is loose (0.95); tests/test_train_tower_gpu.py checks the backward itself against HF
-        # autograd under the SAME upstream gradient (cos >= 0.9999)
-        if cos <= 0.95:
+        if cos < 0.999:
             bad.append((n, cos))
     print("lowest gradient cosines:", sorted(cosines)[:4])
     assert not bad, bad
@@ -148,15 +164,20 @@ def test_hip_rerank_matches_reference_scores(dev):
     with torch.no_grad():
         head.linear.weight.copy_(torch.from_numpy(bw.param_value(2, "rr_head.linear.weight", (1, 768))))
     head = head.to(dev)
-    for pooling in ("first", "mean"):
-        m = RRModel(lm=lm, head=head, pooling=pooling).eval()
-        s = m(pos_pairs={"input_ids": torch.from_numpy(z["input_ids"]).to(dev),
-                         "attention_mask": torch.from_numpy(z["attention_mask"]).to(dev)})
-        ref = z[f"scores_{pooling}"]
-        got = s.float().cpu().numpy()
-        err = np.abs(got - ref).max() / (np.abs(ref).max() + 1e-6)
-        print(f"rerank {pooling}: max rel err {err:.4f}")
-        assert err < 0.02
+    # grad off: the inference kernels; grad on in eval mode (the reference returns differentiable
+    # scores there): the HIP training tower forward, dropout off
+    for grad in (False, True):
+        for pooling in ("first", "mean"):
+            m = RRModel(lm=lm, head=head, pooling=pooling).eval()
+            with torch.set_grad_enabled(grad):
+                s = m(pos_pairs={"input_ids": torch.from_numpy(z["input_ids"]).to(dev),
+                                 "attention_mask": torch.from_numpy(z["attention_mask"]).to(dev)})
+            assert s.requires_grad == grad
+            ref = z[f"scores_{pooling}"]
+            got = s.detach().float().cpu().numpy()
+            err = np.abs(got - ref).max() / (np.abs(ref).max() + 1e-6)
+            print(f"rerank {pooling} grad={grad}: max rel err {err:.4f}")
+            assert err < 0.02
 
 
 @pytest.mark.gpu

@@ -64,14 +64,19 @@ def test_opcheck_search_ops(dev, drt):
     _opcheck(drt.ip_topk.default, (q, p, 50, 3))
     s, i, _ = drt.ip_topk(q, p, 50, 0)
     _opcheck(drt.topk_merge.default, (torch.stack([s, s]), torch.stack([i, i + 5000]), 60))
-    best = drt.dist_sample(q, p, 20000, 50)
-    _opcheck(drt.dist_sample.default, (q, p, 20000, 50))
-    lists = torch.stack([best, best])
+    # a valid two-shard protocol run: rows [0, 5000) and [5000, 10000) of a 10000-row corpus
+    p2 = to_dev_bf16(int_bf16(rng, (5000, 128), -3, 3), dev)
+    _opcheck(drt.dist_sample.default, (q, p, 10000, 50))
+    lists = torch.stack([drt.dist_sample(q, p, 10000, 50), drt.dist_sample(q, p2, 10000, 50)])
     _opcheck(drt.dist_tau.default, (lists, 50))
     tau = drt.dist_tau(lists, 50)
-    _opcheck(drt.dist_filter.default, (q, p, 20000, 50, 0, tau))
-    pk = drt.dist_filter(q, p, 20000, 50, 0, tau)
-    _opcheck(drt.merge_packed.default, (torch.stack([pk, pk]), 50, 20000))
+    _opcheck(drt.dist_filter.default, (q, p2, 10000, 50, 5000, tau))
+    parts = torch.stack([drt.dist_filter(q, p, 10000, 50, 0, tau), drt.dist_filter(q, p2, 10000, 50, 5000, tau)])
+    _opcheck(drt.merge_packed.default, (parts, 50, 10000))
+    ms, mi, st = drt.merge_packed(parts, 50, 10000)
+    assert (st == 0).all()
+    es, ei = drt.ip_topk(q, torch.cat([p, p2]), 50, 0)[:2]
+    assert torch.equal(mi, ei) and torch.equal(ms, es)
 
 
 def test_opcheck_score_ce_with_autograd(dev, drt):
