@@ -1333,12 +1333,14 @@ __global__ __launch_bounds__(kKthThreads) void kth_partial_kernel(const uint32_t
 
 // Element i of list l for query q lives at part[l * lstride + q * qstride + i], i < r.
 // Writes tau[q] (r-th best score; -inf if fewer than r real keys) and/or the
-// sorted best r keys best[q * r + i].
+// sorted best r keys best[q * r + i]; zero (optional): zero[q] = 0 (the filter's hit
+// counters, so the fused distributed filter needs no separate memset launch).
 __global__ __launch_bounds__(kKthThreads) void kth_final_kernel(const uint32_t* part, int nlists, int r,
                                                                 int64_t lstride, int64_t qstride, float* tau,
-                                                                uint32_t* best) {
+                                                                uint32_t* best, uint32_t* zero) {
   __shared__ uint32_t buf[kKthChunk];
   const int64_t q = blockIdx.x;
+  if (zero && threadIdx.x == 0) zero[q] = 0;
   const int tot = nlists * r;
   {
     uint32_t tmp[kKthChunk / kKthThreads];
@@ -2112,13 +2114,12 @@ int drt_ip_topk_bf16(const void* Q, int64_t nq, const void* P, int64_t n, int32_
                        (uint32_t*)(w + p.off_part));
     hipLaunchKernelGGL(kth_final_kernel, dim3((unsigned)nq), dim3(kKthThreads), 0, s,
                        (const uint32_t*)(w + p.off_part), (int)p.nchunk, (int)p.r, (int64_t)p.r,
-                       (int64_t)(p.nchunk * p.r), tau, (uint32_t*)nullptr);
+                       (int64_t)(p.nchunk * p.r), tau, (uint32_t*)nullptr, cnt);   // also zeroes the hit counters
     prof_end(pp, s);
     DRT_CHECK_HIP(hipGetLastError());
   }
 
-  // 2. filter pass
-  DRT_CHECK_HIP(hipMemsetAsync(cnt, 0, p.nq_pad * 4, s));
+  // 2. filter pass (counters zeroed by kth_final above: one launch fewer than a memset)
   a.row0 = 0;
   a.nrows = n;
   a.rstride = 1;
@@ -2302,7 +2303,7 @@ int drt_ip_topk_dist_sample(const void* Q, int64_t nq, const void* P, int64_t n_
                      (uint32_t*)(w + p.off_part));
   hipLaunchKernelGGL(kth_final_kernel, dim3((unsigned)nq), dim3(kKthThreads), 0, s,
                      (const uint32_t*)(w + p.off_part), (int)p.nchunk, (int)r, (int64_t)r, (int64_t)(p.nchunk * r),
-                     (float*)nullptr, best);
+                     (float*)nullptr, best, (uint32_t*)nullptr);
   prof_end(pp, s);
   return hip_status(hipGetLastError());
 }
@@ -2313,7 +2314,7 @@ int drt_ip_topk_dist_tau(const uint32_t* lists, int64_t nq, int32_t nlists, int3
   if (nq == 0) return DRT_OK;
   DRT_REQUIRE(lists && tau);
   hipLaunchKernelGGL(kth_final_kernel, dim3((unsigned)nq), dim3(kKthThreads), 0, (hipStream_t)stream, lists,
-                     (int)nlists, (int)r, (int64_t)nq * r, (int64_t)r, tau, (uint32_t*)nullptr);
+                     (int)nlists, (int)r, (int64_t)nq * r, (int64_t)r, tau, (uint32_t*)nullptr, (uint32_t*)nullptr);
   return hip_status(hipGetLastError());
 }
 
@@ -2344,6 +2345,63 @@ int drt_ip_topk_dist_filter(const void* Q, int64_t nq, const void* P, int64_t n_
   }
   DRT_REQUIRE(P != nullptr);
   DRT_CHECK_HIP(hipMemsetAsync(cnt, 0, p.nq_pad * 4, s));
+  ScanArgs a{};
+  a.Q = (const __bf16*)Q;
+  a.nq = nq;
+  a.ldq = d;
+  a.P = (const __bf16*)P;
+  a.ldp = d;
+  a.row0 = 0;
+  a.nrows = n_local;
+  a.rstride = 1;
+  a.tau = tau;
+  a.counts = cnt;
+  a.out = w + p.off_keys;
+  a.cap = p.cap;
+  const int64_t target = std::max<int64_t>(4096, 4 * (int64_t)k);
+  a.exp_hits = p.sample ? std::max<int64_t>(1, target * n_local / std::max<int64_t>(1, n_global)) : n_local;
+  int rc = launch_scan(a, d, SCAN_FILTER, s, PROF_SCAN);
+  if (rc) return rc;
+  sa.counts = cnt;
+  sa.cap = p.cap;
+  sa.n_total = n_local;
+  return launch_select(sa, SEL_KEYS64, SEL_TOPK, s);
+}
+
+// dist_tau + dist_filter in one call: the threshold kernel also zeroes the hit counters,
+// so the step is 3 launches (tau, filter scan, select) instead of 4 plus a host round trip.
+int drt_ip_topk_dist_filter_lists(const void* Q, int64_t nq, const void* P, int64_t n_local, int64_t n_global,
+                                  int32_t d, int32_t k, int64_t id_offset, const uint32_t* lists, int32_t nlists,
+                                  float* tau_out, uint64_t* packed, void* ws, size_t ws_bytes, void* stream) {
+  DRT_REQUIRE(valid_dist_dims(nq, n_local, n_global, d, k));
+  DRT_REQUIRE(id_offset >= 0 && id_offset + n_local <= n_global);
+  const int32_t r = drt_ip_topk_sample_rank(k);
+  DRT_REQUIRE(r > 0 && nlists >= 1 && (int64_t)nlists * r <= kKthChunk);
+  if (nq == 0) return DRT_OK;
+  DRT_REQUIRE(Q && lists && packed && ws);
+  const TopkPlan p = make_dist_plan(nq, n_local, n_global, k);
+  DRT_REQUIRE(ws_bytes >= p.total);
+  hipStream_t s = (hipStream_t)stream;
+  char* w = (char*)ws;
+  uint32_t* cnt = (uint32_t*)(w + p.off_cnt);
+  float* tau = tau_out ? tau_out : (float*)(w + p.off_tau);
+  hipLaunchKernelGGL(kth_final_kernel, dim3((unsigned)nq), dim3(kKthThreads), 0, s, lists, (int)nlists, (int)r,
+                     (int64_t)nq * r, (int64_t)r, tau, (uint32_t*)nullptr, n_local > 0 ? cnt : (uint32_t*)nullptr);
+  DRT_CHECK_HIP(hipGetLastError());
+  SelectArgs sa{};
+  sa.in = w + p.off_keys;
+  sa.in_stride = p.cap;
+  sa.k = k;
+  sa.nq = nq;
+  sa.id_offset = id_offset;
+  sa.out_packed = packed;
+  sa.global_tau = true;
+  if (n_local == 0) {
+    sa.n_in = 0;
+    sa.n_total = 0;
+    return launch_select(sa, SEL_DENSE32, SEL_TOPK, s);
+  }
+  DRT_REQUIRE(P != nullptr);
   ScanArgs a{};
   a.Q = (const __bf16*)Q;
   a.nq = nq;

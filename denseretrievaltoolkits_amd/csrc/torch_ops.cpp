@@ -176,6 +176,25 @@ Tensor dist_filter(const Tensor& q_, const Tensor& p_, int64_t n_global, int64_t
   return packed;
 }
 
+Tensor dist_filter_lists(const Tensor& q_, const Tensor& p_, int64_t n_global, int64_t k, int64_t id_offset,
+                         const Tensor& lists_) {
+  need(q_, "q", at::kBFloat16, 2);
+  need(p_, "p", at::kBFloat16, 2);
+  need(lists_, "lists", at::kInt, 3);
+  const c10::DeviceGuard g(q_.device());
+  const Tensor q = q_.contiguous(), p = p_.contiguous(), lists = lists_.contiguous();
+  TORCH_CHECK_VALUE(lists.size(1) == q.size(0), "lists must be [nlists, nq, r]");
+  Tensor packed = at::empty({q.size(0), k + 1}, q.options().dtype(at::kLong));
+  size_t wsb = 0;
+  Tensor ws = dist_ws(q, p.size(0), n_global, k, &wsb);
+  check_rc(drt_ip_topk_dist_filter_lists(q.data_ptr(), q.size(0), p.size(0) ? p.data_ptr() : nullptr, p.size(0),
+                                         n_global, (int32_t)q.size(1), (int32_t)k, id_offset,
+                                         (const uint32_t*)lists.data_ptr<int32_t>(), (int32_t)lists.size(0), nullptr,
+                                         (uint64_t*)packed.data_ptr<int64_t>(), ws.data_ptr(), wsb, stream_of(q)),
+           "drt_ip_topk_dist_filter_lists");
+  return packed;
+}
+
 std::tuple<Tensor, Tensor, Tensor> merge_packed(const Tensor& parts_, int64_t k, int64_t n_global) {
   need(parts_, "parts", at::kLong, 3);
   TORCH_CHECK_VALUE(parts_.size(2) == k + 1, "merge_packed expects [nparts, nq, k + 1]");
@@ -350,6 +369,7 @@ TORCH_LIBRARY(drt, m) {
   m.def("dist_sample(Tensor q, Tensor p, int n_global, int k) -> Tensor");
   m.def("dist_tau(Tensor lists, int k) -> Tensor");
   m.def("dist_filter(Tensor q, Tensor p, int n_global, int k, int id_offset, Tensor tau) -> Tensor");
+  m.def("dist_filter_lists(Tensor q, Tensor p, int n_global, int k, int id_offset, Tensor lists) -> Tensor");
   m.def("merge_packed(Tensor parts, int k, int n_global) -> (Tensor, Tensor, Tensor)");
   m.def("score_ce_fwd(Tensor q, Tensor p, int target_stride, float scale) -> (Tensor, Tensor, Tensor)");
   m.def("score_ce_bwd(Tensor grad, Tensor q, Tensor p, Tensor scores, Tensor lse, int target_stride, "
@@ -371,6 +391,7 @@ TORCH_LIBRARY_IMPL(drt, CUDA, m) {   // the GPU dispatch key of torch-ROCm
   m.impl("dist_sample", &dist_sample);
   m.impl("dist_tau", &dist_tau);
   m.impl("dist_filter", &dist_filter);
+  m.impl("dist_filter_lists", &dist_filter_lists);
   m.impl("merge_packed", &merge_packed);
   m.impl("score_ce_fwd", &score_ce_fwd);
   m.impl("score_ce_bwd", &score_ce_bwd);

@@ -106,6 +106,14 @@ def dist_filter(q: torch.Tensor, p: torch.Tensor, n_global: int, k: int, id_offs
     return ops.load().dist_filter(q, p, n_global, k, id_offset, tau)
 
 
+def dist_filter_lists(q: torch.Tensor, p: torch.Tensor, n_global: int, k: int, id_offset: int,
+                      lists: torch.Tensor) -> torch.Tensor:
+    """dist_tau + dist_filter fused (3 launches): this shard's packed top-k against the tau of the
+    gathered sample lists [nlists, nq, r]."""
+    _require_device(q, p, lists)
+    return ops.load().dist_filter_lists(q, p, n_global, k, id_offset, lists)
+
+
 def merge_packed(parts: torch.Tensor, k: int, n_global: int):
     """[nparts, nq, k + 1] packed lists -> (scores [nq,k], ids [nq,k], status [nq] int32; 0 = exact)."""
     _require_device(parts)

@@ -9,7 +9,7 @@ formula of the fused score + cross-entropy op.
     torch.ops.drt.ip_topk(q, p, k, id_offset)          -> (scores, ids, status)   index.py:31-33
     torch.ops.drt.ip_topk_resolve(q, p, k, off, s, i, st) -> n_resolved  (in place, synchronous)
     torch.ops.drt.topk_merge(scores, ids, k_out)        -> (scores, ids)           utils.py:215-229
-    torch.ops.drt.dist_sample / dist_tau / dist_filter / merge_packed   (sharded protocol, §8e)
+    torch.ops.drt.dist_sample / dist_tau / dist_filter / dist_filter_lists / merge_packed  (sharded, §8e)
     torch.ops.drt.score_ce_fwd(q, p, stride, scale)     -> (loss, scores, lse)     biencoder.py:107-119
     torch.ops.drt.score_ce_bwd(g, q, p, scores, lse, stride, scale) -> (dq, dp)
     torch.ops.drt.embed_ln / linear / attention / layernorm / pool / l2_normalize  (BertModel pieces)
@@ -71,6 +71,10 @@ def _register_python_parts():
 
     @lib.register_fake("drt::dist_filter")
     def _(q, p, n_global, k, id_offset, tau):
+        return q.new_empty((q.shape[0], k + 1), dtype=torch.int64)
+
+    @lib.register_fake("drt::dist_filter_lists")
+    def _(q, p, n_global, k, id_offset, lists):
         return q.new_empty((q.shape[0], k + 1), dtype=torch.int64)
 
     @lib.register_fake("drt::merge_packed")

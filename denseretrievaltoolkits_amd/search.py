@@ -170,6 +170,9 @@ class FlatIPIndex:
     def dist_filter(self, q, n_global: int, k: int, id_offset: int, tau: torch.Tensor) -> torch.Tensor:
         return kernels.dist_filter(self._queries(q), self.rows, n_global, k, id_offset, tau)
 
+    def dist_filter_lists(self, q, n_global: int, k: int, id_offset: int, lists: torch.Tensor) -> torch.Tensor:
+        return kernels.dist_filter_lists(self._queries(q), self.rows, n_global, k, id_offset, lists)
+
     # persistence (replaces faiss.write_index / read_index, trainer.py:245,257): a
     # memory-mapped bf16 shard file streamed chunk by chunk (shards.py)
     def save(self, path: str) -> None:
@@ -261,8 +264,12 @@ class ShardedFlatIP:
             return ("done", self.local.search_device(q, k, id_offset=self.offset))
         if self.protocol == "global_tau" and self.ntotal < 0xFFFFFFFF:
             best = self.local.dist_sample(q, self.ntotal, k)                 # [nq, r] u32 keys
-            tau = self.local.dist_tau(self._all_gather(best), k)             # [nq]
-            packed = self.local.dist_filter(q, self.ntotal, k, self.offset, tau)   # [nq, k + 1] u64
+            lists = self._all_gather(best)                                   # [world, nq, r]
+            if hasattr(self.local, "dist_filter_lists"):                     # tau + filter fused
+                packed = self.local.dist_filter_lists(q, self.ntotal, k, self.offset, lists)
+            else:
+                tau = self.local.dist_tau(lists, k)                          # [nq]
+                packed = self.local.dist_filter(q, self.ntotal, k, self.offset, tau)   # [nq, k + 1] u64
             s, i, status = self.merge_packed(self._all_gather(packed), k, self.ntotal)
             # every rank merged the same gathered lists: the same status, the same branch
             return ("gtau", q, k, s, i) + _stage_status(status)

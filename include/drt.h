@@ -116,6 +116,13 @@ int drt_ip_topk_dist_filter(const void* Q, int64_t nq, const void* P, int64_t n_
                             int64_t n_global, int32_t d, int32_t k, int64_t id_offset,
                             const float* tau, uint64_t* packed, void* ws, size_t ws_bytes,
                             void* stream);
+/* 3+4 fused: tau from the gathered lists [nlists][nq][r] (written to tau_out when it is not
+ * NULL) and this shard's packed top-k, with the hit counters zeroed by the threshold kernel
+ * (3 launches).  Same results as drt_ip_topk_dist_tau followed by drt_ip_topk_dist_filter. */
+int drt_ip_topk_dist_filter_lists(const void* Q, int64_t nq, const void* P, int64_t n_local,
+                                  int64_t n_global, int32_t d, int32_t k, int64_t id_offset,
+                                  const uint32_t* lists, int32_t nlists, float* tau_out,
+                                  uint64_t* packed, void* ws, size_t ws_bytes, void* stream);
 int drt_topk_merge_packed(const uint64_t* parts, int64_t nq, int32_t nparts, int32_t k,
                           int64_t n_global, float* out_scores, int64_t* out_ids, int32_t* status,
                           void* stream);

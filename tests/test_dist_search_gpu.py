@@ -29,6 +29,9 @@ def _gpu_protocol(dev, q, p, k, world, check_intermediates=True):
     lists = torch.stack([kernels.dist_sample(qt, sh, n, k) for sh in shards])
     tau = kernels.dist_tau(lists, k)
     parts = torch.stack([kernels.dist_filter(qt, sh, n, k, lo, tau) for sh, (lo, _) in zip(shards, bounds)])
+    # the fused tau + filter entry (the path ShardedFlatIP takes) gives the same packed lists
+    fused = torch.stack([kernels.dist_filter_lists(qt, sh, n, k, lo, lists) for sh, (lo, _) in zip(shards, bounds)])
+    assert torch.equal(fused, parts)
     s, i, st = kernels.merge_packed(parts, k, n)
     torch.cuda.synchronize()
     if check_intermediates:

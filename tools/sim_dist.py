@@ -27,6 +27,7 @@ def main():
     ap.add_argument("--k", type=int, default=1000)
     ap.add_argument("--steps", type=int, default=30)
     ap.add_argument("--check", action="store_true", help="verify global_tau == per_shard results")
+    ap.add_argument("--graph", action="store_true", help="also time the step replayed from a hipGraph")
     a = ap.parse_args()
     import torch
     import bench
@@ -93,15 +94,22 @@ def main():
         res["qps_if_comm_free"] = round(qb / (el / a.steps), 1)
         out[label] = res
 
+    # the all-gathers write every rank's slice into one [world, ...] buffer; here rank R's
+    # slice is written in place (the other slices hold the precomputed data of the other ranks)
     def gt(j):
         best = kernels.dist_sample(queries[j], own, N, k)
-        l = lists[j].clone()
-        l[R] = best
-        tau = kernels.dist_tau(l, k)
+        lists[j][R].copy_(best)
+        pk = kernels.dist_filter_lists(queries[j], own, N, k, lo, lists[j])
+        parts[j][R].copy_(pk)
+        kernels.merge_packed(parts[j], k, N)
+
+    def gt_unfused(j):
+        best = kernels.dist_sample(queries[j], own, N, k)
+        lists[j][R].copy_(best)
+        tau = kernels.dist_tau(lists[j], k)
         pk = kernels.dist_filter(queries[j], own, N, k, lo, tau)
-        p = parts[j].clone()
-        p[R] = pk
-        kernels.merge_packed(p, k, N)
+        parts[j][R].copy_(pk)
+        kernels.merge_packed(parts[j], k, N)
 
     def psh(j):
         s, i, _ = kernels.ip_topk(queries[j], own, k, id_offset=lo, resolve=False)
@@ -110,9 +118,24 @@ def main():
         kernels.topk_merge(S, I, k)
 
     timed(gt, "global_tau")
-    timed(gt, "global_tau_2streams", 2)
-    timed(gt, "global_tau_3streams", 3)
+    timed(gt_unfused, "global_tau_unfused")
     timed(psh, "per_shard")
+    if a.graph:
+        # the rank's compute of one step captured once and replayed: the launch-gap floor
+        g = torch.cuda.CUDAGraph()
+        side = torch.cuda.Stream(device=dev)
+        side.wait_stream(torch.cuda.current_stream(dev))
+        with torch.cuda.stream(side):
+            gt(0)
+        torch.cuda.current_stream(dev).wait_stream(side)
+        with torch.cuda.graph(g):
+            gt(0)
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(a.steps):
+            g.replay()
+        torch.cuda.synchronize()
+        out["global_tau_graph"] = {"ms_per_step": round((time.perf_counter() - t0) / a.steps * 1e3, 4)}
     print(json.dumps(out), flush=True)
 
 
