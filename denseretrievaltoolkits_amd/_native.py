@@ -60,6 +60,8 @@ _SIGNATURES = [
     ("drt_colsum_workspace", c_sz, [c_i64, c_i64]),
     ("drt_colsum_bf16", c_i32, [c_vp, c_i64, c_i64, c_vp, c_vp, c_sz, c_vp]),
     ("drt_gelu_bwd_bf16", c_i32, [c_vp, c_vp, c_i64, c_vp, c_vp]),
+    ("drt_linear_wgrad_workspace", c_sz, [c_i64, c_i64, c_i64]),
+    ("drt_linear_wgrad_bf16", c_i32, [c_vp, c_vp, c_vp, c_i64, c_i64, c_i64, c_vp, c_sz, c_vp]),
     ("drt_transpose_bf16", c_i32, [c_vp, c_i64, c_i64, c_vp, c_vp]),
     ("drt_transpose_bf16_ld", c_i32, [c_vp, c_i64, c_i64, c_vp, c_i64, c_vp]),
     ("drt_embed_ln_pre", c_i32, [c_vp, c_vp, c_i64, c_i64, c_vp, c_vp, c_vp, c_vp, c_vp, c_f32, c_i32, c_vp, c_vp,

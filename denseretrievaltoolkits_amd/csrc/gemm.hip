@@ -573,6 +573,45 @@ __device__ __forceinline__ void stage_panel32(const __bf16* base, int64_t ld, in
   }
 }
 
+// TN operands (weight gradients dW = dY^T X: both stored [t][features], t = the reduction
+// index): a 32-t slab of a 256-column panel is 32 rows of 512 B (whole cache lines) in a
+// [t][256 cols] image with the 16-B chunk XOR-swizzled by tn_swz(row) = 2 (row & 3) ^ 8 ((row >> 3) & 1);
+// the MFMA fragments are read column-wise with ds_read_b64_tr_b16 (two per fragment), which
+// this swizzle keeps conflict-free for every 32-lane half.
+__device__ __forceinline__ int tn_swz(int row) { return (2 * (row & 3)) ^ (8 * ((row >> 3) & 1)); }
+
+// 32 t-rows x 256 columns into the swizzled [t][512 B] image: 16 wave-instructions of 2 rows, 2 per wave.
+// Columns past `cols` are clamped to the last whole chunk (their outputs are masked).
+__device__ __forceinline__ void stage_panel32_tn(const __bf16* base, int64_t ld, int64_t col0, int64_t cols,
+                                                 int64_t t0, uint32_t lds, int wave, int lane) {
+  const int cp = lane & 31;   // chunk position in the LDS row
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    const int J = j * 8 + wave;
+    const int row = 2 * J + (lane >> 5);
+    int64_t col = col0 + (int64_t)((cp ^ tn_swz(row)) * 8);
+    col = col + 8 <= cols ? col : cols - 8;
+    g_glds16(base + (t0 + row) * ld + col, __builtin_amdgcn_readfirstlane(lds + J * 1024));
+  }
+}
+
+typedef short tn_v4i16 __attribute__((ext_vector_type(4)));
+
+// 16x16x32 operand fragment of columns [cb, cb + 16) (cb % 16 == 0, cb < 256) from a TN image:
+// lane l gets column cb + (l & 15), t rows 8 (l >> 4) .. +7.  rowoff = byte offset of row
+// 8 (l >> 4) + ((l & 15) >> 2) (the second read is 4 rows below), s = tn_swz of that row,
+// lo = 16 ((l & 3) >> 1) + 8 (l & 1).
+__device__ __forceinline__ bf16x8 tn_frag(const char* img, int cb, int rowoff, int s, int lo) {
+  const int off = rowoff + ((((cb >> 3)) ^ s) << 4) + lo;
+  typedef __attribute__((address_space(3))) tn_v4i16 lds_v4;
+  const tn_v4i16 a = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4*)(uintptr_t)g_lds_addr(img + off));
+  const tn_v4i16 b = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4*)(uintptr_t)g_lds_addr(img + off + 4 * 512));
+  bf16x8 r;
+  __builtin_memcpy(&r, &a, 8);
+  __builtin_memcpy((char*)&r + 8, &b, 8);
+  return r;
+}
+
 // Tile order inside the contiguous range of tiles an XCD owns (wg = rank in the
 // XCD-remapped grid): 0 row-major (consecutive tiles share the X panel),
 // 1 grouped by 8 m-panels (a round of 32 concurrent tiles = 8 m x 4 n panels),
@@ -814,7 +853,7 @@ __device__ __forceinline__ void pp_epilogue_lds(const GemmArgs& a, f32x4 (&acc)[
 // wave, before the barrier after which group 0 reads it.  WAR: slot (s+3)&3
 // held slab s-1, whose reads both groups drained before the barrier that
 // precedes group 0's memory segment of slab s.
-template <bool OUT_BF16, int EPI, int ABL = 0, int RING = 4>
+template <bool OUT_BF16, int EPI, int ABL = 0, int RING = 4, bool TN = false>
 __global__ __launch_bounds__(kLThreads, 1) void gemm_nt_pp1_kernel(GemmArgs a) {
   constexpr int D = RING - 1;   // slabs in flight
   __shared__ __attribute__((aligned(16))) char smem[RING * kPSlab];
@@ -855,14 +894,23 @@ __global__ __launch_bounds__(kLThreads, 1) void gemm_nt_pp1_kernel(GemmArgs a) {
   const int foff = fr * 64 + ((fc ^ ((fr >> 1) & 2)) << 4);
   const int xoff = grp * 128 * 64 + foff;
   const int woff = kPPanel + wn * 64 * 64 + foff;
+  // TN fragment addressing (tn_frag): row 8 fc + (fr >> 2), chunk half (fr & 3) >> 1, 8-B half fr & 1
+  const int tn_row = 8 * fc + (fr >> 2);
+  const int tn_rowoff = tn_row * 512, tn_s = tn_swz(tn_row), tn_lo = 16 * ((fr & 3) >> 1) + 8 * (fr & 1);
+  auto stage = [&](int64_t t0, uint32_t dst) {
+    if (TN) {
+      stage_panel32_tn(a.A, a.lda, dm0, a.m, t0, dst, wave, lane);
+      stage_panel32_tn(a.B, a.ldb, dn0, a.n, t0, dst + kPPanel, wave, lane);
+    } else {
+      stage_panel32(a.A, a.lda, dm0, a.m, t0, dst, wave, lane);
+      stage_panel32(a.B, a.ldb, dn0, a.n, t0, dst + kPPanel, wave, lane);
+    }
+  };
 
   // prologue: slabs 0..D-1 in flight, slab 0 landed
 #pragma unroll
   for (int p = 0; p < D; ++p) {
-    if (p < ns) {
-      stage_panel32(a.A, a.lda, dm0, a.m, kb + p * 32, lds0 + p * kPSlab, wave, lane);
-      stage_panel32(a.B, a.ldb, dn0, a.n, kb + p * 32, lds0 + p * kPSlab + kPPanel, wave, lane);
-    }
+    if (p < ns) stage(kb + p * 32, lds0 + p * kPSlab);
   }
   vmcnt_slabs_after(ns - 1 < D - 1 ? ns - 1 : D - 1);
   __builtin_amdgcn_s_barrier();
@@ -884,10 +932,17 @@ __global__ __launch_bounds__(kLThreads, 1) void gemm_nt_pp1_kernel(GemmArgs a) {
     const char* slab = smem + slot * kPSlab;
     // ---- memory segment
     bf16x8 wf[4], xf[8];
+    if (TN) {
 #pragma unroll
-    for (int j = 0; j < 4; ++j) wf[j] = (ABL & 8) ? bf16x8{} : *(const bf16x8*)(slab + woff + j * 1024);
+      for (int j = 0; j < 4; ++j) wf[j] = tn_frag(slab + kPPanel, wn * 64 + j * 16, tn_rowoff, tn_s, tn_lo);
 #pragma unroll
-    for (int i = 0; i < 8; ++i) xf[i] = (ABL & 8) ? bf16x8{} : *(const bf16x8*)(slab + xoff + i * 1024);
+      for (int i = 0; i < 8; ++i) xf[i] = tn_frag(slab, grp * 128 + i * 16, tn_rowoff, tn_s, tn_lo);
+    } else {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) wf[j] = (ABL & 8) ? bf16x8{} : *(const bf16x8*)(slab + woff + j * 1024);
+#pragma unroll
+      for (int i = 0; i < 8; ++i) xf[i] = (ABL & 8) ? bf16x8{} : *(const bf16x8*)(slab + xoff + i * 1024);
+    }
     if (ABL & 8) {
 #pragma unroll
       for (int i = 0; i < 8; ++i) asm volatile("" : "+v"(xf[i]));
@@ -897,8 +952,7 @@ __global__ __launch_bounds__(kLThreads, 1) void gemm_nt_pp1_kernel(GemmArgs a) {
     const int left = (ABL & 1) ? 0 : ns - 1 - s;   // slabs after s
     if (left >= D) {
       const uint32_t nslab = lds0 + fill * kPSlab;
-      stage_panel32(a.A, a.lda, dm0, a.m, kb + (int64_t)(s + D) * 32, nslab, wave, lane);
-      stage_panel32(a.B, a.ldb, dn0, a.n, kb + (int64_t)(s + D) * 32, nslab + kPPanel, wave, lane);
+      stage(kb + (int64_t)(s + D) * 32, nslab);
       if (PRE && left == D && pre_on) {
         load_resid_half(a, m0, n0, grp, wn, 0, lane, rv0);
         vmcnt_slabs_after_plus(D - 1, RP);
@@ -1128,6 +1182,58 @@ extern "C" int drt_linear_bf16_ws(const void* X, const void* W, const float* bia
   if (ws && ws_bytes >= drt_linear_workspace(M, N, K) && drt_linear_workspace(M, N, K) > 0) a.ws = (float*)ws;
   const int epi = (bias ? EPI_BIAS : 0) | (gelu ? EPI_GELU : 0) | (residual ? EPI_RESID : 0);
   return launch_gemm(a, !f32, epi, (hipStream_t)stream);
+}
+
+// Weight gradient of nn.Linear without transposed operand copies: dW[N][K] fp32 = dY[T][N]^T . X[T][K]
+// (both operands stored token-major, as the backward has them).  The 256^2 ping-pong kernel in
+// TN mode (whole-line slabs, ds_read_b64_tr_b16 fragments), K = T split over ~1 block per CU with
+// fp32 partials in ws reduced in a fixed order (deterministic), like the transposed path.
+extern "C" size_t drt_linear_wgrad_workspace(int64_t T, int64_t N, int64_t K) {
+  if (T <= 0 || N <= 0 || K <= 0 || T % 32 || N % 8 || K % 8) return 0;
+  int64_t kc = 0;
+  const int ls = large_splits(N, K, T, g_large_min_tiles, &kc);
+  return ls > 1 ? (size_t)ls * (size_t)N * (size_t)K * sizeof(float) : 0;
+}
+
+extern "C" int drt_linear_wgrad_bf16(const void* dY, const void* X, float* dW, int64_t T, int64_t N, int64_t K,
+                                     void* ws, size_t ws_bytes, void* stream) {
+  DRT_REQUIRE(T > 0 && N >= 8 && K >= 8 && T % 32 == 0 && N % 8 == 0 && K % 8 == 0);
+  DRT_REQUIRE(dY && X && dW);
+  hipStream_t s = (hipStream_t)stream;
+  GemmArgs a{};
+  a.A = (const __bf16*)dY;
+  a.B = (const __bf16*)X;
+  a.C = dW;
+  a.m = N;
+  a.n = K;
+  a.k = T;
+  a.lda = N;
+  a.ldb = K;
+  a.ldc = K;
+  a.alpha = 1.0f;
+  a.order = g_gemm_order >= 0 ? g_gemm_order : (T <= 1024 ? 1 : 0);
+  const int64_t tiles_l = ((N + kL - 1) / kL) * ((K + kL - 1) / kL);
+  int64_t kc = 0;
+  const int splits = large_splits(N, K, T, g_large_min_tiles, &kc);
+  const ProfPair pp = prof_begin(PROF_GEMM, s);
+  if (splits > 1) {
+    DRT_REQUIRE(ws && ws_bytes >= (size_t)splits * (size_t)N * (size_t)K * sizeof(float));
+    GemmArgs b = a;
+    b.kchunk = kc;
+    b.C = ws;
+    hipLaunchKernelGGL((gemm_nt_pp1_kernel<false, EPI_NONE, 0, 5, true>), dim3((unsigned)tiles_l, (unsigned)splits),
+                       dim3(kLThreads), 0, s, b);
+    GemmArgs e = a;
+    e.ws = (float*)ws;
+    const int64_t units = (K % 4 == 0) ? N * K / 4 : N * K;
+    const int64_t blocks = (units + 255) / 256 < 4096 ? (units + 255) / 256 : 4096;
+    hipLaunchKernelGGL((splitk_epi_kernel<false, EPI_NONE>), dim3((unsigned)blocks), dim3(256), 0, s, e, splits);
+  } else {
+    hipLaunchKernelGGL((gemm_nt_pp1_kernel<false, EPI_NONE, 0, 5, true>), dim3((unsigned)tiles_l), dim3(kLThreads), 0,
+                       s, a);
+  }
+  prof_end(pp, s);
+  return hip_status(hipGetLastError());
 }
 
 // Testing / benchmarking switch: 0 = automatic, 1 = 128^2 kernel for every size,

@@ -1,17 +1,16 @@
-"""Backward building blocks of the HIP encoder tower (in progress).
+"""Backward building blocks of the HIP encoder tower, used by the
+training tower (model/train_tower.py).
 
 The training step of run_random_sampling.py (DRT/trainer/trainer.py:113-133) differentiates
 HF ``BertModel`` under autograd; these functions restate the gradients of its ops on the HIP
 kernels for the bf16 activations the HIP forward stores:
 
 * ``linear_backward``   nn.Linear: dX = dY W (the NT GEMM against a transposed weight copy),
-                        dW = dY^T X (both operands transposed to k-contiguous rows, then the
-                        split-K NT GEMM with fp32 output), db = column sums of dY;
-* ``layernorm_backward`` / ``gelu_backward`` / ``attention_forward_lse``: thin wrappers of the
-                        C-ABI entries (include/drt.h).
-
-Assembling the tower backward (with attention backward and dropout masks) is the next step;
-until then training keeps the HF module under torch-ROCm autograd (biencoder.py).
+                        dW = dY^T X (``wgrad``: the TN GEMM reading both token-major operands
+                        directly, deterministic split over tokens, fp32 output), db = column
+                        sums of dY;
+* ``layernorm_backward`` / ``gelu_backward``: thin wrappers of the C-ABI entries
+                        (include/drt.h).
 """
 from __future__ import annotations
 
@@ -73,16 +72,38 @@ def linear_backward(dy: torch.Tensor, x: torch.Tensor, w_t: torch.Tensor, want_d
         ws = _ws(nb, dev)
         _native.check(lib.drt_linear_bf16_ws(dy.data_ptr(), w_t.data_ptr(), None, _ptr(resid), dx.data_ptr(), T, K, N,
                                              0, _ptr(ws), nb, s), "dgrad")
+    dW = wgrad(dy, x)
+    return dx, dW, colsum(dy)
+
+
+WGRAD_TN = True   # A/B switch: False = transposed operand copies + NT GEMM (the round-1 path)
+
+
+def wgrad(dy: torch.Tensor, x: torch.Tensor) -> torch.Tensor:
+    """dW [N, K] fp32 = dy[T, N]^T x[T, K].  Token counts that are multiples of 32 go straight to
+    the TN GEMM (drt_linear_wgrad_bf16, no transposed copies); others transpose both operands
+    (zero-padded to 64 tokens) and run the NT GEMM."""
+    lib = _native.load()
+    dev = dy.device
+    s = _native.stream_ptr(dev)
+    T, N = dy.shape
+    K = x.shape[1]
+    dW = torch.empty((N, K), dtype=torch.float32, device=dev)
+    if WGRAD_TN and T % 32 == 0:
+        nb = int(lib.drt_linear_wgrad_workspace(T, N, K))
+        ws = _ws(nb, dev)
+        _native.check(lib.drt_linear_wgrad_bf16(dy.data_ptr(), x.data_ptr(), dW.data_ptr(), T, N, K, _ptr(ws), nb, s),
+                      "drt_linear_wgrad_bf16")
+        return dW
     pad = (-T) % 64
     dyT = transpose_bf16(dy, pad)        # [N, T64]
     xT = transpose_bf16(x, pad)          # [K, T64]
     T64 = T + pad
-    dW = torch.empty((N, K), dtype=torch.float32, device=dev)
     nb = int(lib.drt_linear_workspace(N, K, T64))
     ws = _ws(nb, dev)
     _native.check(lib.drt_linear_bf16_ws(dyT.data_ptr(), xT.data_ptr(), None, None, dW.data_ptr(), N, K, T64, 2,
                                          _ptr(ws), nb, s), "wgrad")
-    return dx, dW, colsum(dy)
+    return dW
 
 
 def layernorm_backward(dy: torch.Tensor, x: torch.Tensor, gamma: torch.Tensor, eps: float,

@@ -208,6 +208,12 @@ int drt_gelu_bwd_bf16(const void* dy, const void* pre, int64_t n, void* dx, void
 int drt_transpose_bf16(const void* x, int64_t R, int64_t C, void* y, void* stream);
 /* drt_transpose_bf16_ld: the same into y with row stride ldy >= R (padded GEMM operands). */
 int drt_transpose_bf16_ld(const void* x, int64_t R, int64_t C, void* y, int64_t ldy, void* stream);
+/* drt_linear_wgrad_bf16: dW [N,K] fp32 = dY[T,N]^T . X[T,K] (nn.Linear weight gradient) straight
+ *   from the token-major operands (no transposed copies): T % 32 == 0, N % 8 == 0, K % 8 == 0;
+ *   ws of drt_linear_wgrad_workspace(T, N, K) bytes (deterministic split over T; 0 = none).  */
+size_t drt_linear_wgrad_workspace(int64_t T, int64_t N, int64_t K);
+int drt_linear_wgrad_bf16(const void* dY, const void* X, float* dW, int64_t T, int64_t N, int64_t K, void* ws,
+                          size_t ws_bytes, void* stream);
 /* drt_attention_bwd_bf16: dqkv [B*L, 3H] (dQ | dK | dV in qkv's packed layout) of the
  * attention forward, from qkv, its ctx = O, dctx = dO, the forward's lse and the key mask;
  * L <= 160, head_dim 64 (BertSelfAttention under autograd, modeling_bert.py:164-204).   */

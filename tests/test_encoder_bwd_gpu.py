@@ -204,3 +204,30 @@ def test_long_k_split_gemm_vs_torch(dev, M, N, K):
                                          ws.data_ptr(), nb, _native.stream_ptr(dev)), "split gemm")
     ref = a.float() @ b.float().T
     torch.testing.assert_close(out, ref, atol=2e-3 * (K / 4096) ** 0.5, rtol=1e-3)
+
+
+@pytest.mark.parametrize("T,N,K", [(16384, 768, 768), (131072, 768, 3072), (19968, 2304, 768), (4096, 3072, 768),
+                                   (64, 264, 200)])
+def test_wgrad_tn_vs_torch_and_transposed_path(dev, T, N, K):
+    """dW = dY^T X straight from the token-major operands (drt_linear_wgrad_bf16: the 256^2 GEMM
+    in TN mode, ds_read_b64_tr_b16 fragments) vs torch fp32, and bit-identical to the transposed
+    path (transposes + NT GEMM) wherever both split the tokens the same way (T % 64 == 0, split)."""
+    import torch
+    from denseretrievaltoolkits_amd import _native
+    from denseretrievaltoolkits_amd.model import encoder_bwd as eb
+    g = torch.Generator(device=dev).manual_seed(T + N + K)
+    x = torch.randn(T, K, generator=g, device=dev).to(torch.bfloat16)
+    dy = torch.randn(T, N, generator=g, device=dev).to(torch.bfloat16)
+    eb.WGRAD_TN = True
+    try:
+        dw_tn = eb.wgrad(dy, x)
+        eb.WGRAD_TN = False
+        dw_nt = eb.wgrad(dy, x)
+    finally:
+        eb.WGRAD_TN = True
+    ref = dy.float().T @ x.float()
+    tol = 2e-3 * T ** 0.5
+    torch.testing.assert_close(dw_tn, ref, atol=tol, rtol=1e-3)
+    split = _native.load().drt_linear_wgrad_workspace(T, N, K) > 0
+    if split and T % 64 == 0:
+        assert torch.equal(dw_tn, dw_nt)
