@@ -249,12 +249,16 @@ def run_train_step(device, bq=512, n=2, q_len=32, p_len=128, steps=3, warmup=1):
     fl = 3 * (bq * flops_per_seq(q_len) + bq * n * flops_per_seq(p_len))
     res = {"metric": "in-batch-negative training step (fwd + bwd of both towers + score/CE), ms",
            "batch": bq, "train_n_passages": n, "q_len": q_len, "p_len": p_len, "flop_per_step": fl}
-    for name, hip in (("hip", True), ("torch_fp32", False)):
+    # torch_bf16_autocast: the same HF module under torch.autocast(bf16) (hipBLASLt GEMMs + sdpa), the
+    # like-for-like arithmetic baseline for the bf16 HIP tower (the reference itself is fp32)
+    for name, hip, amp in (("hip", True, False), ("torch_fp32", False, False), ("torch_bf16_autocast", False, True)):
         m.hip_train = hip
 
         def step():
             lm.zero_grad(set_to_none=True)
-            m(query=qry, passage=psg).loss.backward()
+            with torch.autocast("cuda", dtype=torch.bfloat16, enabled=amp):
+                loss = m(query=qry, passage=psg).loss
+            loss.backward()
 
         for _ in range(warmup):
             step()
@@ -267,4 +271,6 @@ def run_train_step(device, bq=512, n=2, q_len=32, p_len=128, steps=3, warmup=1):
         res[name + "_ms"] = round(ms, 2)
         res[name + "_tflops"] = round(fl / (ms * 1e-3) / 1e12, 1)
     res["speedup"] = round(res["torch_fp32_ms"] / res["hip_ms"], 2)
+    res["speedup_vs_bf16_autocast"] = round(res["torch_bf16_autocast_ms"] / res["hip_ms"], 2)
+    res["mfma_frac"] = round(res["hip_tflops"] / 2500.0, 4)
     return res

@@ -106,16 +106,51 @@ __global__ __launch_bounds__(256) void layernorm_bwd_kernel(const __bf16* dy, co
 
 // out[n] = sum over rows [0, M) of x[row][n]: stage 1 (this kernel with FINAL = false) sums
 // row slabs into part[slab][n]; stage 2 (FINAL = true) sums the slabs in order.  fp32 sums.
+// out[y][n] = sum of x[row][n] over the rows [y * rows_per, (y + 1) * rows_per) of slab y.
+// A wave covers 64 x VEC consecutive columns with 16-B loads (1 KiB per row per instruction);
+// the block's 4 waves take every 4th row of the slab and are added in a fixed order at the end
+// (deterministic).  Columns: full 16-B vectors when N % VEC == 0, element-wise otherwise.
 template <typename T>
 __global__ __launch_bounds__(256) void colsum_kernel(const T* x, int64_t M, int64_t N, int64_t rows_per,
                                                      float* out) {
-  const int64_t n = (int64_t)blockIdx.x * 256 + threadIdx.x;
-  if (n >= N) return;
+  constexpr int VEC = 16 / (int)sizeof(T);
+  __shared__ float red[3][64 * VEC];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int64_t c0 = ((int64_t)blockIdx.x * 64 + lane) * VEC;
   const int64_t r0 = (int64_t)blockIdx.y * rows_per;
   const int64_t r1 = r0 + rows_per < M ? r0 + rows_per : M;
-  float s = 0.f;
-  for (int64_t r = r0; r < r1; ++r) s += (float)x[r * N + n];
-  out[(int64_t)blockIdx.y * N + n] = s;
+  float acc[VEC];
+#pragma unroll
+  for (int v = 0; v < VEC; ++v) acc[v] = 0.f;
+  if (c0 < N) {
+    if (N % VEC == 0) {
+      typedef T tv __attribute__((ext_vector_type(VEC)));
+      int64_t r = r0 + wave;
+#pragma unroll 4
+      for (; r < r1; r += 4) {
+        const tv val = *(const tv*)(x + r * N + c0);
+#pragma unroll
+        for (int v = 0; v < VEC; ++v) acc[v] += (float)val[v];
+      }
+    } else {
+      for (int64_t r = r0 + wave; r < r1; r += 4)
+#pragma unroll
+        for (int v = 0; v < VEC; ++v)
+          if (c0 + v < N) acc[v] += (float)x[r * N + c0 + v];
+    }
+  }
+  if (wave > 0) {
+#pragma unroll
+    for (int v = 0; v < VEC; ++v) red[wave - 1][lane * VEC + v] = acc[v];
+  }
+  __syncthreads();
+  if (wave == 0 && c0 < N) {
+#pragma unroll
+    for (int v = 0; v < VEC; ++v) {
+      const float t = ((acc[v] + red[0][lane * VEC + v]) + red[1][lane * VEC + v]) + red[2][lane * VEC + v];
+      if (c0 + v < N) out[(int64_t)blockIdx.y * N + c0 + v] = t;
+    }
+  }
 }
 
 __global__ __launch_bounds__(256) void gelu_bwd_kernel(const __bf16* dy, const __bf16* pre, int64_t n, __bf16* dx) {
@@ -494,27 +529,35 @@ __global__ __launch_bounds__(256) void dropout_add_kernel(const __bf16* y, const
   }
 }
 
-// Row slabs of the first colsum pass: enough blocks to fill the chip (~1024 with the
-// column blocks), >= 16 rows per slab, <= 1024 slabs (the second pass sums them in order).
+// Row slabs of the first colsum pass: enough blocks to fill the chip (~1024 with the column
+// blocks of 512 bf16 columns), >= 64 rows per slab (16 per wave), <= 512 slabs (the second pass,
+// 256 fp32 columns per block, sums them in order).
 static int64_t colsum_slabs(int64_t M, int64_t N) {
   if (M < 256) return 1;
-  const int64_t gx = (N + 255) / 256;
+  const int64_t gx = (N + 511) / 512;
   int64_t slabs = (1024 + gx - 1) / gx;
-  if (slabs > M / 16) slabs = M / 16;
-  if (slabs > 1024) slabs = 1024;
+  if (slabs > M / 64) slabs = M / 64;
+  if (slabs > 512) slabs = 512;
   return slabs < 1 ? 1 : slabs;
+}
+
+template <typename T>
+static unsigned colsum_gx(int64_t N) {
+  const int64_t cols = 64 * (16 / (int64_t)sizeof(T));
+  return (unsigned)((N + cols - 1) / cols);
 }
 
 template <typename T>
 static int colsum_launch(const T* x, int64_t M, int64_t N, float* out, float* ws, hipStream_t s) {
   const int64_t slabs = colsum_slabs(M, N);
   const int64_t rows_per = (M + slabs - 1) / slabs;
-  const unsigned gx = (unsigned)((N + 255) / 256);
   if (slabs == 1) {
-    hipLaunchKernelGGL(colsum_kernel<T>, dim3(gx, 1), dim3(256), 0, s, x, M, N, M, out);
+    hipLaunchKernelGGL(colsum_kernel<T>, dim3(colsum_gx<T>(N), 1), dim3(256), 0, s, x, M, N, M, out);
   } else {
-    hipLaunchKernelGGL(colsum_kernel<T>, dim3(gx, (unsigned)slabs), dim3(256), 0, s, x, M, N, rows_per, ws);
-    hipLaunchKernelGGL(colsum_kernel<float>, dim3(gx, 1), dim3(256), 0, s, (const float*)ws, slabs, N, slabs, out);
+    hipLaunchKernelGGL(colsum_kernel<T>, dim3(colsum_gx<T>(N), (unsigned)slabs), dim3(256), 0, s, x, M, N, rows_per,
+                       ws);
+    hipLaunchKernelGGL(colsum_kernel<float>, dim3(colsum_gx<float>(N), 1), dim3(256), 0, s, (const float*)ws, slabs, N,
+                       slabs, out);
   }
   return hip_status(hipGetLastError());
 }
