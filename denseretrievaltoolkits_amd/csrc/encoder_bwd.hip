@@ -224,20 +224,19 @@ __global__ __launch_bounds__(256) void transpose_bf16_kernel(const __bf16* x, in
 //   Dv_q = sum_d dO[q][d] O[q][d];   dP = dO V^T;   dS = P (dP - Dv)
 //   dV = P^T dO;   dK = dS^T Qs;   dQ = scale * dS K.
 // LDS: Qs, K, V, dO row-major [Lp][64] (16-B chunk XOR (row >> 1) & 7, as the forward's
-// K image) and Qs^T, K^T, dO^T as [64][Lp] with rows padded by 16 B (an odd number of 16-B
-// chunks per row, so the 16-B pieces of consecutive d land on distinct banks), so every MFMA
-// operand is one conflict-free ds_read_b128; one per-wave 32 x 32 scratch tile (80-B rows)
-// turns the P and then the dS accumulator (rows in registers) into A operands.  Phase 1:
-// wave w owns key blocks w, w + 4 (dK, dV over all query blocks); phase 2: wave w owns query
-// blocks w, w + 4 (dQ over all key blocks, S and dP recomputed).  v_mfma_f32_32x32x16_bf16
-// throughout.  155 KiB of LDS at L = 160.
+// K image), read row-wise with ds_read_b128 (A / B operands along d) and column-wise with
+// ds_read_b64_tr_b16 (the B operands of dV = P^T dO, dK = dS^T Qs, dQ = dS K, along the
+// sequence: no transposed copies); one per-wave 32 x 32 scratch tile (80-B rows) turns the P
+// and then the dS accumulator (rows in registers) into A operands.  Phase 1: wave w owns key
+// blocks w, w + 4 (dK, dV over all query blocks); phase 2: wave w owns query blocks w, w + 4
+// (dQ over all key blocks, S and dP recomputed).  v_mfma_f32_32x32x16_bf16 throughout.
+// 76 KiB of LDS at L = 128 (two work-groups per CU), 92 KiB at L = 160.
 // ---------------------------------------------------------------------------
 constexpr int kAbThreads = 256;
 constexpr int kAbMaxSeq = 160;
 constexpr int kAbRow = 128;               // bytes per [.][64] bf16 row
 constexpr int kAbScr = 80;                // bytes per scratch row (32 bf16 + 16 B pad)
 
-__host__ __device__ constexpr int ab_tstride(int Lp) { return 2 * Lp + 16; }   // bytes per [64][Lp] row
 
 struct AttnBwdArgs {
   const __bf16* qkv;     // [B*L][3H]
@@ -255,7 +254,27 @@ struct AttnBwdArgs {
 
 __device__ __forceinline__ int ab_rc(int row, int chunk) { return row * kAbRow + ((chunk ^ ((row >> 1) & 7)) << 4); }
 
-__global__ __launch_bounds__(kAbThreads) void attention_bwd_kernel(AttnBwdArgs a) {
+typedef short ab_v4i16 __attribute__((ext_vector_type(4)));
+
+// 32x32x16 B operand along the SEQUENCE of a row-major [Lp][64] image: lane (c = lane & 31,
+// h = lane >> 5) gets rows row0 + 0..7 (row0 per lane: the caller's k block, 8 h apart) of
+// column col0 + c.  Two ds_read_b64_tr_b16 per operand: per 16-lane group, lane 4q + p
+// addresses row row0 + q (+ 4), columns col0 + 16 g + 4p .. + 3 of the swizzled image.
+__device__ __forceinline__ bf16x8 ab_tr8(const char* img, int row0, int col0, int lane) {
+  const int i = lane & 15, q = i >> 2, p = i & 3;
+  const int chunk = (col0 + 16 * ((lane >> 4) & 1) + 4 * p) >> 3;
+  const int lo = (p & 1) * 8;
+  const int r1 = row0 + q, r2 = r1 + 4;
+  typedef __attribute__((address_space(3))) ab_v4i16 lds_v4;
+  const ab_v4i16 x = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4*)(img + ab_rc(r1, chunk) + lo));
+  const ab_v4i16 y = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4*)(img + ab_rc(r2, chunk) + lo));
+  bf16x8 v;
+  __builtin_memcpy(&v, &x, 8);
+  __builtin_memcpy((char*)&v + 8, &y, 8);
+  return v;
+}
+
+__global__ __launch_bounds__(kAbThreads, 2) void attention_bwd_kernel(AttnBwdArgs a) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int L = (int)a.L;
   const int Lp = (L + 31) & ~31;
@@ -263,11 +282,7 @@ __global__ __launch_bounds__(kAbThreads) void attention_bwd_kernel(AttnBwdArgs a
   char* Ks = Qs + Lp * kAbRow;
   char* Vs = Ks + Lp * kAbRow;
   char* Os = Vs + Lp * kAbRow;                       // dO
-  const int ts = ab_tstride(Lp);
-  char* QT = Os + Lp * kAbRow;                       // [64][Lp] (+16 B per row)
-  char* KT = QT + 64 * ts;
-  char* OT = KT + 64 * ts;                           // dO^T
-  char* scr = OT + 64 * ts;                          // [4 waves][32][80 B]
+  char* scr = Os + Lp * kAbRow;                      // [4 waves][32][80 B]
   float* lse = (float*)(scr + 4 * 32 * kAbScr);      // [Lp]
   float* dv = lse + Lp;                              // [Lp]  Dv
   float* kb = dv + Lp;                               // [Lp]  key bias
@@ -305,14 +320,6 @@ __global__ __launch_bounds__(kAbThreads) void attention_bwd_kernel(AttnBwdArgs a
     *(bf16x8*)(Ks + ab_rc(row, c)) = k;
     *(bf16x8*)(Vs + ab_rc(row, c)) = v;
     *(bf16x8*)(Os + ab_rc(row, c)) = o;
-#pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      const int d = c * 8 + j;
-      const int off = d * ts + row * 2;
-      *(__bf16*)(QT + off) = q[j];
-      *(__bf16*)(KT + off) = k[j];
-      *(__bf16*)(OT + off) = o[j];
-    }
     // Dv: the 8 chunk-partials of one row sit in 8 consecutive lanes
     part += __shfl_xor(part, 1, 64);
     part += __shfl_xor(part, 2, 64);
@@ -390,7 +397,7 @@ __global__ __launch_bounds__(kAbThreads) void attention_bwd_kernel(AttnBwdArgs a
         const int qc = qb * 32 + 16 * ks + 8 * h;
 #pragma unroll
         for (int t = 0; t < 2; ++t) {
-          const bf16x8 ob = *(const bf16x8*)(OT + (32 * t + r) * ts + qc * 2);
+          const bf16x8 ob = ab_tr8(Os, qc, 32 * t, lane);
           dV[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(pa, ob, dV[t], 0, 0, 0);
         }
       }
@@ -409,7 +416,7 @@ __global__ __launch_bounds__(kAbThreads) void attention_bwd_kernel(AttnBwdArgs a
         const int qc = qb * 32 + 16 * ks + 8 * h;
 #pragma unroll
         for (int t = 0; t < 2; ++t) {
-          const bf16x8 qbt = *(const bf16x8*)(QT + (32 * t + r) * ts + qc * 2);
+          const bf16x8 qbt = ab_tr8(Qs, qc, 32 * t, lane);
           dK[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(sa, qbt, dK[t], 0, 0, 0);
         }
       }
@@ -479,7 +486,7 @@ __global__ __launch_bounds__(kAbThreads) void attention_bwd_kernel(AttnBwdArgs a
         const int kc = kbk * 32 + 16 * ks + 8 * h;
 #pragma unroll
         for (int t = 0; t < 2; ++t) {
-          const bf16x8 kt = *(const bf16x8*)(KT + (32 * t + r) * ts + kc * 2);
+          const bf16x8 kt = ab_tr8(Ks, kc, 32 * t, lane);
           dQ[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(sa, kt, dQ[t], 0, 0, 0);
         }
       }
@@ -652,8 +659,7 @@ int drt_attention_train_bwd_bf16(const void* qkv, const void* ctx, const void* d
   AttnBwdArgs a{(const __bf16*)qkv, (const __bf16*)ctx, (const __bf16*)dctx, lse, mask, (__bf16*)dqkv, B, L,
                 heads, heads * 64, scale, drop_p, seed, site};
   const int Lp = ((int)L + 31) & ~31;
-  const size_t lds = (size_t)4 * Lp * kAbRow + (size_t)3 * 64 * ab_tstride(Lp) + (size_t)4 * 32 * kAbScr +
-                     (size_t)3 * Lp * 4;
+  const size_t lds = (size_t)4 * Lp * kAbRow + (size_t)4 * 32 * kAbScr + (size_t)3 * Lp * 4;
   DRT_REQUIRE(lds <= 160 * 1024);
   static bool attr_set = false;
   if (!attr_set) {
