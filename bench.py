@@ -298,7 +298,7 @@ def main():
                         f"ShardedFlatIP.search_batches ({args.protocol}, certified, pipelined)",
             },
             "roofline": {
-                "kernel": "ip_scan16_kernel<768,FILTER,0,8,false,6> (csrc/search.hip)",
+                "kernel": "ip_scan16r_kernel<768,false> (csrc/search.hip)",
                 "bound": "hbm",
                 "achieved": round(achieved, 1),
                 "peak": HBM_PEAK_GBS,

@@ -650,6 +650,197 @@ __global__ __launch_bounds__(NW * 64, 1) void ip_scan16_kernel(ScanArgs a) {
 }
 
 // ---------------------------------------------------------------------------
+// Production filter scan, round 2: the 16-row / 8-wave kernel above with the LDS
+// fragment reads of tile t+1 rolled into tile t's MFMA sequence.  Fragment s of
+// tile t+1 is read into the register that held fragment s of tile t right after
+// that fragment's MFMA, so no LDS latency sits between the per-tile barrier and
+// the matrix work (the r02 ablation, tools/scan_ab.py: DMA alone 2.44 ms, DMA +
+// fragment reads 2.39, DMA + MFMA on registers 2.47, reads + MFMA 2.80 -> the
+// read-to-MFMA latency after every barrier, in lock step on both waves of a SIMD,
+// was the cost).  Same registers as the 8-wave kernel (the fragments were already
+// held for a whole tile).
+// Ring: NBUF slots, all in use: at iteration t tile t+1 has landed (it is read
+// during t), tiles t+2 .. t+NBUF are in flight, and slot(t) is refilled with tile
+// t+NBUF right after the barrier (its fragments were read in t-1 and drained by
+// that barrier's lgkmcnt(0)).
+// RAW: every wave waits (vmcnt) for its own share of tile t+1 before the barrier
+// of iteration t; reads of t+1 follow that barrier.  WAR: slot(t) is re-issued
+// after the barrier that follows the drain of its last reads.
+// The hit-count check that may flush the LDS hit list runs every 8th tile in the
+// sparse flavour (a full list spills straight to the global lists, so the check
+// only keeps appends cheap; it cost an exposed LDS round trip per tile).
+// ---------------------------------------------------------------------------
+template <int D, bool AGG>
+__global__ __launch_bounds__(512, 1) void ip_scan16r_kernel(ScanArgs a) {
+  constexpr int NW = 8;
+  using C = Scan16Cfg<D, NW>;
+  constexpr int PD = C::NBUF;   // issue distance: every slot in use
+  __shared__ __attribute__((aligned(16))) char smem[C::LDS_BYTES];
+  uint64_t* hk = (uint64_t*)(smem + C::HIT_KEY_OFF);
+  uint16_t* hq = (uint16_t*)(smem + C::HIT_Q_OFF);
+  uint32_t* hit_n = (uint32_t*)(smem + C::HIT_N_OFF);
+  uint32_t* qcnt = (uint32_t*)(smem + C::QCNT_OFF);
+  uint32_t* qoff = qcnt + kQueriesPerWG;
+
+  const int tid = threadIdx.x;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int lane = tid & 63;
+  const int r = lane & 15;
+  const int kq = lane >> 4;
+
+  const int64_t qbase = (int64_t)blockIdx.y * kQueriesPerWG;
+  const int64_t ntiles = (a.nrows + kT16 - 1) / kT16;
+  const int64_t t0 = blockIdx.x;
+  const int64_t tstep = gridDim.x;
+  const int64_t my_tiles = t0 < ntiles ? (ntiles - 1 - t0) / tstep + 1 : 0;
+  if (my_tiles == 0) return;
+  if (tid == 0) *hit_n = 0;
+  const uint32_t ring = lds_addr_of(smem);
+
+  // 16 queries per wave: qbase + 16 * wave + r
+  const int qloc = wave * 16 + r;
+  const int64_t qg = qbase + qloc;
+  const bool qok = qg < a.nq;
+  const int64_t qs = qok ? qg : 0;
+  bf16x8 qf[C::KS];
+#pragma unroll
+  for (int s = 0; s < C::KS; ++s) qf[s] = *(const bf16x8*)(a.Q + qs * a.ldq + s * 32 + kq * 8);
+  float tau = __builtin_nanf("");
+  {
+    const float tv = a.tau[qs];
+    tau = qok ? tv : tau;
+  }
+  if (!qok) {
+#pragma unroll
+    for (int s = 0; s < C::KS; ++s) qf[s] = (bf16x8){};
+  }
+#pragma unroll
+  for (int s = 0; s < C::KS; ++s) asm volatile("" ::"v"(qf[s]));
+  asm volatile("" ::"v"(tau));
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+
+  // prologue: tiles 0 .. PD-1 in flight, tile 0 landed and read into registers
+#pragma unroll
+  for (int p = 0; p < PD; ++p)
+    if (p < my_tiles) issue_tile16<D, NW, true>(a, ring + p * C::TILE_BYTES, t0 + p * tstep, wave, lane);
+  if (wave >= NW / 2) __builtin_amdgcn_s_setprio(1);
+  {
+    const int64_t last = my_tiles - 1 < PD - 1 ? my_tiles - 1 : PD - 1;
+    wait_tiles_younger<C::GLDS_PER_WAVE>((int)last);
+  }
+  lds_barrier();
+
+  const int sw = (r >> 1) & 7;
+  int aoff[2];
+#pragma unroll
+  for (int m = 0; m < 2; ++m) aoff[m] = r * 128 + (((4 * m + kq) ^ sw) << 4);
+  bf16x8 af[C::KS];
+#pragma unroll
+  for (int s = 0; s < C::KS; ++s) af[s] = *(const bf16x8*)(smem + (s >> 1) * (kT16 * 128) + aoff[s & 1]);
+
+  // MFMAs of the tile whose fragments are in af[], each fragment replaced by the same
+  // fragment of the tile in slot `nslot` right after its MFMA (unconditional: on the
+  // last tile the reads hit a stale slot and are never used).
+  auto mma_roll = [&](f32x4& acc, int nslot) {
+    const char* nb = smem + nslot * C::TILE_BYTES;
+    acc = (f32x4){0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int s = 0; s < C::KS; ++s) {
+      acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[s], qf[s], acc, 0, 0, 0);
+      af[s] = *(const bf16x8*)(nb + (s >> 1) * (kT16 * 128) + aoff[s & 1]);
+      // pin the order: a read hoisted above earlier MFMAs would keep both tiles' fragments live
+      __builtin_amdgcn_sched_barrier(0);
+    }
+  };
+  auto epilogue = [&](const f32x4& acc, int64_t rowbase) {
+    const float mx = fmaxf(fmaxf(acc[0], acc[1]), fmaxf(acc[2], acc[3])) - tau;
+    if (__ballot(mx >= 0.0f) == 0ull) return;
+    if (AGG) {
+      uint32_t m = 0;
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+        if (acc[j] >= tau && rowbase + j < a.nrows) m |= 1u << j;
+      const uint32_t c = __builtin_popcount(m);
+      uint32_t incl = c;
+#pragma unroll
+      for (int o = 1; o < 64; o <<= 1) {
+        const uint32_t v = __shfl_up(incl, o, 64);
+        if (lane >= o) incl += v;
+      }
+      const uint32_t tot = __shfl(incl, 63, 64);
+      uint32_t base = 0;
+      if (lane == 0) base = atomicAdd(hit_n, tot);
+      base = __shfl(base, 0, 64) + incl - c;
+      while (m) {
+        const int j = __builtin_ctz(m);
+        m &= m - 1;
+        const uint64_t key = ((uint64_t)desc_key(acc[j]) << 32) | (uint64_t)(uint32_t)(rowbase + j);
+        if (base < (uint32_t)kHitCap) {
+          hk[base] = key;
+          hq[base] = (uint16_t)qloc;
+        } else {
+          const uint32_t g = atomicAdd(a.counts + qg, 1u);
+          if (g < (uint64_t)a.cap) ((uint64_t*)a.out)[qg * a.cap + g] = key;
+        }
+        ++base;
+      }
+    } else {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int64_t row = rowbase + j;
+        if (acc[j] >= tau && row < a.nrows) {
+          const uint64_t key = ((uint64_t)desc_key(acc[j]) << 32) | (uint64_t)(uint32_t)row;
+          push_hit(a, qloc, qg, key, hit_n, hk, hq);
+        }
+      }
+    }
+  };
+
+  f32x4 accA, accB;
+  int64_t rbA = 0, rbB = 0;
+  int buf = 0;   // slot of tile it (its fragments are in af[])
+  // one tile: barrier, ring refill, MFMAs (+ reads of the next tile), deferred epilogue of the
+  // previous tile; the loop body runs two of them in sequence (accA / accB) so the fragment
+  // registers flow straight through and the accumulators are never selected at run time
+  auto iter = [&](int64_t it, f32x4& acc, int64_t& rb, const f32x4& prev, int64_t rb_prev) {
+    const int64_t tile = t0 + it * tstep;
+    if (it + 1 < my_tiles) {
+      const int64_t last = it + PD - 1 < my_tiles - 1 ? it + PD - 1 : my_tiles - 1;
+      wait_tiles_younger<C::GLDS_PER_WAVE>((int)(last - it - 1));
+    }
+    lds_barrier();   // tile it+1 landed (every wave's share); slot(it) fully read
+
+    if (AGG || (it & 7) == 0) {
+      const uint32_t n = *hit_n;
+      if (n >= (uint32_t)(kHitCap / 2)) {
+        if (AGG) flush_hits_agg<NW * 64>(a, qbase, n, hk, hq, qcnt, qoff);
+        else flush_hits<NW * 64>(a, qbase, n, hk, hq);
+        lds_barrier();
+        if (tid == 0) *hit_n = 0;
+        lds_barrier();
+      }
+    }
+    if (it + PD < my_tiles) issue_tile16<D, NW, true>(a, ring + buf * C::TILE_BYTES, tile + PD * tstep, wave, lane);
+    const int nslot = buf + 1 == C::NBUF ? 0 : buf + 1;
+    mma_roll(acc, nslot);
+    if (it > 0) epilogue(prev, rb_prev);
+    rb = tile * kT16 + 4 * kq;
+    buf = nslot;
+  };
+  for (int64_t it = 0; it < my_tiles; it += 2) {
+    iter(it, accA, rbA, accB, rbB);
+    if (it + 1 < my_tiles) iter(it + 1, accB, rbB, accA, rbA);
+  }
+  if (my_tiles & 1) epilogue(accA, rbA);
+  else epilogue(accB, rbB);
+
+  lds_barrier();
+  const uint32_t nf = *hit_n;
+  if (AGG) flush_hits_agg<NW * 64>(a, qbase, nf, hk, hq, qcnt, qoff);
+  else flush_hits<NW * 64>(a, qbase, nf, hk, hq);
+}
+
+// ---------------------------------------------------------------------------
 // Per-query selection.
 //
 // Fast path (every realistic input): one block per query,
@@ -1928,6 +2119,11 @@ static int launch_scan_d(const ScanArgs& a, int mode, hipStream_t s) {
         default: hipLaunchKernelGGL((ip_scan16_kernel<D, SCAN_FILTER, 0, 8, false, 0>), grid, dim3(512), 0, s, a); break;
       }
     }
+    else if (mode == SCAN_FILTER && (g_scan_variant == 20 || g_scan_variant == 21)) {
+      // rolled fragment reads (ip_scan16r_kernel): 20 sparse append, 21 wave-aggregated
+      if (g_scan_variant == 20) hipLaunchKernelGGL((ip_scan16r_kernel<D, false>), grid, dim3(512), 0, s, a);
+      else hipLaunchKernelGGL((ip_scan16r_kernel<D, true>), grid, dim3(512), 0, s, a);
+    }
     else if (mode == SCAN_FILTER && g_scan_variant == 7)
       hipLaunchKernelGGL((ip_scan16_kernel<D, SCAN_FILTER, 0, 8, false>), grid, dim3(512), 0, s, a);
     else if (mode == SCAN_FILTER) {
@@ -1937,11 +2133,11 @@ static int launch_scan_d(const ScanArgs& a, int mode, hipStream_t s) {
       // measured crossover (profiles/r01_*): dense below ~3M rows at cap 16384.
       const double eh = a.exp_hits > 0 ? (double)a.exp_hits : (double)a.cap / 4.0;
       const bool dense_hits = eh * 256.0 / (double)a.nrows >= 0.35;
-      // OPT: non-temporal corpus loads + s_setprio 1 for waves 4-7 (r02 A/B, tools/scan_ab.py,
-      // profiles/r02a_scan_ab.log: -2.3 % per launch vs OPT 0, ids identical)
-      constexpr int kOpt = SOPT_NT | SOPT_PRIO;
-      if (dense_hits) hipLaunchKernelGGL((ip_scan16_kernel<D, SCAN_FILTER, 0, 8, true, kOpt>), grid, dim3(512), 0, s, a);
-      else hipLaunchKernelGGL((ip_scan16_kernel<D, SCAN_FILTER, 0, 8, false, kOpt>), grid, dim3(512), 0, s, a);
+      // ip_scan16r_kernel: fragment reads of the next tile rolled into this tile's MFMAs, non-temporal
+      // corpus loads, s_setprio 1 for waves 4-7 (r02 A/B, tools/scan_ab.py, profiles/r02e_scan_roll.log:
+      // 2.59-2.62 vs 2.93 ms per launch for the round-1 loop with the same options, ids identical)
+      if (dense_hits) hipLaunchKernelGGL((ip_scan16r_kernel<D, true>), grid, dim3(512), 0, s, a);
+      else hipLaunchKernelGGL((ip_scan16r_kernel<D, false>), grid, dim3(512), 0, s, a);
     }
     else
       hipLaunchKernelGGL((ip_scan16_kernel<D, SCAN_DENSE, 0, 8>), grid, dim3(512), 0, s, a);
@@ -2026,9 +2222,11 @@ const char* drt_version(void) { return "drt-mi355x 0.1 (gfx950)"; }
 // ablations (no MFMA / no LDS fragment reads / no filter; d = 768 only); 8-11 = 8-wave
 // ablations (LDS fragment reads only / MFMA on register operands without filter / no filter /
 // no MFMA and no filter); 12-19 = the production filter scan (sparse append) with OPT bits
-// v - 12: 1 no deferred epilogue, 2 non-temporal corpus loads, 4 s_setprio for waves 4-7.
+// v - 12: 1 no deferred epilogue, 2 non-temporal corpus loads, 4 s_setprio for waves 4-7 (the
+// round-1 production loop is 18); 20 / 21 = the production rolled-read kernel, sparse / aggregated
+// append (0 picks between them by the expected hit density).
 int drt_scan_variant(int32_t v) {
-  if (v < 0 || v > 19) return DRT_EINVAL;
+  if (v < 0 || v > 21) return DRT_EINVAL;
   g_scan_variant = v;
   return DRT_OK;
 }

@@ -49,6 +49,33 @@ def test_ip_topk_integer_bit_exact(dev, nq, n, d, k):
     np.testing.assert_array_equal(gs, es)
 
 
+@pytest.mark.parametrize("variant", [18, 20, 21])
+@pytest.mark.parametrize("nq,n,d,k", [
+    (128, 50000, 768, 1000),   # ~12 tiles per work-group
+    (130, 20000, 128, 100),    # fewer tiles per work-group than ring slots (8 at d = 128)
+    (1, 200003, 768, 1000),    # ragged tail tile
+    (64, 70000, 1024, 1000),   # 4-slot ring at d = 1024
+])
+def test_filter_scan_variants_bit_exact(dev, variant, nq, n, d, k):
+    """Each filter-scan kernel forced explicitly (drt_scan_variant): 18 = the round-1 loop,
+    20 / 21 = the rolled-read production kernel with the sparse / wave-aggregated append
+    (production picks one by the expected hit density), all bit-exact vs the oracle."""
+    from denseretrievaltoolkits_amd import _native
+    lib = _native.load()
+    rng = np.random.default_rng(2000 + nq + n + d + k)
+    q = int_bf16(rng, (nq, d), -4, 4)
+    p = int_bf16(rng, (n, d), -4, 4)
+    _native.check(lib.drt_scan_variant(variant), "drt_scan_variant")
+    try:
+        gs, gi, st = _run(dev, q, p, k, resolve=False)
+    finally:
+        _native.check(lib.drt_scan_variant(0), "drt_scan_variant")
+    es, ei = orc.ip_topk(q, p, k)
+    assert (st == 0).all()
+    np.testing.assert_array_equal(gi, ei)
+    np.testing.assert_array_equal(gs, es)
+
+
 def test_ip_topk_gaussian_tolerance(dev):
     rng = np.random.default_rng(7)
     nq, n, d, k = 128, 120000, 768, 1000

@@ -52,11 +52,11 @@ def main():
             times[v].append(tot.value / max(1, cnt.value))
             if rnd == 0:
                 ids = torch.stack([o[1] for o in outs]).cpu()
-                if v == 0:
+                if v == variants[0]:
                     ref["ids"] = ids
                 elif v >= 12:
                     same = bool(torch.equal(ids, ref["ids"]))
-                    print(f"variant {v}: ids identical to variant 0: {same}", flush=True)
+                    print(f"variant {v}: ids identical to variant {variants[0]}: {same}", flush=True)
             print(f"round {rnd} variant {v}: {times[v][-1]:.4f} ms", flush=True)
     _native.check(lib.drt_scan_variant(0), "variant")
     alg = args.n * 768 * 2 + args.qb * 768 * 2 + args.qb * args.k * 12
