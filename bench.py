@@ -50,6 +50,9 @@ def parse():
     ap.add_argument("--no-encode", action="store_true",
                     help="skip the encode leg (passages/sec of the bf16 BERT-base passage tower, every rank)")
     ap.add_argument("--scan-variant", type=int, default=0, help="benchmark-only ablation of the scan kernel")
+    ap.add_argument("--group-queries", type=int, default=-1,
+                    help="queries per group of batches in search_batches (0 = per-batch path; default: "
+                         "search.GROUP_QUERIES)")
     ap.add_argument("--protocol", choices=["global_tau", "per_shard"], default="global_tau",
                     help="N > 1 exchange protocol (per_shard = exact top-k per shard + merge)")
     return ap.parse_args()
@@ -211,7 +214,13 @@ def main():
     queries = torch.randn((nsteps, qb, d), generator=gq, device=dev).to(torch.bfloat16)
 
     gloo = world > 1 and dist.get_backend() == "gloo"
-    use_global = world > 1 and args.protocol == "global_tau"
+    from denseretrievaltoolkits_amd import search as srch
+    if args.group_queries == 0:
+        srch.GROUP_MIN_ROWS = 1 << 62          # one-GPU: per-batch path
+        srch.GROUP_QUERIES = qb                 # several GPUs: one batch per group
+    elif args.group_queries > 0:
+        srch.GROUP_QUERIES = args.group_queries
+    use_global = (world > 1 and args.protocol == "global_tau") or (world == 1 and n_local >= srch.GROUP_MIN_ROWS)
     # the product path: the same index objects and certified, pipelined batch search that
     # BaseFaissIPRetriever.batch_search / Trainer.evaluate use (search.py); every query
     # certified exact inside the timed region (an uncertified one is rescanned there)
@@ -234,7 +243,10 @@ def main():
     torch.cuda.synchronize()
     local_index = index if world == 1 else index.local
     res0 = local_index.resolved
-    fb0 = 0 if world == 1 else index.fallbacks
+
+    def fallbacks():
+        return index.group_fallbacks if world == 1 else index.fallbacks
+    fb0 = fallbacks()
 
     lib.drt_profile_enable(_native.PROF_SCAN, 1)
     if world > 1:
@@ -248,7 +260,7 @@ def main():
     t1 = time.perf_counter()
     lib.drt_profile_enable(_native.PROF_SCAN, 0)
     n_resolved = local_index.resolved - res0
-    n_fallback = (0 if world == 1 else index.fallbacks) - fb0
+    n_fallback = fallbacks() - fb0
     tot_ms = _native.ctypes.c_double(0.0)
     cnt = _native.c_i64(0)
     _native.check(lib.drt_profile_read(_native.PROF_SCAN, _native.ctypes.byref(tot_ms), _native.ctypes.byref(cnt)),
@@ -294,8 +306,12 @@ def main():
                                                     if world > 1 else "")),
                 "n_corpus": args.n_corpus, "dim": d, "query_batch": qb, "k": k,
                 "parallelism": f"row-shard x{world}",
-                "path": "FlatIPIndex.search_batches (certified, pipelined)" if world == 1 else
-                        f"ShardedFlatIP.search_batches ({args.protocol}, certified, pipelined)",
+                "path": ("FlatIPIndex.search_batches (certified, pipelined" +
+                         (f"; sample phase and merge per group of {srch.GROUP_QUERIES} queries, one filter scan "
+                          "per batch)" if use_global else ")")) if world == 1 else
+                        (f"ShardedFlatIP.search_batches ({args.protocol}, certified, pipelined" +
+                         (f"; sample phase, exchanges and merge per group of {srch.GROUP_QUERIES} queries, one "
+                          "filter scan per batch)" if use_global else ")")),
             },
             "roofline": {
                 "kernel": "ip_scan16r_kernel<768,false> (csrc/search.hip)",
@@ -312,6 +328,7 @@ def main():
             },
             "uncertified_queries_resolved": int(n_resolved),
             "global_tau_fallback_batches": int(n_fallback),
+            "query_group": srch.GROUP_QUERIES if use_global else qb,
         }
         if world == 1 and not args.no_cpu_baseline:
             out["cpu_baseline"] = cpu_baseline(args, shard, queries[args.warmup], results[0])

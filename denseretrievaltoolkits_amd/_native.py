@@ -45,6 +45,8 @@ _SIGNATURES = [
                                         c_sz, c_vp]),
     ("drt_ip_topk_dist_filter_lists", c_i32, [c_vp, c_i64, c_vp, c_i64, c_i64, c_i32, c_i32, c_i64, c_vp, c_i32,
                                               c_vp, c_vp, c_vp, c_sz, c_vp]),
+    ("drt_ip_topk_dist_filter_lists_at", c_i32, [c_vp, c_i64, c_vp, c_i64, c_i64, c_i32, c_i32, c_i64, c_vp,
+                                                 c_i32, c_i64, c_vp, c_vp, c_vp, c_sz, c_vp]),
     ("drt_topk_merge_packed", c_i32, [c_vp, c_i64, c_i32, c_i32, c_i64, c_vp, c_vp, c_vp, c_vp]),
     ("drt_topk_merge_packed_variant", c_i32, [c_i32]),
     ("drt_gemm_nt_bf16_f32", c_i32, [c_vp, c_vp, c_vp, c_i64, c_i64, c_i32, c_i64, c_vp]),

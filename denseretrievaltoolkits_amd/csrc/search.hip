@@ -670,7 +670,7 @@ __global__ __launch_bounds__(NW * 64, 1) void ip_scan16_kernel(ScanArgs a) {
 // sparse flavour (a full list spills straight to the global lists, so the check
 // only keeps appends cheap; it cost an exposed LDS round trip per tile).
 // ---------------------------------------------------------------------------
-template <int D, bool AGG>
+template <int D, bool AGG, bool FAGG = AGG>
 __global__ __launch_bounds__(512, 1) void ip_scan16r_kernel(ScanArgs a) {
   constexpr int NW = 8;
   using C = Scan16Cfg<D, NW>;
@@ -813,7 +813,7 @@ __global__ __launch_bounds__(512, 1) void ip_scan16r_kernel(ScanArgs a) {
     if (AGG || (it & 7) == 0) {
       const uint32_t n = *hit_n;
       if (n >= (uint32_t)(kHitCap / 2)) {
-        if (AGG) flush_hits_agg<NW * 64>(a, qbase, n, hk, hq, qcnt, qoff);
+        if (FAGG) flush_hits_agg<NW * 64>(a, qbase, n, hk, hq, qcnt, qoff);
         else flush_hits<NW * 64>(a, qbase, n, hk, hq);
         lds_barrier();
         if (tid == 0) *hit_n = 0;
@@ -836,7 +836,7 @@ __global__ __launch_bounds__(512, 1) void ip_scan16r_kernel(ScanArgs a) {
 
   lds_barrier();
   const uint32_t nf = *hit_n;
-  if (AGG) flush_hits_agg<NW * 64>(a, qbase, nf, hk, hq, qcnt, qoff);
+  if (FAGG) flush_hits_agg<NW * 64>(a, qbase, nf, hk, hq, qcnt, qoff);
   else flush_hits<NW * 64>(a, qbase, nf, hk, hq);
 }
 
@@ -1345,7 +1345,10 @@ __global__ __launch_bounds__(kSelThreads) void select_kernel(SelectArgs a) {
         op[j] = ~0ull;
       }
     }
-    if (tid == 0) op[a.k] = (INPUT == SEL_KEYS64 && c_raw > a.cap) ? 1ull : 0ull;
+    if (tid == 0) {
+      const uint64_t nval = (uint64_t)(kk_total < a.k ? kk_total : a.k);
+      op[a.k] = (nval << 32) | ((INPUT == SEL_KEYS64 && c_raw > a.cap) ? 1ull : 0ull);
+    }
     return;
   }
   float* os = a.out_scores + orow * a.ldo;
@@ -1789,7 +1792,104 @@ __global__ __launch_bounds__(kRankThreads) void merge_packed_rank_kernel(const u
   }
 }
 
-static int g_merge_variant = 0;   // 0 auto, 1 tree, 2 rank (tests / benchmarks)
+// Count merge (round 2, the default where nparts <= 8 and nparts * k <= 8192): entry k of every
+// packed list carries its valid count in bits 32-63, so ONE work-group per query loads only the
+// valid keys of all parts (in the global-threshold regime ~1.3 k / world per part, not k) into
+// LDS, then places every key at rank = its index in its part + its lower bounds in the other
+// parts (branch-free searches advancing in lock step, as in the rank merge).  The rank merge
+// loaded all nparts * k keys of a query in each of its nparts work-groups.
+constexpr int kCntThreads = 1024;
+constexpr int kCntMaxParts = 8;
+constexpr int kCntMaxKeys = 8192;
+__global__ __launch_bounds__(kCntThreads) void merge_packed_count_kernel(const uint64_t* parts, int64_t nq,
+                                                                         int nparts, int k, int64_t n_global,
+                                                                         float* out_s, int64_t* out_i,
+                                                                         int32_t* status) {
+  extern __shared__ __attribute__((aligned(16))) uint64_t P[];   // valid prefixes of all parts, concatenated
+  __shared__ int cnt[kCntMaxParts], off[kCntMaxParts + 1], flg[kCntMaxParts];
+  const int tid = threadIdx.x;
+  const int64_t q = blockIdx.x;
+  const int64_t ps = (int64_t)(k + 1);
+  if (tid < kCntMaxParts) {
+    int c = 0, f = 0;
+    if (tid < nparts) {
+      const uint64_t w = parts[((int64_t)tid * nq + q) * ps + k];
+      c = (int)(w >> 32);
+      c = c < k ? c : k;
+      f = (int)(w & 1ull);
+    }
+    cnt[tid] = c;
+    flg[tid] = f;
+  }
+  __syncthreads();
+  if (tid == 0) {
+    int o = 0;
+    for (int l = 0; l < kCntMaxParts; ++l) {
+      off[l] = o;
+      o += cnt[l];
+    }
+    off[kCntMaxParts] = o;
+  }
+  __syncthreads();
+  const int tot = off[kCntMaxParts];
+  int maxc = 0;
+#pragma unroll
+  for (int l = 0; l < kCntMaxParts; ++l) maxc = cnt[l] > maxc ? cnt[l] : maxc;
+  const int nsteps = 32 - __builtin_clz((unsigned)maxc | 1u);   // halvings until every len <= 1
+  int offs[kCntMaxParts + 1];
+#pragma unroll
+  for (int l = 0; l <= kCntMaxParts; ++l) offs[l] = off[l];
+  auto part_of = [&](int e) {
+    int l = 0;
+#pragma unroll
+    for (int j = 1; j < kCntMaxParts; ++j) l += (e >= offs[j]) ? 1 : 0;
+    return l;
+  };
+  for (int e = tid; e < tot; e += kCntThreads) {
+    const int l = part_of(e);
+    P[e] = parts[((int64_t)l * nq + q) * ps + (e - offs[l])];
+  }
+  __syncthreads();
+  for (int e = tid; e < tot; e += kCntThreads) {
+    const int me = part_of(e);
+    const uint64_t x = P[e];
+    int base[kCntMaxParts], len[kCntMaxParts];
+#pragma unroll
+    for (int l = 0; l < kCntMaxParts; ++l) {
+      base[l] = offs[l];
+      len[l] = (l == me) ? 0 : offs[l + 1] - offs[l];
+    }
+    for (int step = 0; step < nsteps; ++step) {
+#pragma unroll
+      for (int l = 0; l < kCntMaxParts; ++l) {
+        if (len[l] > 1) {
+          const int half = len[l] >> 1;
+          base[l] = P[base[l] + half - 1] < x ? base[l] + half : base[l];
+          len[l] -= half;
+        }
+      }
+    }
+    int rank = e - offs[me];
+#pragma unroll
+    for (int l = 0; l < kCntMaxParts; ++l)
+      rank += (base[l] - offs[l]) + ((len[l] == 1 && P[base[l]] < x) ? 1 : 0);
+    if (rank < k) {
+      out_s[q * k + rank] = desc_key_to_score((uint32_t)(x >> 32));
+      out_i[q * k + rank] = (int64_t)(x & 0xFFFFFFFFull);
+    }
+  }
+  for (int i = (tot < k ? tot : k) + tid; i < k; i += kCntThreads) {
+    out_s[q * k + i] = kPadScore;
+    out_i[q * k + i] = -1;
+  }
+  if (status && tid == 0) {
+    int bad = 0;
+    for (int l = 0; l < kCntMaxParts; ++l) bad |= flg[l];
+    status[q] = (bad || (tot < k && n_global >= (int64_t)k)) ? 1 : 0;
+  }
+}
+
+static int g_merge_variant = 0;   // 0 auto, 1 tree, 2 rank, 3 count (tests / benchmarks)
 
 // Merge of packed per-shard lists [nparts][nq][k + 1] (sorted u64 keys, entry k =
 // flags) into (score, id) [nq][k]; status[q] = 1 unless exact: the k-th merged
@@ -2119,10 +2219,12 @@ static int launch_scan_d(const ScanArgs& a, int mode, hipStream_t s) {
         default: hipLaunchKernelGGL((ip_scan16_kernel<D, SCAN_FILTER, 0, 8, false, 0>), grid, dim3(512), 0, s, a); break;
       }
     }
-    else if (mode == SCAN_FILTER && (g_scan_variant == 20 || g_scan_variant == 21)) {
-      // rolled fragment reads (ip_scan16r_kernel): 20 sparse append, 21 wave-aggregated
+    else if (mode == SCAN_FILTER && g_scan_variant >= 20 && g_scan_variant <= 22) {
+      // rolled fragment reads (ip_scan16r_kernel): 20 sparse append, 21 wave-aggregated append and
+      // flush, 22 sparse append + aggregated flush (one global atomic per (work-group, query))
       if (g_scan_variant == 20) hipLaunchKernelGGL((ip_scan16r_kernel<D, false>), grid, dim3(512), 0, s, a);
-      else hipLaunchKernelGGL((ip_scan16r_kernel<D, true>), grid, dim3(512), 0, s, a);
+      else if (g_scan_variant == 21) hipLaunchKernelGGL((ip_scan16r_kernel<D, true>), grid, dim3(512), 0, s, a);
+      else hipLaunchKernelGGL((ip_scan16r_kernel<D, false, true>), grid, dim3(512), 0, s, a);
     }
     else if (mode == SCAN_FILTER && g_scan_variant == 7)
       hipLaunchKernelGGL((ip_scan16_kernel<D, SCAN_FILTER, 0, 8, false>), grid, dim3(512), 0, s, a);
@@ -2226,7 +2328,7 @@ const char* drt_version(void) { return "drt-mi355x 0.1 (gfx950)"; }
 // round-1 production loop is 18); 20 / 21 = the production rolled-read kernel, sparse / aggregated
 // append (0 picks between them by the expected hit density).
 int drt_scan_variant(int32_t v) {
-  if (v < 0 || v > 21) return DRT_EINVAL;
+  if (v < 0 || v > 22) return DRT_EINVAL;
   g_scan_variant = v;
   return DRT_OK;
 }
@@ -2571,10 +2673,22 @@ int drt_ip_topk_dist_filter(const void* Q, int64_t nq, const void* P, int64_t n_
 int drt_ip_topk_dist_filter_lists(const void* Q, int64_t nq, const void* P, int64_t n_local, int64_t n_global,
                                   int32_t d, int32_t k, int64_t id_offset, const uint32_t* lists, int32_t nlists,
                                   float* tau_out, uint64_t* packed, void* ws, size_t ws_bytes, void* stream) {
+  const int32_t r = drt_ip_topk_sample_rank(k);
+  return drt_ip_topk_dist_filter_lists_at(Q, nq, P, n_local, n_global, d, k, id_offset, lists, nlists,
+                                          r > 0 ? nq * r : 0, tau_out, packed, ws, ws_bytes, stream);
+}
+
+// The same for the query rows [q0, q0 + nq) of lists gathered for a larger query set: list j of
+// this batch starts at lists + j * lists_stride (u32 elements), rows r apart.
+int drt_ip_topk_dist_filter_lists_at(const void* Q, int64_t nq, const void* P, int64_t n_local, int64_t n_global,
+                                     int32_t d, int32_t k, int64_t id_offset, const uint32_t* lists, int32_t nlists,
+                                     int64_t lists_stride, float* tau_out, uint64_t* packed, void* ws,
+                                     size_t ws_bytes, void* stream) {
   DRT_REQUIRE(valid_dist_dims(nq, n_local, n_global, d, k));
   DRT_REQUIRE(id_offset >= 0 && id_offset + n_local <= n_global);
   const int32_t r = drt_ip_topk_sample_rank(k);
   DRT_REQUIRE(r > 0 && nlists >= 1 && (int64_t)nlists * r <= kKthChunk);
+  DRT_REQUIRE(nlists == 1 || lists_stride >= nq * r);
   if (nq == 0) return DRT_OK;
   DRT_REQUIRE(Q && lists && packed && ws);
   const TopkPlan p = make_dist_plan(nq, n_local, n_global, k);
@@ -2584,7 +2698,7 @@ int drt_ip_topk_dist_filter_lists(const void* Q, int64_t nq, const void* P, int6
   uint32_t* cnt = (uint32_t*)(w + p.off_cnt);
   float* tau = tau_out ? tau_out : (float*)(w + p.off_tau);
   hipLaunchKernelGGL(kth_final_kernel, dim3((unsigned)nq), dim3(kKthThreads), 0, s, lists, (int)nlists, (int)r,
-                     (int64_t)nq * r, (int64_t)r, tau, (uint32_t*)nullptr, n_local > 0 ? cnt : (uint32_t*)nullptr);
+                     lists_stride, (int64_t)r, tau, (uint32_t*)nullptr, n_local > 0 ? cnt : (uint32_t*)nullptr);
   DRT_CHECK_HIP(hipGetLastError());
   SelectArgs sa{};
   sa.in = w + p.off_keys;
@@ -2625,7 +2739,7 @@ int drt_ip_topk_dist_filter_lists(const void* Q, int64_t nq, const void* P, int6
 
 // Test / benchmark switch of drt_topk_merge_packed: 0 automatic, 1 tree merge, 2 rank merge (where it fits).
 int drt_topk_merge_packed_variant(int32_t v) {
-  if (v < 0 || v > 2) return DRT_EINVAL;
+  if (v < 0 || v > 3) return DRT_EINVAL;
   g_merge_variant = v;
   return DRT_OK;
 }
@@ -2645,7 +2759,18 @@ int drt_topk_merge_packed(const uint64_t* parts, int64_t nq, int32_t nparts, int
   int rc = DRT_OK;
   const size_t rank_lds = (size_t)nparts * k * 8;
   const bool rank_ok = nparts <= kRankMaxParts && rank_lds <= (size_t)kRankLds;
-  if (rank_ok && g_merge_variant != 1 && (g_merge_variant == 2 || nparts > 1)) {
+  const bool count_ok = nparts <= kCntMaxParts && (int64_t)nparts * k <= kCntMaxKeys;
+  // one part (one GPU): the plain per-query kernel (tools/merge_bench.py: 8 vs 23 us at 2048 queries)
+  if (count_ok && ((g_merge_variant == 0 && nparts > 1) || g_merge_variant == 3)) {
+    static bool attr_set = false;
+    if (!attr_set) {
+      DRT_CHECK_HIP(hipFuncSetAttribute((const void*)merge_packed_count_kernel,
+                                        hipFuncAttributeMaxDynamicSharedMemorySize, kCntMaxKeys * 8));
+      attr_set = true;
+    }
+    hipLaunchKernelGGL(merge_packed_count_kernel, dim3((unsigned)nq), dim3(kCntThreads), rank_lds, s, parts, nq,
+                       (int)nparts, (int)k, n_global, out_scores, out_ids, status);
+  } else if (rank_ok && g_merge_variant != 1 && (g_merge_variant == 2 || nparts > 1)) {
     static bool attr_set = false;
     if (!attr_set) {
       DRT_CHECK_HIP(hipFuncSetAttribute((const void*)merge_packed_rank_kernel,

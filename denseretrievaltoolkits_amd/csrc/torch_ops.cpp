@@ -195,6 +195,34 @@ Tensor dist_filter_lists(const Tensor& q_, const Tensor& p_, int64_t n_global, i
   return packed;
 }
 
+// dist_filter_lists for query rows [q0, q0 + nq) of lists [nlists, NQ, r] gathered for a group of
+// batches, writing the packed lists into `packed` ([nq, k + 1], e.g. a row slice of a group buffer).
+void dist_filter_lists_into(const Tensor& q_, const Tensor& p_, int64_t n_global, int64_t k, int64_t id_offset,
+                            const Tensor& lists, int64_t q0, Tensor& packed) {
+  need(q_, "q", at::kBFloat16, 2);
+  need(p_, "p", at::kBFloat16, 2);
+  need(lists, "lists", at::kInt, 3);
+  need(packed, "packed", at::kLong, 2);
+  const c10::DeviceGuard g(q_.device());
+  const Tensor q = q_.contiguous(), p = p_.contiguous();
+  TORCH_CHECK_VALUE(lists.is_contiguous(), "lists must be a contiguous [nlists, NQ, r] tensor");
+  TORCH_CHECK_VALUE(q0 >= 0 && q0 + q.size(0) <= lists.size(1), "query rows [", q0, ", ", q0 + q.size(0),
+                    ") outside the lists' ", lists.size(1), " rows");
+  TORCH_CHECK_VALUE(packed.is_contiguous() && packed.size(0) == q.size(0) && packed.size(1) == k + 1,
+                    "packed must be a contiguous [nq, k + 1] tensor");
+  const int64_t r = lists.size(2);
+  TORCH_CHECK_VALUE(r == drt_ip_topk_sample_rank((int32_t)k), "lists hold ", r, " keys per query, k=", k, " needs ",
+                    drt_ip_topk_sample_rank((int32_t)k));
+  size_t wsb = 0;
+  Tensor ws = dist_ws(q, p.size(0), n_global, k, &wsb);
+  check_rc(drt_ip_topk_dist_filter_lists_at(q.data_ptr(), q.size(0), p.size(0) ? p.data_ptr() : nullptr, p.size(0),
+                                            n_global, (int32_t)q.size(1), (int32_t)k, id_offset,
+                                            (const uint32_t*)lists.data_ptr<int32_t>() + q0 * r,
+                                            (int32_t)lists.size(0), lists.size(1) * r, nullptr,
+                                            (uint64_t*)packed.data_ptr<int64_t>(), ws.data_ptr(), wsb, stream_of(q)),
+           "drt_ip_topk_dist_filter_lists_at");
+}
+
 std::tuple<Tensor, Tensor, Tensor> merge_packed(const Tensor& parts_, int64_t k, int64_t n_global) {
   need(parts_, "parts", at::kLong, 3);
   TORCH_CHECK_VALUE(parts_.size(2) == k + 1, "merge_packed expects [nparts, nq, k + 1]");
@@ -370,6 +398,8 @@ TORCH_LIBRARY(drt, m) {
   m.def("dist_tau(Tensor lists, int k) -> Tensor");
   m.def("dist_filter(Tensor q, Tensor p, int n_global, int k, int id_offset, Tensor tau) -> Tensor");
   m.def("dist_filter_lists(Tensor q, Tensor p, int n_global, int k, int id_offset, Tensor lists) -> Tensor");
+  m.def("dist_filter_lists_into(Tensor q, Tensor p, int n_global, int k, int id_offset, Tensor lists, int q0, "
+        "Tensor(a!) packed) -> ()");
   m.def("merge_packed(Tensor parts, int k, int n_global) -> (Tensor, Tensor, Tensor)");
   m.def("score_ce_fwd(Tensor q, Tensor p, int target_stride, float scale) -> (Tensor, Tensor, Tensor)");
   m.def("score_ce_bwd(Tensor grad, Tensor q, Tensor p, Tensor scores, Tensor lse, int target_stride, "
@@ -392,6 +422,7 @@ TORCH_LIBRARY_IMPL(drt, CUDA, m) {   // the GPU dispatch key of torch-ROCm
   m.impl("dist_tau", &dist_tau);
   m.impl("dist_filter", &dist_filter);
   m.impl("dist_filter_lists", &dist_filter_lists);
+  m.impl("dist_filter_lists_into", &dist_filter_lists_into);
   m.impl("merge_packed", &merge_packed);
   m.impl("score_ce_fwd", &score_ce_fwd);
   m.impl("score_ce_bwd", &score_ce_bwd);

@@ -114,6 +114,15 @@ def dist_filter_lists(q: torch.Tensor, p: torch.Tensor, n_global: int, k: int, i
     return ops.load().dist_filter_lists(q, p, n_global, k, id_offset, lists)
 
 
+def dist_filter_lists_into(q: torch.Tensor, p: torch.Tensor, n_global: int, k: int, id_offset: int,
+                           lists: torch.Tensor, q0: int, packed: torch.Tensor) -> None:
+    """dist_filter_lists for the query rows [q0, q0 + nq) of lists [nlists, NQ, r] gathered for a
+    group of batches; the packed lists land in ``packed`` ([nq, k + 1], e.g. a row slice of a
+    group buffer)."""
+    _require_device(q, p, lists, packed)
+    ops.load().dist_filter_lists_into(q, p, n_global, k, id_offset, lists, q0, packed)
+
+
 def merge_packed(parts: torch.Tensor, k: int, n_global: int):
     """[nparts, nq, k + 1] packed lists -> (scores [nq,k], ids [nq,k], status [nq] int32; 0 = exact)."""
     _require_device(parts)

@@ -66,6 +66,66 @@ def _pipeline(batches, enqueue, finish):
     return res
 
 
+# Batched search (search_batches): the per-batch fixed costs of the global-threshold protocol --
+# the sample scan + its k-th selection and, across shards, the sample-list all-gather, the packed
+# all-gather and the merge -- are paid once per GROUP of query batches; every batch still streams
+# the whole shard once in its own filter scan.  Queries per group (16 batches of 128):
+GROUP_QUERIES = 2048
+# one-GPU indexes smaller than this keep the per-batch path (nothing to amortise)
+GROUP_MIN_ROWS = 1 << 20
+
+
+def _groups(batches, cap=GROUP_QUERIES):
+    grp, n = [], 0
+    for q in batches:
+        if grp and n + q.shape[0] > cap:
+            yield grp
+            grp, n = [], 0
+        grp.append(q)
+        n += q.shape[0]
+    if grp:
+        yield grp
+
+
+def _gtau_enqueue_group(local, qs, k: int, n_global: int, offset: int, gather):
+    """One group of query batches through the global-threshold protocol (see ShardedFlatIP):
+    ONE sample launch for all of the group's queries, one exchange of the sample lists, one
+    filter scan (+ threshold, select) per batch writing its packed top-k into a group buffer,
+    one exchange of that buffer and one merge that certifies every query.  ``gather(t)`` ->
+    [world, *t.shape] (identity stack on one GPU)."""
+    sizes = [q.shape[0] for q in qs]
+    qg = qs[0] if len(qs) == 1 else torch.cat(qs)
+    best = local.dist_sample(qg, n_global, k)                       # [Qg, r]
+    lists = gather(best).contiguous()                               # [world, Qg, r]
+    packed = torch.empty((qg.shape[0], k + 1), dtype=torch.int64, device=qg.device)
+    o = 0
+    for q, nb in zip(qs, sizes):
+        kernels.dist_filter_lists_into(q, local.rows, n_global, k, offset, lists, o, packed[o:o + nb])
+        o += nb
+    s, i, st = kernels.merge_packed(gather(packed), k, n_global)
+    h, ev = _stage_status(st)
+    return qs, sizes, s, i, h, ev
+
+
+def _gtau_finish_group(pend, redo):
+    """Per-batch results of a group; a batch with an uncertified query is redone by ``redo(q)``
+    (the exact path).  Every rank merged the same gathered lists, so all ranks redo the same
+    batches (their collectives stay matched)."""
+    qs, sizes, s, i, h, ev = pend
+    if ev is not None:
+        ev.synchronize()
+    bad = (h != 0)
+    res, o, nredo = [], 0, 0
+    for q, nb in zip(qs, sizes):
+        if bool(bad[o:o + nb].any()):
+            res.append(redo(q))
+            nredo += 1
+        else:
+            res.append((s[o:o + nb], i[o:o + nb]))
+        o += nb
+    return res, nredo
+
+
 class FlatIPIndex:
     """Exact IP index over bf16 rows resident on one GPU (IndexFlatIP semantics)."""
 
@@ -141,14 +201,33 @@ class FlatIPIndex:
     def search_device(self, q, k: int, id_offset: int = 0) -> Tuple[torch.Tensor, torch.Tensor]:
         return self._finish(self._enqueue(q, k, id_offset))
 
+    group_fallbacks = 0   # batches of grouped searches redone by the exact per-batch path
+
     def search_batches(self, batches, k: int, id_offset: int = 0, outs=None):
-        """Certified top-k of every query batch (device tensors), pipelined: batch j + 1 is
-        enqueued before the host checks batch j's status, so the per-batch certification
-        costs an event wait on finished work, not a drained stream.  ``outs[j]`` = optional
-        (scores, ids) output buffers of batch j.  This is the path BaseFaissIPRetriever
-        .batch_search, Trainer.evaluate and bench.py time."""
+        """Certified top-k of every query batch (device tensors), pipelined: the next batch (or
+        group of batches) is enqueued before the host checks the previous one's status, so the
+        certification costs an event wait on finished work, not a drained stream.  On a large
+        shard the batches run in groups (GROUP_QUERIES): one sample launch and one merge per
+        group, one filter scan per batch (_gtau_enqueue_group).  ``outs[j]`` = optional
+        (scores, ids) output buffers of batch j (per-batch path).  This is the path
+        BaseFaissIPRetriever.batch_search, Trainer.evaluate and bench.py time."""
+        batches = list(batches)
+        if outs is None and self.ntotal >= GROUP_MIN_ROWS and self.ntotal < 0xFFFFFFFF:
+            return self._search_groups(batches, k, id_offset)
         return _pipeline(batches, lambda j, q: self._enqueue(q, k, id_offset, outs[j] if outs else None),
                          self._finish)
+
+    def _search_groups(self, batches, k: int, id_offset: int):
+        groups = [[self._queries(q) for q in g] for g in _groups(batches)]
+
+        def fin(pend):
+            res, nredo = _gtau_finish_group(pend, lambda q: self.search_device(q, k, id_offset))
+            self.group_fallbacks += nredo
+            return res
+
+        out = _pipeline(groups, lambda j, g: _gtau_enqueue_group(self, g, k, self.ntotal, id_offset,
+                                                                 lambda t: t.unsqueeze(0)), fin)
+        return [r for g in out for r in g]
 
     def search(self, q, k: int) -> Tuple[np.ndarray, np.ndarray]:
         s, i = self.search_device(q, k)
@@ -249,8 +328,26 @@ class ShardedFlatIP:
         return self._finish(self._enqueue(q, k))
 
     def search_batches(self, batches, k: int):
-        """search_device over a sequence of query batches, batch j + 1 enqueued (scan, exchange,
-        merge) before the host checks batch j's certificate (see FlatIPIndex.search_batches)."""
+        """search_device over a sequence of query batches.  Global-threshold protocol on the
+        HIP shard: the batches run in groups of GROUP_QUERIES queries (_gtau_enqueue_group: one
+        sample launch, one sample-list all-gather, one packed all-gather and one merge per
+        group; one filter scan per batch), group g + 1 enqueued before the host checks group
+        g's certificates.  Otherwise batch j + 1 is enqueued (scan, exchange, merge) before
+        the host checks batch j's certificate (see FlatIPIndex.search_batches)."""
+        batches = list(batches)
+        if self.world > 1 and self.protocol == "global_tau" and self.ntotal < 0xFFFFFFFF \
+                and isinstance(self.local, FlatIPIndex):
+            groups = [[self.local._queries(q) for q in g] for g in _groups(batches)]
+
+            def fin(pend):
+                res, nredo = _gtau_finish_group(pend, lambda q: self._finish(
+                    ("pshard", q, k) + self._per_shard_enqueue(q, k)))
+                self.fallbacks += nredo
+                return res
+
+            out = _pipeline(groups, lambda j, g: _gtau_enqueue_group(self.local, g, k, self.ntotal, self.offset,
+                                                                     self._all_gather), fin)
+            return [r for g in out for r in g]
         return _pipeline(batches, lambda j, q: self._enqueue(q, k), self._finish)
 
     def _all_gather(self, t: torch.Tensor) -> torch.Tensor:

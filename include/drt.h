@@ -99,7 +99,8 @@ int drt_topk_merge(const float* scores, const int64_t* ids, int64_t nq, int32_t 
  *   3. drt_ip_topk_dist_tau      tau[q] = r-th best over all lists
  *   4. drt_ip_topk_dist_filter   per shard: packed top-k [nq][k + 1] u64
  *        entry j < k: (desc score key << 32) | global id  (ascending = score
- *        desc, id asc; ~0 = empty), entry k: flags (bit 0 = shard overflow)
+ *        desc, id asc; ~0 = empty), entry k: (valid entries << 32) | flags
+ *        (bit 0 = shard overflow)
  *   5. caller all-gathers packed -> [world][nq][k + 1]
  *   6. drt_topk_merge_packed     exact merged top-k + status[q] (1 = not
  *        certified: fall back to the per-shard exact path for that batch)
@@ -123,12 +124,22 @@ int drt_ip_topk_dist_filter_lists(const void* Q, int64_t nq, const void* P, int6
                                   int64_t n_global, int32_t d, int32_t k, int64_t id_offset,
                                   const uint32_t* lists, int32_t nlists, float* tau_out,
                                   uint64_t* packed, void* ws, size_t ws_bytes, void* stream);
+/* The same for query rows [q0, q0 + nq) of lists gathered for a larger query set (the batched
+ * sample phase of a group of query batches): list j of this batch starts at
+ * lists + j * lists_stride (u32 elements; lists_stride >= nq * r unless nlists == 1). */
+int drt_ip_topk_dist_filter_lists_at(const void* Q, int64_t nq, const void* P, int64_t n_local,
+                                     int64_t n_global, int32_t d, int32_t k, int64_t id_offset,
+                                     const uint32_t* lists, int32_t nlists, int64_t lists_stride,
+                                     float* tau_out, uint64_t* packed, void* ws, size_t ws_bytes,
+                                     void* stream);
 int drt_topk_merge_packed(const uint64_t* parts, int64_t nq, int32_t nparts, int32_t k,
                           int64_t n_global, float* out_scores, int64_t* out_ids, int32_t* status,
                           void* stream);
-/* Test / benchmark switch of drt_topk_merge_packed's kernel: 0 automatic (rank merge, one
- * work-group per (query, part), when nparts * k * 8 B <= 64 KiB; else the per-query bitonic tree
- * merge), 1 tree merge, 2 rank merge wherever it fits.  Same results for every setting.     */
+/* Test / benchmark switch of drt_topk_merge_packed's kernel: 0 automatic (count merge, one
+ * work-group per query over the valid entries only, when nparts <= 8 and nparts * k <= 8192;
+ * else the rank merge, one work-group per (query, part), when nparts * k * 8 B <= 64 KiB; else the
+ * per-query bitonic tree merge), 1 tree merge, 2 rank merge wherever it fits, 3 count merge
+ * wherever it fits.  Same results for every setting.                                         */
 int drt_topk_merge_packed_variant(int32_t v);
 
 /* Dense score matrix C[m, n] = A[m, d] . B[n, d]^T with fp32 accumulation

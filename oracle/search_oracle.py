@@ -235,7 +235,8 @@ def dist_tau(lists, k):
 
 def dist_filter(q, p_local, n_global, k, id_offset, tau):
     """Packed uint64 [nq, k + 1]: sorted (desc_key << 32 | global id) of rows with score >= tau;
-    entry k = flags (bit 0: more than cap candidates, i.e. the GPU buffer overflowed)."""
+    entry k = (valid entries << 32) | flags (bit 0: more than cap candidates, i.e. the GPU buffer
+    overflowed)."""
     plan = dist_plan(p_local.shape[0], n_global, k)
     nq = np.asarray(q).shape[0]
     out = np.full((nq, k + 1), PAD_KEY64, dtype=np.uint64)
@@ -250,6 +251,7 @@ def dist_filter(q, p_local, n_global, k, id_offset, tau):
         keys = (desc_key(s[i, sel]).astype(np.uint64) << np.uint64(32)) | (sel + id_offset).astype(np.uint64)
         keys = np.sort(keys)[:k]
         out[i, :len(keys)] = keys
+        out[i, k] |= np.uint64(len(keys)) << np.uint64(32)
     return out
 
 

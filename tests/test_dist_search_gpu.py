@@ -131,8 +131,9 @@ def test_dist_shape_errors(dev):
                                               (5, 9, 10, 0.3), (9, 4, 1000, 0.4), (16, 3, 1000, 0.2),
                                               (8, 2, 1000, 0.05), (1, 6, 64, 0.7)])
 def test_merge_packed_variants_vs_oracle(dev, nparts, nq, k, fill):
-    """drt_topk_merge_packed's rank merge (one work-group per (query, part)) and tree merge against
-    the oracle on random packed lists: unique keys, ragged fills, empty parts, overflow flags."""
+    """drt_topk_merge_packed's count merge (one work-group per query, valid entries only), rank merge
+    (one work-group per (query, part)) and tree merge against the oracle on random packed lists:
+    unique keys, ragged fills, empty parts, overflow flags."""
     import torch
     from denseretrievaltoolkits_amd import _native, kernels
     lib = _native.load()
@@ -146,10 +147,10 @@ def test_merge_packed_variants_vs_oracle(dev, nparts, nq, k, fill):
         for l in range(nparts):
             cnt = int(rng.binomial(k, fill)) if fill < 1.0 else k
             parts[l, q, :cnt] = np.sort(keys[l * k: l * k + cnt])
-            parts[l, q, k] = np.uint64(rng.random() < 0.1)            # overflow flag
+            parts[l, q, k] = (np.uint64(cnt) << np.uint64(32)) | np.uint64(rng.random() < 0.1)  # count | overflow
     es, ei, est = orc.merge_packed(parts, k, n_global)
     pt = torch.from_numpy(parts.view(np.int64)).to(dev)
-    for v in (0, 1, 2):
+    for v in (0, 1, 2, 3):
         _native.check(lib.drt_topk_merge_packed_variant(v), "variant")
         s, i, st = kernels.merge_packed(pt, k, n_global)
         np.testing.assert_array_equal(i.cpu().numpy(), ei, err_msg=f"variant {v}")

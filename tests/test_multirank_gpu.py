@@ -128,13 +128,27 @@ def _w_sharded(rank, world, dev, case):
             np.testing.assert_array_equal(i, gids)
             np.testing.assert_array_equal(s, gscores)
         out[proto] = idx.fallbacks
+        # batched search: ragged batches of 5 in groups of <= 16 queries (3 groups of up to 3 batches)
+        from denseretrievaltoolkits_amd import search as srch
+        saved = srch.GROUP_QUERIES
+        srch.GROUP_QUERIES = 16
+        try:
+            fb0 = idx.fallbacks
+            qd = to_dev_bf16(q, dev)
+            res = idx.search_batches([qd[a: a + 5] for a in range(0, q.shape[0], 5)], k)
+            torch.cuda.synchronize()
+        finally:
+            srch.GROUP_QUERIES = saved
+        np.testing.assert_array_equal(torch.cat([r[1] for r in res]).cpu().numpy(), ei)
+        np.testing.assert_array_equal(torch.cat([r[0] for r in res]).cpu().numpy(), es)
+        out[proto + "_batched"] = idx.fallbacks - fb0
     return out
 
 
 @pytest.mark.parametrize("world", [2, 3])
 def test_sharded_search_multiprocess_integer(world):
     res = _spawn(_w_sharded, world, "int")
-    assert all(v["global_tau"] == 0 for v in res.values()), res
+    assert all(v["global_tau"] == 0 and v["global_tau_batched"] == 0 for v in res.values()), res
 
 
 def test_sharded_search_multiprocess_reference_golden():
@@ -144,7 +158,8 @@ def test_sharded_search_multiprocess_reference_golden():
 
 def test_sharded_search_multiprocess_fallback():
     res = _spawn(_w_sharded, 2, "ties")
-    assert all(v["global_tau"] == 1 for v in res.values()), res
+    # one batch of 9 queries; batched: batches of 5 + 4 in one group, both redone exactly
+    assert all(v["global_tau"] == 1 and v["global_tau_batched"] == 2 for v in res.values()), res
 
 
 # ---------------------------------------------------------------------------

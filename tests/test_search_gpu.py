@@ -76,6 +76,40 @@ def test_filter_scan_variants_bit_exact(dev, variant, nq, n, d, k):
     np.testing.assert_array_equal(gs, es)
 
 
+@pytest.mark.parametrize("case", ["int", "gauss", "ties"])
+def test_flat_index_search_batches_grouped(dev, case, monkeypatch):
+    """FlatIPIndex.search_batches in groups (one sample launch + one merge per group, one filter
+    scan per batch): ragged batches over several groups vs the oracle; the all-ties corpus makes
+    every batch uncertified, so each is redone by the exact per-batch path."""
+    import torch
+    from denseretrievaltoolkits_amd import search as srch
+    monkeypatch.setattr(srch, "GROUP_MIN_ROWS", 0)
+    monkeypatch.setattr(srch, "GROUP_QUERIES", 64)
+    rng = np.random.default_rng(77)
+    if case == "int":
+        q, p, k = int_bf16(rng, (150, 768), -4, 4), int_bf16(rng, (120001, 768), -4, 4), 1000
+    elif case == "gauss":
+        q, p, k = gauss_bf16(rng, (100, 768)), gauss_bf16(rng, (200000, 768)), 1000
+    else:
+        q, p, k = int_bf16(rng, (10, 256), -3, 3), np.repeat(int_bf16(rng, (1, 256), -3, 3), 50000, axis=0), 100
+    idx = srch.FlatIPIndex.from_rows(to_dev_bf16(p, dev))
+    qd = to_dev_bf16(q, dev)
+    step = 30 if case != "ties" else 4
+    res = idx.search_batches([qd[a: a + step] for a in range(0, q.shape[0], step)], k)
+    torch.cuda.synchronize()
+    gs = torch.cat([r[0] for r in res]).cpu().numpy()
+    gi = torch.cat([r[1] for r in res]).cpu().numpy()
+    es, ei = orc.ip_topk(q, p, k)
+    if case == "gauss":
+        np.testing.assert_allclose(gs, es, atol=SCORE_ATOL, rtol=0)
+        assert (gi == ei).mean() > 0.99
+        assert idx.group_fallbacks == 0
+    else:
+        np.testing.assert_array_equal(gi, ei)
+        np.testing.assert_array_equal(gs, es)
+        assert idx.group_fallbacks == (0 if case == "int" else 3)
+
+
 def test_ip_topk_gaussian_tolerance(dev):
     rng = np.random.default_rng(7)
     nq, n, d, k = 128, 120000, 768, 1000

@@ -28,6 +28,7 @@ def main():
     ap.add_argument("--steps", type=int, default=30)
     ap.add_argument("--check", action="store_true", help="verify global_tau == per_shard results")
     ap.add_argument("--graph", action="store_true", help="also time the step replayed from a hipGraph")
+    ap.add_argument("--group", type=int, default=16, help="batches per group (grouped protocol)")
     a = ap.parse_args()
     import torch
     import bench
@@ -117,6 +118,56 @@ def main():
         S[R], I[R] = s, i
         kernels.topk_merge(S, I, k)
 
+    # grouped (search.py _gtau_enqueue_group): one sample launch and one merge per group of
+    # G batches, one filter scan per batch
+    G = a.group
+    groups = [list(range(s0, min(s0 + G, a.steps))) for s0 in range(0, a.steps, G)]
+    glists = [torch.cat([lists[j] for j in g], 1).contiguous() for g in groups]
+    gparts = [torch.cat([parts[j] for j in g], 1).contiguous() for g in groups]
+    gq = [torch.cat([queries[j] for j in g]).contiguous() for g in groups]
+
+    def gt_grouped(gi):
+        best = kernels.dist_sample(gq[gi], own, N, k)
+        glists[gi][R].copy_(best)
+        for b, j in enumerate(groups[gi]):
+            kernels.dist_filter_lists_into(queries[j], own, N, k, lo, glists[gi], b * qb,
+                                           gparts[gi][R, b * qb:(b + 1) * qb])
+        kernels.merge_packed(gparts[gi], k, N)
+
+    def timed_groups(label):
+        gt_grouped(0)
+        torch.cuda.synchronize()
+        for f in fams.values():
+            lib.drt_profile_enable(f, 1)
+        t0 = time.perf_counter()
+        for gi in range(len(groups)):
+            gt_grouped(gi)
+        torch.cuda.synchronize()
+        el = time.perf_counter() - t0
+        res = {"ms_per_step": round(el / a.steps * 1e3, 4), "group_batches": G}
+        for name, f in fams.items():
+            lib.drt_profile_enable(f, 0)
+            tot = _native.ctypes.c_double(0.0)
+            cnt = _native.c_i64(0)
+            lib.drt_profile_read(f, _native.ctypes.byref(tot), _native.ctypes.byref(cnt))
+            if cnt.value:
+                res[f"{name}_ms"] = round(tot.value / cnt.value, 4)
+                res[f"{name}_launches_per_step"] = round(cnt.value / a.steps, 2)
+        res["qps_if_comm_free"] = round(qb / (el / a.steps), 1)
+        out[label] = res
+
+    if a.check:
+        bad = 0
+        for gi, g in enumerate(groups):
+            gt_grouped(gi)
+            s1, i1, st = kernels.merge_packed(gparts[gi], k, N)
+            for b, j in enumerate(g):
+                s2, i2 = kernels.topk_merge(ps[j][0], ps[j][1], k)
+                sl = slice(b * qb, (b + 1) * qb)
+                bad += int((st[sl] != 0).sum()) + int((i1[sl] != i2).any(dim=1).sum())
+        out["check_grouped_mismatched_queries"] = bad
+
+    timed_groups("global_tau_grouped")
     timed(gt, "global_tau")
     timed(gt_unfused, "global_tau_unfused")
     timed(psh, "per_shard")
