@@ -314,7 +314,7 @@ def main():
                           "filter scan per batch)" if use_global else ")")),
             },
             "roofline": {
-                "kernel": "ip_scan16r_kernel<768,false> (csrc/search.hip)",
+                "kernel": "ip_scan16r_kernel<768,false,true> (csrc/search.hip)",
                 "bound": "hbm",
                 "achieved": round(achieved, 1),
                 "peak": HBM_PEAK_GBS,

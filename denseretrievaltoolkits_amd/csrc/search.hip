@@ -32,6 +32,10 @@ constexpr int kTileRows = 32;   // corpus rows per MFMA tile (32x32x16)
 constexpr int kScanThreads = 256;  // 4 waves, one per SIMD
 constexpr int kQueriesPerWG = 128;  // 4 waves x 32 query columns
 constexpr int kHitCap = 1024;       // LDS hit list entries per work-group
+// Per-query hit counters sit one 128-B line apart (index q * kCntStride): every work-group's
+// flush increments the counters of all 128 queries of its block, and packed into 4 lines they
+// serialised in L2 (r02 A/B: see DESIGN.md §3).
+constexpr int kCntStride = 32;
 
 enum { SCAN_FILTER = 0, SCAN_DENSE = 1 };
 
@@ -45,7 +49,7 @@ struct ScanArgs {
   int64_t nrows;
   int64_t rstride;
   const float* tau;   // FILTER: [nq] thresholds (NaN = inactive query)
-  uint32_t* counts;   // FILTER: [nq] hit counters (zeroed by the caller)
+  uint32_t* counts;   // FILTER: hit counter of query q at counts[q * kCntStride] (zeroed by the caller)
   void* out;          // FILTER: u64 [nq][cap] keys; DENSE: u32 [nq][cap] desc keys
   int64_t cap;
   int64_t exp_hits;   // FILTER: expected hits per query (0: cap / 4); picks the append flavour
@@ -147,7 +151,7 @@ __device__ __forceinline__ void push_hit(const ScanArgs& a, int q_local,
     hk[p] = key;
     hq[p] = (uint16_t)q_local;
   } else {
-    const uint32_t g = atomicAdd(a.counts + q, 1u);
+    const uint32_t g = atomicAdd(a.counts + q * kCntStride, 1u);
     if (g < (uint64_t)a.cap) ((uint64_t*)a.out)[q * a.cap + g] = key;
   }
 }
@@ -169,7 +173,7 @@ __device__ __forceinline__ void flush_hits_agg(const ScanArgs& a, int64_t qbase,
   lds_barrier();
   for (int q = threadIdx.x; q < kQueriesPerWG; q += NT) {
     const uint32_t c = qcnt[q];
-    qoff[q] = (c && qbase + q < a.nq) ? atomicAdd(a.counts + qbase + q, c) : 0u;
+    qoff[q] = (c && qbase + q < a.nq) ? atomicAdd(a.counts + (qbase + q) * kCntStride, c) : 0u;
   }
   lds_barrier();
 #pragma unroll
@@ -189,7 +193,7 @@ __device__ __forceinline__ void flush_hits(const ScanArgs& a, int64_t qbase, uin
   n = n < (uint32_t)kHitCap ? n : (uint32_t)kHitCap;
   for (uint32_t i = threadIdx.x; i < n; i += NT) {
     const int64_t q = qbase + hq[i];
-    const uint32_t g = atomicAdd(a.counts + q, 1u);
+    const uint32_t g = atomicAdd(a.counts + q * kCntStride, 1u);
     if (g < (uint64_t)a.cap) ((uint64_t*)a.out)[q * a.cap + g] = hk[i];
   }
 }
@@ -558,7 +562,7 @@ __global__ __launch_bounds__(NW * 64, 1) void ip_scan16_kernel(ScanArgs a) {
               hk[base] = key;
               hq[base] = (uint16_t)qloc[b];
             } else {
-              const uint32_t g = atomicAdd(a.counts + qg[b], 1u);
+              const uint32_t g = atomicAdd(a.counts + qg[b] * kCntStride, 1u);
               if (g < (uint64_t)a.cap) ((uint64_t*)a.out)[qg[b] * a.cap + g] = key;
             }
             ++base;
@@ -779,7 +783,7 @@ __global__ __launch_bounds__(512, 1) void ip_scan16r_kernel(ScanArgs a) {
           hk[base] = key;
           hq[base] = (uint16_t)qloc;
         } else {
-          const uint32_t g = atomicAdd(a.counts + qg, 1u);
+          const uint32_t g = atomicAdd(a.counts + qg * kCntStride, 1u);
           if (g < (uint64_t)a.cap) ((uint64_t*)a.out)[qg * a.cap + g] = key;
         }
         ++base;
@@ -1023,7 +1027,7 @@ __global__ __launch_bounds__(kSelThreads) void select_kernel(SelectArgs a) {
   const int64_t q = blockIdx.x;
   int64_t c_raw, c;
   if (INPUT == SEL_KEYS64) {
-    c_raw = a.counts[q];
+    c_raw = a.counts[q * kCntStride];
     c = c_raw < a.cap ? c_raw : a.cap;
   } else {
     c_raw = a.n_in;
@@ -1534,7 +1538,7 @@ __global__ __launch_bounds__(kKthThreads) void kth_final_kernel(const uint32_t* 
                                                                 uint32_t* best, uint32_t* zero) {
   __shared__ uint32_t buf[kKthChunk];
   const int64_t q = blockIdx.x;
-  if (zero && threadIdx.x == 0) zero[q] = 0;
+  if (zero && threadIdx.x == 0) zero[q * kCntStride] = 0;
   const int tot = nlists * r;
   {
     uint32_t tmp[kKthChunk / kKthThreads];
@@ -2112,7 +2116,7 @@ static TopkPlan make_plan(int64_t nq, int64_t n, int64_t k) {
   p.off_tau = o;
   o = align_up(o + p.nq_pad * 4, 256);
   p.off_cnt = o;
-  o = align_up(o + p.nq_pad * 4, 256);
+  o = align_up(o + p.nq_pad * 4 * kCntStride, 256);
   p.off_keys = o;
   if (p.sample) o = align_up(o + (size_t)p.nq_pad * p.cap * 8, 256);
   else o = align_up(o + (size_t)p.nq_pad * p.cap * 4, 256);
@@ -2156,7 +2160,7 @@ static TopkPlan make_dist_plan(int64_t nq, int64_t n_local, int64_t n_global, in
   p.off_tau = o;
   o = align_up(o + p.nq_pad * 4, 256);
   p.off_cnt = o;
-  o = align_up(o + p.nq_pad * 4, 256);
+  o = align_up(o + p.nq_pad * 4 * kCntStride, 256);
   p.off_keys = o;
   o = align_up(o + (size_t)p.nq_pad * p.cap * 8, 256);
   p.off_sample = o;
@@ -2238,8 +2242,10 @@ static int launch_scan_d(const ScanArgs& a, int mode, hipStream_t s) {
       // ip_scan16r_kernel: fragment reads of the next tile rolled into this tile's MFMAs, non-temporal
       // corpus loads, s_setprio 1 for waves 4-7 (r02 A/B, tools/scan_ab.py, profiles/r02e_scan_roll.log:
       // 2.59-2.62 vs 2.93 ms per launch for the round-1 loop with the same options, ids identical)
+      // sparse flavour: per-hit LDS append, aggregated flush (one global atomic per (work-group,
+      // query); r02 A/B, profiles/r02g_scan_flush.log: -3 % per launch vs the per-hit flush)
       if (dense_hits) hipLaunchKernelGGL((ip_scan16r_kernel<D, true>), grid, dim3(512), 0, s, a);
-      else hipLaunchKernelGGL((ip_scan16r_kernel<D, false>), grid, dim3(512), 0, s, a);
+      else hipLaunchKernelGGL((ip_scan16r_kernel<D, false, true>), grid, dim3(512), 0, s, a);
     }
     else
       hipLaunchKernelGGL((ip_scan16_kernel<D, SCAN_DENSE, 0, 8>), grid, dim3(512), 0, s, a);
@@ -2644,7 +2650,7 @@ int drt_ip_topk_dist_filter(const void* Q, int64_t nq, const void* P, int64_t n_
     return launch_select(sa, SEL_DENSE32, SEL_TOPK, s);
   }
   DRT_REQUIRE(P != nullptr);
-  DRT_CHECK_HIP(hipMemsetAsync(cnt, 0, p.nq_pad * 4, s));
+  DRT_CHECK_HIP(hipMemsetAsync(cnt, 0, p.nq_pad * 4 * kCntStride, s));
   ScanArgs a{};
   a.Q = (const __bf16*)Q;
   a.nq = nq;
