@@ -26,6 +26,7 @@ c_i64 = ctypes.c_int64
 c_sz = ctypes.c_size_t
 c_vp = ctypes.c_void_p
 c_f32 = ctypes.c_float
+c_u64 = ctypes.c_uint64
 
 # (name, restype, argtypes) — one line per entry point of include/drt.h
 _SIGNATURES = [
@@ -57,6 +58,10 @@ _SIGNATURES = [
     ("drt_layernorm_f32_bf16", c_i32, [c_vp, c_i64, c_i32, c_vp, c_vp, c_f32, c_vp, c_vp]),
     ("drt_attention_fwd_lse_bf16", c_i32, [c_vp, c_vp, c_vp, c_vp, c_i64, c_i64, c_i32, c_i32, c_f32, c_vp]),
     ("drt_layernorm_bwd_workspace", c_sz, [c_i64, c_i32]),
+    ("drt_layernorm_bwd_drop_bf16", c_i32, [c_vp, c_vp, c_vp, c_f32, c_i64, c_i32, c_vp, c_vp, c_vp, c_f32, c_u64,
+                                            c_u64, c_vp, c_vp, c_vp, c_sz, c_vp]),
+    ("drt_linear_bf16_ex", c_i32, [c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_i64, c_i64, c_i64, c_i32, c_f32, c_u64,
+                                   c_u64, c_vp, c_sz, c_vp]),
     ("drt_layernorm_bwd_bf16", c_i32, [c_vp, c_vp, c_vp, c_f32, c_i64, c_i32, c_vp, c_vp, c_vp, c_vp, c_vp, c_sz,
                                        c_vp]),
     ("drt_colsum_workspace", c_sz, [c_i64, c_i64]),

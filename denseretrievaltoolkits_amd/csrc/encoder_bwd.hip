@@ -30,7 +30,8 @@ constexpr int kLnBwdBlocks = 1024;   // grid of the row pass = rows of the param
 template <int EPL>
 __global__ __launch_bounds__(256) void layernorm_bwd_kernel(const __bf16* dy, const __bf16* x, const float* gamma,
                                                             float eps, int64_t M, int H, const __bf16* dres,
-                                                            __bf16* dx, float* part) {
+                                                            __bf16* dx, float* part, __bf16* dxd, float drop_p,
+                                                            uint64_t seed, uint64_t site) {
   __shared__ float red[4][2][EPL * 64];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   float dg[EPL], db[EPL], gm[EPL];
@@ -87,6 +88,17 @@ __global__ __launch_bounds__(256) void layernorm_bwd_kernel(const __bf16* dy, co
         o[u] = (__bf16)(rstd * (gv[e] - mg - xv[e] * mgx) + (dres ? (float)r[u] : 0.f));
       }
       *(bf16x4*)(dx + t * H + c) = o;
+      if (dxd) {   // dropout of the rounded dx (what drt_dropout_add_bf16 would compute from it)
+        const uint32_t thr = drop_threshold(drop_p);
+        const float inv = 1.0f / (1.0f - drop_p);
+        bf16x4 od;
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          const bool keep = drop_hash24(seed, site, (uint64_t)(t * H + c + u)) >= thr;
+          od[u] = (__bf16)(keep ? (float)o[u] * inv : 0.0f);
+        }
+        *(bf16x4*)(dxd + t * H + c) = od;
+      }
     }
   }
   // fixed-order block reduction of the 4 waves' parameter-gradient sums
@@ -598,16 +610,31 @@ size_t drt_layernorm_bwd_workspace(int64_t M, int32_t H) {
 
 // dx = LN backward of dy through out = LN(x) (gamma; x = the bf16 pre-LN sums the forward
 // stored) + dres (residual gradient, may be NULL); dgamma / dbeta fp32 [H] (deterministic).
+int drt_layernorm_bwd_drop_bf16(const void* dy, const void* x, const float* gamma, float eps, int64_t M, int32_t H,
+                                const void* dres, void* dx, void* dx_drop, float drop_p, uint64_t seed, uint64_t site,
+                                float* dgamma, float* dbeta, void* ws, size_t ws_bytes, void* stream);
+
 int drt_layernorm_bwd_bf16(const void* dy, const void* x, const float* gamma, float eps, int64_t M, int32_t H,
                            const void* dres, void* dx, float* dgamma, float* dbeta, void* ws, size_t ws_bytes,
                            void* stream) {
+  return drt_layernorm_bwd_drop_bf16(dy, x, gamma, eps, M, H, dres, dx, nullptr, 0.f, 0, 0, dgamma, dbeta, ws,
+                                     ws_bytes, stream);
+}
+
+// The same, also writing dx_drop = dropout(dx) with drt_dropout_add_bf16's mask of (drop_p, seed, site)
+// (the gradient entering the linear whose output HF dropped before this LayerNorm's residual add).
+int drt_layernorm_bwd_drop_bf16(const void* dy, const void* x, const float* gamma, float eps, int64_t M, int32_t H,
+                                const void* dres, void* dx, void* dx_drop, float drop_p, uint64_t seed, uint64_t site,
+                                float* dgamma, float* dbeta, void* ws, size_t ws_bytes, void* stream) {
   DRT_REQUIRE(M > 0 && H > 0 && H % 256 == 0 && H <= 1024);
+  DRT_REQUIRE(!dx_drop || (drop_p >= 0.f && drop_p < 1.f));
   DRT_REQUIRE(dy && x && gamma && dx && dgamma && dbeta && ws && ws_bytes >= drt_layernorm_bwd_workspace(M, H));
   hipStream_t s = (hipStream_t)stream;
   float* part = (float*)ws;   // [2 * blocks][H]: dgamma rows then dbeta rows
   const dim3 grid(kLnBwdBlocks);
 #define LNB(E) hipLaunchKernelGGL(layernorm_bwd_kernel<E>, grid, dim3(256), 0, s, (const __bf16*)dy, (const __bf16*)x, \
-                                  gamma, eps, M, (int)H, (const __bf16*)dres, (__bf16*)dx, part)
+                                  gamma, eps, M, (int)H, (const __bf16*)dres, (__bf16*)dx, part, (__bf16*)dx_drop, \
+                                  drop_p, seed, site)
   switch (H / 64) {
     case 4: LNB(4); break;
     case 8: LNB(8); break;

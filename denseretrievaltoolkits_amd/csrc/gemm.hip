@@ -35,6 +35,9 @@ struct GemmArgs {
   int order;                // tile order within an XCD's range (tile_order)
   int64_t kchunk;           // split-K (128^2 kernel, PART): k per split; ws [splits][m][n] fp32
   float* ws;
+  void* C2;                 // EPI_PRE: bf16 [m][ldc] pre-activation (bias added, before GELU)
+  float drop_p;             // EPI_DROP: dropout probability, hash seed and site (drt_common.h)
+  uint64_t seed, site;
 };
 static unsigned long long* g_gemm_dbg = nullptr;
 
@@ -92,7 +95,40 @@ __device__ __forceinline__ float gelu_fast(float x) {
   return 0.5f * x * (1.0f + erf_v);
 }
 
-enum { EPI_NONE = 0, EPI_BIAS = 1, EPI_GELU = 2, EPI_RESID = 4 };
+// EPI_DGELU: multiply by GELU'(R) (the dgrad of a GELU input: R = the bf16 pre-activation);
+// EPI_PRE: also store the pre-activation to C2 (the training forward keeps it for the backward);
+// EPI_DROP: dropout (counter hash of the flat output index, the mask drt_dropout_add_bf16 draws)
+// applied after bias / GELU, before the residual.
+enum { EPI_NONE = 0, EPI_BIAS = 1, EPI_GELU = 2, EPI_RESID = 4, EPI_DGELU = 8, EPI_PRE = 16, EPI_DROP = 32 };
+constexpr int EPI_AUX = EPI_RESID | EPI_DGELU;   // epilogues that read R
+
+// d/dx [x Phi(x)] = Phi(x) + x phi(x), erf by Abramowitz & Stegun 7.1.26 as gelu_fast
+// (phi shares gelu_fast's exp(-x^2 / 2)).
+__device__ __forceinline__ float gelu_grad(float x) {
+  const float z = fabsf(x) * 0.70710678118654752f;
+  const float t = __builtin_amdgcn_rcpf(fmaf(0.3275911f, z, 1.0f));
+  float p = fmaf(1.061405429f, t, -1.453152027f);
+  p = fmaf(p, t, 1.421413741f);
+  p = fmaf(p, t, -0.284496736f);
+  p = fmaf(p, t, 0.254829592f);
+  p *= t;
+  const float e = __builtin_amdgcn_exp2f(-z * z * 1.4426950408889634f);
+  const float erf_abs = fmaf(-p, e, 1.0f);
+  const float erf_v = x < 0.f ? -erf_abs : erf_abs;
+  return fmaf(x * 0.39894228040143268f, e, 0.5f * (1.0f + erf_v));
+}
+
+// The part of the epilogue after bias / GELU, element (row, col): dropout, residual, GELU'.
+template <int EPI>
+__device__ __forceinline__ float epi_post(const GemmArgs& a, float v, int64_t row, int64_t col, float aux) {
+  if (EPI & EPI_DROP) {
+    const bool keep = drop_hash24(a.seed, a.site, (uint64_t)(row * a.ldc + col)) >= drop_threshold(a.drop_p);
+    v = keep ? v * (1.0f / (1.0f - a.drop_p)) : 0.0f;
+  }
+  if (EPI & EPI_RESID) v += aux;
+  if (EPI & EPI_DGELU) v *= gelu_grad(aux);
+  return v;
+}
 
 static int g_gemm_variant = 0;
 static int64_t g_large_min_tiles = 128;   // 256^2 kernel from this many 256^2 tiles up (tools/qsweep.py: 128 beats 512 by 16-22 % on 4k-16k-token batches)
@@ -197,8 +233,9 @@ __global__ __launch_bounds__(kGemmThreads, 2) void gemm_nt_kernel(GemmArgs a) {
         const int64_t row = m0 + wm * 64 + i * 32 + (e & 3) + 8 * (e >> 2) + 4 * h;
         if (row >= a.m) continue;
         float v = acc[i][j][e] * a.alpha + bv;
+        if (EPI & EPI_PRE) ((__bf16*)a.C2)[row * a.ldc + col] = (__bf16)v;
         if (EPI & EPI_GELU) v = gelu_erf(v);
-        if (EPI & EPI_RESID) v += (float)a.R[row * a.ldr + col];
+        v = epi_post<EPI>(a, v, row, col, (EPI & EPI_AUX) ? (float)a.R[row * a.ldr + col] : 0.f);
         if (OUT_BF16) ((__bf16*)a.C)[row * a.ldc + col] = (__bf16)v;
         else ((float*)a.C)[row * a.ldc + col] = v;
       }
@@ -211,7 +248,7 @@ __global__ __launch_bounds__(kGemmThreads, 2) void gemm_nt_kernel(GemmArgs a) {
 template <bool OUT_BF16, int EPI>
 __global__ __launch_bounds__(256) void splitk_epi_kernel(GemmArgs a, int splits) {
   const int64_t mn = a.m * a.n;
-  const bool v4 = (a.n % 4 == 0) && (a.ldc % 4 == 0) && (!(EPI & EPI_RESID) || a.ldr % 4 == 0);
+  const bool v4 = (a.n % 4 == 0) && (a.ldc % 4 == 0) && (!(EPI & EPI_AUX) || a.ldr % 4 == 0);
   const int64_t units = v4 ? mn / 4 : mn;
   for (int64_t u = (int64_t)blockIdx.x * 256 + threadIdx.x; u < units; u += (int64_t)gridDim.x * 256) {
     const int64_t e0 = v4 ? u * 4 : u;
@@ -234,8 +271,9 @@ __global__ __launch_bounds__(256) void splitk_epi_kernel(GemmArgs a, int splits)
     for (int q = 0; q < w; ++q) {
       float x = v[q] * a.alpha;
       if (EPI & EPI_BIAS) x += a.bias[col + q];
+      if (EPI & EPI_PRE) ((__bf16*)a.C2)[row * a.ldc + col + q] = (__bf16)x;
       if (EPI & EPI_GELU) x = gelu_erf(x);
-      if (EPI & EPI_RESID) x += (float)a.R[row * a.ldr + col + q];
+      x = epi_post<EPI>(a, x, row, col + q, (EPI & EPI_AUX) ? (float)a.R[row * a.ldr + col + q] : 0.f);
       if (OUT_BF16) ((__bf16*)a.C)[row * a.ldc + col + q] = (__bf16)x;
       else ((float*)a.C)[row * a.ldc + col + q] = x;
     }
@@ -681,51 +719,22 @@ __device__ __forceinline__ void pp_epilogue(const GemmArgs& a, f32x4 (&acc)[8][4
                                             int wn, int fr, int fc) {
   // Epilogue. acc[i][j][u]: token row m0 + grp*128 + i*16 + fr,
   //                         output col n0 + wn*64 + j*16 + 4*fc + u.
-  const bool full_n = (n0 + kL <= a.n) && (a.ldc % 4 == 0) && (!(EPI & EPI_RESID) || a.ldr % 4 == 0);
 #pragma unroll
   for (int j = 0; j < 4; ++j) {
     const int64_t col = n0 + wn * 64 + j * 16 + 4 * fc;
-    f32x4 bv = {0.f, 0.f, 0.f, 0.f};
-    if (EPI & EPI_BIAS) {
-      if (full_n) bv = *(const f32x4*)(a.bias + col);
-      else
-#pragma unroll
-        for (int u = 0; u < 4; ++u) bv[u] = col + u < a.n ? a.bias[col + u] : 0.f;
-    }
 #pragma unroll
     for (int i = 0; i < 8; ++i) {
       const int64_t row = m0 + grp * 128 + i * 16 + fr;
       if (row >= a.m) continue;
-      f32x4 v;
 #pragma unroll
       for (int u = 0; u < 4; ++u) {
-        float x = acc[i][j][u] * a.alpha + bv[u];
+        if (col + u >= a.n) continue;
+        float x = acc[i][j][u] * a.alpha + ((EPI & EPI_BIAS) ? a.bias[col + u] : 0.f);
+        if (EPI & EPI_PRE) ((__bf16*)a.C2)[row * a.ldc + col + u] = (__bf16)x;
         if (EPI & EPI_GELU) x = gelu_erf(x);
-        v[u] = x;
-      }
-      if (full_n) {
-        if (EPI & EPI_RESID) {
-          const bf16x4 rv = *(const bf16x4*)(a.R + row * a.ldr + col);
-#pragma unroll
-          for (int u = 0; u < 4; ++u) v[u] += (float)rv[u];
-        }
-        if (OUT_BF16) {
-          bf16x4 o;
-#pragma unroll
-          for (int u = 0; u < 4; ++u) o[u] = (__bf16)v[u];
-          *(bf16x4*)((__bf16*)a.C + row * a.ldc + col) = o;
-        } else {
-          *(f32x4*)((float*)a.C + row * a.ldc + col) = v;
-        }
-      } else {
-#pragma unroll
-        for (int u = 0; u < 4; ++u) {
-          if (col + u >= a.n) continue;
-          float x = v[u];
-          if (EPI & EPI_RESID) x += (float)a.R[row * a.ldr + col + u];
-          if (OUT_BF16) ((__bf16*)a.C)[row * a.ldc + col + u] = (__bf16)x;
-          else ((float*)a.C)[row * a.ldc + col + u] = x;
-        }
+        x = epi_post<EPI>(a, x, row, col + u, (EPI & EPI_AUX) ? (float)a.R[row * a.ldr + col + u] : 0.f);
+        if (OUT_BF16) ((__bf16*)a.C)[row * a.ldc + col + u] = (__bf16)x;
+        else ((float*)a.C)[row * a.ldc + col + u] = x;
       }
     }
   }
@@ -760,32 +769,38 @@ __device__ __forceinline__ void pp_epilogue_lds(const GemmArgs& a, f32x4 (&acc)[
     bv[j] = f32x4{0.f, 0.f, 0.f, 0.f};
     if (EPI & EPI_BIAS) bv[j] = *(const f32x4*)(a.bias + colw + j * 16 + 4 * fc);
   }
-  if (OUT_BF16 && !(EPI & EPI_RESID)) {
-    // [128 rows][8 x 16 B], chunk ^= row & 7
+  if (OUT_BF16 && !(EPI & (EPI_AUX | EPI_DROP))) {
+    // [128 rows][8 x 16 B], chunk ^= row & 7; EPI_PRE: a first pass stores the pre-activation
 #pragma unroll
-    for (int i = 0; i < 8; ++i) {
-      const int r = i * 16 + fr;
+    for (int pass = (EPI & EPI_PRE) ? 0 : 1; pass < 2; ++pass) {
+      const bool act = pass == 1;
 #pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        bf16x4 o;
+      for (int i = 0; i < 8; ++i) {
+        const int r = i * 16 + fr;
 #pragma unroll
-        for (int u = 0; u < 4; ++u) {
-          float x = acc[i][j][u] * a.alpha + bv[j][u];
-          if (EPI & EPI_GELU) x = gelu_fast(x);
-          o[u] = (__bf16)x;
+        for (int j = 0; j < 4; ++j) {
+          bf16x4 o;
+#pragma unroll
+          for (int u = 0; u < 4; ++u) {
+            float x = acc[i][j][u] * a.alpha + bv[j][u];
+            if ((EPI & EPI_GELU) && act) x = gelu_fast(x);
+            o[u] = (__bf16)x;
+          }
+          const int chunk = (2 * j + (fc >> 1)) ^ (r & 7);
+          *(bf16x4*)(lds_wave + r * 128 + chunk * 16 + (fc & 1) * 8) = o;
         }
-        const int chunk = (2 * j + (fc >> 1)) ^ (r & 7);
-        *(bf16x4*)(lds_wave + r * 128 + chunk * 16 + (fc & 1) * 8) = o;
       }
-    }
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    const int c = lane & 7;
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      const int c = lane & 7;
+      __bf16* dst = act ? (__bf16*)a.C : (__bf16*)a.C2;
 #pragma unroll
-    for (int p = 0; p < 16; ++p) {
-      const int r = p * 8 + (lane >> 3);
-      const bf16x8 v = *(const bf16x8*)(lds_wave + r * 128 + ((c ^ (r & 7)) << 4));
-      const int64_t row = m0 + grp * 128 + r;
-      if (row < a.m) *(bf16x8*)((__bf16*)a.C + row * a.ldc + colw + c * 8) = v;
+      for (int p = 0; p < 16; ++p) {
+        const int r = p * 8 + (lane >> 3);
+        const bf16x8 v = *(const bf16x8*)(lds_wave + r * 128 + ((c ^ (r & 7)) << 4));
+        const int64_t row = m0 + grp * 128 + r;
+        if (row < a.m) *(bf16x8*)(dst + row * a.ldc + colw + c * 8) = v;
+      }
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     }
   } else {
     // two passes of 64 rows: [64 rows][16 x 16 B] fp32, chunk ^= row & 7.  Residual rows
@@ -794,7 +809,7 @@ __device__ __forceinline__ void pp_epilogue_lds(const GemmArgs& a, f32x4 (&acc)[
     // rounded once, at the store (8-B pieces, 128-B row segments).
     const int c = lane & 15;
     bf16x4 rv1[16];
-    if (EPI & EPI_RESID) {
+    if (EPI & EPI_AUX) {
       if (!PRE) load_resid_half(a, m0, n0, grp, wn, 0, lane, rv0);
       load_resid_half(a, m0, n0, grp, wn, 1, lane, rv1);
     }
@@ -810,6 +825,8 @@ __device__ __forceinline__ void pp_epilogue_lds(const GemmArgs& a, f32x4 (&acc)[
 #pragma unroll
           for (int u = 0; u < 4; ++u) {
             float x = acc[h * 4 + i][j][u] * a.alpha + bv[j][u];
+            if ((EPI & EPI_PRE) && m0 + grp * 128 + h * 64 + r < a.m)
+              ((__bf16*)a.C2)[(m0 + grp * 128 + h * 64 + r) * a.ldc + colw + j * 16 + 4 * fc + u] = (__bf16)x;
             if (EPI & EPI_GELU) x = gelu_fast(x);
             v[u] = x;
           }
@@ -824,9 +841,10 @@ __device__ __forceinline__ void pp_epilogue_lds(const GemmArgs& a, f32x4 (&acc)[
         f32x4 v = *(const f32x4*)(lds_wave + r * 256 + ((c ^ (r & 7)) << 4));
         const int64_t row = m0 + grp * 128 + h * 64 + r;
         if (row < a.m) {
-          if (EPI & EPI_RESID) {
+          if (EPI & (EPI_AUX | EPI_DROP)) {
 #pragma unroll
-            for (int u = 0; u < 4; ++u) v[u] += (float)rv[p][u];
+            for (int u = 0; u < 4; ++u)
+              v[u] = epi_post<EPI>(a, v[u], row, colw + c * 4 + u, (EPI & EPI_AUX) ? (float)rv[p][u] : 0.f);
           }
           if (OUT_BF16) {
             bf16x4 o;
@@ -992,7 +1010,7 @@ __global__ __launch_bounds__(kLThreads, 1) void gemm_nt_pp1_kernel(GemmArgs a) {
   }
   if (grp == 0 && !(ABL & 4)) __builtin_amdgcn_s_barrier();
   if (ABL & 32) st2 = __builtin_amdgcn_s_memtime();
-  const bool full = (n0 + kL <= a.n) && (a.ldc % 8 == 0) && (!(EPI & EPI_RESID) || a.ldr % 4 == 0);
+  const bool full = (n0 + kL <= a.n) && (a.ldc % 8 == 0) && (!(EPI & EPI_AUX) || a.ldr % 4 == 0);
   if (full) {
     GemmArgs ae = a;
     if (a.kchunk) ae.C = (float*)a.C + (int64_t)blockIdx.y * a.m * a.ldc;
@@ -1026,8 +1044,26 @@ static int launch_gemm_t(const GemmArgs& a0, hipStream_t s) {
   // large tiles once there are >= 2 tiles per CU of them; small problems keep 128^2
   const int64_t tiles_l = ((a.m + kL - 1) / kL) * ((a.n + kL - 1) / kL);
   int64_t kc_l = 0;
-  if (tiles_l >= g_large_min_tiles && g_gemm_variant == 0) {
+  // the experimental kernel variants (switch values 2, 7-9, 16+) know only bias / GELU / residual
+  constexpr bool kBasicEpi = (EPI & ~(EPI_BIAS | EPI_GELU | EPI_RESID)) == 0;
+  if (tiles_l >= g_large_min_tiles && (g_gemm_variant == 0 || !kBasicEpi)) {
     hipLaunchKernelGGL((gemm_nt_pp1_kernel<OUT_BF16, EPI, 0, 5>), dim3((unsigned)tiles_l), dim3(kLThreads), 0, s, a);
+  } else if (!kBasicEpi) {
+    // below the 256^2 threshold: 128^2 kernel (split-K when the caller gave a workspace)
+    const int64_t tiles = ((a.m + kBM - 1) / kBM) * ((a.n + kBN - 1) / kBN);
+    int64_t kc = 0;
+    const int splits = a.ws ? small_splits(a.m, a.n, a.k, &kc) : 0;
+    if (splits > 1) {
+      GemmArgs b = a;
+      b.kchunk = kc;
+      hipLaunchKernelGGL((gemm_nt_kernel<OUT_BF16, EPI, true>), dim3((unsigned)tiles, 1, (unsigned)splits),
+                         dim3(kGemmThreads), 0, s, b);
+      const int64_t units = (a.n % 4 == 0) ? a.m * a.n / 4 : a.m * a.n;
+      const int64_t blocks = (units + 255) / 256 < 4096 ? (units + 255) / 256 : 4096;
+      hipLaunchKernelGGL((splitk_epi_kernel<OUT_BF16, EPI>), dim3((unsigned)blocks), dim3(256), 0, s, b, splits);
+    } else {
+      hipLaunchKernelGGL((gemm_nt_kernel<OUT_BF16, EPI>), dim3((unsigned)tiles), dim3(kGemmThreads), 0, s, a);
+    }
   } else if (tiles_l >= 512 && g_gemm_variant == 9) {
     hipLaunchKernelGGL((gemm_nt_l_kernel<OUT_BF16, EPI>), dim3((unsigned)tiles_l), dim3(kLThreads), 0, s, a);
   } else if (tiles_l >= 512 && g_gemm_variant == 2) {
@@ -1105,6 +1141,10 @@ int launch_gemm(const GemmArgs& a, bool out_bf16, int epi, hipStream_t s) {
     case EPI_BIAS | EPI_RESID: return launch_gemm_t<true, EPI_BIAS | EPI_RESID>(a, s);
     case EPI_RESID: return launch_gemm_t<true, EPI_RESID>(a, s);   // backward dgrad + residual branch
     case EPI_GELU: return launch_gemm_t<true, EPI_GELU>(a, s);
+    // training tower fusions (drt_linear_bf16_ex)
+    case EPI_BIAS | EPI_GELU | EPI_PRE: return launch_gemm_t<true, EPI_BIAS | EPI_GELU | EPI_PRE>(a, s);
+    case EPI_DGELU: return launch_gemm_t<true, EPI_DGELU>(a, s);
+    case EPI_BIAS | EPI_DROP | EPI_RESID: return launch_gemm_t<true, EPI_BIAS | EPI_DROP | EPI_RESID>(a, s);
     default: return DRT_EINVAL;
   }
 }
@@ -1181,6 +1221,46 @@ extern "C" int drt_linear_bf16_ws(const void* X, const void* W, const float* bia
   // split-K only with a large-enough caller workspace (else the unsplit kernel)
   if (ws && ws_bytes >= drt_linear_workspace(M, N, K) && drt_linear_workspace(M, N, K) > 0) a.ws = (float*)ws;
   const int epi = (bias ? EPI_BIAS : 0) | (gelu ? EPI_GELU : 0) | (residual ? EPI_RESID : 0);
+  return launch_gemm(a, !f32, epi, (hipStream_t)stream);
+}
+
+// drt_linear_bf16_ws plus the training tower's epilogue fusions (include/drt.h):
+//   gelu_pre != NULL: Y = (X W^T) * GELU'(gelu_pre)  (the dgrad through GELU; no bias / residual / GELU);
+//   Y_pre != NULL (with GELU): Y_pre = X W^T + b, Y = GELU(Y_pre)  (both bf16);
+//   flags & 4 (DROP): Y = dropout(X W^T + b) + residual with drt_dropout_add_bf16's mask of (seed, site).
+extern "C" int drt_linear_bf16_ex(const void* X, const void* W, const float* bias, const void* residual,
+                                  const void* gelu_pre, void* Y, void* Y_pre, int64_t M, int64_t N, int64_t K,
+                                  int32_t flags, float drop_p, uint64_t seed, uint64_t site, void* ws,
+                                  size_t ws_bytes, void* stream) {
+  DRT_REQUIRE(M >= 0 && N > 0 && K > 0 && K % 64 == 0);
+  if (M == 0) return DRT_OK;
+  DRT_REQUIRE(X && W && Y);
+  const bool gelu = flags & 1, f32 = flags & 2, drop = flags & 4;
+  DRT_REQUIRE(!f32 || (!gelu_pre && !Y_pre && !drop));
+  DRT_REQUIRE(!gelu_pre || (!bias && !residual && !gelu && !Y_pre && !drop));
+  DRT_REQUIRE(!Y_pre || (gelu && !residual && !drop));
+  DRT_REQUIRE(!drop || (drop_p >= 0.f && drop_p < 1.f && !gelu));
+  GemmArgs a{};
+  a.A = (const __bf16*)X;
+  a.B = (const __bf16*)W;
+  a.C = Y;
+  a.C2 = Y_pre;
+  a.bias = bias;
+  a.R = (const __bf16*)(gelu_pre ? gelu_pre : residual);
+  a.m = M;
+  a.n = N;
+  a.k = K;
+  a.lda = K;
+  a.ldb = K;
+  a.ldc = N;
+  a.ldr = N;
+  a.alpha = 1.0f;
+  a.drop_p = drop_p;
+  a.seed = seed;
+  a.site = site;
+  if (ws && ws_bytes >= drt_linear_workspace(M, N, K) && drt_linear_workspace(M, N, K) > 0) a.ws = (float*)ws;
+  const int epi = (bias ? EPI_BIAS : 0) | (gelu ? EPI_GELU : 0) | (residual ? EPI_RESID : 0) |
+                  (gelu_pre ? EPI_DGELU : 0) | (Y_pre ? EPI_PRE : 0) | (drop ? EPI_DROP : 0);
   return launch_gemm(a, !f32, epi, (hipStream_t)stream);
 }
 

@@ -53,11 +53,13 @@ def colsum(x: torch.Tensor) -> torch.Tensor:
 
 
 def linear_backward(dy: torch.Tensor, x: torch.Tensor, w_t: torch.Tensor, want_dx: bool = True,
-                    resid: Optional[torch.Tensor] = None
+                    resid: Optional[torch.Tensor] = None, gelu_pre: Optional[torch.Tensor] = None
                     ) -> Tuple[Optional[torch.Tensor], torch.Tensor, torch.Tensor]:
     """Gradients of y = x W^T + b (nn.Linear, W [N, K]) for dy [T, N], x [T, K] (bf16 CUDA),
     given w_t = W^T [K, N] bf16.  Returns (dx bf16 [T, K] or None, dW fp32 [N, K], db fp32 [N]);
-    ``resid`` [T, K] bf16 is added to dx in the dgrad GEMM's epilogue (a residual branch)."""
+    ``resid`` [T, K] bf16 is added to dx in the dgrad GEMM's epilogue (a residual branch);
+    ``gelu_pre`` [T, K] (x = GELU(gelu_pre)) makes dx the gradient of gelu_pre instead, the GELU
+    backward applied in the same epilogue (drt_linear_bf16_ex)."""
     lib = _native.load()
     dev = dy.device
     s = _native.stream_ptr(dev)
@@ -70,8 +72,15 @@ def linear_backward(dy: torch.Tensor, x: torch.Tensor, w_t: torch.Tensor, want_d
         dx = torch.empty((T, K), dtype=torch.bfloat16, device=dev)
         nb = int(lib.drt_linear_workspace(T, K, N))
         ws = _ws(nb, dev)
-        _native.check(lib.drt_linear_bf16_ws(dy.data_ptr(), w_t.data_ptr(), None, _ptr(resid), dx.data_ptr(), T, K, N,
-                                             0, _ptr(ws), nb, s), "dgrad")
+        if gelu_pre is not None:
+            if resid is not None:
+                raise ValueError("linear_backward: gelu_pre and resid are exclusive")
+            _native.check(lib.drt_linear_bf16_ex(dy.data_ptr(), w_t.data_ptr(), None, None, gelu_pre.data_ptr(),
+                                                 dx.data_ptr(), None, T, K, N, 0, 0.0, 0, 0, _ptr(ws), nb, s),
+                          "dgrad (GELU backward epilogue)")
+        else:
+            _native.check(lib.drt_linear_bf16_ws(dy.data_ptr(), w_t.data_ptr(), None, _ptr(resid), dx.data_ptr(), T, K,
+                                                 N, 0, _ptr(ws), nb, s), "dgrad")
     dW = wgrad(dy, x)
     return dx, dW, colsum(dy)
 
@@ -107,8 +116,10 @@ def wgrad(dy: torch.Tensor, x: torch.Tensor) -> torch.Tensor:
 
 
 def layernorm_backward(dy: torch.Tensor, x: torch.Tensor, gamma: torch.Tensor, eps: float,
-                       dres: Optional[torch.Tensor] = None):
-    """(dx bf16 [M, H], dgamma fp32 [H], dbeta fp32 [H]) of out = LN(x) (x = the bf16 pre-LN sums)."""
+                       dres: Optional[torch.Tensor] = None, drop=None):
+    """(dx bf16 [M, H], dgamma fp32 [H], dbeta fp32 [H]) of out = LN(x) (x = the bf16 pre-LN sums).
+    ``drop`` = (p, seed, site): also return dropout(dx) with that mask (drt_layernorm_bwd_drop_bf16)
+    as a fourth value."""
     lib = _native.load()
     M, H = x.shape
     dev = x.device
@@ -117,9 +128,14 @@ def layernorm_backward(dy: torch.Tensor, x: torch.Tensor, gamma: torch.Tensor, e
     db = torch.empty(H, dtype=torch.float32, device=dev)
     nb = int(lib.drt_layernorm_bwd_workspace(M, H))
     ws = _ws(nb, dev)
-    _native.check(lib.drt_layernorm_bwd_bf16(dy.data_ptr(), x.data_ptr(), gamma.data_ptr(), float(eps), M, H,
-                                             _ptr(dres), dx.data_ptr(), dg.data_ptr(), db.data_ptr(), _ptr(ws), nb,
-                                             _native.stream_ptr(dev)), "drt_layernorm_bwd_bf16")
+    dxd = torch.empty_like(dx) if drop is not None else None
+    p, seed, site = drop if drop is not None else (0.0, 0, 0)
+    _native.check(lib.drt_layernorm_bwd_drop_bf16(dy.data_ptr(), x.data_ptr(), gamma.data_ptr(), float(eps), M, H,
+                                                  _ptr(dres), dx.data_ptr(), _ptr(dxd), float(p), seed, site,
+                                                  dg.data_ptr(), db.data_ptr(), _ptr(ws), nb,
+                                                  _native.stream_ptr(dev)), "drt_layernorm_bwd_drop_bf16")
+    if drop is not None:
+        return dx, dg, db, dxd
     return dx, dg, db
 
 

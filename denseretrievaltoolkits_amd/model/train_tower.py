@@ -28,7 +28,7 @@ import torch
 
 from .. import _native
 from .encoder import BertShape, _check_supported
-from .encoder_bwd import _ptr, gelu_backward, layernorm_backward, linear_backward
+from .encoder_bwd import _ptr, layernorm_backward, linear_backward
 
 MAX_TRAIN_SEQ = 160
 
@@ -91,12 +91,20 @@ class _Weights:
         self.emb_b = sd[e + "LayerNorm.bias"].detach().float().contiguous()
 
 
-def _lin(lib, x, w, b, out, resid=None, gelu=False, stream=None):
+def _lin(lib, x, w, b, out, resid=None, gelu=False, stream=None, pre_out=None, drop=None):
+    """out = x W^T + b (GELU) (+ resid); ``pre_out``: also store the pre-activation (GELU);
+    ``drop`` = (p, seed, site): out = dropout(x W^T + b) + resid (drt_linear_bf16_ex epilogues)."""
     m, k = x.shape
     n = w.shape[0]
     flags = (1 if gelu else 0) | (2 if out.dtype == torch.float32 else 0)
     nb = int(lib.drt_linear_workspace(m, n, k))
     ws = torch.empty((nb + 3) // 4, dtype=torch.float32, device=x.device) if nb else None
+    if pre_out is not None or drop is not None:
+        p, seed, site = drop if drop is not None else (0.0, 0, 0)
+        _native.check(lib.drt_linear_bf16_ex(x.data_ptr(), w.data_ptr(), _ptr(b), _ptr(resid), None, out.data_ptr(),
+                                             _ptr(pre_out), m, n, k, flags | (4 if drop is not None else 0), float(p),
+                                             seed, site, _ptr(ws), nb, stream), "drt_linear_bf16_ex")
+        return out
     _native.check(lib.drt_linear_bf16_ws(x.data_ptr(), w.data_ptr(), _ptr(b), _ptr(resid), out.data_ptr(), m, n, k,
                                          flags, _ptr(ws), nb, stream), "drt_linear_bf16_ws")
     return out
@@ -151,21 +159,16 @@ def tower_forward(model, W: _Weights, ids: torch.Tensor, mask: Optional[torch.Te
         _native.check(lib.drt_attention_train_fwd_bf16(qkv.data_ptr(), _ptr(mask), ctx.data_ptr(), lse.data_ptr(),
                                                        B, L, heads, H // heads, scale, float(pa), seed, s_att, s),
                       "drt_attention_train_fwd_bf16")
-        if ph > 0:   # x1 = dropout(ctx Wo^T + bo) + h
-            x1 = _dropout(lib, _lin(lib, ctx, ly["wo"], ly["bo"], torch.empty_like(h), stream=s), ph, seed, s_out1, s,
-                          resid=h)
-        else:
-            x1 = _lin(lib, ctx, ly["wo"], ly["bo"], torch.empty_like(h), resid=h, stream=s)
+        # x1 = dropout(ctx Wo^T + bo) + h, dropout in the GEMM epilogue
+        x1 = _lin(lib, ctx, ly["wo"], ly["bo"], torch.empty_like(h), resid=h, stream=s,
+                  drop=(ph, seed, s_out1) if ph > 0 else None)
         h1 = _layernorm(lib, x1, ly["g1"], ly["b1"], eps, s)
-        fpre = _lin(lib, h1, ly["wi"], ly["bi"],
-                    torch.empty((T, ly["wi"].shape[0]), dtype=torch.bfloat16, device=dev), stream=s)
-        f = torch.empty_like(fpre)
-        _native.check(lib.drt_gelu_bf16(fpre.data_ptr(), fpre.numel(), f.data_ptr(), s), "drt_gelu_bf16")
-        if ph > 0:   # x2 = dropout(f Wf^T + bf) + h1
-            x2 = _dropout(lib, _lin(lib, f, ly["wf"], ly["bf"], torch.empty_like(h), stream=s), ph, seed, s_out2, s,
-                          resid=h1)
-        else:
-            x2 = _lin(lib, f, ly["wf"], ly["bf"], torch.empty_like(h), resid=h1, stream=s)
+        # f = GELU(fpre), fpre = h1 Wi^T + bi: both from the one GEMM epilogue
+        fpre = torch.empty((T, ly["wi"].shape[0]), dtype=torch.bfloat16, device=dev)
+        f = _lin(lib, h1, ly["wi"], ly["bi"], torch.empty_like(fpre), gelu=True, stream=s, pre_out=fpre)
+        # x2 = dropout(f Wf^T + bf) + h1
+        x2 = _lin(lib, f, ly["wf"], ly["bf"], torch.empty_like(h), resid=h1, stream=s,
+                  drop=(ph, seed, s_out2) if ph > 0 else None)
         saved.append((h, qkv, ctx, lse, x1, h1, fpre, f, x2))
         h = _layernorm(lib, x2, ly["g2"], ly["b2"], eps, s)
     return h.view(B, L, H), (emb_pre, saved)
@@ -190,13 +193,21 @@ def tower_backward(model, W: _Weights, ids, mask, saved, d_hidden: torch.Tensor,
         ly = W.layers[i]
         p = f"encoder.layer.{i}."
         s_att, s_out1, s_out2 = dropout_sites(i)
-        dx2, dg2, db2 = layernorm_backward(d, x2, ly["g2"], eps)
-        df, dwf, dbf = linear_backward(_dropout(lib, dx2, ph, seed, s_out2, s) if ph > 0 else dx2, f, ly["wf_t"])
-        dfpre = gelu_backward(df, fpre)
+        # LN backward also emits the dropped gradient entering FFN2; FFN2's dgrad applies the GELU
+        # backward in its epilogue (-> d fpre)
+        if ph > 0:
+            dx2, dg2, db2, dy2 = layernorm_backward(d, x2, ly["g2"], eps, drop=(ph, seed, s_out2))
+        else:
+            dx2, dg2, db2 = layernorm_backward(d, x2, ly["g2"], eps)
+            dy2 = dx2
+        dfpre, dwf, dbf = linear_backward(dy2, f, ly["wf_t"], gelu_pre=fpre)
         dh1, dwi, dbi = linear_backward(dfpre, h1, ly["wi_t"], resid=dx2)
-        dx1, dg1, db1 = layernorm_backward(dh1, x1, ly["g1"], eps)
-        dctx, dwo, dbo = linear_backward(_dropout(lib, dx1, ph, seed, s_out1, s) if ph > 0 else dx1, ctx,
-                                         ly["wo_t"])
+        if ph > 0:
+            dx1, dg1, db1, dy1 = layernorm_backward(dh1, x1, ly["g1"], eps, drop=(ph, seed, s_out1))
+        else:
+            dx1, dg1, db1 = layernorm_backward(dh1, x1, ly["g1"], eps)
+            dy1 = dx1
+        dctx, dwo, dbo = linear_backward(dy1, ctx, ly["wo_t"])
         dqkv = torch.empty_like(qkv)
         _native.check(lib.drt_attention_train_bwd_bf16(qkv.data_ptr(), ctx.data_ptr(), dctx.data_ptr(),
                                                        lse.data_ptr(), _ptr(mask), dqkv.data_ptr(), B, L, heads,

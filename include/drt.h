@@ -183,6 +183,18 @@ size_t drt_linear_workspace(int64_t M, int64_t N, int64_t K);
 int drt_linear_bf16_ws(const void* X, const void* W, const float* bias, const void* residual,
                        void* Y, int64_t M, int64_t N, int64_t K, int32_t flags, void* ws,
                        size_t ws_bytes, void* stream);
+/* drt_linear_bf16_ws plus the training tower's epilogue fusions (bf16 Y):
+ *   gelu_pre [M, N] != NULL: Y = (X W^T) * GELU'(gelu_pre)  (dgrad through an erf GELU whose input
+ *     was gelu_pre; bias / residual / GELU / Y_pre / DROP must be off);
+ *   Y_pre [M, N] != NULL (requires flags GELU): Y_pre = X W^T + b and Y = GELU(Y_pre);
+ *   flags & 4 (DROP): Y = dropout(X W^T + b) + residual, the mask of drt_dropout_add_bf16 for
+ *     (drop_p, seed, site) at the flat index m * N + n.
+ * Replaces linear -> drt_gelu_bf16, dgrad -> drt_gelu_bwd_bf16 and linear -> drt_dropout_add_bf16
+ * pairs of the training tower (BertIntermediate / BertOutput / BertSelfOutput under autograd). */
+int drt_linear_bf16_ex(const void* X, const void* W, const float* bias, const void* residual,
+                       const void* gelu_pre, void* Y, void* Y_pre, int64_t M, int64_t N, int64_t K,
+                       int32_t flags, float drop_p, uint64_t seed, uint64_t site, void* ws,
+                       size_t ws_bytes, void* stream);
 int drt_layernorm_f32_bf16(const float* X, int64_t M, int32_t H, const float* gamma,
                            const float* beta, float eps, void* out, void* stream);
 int drt_layernorm_bf16(const void* X, int64_t M, int32_t H, const float* gamma,
@@ -212,6 +224,13 @@ size_t drt_layernorm_bwd_workspace(int64_t M, int32_t H);
 int drt_layernorm_bwd_bf16(const void* dy, const void* x, const float* gamma, float eps, int64_t M,
                            int32_t H, const void* dres, void* dx, float* dgamma, float* dbeta,
                            void* ws, size_t ws_bytes, void* stream);
+/* The same, also writing dx_drop = dropout(dx) with drt_dropout_add_bf16's mask of
+ * (drop_p, seed, site) at the flat index m * H + h (the gradient of a linear whose output was
+ * dropped before this LayerNorm's residual add; replaces a separate dropout pass).          */
+int drt_layernorm_bwd_drop_bf16(const void* dy, const void* x, const float* gamma, float eps,
+                                int64_t M, int32_t H, const void* dres, void* dx, void* dx_drop,
+                                float drop_p, uint64_t seed, uint64_t site, float* dgamma,
+                                float* dbeta, void* ws, size_t ws_bytes, void* stream);
 size_t drt_colsum_workspace(int64_t M, int64_t N);
 int drt_colsum_bf16(const void* x, int64_t M, int64_t N, float* out, void* ws, size_t ws_bytes,
                     void* stream);
@@ -231,8 +250,10 @@ int drt_linear_wgrad_bf16(const void* dY, const void* X, float* dW, int64_t T, i
 /* drt_embed_ln_pre: drt_embed_ln that also writes the bf16 pre-LN sum (word + type + pos).
  * drt_gelu_bf16: y = GELU(x) elementwise (erf form).
  * drt_embedding_bwd: scatter-add of d [B*L, H] (gradient of the pre-LN embedding sum) into
- *   dword [V,H], dpos [P,H], dtype [types,H] fp32 (atomics; caller zeroes them); tokens
- *   equal to padding_idx (nn.Embedding(padding_idx), -1 = none) add nothing to dword.      */
+ *   dword [V,H], dpos [P,H], dtype [types,H] fp32 (caller zeroes them: word rows by atomics,
+ *   position rows by chunked column sums, token type 0 from the position sums when
+ *   type_ids is NULL); tokens equal to padding_idx (nn.Embedding(padding_idx), -1 = none)
+ *   add nothing to dword.                                                                   */
 int drt_embed_ln_pre(const int64_t* ids, const int64_t* type_ids, int64_t B, int64_t L,
                      const float* word_emb, const float* pos_emb, const float* type_emb,
                      const float* gamma, const float* beta, float eps, int32_t H, void* out, void* pre,

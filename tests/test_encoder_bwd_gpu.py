@@ -231,3 +231,119 @@ def test_wgrad_tn_vs_torch_and_transposed_path(dev, T, N, K):
     split = _native.load().drt_linear_wgrad_workspace(T, N, K) > 0
     if split and T % 64 == 0:
         assert torch.equal(dw_tn, dw_nt)
+
+
+def _lin_ex(lib, dev, x, w, bias=None, resid=None, gelu_pre=None, pre_out=None, gelu=False, drop=None, out=None):
+    import torch
+    from denseretrievaltoolkits_amd import _native
+    M, K = x.shape
+    N = w.shape[0]
+    y = out if out is not None else torch.empty((M, N), dtype=torch.bfloat16, device=dev)
+    nb = int(lib.drt_linear_workspace(M, N, K))
+    ws = torch.empty(max(1, (nb + 3) // 4), dtype=torch.float32, device=dev)
+    p, seed, site = drop if drop is not None else (0.0, 0, 0)
+    ptr = (lambda t: t.data_ptr() if t is not None else None)
+    _native.check(lib.drt_linear_bf16_ex(x.data_ptr(), w.data_ptr(), ptr(bias), ptr(resid), ptr(gelu_pre),
+                                         y.data_ptr(), ptr(pre_out), M, N, K,
+                                         (1 if gelu else 0) | (4 if drop is not None else 0), float(p), seed, site,
+                                         ws.data_ptr(), nb, _native.stream_ptr(dev)), "drt_linear_bf16_ex")
+    return y
+
+
+@pytest.mark.parametrize("M,N,K", [(65536, 3072, 768), (2000, 3072, 768), (64, 256, 128)])
+def test_linear_ex_gelu_pre_outputs_equal_separate_linears(dev, M, N, K):
+    """EPI_PRE: one GEMM stores the pre-activation and GELU of it, bit-identical to the linear
+    without / with the GELU epilogue (the training forward keeps both)."""
+    import torch
+    from denseretrievaltoolkits_amd import _native
+    lib = _native.load()
+    g = torch.Generator(device=dev).manual_seed(M + N)
+    x = torch.randn(M, K, generator=g, device=dev).to(torch.bfloat16)
+    w = (0.05 * torch.randn(N, K, generator=g, device=dev)).to(torch.bfloat16)
+    b = 0.1 * torch.randn(N, generator=g, device=dev)
+    pre = torch.empty((M, N), dtype=torch.bfloat16, device=dev)
+    f = _lin_ex(lib, dev, x, w, bias=b, gelu=True, pre_out=pre)
+    plain = torch.empty_like(pre)
+    act = torch.empty_like(pre)
+    for out, flags in ((plain, 0), (act, 1)):
+        _native.check(lib.drt_linear_bf16(x.data_ptr(), w.data_ptr(), b.data_ptr(), None, out.data_ptr(), M, N, K,
+                                          flags, _native.stream_ptr(dev)), "linear")
+    torch.cuda.synchronize()
+    assert torch.equal(pre, plain)
+    assert torch.equal(f, act)
+
+
+@pytest.mark.parametrize("M,N,K", [(131072, 3072, 768), (4096, 3072, 768), (100, 256, 64)])
+def test_linear_ex_dgelu_vs_fp32(dev, M, N, K):
+    """EPI_DGELU: dgrad through GELU in the epilogue, vs fp32 torch of (dy W) * GELU'(pre); not
+    worse than the unfused dgrad -> drt_gelu_bwd_bf16 path it replaces."""
+    import torch
+    from denseretrievaltoolkits_amd import _native
+    from denseretrievaltoolkits_amd.model.encoder_bwd import gelu_backward
+    lib = _native.load()
+    g = torch.Generator(device=dev).manual_seed(M + K)
+    dy = torch.randn(M, K, generator=g, device=dev).to(torch.bfloat16)
+    wt = (0.05 * torch.randn(N, K, generator=g, device=dev)).to(torch.bfloat16)   # W^T rows: [N out, K in]
+    pre = (1.5 * torch.randn(M, N, generator=g, device=dev)).to(torch.bfloat16)
+    fused = _lin_ex(lib, dev, dy, wt, gelu_pre=pre)
+    df = _lin_ex(lib, dev, dy, wt, bias=None)   # plain dgrad (no flags)
+    unfused = gelu_backward(df, pre)
+    xf = pre.float().requires_grad_(True)
+    gl = torch.nn.functional.gelu(xf)
+    ref = torch.autograd.grad(gl, xf, (dy.float() @ wt.float().t()))[0]
+    err_f = (fused.float() - ref).abs().max().item()
+    err_u = (unfused.float() - ref).abs().max().item()
+    scale = ref.abs().max().item()
+    assert err_f <= 1.05 * err_u + 1e-3 * scale, (err_f, err_u, scale)
+    assert err_f <= 1e-2 * scale
+
+
+@pytest.mark.parametrize("M,N,K,p", [(131072, 768, 3072, 0.1), (16384, 768, 768, 0.1), (300, 768, 64, 0.5)])
+def test_linear_ex_dropout_vs_dropout_add(dev, M, N, K, p):
+    """EPI_DROP: dropout(x W^T + b) + resid in the epilogue, with drt_dropout_add_bf16's mask:
+    same dropped positions, values within the one extra bf16 rounding of the unfused path."""
+    import torch
+    from denseretrievaltoolkits_amd import _native
+    lib = _native.load()
+    g = torch.Generator(device=dev).manual_seed(M + K)
+    x = torch.randn(M, K, generator=g, device=dev).to(torch.bfloat16)
+    w = (0.05 * torch.randn(N, K, generator=g, device=dev)).to(torch.bfloat16)
+    b = 0.1 * torch.randn(N, generator=g, device=dev)
+    resid = torch.randn(M, N, generator=g, device=dev).to(torch.bfloat16)
+    seed, site = 123456789, 7
+    fused = _lin_ex(lib, dev, x, w, bias=b, resid=resid, drop=(p, seed, site))
+    y = torch.empty((M, N), dtype=torch.bfloat16, device=dev)
+    _native.check(lib.drt_linear_bf16(x.data_ptr(), w.data_ptr(), b.data_ptr(), None, y.data_ptr(), M, N, K, 0,
+                                      _native.stream_ptr(dev)), "linear")
+    ref = torch.empty_like(y)
+    _native.check(lib.drt_dropout_add_bf16(y.data_ptr(), resid.data_ptr(), y.numel(), p, seed, site,
+                                           ref.data_ptr(), _native.stream_ptr(dev)), "dropout_add")
+    torch.cuda.synchronize()
+    dropped_ref = ref == resid
+    keep_frac = 1.0 - (fused == resid).float().mean().item()
+    assert abs(keep_frac - (1.0 - p)) < 0.02
+    # wherever the unfused path kept the element, both agree to one bf16 rounding of the sum
+    torch.testing.assert_close(fused.float(), ref.float(), atol=2e-2, rtol=1e-2)
+    assert ((fused == resid) | ~dropped_ref).float().mean().item() > 0.999
+
+
+@pytest.mark.parametrize("M,H", [(131072, 768), (37, 256)])
+def test_layernorm_bwd_drop_output_equals_dropout_kernel(dev, M, H):
+    """drt_layernorm_bwd_drop_bf16: dx identical to drt_layernorm_bwd_bf16 and dx_drop bit-identical
+    to drt_dropout_add_bf16(dx) with the same (p, seed, site)."""
+    import torch
+    from denseretrievaltoolkits_amd import _native
+    from denseretrievaltoolkits_amd.model.encoder_bwd import layernorm_backward
+    lib = _native.load()
+    g = torch.Generator(device=dev).manual_seed(M + H)
+    x = (2.0 * torch.randn(M, H, generator=g, device=dev)).to(torch.bfloat16)
+    gamma = 1.0 + 0.2 * torch.randn(H, generator=g, device=dev)
+    dy = torch.randn(M, H, generator=g, device=dev).to(torch.bfloat16)
+    dx, dg, db, dxd = layernorm_backward(dy, x, gamma, 1e-12, drop=(0.1, 99, 5))
+    dx0, dg0, db0 = layernorm_backward(dy, x, gamma, 1e-12)
+    ref = torch.empty_like(dx)
+    _native.check(lib.drt_dropout_add_bf16(dx0.data_ptr(), None, dx0.numel(), 0.1, 99, 5, ref.data_ptr(),
+                                           _native.stream_ptr(dev)), "dropout")
+    torch.cuda.synchronize()
+    assert torch.equal(dx, dx0) and torch.equal(dg, dg0) and torch.equal(db, db0)
+    assert torch.equal(dxd, ref)
