@@ -282,6 +282,9 @@ __global__ __launch_bounds__(256) void splitk_epi_kernel(GemmArgs a, int splits)
 
 // Split plan of the 128^2 kernel for problems too small to fill the chip (query-sized
 // batches): enough splits for ~2 blocks per CU, >= 128 k per split.  0 = no split.
+// split-K planning knobs (drt_gemm_split_config): the 256^2 kernel splits K >= g_lsplit_min_k into
+// chunks of >= g_lsplit_k_per; the 128^2 kernel keeps its fp32 partials <= g_ssplit_cap bytes
+static int64_t g_lsplit_min_k = 8192, g_lsplit_k_per = 512, g_ssplit_cap = 16 << 20;
 static int small_splits(int64_t m, int64_t n, int64_t k, int64_t* kchunk) {
   const int64_t tiles = ((m + kBM - 1) / kBM) * ((n + kBN - 1) / kBN);
   if (tiles >= 384 || k < 256) return 0;
@@ -289,7 +292,7 @@ static int small_splits(int64_t m, int64_t n, int64_t k, int64_t* kchunk) {
   if (splits > k / 128) splits = k / 128;
   // partials must stay small enough to be re-read from the caches: at 4096 x 768 (a 128-query
   // batch) 3 splits = 38 MB of partials measured slower than the unsplit kernel
-  const int64_t cap = (int64_t)(16 << 20) / (m * n * 4);
+  const int64_t cap = g_ssplit_cap / (m * n * 4);
   if (splits > cap) splits = cap;
   if (splits < 2) return 0;
   int64_t kc = (k + splits - 1) / splits;
@@ -305,9 +308,9 @@ static int small_splits(int64_t m, int64_t n, int64_t k, int64_t* kchunk) {
 // split, fp32 partials <= 256 MiB.  0 = no split.
 static int large_splits(int64_t m, int64_t n, int64_t k, int64_t min_tiles, int64_t* kchunk) {
   const int64_t tiles = ((m + 255) / 256) * ((n + 255) / 256);
-  if (tiles >= min_tiles || k < 8192 || k % 32) return 0;
+  if (tiles >= min_tiles || k < g_lsplit_min_k || k % 32) return 0;
   int64_t splits = (256 + tiles - 1) / tiles;
-  if (splits > k / 512) splits = k / 512;
+  if (splits > k / g_lsplit_k_per) splits = k / g_lsplit_k_per;
   const int64_t cap = (int64_t)(256ll << 20) / (m * n * 4);
   if (splits > cap) splits = cap;
   if (splits < 2) return 0;
@@ -1331,6 +1334,14 @@ extern "C" int drt_gemm_debug_buffer(void* buf) {
 }
 
 // Benchmark switch: smallest grid (in 256^2 tiles) that takes the 256^2 kernel.
+// Benchmark switch of the split-K planning (see g_lsplit_* / g_ssplit_cap); non-positive = keep.
+extern "C" int drt_gemm_split_config(int64_t large_min_k, int64_t large_k_per_split, int64_t small_cap_bytes) {
+  if (large_min_k > 0) g_lsplit_min_k = large_min_k;
+  if (large_k_per_split > 0) g_lsplit_k_per = large_k_per_split;
+  if (small_cap_bytes > 0) g_ssplit_cap = small_cap_bytes;
+  return DRT_OK;
+}
+
 extern "C" int drt_gemm_large_min_tiles(int64_t tiles) {
   if (tiles < 1) return DRT_EINVAL;
   g_large_min_tiles = tiles;

@@ -289,6 +289,10 @@ int drt_l2_normalize_f32(float* x, int64_t B, int32_t H, void* out_bf16, void* s
  * builds (ablations / cycle stamps, need drt_gemm_debug_buffer).            */
 int drt_gemm_force_small(int32_t on);
 /* Benchmark switch: smallest grid, in 256x256 tiles, that takes the 256x256 kernel. */
+/* Benchmark switch of the split-K planning: the 256^2 kernel splits K >= large_min_k (default
+ * 8192) into chunks of >= large_k_per_split (512); the 128^2 kernel keeps its fp32 partials <=
+ * small_cap_bytes (16 MiB).  Non-positive arguments keep the current value.                 */
+int drt_gemm_split_config(int64_t large_min_k, int64_t large_k_per_split, int64_t small_cap_bytes);
 int drt_gemm_large_min_tiles(int64_t tiles);
 /* Diagnostic only: device buffer for the GEMM cycle-stamp variants (drt_gemm_force_small >= 16). */
 int drt_gemm_debug_buffer(void* buf);
