@@ -195,6 +195,27 @@ Tensor dist_filter_lists(const Tensor& q_, const Tensor& p_, int64_t n_global, i
   return packed;
 }
 
+// dist_filter writing into `packed` ([nq, k + 1] contiguous, e.g. a row slice of a group buffer); tau is
+// this batch's [nq] slice of a group's thresholds.
+void dist_filter_into(const Tensor& q_, const Tensor& p_, int64_t n_global, int64_t k, int64_t id_offset,
+                      const Tensor& tau_, Tensor& packed) {
+  need(q_, "q", at::kBFloat16, 2);
+  need(p_, "p", at::kBFloat16, 2);
+  need(tau_, "tau", at::kFloat, 1);
+  need(packed, "packed", at::kLong, 2);
+  const c10::DeviceGuard g(q_.device());
+  const Tensor q = q_.contiguous(), p = p_.contiguous(), tau = tau_.contiguous();
+  TORCH_CHECK_VALUE(tau.size(0) == q.size(0), "tau must hold one threshold per query");
+  TORCH_CHECK_VALUE(packed.is_contiguous() && packed.size(0) == q.size(0) && packed.size(1) == k + 1,
+                    "packed must be a contiguous [nq, k + 1] tensor");
+  size_t wsb = 0;
+  Tensor ws = dist_ws(q, p.size(0), n_global, k, &wsb);
+  check_rc(drt_ip_topk_dist_filter(q.data_ptr(), q.size(0), p.size(0) ? p.data_ptr() : nullptr, p.size(0), n_global,
+                                   (int32_t)q.size(1), (int32_t)k, id_offset, tau.data_ptr<float>(),
+                                   (uint64_t*)packed.data_ptr<int64_t>(), ws.data_ptr(), wsb, stream_of(q)),
+           "drt_ip_topk_dist_filter");
+}
+
 // dist_filter_lists for query rows [q0, q0 + nq) of lists [nlists, NQ, r] gathered for a group of
 // batches, writing the packed lists into `packed` ([nq, k + 1], e.g. a row slice of a group buffer).
 void dist_filter_lists_into(const Tensor& q_, const Tensor& p_, int64_t n_global, int64_t k, int64_t id_offset,
@@ -400,6 +421,7 @@ TORCH_LIBRARY(drt, m) {
   m.def("dist_filter_lists(Tensor q, Tensor p, int n_global, int k, int id_offset, Tensor lists) -> Tensor");
   m.def("dist_filter_lists_into(Tensor q, Tensor p, int n_global, int k, int id_offset, Tensor lists, int q0, "
         "Tensor(a!) packed) -> ()");
+  m.def("dist_filter_into(Tensor q, Tensor p, int n_global, int k, int id_offset, Tensor tau, Tensor(a!) packed) -> ()");
   m.def("merge_packed(Tensor parts, int k, int n_global) -> (Tensor, Tensor, Tensor)");
   m.def("score_ce_fwd(Tensor q, Tensor p, int target_stride, float scale) -> (Tensor, Tensor, Tensor)");
   m.def("score_ce_bwd(Tensor grad, Tensor q, Tensor p, Tensor scores, Tensor lse, int target_stride, "
@@ -423,6 +445,7 @@ TORCH_LIBRARY_IMPL(drt, CUDA, m) {   // the GPU dispatch key of torch-ROCm
   m.impl("dist_filter", &dist_filter);
   m.impl("dist_filter_lists", &dist_filter_lists);
   m.impl("dist_filter_lists_into", &dist_filter_lists_into);
+  m.impl("dist_filter_into", &dist_filter_into);
   m.impl("merge_packed", &merge_packed);
   m.impl("score_ce_fwd", &score_ce_fwd);
   m.impl("score_ce_bwd", &score_ce_bwd);

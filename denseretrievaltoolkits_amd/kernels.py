@@ -114,6 +114,14 @@ def dist_filter_lists(q: torch.Tensor, p: torch.Tensor, n_global: int, k: int, i
     return ops.load().dist_filter_lists(q, p, n_global, k, id_offset, lists)
 
 
+def dist_filter_into(q: torch.Tensor, p: torch.Tensor, n_global: int, k: int, id_offset: int, tau: torch.Tensor,
+                     packed: torch.Tensor) -> None:
+    """dist_filter (threshold tau [nq] given) writing this shard's packed lists into ``packed``
+    ([nq, k + 1], e.g. a row slice of a group buffer)."""
+    _require_device(q, p, tau, packed)
+    ops.load().dist_filter_into(q, p, n_global, k, id_offset, tau, packed)
+
+
 def dist_filter_lists_into(q: torch.Tensor, p: torch.Tensor, n_global: int, k: int, id_offset: int,
                            lists: torch.Tensor, q0: int, packed: torch.Tensor) -> None:
     """dist_filter_lists for the query rows [q0, q0 + nq) of lists [nlists, NQ, r] gathered for a

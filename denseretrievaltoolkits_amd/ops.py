@@ -77,6 +77,10 @@ def _register_python_parts():
     def _(q, p, n_global, k, id_offset, lists):
         return q.new_empty((q.shape[0], k + 1), dtype=torch.int64)
 
+    @lib.register_fake("drt::dist_filter_into")
+    def _(q, p, n_global, k, id_offset, tau, packed):
+        return None
+
     @lib.register_fake("drt::dist_filter_lists_into")
     def _(q, p, n_global, k, id_offset, lists, q0, packed):
         return None

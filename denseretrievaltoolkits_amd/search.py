@@ -71,8 +71,12 @@ def _pipeline(batches, enqueue, finish):
 # all-gather and the merge -- are paid once per GROUP of query batches; every batch still streams
 # the whole shard once in its own filter scan.  Queries per group (16 batches of 128):
 GROUP_QUERIES = 2048
-# one-GPU indexes smaller than this keep the per-batch path (nothing to amortise)
-GROUP_MIN_ROWS = 1 << 20
+# one-GPU indexes take the grouped path from this many rows up.  Off by default: on one GPU the
+# group's sample launch (2048 queries over ~0.7 % of the rows, every score written out) costs
+# what the per-batch sample launches cost, and the back-to-back filter scans measured 2-3 %
+# slower (tools/search_ab.py, bench.py --group-queries 0 vs default on one box:
+# profiles/r02j_bench_*.json); across GPUs the group also saves two collectives per batch.
+GROUP_MIN_ROWS = 1 << 62
 
 
 def _groups(batches, cap=GROUP_QUERIES):
@@ -90,17 +94,18 @@ def _groups(batches, cap=GROUP_QUERIES):
 def _gtau_enqueue_group(local, qs, k: int, n_global: int, offset: int, gather):
     """One group of query batches through the global-threshold protocol (see ShardedFlatIP):
     ONE sample launch for all of the group's queries, one exchange of the sample lists, one
-    filter scan (+ threshold, select) per batch writing its packed top-k into a group buffer,
+    threshold launch, one filter scan (+ select) per batch writing its packed top-k into a group buffer,
     one exchange of that buffer and one merge that certifies every query.  ``gather(t)`` ->
     [world, *t.shape] (identity stack on one GPU)."""
     sizes = [q.shape[0] for q in qs]
     qg = qs[0] if len(qs) == 1 else torch.cat(qs)
     best = local.dist_sample(qg, n_global, k)                       # [Qg, r]
     lists = gather(best).contiguous()                               # [world, Qg, r]
+    tau = kernels.dist_tau(lists, k)                                # [Qg]: one launch for the group
     packed = torch.empty((qg.shape[0], k + 1), dtype=torch.int64, device=qg.device)
     o = 0
     for q, nb in zip(qs, sizes):
-        kernels.dist_filter_lists_into(q, local.rows, n_global, k, offset, lists, o, packed[o:o + nb])
+        kernels.dist_filter_into(q, local.rows, n_global, k, offset, tau[o:o + nb], packed[o:o + nb])
         o += nb
     s, i, st = kernels.merge_packed(gather(packed), k, n_global)
     h, ev = _stage_status(st)

@@ -4,7 +4,7 @@ real CPU tensors are refused by the dispatcher (no CPU fallback exists)."""
 import pytest
 import torch
 
-OPS = ["ip_topk", "ip_topk_resolve", "topk_merge", "dist_sample", "dist_tau", "dist_filter", "dist_filter_lists", "dist_filter_lists_into", "merge_packed",
+OPS = ["ip_topk", "ip_topk_resolve", "topk_merge", "dist_sample", "dist_tau", "dist_filter", "dist_filter_lists", "dist_filter_lists_into", "dist_filter_into", "merge_packed",
        "score_ce_fwd", "score_ce_bwd", "embed_ln", "linear", "attention", "layernorm", "pool", "l2_normalize"]
 
 

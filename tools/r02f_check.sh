@@ -10,7 +10,7 @@ rc=$?; tail -3 gpurun_out/pytest_f.log
 if [ $rc -ne 0 ]; then exit $rc; fi
 timeout -k 10 300 python tools/sim_dist.py --world 8 --steps 32 --check > gpurun_out/sim8f.log 2>&1 || exit $?
 tail -1 gpurun_out/sim8f.log
-timeout -k 10 400 python bench.py --steps 32 --warmup 3 --no-encode --no-cpu-baseline > gpurun_out/bench_f.log 2>&1 || exit $?
+timeout -k 10 400 python bench.py --steps 32 --warmup 3 --no-encode --no-cpu-baseline --group-queries 2048 > gpurun_out/bench_f.log 2>&1 || exit $?
 grep '^{' gpurun_out/bench_f.log | tail -1
 timeout -k 10 400 python bench.py --steps 32 --warmup 3 --no-encode --no-cpu-baseline --group-queries 0 > gpurun_out/bench_f0.log 2>&1 || exit $?
 grep '^{' gpurun_out/bench_f0.log | tail -1

@@ -38,7 +38,7 @@ def main():
             if v == 0:
                 srch.GROUP_MIN_ROWS = 1 << 62
             else:
-                srch.GROUP_MIN_ROWS = 1 << 20
+                srch.GROUP_MIN_ROWS = 0
                 srch.GROUP_QUERIES = v
             idx.search_batches(batches[:2], 1000)
             torch.cuda.synchronize()

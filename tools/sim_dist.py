@@ -129,9 +129,10 @@ def main():
     def gt_grouped(gi):
         best = kernels.dist_sample(gq[gi], own, N, k)
         glists[gi][R].copy_(best)
+        tau = kernels.dist_tau(glists[gi], k)
         for b, j in enumerate(groups[gi]):
-            kernels.dist_filter_lists_into(queries[j], own, N, k, lo, glists[gi], b * qb,
-                                           gparts[gi][R, b * qb:(b + 1) * qb])
+            kernels.dist_filter_into(queries[j], own, N, k, lo, tau[b * qb:(b + 1) * qb],
+                                     gparts[gi][R, b * qb:(b + 1) * qb])
         kernels.merge_packed(gparts[gi], k, N)
 
     def timed_groups(label):
