@@ -10,8 +10,9 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from denseretrievaltoolkits_amd import _native  # noqa: E402
 
 
-def main(M=65536, reps=20):
+def main(M=65536, reps=20, variant=0):
     lib = _native.load()
+    lib.drt_gemm_force_small(variant)
     dev = torch.device("cuda", 0)
     g = torch.Generator(device=dev).manual_seed(0)
     cases = [("qkv_bias", 2304, 768, 0, True, False), ("qkv_none", 2304, 768, 0, False, False),
@@ -39,8 +40,10 @@ def main(M=65536, reps=20):
         torch.cuda.synchronize()
         ms = e0.elapsed_time(e1) / reps
         res[name] = {"us": round(ms * 1e3, 1), "tflops": round(2 * M * N * K / ms / 1e9, 1)}
-    print(json.dumps(res))
+    lib.drt_gemm_force_small(0)
+    print(json.dumps({"variant": variant, "epi": res}))
 
 
 if __name__ == "__main__":
-    main()
+    for v in (sys.argv[1].split(",") if len(sys.argv) > 1 else ["0"]):
+        main(variant=int(v))
