@@ -1040,151 +1040,44 @@ __global__ __launch_bounds__(kLThreads, 1) void gemm_nt_pp1_kernel(GemmArgs a) {
 }
 
 // ---------------------------------------------------------------------------
-// Ping-pong 256 x 256 kernel on whole-line K-tiles (round 3 of the encoder GEMM).
+// Whole-line K-tiles (the encoder projections' main path since round 2).
 //
-// pp1 lands 32-deep slabs: every LDS-DMA wave-instruction covers 16 rows x 64 B,
-// i.e. 16 HALF cache lines (the fragment-shaped pattern that doubles TA work per
-// byte).  Here a K-tile is 64 deep: one wave-instruction = 8 rows x 128 B (whole
-// lines), panel image [256 rows][8 x 16 B] with the 16-B chunk XOR (row & 7)
-// (conflict-free ds_read_b128 for every lane group of the 16x16x32 fragment map).
-//  * 2 K-tile buffers (2 x 64 KiB); tile t+1 is landed into the buffer tile t-1 used.
-//  * per wave and K-tile, two phases (k-half 0 / 1): memory segment (12 fragment
-//    reads) and matrix segment (32 v_mfma_f32_16x16x32_bf16), ping-ponged with the
-//    partner wave of the other group, which runs one s_barrier behind (as pp1).
-//  * intervals of K-tile t (G0 = waves 0-3, G1 = waves 4-7):
-//      4t   G0 mem(t,0) + DMA of tile t+1 | G1 mat(t-1,1)
-//      4t+1 G0 mat(t,0)                   | G1 mem(t,0) + DMA of tile t+1
-//      4t+2 G0 mem(t,1)                   | G1 mat(t,0)
-//      4t+3 G0 mat(t,1) + vmcnt(0)        | G1 mem(t,1) + vmcnt(0)
-//    WAR: tile t-1's last reads (G1 mem(t-1,1), interval 4t-1) drain (lgkmcnt(0))
-//    before the barrier that opens interval 4t.  RAW: both groups' DMAs of tile t+1
-//    are waited for before the barrier that closes interval 4t+3; G0 reads them in 4t+4.
-//  * ABL & 1: G1 issues its DMA of tile t+1 at the head of its mat(t-1,1) (interval
-//    4t, after that opening barrier) instead of in mem(t,0): one interval more lead.
-//  * swapped operands (D = W . X^T) and the LDS epilogue of pp1 (acc layout identical).
+// pp1 lands 32-deep slabs: every LDS-DMA wave-instruction covers 16 rows x 64 B, i.e. 16
+// HALF cache lines (the fragment-shaped pattern that doubles TA work per byte).  Here a
+// K-tile is 64 deep: one wave-instruction = 8 rows x 128 B (whole lines), panel image
+// [256 rows][8 x 16 B] with the 16-B chunk XOR (row & 7) (conflict-free ds_read_b128 for
+// every lane group of the 16x16x32 fragment map).  Measured on the way (tools/gemm_ab.py,
+// profiles/r02m_gemm_ab.log): the same ping-pong on two 64-KiB K-tile buffers (8 DMA per
+// wave in one memory segment, none in the other) gained only 1-6 % over pp1; the panel ring
+// below spreads them 4 + 4 and gains 5-18 %; a persistent form of the ring (panel stream
+// across tiles, next tile's first panels landing during the epilogue) measured no faster.
 // ---------------------------------------------------------------------------
 constexpr int kQPanel = kL * 128;        // 32 KiB: 256 rows x 64 k
-constexpr int kQTile = 2 * kQPanel;      // 64 KiB
 
 // 256 rows x 64 k into a [row][8 x 16 B] panel (chunk ^= row & 7): 32 wave-instructions
-// of 8 whole rows, 4 per wave.
+// of 8 whole rows, 4 per wave.  Lane l covers row 8J + (l >> 3), chunk (l & 7) ^ (l >> 3): its
+// byte offset from the wave-uniform row-block address is a per-lane constant (one VGPR), the
+// block address lives in SGPRs.  Rows past `rows` are clamped (masked in the epilogue): only a
+// row block that crosses `rows` takes the per-lane clamp.
+__device__ __forceinline__ int panel64_lane_off(int64_t ld, int lane) {
+  const int rsub = lane >> 3;
+  return (int)(rsub * ld * 2) + (((lane & 7) ^ rsub) << 4);
+}
 __device__ __forceinline__ void stage_panel64(const __bf16* base, int64_t ld, int64_t row0, int64_t rows,
-                                              int64_t k0, uint32_t lds, int wave, int lane) {
-  const int rsub = lane >> 3, pos = lane & 7;
+                                              int64_t k0, uint32_t lds, int wave, int lane, int lane_off) {
 #pragma unroll
   for (int j = 0; j < 4; ++j) {
     const int J = j * 8 + wave;           // 0..31
-    const int row = J * 8 + rsub;         // 0..255
-    int64_t gr = row0 + row;
-    gr = gr < rows ? gr : rows - 1;
-    const int c = pos ^ (row & 7);
-    g_glds16(base + gr * ld + k0 + c * 8, __builtin_amdgcn_readfirstlane(lds + J * 1024));
+    const int64_t r = row0 + J * 8;       // wave-uniform
+    const char* p = (const char*)(base + r * ld + k0);
+    int off = lane_off;
+    if (r + 8 > rows) {
+      const int rsub = lane >> 3;
+      const int64_t gr = r + rsub < rows ? r + rsub : rows - 1;
+      off = (int)((gr - r) * ld * 2) + (((lane & 7) ^ rsub) << 4);
+    }
+    g_glds16(p + off, __builtin_amdgcn_readfirstlane(lds + J * 1024));
   }
-}
-
-template <bool OUT_BF16, int EPI, int ABL = 0>
-__global__ __launch_bounds__(kLThreads, 1) void gemm_nt_pp64_kernel(GemmArgs a) {
-  __shared__ __attribute__((aligned(16))) char smem[2 * kQTile];
-  const int tid = threadIdx.x;
-  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int lane = tid & 63;
-  const int grp = wave >> 2;
-  const int wn = wave & 3;
-  constexpr bool kEarly = ABL & 1;
-
-  const int nwg = gridDim.x;
-  const int bid = blockIdx.x;
-  const int xcd = bid & 7, q8 = nwg >> 3, r8 = nwg & 7;
-  const int wg = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (bid >> 3);
-  const int tiles_n = (int)((a.n + kL - 1) / kL);
-  int tm, tn;
-  tile_order(a.order, wg, nwg, tiles_n, tm, tn);
-  const int64_t m0 = (int64_t)tm * kL;
-  const int64_t n0 = (int64_t)tn * kL;
-  const uint32_t lds0 = g_lds_addr(smem);
-  const int nt = (int)(a.k / 64);
-
-  f32x4 acc[8][4];
-#pragma unroll
-  for (int i = 0; i < 8; ++i)
-#pragma unroll
-    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-
-  const int fr = lane & 15, fc = lane >> 4;
-  const int foff0 = fr * 128 + ((fc ^ (fr & 7)) << 4);
-  const int foff1 = fr * 128 + (((4 + fc) ^ (fr & 7)) << 4);
-  const int xbase = grp * 128 * 128;
-  const int wbase = kQPanel + wn * 64 * 128;
-  auto stage = [&](int t, int b) {
-    const uint32_t dst = lds0 + b * kQTile;
-    stage_panel64(a.A, a.lda, m0, a.m, (int64_t)t * 64, dst, wave, lane);
-    stage_panel64(a.B, a.ldb, n0, a.n, (int64_t)t * 64, dst + kQPanel, wave, lane);
-  };
-
-  // prologue: tile 0 landed (G1 with kEarly also has tile 1 in flight)
-  stage(0, 0);
-  if (kEarly && grp == 1 && nt > 1) {
-    stage(1, 1);
-    asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
-  } else {
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  }
-  __builtin_amdgcn_s_barrier();
-  if (grp == 1) __builtin_amdgcn_s_barrier();
-  __builtin_amdgcn_sched_barrier(0);
-
-  for (int t = 0; t < nt; ++t) {
-    const char* buf = smem + (t & 1) * kQTile;
-    bf16x8 wf[4], xf[8];
-    // ---- phase 0: memory segment
-#pragma unroll
-    for (int j = 0; j < 4; ++j) wf[j] = *(const bf16x8*)(buf + wbase + j * 16 * 128 + foff0);
-#pragma unroll
-    for (int i = 0; i < 8; ++i) xf[i] = *(const bf16x8*)(buf + xbase + i * 16 * 128 + foff0);
-    if (t + 1 < nt && !(kEarly && grp == 1)) stage(t + 1, (t + 1) & 1);
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    __builtin_amdgcn_sched_barrier(0);
-    __builtin_amdgcn_s_barrier();
-    // ---- phase 0: matrix segment
-    __builtin_amdgcn_sched_barrier(0);
-    __builtin_amdgcn_s_setprio(1);
-#pragma unroll
-    for (int i = 0; i < 8; ++i)
-#pragma unroll
-      for (int j = 0; j < 4; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[j], xf[i], acc[i][j], 0, 0, 0);
-    __builtin_amdgcn_s_setprio(0);
-    __builtin_amdgcn_sched_barrier(0);
-    __builtin_amdgcn_s_barrier();
-    // ---- phase 1: memory segment
-#pragma unroll
-    for (int j = 0; j < 4; ++j) wf[j] = *(const bf16x8*)(buf + wbase + j * 16 * 128 + foff1);
-#pragma unroll
-    for (int i = 0; i < 8; ++i) xf[i] = *(const bf16x8*)(buf + xbase + i * 16 * 128 + foff1);
-    if (grp == 1) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    __builtin_amdgcn_sched_barrier(0);
-    __builtin_amdgcn_s_barrier();
-    // ---- phase 1: matrix segment (G1 with kEarly: DMA of tile t+2 first; its buffer's last
-    // reads, G1's own mem(t,1) and G0's mem(t,1), drained before the barrier just passed)
-    __builtin_amdgcn_sched_barrier(0);
-    if (kEarly && grp == 1 && t + 2 < nt) stage(t + 2, t & 1);
-    __builtin_amdgcn_sched_barrier(0);
-    __builtin_amdgcn_s_setprio(1);
-#pragma unroll
-    for (int i = 0; i < 8; ++i)
-#pragma unroll
-      for (int j = 0; j < 4; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[j], xf[i], acc[i][j], 0, 0, 0);
-    __builtin_amdgcn_s_setprio(0);
-    __builtin_amdgcn_sched_barrier(0);
-    if (grp == 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __builtin_amdgcn_s_barrier();
-  }
-  if (grp == 0) __builtin_amdgcn_s_barrier();
-  // every wave's reads drained and no DMA in flight: the whole LDS is free for the epilogue
-  const bool full = (n0 + kL <= a.n) && (a.ldc % 8 == 0) && (!(EPI & EPI_AUX) || a.ldr % 4 == 0);
-  bf16x4 rv0[16];
-  if (full) pp_epilogue_lds<OUT_BF16, EPI, false>(a, acc, m0, n0, grp, wn, fr, fc, smem + wave * 16384, lane, rv0);
-  else pp_epilogue<OUT_BF16, EPI>(a, acc, m0, n0, grp, wn, fr, fc);
 }
 
 // ---------------------------------------------------------------------------
@@ -1192,13 +1085,13 @@ __global__ __launch_bounds__(kLThreads, 1) void gemm_nt_pp64_kernel(GemmArgs a) 
 // operand panel of one K-tile (X_t or W_t, [256 rows][128 B] = 32 KiB), panel P = 2t + op
 // in slot P mod 5.  While tile t is read (its 2 panels), the other 3 slots take W_{t+1}
 // and X_{t+2}: X panels land 1.5 K-tiles ahead, W panels one ahead, and every memory
-// segment carries 4 LDS-DMA per wave instead of pp64's 8-then-0.
+// segment carries 4 LDS-DMA per wave (the 2-buffer form carried 8, then 0).
 //   mem(t,0): 12 fragment reads (k-half 0) + W_{t+1} (into X_{t-1}'s slot)
 //   mat(t,0): 32 MFMA
 //   mem(t,1): 12 fragment reads (k-half 1) + X_{t+2} (into W_{t-1}'s slot), then
 //             vmcnt(4): X_{t+1} and W_{t+1} landed (X_{t+2} may stay in flight)
 //   mat(t,1): 32 MFMA
-// G1 one barrier behind G0 as in pp1 / pp64.  WAR: X_{t-1} and W_{t-1} were last read in
+// G1 one barrier behind G0 as in pp1.  WAR: X_{t-1} and W_{t-1} were last read in
 // G1's mem(t-1,1) (interval 4t-1), drained before the barrier that opens 4t, the first
 // interval in which any wave stages into their slots.  RAW: both groups wait in their
 // mem(t,1) (intervals 4t+2 / 4t+3) before the barrier that closes 4t+3; tile t+1 is first
@@ -1234,13 +1127,14 @@ __global__ __launch_bounds__(kLThreads, 1) void gemm_nt_pr5_kernel(GemmArgs a) {
   const int fr = lane & 15, fc = lane >> 4;
   const int foff0 = fr * 128 + ((fc ^ (fr & 7)) << 4);
   const int foff1 = fr * 128 + (((4 + fc) ^ (fr & 7)) << 4);
+  const int loffA = panel64_lane_off(a.lda, lane), loffB = panel64_lane_off(a.ldb, lane);
   const int xrow = grp * 128 * 128;
   const int wrow = wn * 64 * 128;
   auto stage_x = [&](int t, int slot) {
-    stage_panel64(a.A, a.lda, m0, a.m, (int64_t)t * 64, lds0 + slot * kQPanel, wave, lane);
+    stage_panel64(a.A, a.lda, m0, a.m, (int64_t)t * 64, lds0 + slot * kQPanel, wave, lane, loffA);
   };
   auto stage_w = [&](int t, int slot) {
-    stage_panel64(a.B, a.ldb, n0, a.n, (int64_t)t * 64, lds0 + slot * kQPanel, wave, lane);
+    stage_panel64(a.B, a.ldb, n0, a.n, (int64_t)t * 64, lds0 + slot * kQPanel, wave, lane, loffB);
   };
 
   // prologue: X_0 (slot 0), W_0 (slot 1) landed, X_1 (slot 2) in flight
@@ -1324,11 +1218,6 @@ static int launch_gemm_t(const GemmArgs& a0, hipStream_t s) {
   constexpr bool kBasicEpi = (EPI & ~(EPI_BIAS | EPI_GELU | EPI_RESID)) == 0;
   if (tiles_l >= g_large_min_tiles && g_gemm_variant == 12) {
     hipLaunchKernelGGL((gemm_nt_pr5_kernel<OUT_BF16, EPI>), dim3((unsigned)tiles_l), dim3(kLThreads), 0, s, a);
-  } else if (tiles_l >= g_large_min_tiles && (g_gemm_variant == 10 || g_gemm_variant == 11)) {
-    if (g_gemm_variant == 10)
-      hipLaunchKernelGGL((gemm_nt_pp64_kernel<OUT_BF16, EPI, 0>), dim3((unsigned)tiles_l), dim3(kLThreads), 0, s, a);
-    else
-      hipLaunchKernelGGL((gemm_nt_pp64_kernel<OUT_BF16, EPI, 1>), dim3((unsigned)tiles_l), dim3(kLThreads), 0, s, a);
   } else if (tiles_l >= g_large_min_tiles && (g_gemm_variant == 0 || !kBasicEpi)) {
     // round 2: whole-line K-tiles in the 5-slot panel ring (tools/gemm_ab.py: +5-18 % over pp1,
     // bit-identical outputs)

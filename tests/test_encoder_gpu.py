@@ -100,7 +100,7 @@ def test_large_tile_gemm_vs_torch_and_small_kernel(dev, M, N, K, flags):
     """256x256-tile kernels (>= 512 tiles) against torch fp32 and the 128x128 kernel.
     Variants: 0 auto (whole-line panel ring, = 12), 1 128x128, 2 half-K ring,
     7 / 8 ping-pong on 32-deep slabs (4 / 5-slot ring), 9 full-K 32x32x16 kernel,
-    10 ping-pong on 64-deep whole-line K-tiles (2 buffers), 12 the 5-slot panel ring."""
+    12 the whole-line 5-slot panel ring."""
     import torch
     from denseretrievaltoolkits_amd import _native
     lib = _native.load()
@@ -117,7 +117,7 @@ def test_large_tile_gemm_vs_torch_and_small_kernel(dev, M, N, K, flags):
         ref = ref + r.float()
     dt = torch.float32 if flags & 2 else torch.bfloat16
     outs = []
-    variants = (0, 1, 2, 7, 8, 9, 10, 12)
+    variants = (0, 1, 2, 7, 8, 9, 12)
     for force in variants:
         lib.drt_gemm_force_small(force)
         out = torch.empty(M, N, dtype=dt, device=dev)
@@ -135,7 +135,7 @@ def test_large_tile_gemm_vs_torch_and_small_kernel(dev, M, N, K, flags):
         by = dict(zip(variants, outs))
         assert torch.equal(by[1], by[2]) and torch.equal(by[1], by[9])
         assert torch.equal(by[0], by[7]) and torch.equal(by[0], by[8])
-        assert torch.equal(by[0], by[10]) and torch.equal(by[0], by[12])
+        assert torch.equal(by[0], by[12])
 
 
 @pytest.mark.parametrize("M,H", [(1, 768), (1003, 768), (64, 256), (37, 1024)])
