@@ -303,6 +303,27 @@ static int small_splits(int64_t m, int64_t n, int64_t k, int64_t* kchunk) {
   return (int)splits;
 }
 
+// Split plan of the 256^2 whole-line kernel for mid-size problems (query batches of 1k-16k
+// tokens: fewer 256^2 tiles than g_large_min_tiles, i.e. the chip is not filled): splits so the
+// grid reaches ~one block per CU, >= g_msplit_min_kt K-tiles of 64 per split, fp32 partials
+// <= g_msplit_cap bytes.  M < g_msplit_min_m stays on the 128^2 kernel.  0 = no split (the
+// 256^2 kernel unsplit when M >= g_msplit_min_m).
+static int64_t g_msplit_min_m = 1 << 30, g_msplit_cap = 64 << 20, g_msplit_min_kt = 4;
+static int mid_splits(int64_t m, int64_t n, int64_t k, int64_t* kchunk) {
+  const int64_t tiles = ((m + 255) / 256) * ((n + 255) / 256);
+  int64_t splits = (256 + tiles - 1) / tiles;
+  if (splits > k / (64 * g_msplit_min_kt)) splits = k / (64 * g_msplit_min_kt);
+  const int64_t cap = g_msplit_cap / (m * n * 4);
+  if (splits > cap) splits = cap;
+  if (splits < 2) return 0;
+  int64_t kc = (k + splits - 1) / splits;
+  kc = (kc + 63) / 64 * 64;
+  splits = (k + kc - 1) / kc;
+  if (splits < 2) return 0;
+  *kchunk = kc;
+  return (int)splits;
+}
+
 // Split plan of the 256^2 kernel for long-K problems whose 256^2 grid is small (weight
 // gradients dW = dY^T X: K = tokens, M x N = a weight matrix): ~256 blocks, >= 16 slabs per
 // split, fp32 partials <= 256 MiB.  0 = no split.
@@ -806,19 +827,24 @@ __device__ __forceinline__ void pp_epilogue_lds(const GemmArgs& a, f32x4 (&acc)[
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     }
   } else {
-    // two passes of 64 rows: [64 rows][16 x 16 B] fp32, chunk ^= row & 7.  Residual rows
-    // of both passes are requested before any staging (pass 0's possibly in the K loop).
-    // bf16 output with a residual (pre-LayerNorm sums) also stages fp32, so the sum is
-    // rounded once, at the store (8-B pieces, 128-B row segments).
-    const int c = lane & 15;
-    bf16x4 rv1[16];
-    if (EPI & EPI_AUX) {
-      if (!PRE) load_resid_half(a, m0, n0, grp, wn, 0, lane, rv0);
-      load_resid_half(a, m0, n0, grp, wn, 1, lane, rv1);
-    }
+    // two passes of 64 rows: [64 rows][16 x 16 B] fp32, chunk ^= row & 7, read back as 8
+    // consecutive columns per lane (two chunks: conflict-free for every ds_read_b128 lane group),
+    // so residual loads and bf16 stores are 16 B per lane (fp32 stores 2 x 16 B).  bf16 output
+    // with a residual (pre-LayerNorm sums) stages fp32, so the sum is rounded once, at the store.
+    // Residual rows of pass 1 are requested once pass 0 is staged (its accumulators are dead).
+    const int c8 = lane & 7;
+    bf16x8 rq[2][8];
+    auto load_rq = [&](int h) {
+#pragma unroll
+      for (int p = 0; p < 8; ++p) {
+        int64_t row = m0 + grp * 128 + h * 64 + p * 8 + (lane >> 3);
+        row = row < a.m ? row : a.m - 1;
+        rq[h][p] = *(const bf16x8*)(a.R + row * a.ldr + colw + c8 * 8);
+      }
+    };
+    if (EPI & EPI_AUX) load_rq(0);
 #pragma unroll
     for (int h = 0; h < 2; ++h) {
-      const bf16x4 (&rv)[16] = h == 0 ? rv0 : rv1;
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
         const int r = i * 16 + fr;
@@ -838,24 +864,33 @@ __device__ __forceinline__ void pp_epilogue_lds(const GemmArgs& a, f32x4 (&acc)[
         }
       }
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      if ((EPI & EPI_AUX) && h == 0) load_rq(1);
 #pragma unroll
-      for (int p = 0; p < 16; ++p) {
-        const int r = p * 4 + (lane >> 4);
-        f32x4 v = *(const f32x4*)(lds_wave + r * 256 + ((c ^ (r & 7)) << 4));
+      for (int p = 0; p < 8; ++p) {
+        const int r = p * 8 + (lane >> 3);
+        const f32x4 v0 = *(const f32x4*)(lds_wave + r * 256 + (((2 * c8) ^ (r & 7)) << 4));
+        const f32x4 v1 = *(const f32x4*)(lds_wave + r * 256 + (((2 * c8 + 1) ^ (r & 7)) << 4));
         const int64_t row = m0 + grp * 128 + h * 64 + r;
         if (row < a.m) {
+          float v[8];
+#pragma unroll
+          for (int u = 0; u < 4; ++u) {
+            v[u] = v0[u];
+            v[4 + u] = v1[u];
+          }
           if (EPI & (EPI_AUX | EPI_DROP)) {
 #pragma unroll
-            for (int u = 0; u < 4; ++u)
-              v[u] = epi_post<EPI>(a, v[u], row, colw + c * 4 + u, (EPI & EPI_AUX) ? (float)rv[p][u] : 0.f);
+            for (int u = 0; u < 8; ++u)
+              v[u] = epi_post<EPI>(a, v[u], row, colw + c8 * 8 + u, (EPI & EPI_AUX) ? (float)rq[h][p][u] : 0.f);
           }
           if (OUT_BF16) {
-            bf16x4 o;
+            bf16x8 o;
 #pragma unroll
-            for (int u = 0; u < 4; ++u) o[u] = (__bf16)v[u];
-            *(bf16x4*)((__bf16*)a.C + row * a.ldc + colw + c * 4) = o;
+            for (int u = 0; u < 8; ++u) o[u] = (__bf16)v[u];
+            *(bf16x8*)((__bf16*)a.C + row * a.ldc + colw + c8 * 8) = o;
           } else {
-            *(f32x4*)((float*)a.C + row * a.ldc + colw + c * 4) = v;
+            *(f32x4*)((float*)a.C + row * a.ldc + colw + c8 * 8) = f32x4{v[0], v[1], v[2], v[3]};
+            *(f32x4*)((float*)a.C + row * a.ldc + colw + c8 * 8 + 4) = f32x4{v[4], v[5], v[6], v[7]};
           }
         }
       }
@@ -1013,7 +1048,7 @@ __global__ __launch_bounds__(kLThreads, 1) void gemm_nt_pp1_kernel(GemmArgs a) {
   }
   if (grp == 0 && !(ABL & 4)) __builtin_amdgcn_s_barrier();
   if (ABL & 32) st2 = __builtin_amdgcn_s_memtime();
-  const bool full = (n0 + kL <= a.n) && (a.ldc % 8 == 0) && (!(EPI & EPI_AUX) || a.ldr % 4 == 0);
+  const bool full = (n0 + kL <= a.n) && (a.ldc % 8 == 0) && (!(EPI & EPI_AUX) || a.ldr % 8 == 0);
   if (full) {
     GemmArgs ae = a;
     if (a.kchunk) ae.C = (float*)a.C + (int64_t)blockIdx.y * a.m * a.ldc;
@@ -1116,7 +1151,11 @@ __global__ __launch_bounds__(kLThreads, 1) void gemm_nt_pr5_kernel(GemmArgs a) {
   const int64_t m0 = (int64_t)tm * kL;
   const int64_t n0 = (int64_t)tn * kL;
   const uint32_t lds0 = g_lds_addr(smem);
-  const int nt = (int)(a.k / 64);
+  // split-K (kchunk > 0): this block sums k in [kb, kb + kchunk) of split blockIdx.y and stores raw
+  // fp32 partials at C + blockIdx.y * m * ldc (splitk_epi_kernel finishes in a fixed split order)
+  const int64_t kb = a.kchunk ? (int64_t)blockIdx.y * a.kchunk : 0;
+  const int64_t ke = a.kchunk ? (kb + a.kchunk < a.k ? kb + a.kchunk : a.k) : a.k;
+  const int nt = (int)((ke - kb) / 64);
 
   f32x4 acc[8][4];
 #pragma unroll
@@ -1131,10 +1170,10 @@ __global__ __launch_bounds__(kLThreads, 1) void gemm_nt_pr5_kernel(GemmArgs a) {
   const int xrow = grp * 128 * 128;
   const int wrow = wn * 64 * 128;
   auto stage_x = [&](int t, int slot) {
-    stage_panel64(a.A, a.lda, m0, a.m, (int64_t)t * 64, lds0 + slot * kQPanel, wave, lane, loffA);
+    stage_panel64(a.A, a.lda, m0, a.m, kb + (int64_t)t * 64, lds0 + slot * kQPanel, wave, lane, loffA);
   };
   auto stage_w = [&](int t, int slot) {
-    stage_panel64(a.B, a.ldb, n0, a.n, (int64_t)t * 64, lds0 + slot * kQPanel, wave, lane, loffB);
+    stage_panel64(a.B, a.ldb, n0, a.n, kb + (int64_t)t * 64, lds0 + slot * kQPanel, wave, lane, loffB);
   };
 
   // prologue: X_0 (slot 0), W_0 (slot 1) landed, X_1 (slot 2) in flight
@@ -1200,10 +1239,12 @@ __global__ __launch_bounds__(kLThreads, 1) void gemm_nt_pr5_kernel(GemmArgs a) {
     xs = xs + 2 >= 5 ? xs - 3 : xs + 2;
   }
   if (grp == 0) __builtin_amdgcn_s_barrier();
-  const bool full = (n0 + kL <= a.n) && (a.ldc % 8 == 0) && (!(EPI & EPI_AUX) || a.ldr % 4 == 0);
+  GemmArgs ae = a;
+  if (a.kchunk) ae.C = (float*)a.C + (int64_t)blockIdx.y * a.m * a.ldc;
+  const bool full = (n0 + kL <= a.n) && (a.ldc % 8 == 0) && (!(EPI & EPI_AUX) || a.ldr % 8 == 0);
   bf16x4 rv0[16];
-  if (full) pp_epilogue_lds<OUT_BF16, EPI, false>(a, acc, m0, n0, grp, wn, fr, fc, smem + wave * 16384, lane, rv0);
-  else pp_epilogue<OUT_BF16, EPI>(a, acc, m0, n0, grp, wn, fr, fc);
+  if (full) pp_epilogue_lds<OUT_BF16, EPI, false>(ae, acc, m0, n0, grp, wn, fr, fc, smem + wave * 16384, lane, rv0);
+  else pp_epilogue<OUT_BF16, EPI>(ae, acc, m0, n0, grp, wn, fr, fc);
 }
 
 template <bool OUT_BF16, int EPI>
@@ -1218,6 +1259,26 @@ static int launch_gemm_t(const GemmArgs& a0, hipStream_t s) {
   constexpr bool kBasicEpi = (EPI & ~(EPI_BIAS | EPI_GELU | EPI_RESID)) == 0;
   if (tiles_l >= g_large_min_tiles && g_gemm_variant == 12) {
     hipLaunchKernelGGL((gemm_nt_pr5_kernel<OUT_BF16, EPI>), dim3((unsigned)tiles_l), dim3(kLThreads), 0, s, a);
+  } else if (tiles_l < g_large_min_tiles && a.m >= g_msplit_min_m && g_gemm_variant == 0 && a.k < g_lsplit_min_k) {
+    // mid-size: the whole-line kernel, K split over ~one block per CU when the caller gave scratch
+    int64_t kc = 0;
+    const int splits = a.ws ? mid_splits(a.m, a.n, a.k, &kc) : 0;
+    if (splits > 1) {
+      GemmArgs b = a;
+      b.kchunk = kc;
+      b.C = a.ws;
+      b.ldc = a.n;
+      b.bias = nullptr;
+      b.R = nullptr;
+      b.alpha = 1.0f;
+      hipLaunchKernelGGL((gemm_nt_pr5_kernel<false, EPI_NONE>), dim3((unsigned)tiles_l, (unsigned)splits),
+                         dim3(kLThreads), 0, s, b);
+      const int64_t units = (a.n % 4 == 0) ? a.m * a.n / 4 : a.m * a.n;
+      const int64_t blocks = (units + 255) / 256 < 4096 ? (units + 255) / 256 : 4096;
+      hipLaunchKernelGGL((splitk_epi_kernel<OUT_BF16, EPI>), dim3((unsigned)blocks), dim3(256), 0, s, a, splits);
+    } else {
+      hipLaunchKernelGGL((gemm_nt_pr5_kernel<OUT_BF16, EPI>), dim3((unsigned)tiles_l), dim3(kLThreads), 0, s, a);
+    }
   } else if (tiles_l >= g_large_min_tiles && (g_gemm_variant == 0 || !kBasicEpi)) {
     // round 2: whole-line K-tiles in the 5-slot panel ring (tools/gemm_ab.py: +5-18 % over pp1,
     // bit-identical outputs)
@@ -1353,6 +1414,10 @@ extern "C" size_t drt_linear_workspace(int64_t M, int64_t N, int64_t K) {
   const int64_t tiles_l = ((M + kL - 1) / kL) * ((N + kL - 1) / kL);
   if (tiles_l >= g_large_min_tiles) return 0;   // the 256^2 path does not split
   int64_t kc = 0;
+  if (M >= g_msplit_min_m && K < g_lsplit_min_k) {
+    const int ms = mid_splits(M, N, K, &kc);
+    return ms > 1 ? (size_t)ms * (size_t)M * (size_t)N * sizeof(float) : 0;
+  }
   const int ls = large_splits(M, N, K, g_large_min_tiles, &kc);
   if (ls > 1) return (size_t)ls * (size_t)M * (size_t)N * sizeof(float);
   const int splits = small_splits(M, N, K, &kc);
@@ -1510,6 +1575,16 @@ extern "C" int drt_gemm_split_config(int64_t large_min_k, int64_t large_k_per_sp
   if (large_min_k > 0) g_lsplit_min_k = large_min_k;
   if (large_k_per_split > 0) g_lsplit_k_per = large_k_per_split;
   if (small_cap_bytes > 0) g_ssplit_cap = small_cap_bytes;
+  return DRT_OK;
+}
+
+// Benchmark switch of the mid-size plan (mid_splits): M from which problems below the 256^2
+// threshold take the whole-line kernel (split over ~one block per CU), the fp32 partials cap and
+// the minimum K-tiles per split.  Non-positive arguments keep the current value.
+extern "C" int drt_gemm_mid_config(int64_t min_m, int64_t cap_bytes, int64_t min_ktiles) {
+  if (min_m > 0) g_msplit_min_m = min_m;
+  if (cap_bytes > 0) g_msplit_cap = cap_bytes;
+  if (min_ktiles > 0) g_msplit_min_kt = min_ktiles;
   return DRT_OK;
 }
 

@@ -294,6 +294,11 @@ int drt_gemm_force_small(int32_t on);
  * small_cap_bytes (16 MiB).  Non-positive arguments keep the current value.                 */
 int drt_gemm_split_config(int64_t large_min_k, int64_t large_k_per_split, int64_t small_cap_bytes);
 int drt_gemm_large_min_tiles(int64_t tiles);
+/* Benchmark switch of the mid-size GEMM plan: problems below the 256x256 threshold with
+ * M >= min_m take the whole-line 256x256 kernel, K split over ~one block per CU (fp32 partials
+ * <= cap_bytes, >= min_ktiles K-tiles of 64 per split) when drt_linear_bf16_ws gets scratch
+ * (drt_linear_workspace sizes it).  Non-positive arguments keep the current value.          */
+int drt_gemm_mid_config(int64_t min_m, int64_t cap_bytes, int64_t min_ktiles);
 /* Diagnostic only: device buffer for the GEMM cycle-stamp variants (drt_gemm_force_small >= 16). */
 int drt_gemm_debug_buffer(void* buf);
 /* Benchmark switch: tile order of the 256x256 ping-pong GEMM inside each XCD's tile range
