@@ -327,10 +327,27 @@ static int mid_splits(int64_t m, int64_t n, int64_t k, int64_t* kchunk) {
 // Split plan of the 256^2 kernel for long-K problems whose 256^2 grid is small (weight
 // gradients dW = dY^T X: K = tokens, M x N = a weight matrix): ~256 blocks, >= 16 slabs per
 // split, fp32 partials <= 256 MiB.  0 = no split.
+// Compute units of the current device, looked up once per process.
+static int gemm_cus() {
+  static int cus = 0;
+  if (cus == 0) {
+    int dev = 0, v = 0;
+    cus = (hipGetDevice(&dev) == hipSuccess &&
+           hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess && v > 0)
+              ? v
+              : 256;
+  }
+  return cus;
+}
+
+// Round 2: at most ONE round of blocks (floor(CUs / tiles) splits): the ceiling this plan used
+// before put e.g. 9 tiles x 29 splits = 261 blocks on 256 CUs, so 5 blocks ran a second full
+// round and the launch took ~2x its one-round time (drt_gemm_force_small(14) restores it for A/B).
 static int large_splits(int64_t m, int64_t n, int64_t k, int64_t min_tiles, int64_t* kchunk) {
   const int64_t tiles = ((m + 255) / 256) * ((n + 255) / 256);
   if (tiles >= min_tiles || k < g_lsplit_min_k || k % 32) return 0;
-  int64_t splits = (256 + tiles - 1) / tiles;
+  const int64_t cus = gemm_cus();
+  int64_t splits = g_gemm_variant == 14 ? (256 + tiles - 1) / tiles : cus / tiles;
   if (splits > k / g_lsplit_k_per) splits = k / g_lsplit_k_per;
   const int64_t cap = (int64_t)(256ll << 20) / (m * n * 4);
   if (splits > cap) splits = cap;
