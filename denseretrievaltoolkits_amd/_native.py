@@ -89,6 +89,7 @@ _SIGNATURES = [
     ("drt_gemm_large_min_tiles", c_i32, [c_i64]),
     ("drt_gemm_mid_config", c_i32, [c_i64, c_i64, c_i64]),
     ("drt_gemm_force_small", c_i32, [c_i32]),
+    ("drt_attention_force4", c_i32, [c_i32]),
     ("drt_gemm_debug_buffer", c_i32, [c_vp]),
     ("drt_gemm_tile_order", c_i32, [c_i32]),
     ("drt_gemm_nt_f32", c_i32, [c_vp, c_vp, c_vp, c_i64, c_i64, c_i64, c_i64, c_i64, c_i64, c_vp]),

@@ -192,6 +192,8 @@ __global__ __launch_bounds__(256) void layernorm_bf16_kernel(const __bf16* X, in
 // with a padded row stride (A operand of O^T = V^T P^T).
 // ---------------------------------------------------------------------------
 constexpr int kAttnThreads = 256;
+// A/B switch (drt_attention_force4): 1 keeps 4-wave work-groups at every length
+static int g_attn_force4 = 0;
 constexpr int kHeadDim = 64;
 constexpr int kMaxSeq = 512;
 
@@ -208,8 +210,12 @@ struct AttnArgs {
   uint64_t seed, site;    //   mask = drop_hash24(seed, site, ((b * heads + head) * L + q) * L + key)
 };
 
-template <bool DROP>
-__global__ __launch_bounds__(kAttnThreads, 4) void attention_kernel(AttnArgs a) {
+// NW = waves per work-group (the launcher uses 4; an 8-wave form for 5-8 query blocks measured
+// slower, see drt_attention_train_fwd_bf16).  Each block's arithmetic is the same whichever wave
+// runs it.
+template <bool DROP, int NW = 4>
+__global__ __launch_bounds__(NW * 64, NW == 4 ? 4 : 2) void attention_kernel(AttnArgs a) {
+  constexpr int NT = NW * 64;
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int L = (int)a.L;
   const int Lp = (L + 31) & ~31;           // keys padded to the 32-key tile
@@ -229,7 +235,7 @@ __global__ __launch_bounds__(kAttnThreads, 4) void attention_kernel(AttnArgs a) 
   const __bf16* Kg = Qg + a.H;
   const __bf16* Vg = Qg + 2 * a.H;
 
-  // ---- stage K (swizzled rows) and V^T, key bias.  Passes of 128 keys: thread (key group
+  // ---- stage K (swizzled rows) and V^T, key bias.  Passes of NT / 2 keys: thread (key group
   // kg = tid >> 3, 16-B chunk c = tid & 7) owns keys 4 kg .. 4 kg + 3 of chunk c, issues all 8
   // global loads of the pass before any LDS store, and writes V^T as 8 ds_write_b64 (4 keys
   // of one d per store) instead of 32 ds_write_b16.  The first Q block's fragments are
@@ -240,7 +246,7 @@ __global__ __launch_bounds__(kAttnThreads, 4) void attention_kernel(AttnArgs a) 
   bf16x8 q0[4];
 #pragma unroll
   for (int st = 0; st < 4; ++st) q0[st] = *(const bf16x8*)(Qg + (int64_t)qrow0 * ld + st * 16 + (lane >> 5) * 8);
-  for (int kp = 0; kp < Lp; kp += 128) {
+  for (int kp = 0; kp < Lp; kp += NT / 2) {
     u32x4 kv[4], vv[4];
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
@@ -269,7 +275,7 @@ __global__ __launch_bounds__(kAttnThreads, 4) void attention_kernel(AttnArgs a) 
       }
     }
   }
-  for (int i = tid; i < Lp; i += kAttnThreads) {
+  for (int i = tid; i < Lp; i += NT) {
     float bv = 0.0f;
     if (i >= L) bv = -3.402823466e+38f;
     else if (a.mask && a.mask[b * a.L + i] == 0) bv = -3.402823466e+38f;  // (1 - mask) * finfo.min
@@ -279,7 +285,7 @@ __global__ __launch_bounds__(kAttnThreads, 4) void attention_kernel(AttnArgs a) 
 
   const int sw = (r >> 1) & 7;
   const int nqb = Lp / 32;
-  for (int qb = wave; qb < nqb; qb += 4) {
+  for (int qb = wave; qb < nqb; qb += NW) {
     // Q fragment (B operand, B[k=d][col=q] = Q[q][d]) scaled by 1/sqrt(dh)
     int qrow = qb * 32 + r;
     qrow = qrow < L ? qrow : L - 1;
@@ -441,6 +447,15 @@ using namespace drt;
 
 extern "C" {
 
+// Benchmark / test switch: 1 keeps the 4-wave attention BACKWARD work-groups at every sequence
+// length, 0 (default) takes 8 waves for 5 blocks (L 129-160; tools/attn_bwd_probe.py).
+int drt_attention_force4(int32_t on) {
+  if (on < 0 || on > 1) return DRT_EINVAL;
+  g_attn_force4 = on;
+  return DRT_OK;
+}
+int drt_attention_force4_get(void) { return g_attn_force4; }
+
 int drt_embed_ln_pre(const int64_t* ids, const int64_t* type_ids, int64_t B, int64_t L, const float* word_emb,
                      const float* pos_emb, const float* type_emb, const float* gamma, const float* beta, float eps,
                      int32_t H, void* out, void* pre, void* stream);
@@ -566,18 +581,19 @@ int drt_attention_train_fwd_bf16(const void* qkv, const int64_t* mask, void* ctx
   const size_t lds = (size_t)Lp * 128 + (size_t)64 * (Lp * 2 + 8) + (size_t)Lp * 4;
   static bool attr_set = false;
   if (!attr_set) {
-    DRT_CHECK_HIP(hipFuncSetAttribute((const void*)attention_kernel<false>,
+    DRT_CHECK_HIP(hipFuncSetAttribute((const void*)attention_kernel<false, 4>,
                                       hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
-    DRT_CHECK_HIP(hipFuncSetAttribute((const void*)attention_kernel<true>,
+    DRT_CHECK_HIP(hipFuncSetAttribute((const void*)attention_kernel<true, 4>,
                                       hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
     attr_set = true;
   }
+  // 4 waves at every length: the 8-wave form (NW = 8) measured slower at L = 156 (570 vs 390 us
+  // with dropout: 130 VGPRs -> one work-group per CU instead of four), unlike the backward
+  const dim3 grid((unsigned)(B * heads));
   if (drop_p > 0.0f)
-    hipLaunchKernelGGL(attention_kernel<true>, dim3((unsigned)(B * heads)), dim3(kAttnThreads), lds,
-                       (hipStream_t)stream, a);
+    hipLaunchKernelGGL((attention_kernel<true, 4>), grid, dim3(256), lds, (hipStream_t)stream, a);
   else
-    hipLaunchKernelGGL(attention_kernel<false>, dim3((unsigned)(B * heads)), dim3(kAttnThreads), lds,
-                       (hipStream_t)stream, a);
+    hipLaunchKernelGGL((attention_kernel<false, 4>), grid, dim3(256), lds, (hipStream_t)stream, a);
   return hip_status(hipGetLastError());
 }
 

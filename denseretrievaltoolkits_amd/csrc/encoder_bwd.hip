@@ -286,7 +286,12 @@ __device__ __forceinline__ bf16x8 ab_tr8(const char* img, int row0, int col0, in
   return v;
 }
 
-__global__ __launch_bounds__(kAbThreads, 2) void attention_bwd_kernel(AttnBwdArgs a) {
+// NW = waves per work-group: 4 for L <= 128 (one 32-row block per wave in each phase), 8 for
+// 129 <= L <= 160 (5 blocks: 4 waves ran wave 0 twice per phase while 3 waves idled); the LDS
+// (92-104 KiB at L = 160) allows one work-group per CU either way.  Bit-identical block math.
+template <int NW = 4>
+__global__ __launch_bounds__(NW * 64, NW == 4 ? 2 : 1) void attention_bwd_kernel(AttnBwdArgs a) {
+  constexpr int NT = NW * 64;
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int L = (int)a.L;
   const int Lp = (L + 31) & ~31;
@@ -294,8 +299,8 @@ __global__ __launch_bounds__(kAbThreads, 2) void attention_bwd_kernel(AttnBwdArg
   char* Ks = Qs + Lp * kAbRow;
   char* Vs = Ks + Lp * kAbRow;
   char* Os = Vs + Lp * kAbRow;                       // dO
-  char* scr = Os + Lp * kAbRow;                      // [4 waves][32][80 B]
-  float* lse = (float*)(scr + 4 * 32 * kAbScr);      // [Lp]
+  char* scr = Os + Lp * kAbRow;                      // [NW waves][32][80 B]
+  float* lse = (float*)(scr + NW * 32 * kAbScr);     // [Lp]
   float* dv = lse + Lp;                              // [Lp]  Dv
   float* kb = dv + Lp;                               // [Lp]  key bias
 
@@ -312,7 +317,7 @@ __global__ __launch_bounds__(kAbThreads, 2) void attention_bwd_kernel(AttnBwdArg
   const __bf16* dOg = a.dctx + row0 * a.H + hd * 64;
 
   // ---- staging: rows (row-major images) and the transposed images, element by element
-  for (int i = tid; i < Lp * 8; i += kAbThreads) {
+  for (int i = tid; i < Lp * 8; i += NT) {
     const int row = i >> 3, c = i & 7;
     bf16x8 q = {}, k = {}, v = {}, o = {}, oo = {};
     if (row < L) {
@@ -338,7 +343,7 @@ __global__ __launch_bounds__(kAbThreads, 2) void attention_bwd_kernel(AttnBwdArg
     part += __shfl_xor(part, 4, 64);
     if (c == 0) dv[row] = part;
   }
-  for (int i = tid; i < Lp; i += kAbThreads) {
+  for (int i = tid; i < Lp; i += NT) {
     float bv = 0.0f;
     if (i >= L) bv = -3.402823466e+38f;
     else if (a.mask && a.mask[b * a.L + i] == 0) bv = -3.402823466e+38f;
@@ -354,7 +359,7 @@ __global__ __launch_bounds__(kAbThreads, 2) void attention_bwd_kernel(AttnBwdArg
   char* sT = scr + wave * 32 * kAbScr;   // P, then dS (phase 1); dS (phase 2)
 
   // ---- phase 1: dK, dV for key block kbk (rows = keys in the D layout, cols = q / d)
-  for (int kbk = wave; kbk < nblk; kbk += 4) {
+  for (int kbk = wave; kbk < nblk; kbk += NW) {
     f32x16 dK[2], dV[2];
 #pragma unroll
     for (int t = 0; t < 2; ++t)
@@ -451,7 +456,7 @@ __global__ __launch_bounds__(kAbThreads, 2) void attention_bwd_kernel(AttnBwdArg
   }
 
   // ---- phase 2: dQ for query block qbq (rows = queries, cols = keys / d)
-  for (int qbq = wave; qbq < nblk; qbq += 4) {
+  for (int qbq = wave; qbq < nblk; qbq += NW) {
     f32x16 dQ[2];
 #pragma unroll
     for (int t = 0; t < 2; ++t)
@@ -587,6 +592,8 @@ using namespace drt;
 
 extern "C" {
 
+int drt_attention_force4_get(void);   // csrc/encoder.hip
+
 size_t drt_colsum_workspace(int64_t M, int64_t N) {
   if (M <= 0 || N <= 0) return 0;
   const int64_t slabs = colsum_slabs(M, N);
@@ -686,15 +693,22 @@ int drt_attention_train_bwd_bf16(const void* qkv, const void* ctx, const void* d
   AttnBwdArgs a{(const __bf16*)qkv, (const __bf16*)ctx, (const __bf16*)dctx, lse, mask, (__bf16*)dqkv, B, L,
                 heads, heads * 64, scale, drop_p, seed, site};
   const int Lp = ((int)L + 31) & ~31;
-  const size_t lds = (size_t)4 * Lp * kAbRow + (size_t)4 * 32 * kAbScr + (size_t)3 * Lp * 4;
+  const bool w8 = Lp / 32 > 4 && !drt_attention_force4_get();
+  const int nw = w8 ? 8 : 4;
+  const size_t lds = (size_t)4 * Lp * kAbRow + (size_t)nw * 32 * kAbScr + (size_t)3 * Lp * 4;
   DRT_REQUIRE(lds <= 160 * 1024);
   static bool attr_set = false;
   if (!attr_set) {
-    DRT_CHECK_HIP(hipFuncSetAttribute((const void*)attention_bwd_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                      160 * 1024));
+    DRT_CHECK_HIP(hipFuncSetAttribute((const void*)attention_bwd_kernel<4>,
+                                      hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
+    DRT_CHECK_HIP(hipFuncSetAttribute((const void*)attention_bwd_kernel<8>,
+                                      hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
     attr_set = true;
   }
-  hipLaunchKernelGGL(attention_bwd_kernel, dim3((unsigned)(B * heads)), dim3(kAbThreads), lds, (hipStream_t)stream, a);
+  if (w8)
+    hipLaunchKernelGGL(attention_bwd_kernel<8>, dim3((unsigned)(B * heads)), dim3(512), lds, (hipStream_t)stream, a);
+  else
+    hipLaunchKernelGGL(attention_bwd_kernel<4>, dim3((unsigned)(B * heads)), dim3(256), lds, (hipStream_t)stream, a);
   return hip_status(hipGetLastError());
 }
 

@@ -288,6 +288,10 @@ int drt_l2_normalize_f32(float* x, int64_t B, int32_t H, void* out_bf16, void* s
  * 7/8 ping-pong 4/5-slot ring, 9 full-K 32x32x16 256x256; >= 16 diagnostic
  * builds (ablations / cycle stamps, need drt_gemm_debug_buffer).            */
 int drt_gemm_force_small(int32_t on);
+/* Benchmark / test switch: 1 keeps 4-wave attention-backward work-groups at every sequence
+ * length; 0 (default) runs 8 waves per (sequence, head) for 5 blocks of 32 rows (L 129-160,
+ * e.g. the recipe's 156-token passages).  Outputs are bit-identical either way.              */
+int drt_attention_force4(int32_t on);
 /* Benchmark switch: smallest grid, in 256x256 tiles, that takes the 256x256 kernel. */
 /* Benchmark switch of the split-K planning: the 256^2 kernel splits K >= large_min_k (default
  * 8192) into chunks of >= large_k_per_split (512); the 128^2 kernel keeps its fp32 partials <=

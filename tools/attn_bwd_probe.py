@@ -1,0 +1,55 @@
+"""Attention forward / backward at the C3 passage shape (1024 x 128, 12 heads) and the recipe
+shape (1024 x 156): time with and without attention-probability dropout (HIP events), and the
+memory floor of each (bytes read + written / 6.3 TB/s)."""
+import json
+import os
+import sys
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from denseretrievaltoolkits_amd import _native  # noqa: E402
+
+
+def main(reps=10):
+    lib = _native.load()
+    dev = torch.device("cuda", 0)
+    s = _native.stream_ptr(dev)
+    res = {}
+    for B, L in ((1024, 128), (1024, 156), (512, 32)):
+        H, heads = 768, 12
+        T = B * L
+        qkv = (0.5 * torch.randn(T, 3 * H, device=dev)).to(torch.bfloat16)
+        ctx = torch.empty(T, H, dtype=torch.bfloat16, device=dev)
+        lse = torch.empty(B * heads * L, dtype=torch.float32, device=dev)
+        dctx = (0.1 * torch.randn(T, H, device=dev)).to(torch.bfloat16)
+        dqkv = torch.empty_like(qkv)
+        mask = torch.ones(B, L, dtype=torch.int64, device=dev)
+        for p, f4 in ((0.0, 0), (0.1, 0), (0.1, 1)):
+            lib.drt_attention_force4(f4)
+            def fwd():
+                return lib.drt_attention_train_fwd_bf16(qkv.data_ptr(), mask.data_ptr(), ctx.data_ptr(), lse.data_ptr(),
+                                                        B, L, heads, 64, 0.125, p, 123, 4, s)
+
+            def bwd():
+                return lib.drt_attention_train_bwd_bf16(qkv.data_ptr(), ctx.data_ptr(), dctx.data_ptr(), lse.data_ptr(),
+                                                        mask.data_ptr(), dqkv.data_ptr(), B, L, heads, 64, 0.125, p,
+                                                        123, 4, s)
+            for name, fn in (("fwd", fwd), ("bwd", bwd)):
+                _native.check(fn(), name)
+                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                e0.record()
+                for _ in range(reps):
+                    fn()
+                e1.record()
+                torch.cuda.synchronize()
+                res[f"B{B}_L{L}_{name}_p{p}" + ("_4w" if f4 else "")] = round(e0.elapsed_time(e1) / reps * 1e3, 1)
+        lib.drt_attention_force4(0)
+        fwd_bytes = T * 3 * H * 2 + T * H * 2
+        bwd_bytes = T * 3 * H * 2 + 2 * T * H * 2 + T * 3 * H * 2
+        res[f"B{B}_L{L}_floor_us"] = {"fwd": round(fwd_bytes / 6.3e12 * 1e6, 1), "bwd": round(bwd_bytes / 6.3e12 * 1e6, 1)}
+    print(json.dumps(res))
+
+
+if __name__ == "__main__":
+    main()
