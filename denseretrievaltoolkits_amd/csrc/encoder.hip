@@ -450,7 +450,7 @@ extern "C" {
 // Benchmark / test switch: 1 keeps the 4-wave attention BACKWARD work-groups at every sequence
 // length, 0 (default) takes 8 waves for 5 blocks (L 129-160; tools/attn_bwd_probe.py).
 int drt_attention_force4(int32_t on) {
-  if (on < 0 || on > 1) return DRT_EINVAL;
+  if (on < 0 || on > 31) return DRT_EINVAL;   // >= 16: diagnostic backward ablations
   g_attn_force4 = on;
   return DRT_OK;
 }

@@ -289,7 +289,9 @@ __device__ __forceinline__ bf16x8 ab_tr8(const char* img, int row0, int col0, in
 // NW = waves per work-group: 4 for L <= 128 (one 32-row block per wave in each phase), 8 for
 // 129 <= L <= 160 (5 blocks: 4 waves ran wave 0 twice per phase while 3 waves idled); the LDS
 // (92-104 KiB at L = 160) allows one work-group per CU either way.  Bit-identical block math.
-template <int NW = 4>
+// ABL (diagnostic builds only, drt_attention_force4(16 + ABL)): 1 skips phase 2, 2 skips phase 1,
+// 4 replaces the softmax exp by the raw score, 8 skips the P / dS stores to the wave's LDS scratch.
+template <int NW = 4, int ABL = 0>
 __global__ __launch_bounds__(NW * 64, NW == 4 ? 2 : 1) void attention_bwd_kernel(AttnBwdArgs a) {
   constexpr int NT = NW * 64;
   extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -316,32 +318,51 @@ __global__ __launch_bounds__(NW * 64, NW == 4 ? 2 : 1) void attention_bwd_kernel
   const __bf16* Og = a.ctx + row0 * a.H + hd * 64;
   const __bf16* dOg = a.dctx + row0 * a.H + hd * 64;
 
-  // ---- staging: rows (row-major images) and the transposed images, element by element
-  for (int i = tid; i < Lp * 8; i += NT) {
-    const int row = i >> 3, c = i & 7;
-    bf16x8 q = {}, k = {}, v = {}, o = {}, oo = {};
-    if (row < L) {
-      q = *(const bf16x8*)(Qg + (int64_t)row * ld + c * 8);
-      k = *(const bf16x8*)(Kg + (int64_t)row * ld + c * 8);
-      v = *(const bf16x8*)(Vg + (int64_t)row * ld + c * 8);
-      o = *(const bf16x8*)(dOg + (int64_t)row * a.H + c * 8);
-      oo = *(const bf16x8*)(Og + (int64_t)row * a.H + c * 8);
-    }
-    float part = 0.f;
+  // ---- staging: row-major images (transposed operands are read with ds_read_b64_tr_b16).  All
+  // global loads of the work-group's rows are issued before the first LDS store (up to MAXIT
+  // 16-B chunks of each of Q, K, V, dO, O per thread), so the HBM latency is paid once, not once
+  // per pass.  Lp * 8 is a multiple of 256: the pass predicate is wave-uniform.
+  {
+    constexpr int MAXIT = (kAbMaxSeq * 8 + NT - 1) / NT;
+    bf16x8 q[MAXIT], k[MAXIT], v[MAXIT], o[MAXIT], oo[MAXIT];
 #pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      q[j] = (__bf16)((float)q[j] * a.scale);
-      part += (float)o[j] * (float)oo[j];
+    for (int it = 0; it < MAXIT; ++it) {
+      const int i = tid + it * NT;
+      const int row = i >> 3, c = i & 7;
+      q[it] = bf16x8{};
+      k[it] = bf16x8{};
+      v[it] = bf16x8{};
+      o[it] = bf16x8{};
+      oo[it] = bf16x8{};
+      if (i < Lp * 8 && row < L) {
+        q[it] = *(const bf16x8*)(Qg + (int64_t)row * ld + c * 8);
+        k[it] = *(const bf16x8*)(Kg + (int64_t)row * ld + c * 8);
+        v[it] = *(const bf16x8*)(Vg + (int64_t)row * ld + c * 8);
+        o[it] = *(const bf16x8*)(dOg + (int64_t)row * a.H + c * 8);
+        oo[it] = *(const bf16x8*)(Og + (int64_t)row * a.H + c * 8);
+      }
     }
-    *(bf16x8*)(Qs + ab_rc(row, c)) = q;
-    *(bf16x8*)(Ks + ab_rc(row, c)) = k;
-    *(bf16x8*)(Vs + ab_rc(row, c)) = v;
-    *(bf16x8*)(Os + ab_rc(row, c)) = o;
-    // Dv: the 8 chunk-partials of one row sit in 8 consecutive lanes
-    part += __shfl_xor(part, 1, 64);
-    part += __shfl_xor(part, 2, 64);
-    part += __shfl_xor(part, 4, 64);
-    if (c == 0) dv[row] = part;
+#pragma unroll
+    for (int it = 0; it < MAXIT; ++it) {
+      const int i = tid + it * NT;
+      if (i >= Lp * 8) break;
+      const int row = i >> 3, c = i & 7;
+      float part = 0.f;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        q[it][j] = (__bf16)((float)q[it][j] * a.scale);
+        part += (float)o[it][j] * (float)oo[it][j];
+      }
+      *(bf16x8*)(Qs + ab_rc(row, c)) = q[it];
+      *(bf16x8*)(Ks + ab_rc(row, c)) = k[it];
+      *(bf16x8*)(Vs + ab_rc(row, c)) = v[it];
+      *(bf16x8*)(Os + ab_rc(row, c)) = o[it];
+      // Dv: the 8 chunk-partials of one row sit in 8 consecutive lanes
+      part += __shfl_xor(part, 1, 64);
+      part += __shfl_xor(part, 2, 64);
+      part += __shfl_xor(part, 4, 64);
+      if (c == 0) dv[row] = part;
+    }
   }
   for (int i = tid; i < Lp; i += NT) {
     float bv = 0.0f;
@@ -359,7 +380,7 @@ __global__ __launch_bounds__(NW * 64, NW == 4 ? 2 : 1) void attention_bwd_kernel
   char* sT = scr + wave * 32 * kAbScr;   // P, then dS (phase 1); dS (phase 2)
 
   // ---- phase 1: dK, dV for key block kbk (rows = keys in the D layout, cols = q / d)
-  for (int kbk = wave; kbk < nblk; kbk += NW) {
+  for (int kbk = wave; !(ABL & 2) && kbk < nblk; kbk += NW) {
     f32x16 dK[2], dV[2];
 #pragma unroll
     for (int t = 0; t < 2; ++t)
@@ -395,7 +416,7 @@ __global__ __launch_bounds__(NW * 64, NW == 4 ? 2 : 1) void attention_bwd_kernel
 #pragma unroll
       for (int e = 0; e < 16; ++e) {
         const int kr = (e & 3) + 8 * (e >> 2) + 4 * h;
-        const float p = __expf(st[e] + kb[kbk * 32 + kr] - lq);
+        const float p = (ABL & 4) ? st[e] : __expf(st[e] + kb[kbk * 32 + kr] - lq);
         float pd = p, dpe = dpt[e];
         if (drop) {
           const int key = kbk * 32 + kr;
@@ -404,7 +425,7 @@ __global__ __launch_bounds__(NW * 64, NW == 4 ? 2 : 1) void attention_bwd_kernel
           dpe = keep ? dpe * inv : 0.f;
         }
         ds[e] = p * (dpe - dq);
-        *(__bf16*)(sT + kr * kAbScr + r * 2) = (__bf16)pd;
+        if (!(ABL & 8)) *(__bf16*)(sT + kr * kAbScr + r * 2) = (__bf16)pd;
       }
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
       __builtin_amdgcn_wave_barrier();
@@ -423,7 +444,7 @@ __global__ __launch_bounds__(NW * 64, NW == 4 ? 2 : 1) void attention_bwd_kernel
 #pragma unroll
       for (int e = 0; e < 16; ++e) {
         const int kr = (e & 3) + 8 * (e >> 2) + 4 * h;
-        *(__bf16*)(sT + kr * kAbScr + r * 2) = (__bf16)ds[e];
+        if (!(ABL & 8)) *(__bf16*)(sT + kr * kAbScr + r * 2) = (__bf16)ds[e];
       }
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
       __builtin_amdgcn_wave_barrier();
@@ -456,7 +477,7 @@ __global__ __launch_bounds__(NW * 64, NW == 4 ? 2 : 1) void attention_bwd_kernel
   }
 
   // ---- phase 2: dQ for query block qbq (rows = queries, cols = keys / d)
-  for (int qbq = wave; qbq < nblk; qbq += NW) {
+  for (int qbq = wave; !(ABL & 1) && qbq < nblk; qbq += NW) {
     f32x16 dQ[2];
 #pragma unroll
     for (int t = 0; t < 2; ++t)
@@ -486,14 +507,14 @@ __global__ __launch_bounds__(NW * 64, NW == 4 ? 2 : 1) void attention_bwd_kernel
       for (int e = 0; e < 16; ++e) {
         const int qr = (e & 3) + 8 * (e >> 2) + 4 * h;
         const int q = qbq * 32 + qr;
-        const float p = __expf(sv[e] + kbias - lse[q]);
+        const float p = (ABL & 4) ? sv[e] : __expf(sv[e] + kbias - lse[q]);
         float dpe = dp[e];
         if (drop) {
           const uint64_t idx = (((uint64_t)b * a.heads + hd) * L + q) * (uint64_t)L + kcol;
           const bool keep = kcol < L && q < L && drop_hash24(a.seed, a.site, idx) >= thr;
           dpe = keep ? dpe * inv : 0.f;
         }
-        *(__bf16*)(sT + qr * kAbScr + r * 2) = (__bf16)(p * (dpe - dv[q]));
+        if (!(ABL & 8)) *(__bf16*)(sT + qr * kAbScr + r * 2) = (__bf16)(p * (dpe - dv[q]));
       }
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
       __builtin_amdgcn_wave_barrier();
@@ -693,7 +714,7 @@ int drt_attention_train_bwd_bf16(const void* qkv, const void* ctx, const void* d
   AttnBwdArgs a{(const __bf16*)qkv, (const __bf16*)ctx, (const __bf16*)dctx, lse, mask, (__bf16*)dqkv, B, L,
                 heads, heads * 64, scale, drop_p, seed, site};
   const int Lp = ((int)L + 31) & ~31;
-  const bool w8 = Lp / 32 > 4 && !drt_attention_force4_get();
+  const bool w8 = Lp / 32 > 4 && drt_attention_force4_get() == 0;
   const int nw = w8 ? 8 : 4;
   const size_t lds = (size_t)4 * Lp * kAbRow + (size_t)nw * 32 * kAbScr + (size_t)3 * Lp * 4;
   DRT_REQUIRE(lds <= 160 * 1024);
@@ -703,12 +724,29 @@ int drt_attention_train_bwd_bf16(const void* qkv, const void* ctx, const void* d
                                       hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
     DRT_CHECK_HIP(hipFuncSetAttribute((const void*)attention_bwd_kernel<8>,
                                       hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
+    const void* abl_k[] = {(const void*)attention_bwd_kernel<4, 1>, (const void*)attention_bwd_kernel<4, 2>,
+                           (const void*)attention_bwd_kernel<4, 4>, (const void*)attention_bwd_kernel<4, 8>,
+                           (const void*)attention_bwd_kernel<4, 12>};
+    for (const void* f : abl_k)
+      DRT_CHECK_HIP(hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
     attr_set = true;
   }
-  if (w8)
-    hipLaunchKernelGGL(attention_bwd_kernel<8>, dim3((unsigned)(B * heads)), dim3(512), lds, (hipStream_t)stream, a);
-  else
-    hipLaunchKernelGGL(attention_bwd_kernel<4>, dim3((unsigned)(B * heads)), dim3(256), lds, (hipStream_t)stream, a);
+  const int abl = drt_attention_force4_get() >= 16 ? drt_attention_force4_get() - 16 : 0;
+  const dim3 grid((unsigned)(B * heads));
+  if (abl) {
+    switch (abl) {   // diagnostic ablations (4 waves)
+      case 1: hipLaunchKernelGGL((attention_bwd_kernel<4, 1>), grid, dim3(256), lds, (hipStream_t)stream, a); break;
+      case 2: hipLaunchKernelGGL((attention_bwd_kernel<4, 2>), grid, dim3(256), lds, (hipStream_t)stream, a); break;
+      case 4: hipLaunchKernelGGL((attention_bwd_kernel<4, 4>), grid, dim3(256), lds, (hipStream_t)stream, a); break;
+      case 8: hipLaunchKernelGGL((attention_bwd_kernel<4, 8>), grid, dim3(256), lds, (hipStream_t)stream, a); break;
+      case 12: hipLaunchKernelGGL((attention_bwd_kernel<4, 12>), grid, dim3(256), lds, (hipStream_t)stream, a); break;
+      default: return DRT_EINVAL;
+    }
+  } else if (w8) {
+    hipLaunchKernelGGL((attention_bwd_kernel<8>), grid, dim3(512), lds, (hipStream_t)stream, a);
+  } else {
+    hipLaunchKernelGGL((attention_bwd_kernel<4>), grid, dim3(256), lds, (hipStream_t)stream, a);
+  }
   return hip_status(hipGetLastError());
 }
 
