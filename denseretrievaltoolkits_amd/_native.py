@@ -55,6 +55,8 @@ _SIGNATURES = [
     ("drt_linear_bf16", c_i32, [c_vp, c_vp, c_vp, c_vp, c_vp, c_i64, c_i64, c_i64, c_i32, c_vp]),
     ("drt_linear_workspace", c_sz, [c_i64, c_i64, c_i64]),
     ("drt_linear_bf16_ws", c_i32, [c_vp, c_vp, c_vp, c_vp, c_vp, c_i64, c_i64, c_i64, c_i32, c_vp, c_sz, c_vp]),
+    ("drt_linear_ln_bf16_ws", c_i32, [c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_f32, c_vp, c_vp, c_i64, c_i64, c_i64,
+                                      c_vp, c_sz, c_vp]),
     ("drt_layernorm_f32_bf16", c_i32, [c_vp, c_i64, c_i32, c_vp, c_vp, c_f32, c_vp, c_vp]),
     ("drt_attention_fwd_lse_bf16", c_i32, [c_vp, c_vp, c_vp, c_vp, c_i64, c_i64, c_i32, c_i32, c_f32, c_vp]),
     ("drt_layernorm_bwd_workspace", c_sz, [c_i64, c_i32]),

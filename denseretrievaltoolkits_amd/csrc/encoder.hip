@@ -13,43 +13,9 @@
 //   pool            first / masked-mean / masked-max pooling (utils.py:233-240)
 //   l2norm          F.normalize(reps, dim=1) (biencoder.py:149-150)
 #include "drt_common.h"
+#include "ln_row.h"
 
 namespace drt {
-
-// ---------------------------------------------------------------------------
-// Row LayerNorm helpers: one wave per row, H = 64 * EPL (EPL <= 16).
-// ---------------------------------------------------------------------------
-__device__ __forceinline__ float wave_sum(float v) {
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
-  return v;
-}
-
-template <int EPL>
-__device__ __forceinline__ void ln_row(float (&x)[EPL], const float* gamma, const float* beta, float eps, int lane,
-                                       int H, __bf16* out_row) {
-  float s = 0.f;
-#pragma unroll
-  for (int e = 0; e < EPL; ++e) s += x[e];
-  const float mean = wave_sum(s) / (float)H;
-  float v = 0.f;
-#pragma unroll
-  for (int e = 0; e < EPL; ++e) {
-    const float d = x[e] - mean;
-    v += d * d;
-  }
-  const float var = wave_sum(v) / (float)H;
-  const float rstd = rsqrtf(var + eps);
-  // element e of lane: column c = (e / 4) * 256 + lane * 4 + (e % 4)   (4-wide chunks)
-#pragma unroll
-  for (int e4 = 0; e4 < EPL / 4; ++e4) {
-    const int c = e4 * 256 + lane * 4;
-    bf16x4 o;
-#pragma unroll
-    for (int u = 0; u < 4; ++u) o[u] = (__bf16)((x[e4 * 4 + u] - mean) * rstd * gamma[c + u] + beta[c + u]);
-    *(bf16x4*)(out_row + c) = o;
-  }
-}
 
 template <int EPL>
 __global__ __launch_bounds__(256) void embed_ln_kernel(const int64_t* ids, const int64_t* type_ids, int64_t T,

@@ -11,6 +11,7 @@
 // same XOR-swizzled [row][8 x 16 B] image as the search scan so the
 // ds_read_b128 fragment reads are bank-conflict free.
 #include "drt_common.h"
+#include "ln_row.h"
 #include "profile.h"
 
 namespace drt {
@@ -278,6 +279,58 @@ __global__ __launch_bounds__(256) void splitk_epi_kernel(GemmArgs a, int splits)
       else ((float*)a.C)[row * a.ldc + col + q] = x;
     }
   }
+}
+
+// Split-K finish of a pre-LayerNorm sublayer sum fused with that LayerNorm (query-sized batches,
+// BertSelfOutput / BertOutput, modeling_bert.py:282-352): per row, x = bf16(sum_z ws[z] * alpha + bias
+// + resid) exactly as splitk_epi_kernel<true, EPI_BIAS | EPI_RESID> stores it, then ln_row over those
+// values exactly as layernorm_bf16_kernel reads them back: bit-identical to the two launches it
+// replaces.  One wave per row (H = 64 * EPL); out may alias resid (a row is read before it is written).
+template <int EPL>
+__global__ __launch_bounds__(256) void splitk_ln_kernel(const float* ws, int splits, int64_t M, int H, float alpha,
+                                                        const float* bias, const __bf16* resid, const float* gamma,
+                                                        const float* beta, float eps, __bf16* out) {
+  const int lane = threadIdx.x & 63;
+  const int64_t t = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (t >= M) return;
+  const int64_t mn = M * H;
+  constexpr int C4 = EPL / 4;
+  // the split sums, 4 splits x C4 chunks of loads in flight per step (one wave per row: a serial
+  // load-add chain per split would pay one L2 round trip per split and chunk); the additions keep
+  // splitk_epi_kernel's z order
+  f32x4 s4[C4];
+  const float* row = ws + t * H + lane * 4;
+#pragma unroll
+  for (int e4 = 0; e4 < C4; ++e4) s4[e4] = *(const f32x4*)(row + e4 * 256);
+  int z = 1;
+  for (; z + 4 <= splits; z += 4) {
+    f32x4 q[4][C4];
+#pragma unroll
+    for (int zz = 0; zz < 4; ++zz)
+#pragma unroll
+      for (int e4 = 0; e4 < C4; ++e4) q[zz][e4] = *(const f32x4*)(row + (int64_t)(z + zz) * mn + e4 * 256);
+#pragma unroll
+    for (int zz = 0; zz < 4; ++zz)
+#pragma unroll
+      for (int e4 = 0; e4 < C4; ++e4) s4[e4] += q[zz][e4];
+  }
+  for (; z < splits; ++z)
+#pragma unroll
+    for (int e4 = 0; e4 < C4; ++e4) s4[e4] += *(const f32x4*)(row + (int64_t)z * mn + e4 * 256);
+  float x[EPL];
+#pragma unroll
+  for (int e4 = 0; e4 < C4; ++e4) {
+    const int c = e4 * 256 + lane * 4;
+    const bf16x4 r = *(const bf16x4*)(resid + t * H + c);
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      float v = s4[e4][u] * alpha;
+      v += bias[c + u];
+      v += (float)r[u];
+      x[e4 * 4 + u] = (float)(__bf16)v;
+    }
+  }
+  ln_row<EPL>(x, gamma, beta, eps, lane, H, out + t * H);
 }
 
 // Split plan of the 128^2 kernel for problems too small to fill the chip (query-sized
@@ -1478,6 +1531,69 @@ extern "C" int drt_linear_bf16_ws(const void* X, const void* W, const float* bia
   if (ws && ws_bytes >= drt_linear_workspace(M, N, K) && drt_linear_workspace(M, N, K) > 0) a.ws = (float*)ws;
   const int epi = (bias ? EPI_BIAS : 0) | (gelu ? EPI_GELU : 0) | (residual ? EPI_RESID : 0);
   return launch_gemm(a, !f32, epi, (hipStream_t)stream);
+}
+
+extern "C" int drt_layernorm_bf16(const void* X, int64_t M, int32_t H, const float* gamma, const float* beta, float eps,
+                                  void* out, void* stream);
+
+// LayerNorm(bf16(X W^T + bias + residual)) -> out (BertSelfOutput / BertOutput: dense + residual +
+// LayerNorm).  When the 128^2 kernel's split plan applies (query-sized batches, caller scratch >=
+// drt_linear_workspace) the K-split partials are finished by one fused split-K + LayerNorm launch
+// (splitk_ln_kernel); otherwise the linear writes its bf16 pre-LayerNorm sum to `presum` and
+// drt_layernorm_bf16 normalises it.  Either way bit-identical to drt_linear_bf16_ws + drt_layernorm_bf16.
+// out may alias residual.  N % 256 == 0, N <= 1024.
+extern "C" int drt_linear_ln_bf16_ws(const void* X, const void* W, const float* bias, const void* residual,
+                                     const float* gamma, const float* beta, float eps, void* presum, void* out,
+                                     int64_t M, int64_t N, int64_t K, void* ws, size_t ws_bytes, void* stream) {
+  DRT_REQUIRE(M >= 0 && N > 0 && N % 256 == 0 && N <= 1024 && K > 0 && K % 64 == 0);
+  if (M == 0) return DRT_OK;
+  DRT_REQUIRE(X && W && bias && residual && gamma && beta && presum && out);
+  hipStream_t s = (hipStream_t)stream;
+  const int64_t tiles_l = ((M + kL - 1) / kL) * ((N + kL - 1) / kL);
+  const int64_t tiles = ((M + kBM - 1) / kBM) * ((N + kBN - 1) / kBN);
+  int64_t kc = 0;
+  const size_t need = drt_linear_workspace(M, N, K);
+  const bool small_path = tiles_l < g_large_min_tiles && !(M >= g_msplit_min_m && K < g_lsplit_min_k) &&
+                          !(large_splits(M, N, K, g_large_min_tiles, &kc) > 1) && g_gemm_variant == 0;
+  kc = 0;
+  const int splits = (small_path && ws && need > 0 && ws_bytes >= need) ? small_splits(M, N, K, &kc) : 0;
+  if (splits < 2) {
+    const int rc = drt_linear_bf16_ws(X, W, bias, residual, presum, M, N, K, 0, ws, ws_bytes, stream);
+    if (rc != DRT_OK) return rc;
+    return drt_layernorm_bf16(presum, M, (int32_t)N, gamma, beta, eps, out, stream);
+  }
+  GemmArgs b{};
+  b.A = (const __bf16*)X;
+  b.B = (const __bf16*)W;
+  b.C = presum;   // unused by the partial kernel (PART writes b.ws)
+  b.m = M;
+  b.n = N;
+  b.k = K;
+  b.lda = K;
+  b.ldb = K;
+  b.ldc = N;
+  b.ldr = N;
+  b.alpha = 1.0f;
+  b.ws = (float*)ws;
+  b.kchunk = kc;
+  b.order = g_gemm_order >= 0 ? g_gemm_order : (K <= 1024 ? 1 : 0);
+  const ProfPair pp = prof_begin(PROF_GEMM, s);
+  hipLaunchKernelGGL((gemm_nt_kernel<true, EPI_BIAS | EPI_RESID, true>), dim3((unsigned)tiles, 1, (unsigned)splits),
+                     dim3(kGemmThreads), 0, s, b);
+  const dim3 grid((unsigned)((M + 3) / 4));
+  switch (N / 64) {
+    case 4: hipLaunchKernelGGL(splitk_ln_kernel<4>, grid, dim3(256), 0, s, (const float*)ws, splits, M, (int)N, 1.0f,
+                               bias, (const __bf16*)residual, gamma, beta, eps, (__bf16*)out); break;
+    case 8: hipLaunchKernelGGL(splitk_ln_kernel<8>, grid, dim3(256), 0, s, (const float*)ws, splits, M, (int)N, 1.0f,
+                               bias, (const __bf16*)residual, gamma, beta, eps, (__bf16*)out); break;
+    case 12: hipLaunchKernelGGL(splitk_ln_kernel<12>, grid, dim3(256), 0, s, (const float*)ws, splits, M, (int)N, 1.0f,
+                                bias, (const __bf16*)residual, gamma, beta, eps, (__bf16*)out); break;
+    case 16: hipLaunchKernelGGL(splitk_ln_kernel<16>, grid, dim3(256), 0, s, (const float*)ws, splits, M, (int)N, 1.0f,
+                                bias, (const __bf16*)residual, gamma, beta, eps, (__bf16*)out); break;
+    default: return DRT_EINVAL;
+  }
+  prof_end(pp, s);
+  return hip_status(hipGetLastError());
 }
 
 // drt_linear_bf16_ws plus the training tower's epilogue fusions (include/drt.h):

@@ -78,6 +78,7 @@ class HipBertEncoder:
         self.graph_cache_size = 8
         self._graph_cache = {}
         self.split_streams = True       # two halves on two streams from split_min_tokens up
+        self.fuse_ln = True             # dense + residual + LayerNorm in one call (_lin_ln)
         self.split_min_tokens = 65536
         self._streams = None
         self._ws_plan = {}
@@ -136,6 +137,25 @@ class HipBertEncoder:
                                                   ws.numel() * 4 if ws is not None else 0, self.stream),
                       "drt_linear_bf16_ws")
         return out
+
+    def _lin_ln(self, x, w, b, h, g, beta, x32, ln):
+        """h = LayerNorm(x w^T + b + h) (BertSelfOutput / BertOutput, modeling_bert.py:282-352).  bf16
+        pre-LayerNorm sums: one call that finishes a split-K GEMM and the LayerNorm in a single launch
+        when the split plan applies (query-sized batches), bit-identical to linear + LayerNorm."""
+        m, k = x.shape
+        n = w.shape[0]
+        T, H = h.shape
+        if self.fuse_ln and x32.dtype == torch.bfloat16 and H % 256 == 0 and H <= 1024:
+            ws = self._ws
+            _native.check(self.lib.drt_linear_ln_bf16_ws(
+                x.data_ptr(), w.data_ptr(), b.data_ptr(), h.data_ptr(), g.data_ptr(), beta.data_ptr(),
+                self.shape.eps, x32.data_ptr(), h.data_ptr(), m, n, k, ws.data_ptr() if ws is not None else None,
+                ws.numel() * 4 if ws is not None else 0, self.stream), "drt_linear_ln_bf16_ws")
+            return h
+        self._lin(x, w, b, x32, resid=h)
+        _native.check(ln(x32.data_ptr(), T, H, g.data_ptr(), beta.data_ptr(), self.shape.eps, h.data_ptr(),
+                         self.stream), "drt_layernorm")
+        return h
 
     def _ws_bytes(self, T: int) -> int:
         """Split-K scratch for this token count (small batches only; 0 at encode sizes)."""
@@ -248,13 +268,9 @@ class HipBertEncoder:
             _native.check(self.lib.drt_attention_bf16(qkv.data_ptr(), mask.data_ptr() if mask is not None else None,
                                                       ctx.data_ptr(), B, L, sh.heads, H // sh.heads, scale,
                                                       self.stream), "drt_attention_bf16")
-            self._lin(ctx, ly["wo"], ly["bo"], x32, resid=h)
-            _native.check(ln(x32.data_ptr(), T, H, ly["g1"].data_ptr(), ly["b1"].data_ptr(), sh.eps, h.data_ptr(),
-                             self.stream), "drt_layernorm")
+            self._lin_ln(ctx, ly["wo"], ly["bo"], h, ly["g1"], ly["b1"], x32, ln)
             self._lin(h, ly["wi"], ly["bi"], ffn, gelu=True)
-            self._lin(ffn, ly["wf"], ly["bf"], x32, resid=h)
-            _native.check(ln(x32.data_ptr(), T, H, ly["g2"].data_ptr(), ly["b2"].data_ptr(), sh.eps, h.data_ptr(),
-                             self.stream), "drt_layernorm")
+            self._lin_ln(ffn, ly["wf"], ly["bf"], h, ly["g2"], ly["b2"], x32, ln)
         return h.view(B, L, H)
 
     __call__ = forward

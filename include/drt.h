@@ -183,6 +183,15 @@ size_t drt_linear_workspace(int64_t M, int64_t N, int64_t K);
 int drt_linear_bf16_ws(const void* X, const void* W, const float* bias, const void* residual,
                        void* Y, int64_t M, int64_t N, int64_t K, int32_t flags, void* ws,
                        size_t ws_bytes, void* stream);
+/* BertSelfOutput / BertOutput (modeling_bert.py:282-352: dense + residual + LayerNorm):
+ * out = LayerNorm(bf16(X W^T + bias + residual)) * gamma + beta.  With a split-K plan (query-sized
+ * batches, ws_bytes >= drt_linear_workspace) the partials are finished by ONE fused split-K +
+ * LayerNorm launch; otherwise the bf16 pre-LayerNorm sum goes to `presum` [M, N] and is normalised.
+ * Bit-identical to drt_linear_bf16_ws + drt_layernorm_bf16.  out may alias residual; N % 256 == 0,
+ * N <= 1024.                                                                                       */
+int drt_linear_ln_bf16_ws(const void* X, const void* W, const float* bias, const void* residual,
+                          const float* gamma, const float* beta, float eps, void* presum, void* out,
+                          int64_t M, int64_t N, int64_t K, void* ws, size_t ws_bytes, void* stream);
 /* drt_linear_bf16_ws plus the training tower's epilogue fusions (bf16 Y):
  *   gelu_pre [M, N] != NULL: Y = (X W^T) * GELU'(gelu_pre)  (dgrad through an erf GELU whose input
  *     was gelu_pre; bias / residual / GELU / Y_pre / DROP must be off);

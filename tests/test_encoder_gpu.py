@@ -265,3 +265,40 @@ def test_two_stream_halves(dev):
         else:
             err = (a.float() - b.float()).abs().max().item()
             assert err < 0.1, err   # LN outputs O(1): a few bf16 ulps through 2 layers
+
+
+@pytest.mark.parametrize("M,N,K", [(256, 768, 768), (256, 768, 3072), (37, 768, 3072), (4096, 768, 768),
+                                   (96, 1024, 512)])
+def test_linear_ln_fused_bit_identical(dev, M, N, K):
+    """drt_linear_ln_bf16_ws (split-K partials finished by one fused split-K + LayerNorm launch at
+    query-sized M, linear + LayerNorm otherwise), in place over the residual, against the two-call
+    path drt_linear_bf16_ws + drt_layernorm_bf16 with the same workspace: bit for bit."""
+    import torch
+    from denseretrievaltoolkits_amd import _native
+    lib = _native.load()
+    g = torch.Generator(device=dev).manual_seed(M * 7 + K)
+    x = torch.randn(M, K, generator=g, device=dev).to(torch.bfloat16)
+    w = (0.05 * torch.randn(N, K, generator=g, device=dev)).to(torch.bfloat16)
+    b = torch.randn(N, generator=g, device=dev)
+    r = torch.randn(M, N, generator=g, device=dev).to(torch.bfloat16)
+    gam = 1.0 + 0.1 * torch.randn(N, generator=g, device=dev)
+    bet = 0.1 * torch.randn(N, generator=g, device=dev)
+    s = _native.stream_ptr(dev)
+    nb = int(lib.drt_linear_workspace(M, N, K))
+    ws = torch.empty(max(1, (nb + 3) // 4), dtype=torch.float32, device=dev)
+    pre = torch.empty(M, N, dtype=torch.bfloat16, device=dev)
+    ref = torch.empty(M, N, dtype=torch.bfloat16, device=dev)
+    _native.check(lib.drt_linear_bf16_ws(x.data_ptr(), w.data_ptr(), b.data_ptr(), r.data_ptr(), pre.data_ptr(), M, N,
+                                         K, 0, ws.data_ptr(), nb, s), "linear")
+    _native.check(lib.drt_layernorm_bf16(pre.data_ptr(), M, N, gam.data_ptr(), bet.data_ptr(), 1e-12, ref.data_ptr(), s),
+                  "ln")
+    h = r.clone()
+    _native.check(lib.drt_linear_ln_bf16_ws(x.data_ptr(), w.data_ptr(), b.data_ptr(), h.data_ptr(), gam.data_ptr(),
+                                            bet.data_ptr(), 1e-12, pre.data_ptr(), h.data_ptr(), M, N, K, ws.data_ptr(),
+                                            nb, s), "linear_ln")
+    torch.cuda.synchronize()
+    assert torch.equal(h, ref)
+    # and against torch fp32 (bf16 pre-LayerNorm sum, as the HF reference rounded at the same point)
+    y = (x.float() @ w.float().T + b + r.float()).to(torch.bfloat16).float()
+    want = torch.nn.functional.layer_norm(y, (N,), gam, bet, 1e-12)
+    torch.testing.assert_close(h.float(), want, atol=3e-2, rtol=1e-2)
