@@ -49,7 +49,8 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-encode", action="store_true",
                     help="skip the encode leg (passages/sec of the bf16 BERT-base passage tower, every rank)")
-    ap.add_argument("--scan-variant", type=int, default=0, help="benchmark-only ablation of the scan kernel")
+    ap.add_argument("--no-evaluate", action="store_true", help="skip the C2 Trainer.evaluate leg")
+    ap.add_argument("--c2-passages", type=int, default=1_000_000, help="corpus size of the C2 evaluate leg")
     ap.add_argument("--group-queries", type=int, default=-1,
                     help="queries per group of batches in search_batches (0 = per-batch path; default: "
                          "search.GROUP_QUERIES)")
@@ -106,12 +107,36 @@ def _cpu_threads():
     return info
 
 
+def _tie_check(q, shard, gi, ci):
+    """Every (query, rank) where the GPU's id differs from the CPU baseline's: recompute both rows'
+    scores in fp64 from the same bf16 rows and report the largest gap.  A gap within fp32 summation
+    noise (<= 1e-3, north_star's score tolerance) means the two rows are a near-tie that fp32 BLAS
+    and the MFMA sum order rank differently -- not a wrong answer."""
+    import numpy as np
+    qi, ri = np.nonzero(gi != ci)
+    if qi.size == 0:
+        return 0, 0.0
+    import torch
+    ids = np.unique(np.concatenate([gi[qi, ri], ci[qi, ri]]))
+    ids = ids[ids >= 0]
+    rows = shard[torch.from_numpy(ids).to(shard.device)].double().cpu().numpy()
+    pos = {int(x): j for j, x in enumerate(ids)}
+    qd = q.astype(np.float64)
+    gap = 0.0
+    for a, b in zip(qi, ri):
+        sg = float(qd[a] @ rows[pos[int(gi[a, b])]]) if gi[a, b] >= 0 else -np.inf
+        sc = float(qd[a] @ rows[pos[int(ci[a, b])]]) if ci[a, b] >= 0 else -np.inf
+        gap = max(gap, abs(sg - sc))
+    return int(qi.size), gap
+
+
 def cpu_baseline(args, shard, queries, gpu_result):
     """The oracle (numpy fp32 BLAS, like faiss IndexFlatIP's sgemm + top-k) timed on the host
     cores against the SAME 10M-row corpus the GPU searched: the shard streams to host in
     262,144-row chunks (bf16 -> fp32 conversion untimed, as building a faiss index would be),
     and ONE query batch is scored and selected chunk by chunk (timed).  Also checks the GPU's
-    top-k of that batch against the CPU result at full size."""
+    top-k of that batch against the CPU result at full size: every differing (query, rank) is
+    recomputed in fp64 and must be a near-tie (|gap| <= 1e-3)."""
     import numpy as np
     from oracle.search_oracle import ip_topk, merge_topk
     thr = _cpu_threads()
@@ -133,21 +158,31 @@ def cpu_baseline(args, shard, queries, gpu_result):
     gi = gi.cpu().numpy()
     gs = gs.cpu().numpy()
     same = float((gi == best_i).mean())
+    n_mis, gap = _tie_check(q, shard, gi, best_i)
+    cores = int(thr["blas_threads"] or thr["torch_threads"])
+    value = q.shape[0] / t_comp
     return {
-        "value": round(q.shape[0] / t_comp, 3),
+        "value": round(value, 3),
         "unit": "queries/s",
-        "cores": int(thr["blas_threads"] or thr["torch_threads"]),
+        "cores": cores,
         "kind": "port",
-        "sample": (f"oracle/search_oracle.ip_topk fp32 (numpy BLAS, {thr['blas_threads']} threads) on one batch of "
+        "sample": (f"oracle/search_oracle.ip_topk fp32 (numpy BLAS, {cores} threads = the box's CPU share per GPU; "
+                   f"OMP_NUM_THREADS={os.environ.get('OMP_NUM_THREADS')}) on one batch of "
                    f"{q.shape[0]} queries against the full {n}-row bf16 corpus streamed from the GPU in "
                    f"{chunk}-row chunks (fp32 conversion untimed); {t_comp:.1f} s of compute"),
+        # the reference runs faiss with OMP_NUM_THREADS=40 (run.sh:24); linear scaling from the measured
+        # threads is an upper bound for that configuration on this host
+        "projected_40_threads_upper_bound": round(value * 40 / max(1, cores), 3),
         **thr,
         "parity_vs_gpu": {"ids_equal_frac": round(same, 6),
-                          "max_abs_score_diff": float(np.abs(gs - best_s).max())},
+                          "max_abs_score_diff": float(np.abs(gs - best_s).max()),
+                          "n_mismatch": n_mis,
+                          "max_tie_gap_fp64": gap,
+                          "all_mismatches_near_ties": bool(gap <= 1e-3)},
     }
 
 
-def encode_cpu_baseline(batch=32, L=128, steps=2):
+def encode_cpu_baseline(batch=32, L=128, min_seconds=10.0):
     """torch-CPU fp32 DRModel.encode (the reference's arithmetic: HF BertModel fp32 + [CLS]
     pooling through this build's DRModelForInference, which is pinned to the reference's
     golden reps on CPU), BERT-base random init, B = 32, L = 128."""
@@ -161,10 +196,13 @@ def encode_cpu_baseline(batch=32, L=128, steps=2):
     ids = torch.randint(1000, 30522, (batch, L), dtype=torch.int64)
     ids[:, 0], ids[:, -1] = 101, 102
     item = {"input_ids": ids, "attention_mask": torch.ones((batch, L), dtype=torch.int64)}
-    m(passage=item)
-    t0 = time.perf_counter()
-    for _ in range(steps):
+    with torch.no_grad():
         m(passage=item)
+        t0 = time.perf_counter()
+        steps = 0
+        while time.perf_counter() - t0 < min_seconds:
+            m(passage=item)
+            steps += 1
     el = time.perf_counter() - t0
     return {"value": round(steps * batch / el, 2), "unit": "passages/s", "cores": int(thr["torch_threads"]),
             "kind": "port", "sample": f"{steps} batches of {batch} x {L} tokens, fp32, {el:.1f} s", **thr}
@@ -188,11 +226,8 @@ def pmc_traffic(args, world):
 
 
 def encode_leg(args, device):
-    try:
-        from denseretrievaltoolkits_amd import bench_encode
-    except ImportError:
-        return None
-    return bench_encode.run(device)
+    import bench_legs
+    return bench_legs.run(device)
 
 
 def main():
@@ -204,7 +239,6 @@ def main():
     from denseretrievaltoolkits_amd import _native, kernels
 
     lib = _native.load()
-    _native.check(lib.drt_scan_variant(args.scan_variant), "drt_scan_variant")
     d, k, qb = args.dim, args.k, args.qb
     shard, lo, hi = gen_shard(args.n_corpus, world, rank, d, dev)
     n_local = hi - lo
@@ -348,7 +382,7 @@ def main():
         if out is not None:
             out["encode"] = enc
     if rank == 0 and not args.no_encode and world == 1:
-        from denseretrievaltoolkits_amd import bench_encode
+        import bench_legs as bench_encode
         if not args.no_cpu_baseline:
             out["encode"]["cpu_baseline"] = encode_cpu_baseline()
         out["rerank"] = bench_encode.run_rerank(dev)
@@ -357,6 +391,8 @@ def main():
         out["train_step"] = bench_encode.run_train_step(dev)
         # the reference recipe's shapes (run.sh:16-19: train_n_passages 8, p_max_len 156) at batch 128
         out["train_step_recipe"] = bench_encode.run_train_step(dev, bq=128, n=8, p_len=156)
+        if not args.no_evaluate:
+            out["evaluate_c2"] = bench_encode.run_evaluate_c2(dev, n_passages=args.c2_passages)
     if rank == 0:
         print(json.dumps(out), flush=True)
     if world > 1:

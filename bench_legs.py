@@ -22,8 +22,8 @@ def flops_per_seq(L, H=768, layers=12, inter=3072):
 
 def run(device, batch=512, L=128, steps=10, warmup=2):
     from transformers import BertConfig, BertModel
-    from .model.encoder import HipBertEncoder
-    from . import _native
+    from denseretrievaltoolkits_amd.model.encoder import HipBertEncoder
+    from denseretrievaltoolkits_amd import _native
     torch.manual_seed(0)
     m = BertModel(BertConfig(), add_pooling_layer=False).eval()
     enc = HipBertEncoder.from_hf(m, device)
@@ -79,7 +79,7 @@ def run_query_encode(device, batches=(8, 128), L=32, steps=50, warmup=3):
     HIP forward + [CLS] pooling, eager launches vs hipGraph replay (HipBertEncoder._replay), at a
     small interactive batch (8: host-bound when eager) and the search batch (128: GPU-bound)."""
     from transformers import BertConfig, BertModel
-    from .model.encoder import HipBertEncoder
+    from denseretrievaltoolkits_amd.model.encoder import HipBertEncoder
     torch.manual_seed(0)
     m = BertModel(BertConfig(), add_pooling_layer=False).eval()
     enc = HipBertEncoder.from_hf(m, device)
@@ -119,7 +119,7 @@ def run_rerank(device, pairs=1000, q_len=32, p_len=128, steps=3, warmup=1):
     1000 pairs [CLS] q [SEP] p [SEP] of L = q_len + p_len = 160 tokens through the bf16
     BERT-base tower, [CLS] pooling, LinearHead(768 -> 1)."""
     from transformers import BertConfig, BertModel
-    from .model.encoder import HipBertEncoder, linear_head
+    from denseretrievaltoolkits_amd.model.encoder import HipBertEncoder, linear_head
     torch.manual_seed(0)
     m = BertModel(BertConfig(), add_pooling_layer=False).eval()
     enc = HipBertEncoder.from_hf(m, device)
@@ -163,7 +163,7 @@ def run_train_scores(device, bq=512, d=768, n_passages=(2, 8), steps=20, warmup=
     [512, 512 n], CrossEntropy(mean) with target i * n, and its backward (dq, dp),
     fp32 end to end on the HIP op (torch.ops.drt.score_ce_fwd, score_ce.py), next to torch's fp32
     matmul + cross_entropy + autograd on the same device."""
-    from .score_ce import score_ce
+    from denseretrievaltoolkits_amd.score_ce import score_ce
     g = torch.Generator(device=device)
     g.manual_seed(3)
     res = {"metric": "in-batch-negative score+CE forward+backward, ms per step (fp32)", "batch": bq, "dim": d}
@@ -231,7 +231,7 @@ def run_train_step(device, bq=512, n=2, q_len=32, p_len=128, steps=3, warmup=1):
     HF's own masks vs the tower's hash masks).  Optimizer update excluded (identical for both)."""
     from types import SimpleNamespace
     from transformers import BertConfig, BertModel
-    from .model.biencoder import DRModel
+    from denseretrievaltoolkits_amd.model.biencoder import DRModel
     torch.manual_seed(0)
     lm = BertModel(BertConfig(), add_pooling_layer=False).to(device).train()
     m = DRModel(lm_q=lm, lm_p=lm, pooling="first", data_args=SimpleNamespace(train_n_passages=n),
@@ -274,3 +274,123 @@ def run_train_step(device, bq=512, n=2, q_len=32, p_len=128, steps=3, warmup=1):
     res["speedup_vs_bf16_autocast"] = round(res["torch_bf16_autocast_ms"] / res["hip_ms"], 2)
     res["mfma_frac"] = round(res["hip_tflops"] / 2500.0, 4)
     return res
+
+
+WORDS = ["paris", "tower", "river", "york", "music", "rock", "roll", "bank", "tokyo", "alps", "city", "bridge",
+         "history", "capital", "song", "album", "band", "film", "actor", "war", "king", "queen", "ship", "island",
+         "mountain", "lake", "france", "england", "germany", "spain", "china", "japan"]
+
+
+class _SyntheticCorpus:
+    """Passages in the reference's CorpusDataset item format ({'original': text}), generated from the
+    doc id (no storage): 12 words of a small vocabulary."""
+
+    def __init__(self, n):
+        self.n = n
+
+    def __len__(self):
+        return self.n
+
+    def __getitem__(self, i):
+        w = WORDS
+        return {"original": " ".join(w[(i * 7 + j * 13 + (i >> 5)) % len(w)] for j in range(12))}
+
+
+class _Loader:
+    """Collated batches in the reference collators' formats (PPCollator: (ids, {input_ids,
+    attention_mask}); EVCollator: (qids, {...}, answers, query texts)), token ids generated on the host
+    per batch (uniform in [1000, 30521], [CLS] = 101 first, [SEP] = 102 last, no padding)."""
+
+    def __init__(self, n, bs, L, seed, dataset=None, queries=False):
+        self.n, self.bs, self.L, self.seed, self.dataset, self.queries = n, bs, L, seed, dataset, queries
+        self.sampler = None
+
+    def __len__(self):
+        return -(-self.n // self.bs)
+
+    def __iter__(self):
+        import numpy as np
+        for j, a in enumerate(range(0, self.n, self.bs)):
+            b = min(self.n, a + self.bs)
+            rng = np.random.default_rng((self.seed, j))
+            ids = rng.integers(1000, 30522, size=(b - a, self.L), dtype=np.int64)
+            ids[:, 0], ids[:, -1] = 101, 102
+            item = {"input_ids": torch.from_numpy(ids), "attention_mask": torch.ones((b - a, self.L), dtype=torch.int64)}
+            if self.queries:
+                yield (list(range(a, b)), item, [[WORDS[(q * 5) % len(WORDS)]] for q in range(a, b)],
+                       [f"query {q}" for q in range(a, b)])
+            else:
+                yield list(range(a, b)), item
+
+
+def run_evaluate_c2(device, n_passages=1_000_000, n_queries=10_000, k=1000, p_len=128, q_len=32, p_batch=512,
+                    q_batch=128):
+    """Config C2 end to end through the reference's own hot caller (DRT/trainer/trainer.py:191-218,
+    269-346): Trainer.evaluate over BERT-base (random init) -> _encoding_corpus of n_passages
+    128-token passages into the HBM shard -> 10k 32-token queries (loader batches of 128) encoded,
+    searched at top-k=1000 and matched against their answers -> get_metrics.  Stage times come from
+    the Trainer's own timers (profile_eval: one device sync between the corpus and query stages);
+    the device-only query stage (query tower and search alone, same reps) is timed beside it.
+    Retrieval output files are off (retrieve_dir ''): 10M JSON lines are file I/O, not the path."""
+    from types import SimpleNamespace
+    from transformers import BertConfig, BertModel
+    from denseretrievaltoolkits_amd.model.biencoder import DRModel
+    from denseretrievaltoolkits_amd.trainer.trainer import Trainer
+    torch.manual_seed(0)
+    lm = BertModel(BertConfig(), add_pooling_layer=False).eval()
+    model = DRModel(lm_q=lm, lm_p=lm, pooling="first")
+    args = SimpleNamespace(loss_fn="SimpleContrastiveLoss", learning_rate=1e-5, optimizer="adamw",
+                           topk="1,5,20,100,1000", retrieve_num=k, retrieve_dir="", cache_train_dir="",
+                           encode_corpus_dir="", index_order_dir="", max_epochs=0, save_per_train=1,
+                           eval_per_train=1)
+    corpus = _SyntheticCorpus(n_passages)
+
+    def loaders(n_p, n_q):
+        return (_Loader(n_p, p_batch, p_len, 11, dataset=corpus),
+                _Loader(n_q, q_batch, q_len, 12, queries=True))
+
+    cl, ql = loaders(4 * p_batch, 2 * q_batch)                   # warm-up: kernels, weight snapshot
+    tr = Trainer(args, model, corpus_dataloader=cl, eval_loader=ql)
+    tr.evaluate(ql, 0)
+    cl, ql = loaders(n_passages, n_queries)
+    tr.corpus_dataloader = cl
+    tr.profile_eval = True
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    m = tr.evaluate(ql, 1)
+    torch.cuda.synchronize()
+    total = time.perf_counter() - t0
+    tm = dict(tr.last_eval_timing)
+    # device-only query stage on the same index: the query tower over the loader's batches (windows of
+    # Trainer.ENCODE_WINDOW), then the certified pipelined search of the reps in batches of 128
+    wins = list(tr._query_windows(ql))
+    torch.cuda.synchronize()
+    t1 = time.perf_counter()
+    reps = torch.cat([tr._encode_window(w) for w in wins])
+    torch.cuda.synchronize()
+    t2 = time.perf_counter()
+    res = tr.index.local.search_batches([reps[a: a + q_batch] for a in range(0, reps.shape[0], q_batch)], k)
+    torch.cuda.synchronize()
+    t3 = time.perf_counter()
+    del res
+    qps_e2e = n_queries / tm["queries_s"]
+    return {
+        "metric": "C2 through Trainer.evaluate: passages encoded/sec + queries/sec@top-1000 (encode + search + "
+                  "answer matching + metrics)",
+        "n_passages": n_passages, "n_queries": n_queries, "k": k, "p_len": p_len, "q_len": q_len,
+        "corpus_batch": p_batch, "query_batch": q_batch,
+        "passages_per_s": round(n_passages / tm["corpus_s"], 1),
+        "queries_per_s_end_to_end": round(qps_e2e, 1),
+        "total_s": round(total, 2),
+        "stages_s": {k_: round(v, 3) for k_, v in tm.items()},
+        "host_match_ms_per_query": round(tm["host_match_s"] / n_queries * 1e3, 4),
+        "device_only": {
+            "query_encode_s": round(t2 - t1, 4),
+            "query_encode_qps": round(n_queries / (t2 - t1), 1),
+            "search_s": round(t3 - t2, 4),
+            "search_qps": round(n_queries / (t3 - t2), 1),
+        },
+        "query_num": m["query_num"],
+        "recall@1000": m.get("Recall@1000"),
+        "data": "synthetic: random-init BERT-base, uniform token ids, 12-word synthetic passages, one-word answers",
+    }

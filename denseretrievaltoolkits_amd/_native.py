@@ -36,7 +36,6 @@ _SIGNATURES = [
     ("drt_ip_topk_resolve_workspace", c_sz, [c_i64, c_i64, c_i32]),
     ("drt_ip_topk_resolve", c_i32, [c_vp, c_i64, c_vp, c_i64, c_i32, c_i32, c_i64, c_vp, c_vp, c_vp, c_vp, c_sz,
                                     c_vp, c_vp]),
-    ("drt_scan_variant", c_i32, [c_i32]),
     ("drt_topk_merge", c_i32, [c_vp, c_vp, c_i64, c_i32, c_i32, c_i32, c_vp, c_vp, c_vp]),
     ("drt_ip_topk_sample_rank", c_i32, [c_i32]),
     ("drt_ip_topk_dist_workspace", c_sz, [c_i64, c_i64, c_i64, c_i32, c_i32]),
@@ -49,7 +48,6 @@ _SIGNATURES = [
     ("drt_ip_topk_dist_filter_lists_at", c_i32, [c_vp, c_i64, c_vp, c_i64, c_i64, c_i32, c_i32, c_i64, c_vp,
                                                  c_i32, c_i64, c_vp, c_vp, c_vp, c_sz, c_vp]),
     ("drt_topk_merge_packed", c_i32, [c_vp, c_i64, c_i32, c_i32, c_i64, c_vp, c_vp, c_vp, c_vp]),
-    ("drt_topk_merge_packed_variant", c_i32, [c_i32]),
     ("drt_gemm_nt_bf16_f32", c_i32, [c_vp, c_vp, c_vp, c_i64, c_i64, c_i32, c_i64, c_vp]),
     ("drt_embed_ln", c_i32, [c_vp, c_vp, c_i64, c_i64, c_vp, c_vp, c_vp, c_vp, c_vp, c_f32, c_i32, c_vp, c_vp]),
     ("drt_linear_bf16", c_i32, [c_vp, c_vp, c_vp, c_vp, c_vp, c_i64, c_i64, c_i64, c_i32, c_vp]),
@@ -87,13 +85,6 @@ _SIGNATURES = [
     ("drt_attention_bf16", c_i32, [c_vp, c_vp, c_vp, c_i64, c_i64, c_i32, c_i32, c_f32, c_vp]),
     ("drt_pool_bf16", c_i32, [c_vp, c_vp, c_i64, c_i64, c_i32, c_i32, c_vp, c_vp, c_vp]),
     ("drt_l2_normalize_f32", c_i32, [c_vp, c_i64, c_i32, c_vp, c_vp]),
-    ("drt_gemm_split_config", c_i32, [c_i64, c_i64, c_i64]),
-    ("drt_gemm_large_min_tiles", c_i32, [c_i64]),
-    ("drt_gemm_mid_config", c_i32, [c_i64, c_i64, c_i64]),
-    ("drt_gemm_force_small", c_i32, [c_i32]),
-    ("drt_attention_force4", c_i32, [c_i32]),
-    ("drt_gemm_debug_buffer", c_i32, [c_vp]),
-    ("drt_gemm_tile_order", c_i32, [c_i32]),
     ("drt_gemm_nt_f32", c_i32, [c_vp, c_vp, c_vp, c_i64, c_i64, c_i64, c_i64, c_i64, c_i64, c_vp]),
     ("drt_gemm_f32", c_i32, [c_vp, c_vp, c_vp, c_i64, c_i64, c_i64, c_i64, c_i64, c_i64, c_i32, c_i32, c_i32, c_vp, c_vp]),
     ("drt_ce_fwd", c_i32, [c_vp, c_i64, c_i64, c_i64, c_f32, c_vp, c_vp, c_vp, c_vp]),

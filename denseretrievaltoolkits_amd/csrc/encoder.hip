@@ -158,8 +158,6 @@ __global__ __launch_bounds__(256) void layernorm_bf16_kernel(const __bf16* X, in
 // with a padded row stride (A operand of O^T = V^T P^T).
 // ---------------------------------------------------------------------------
 constexpr int kAttnThreads = 256;
-// A/B switch (drt_attention_force4): 1 keeps 4-wave work-groups at every length
-static int g_attn_force4 = 0;
 constexpr int kHeadDim = 64;
 constexpr int kMaxSeq = 512;
 
@@ -412,15 +410,6 @@ __global__ __launch_bounds__(256) void l2norm_kernel(float* x, int64_t B, int H,
 using namespace drt;
 
 extern "C" {
-
-// Benchmark / test switch: 1 keeps the 4-wave attention BACKWARD work-groups at every sequence
-// length, 0 (default) takes 8 waves for 5 blocks (L 129-160; tools/attn_bwd_probe.py).
-int drt_attention_force4(int32_t on) {
-  if (on < 0 || on > 31) return DRT_EINVAL;   // >= 16: diagnostic backward ablations
-  g_attn_force4 = on;
-  return DRT_OK;
-}
-int drt_attention_force4_get(void) { return g_attn_force4; }
 
 int drt_embed_ln_pre(const int64_t* ids, const int64_t* type_ids, int64_t B, int64_t L, const float* word_emb,
                      const float* pos_emb, const float* type_emb, const float* gamma, const float* beta, float eps,

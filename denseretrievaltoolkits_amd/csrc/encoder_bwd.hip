@@ -613,8 +613,6 @@ using namespace drt;
 
 extern "C" {
 
-int drt_attention_force4_get(void);   // csrc/encoder.hip
-
 size_t drt_colsum_workspace(int64_t M, int64_t N) {
   if (M <= 0 || N <= 0) return 0;
   const int64_t slabs = colsum_slabs(M, N);
@@ -714,7 +712,7 @@ int drt_attention_train_bwd_bf16(const void* qkv, const void* ctx, const void* d
   AttnBwdArgs a{(const __bf16*)qkv, (const __bf16*)ctx, (const __bf16*)dctx, lse, mask, (__bf16*)dqkv, B, L,
                 heads, heads * 64, scale, drop_p, seed, site};
   const int Lp = ((int)L + 31) & ~31;
-  const bool w8 = Lp / 32 > 4 && drt_attention_force4_get() == 0;
+  const bool w8 = Lp / 32 > 4;
   const int nw = w8 ? 8 : 4;
   const size_t lds = (size_t)4 * Lp * kAbRow + (size_t)nw * 32 * kAbScr + (size_t)3 * Lp * 4;
   DRT_REQUIRE(lds <= 160 * 1024);
@@ -724,25 +722,10 @@ int drt_attention_train_bwd_bf16(const void* qkv, const void* ctx, const void* d
                                       hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
     DRT_CHECK_HIP(hipFuncSetAttribute((const void*)attention_bwd_kernel<8>,
                                       hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
-    const void* abl_k[] = {(const void*)attention_bwd_kernel<4, 1>, (const void*)attention_bwd_kernel<4, 2>,
-                           (const void*)attention_bwd_kernel<4, 4>, (const void*)attention_bwd_kernel<4, 8>,
-                           (const void*)attention_bwd_kernel<4, 12>};
-    for (const void* f : abl_k)
-      DRT_CHECK_HIP(hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
     attr_set = true;
   }
-  const int abl = drt_attention_force4_get() >= 16 ? drt_attention_force4_get() - 16 : 0;
   const dim3 grid((unsigned)(B * heads));
-  if (abl) {
-    switch (abl) {   // diagnostic ablations (4 waves)
-      case 1: hipLaunchKernelGGL((attention_bwd_kernel<4, 1>), grid, dim3(256), lds, (hipStream_t)stream, a); break;
-      case 2: hipLaunchKernelGGL((attention_bwd_kernel<4, 2>), grid, dim3(256), lds, (hipStream_t)stream, a); break;
-      case 4: hipLaunchKernelGGL((attention_bwd_kernel<4, 4>), grid, dim3(256), lds, (hipStream_t)stream, a); break;
-      case 8: hipLaunchKernelGGL((attention_bwd_kernel<4, 8>), grid, dim3(256), lds, (hipStream_t)stream, a); break;
-      case 12: hipLaunchKernelGGL((attention_bwd_kernel<4, 12>), grid, dim3(256), lds, (hipStream_t)stream, a); break;
-      default: return DRT_EINVAL;
-    }
-  } else if (w8) {
+  if (w8) {
     hipLaunchKernelGGL((attention_bwd_kernel<8>), grid, dim3(512), lds, (hipStream_t)stream, a);
   } else {
     hipLaunchKernelGGL((attention_bwd_kernel<4>), grid, dim3(256), lds, (hipStream_t)stream, a);

@@ -22,6 +22,8 @@ constexpr int kTileA = kBM * kBK * 2;  // 16 KiB
 constexpr int kTileB = kBN * kBK * 2;  // 16 KiB
 constexpr int kStage = kTileA + kTileB;
 constexpr int kGemmLds = 2 * kStage;   // 64 KiB -> 2 work-groups per CU
+constexpr int kL = 256;                // 256^2 kernels: tile edge
+constexpr int kLThreads = 512;
 
 struct GemmArgs {
   const __bf16* A;   // [m][lda]
@@ -32,7 +34,6 @@ struct GemmArgs {
   int64_t m, n, k;
   int64_t lda, ldb, ldc, ldr;
   float alpha;
-  unsigned long long* dbg;  // diagnostic builds only (segment stamps)
   int order;                // tile order within an XCD's range (tile_order)
   int64_t kchunk;           // split-K (128^2 kernel, PART): k per split; ws [splits][m][n] fp32
   float* ws;
@@ -40,7 +41,6 @@ struct GemmArgs {
   float drop_p;             // EPI_DROP: dropout probability, hash seed and site (drt_common.h)
   uint64_t seed, site;
 };
-static unsigned long long* g_gemm_dbg = nullptr;
 
 __device__ __forceinline__ void g_glds16(const void* gsrc, uint32_t lds_addr) {
   uint32_t keep;
@@ -131,9 +131,11 @@ __device__ __forceinline__ float epi_post(const GemmArgs& a, float v, int64_t ro
   return v;
 }
 
-static int g_gemm_variant = 0;
-static int64_t g_large_min_tiles = 128;   // 256^2 kernel from this many 256^2 tiles up (tools/qsweep.py: 128 beats 512 by 16-22 % on 4k-16k-token batches)
-static int g_gemm_order = -1;   // -1 auto: grouped-8 for K <= 1024 (small panels), row-major otherwise  // A/B switch: 0 auto (large full-K), 1 small 128^2, 2 large half-K ring
+// 256^2 kernel from this many 256^2 tiles up (tools/qsweep.py: 128 beats 512 by 16-22 % on 4k-16k-token
+// batches); tile order inside an XCD's range: grouped-8 for K <= 1024 (small panels), row-major otherwise
+// (profiles/r02o_gemm_tile_order.log: orders within noise).
+constexpr int64_t kLargeMinTiles = 128;
+__host__ __device__ constexpr int auto_tile_order(int64_t k) { return k <= 1024 ? 1 : 0; }
 
 template <bool OUT_BF16, int EPI, bool PART = false>
 __global__ __launch_bounds__(kGemmThreads, 2) void gemm_nt_kernel(GemmArgs a) {
@@ -333,53 +335,29 @@ __global__ __launch_bounds__(256) void splitk_ln_kernel(const float* ws, int spl
   ln_row<EPL>(x, gamma, beta, eps, lane, H, out + t * H);
 }
 
-// Split plan of the 128^2 kernel for problems too small to fill the chip (query-sized
-// batches): enough splits for ~2 blocks per CU, >= 128 k per split.  0 = no split.
-// split-K planning knobs (drt_gemm_split_config): the 256^2 kernel splits K >= g_lsplit_min_k into
-// chunks of >= g_lsplit_k_per; the 128^2 kernel keeps its fp32 partials <= g_ssplit_cap bytes
-static int64_t g_lsplit_min_k = 8192, g_lsplit_k_per = 512, g_ssplit_cap = 16 << 20;
-static int small_splits(int64_t m, int64_t n, int64_t k, int64_t* kchunk) {
-  const int64_t tiles = ((m + kBM - 1) / kBM) * ((n + kBN - 1) / kBN);
-  if (tiles >= 384 || k < 256) return 0;
-  int64_t splits = (512 + tiles - 1) / tiles;
-  if (splits > k / 128) splits = k / 128;
-  // partials must stay small enough to be re-read from the caches: at 4096 x 768 (a 128-query
-  // batch) 3 splits = 38 MB of partials measured slower than the unsplit kernel
-  const int64_t cap = g_ssplit_cap / (m * n * 4);
-  if (splits > cap) splits = cap;
-  if (splits < 2) return 0;
-  int64_t kc = (k + splits - 1) / splits;
-  kc = (kc + kBK - 1) / kBK * kBK;
-  splits = (k + kc - 1) / kc;
-  if (splits < 2) return 0;
-  *kchunk = kc;
-  return (int)splits;
-}
+// ---------------------------------------------------------------------------
+// GEMM plan: ONE function decides the kernel and the K split of a problem, and both the
+// workspace query (drt_linear_workspace) and every launcher use it, so the scratch a caller
+// sizes is exactly the scratch the launch writes.
+//   LARGE        >= kLargeMinTiles 256^2 tiles: the whole-line 256^2 kernel, unsplit
+//   LARGE_SPLIT  long K (>= kLSplitMinK) on a small 256^2 grid: K split so the grid is at most
+//                ONE round of blocks (floor(CUs / tiles) splits; a ceiling put e.g. 9 tiles x 29
+//                splits = 261 blocks on 256 CUs and the launch took ~2x its one-round time),
+//                >= kLSplitKPer per split, fp32 partials <= 256 MiB, fixed-order reduction
+//   SMALL_SPLIT  query-sized problems (< 384 tiles of 128^2, K >= 256): 128^2 kernel, ~2 blocks
+//                per CU, >= 128 K per split, partials <= 16 MiB (at 4096 x 768 -- a 128-query
+//                batch -- 3 splits = 38 MB of partials measured slower than unsplit)
+//   SMALL        everything else (and any split plan whose scratch the caller did not give)
+// ---------------------------------------------------------------------------
+constexpr int64_t kLSplitMinK = 8192, kLSplitKPer = 512, kSSplitCap = 16 << 20;
+enum GemmPath { GP_LARGE, GP_LARGE_SPLIT, GP_SMALL_SPLIT, GP_SMALL };
+struct GemmPlan {
+  int path = GP_SMALL;
+  int splits = 0;
+  int64_t kchunk = 0;
+  size_t ws_bytes = 0;   // fp32 partials the split needs
+};
 
-// Split plan of the 256^2 whole-line kernel for mid-size problems (query batches of 1k-16k
-// tokens: fewer 256^2 tiles than g_large_min_tiles, i.e. the chip is not filled): splits so the
-// grid reaches ~one block per CU, >= g_msplit_min_kt K-tiles of 64 per split, fp32 partials
-// <= g_msplit_cap bytes.  M < g_msplit_min_m stays on the 128^2 kernel.  0 = no split (the
-// 256^2 kernel unsplit when M >= g_msplit_min_m).
-static int64_t g_msplit_min_m = 1 << 30, g_msplit_cap = 64 << 20, g_msplit_min_kt = 4;
-static int mid_splits(int64_t m, int64_t n, int64_t k, int64_t* kchunk) {
-  const int64_t tiles = ((m + 255) / 256) * ((n + 255) / 256);
-  int64_t splits = (256 + tiles - 1) / tiles;
-  if (splits > k / (64 * g_msplit_min_kt)) splits = k / (64 * g_msplit_min_kt);
-  const int64_t cap = g_msplit_cap / (m * n * 4);
-  if (splits > cap) splits = cap;
-  if (splits < 2) return 0;
-  int64_t kc = (k + splits - 1) / splits;
-  kc = (kc + 63) / 64 * 64;
-  splits = (k + kc - 1) / kc;
-  if (splits < 2) return 0;
-  *kchunk = kc;
-  return (int)splits;
-}
-
-// Split plan of the 256^2 kernel for long-K problems whose 256^2 grid is small (weight
-// gradients dW = dY^T X: K = tokens, M x N = a weight matrix): ~256 blocks, >= 16 slabs per
-// split, fp32 partials <= 256 MiB.  0 = no split.
 // Compute units of the current device, looked up once per process.
 static int gemm_cus() {
   static int cus = 0;
@@ -393,273 +371,67 @@ static int gemm_cus() {
   return cus;
 }
 
-// Round 2: at most ONE round of blocks (floor(CUs / tiles) splits): the ceiling this plan used
-// before put e.g. 9 tiles x 29 splits = 261 blocks on 256 CUs, so 5 blocks ran a second full
-// round and the launch took ~2x its one-round time (drt_gemm_force_small(14) restores it for A/B).
-static int large_splits(int64_t m, int64_t n, int64_t k, int64_t min_tiles, int64_t* kchunk) {
-  const int64_t tiles = ((m + 255) / 256) * ((n + 255) / 256);
-  if (tiles >= min_tiles || k < g_lsplit_min_k || k % 32) return 0;
-  const int64_t cus = gemm_cus();
-  int64_t splits = g_gemm_variant == 14 ? (256 + tiles - 1) / tiles : cus / tiles;
-  if (splits > k / g_lsplit_k_per) splits = k / g_lsplit_k_per;
-  const int64_t cap = (int64_t)(256ll << 20) / (m * n * 4);
-  if (splits > cap) splits = cap;
+// splits -> (splits, kchunk) with kchunk a multiple of `align`; < 2 splits = none
+static int round_splits(int64_t k, int64_t splits, int64_t align, int64_t* kchunk) {
   if (splits < 2) return 0;
   int64_t kc = (k + splits - 1) / splits;
-  kc = (kc + 63) / 64 * 64;
+  kc = (kc + align - 1) / align * align;
   splits = (k + kc - 1) / kc;
   if (splits < 2) return 0;
   *kchunk = kc;
   return (int)splits;
 }
 
-// ---------------------------------------------------------------------------
-// Large-tile variant for the encoder projections (M = tokens >> 256).
-//  * 256 x 256 output tile, 8 waves (2 along M x 4 along N), wave tile 128 x 64.
-//  * K streamed in half-tiles of 32: A and B halves (256 rows x 64 B each,
-//    16 KiB) land by LDS-DMA in a 4-slot ring (128 KiB); three half-tiles stay
-//    in flight across the raw s_barrier (counted vmcnt, never 0 in the loop).
-//  * operands swapped (D = W . X^T): each lane owns one token row and four
-//    consecutive output columns per register group, so the epilogue issues
-//    16-B (fp32) / 8-B (bf16) stores and 16-B bias / 8-B residual loads.
-// LDS half-tile image: [row][4 x 16 B], chunk XOR-swizzled by (row >> 2) & 3
-// (conflict-free ds_read_b128 for 32-row fragment reads).
-// ---------------------------------------------------------------------------
-constexpr int kL = 256;                  // tile edge
-constexpr int kLThreads = 512;
-constexpr int kLHalf = kL * 32 * 2;      // 16 KiB: one operand, 32 k
-constexpr int kLSlot = 2 * kLHalf;       // A half + B half
-constexpr int kLSlots = 4;
-constexpr int kLGlds = 2 * kLHalf / 1024 / 8;   // LDS-DMA instructions per wave per slot (4)
-
-// 256 rows x 32 k: 16 wave-instructions of 16 rows x 64 B, 2 per wave.
-__device__ __forceinline__ void stage_half256(const __bf16* base, int64_t ld, int64_t row0, int64_t rows,
-                                              int64_t k0, uint32_t lds, int wave, int lane) {
-  const int rsub = lane >> 2, pos = lane & 3;
-#pragma unroll
-  for (int j = 0; j < 2; ++j) {
-    const int J = j * 8 + wave;           // 0..15
-    const int row = J * 16 + rsub;        // 0..255
-    int64_t gr = row0 + row;
-    gr = gr < rows ? gr : rows - 1;
-    const int c = pos ^ ((row >> 2) & 3);
-    g_glds16(base + gr * ld + k0 + c * 8, __builtin_amdgcn_readfirstlane(lds + J * 1024));
-  }
+static int large_splits(int64_t m, int64_t n, int64_t k, int64_t* kchunk) {
+  const int64_t tiles = ((m + 255) / 256) * ((n + 255) / 256);
+  if (tiles >= kLargeMinTiles || k < kLSplitMinK || k % 32) return 0;
+  int64_t splits = gemm_cus() / tiles;
+  if (splits > k / kLSplitKPer) splits = k / kLSplitKPer;
+  const int64_t cap = (int64_t)(256ll << 20) / (m * n * 4);
+  if (splits > cap) splits = cap;
+  return round_splits(k, splits, 64, kchunk);
 }
 
-template <bool OUT_BF16, int EPI>
-__global__ __launch_bounds__(kLThreads, 1) void gemm_nt_lh_kernel(GemmArgs a) {
-  __shared__ __attribute__((aligned(16))) char smem[kLSlots * kLSlot];
-  const int tid = threadIdx.x;
-  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int lane = tid & 63;
-  const int r = lane & 31, h = lane >> 5;
-  const int wm = wave >> 2, wn = wave & 3;   // 2 x 4 waves
-
-  const int nwg = gridDim.x;
-  const int bid = blockIdx.x;
-  const int xcd = bid & 7, q8 = nwg >> 3, r8 = nwg & 7;
-  const int wg = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (bid >> 3);
-  const int tiles_n = (int)((a.n + kL - 1) / kL);
-  const int64_t m0 = (int64_t)(wg / tiles_n) * kL;
-  const int64_t n0 = (int64_t)(wg % tiles_n) * kL;
-
-  const uint32_t lds0 = g_lds_addr(smem);
-  const int nh = (int)(a.k / 32);   // half-tiles
-
-  // acc[j][i]: D rows = W rows (n), cols = X rows (m)
-  f32x16 acc[2][4];
-#pragma unroll
-  for (int j = 0; j < 2; ++j)
-#pragma unroll
-    for (int i = 0; i < 4; ++i)
-#pragma unroll
-      for (int e = 0; e < 16; ++e) acc[j][i][e] = 0.0f;
-
-  const int sw = (r >> 2) & 3;
-  int aoff[2];
-#pragma unroll
-  for (int s = 0; s < 2; ++s) aoff[s] = r * 64 + ((((2 * s) | h) ^ sw) << 4);
-
-  // prologue: three half-tiles in flight
-#pragma unroll
-  for (int p = 0; p < 3; ++p) {
-    if (p < nh) {
-      const uint32_t sl = lds0 + p * kLSlot;
-      stage_half256(a.A, a.lda, m0, a.m, (int64_t)p * 32, sl, wave, lane);
-      stage_half256(a.B, a.ldb, n0, a.n, (int64_t)p * 32, sl + kLHalf, wave, lane);
-    }
-  }
-
-  for (int hs = 0; hs < nh; ++hs) {
-    const int younger = nh - 1 - hs;   // half-tiles issued after this one (<= 2)
-    if (younger >= 2) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
-    else if (younger == 1) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
-    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    __builtin_amdgcn_s_barrier();
-    if (hs + 3 < nh) {
-      const uint32_t sl = lds0 + ((hs + 3) & 3) * kLSlot;
-      stage_half256(a.A, a.lda, m0, a.m, (int64_t)(hs + 3) * 32, sl, wave, lane);
-      stage_half256(a.B, a.ldb, n0, a.n, (int64_t)(hs + 3) * 32, sl + kLHalf, wave, lane);
-    }
-    const char* Xs = smem + (hs & 3) * kLSlot + wm * 128 * 64;            // A panel (tokens)
-    const char* Ws = smem + (hs & 3) * kLSlot + kLHalf + wn * 64 * 64;    // B panel (weights)
-#pragma unroll
-    for (int s = 0; s < 2; ++s) {
-      bf16x8 wf[2], xf[4];
-#pragma unroll
-      for (int j = 0; j < 2; ++j) wf[j] = *(const bf16x8*)(Ws + j * 32 * 64 + aoff[s]);
-#pragma unroll
-      for (int i = 0; i < 4; ++i) xf[i] = *(const bf16x8*)(Xs + i * 32 * 64 + aoff[s]);
-      __builtin_amdgcn_s_setprio(1);
-#pragma unroll
-      for (int j = 0; j < 2; ++j)
-#pragma unroll
-        for (int i = 0; i < 4; ++i)
-          acc[j][i] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wf[j], xf[i], acc[j][i], 0, 0, 0);
-      __builtin_amdgcn_s_setprio(0);
-    }
-  }
-
-  l_epilogue<OUT_BF16, EPI>(a, acc, m0, n0, wm, wn, r, h);
+static int small_splits(int64_t m, int64_t n, int64_t k, int64_t* kchunk) {
+  const int64_t tiles = ((m + kBM - 1) / kBM) * ((n + kBN - 1) / kBN);
+  if (tiles >= 384 || k < 256) return 0;
+  int64_t splits = (512 + tiles - 1) / tiles;
+  if (splits > k / 128) splits = k / 128;
+  const int64_t cap = kSSplitCap / (m * n * 4);
+  if (splits > cap) splits = cap;
+  return round_splits(k, splits, kBK, kchunk);
 }
 
-// Full-K-tile large kernel: BK = 64, 128-B row image ([row][8 x 16 B], chunk
-// XOR (row >> 1) & 7), 2-slot ring (2 x 64 KiB), one vmcnt(0) + barrier per
-// K-tile, next K-tile staged before the current one's MFMAs; swapped-operand
-// epilogue as above.
-__device__ __forceinline__ void stage_full256(const __bf16* base, int64_t ld, int64_t row0, int64_t rows,
-                                              int64_t k0, uint32_t lds, int wave, int lane) {
-  const int rsub = lane >> 3, pos = lane & 7;
-#pragma unroll
-  for (int j = 0; j < 4; ++j) {
-    const int J = j * 8 + wave;           // 0..31
-    const int row = J * 8 + rsub;         // 0..255
-    int64_t gr = row0 + row;
-    gr = gr < rows ? gr : rows - 1;
-    const int c = pos ^ ((row >> 1) & 7);
-    g_glds16(base + gr * ld + k0 + c * 8, __builtin_amdgcn_readfirstlane(lds + J * 1024));
+static GemmPlan plan_gemm(int64_t m, int64_t n, int64_t k) {
+  GemmPlan p;
+  if (m <= 0 || n <= 0 || k <= 0) return p;
+  const int64_t tiles_l = ((m + kL - 1) / kL) * ((n + kL - 1) / kL);
+  if (tiles_l >= kLargeMinTiles) {
+    p.path = GP_LARGE;
+    return p;
   }
+  int64_t kc = 0;
+  int s = large_splits(m, n, k, &kc);
+  if (s > 1) {
+    p.path = GP_LARGE_SPLIT;
+  } else {
+    s = small_splits(m, n, k, &kc);
+    if (s > 1) p.path = GP_SMALL_SPLIT;
+  }
+  if (s > 1) {
+    p.splits = s;
+    p.kchunk = kc;
+    p.ws_bytes = (size_t)s * (size_t)m * (size_t)n * sizeof(float);
+  }
+  return p;
 }
 
-template <bool OUT_BF16, int EPI>
-__device__ __forceinline__ void l_epilogue(const GemmArgs& a, f32x16 (&acc)[2][4], int64_t m0, int64_t n0, int wm,
-                                           int wn, int r, int h) {
-  const bool full_n = (n0 + kL <= a.n) && (a.ldc % 4 == 0) && (!(EPI & EPI_RESID) || a.ldr % 4 == 0);
-#pragma unroll
-  for (int j = 0; j < 2; ++j) {
-#pragma unroll
-    for (int g = 0; g < 4; ++g) {
-      const int64_t col = n0 + wn * 64 + j * 32 + 8 * g + 4 * h;
-      f32x4 bv = {0.f, 0.f, 0.f, 0.f};
-      if (EPI & EPI_BIAS) {
-        if (full_n) bv = *(const f32x4*)(a.bias + col);
-        else
-#pragma unroll
-          for (int u = 0; u < 4; ++u) bv[u] = col + u < a.n ? a.bias[col + u] : 0.f;
-      }
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const int64_t row = m0 + wm * 128 + i * 32 + r;
-        if (row >= a.m) continue;
-        f32x4 v;
-#pragma unroll
-        for (int u = 0; u < 4; ++u) {
-          float x = acc[j][i][4 * g + u] * a.alpha + bv[u];
-          if (EPI & EPI_GELU) x = gelu_erf(x);
-          v[u] = x;
-        }
-        if (full_n) {
-          if (EPI & EPI_RESID) {
-            const bf16x4 rv = *(const bf16x4*)(a.R + row * a.ldr + col);
-#pragma unroll
-            for (int u = 0; u < 4; ++u) v[u] += (float)rv[u];
-          }
-          if (OUT_BF16) {
-            bf16x4 o;
-#pragma unroll
-            for (int u = 0; u < 4; ++u) o[u] = (__bf16)v[u];
-            *(bf16x4*)((__bf16*)a.C + row * a.ldc + col) = o;
-          } else {
-            *(f32x4*)((float*)a.C + row * a.ldc + col) = v;
-          }
-        } else {
-#pragma unroll
-          for (int u = 0; u < 4; ++u) {
-            if (col + u >= a.n) continue;
-            float x = v[u];
-            if (EPI & EPI_RESID) x += (float)a.R[row * a.ldr + col + u];
-            if (OUT_BF16) ((__bf16*)a.C)[row * a.ldc + col + u] = (__bf16)x;
-            else ((float*)a.C)[row * a.ldc + col + u] = x;
-          }
-        }
-      }
-    }
-  }
-}
-
-template <bool OUT_BF16, int EPI>
-__global__ __launch_bounds__(kLThreads, 1) void gemm_nt_l_kernel(GemmArgs a) {
-  constexpr int kPanel = kL * kBK * 2;   // 32 KiB
-  constexpr int kStageL = 2 * kPanel;
-  __shared__ __attribute__((aligned(16))) char smem[2 * kStageL];
-  const int tid = threadIdx.x;
-  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int lane = tid & 63;
-  const int r = lane & 31, h = lane >> 5;
-  const int wm = wave >> 2, wn = wave & 3;
-  const int nwg = gridDim.x;
-  const int bid = blockIdx.x;
-  const int xcd = bid & 7, q8 = nwg >> 3, r8 = nwg & 7;
-  const int wg = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (bid >> 3);
-  const int tiles_n = (int)((a.n + kL - 1) / kL);
-  const int64_t m0 = (int64_t)(wg / tiles_n) * kL;
-  const int64_t n0 = (int64_t)(wg % tiles_n) * kL;
-  const uint32_t lds0 = g_lds_addr(smem);
-  const int ksteps = (int)(a.k / kBK);
-  f32x16 acc[2][4];
-#pragma unroll
-  for (int j = 0; j < 2; ++j)
-#pragma unroll
-    for (int i = 0; i < 4; ++i)
-#pragma unroll
-      for (int e = 0; e < 16; ++e) acc[j][i][e] = 0.0f;
-  const int sw = (r >> 1) & 7;
-  int aoff[4];
-#pragma unroll
-  for (int s = 0; s < 4; ++s) aoff[s] = r * 128 + ((((2 * s) | h) ^ sw) << 4);
-  stage_full256(a.A, a.lda, m0, a.m, 0, lds0, wave, lane);
-  stage_full256(a.B, a.ldb, n0, a.n, 0, lds0 + kPanel, wave, lane);
-  for (int kt = 0; kt < ksteps; ++kt) {
-    const int slot = kt & 1;
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    __builtin_amdgcn_s_barrier();
-    if (kt + 1 < ksteps) {
-      const uint32_t nb = lds0 + (slot ^ 1) * kStageL;
-      stage_full256(a.A, a.lda, m0, a.m, (int64_t)(kt + 1) * kBK, nb, wave, lane);
-      stage_full256(a.B, a.ldb, n0, a.n, (int64_t)(kt + 1) * kBK, nb + kPanel, wave, lane);
-    }
-    const char* Xs = smem + slot * kStageL + wm * 128 * 128;
-    const char* Ws = smem + slot * kStageL + kPanel + wn * 64 * 128;
-#pragma unroll
-    for (int s = 0; s < 4; ++s) {
-      bf16x8 wf[2], xf[4];
-#pragma unroll
-      for (int j = 0; j < 2; ++j) wf[j] = *(const bf16x8*)(Ws + j * 32 * 128 + aoff[s]);
-#pragma unroll
-      for (int i = 0; i < 4; ++i) xf[i] = *(const bf16x8*)(Xs + i * 32 * 128 + aoff[s]);
-      __builtin_amdgcn_s_setprio(1);
-#pragma unroll
-      for (int j = 0; j < 2; ++j)
-#pragma unroll
-        for (int i = 0; i < 4; ++i)
-          acc[j][i] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wf[j], xf[i], acc[j][i], 0, 0, 0);
-      __builtin_amdgcn_s_setprio(0);
-    }
-  }
-  l_epilogue<OUT_BF16, EPI>(a, acc, m0, n0, wm, wn, r, h);
+// The plan a launch actually runs: a split plan degrades to the unsplit 128^2 kernel when the
+// caller's scratch is missing or smaller than the plan needs (never writes past ws_bytes).
+static GemmPlan plan_for_launch(int64_t m, int64_t n, int64_t k, const void* ws, size_t ws_bytes) {
+  GemmPlan p = plan_gemm(m, n, k);
+  if (p.splits > 1 && (ws == nullptr || ws_bytes < p.ws_bytes)) p = GemmPlan{};
+  return p;
 }
 
 // ---------------------------------------------------------------------------
@@ -689,21 +461,6 @@ __global__ __launch_bounds__(kLThreads, 1) void gemm_nt_l_kernel(GemmArgs a) {
 constexpr int kPPanel = kL * 32 * 2;     // 16 KiB
 constexpr int kPSlab = 2 * kPPanel;      // 32 KiB
 constexpr int kPRing = 4;
-
-// 256 rows x 32 k into a [row][4 x 16 B] panel: 16 wave-instructions of 16 rows, 2 per wave.
-__device__ __forceinline__ void stage_panel32(const __bf16* base, int64_t ld, int64_t row0, int64_t rows,
-                                              int64_t k0, uint32_t lds, int wave, int lane) {
-  const int rsub = lane >> 2, pos = lane & 3;
-#pragma unroll
-  for (int j = 0; j < 2; ++j) {
-    const int J = j * 8 + wave;
-    const int row = J * 16 + rsub;
-    int64_t gr = row0 + row;
-    gr = gr < rows ? gr : rows - 1;
-    const int c = pos ^ ((row >> 1) & 2);
-    g_glds16(base + gr * ld + k0 + c * 8, __builtin_amdgcn_readfirstlane(lds + J * 1024));
-  }
-}
 
 // TN operands (weight gradients dW = dY^T X: both stored [t][features], t = the reduction
 // index): a 32-t slab of a 256-column panel is 32 rows of 512 B (whole cache lines) in a
@@ -775,28 +532,6 @@ __device__ __forceinline__ void tile_order(int order, int wg, int nwg, int tiles
   tn = l / gm;
 }
 
-// s_waitcnt vmcnt(4 * n + extra), extra in {0, 16}: the n youngest slabs plus `extra`
-// younger non-DMA loads may stay in flight.
-__device__ __forceinline__ void vmcnt_slabs_after_plus(int n, int extra) {
-  if (extra == 0) {
-    switch (n) {
-      case 0: asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); break;
-      case 1: asm volatile("s_waitcnt vmcnt(4)" ::: "memory"); break;
-      case 2: asm volatile("s_waitcnt vmcnt(8)" ::: "memory"); break;
-      case 3: asm volatile("s_waitcnt vmcnt(12)" ::: "memory"); break;
-      default: asm volatile("s_waitcnt vmcnt(16)" ::: "memory"); break;
-    }
-    return;
-  }
-  switch (n) {
-    case 0: asm volatile("s_waitcnt vmcnt(16)" ::: "memory"); break;
-    case 1: asm volatile("s_waitcnt vmcnt(20)" ::: "memory"); break;
-    case 2: asm volatile("s_waitcnt vmcnt(24)" ::: "memory"); break;
-    case 3: asm volatile("s_waitcnt vmcnt(28)" ::: "memory"); break;
-    default: asm volatile("s_waitcnt vmcnt(32)" ::: "memory"); break;
-  }
-}
-
 // s_waitcnt vmcnt(4 * n): all but the n youngest slabs (4 LDS-DMA per wave each) landed.
 __device__ __forceinline__ void vmcnt_slabs_after(int n) {
   switch (n) {
@@ -838,24 +573,9 @@ __device__ __forceinline__ void pp_epilogue(const GemmArgs& a, f32x4 (&acc)[8][4
 // slice in a private LDS region (row-per-lane 8-B pieces in, 16-B row-contiguous
 // pieces out, 16-B chunks XOR-swizzled by row), then writes whole 128-B (bf16) /
 // 256-B (fp32) row segments.  Needs a full tile in n; rows are masked.
-// Residual rows of one 64-row half of a wave's slice, in the read-back lane map of the
-// fp32 LDS epilogue (row p * 4 + lane / 16, 4 columns at (lane & 15) * 4).
-__device__ __forceinline__ void load_resid_half(const GemmArgs& a, int64_t m0, int64_t n0, int grp, int wn, int h,
-                                                int lane, bf16x4 (&rv)[16]) {
-  const int64_t colw = n0 + wn * 64;
-  const int c = lane & 15;
-#pragma unroll
-  for (int p = 0; p < 16; ++p) {
-    int64_t row = m0 + grp * 128 + h * 64 + p * 4 + (lane >> 4);
-    row = row < a.m ? row : a.m - 1;
-    rv[p] = *(const bf16x4*)(a.R + row * a.ldr + colw + c * 4);
-  }
-}
-
-template <bool OUT_BF16, int EPI, bool PRE = false>
+template <bool OUT_BF16, int EPI>
 __device__ __forceinline__ void pp_epilogue_lds(const GemmArgs& a, f32x4 (&acc)[8][4], int64_t m0, int64_t n0,
-                                                int grp, int wn, int fr, int fc, char* lds_wave, int lane,
-                                                bf16x4 (&rv0)[16]) {
+                                                int grp, int wn, int fr, int fc, char* lds_wave, int lane) {
   const int64_t colw = n0 + wn * 64;   // first column of this wave's slice
   f32x4 bv[4];
 #pragma unroll
@@ -969,19 +689,18 @@ __device__ __forceinline__ void pp_epilogue_lds(const GemmArgs& a, f32x4 (&acc)[
   }
 }
 
-// One phase per slab: per wave, a memory segment (12 fragment reads of slab s,
-// LDS-DMA of slab s+3, vmcnt for slab s+1, lgkmcnt(0)) and a 32-MFMA segment,
-// ping-ponged with the partner wave of the other group.  Because the reading
-// wave drains its own fragment reads before the barrier that ends its memory
-// segment, the ring slot of slab s is free one barrier later: 4 slots carry
-// 3 slabs in flight (96 KiB per CU).
-// RAW: slab s+1 is waited for (vmcnt) in the memory segment of slab s by every
-// wave, before the barrier after which group 0 reads it.  WAR: slot (s+3)&3
-// held slab s-1, whose reads both groups drained before the barrier that
-// precedes group 0's memory segment of slab s.
-template <bool OUT_BF16, int EPI, int ABL = 0, int RING = 4, bool TN = false>
-__global__ __launch_bounds__(kLThreads, 1) void gemm_nt_pp1_kernel(GemmArgs a) {
-  constexpr int D = RING - 1;   // slabs in flight
+// Weight-gradient (TN) kernel: dW = dY^T X with both operands token-major.  One phase per
+// 32-token slab: per wave, a memory segment (12 column-wise fragment reads of slab s,
+// LDS-DMA of slab s+4, vmcnt for slab s+1, lgkmcnt(0)) and a 32-MFMA segment, ping-ponged
+// with the partner wave of the other group.  Because the reading wave drains its own
+// fragment reads before the barrier that ends its memory segment, the ring slot of slab s
+// is free one barrier later: 5 slots carry 4 slabs in flight (128 KiB per CU).
+// RAW: slab s+1 is waited for (vmcnt) in the memory segment of slab s by every wave, before
+// the barrier after which group 0 reads it.  WAR: slot (s+4) % 5 held slab s-1, whose reads
+// both groups drained before the barrier that precedes group 0's memory segment of slab s.
+constexpr int kTnRing = 5;
+__global__ __launch_bounds__(kLThreads, 1) void gemm_tn_kernel(GemmArgs a) {
+  constexpr int RING = kTnRing, D = RING - 1;   // slabs in flight
   __shared__ __attribute__((aligned(16))) char smem[RING * kPSlab];
   const int tid = threadIdx.x;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -1000,15 +719,11 @@ __global__ __launch_bounds__(kLThreads, 1) void gemm_nt_pp1_kernel(GemmArgs a) {
   const int64_t n0 = (int64_t)tn * kL;
 
   const uint32_t lds0 = g_lds_addr(smem);
-  // split-K (kchunk > 0, weight gradients: K = tokens): this block sums k in [kb, kb + kchunk) of
-  // split blockIdx.y and stores raw fp32 partials at C + blockIdx.y * m * ldc (splitk_epi_kernel finishes)
+  // split over tokens (kchunk > 0): this block sums t in [kb, kb + kchunk) of split blockIdx.y and
+  // stores raw fp32 partials at C + blockIdx.y * m * ldc (splitk_epi_kernel finishes)
   const int64_t kb = a.kchunk ? (int64_t)blockIdx.y * a.kchunk : 0;
   const int64_t ke = a.kchunk ? (kb + a.kchunk < a.k ? kb + a.kchunk : a.k) : a.k;
   const int ns = (int)((ke - kb) / 32);
-  // ABL & 64 (diagnostic): every tile streams the panels of tile (0, 0) -> all L2 hits
-  const int64_t dm0 = (ABL & 64) ? 0 : m0, dn0 = (ABL & 64) ? 0 : n0;
-  unsigned long long st0 = 0, st1 = 0, st2 = 0;
-  if (ABL & 32) st0 = __builtin_amdgcn_s_memtime();
 
   f32x4 acc[8][4];
 #pragma unroll
@@ -1017,20 +732,12 @@ __global__ __launch_bounds__(kLThreads, 1) void gemm_nt_pp1_kernel(GemmArgs a) {
     for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
   const int fr = lane & 15, fc = lane >> 4;
-  const int foff = fr * 64 + ((fc ^ ((fr >> 1) & 2)) << 4);
-  const int xoff = grp * 128 * 64 + foff;
-  const int woff = kPPanel + wn * 64 * 64 + foff;
-  // TN fragment addressing (tn_frag): row 8 fc + (fr >> 2), chunk half (fr & 3) >> 1, 8-B half fr & 1
+  // fragment addressing (tn_frag): row 8 fc + (fr >> 2), chunk half (fr & 3) >> 1, 8-B half fr & 1
   const int tn_row = 8 * fc + (fr >> 2);
   const int tn_rowoff = tn_row * 512, tn_s = tn_swz(tn_row), tn_lo = 16 * ((fr & 3) >> 1) + 8 * (fr & 1);
   auto stage = [&](int64_t t0, uint32_t dst) {
-    if (TN) {
-      stage_panel32_tn(a.A, a.lda, dm0, a.m, t0, dst, wave, lane);
-      stage_panel32_tn(a.B, a.ldb, dn0, a.n, t0, dst + kPPanel, wave, lane);
-    } else {
-      stage_panel32(a.A, a.lda, dm0, a.m, t0, dst, wave, lane);
-      stage_panel32(a.B, a.ldb, dn0, a.n, t0, dst + kPPanel, wave, lane);
-    }
+    stage_panel32_tn(a.A, a.lda, m0, a.m, t0, dst, wave, lane);
+    stage_panel32_tn(a.B, a.ldb, n0, a.n, t0, dst + kPPanel, wave, lane);
   };
 
   // prologue: slabs 0..D-1 in flight, slab 0 landed
@@ -1040,53 +747,22 @@ __global__ __launch_bounds__(kLThreads, 1) void gemm_nt_pp1_kernel(GemmArgs a) {
   }
   vmcnt_slabs_after(ns - 1 < D - 1 ? ns - 1 : D - 1);
   __builtin_amdgcn_s_barrier();
-  if (grp == 1 && !(ABL & 4)) __builtin_amdgcn_s_barrier();
+  if (grp == 1) __builtin_amdgcn_s_barrier();
   __builtin_amdgcn_sched_barrier(0);
 
-  if (ABL & 32) st1 = __builtin_amdgcn_s_memtime();
-  unsigned long long t_start = 0;
-  if (ABL & 16) t_start = __builtin_amdgcn_s_memtime();
-  // fp32 + residual epilogue: the residual rows of pass 0 are requested right after the
-  // tile's last LDS-DMA, so their latency hides behind the last D slabs of the K loop
-  // (measured: prefetching here costs 32 VGPRs in the loop -> spills; kept off)
-  constexpr bool PRE = false;
-  constexpr int RP = PRE ? 16 : 0;   // vector-memory ops of that prefetch (younger than every DMA)
-  const bool pre_on = PRE && ns > D;
-  bf16x4 rv0[16];
   int slot = 0, fill = D % RING;
   for (int s = 0; s < ns; ++s) {
     const char* slab = smem + slot * kPSlab;
     // ---- memory segment
     bf16x8 wf[4], xf[8];
-    if (TN) {
 #pragma unroll
-      for (int j = 0; j < 4; ++j) wf[j] = tn_frag(slab + kPPanel, wn * 64 + j * 16, tn_rowoff, tn_s, tn_lo);
+    for (int j = 0; j < 4; ++j) wf[j] = tn_frag(slab + kPPanel, wn * 64 + j * 16, tn_rowoff, tn_s, tn_lo);
 #pragma unroll
-      for (int i = 0; i < 8; ++i) xf[i] = tn_frag(slab, grp * 128 + i * 16, tn_rowoff, tn_s, tn_lo);
-    } else {
-#pragma unroll
-      for (int j = 0; j < 4; ++j) wf[j] = (ABL & 8) ? bf16x8{} : *(const bf16x8*)(slab + woff + j * 1024);
-#pragma unroll
-      for (int i = 0; i < 8; ++i) xf[i] = (ABL & 8) ? bf16x8{} : *(const bf16x8*)(slab + xoff + i * 1024);
-    }
-    if (ABL & 8) {
-#pragma unroll
-      for (int i = 0; i < 8; ++i) asm volatile("" : "+v"(xf[i]));
-#pragma unroll
-      for (int j = 0; j < 4; ++j) asm volatile("" : "+v"(wf[j]));
-    }
-    const int left = (ABL & 1) ? 0 : ns - 1 - s;   // slabs after s
+    for (int i = 0; i < 8; ++i) xf[i] = tn_frag(slab, grp * 128 + i * 16, tn_rowoff, tn_s, tn_lo);
+    const int left = ns - 1 - s;   // slabs after s
     if (left >= D) {
-      const uint32_t nslab = lds0 + fill * kPSlab;
-      stage(kb + (int64_t)(s + D) * 32, nslab);
-      if (PRE && left == D && pre_on) {
-        load_resid_half(a, m0, n0, grp, wn, 0, lane, rv0);
-        vmcnt_slabs_after_plus(D - 1, RP);
-      } else {
-        vmcnt_slabs_after(D - 1);
-      }
-    } else if (PRE && pre_on) {
-      vmcnt_slabs_after_plus(left > 0 ? left - 1 : 0, RP);
+      stage(kb + (int64_t)(s + D) * 32, lds0 + fill * kPSlab);
+      vmcnt_slabs_after(D - 1);
     } else {
       vmcnt_slabs_after(left > 0 ? left - 1 : 0);
     }
@@ -1094,54 +770,24 @@ __global__ __launch_bounds__(kLThreads, 1) void gemm_nt_pp1_kernel(GemmArgs a) {
     fill = fill + 1 == RING ? 0 : fill + 1;
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_sched_barrier(0);
-    if (!(ABL & 4)) __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_s_barrier();
     // ---- matrix segment
     __builtin_amdgcn_sched_barrier(0);
     __builtin_amdgcn_s_setprio(1);
 #pragma unroll
     for (int i = 0; i < 8; ++i)
 #pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        if (ABL & 2) { asm volatile("" :: "v"(wf[j]), "v"(xf[i])); continue; }
-        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[j], xf[i], acc[i][j], 0, 0, 0);
-      }
+      for (int j = 0; j < 4; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[j], xf[i], acc[i][j], 0, 0, 0);
     __builtin_amdgcn_s_setprio(0);
     __builtin_amdgcn_sched_barrier(0);
-    if (!(ABL & 4)) __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_s_barrier();
   }
-  if (ABL & 16) {
-    const unsigned long long t_end = __builtin_amdgcn_s_memtime();
-    if (lane == 0 && blockIdx.x < 64) {
-      a.dbg[(blockIdx.x * 8 + wave) * 2] = t_start;
-      a.dbg[(blockIdx.x * 8 + wave) * 2 + 1] = t_end;
-    }
-  }
-  if (grp == 0 && !(ABL & 4)) __builtin_amdgcn_s_barrier();
-  if (ABL & 32) st2 = __builtin_amdgcn_s_memtime();
-  const bool full = (n0 + kL <= a.n) && (a.ldc % 8 == 0) && (!(EPI & EPI_AUX) || a.ldr % 8 == 0);
-  if (full) {
-    GemmArgs ae = a;
-    if (a.kchunk) ae.C = (float*)a.C + (int64_t)blockIdx.y * a.m * a.ldc;
-    if (pre_on) pp_epilogue_lds<OUT_BF16, EPI, true>(ae, acc, m0, n0, grp, wn, fr, fc, smem + wave * 16384, lane, rv0);
-    else pp_epilogue_lds<OUT_BF16, EPI, false>(ae, acc, m0, n0, grp, wn, fr, fc, smem + wave * 16384, lane, rv0);
-  }
-  else {
-    GemmArgs ae = a;
-    if (a.kchunk) ae.C = (float*)a.C + (int64_t)blockIdx.y * a.m * a.ldc;
-    pp_epilogue<OUT_BF16, EPI>(ae, acc, m0, n0, grp, wn, fr, fc);
-  }
-  if (ABL & 32) {
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    const unsigned long long st3 = __builtin_amdgcn_s_memtime();
-    unsigned xcc;
-    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
-    unsigned hw;
-    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hw));
-    if (lane == 0 && wave == 0) {
-      unsigned long long* d = a.dbg + blockIdx.x * 6;
-      d[0] = st0; d[1] = st1; d[2] = st2; d[3] = st3; d[4] = xcc; d[5] = hw;
-    }
-  }
+  if (grp == 0) __builtin_amdgcn_s_barrier();
+  GemmArgs ae = a;
+  if (a.kchunk) ae.C = (float*)a.C + (int64_t)blockIdx.y * a.m * a.ldc;
+  const bool full = (n0 + kL <= a.n) && (a.ldc % 8 == 0);
+  if (full) pp_epilogue_lds<false, EPI_NONE>(ae, acc, m0, n0, grp, wn, fr, fc, smem + wave * 16384, lane);
+  else pp_epilogue<false, EPI_NONE>(ae, acc, m0, n0, grp, wn, fr, fc);
 }
 
 // ---------------------------------------------------------------------------
@@ -1312,144 +958,88 @@ __global__ __launch_bounds__(kLThreads, 1) void gemm_nt_pr5_kernel(GemmArgs a) {
   GemmArgs ae = a;
   if (a.kchunk) ae.C = (float*)a.C + (int64_t)blockIdx.y * a.m * a.ldc;
   const bool full = (n0 + kL <= a.n) && (a.ldc % 8 == 0) && (!(EPI & EPI_AUX) || a.ldr % 8 == 0);
-  bf16x4 rv0[16];
-  if (full) pp_epilogue_lds<OUT_BF16, EPI, false>(ae, acc, m0, n0, grp, wn, fr, fc, smem + wave * 16384, lane, rv0);
+  if (full) pp_epilogue_lds<OUT_BF16, EPI>(ae, acc, m0, n0, grp, wn, fr, fc, smem + wave * 16384, lane);
   else pp_epilogue<OUT_BF16, EPI>(ae, acc, m0, n0, grp, wn, fr, fc);
 }
 
+static int64_t ceil_div(int64_t a, int64_t b) { return (a + b - 1) / b; }
+
+// Finish a split: out = epilogue(sum_z ws[z]) in a fixed z order.
 template <bool OUT_BF16, int EPI>
-static int launch_gemm_t(const GemmArgs& a0, hipStream_t s) {
+static void launch_splitk_epi(const GemmArgs& a, int splits, hipStream_t s) {
+  const int64_t units = (a.n % 4 == 0) ? a.m * a.n / 4 : a.m * a.n;
+  const int64_t blocks = ceil_div(units, 256) < 4096 ? ceil_div(units, 256) : 4096;
+  hipLaunchKernelGGL((splitk_epi_kernel<OUT_BF16, EPI>), dim3((unsigned)blocks), dim3(256), 0, s, a, splits);
+}
+
+template <bool OUT_BF16, int EPI>
+static int launch_gemm_t(const GemmArgs& a0, size_t ws_bytes, hipStream_t s) {
   GemmArgs a = a0;
-  a.order = g_gemm_order >= 0 ? g_gemm_order : (a.k <= 1024 ? 1 : 0);
+  a.order = auto_tile_order(a.k);
+  const GemmPlan p = plan_for_launch(a.m, a.n, a.k, a.ws, ws_bytes);
   const ProfPair pp = prof_begin(PROF_GEMM, s);
-  // large tiles once there are >= 2 tiles per CU of them; small problems keep 128^2
-  const int64_t tiles_l = ((a.m + kL - 1) / kL) * ((a.n + kL - 1) / kL);
-  int64_t kc_l = 0;
-  // the experimental kernel variants (switch values 2, 7-9, 16+) know only bias / GELU / residual
-  constexpr bool kBasicEpi = (EPI & ~(EPI_BIAS | EPI_GELU | EPI_RESID)) == 0;
-  if (tiles_l >= g_large_min_tiles && g_gemm_variant == 12) {
-    hipLaunchKernelGGL((gemm_nt_pr5_kernel<OUT_BF16, EPI>), dim3((unsigned)tiles_l), dim3(kLThreads), 0, s, a);
-  } else if (tiles_l < g_large_min_tiles && a.m >= g_msplit_min_m && g_gemm_variant == 0 && a.k < g_lsplit_min_k) {
-    // mid-size: the whole-line kernel, K split over ~one block per CU when the caller gave scratch
-    int64_t kc = 0;
-    const int splits = a.ws ? mid_splits(a.m, a.n, a.k, &kc) : 0;
-    if (splits > 1) {
+  const int64_t tiles_l = ceil_div(a.m, kL) * ceil_div(a.n, kL);
+  const int64_t tiles = ceil_div(a.m, kBM) * ceil_div(a.n, kBN);
+  switch (p.path) {
+    case GP_LARGE:
+      // whole-line K-tiles in the 5-slot panel ring (tools/gemm_ab.py: +5-18 % over the 32-deep
+      // slab ring, bit-identical outputs)
+      hipLaunchKernelGGL((gemm_nt_pr5_kernel<OUT_BF16, EPI>), dim3((unsigned)tiles_l), dim3(kLThreads), 0, s, a);
+      break;
+    case GP_LARGE_SPLIT: {
+      // long K, small output: raw fp32 partials per split, then one fixed-order reduction
+      // applying the epilogue
       GemmArgs b = a;
-      b.kchunk = kc;
+      b.kchunk = p.kchunk;
       b.C = a.ws;
       b.ldc = a.n;
       b.bias = nullptr;
       b.R = nullptr;
       b.alpha = 1.0f;
-      hipLaunchKernelGGL((gemm_nt_pr5_kernel<false, EPI_NONE>), dim3((unsigned)tiles_l, (unsigned)splits),
+      hipLaunchKernelGGL((gemm_nt_pr5_kernel<false, EPI_NONE>), dim3((unsigned)tiles_l, (unsigned)p.splits),
                          dim3(kLThreads), 0, s, b);
-      const int64_t units = (a.n % 4 == 0) ? a.m * a.n / 4 : a.m * a.n;
-      const int64_t blocks = (units + 255) / 256 < 4096 ? (units + 255) / 256 : 4096;
-      hipLaunchKernelGGL((splitk_epi_kernel<OUT_BF16, EPI>), dim3((unsigned)blocks), dim3(256), 0, s, a, splits);
-    } else {
-      hipLaunchKernelGGL((gemm_nt_pr5_kernel<OUT_BF16, EPI>), dim3((unsigned)tiles_l), dim3(kLThreads), 0, s, a);
+      launch_splitk_epi<OUT_BF16, EPI>(a, p.splits, s);
+      break;
     }
-  } else if (tiles_l >= g_large_min_tiles && (g_gemm_variant == 0 || !kBasicEpi)) {
-    // round 2: whole-line K-tiles in the 5-slot panel ring (tools/gemm_ab.py: +5-18 % over pp1,
-    // bit-identical outputs)
-    hipLaunchKernelGGL((gemm_nt_pr5_kernel<OUT_BF16, EPI>), dim3((unsigned)tiles_l), dim3(kLThreads), 0, s, a);
-  } else if (!kBasicEpi) {
-    // below the 256^2 threshold: 128^2 kernel (split-K when the caller gave a workspace)
-    const int64_t tiles = ((a.m + kBM - 1) / kBM) * ((a.n + kBN - 1) / kBN);
-    int64_t kc = 0;
-    const int splits = a.ws ? small_splits(a.m, a.n, a.k, &kc) : 0;
-    if (splits > 1) {
+    case GP_SMALL_SPLIT: {
       GemmArgs b = a;
-      b.kchunk = kc;
-      hipLaunchKernelGGL((gemm_nt_kernel<OUT_BF16, EPI, true>), dim3((unsigned)tiles, 1, (unsigned)splits),
+      b.kchunk = p.kchunk;
+      hipLaunchKernelGGL((gemm_nt_kernel<OUT_BF16, EPI, true>), dim3((unsigned)tiles, 1, (unsigned)p.splits),
                          dim3(kGemmThreads), 0, s, b);
-      const int64_t units = (a.n % 4 == 0) ? a.m * a.n / 4 : a.m * a.n;
-      const int64_t blocks = (units + 255) / 256 < 4096 ? (units + 255) / 256 : 4096;
-      hipLaunchKernelGGL((splitk_epi_kernel<OUT_BF16, EPI>), dim3((unsigned)blocks), dim3(256), 0, s, b, splits);
-    } else {
+      launch_splitk_epi<OUT_BF16, EPI>(b, p.splits, s);
+      break;
+    }
+    default:
       hipLaunchKernelGGL((gemm_nt_kernel<OUT_BF16, EPI>), dim3((unsigned)tiles), dim3(kGemmThreads), 0, s, a);
-    }
-  } else if (tiles_l >= 512 && g_gemm_variant == 9) {
-    hipLaunchKernelGGL((gemm_nt_l_kernel<OUT_BF16, EPI>), dim3((unsigned)tiles_l), dim3(kLThreads), 0, s, a);
-  } else if (tiles_l >= 512 && g_gemm_variant == 2) {
-    hipLaunchKernelGGL((gemm_nt_lh_kernel<OUT_BF16, EPI>), dim3((unsigned)tiles_l), dim3(kLThreads), 0, s, a);
-  } else if (tiles_l >= 512 && g_gemm_variant >= 16 && g_gemm_dbg) {
-    GemmArgs b = a;
-    b.dbg = g_gemm_dbg;
-    dim3 G((unsigned)tiles_l), T(kLThreads);
-    switch (g_gemm_variant - 16) {
-      case 0: hipLaunchKernelGGL((gemm_nt_pp1_kernel<OUT_BF16, EPI, 16>), G, T, 0, s, b); break;
-      case 1: hipLaunchKernelGGL((gemm_nt_pp1_kernel<OUT_BF16, EPI, 17>), G, T, 0, s, b); break;
-      case 13: hipLaunchKernelGGL((gemm_nt_pp1_kernel<OUT_BF16, EPI, 29>), G, T, 0, s, b); break;
-      case 15: hipLaunchKernelGGL((gemm_nt_pp1_kernel<OUT_BF16, EPI, 32>), G, T, 0, s, b); break;
-      case 7: hipLaunchKernelGGL((gemm_nt_pp1_kernel<OUT_BF16, EPI, 16, 5>), G, T, 0, s, b); break;
-      case 10: hipLaunchKernelGGL((gemm_nt_pp1_kernel<OUT_BF16, EPI, 16 | 2 | 8, 5>), G, T, 0, s, b); break;
-      default: return DRT_EINVAL;
-    }
-  } else if (tiles_l >= 512 && g_gemm_variant == 7) {
-    hipLaunchKernelGGL((gemm_nt_pp1_kernel<OUT_BF16, EPI>), dim3((unsigned)tiles_l), dim3(kLThreads), 0, s, a);
-  } else if (tiles_l >= 512 && g_gemm_variant == 8) {
-    hipLaunchKernelGGL((gemm_nt_pp1_kernel<OUT_BF16, EPI, 0, 5>), dim3((unsigned)tiles_l), dim3(kLThreads), 0, s, a);
-  } else if (g_gemm_variant == 0 && a.ws && large_splits(a.m, a.n, a.k, g_large_min_tiles, &kc_l) > 1) {
-    // long K, small output (weight gradients): split K over the 256^2 kernel, then one
-    // fixed-order reduction applying the epilogue
-    const int splits = large_splits(a.m, a.n, a.k, g_large_min_tiles, &kc_l);
-    GemmArgs b = a;
-    b.kchunk = kc_l;
-    b.C = a.ws;
-    b.ldc = a.n;
-    b.bias = nullptr;
-    b.R = nullptr;
-    b.alpha = 1.0f;
-    hipLaunchKernelGGL((gemm_nt_pp1_kernel<false, EPI_NONE, 0, 5>), dim3((unsigned)tiles_l, (unsigned)splits),
-                       dim3(kLThreads), 0, s, b);
-    GemmArgs e = a;
-    const int64_t units = (a.n % 4 == 0) ? a.m * a.n / 4 : a.m * a.n;
-    const int64_t blocks = (units + 255) / 256 < 4096 ? (units + 255) / 256 : 4096;
-    hipLaunchKernelGGL((splitk_epi_kernel<OUT_BF16, EPI>), dim3((unsigned)blocks), dim3(256), 0, s, e, splits);
-  } else {
-    const int64_t tiles = ((a.m + kBM - 1) / kBM) * ((a.n + kBN - 1) / kBN);
-    int64_t kc = 0;
-    const int splits = a.ws ? small_splits(a.m, a.n, a.k, &kc) : 0;
-    if (splits > 1) {
-      GemmArgs b = a;
-      b.kchunk = kc;
-      hipLaunchKernelGGL((gemm_nt_kernel<OUT_BF16, EPI, true>), dim3((unsigned)tiles, 1, (unsigned)splits),
-                         dim3(kGemmThreads), 0, s, b);
-      const int64_t units = (a.n % 4 == 0) ? a.m * a.n / 4 : a.m * a.n;
-      const int64_t blocks = (units + 255) / 256 < 4096 ? (units + 255) / 256 : 4096;
-      hipLaunchKernelGGL((splitk_epi_kernel<OUT_BF16, EPI>), dim3((unsigned)blocks), dim3(256), 0, s, b, splits);
-    } else {
-      hipLaunchKernelGGL((gemm_nt_kernel<OUT_BF16, EPI>), dim3((unsigned)tiles), dim3(kGemmThreads), 0, s, a);
-    }
+      break;
   }
   prof_end(pp, s);
   return hip_status(hipGetLastError());
 }
 
-int launch_gemm(const GemmArgs& a, bool out_bf16, int epi, hipStream_t s) {
+int launch_gemm(const GemmArgs& a, bool out_bf16, int epi, size_t ws_bytes, hipStream_t s) {
   if (a.m == 0 || a.n == 0) return DRT_OK;
   if (a.k <= 0 || a.k % kBK != 0) return DRT_EINVAL;
   if (!out_bf16) {
     switch (epi) {
-      case EPI_NONE: return launch_gemm_t<false, EPI_NONE>(a, s);
-      case EPI_BIAS: return launch_gemm_t<false, EPI_BIAS>(a, s);
-      case EPI_BIAS | EPI_RESID: return launch_gemm_t<false, EPI_BIAS | EPI_RESID>(a, s);
-      case EPI_RESID: return launch_gemm_t<false, EPI_RESID>(a, s);
+      case EPI_NONE: return launch_gemm_t<false, EPI_NONE>(a, ws_bytes, s);
+      case EPI_BIAS: return launch_gemm_t<false, EPI_BIAS>(a, ws_bytes, s);
+      case EPI_BIAS | EPI_RESID: return launch_gemm_t<false, EPI_BIAS | EPI_RESID>(a, ws_bytes, s);
+      case EPI_RESID: return launch_gemm_t<false, EPI_RESID>(a, ws_bytes, s);
       default: return DRT_EINVAL;
     }
   }
   switch (epi) {
-    case EPI_NONE: return launch_gemm_t<true, EPI_NONE>(a, s);
-    case EPI_BIAS: return launch_gemm_t<true, EPI_BIAS>(a, s);
-    case EPI_BIAS | EPI_GELU: return launch_gemm_t<true, EPI_BIAS | EPI_GELU>(a, s);
-    case EPI_BIAS | EPI_RESID: return launch_gemm_t<true, EPI_BIAS | EPI_RESID>(a, s);
-    case EPI_RESID: return launch_gemm_t<true, EPI_RESID>(a, s);   // backward dgrad + residual branch
-    case EPI_GELU: return launch_gemm_t<true, EPI_GELU>(a, s);
+    case EPI_NONE: return launch_gemm_t<true, EPI_NONE>(a, ws_bytes, s);
+    case EPI_BIAS: return launch_gemm_t<true, EPI_BIAS>(a, ws_bytes, s);
+    case EPI_BIAS | EPI_GELU: return launch_gemm_t<true, EPI_BIAS | EPI_GELU>(a, ws_bytes, s);
+    case EPI_BIAS | EPI_RESID: return launch_gemm_t<true, EPI_BIAS | EPI_RESID>(a, ws_bytes, s);
+    case EPI_RESID: return launch_gemm_t<true, EPI_RESID>(a, ws_bytes, s);   // backward dgrad + residual branch
+    case EPI_GELU: return launch_gemm_t<true, EPI_GELU>(a, ws_bytes, s);
     // training tower fusions (drt_linear_bf16_ex)
-    case EPI_BIAS | EPI_GELU | EPI_PRE: return launch_gemm_t<true, EPI_BIAS | EPI_GELU | EPI_PRE>(a, s);
-    case EPI_DGELU: return launch_gemm_t<true, EPI_DGELU>(a, s);
-    case EPI_BIAS | EPI_DROP | EPI_RESID: return launch_gemm_t<true, EPI_BIAS | EPI_DROP | EPI_RESID>(a, s);
+    case EPI_BIAS | EPI_GELU | EPI_PRE: return launch_gemm_t<true, EPI_BIAS | EPI_GELU | EPI_PRE>(a, ws_bytes, s);
+    case EPI_DGELU: return launch_gemm_t<true, EPI_DGELU>(a, ws_bytes, s);
+    case EPI_BIAS | EPI_DROP | EPI_RESID: return launch_gemm_t<true, EPI_BIAS | EPI_DROP | EPI_RESID>(a, ws_bytes, s);
     default: return DRT_EINVAL;
   }
 }
@@ -1474,24 +1064,14 @@ extern "C" int drt_gemm_nt_bf16_f32(const void* A, const void* B, float* C, int6
   a.ldb = d;
   a.ldc = ldc;
   a.alpha = 1.0f;
-  return launch_gemm(a, false, EPI_NONE, (hipStream_t)stream);
+  return launch_gemm(a, false, EPI_NONE, 0, (hipStream_t)stream);
 }
 
-// Workspace that lets drt_linear_bf16_ws split K on problems too small to fill the chip
-// (0 when no split is planned for this shape).
+// Workspace that lets drt_linear_bf16_ws / _ln_ / _ex split K on problems too small to fill the
+// chip: exactly the plan's fp32 partials (0 when the plan does not split this shape).
 extern "C" size_t drt_linear_workspace(int64_t M, int64_t N, int64_t K) {
   if (M <= 0 || N <= 0 || K <= 0 || K % 64) return 0;
-  const int64_t tiles_l = ((M + kL - 1) / kL) * ((N + kL - 1) / kL);
-  if (tiles_l >= g_large_min_tiles) return 0;   // the 256^2 path does not split
-  int64_t kc = 0;
-  if (M >= g_msplit_min_m && K < g_lsplit_min_k) {
-    const int ms = mid_splits(M, N, K, &kc);
-    return ms > 1 ? (size_t)ms * (size_t)M * (size_t)N * sizeof(float) : 0;
-  }
-  const int ls = large_splits(M, N, K, g_large_min_tiles, &kc);
-  if (ls > 1) return (size_t)ls * (size_t)M * (size_t)N * sizeof(float);
-  const int splits = small_splits(M, N, K, &kc);
-  return splits > 1 ? (size_t)splits * (size_t)M * (size_t)N * sizeof(float) : 0;
+  return plan_gemm(M, N, K).ws_bytes;
 }
 
 extern "C" int drt_linear_bf16_ws(const void* X, const void* W, const float* bias, const void* residual, void* Y,
@@ -1527,17 +1107,16 @@ extern "C" int drt_linear_bf16_ws(const void* X, const void* W, const float* bia
   a.ldc = N;
   a.ldr = N;
   a.alpha = 1.0f;
-  // split-K only with a large-enough caller workspace (else the unsplit kernel)
-  if (ws && ws_bytes >= drt_linear_workspace(M, N, K) && drt_linear_workspace(M, N, K) > 0) a.ws = (float*)ws;
+  a.ws = (float*)ws;
   const int epi = (bias ? EPI_BIAS : 0) | (gelu ? EPI_GELU : 0) | (residual ? EPI_RESID : 0);
-  return launch_gemm(a, !f32, epi, (hipStream_t)stream);
+  return launch_gemm(a, !f32, epi, ws ? ws_bytes : 0, (hipStream_t)stream);
 }
 
 extern "C" int drt_layernorm_bf16(const void* X, int64_t M, int32_t H, const float* gamma, const float* beta, float eps,
                                   void* out, void* stream);
 
 // LayerNorm(bf16(X W^T + bias + residual)) -> out (BertSelfOutput / BertOutput: dense + residual +
-// LayerNorm).  When the 128^2 kernel's split plan applies (query-sized batches, caller scratch >=
+// LayerNorm).  When the plan is the 128^2 split (query-sized batches, caller scratch >=
 // drt_linear_workspace) the K-split partials are finished by one fused split-K + LayerNorm launch
 // (splitk_ln_kernel); otherwise the linear writes its bf16 pre-LayerNorm sum to `presum` and
 // drt_layernorm_bf16 normalises it.  Either way bit-identical to drt_linear_bf16_ws + drt_layernorm_bf16.
@@ -1549,15 +1128,8 @@ extern "C" int drt_linear_ln_bf16_ws(const void* X, const void* W, const float* 
   if (M == 0) return DRT_OK;
   DRT_REQUIRE(X && W && bias && residual && gamma && beta && presum && out);
   hipStream_t s = (hipStream_t)stream;
-  const int64_t tiles_l = ((M + kL - 1) / kL) * ((N + kL - 1) / kL);
-  const int64_t tiles = ((M + kBM - 1) / kBM) * ((N + kBN - 1) / kBN);
-  int64_t kc = 0;
-  const size_t need = drt_linear_workspace(M, N, K);
-  const bool small_path = tiles_l < g_large_min_tiles && !(M >= g_msplit_min_m && K < g_lsplit_min_k) &&
-                          !(large_splits(M, N, K, g_large_min_tiles, &kc) > 1) && g_gemm_variant == 0;
-  kc = 0;
-  const int splits = (small_path && ws && need > 0 && ws_bytes >= need) ? small_splits(M, N, K, &kc) : 0;
-  if (splits < 2) {
+  const GemmPlan p = plan_for_launch(M, N, K, ws, ws ? ws_bytes : 0);
+  if (p.path != GP_SMALL_SPLIT) {
     const int rc = drt_linear_bf16_ws(X, W, bias, residual, presum, M, N, K, 0, ws, ws_bytes, stream);
     if (rc != DRT_OK) return rc;
     return drt_layernorm_bf16(presum, M, (int32_t)N, gamma, beta, eps, out, stream);
@@ -1575,12 +1147,14 @@ extern "C" int drt_linear_ln_bf16_ws(const void* X, const void* W, const float* 
   b.ldr = N;
   b.alpha = 1.0f;
   b.ws = (float*)ws;
-  b.kchunk = kc;
-  b.order = g_gemm_order >= 0 ? g_gemm_order : (K <= 1024 ? 1 : 0);
+  b.kchunk = p.kchunk;
+  b.order = auto_tile_order(K);
+  const int64_t tiles = ceil_div(M, kBM) * ceil_div(N, kBN);
   const ProfPair pp = prof_begin(PROF_GEMM, s);
-  hipLaunchKernelGGL((gemm_nt_kernel<true, EPI_BIAS | EPI_RESID, true>), dim3((unsigned)tiles, 1, (unsigned)splits),
+  hipLaunchKernelGGL((gemm_nt_kernel<true, EPI_BIAS | EPI_RESID, true>), dim3((unsigned)tiles, 1, (unsigned)p.splits),
                      dim3(kGemmThreads), 0, s, b);
   const dim3 grid((unsigned)((M + 3) / 4));
+  const int splits = p.splits;
   switch (N / 64) {
     case 4: hipLaunchKernelGGL(splitk_ln_kernel<4>, grid, dim3(256), 0, s, (const float*)ws, splits, M, (int)N, 1.0f,
                                bias, (const __bf16*)residual, gamma, beta, eps, (__bf16*)out); break;
@@ -1600,6 +1174,7 @@ extern "C" int drt_linear_ln_bf16_ws(const void* X, const void* W, const float* 
 //   gelu_pre != NULL: Y = (X W^T) * GELU'(gelu_pre)  (the dgrad through GELU; no bias / residual / GELU);
 //   Y_pre != NULL (with GELU): Y_pre = X W^T + b, Y = GELU(Y_pre)  (both bf16);
 //   flags & 4 (DROP): Y = dropout(X W^T + b) + residual with drt_dropout_add_bf16's mask of (seed, site).
+// The split plan is the same as drt_linear_bf16_ws's (plan_gemm), so drt_linear_workspace sizes it.
 extern "C" int drt_linear_bf16_ex(const void* X, const void* W, const float* bias, const void* residual,
                                   const void* gelu_pre, void* Y, void* Y_pre, int64_t M, int64_t N, int64_t K,
                                   int32_t flags, float drop_p, uint64_t seed, uint64_t site, void* ws,
@@ -1630,20 +1205,20 @@ extern "C" int drt_linear_bf16_ex(const void* X, const void* W, const float* bia
   a.drop_p = drop_p;
   a.seed = seed;
   a.site = site;
-  if (ws && ws_bytes >= drt_linear_workspace(M, N, K) && drt_linear_workspace(M, N, K) > 0) a.ws = (float*)ws;
+  a.ws = (float*)ws;
   const int epi = (bias ? EPI_BIAS : 0) | (gelu ? EPI_GELU : 0) | (residual ? EPI_RESID : 0) |
                   (gelu_pre ? EPI_DGELU : 0) | (Y_pre ? EPI_PRE : 0) | (drop ? EPI_DROP : 0);
-  return launch_gemm(a, !f32, epi, (hipStream_t)stream);
+  return launch_gemm(a, !f32, epi, ws ? ws_bytes : 0, (hipStream_t)stream);
 }
 
 // Weight gradient of nn.Linear without transposed operand copies: dW[N][K] fp32 = dY[T][N]^T . X[T][K]
-// (both operands stored token-major, as the backward has them).  The 256^2 ping-pong kernel in
-// TN mode (whole-line slabs, ds_read_b64_tr_b16 fragments), K = T split over ~1 block per CU with
-// fp32 partials in ws reduced in a fixed order (deterministic), like the transposed path.
+// (both operands stored token-major, as the backward has them).  The 256^2 ping-pong TN kernel
+// (whole-line slabs, ds_read_b64_tr_b16 fragments), K = T split over ~1 block per CU with fp32
+// partials in ws reduced in a fixed order (deterministic): the LARGE_SPLIT plan of plan_gemm.
 extern "C" size_t drt_linear_wgrad_workspace(int64_t T, int64_t N, int64_t K) {
   if (T <= 0 || N <= 0 || K <= 0 || T % 32 || N % 8 || K % 8) return 0;
   int64_t kc = 0;
-  const int ls = large_splits(N, K, T, g_large_min_tiles, &kc);
+  const int ls = large_splits(N, K, T, &kc);
   return ls > 1 ? (size_t)ls * (size_t)N * (size_t)K * sizeof(float) : 0;
 }
 
@@ -1663,73 +1238,23 @@ extern "C" int drt_linear_wgrad_bf16(const void* dY, const void* X, float* dW, i
   a.ldb = K;
   a.ldc = K;
   a.alpha = 1.0f;
-  a.order = g_gemm_order >= 0 ? g_gemm_order : (T <= 1024 ? 1 : 0);
-  const int64_t tiles_l = ((N + kL - 1) / kL) * ((K + kL - 1) / kL);
+  a.order = auto_tile_order(T);
+  const int64_t tiles_l = ceil_div(N, kL) * ceil_div(K, kL);
   int64_t kc = 0;
-  const int splits = large_splits(N, K, T, g_large_min_tiles, &kc);
+  const int splits = large_splits(N, K, T, &kc);
+  if (splits > 1) DRT_REQUIRE(ws && ws_bytes >= (size_t)splits * (size_t)N * (size_t)K * sizeof(float));
   const ProfPair pp = prof_begin(PROF_GEMM, s);
   if (splits > 1) {
-    DRT_REQUIRE(ws && ws_bytes >= (size_t)splits * (size_t)N * (size_t)K * sizeof(float));
     GemmArgs b = a;
     b.kchunk = kc;
     b.C = ws;
-    hipLaunchKernelGGL((gemm_nt_pp1_kernel<false, EPI_NONE, 0, 5, true>), dim3((unsigned)tiles_l, (unsigned)splits),
-                       dim3(kLThreads), 0, s, b);
+    hipLaunchKernelGGL(gemm_tn_kernel, dim3((unsigned)tiles_l, (unsigned)splits), dim3(kLThreads), 0, s, b);
     GemmArgs e = a;
     e.ws = (float*)ws;
-    const int64_t units = (K % 4 == 0) ? N * K / 4 : N * K;
-    const int64_t blocks = (units + 255) / 256 < 4096 ? (units + 255) / 256 : 4096;
-    hipLaunchKernelGGL((splitk_epi_kernel<false, EPI_NONE>), dim3((unsigned)blocks), dim3(256), 0, s, e, splits);
+    launch_splitk_epi<false, EPI_NONE>(e, splits, s);
   } else {
-    hipLaunchKernelGGL((gemm_nt_pp1_kernel<false, EPI_NONE, 0, 5, true>), dim3((unsigned)tiles_l), dim3(kLThreads), 0,
-                       s, a);
+    hipLaunchKernelGGL(gemm_tn_kernel, dim3((unsigned)tiles_l), dim3(kLThreads), 0, s, a);
   }
   prof_end(pp, s);
   return hip_status(hipGetLastError());
-}
-
-// Testing / benchmarking switch: 0 = automatic, 1 = 128^2 kernel for every size,
-// 2 = large half-K-ring kernel where the large kernel applies, 3 = ping-pong 256^2 kernel.
-extern "C" int drt_gemm_force_small(int32_t on) {
-  if (on < 0 || on > 31) return DRT_EINVAL;
-  g_gemm_variant = on;
-  return DRT_OK;
-}
-
-// Diagnostic: device buffer for the variant-6 segment stamps (16 blocks x 8 waves x 4 slabs x 4 u64).
-extern "C" int drt_gemm_debug_buffer(void* buf) {
-  g_gemm_dbg = (unsigned long long*)buf;
-  return DRT_OK;
-}
-
-// Benchmark switch: smallest grid (in 256^2 tiles) that takes the 256^2 kernel.
-// Benchmark switch of the split-K planning (see g_lsplit_* / g_ssplit_cap); non-positive = keep.
-extern "C" int drt_gemm_split_config(int64_t large_min_k, int64_t large_k_per_split, int64_t small_cap_bytes) {
-  if (large_min_k > 0) g_lsplit_min_k = large_min_k;
-  if (large_k_per_split > 0) g_lsplit_k_per = large_k_per_split;
-  if (small_cap_bytes > 0) g_ssplit_cap = small_cap_bytes;
-  return DRT_OK;
-}
-
-// Benchmark switch of the mid-size plan (mid_splits): M from which problems below the 256^2
-// threshold take the whole-line kernel (split over ~one block per CU), the fp32 partials cap and
-// the minimum K-tiles per split.  Non-positive arguments keep the current value.
-extern "C" int drt_gemm_mid_config(int64_t min_m, int64_t cap_bytes, int64_t min_ktiles) {
-  if (min_m > 0) g_msplit_min_m = min_m;
-  if (cap_bytes > 0) g_msplit_cap = cap_bytes;
-  if (min_ktiles > 0) g_msplit_min_kt = min_ktiles;
-  return DRT_OK;
-}
-
-extern "C" int drt_gemm_large_min_tiles(int64_t tiles) {
-  if (tiles < 1) return DRT_EINVAL;
-  g_large_min_tiles = tiles;
-  return DRT_OK;
-}
-
-// Benchmark switch: tile order of the ping-pong kernel (0 row-major, 1 grouped-8, 2 column-major per XCD).
-extern "C" int drt_gemm_tile_order(int32_t order) {
-  if (order < -1 || order > 4) return DRT_EINVAL;
-  g_gemm_order = order;
-  return DRT_OK;
 }

@@ -28,7 +28,6 @@
 
 namespace drt {
 
-constexpr int kTileRows = 32;   // corpus rows per MFMA tile (32x32x16)
 constexpr int kScanThreads = 256;  // 4 waves, one per SIMD
 constexpr int kQueriesPerWG = 128;  // 4 waves x 32 query columns
 constexpr int kHitCap = 1024;       // LDS hit list entries per work-group
@@ -53,23 +52,6 @@ struct ScanArgs {
   void* out;          // FILTER: u64 [nq][cap] keys; DENSE: u32 [nq][cap] desc keys
   int64_t cap;
   int64_t exp_hits;   // FILTER: expected hits per query (0: cap / 4); picks the append flavour
-};
-
-template <int D>
-struct ScanCfg {
-  static_assert(D % 64 == 0 && D <= 1024, "d must be a multiple of 64, <= 1024");
-  static constexpr int KS = D / 16;                         // MFMA k-steps
-  static constexpr int TILE_BYTES = kTileRows * D * 2;      // one 32-row tile
-  static constexpr int GLDS_PER_TILE = TILE_BYTES / 1024;   // 1 KiB per wave-instr
-  static constexpr int GLDS_PER_WAVE = GLDS_PER_TILE / 4;
-  static constexpr int NBUF = (3 * TILE_BYTES + 16 * 1024 <= 160 * 1024) ? 3 : 2;
-  static constexpr int PD = NBUF - 1;  // prefetch distance in tiles
-  static constexpr int RING_BYTES = NBUF * TILE_BYTES;
-  static constexpr int HIT_KEY_OFF = RING_BYTES;
-  static constexpr int HIT_Q_OFF = HIT_KEY_OFF + kHitCap * 8;
-  static constexpr int HIT_N_OFF = HIT_Q_OFF + kHitCap * 2;
-  static constexpr int LDS_BYTES = HIT_N_OFF + 16;
-  static_assert(LDS_BYTES <= 160 * 1024, "LDS budget");
 };
 
 // LDS-DMA of 16 B per lane.  Issued through inline asm on purpose: with the
@@ -106,30 +88,6 @@ __device__ __forceinline__ void glds16_nt(const void* gsrc, uint32_t lds_addr) {
 
 __device__ __forceinline__ uint32_t lds_addr_of(const void* p) {
   return (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) char*)p;
-}
-
-// LDS image of one tile: [chunk-group g (128 B of every row)][row 0..31][8 x 16 B]
-// with the 16-B chunk position XOR-swizzled by (row >> 1) & 7 so that the
-// MFMA A-fragment reads (ds_read_b128, 32 rows x same chunk) are
-// bank-conflict free.  One global_load_lds_dwordx4 wave-instruction fills
-// 8 rows x 128 B (coalesced 128-B row segments).
-template <int D>
-__device__ __forceinline__ void issue_tile(const ScanArgs& a, uint32_t buf_lds, int64_t tile, int wave,
-                                           int lane) {
-  using C = ScanCfg<D>;
-  const int rsub = lane >> 3;    // row within the 8-row group
-  const int pos = lane & 7;      // LDS chunk slot
-#pragma unroll
-  for (int j = 0; j < C::GLDS_PER_WAVE; ++j) {
-    const int J = j * 4 + wave;            // wave-instruction index in the tile
-    const int g = J >> 2;                  // chunk group
-    const int row = ((J & 3) << 3) + rsub;  // tile row 0..31
-    int64_t li = tile * kTileRows + row;
-    li = li < a.nrows ? li : a.nrows - 1;  // clamp: tail rows are masked later
-    const int c = pos ^ ((row >> 1) & 7);
-    const __bf16* src = a.P + (a.row0 + li * a.rstride) * a.ldp + g * 64 + c * 8;
-    glds16(src, __builtin_amdgcn_readfirstlane(buf_lds + J * 1024));  // wave-uniform base
-  }
 }
 
 template <int N>
@@ -195,151 +153,6 @@ __device__ __forceinline__ void flush_hits(const ScanArgs& a, int64_t qbase, uin
     const int64_t q = qbase + hq[i];
     const uint32_t g = atomicAdd(a.counts + q * kCntStride, 1u);
     if (g < (uint64_t)a.cap) ((uint64_t*)a.out)[q * a.cap + g] = hk[i];
-  }
-}
-
-template <int D, int MODE, bool NOMMA = false>
-__global__ __launch_bounds__(kScanThreads, 1) void ip_scan_kernel(ScanArgs a) {
-  using C = ScanCfg<D>;
-  __shared__ __attribute__((aligned(16))) char smem[C::LDS_BYTES];
-  uint64_t* hk = (uint64_t*)(smem + C::HIT_KEY_OFF);
-  uint16_t* hq = (uint16_t*)(smem + C::HIT_Q_OFF);
-  uint32_t* hit_n = (uint32_t*)(smem + C::HIT_N_OFF);
-
-  const int tid = threadIdx.x;
-  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int lane = tid & 63;
-  const int r = lane & 31;   // MFMA column (query) / A-row (corpus row)
-  const int h = lane >> 5;   // k-half
-
-  const int64_t qbase = (int64_t)blockIdx.y * kQueriesPerWG;
-  const int q_local = wave * 32 + r;
-  const int64_t q = qbase + q_local;
-  const bool q_ok = q < a.nq;
-
-  const int64_t ntiles = (a.nrows + kTileRows - 1) / kTileRows;
-  const int64_t t0 = blockIdx.x;
-  const int64_t tstep = gridDim.x;
-  const int64_t my_tiles = t0 < ntiles ? (ntiles - 1 - t0) / tstep + 1 : 0;
-  if (my_tiles == 0) return;  // uniform per work-group
-
-  if (MODE == SCAN_FILTER && tid == 0) *hit_n = 0;
-
-  const uint32_t ring = lds_addr_of(smem);
-
-  // Query fragments stay in VGPRs for the whole launch: B[k][col] = Q[col][k].
-  // Loaded before the ring is primed so hipcc's own vmcnt waits for them do
-  // not drain LDS-DMA.  Out-of-range query columns load row 0 and are zeroed.
-  const int64_t qs = q_ok ? q : 0;
-  bf16x8 qf[C::KS];
-#pragma unroll
-  for (int s = 0; s < C::KS; ++s) qf[s] = *(const bf16x8*)(a.Q + qs * a.ldq + s * 16 + h * 8);
-  float tau = __builtin_nanf("");
-  if (MODE == SCAN_FILTER) {
-    const float tv = a.tau[qs];
-    tau = q_ok ? tv : tau;
-  }
-  if (!q_ok) {
-#pragma unroll
-    for (int s = 0; s < C::KS; ++s) qf[s] = (bf16x8){};
-  }
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-
-  // Prologue: PD tiles in flight.
-  issue_tile<D>(a, ring, t0, wave, lane);
-  if (C::PD > 1 && my_tiles > 1) issue_tile<D>(a, ring + C::TILE_BYTES, t0 + tstep, wave, lane);
-
-  // Per-lane swizzled A-fragment offsets inside one chunk group (4 distinct
-  // even chunk ids per group; chunk = 2s + h).
-  const int sw = (r >> 1) & 7;
-  int aoff[4];
-#pragma unroll
-  for (int m = 0; m < 4; ++m) aoff[m] = r * 128 + ((((2 * m) | h) ^ sw) << 4);
-
-  int buf = 0;                    // ring slot of tile `it`
-  int nbuf2 = C::PD;               // ring slot of tile `it + PD` (== slot of it - 1)
-  for (int64_t it = 0; it < my_tiles; ++it) {
-    const int64_t tile = t0 + it * tstep;
-    // Tile `it` landed (this wave's share); with PD = 2 tile it+1 may stay
-    // in flight.  Only LDS-DMA is outstanding here in FILTER mode; DENSE
-    // stores are younger and only make the wait stricter.
-    if (C::PD > 1 && it + 1 < my_tiles) wait_vmcnt<C::GLDS_PER_WAVE>();
-    else wait_vmcnt<0>();
-    lds_barrier();  // every wave's share landed; tile it-1 fully consumed
-
-    if (MODE == SCAN_FILTER) {
-      const uint32_t n = *hit_n;
-      if (n >= (uint32_t)(kHitCap / 2)) {
-        flush_hits(a, qbase, n, hk, hq);
-        lds_barrier();
-        if (tid == 0) *hit_n = 0;
-        lds_barrier();
-      }
-    }
-
-    if (it + C::PD < my_tiles)
-      issue_tile<D>(a, ring + nbuf2 * C::TILE_BYTES, tile + C::PD * tstep, wave, lane);
-
-    const char* tb = smem + buf * C::TILE_BYTES;
-    f32x16 acc;
-#pragma unroll
-    for (int i = 0; i < 16; ++i) acc[i] = 0.0f;
-    if (NOMMA) {
-      // ablation (memory-pipeline ceiling): touch the tile, no MFMA, no hits
-      const bf16x8 af = *(const bf16x8*)(tb + aoff[0]);
-      acc[0] = -__builtin_inff() + 0.0f * (float)af[0];
-    } else {
-#pragma unroll
-      for (int s = 0; s < C::KS; ++s) {
-        const bf16x8 af = *(const bf16x8*)(tb + (s >> 2) * (kTileRows * 128) + aoff[s & 3]);
-        acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af, qf[s], acc, 0, 0, 0);
-      }
-    }
-
-    // acc[i]: query column r, corpus row (i&3) + 8*(i>>2) + 4*h of the tile.
-    const int64_t rowbase = tile * kTileRows + 4 * h;
-    if (MODE == SCAN_FILTER) {
-      float mx = acc[0];
-#pragma unroll
-      for (int i = 1; i < 16; ++i) mx = fmaxf(mx, acc[i]);
-      if (__ballot(mx >= tau) != 0ull) {
-#pragma unroll
-        for (int i = 0; i < 16; ++i) {
-          const int64_t row = rowbase + (i & 3) + 8 * (i >> 2);
-          if (acc[i] >= tau && row < a.nrows) {
-            const uint64_t key = ((uint64_t)desc_key(acc[i]) << 32) | (uint64_t)(uint32_t)row;
-            push_hit(a, q_local, q, key, hit_n, hk, hq);
-          }
-        }
-      }
-    } else {
-      if (q_ok) {
-        uint32_t* o = (uint32_t*)a.out + q * a.cap;
-#pragma unroll
-        for (int m = 0; m < 4; ++m) {
-          const int64_t row = rowbase + 8 * m;
-          u32x4 v;
-          v[0] = desc_key(acc[4 * m + 0]);
-          v[1] = desc_key(acc[4 * m + 1]);
-          v[2] = desc_key(acc[4 * m + 2]);
-          v[3] = desc_key(acc[4 * m + 3]);
-          if (row + 3 < a.nrows) {
-            *(u32x4*)(o + row) = v;
-          } else {
-#pragma unroll
-            for (int j = 0; j < 4; ++j)
-              if (row + j < a.nrows) o[row + j] = v[j];
-          }
-        }
-      }
-    }
-    buf = (buf + 1 == C::NBUF) ? 0 : buf + 1;
-    nbuf2 = (nbuf2 + 1 == C::NBUF) ? 0 : nbuf2 + 1;
-  }
-
-  if (MODE == SCAN_FILTER) {
-    lds_barrier();
-    flush_hits(a, qbase, *hit_n, hk, hq);
   }
 }
 
@@ -412,14 +225,7 @@ __device__ __forceinline__ void wait_tiles_younger(int younger) {
   }
 }
 
-// ABL (benchmark ablations, FILTER only): 0 production, 1 no MFMA and no filter,
-// 2 MFMA on register operands (no LDS fragment reads), 3 no filter, 4 LDS fragment reads
-// only (no MFMA, no filter), 5 MFMA on register operands, no filter.
-// OPT (A/B switches of the production loop): bit 0 = no deferred epilogue (each tile's filter
-// right after its own MFMAs), bit 1 = non-temporal corpus loads, bit 2 = s_setprio 1 for
-// waves NW/2.. (the second-dispatched half of each SIMD pair).
-enum { SOPT_NOPIPE = 1, SOPT_NT = 2, SOPT_PRIO = 4 };
-template <int D, int MODE, int ABL = 0, int NW = 4, bool AGG = true, int OPT = 0>
+template <int D, int MODE, int NW = 8, bool AGG = true>
 __global__ __launch_bounds__(NW * 64, 1) void ip_scan16_kernel(ScanArgs a) {
   using C = Scan16Cfg<D, NW>;
   constexpr int QB = 128 / (NW * 16);   // 16-query column blocks per wave
@@ -483,8 +289,7 @@ __global__ __launch_bounds__(NW * 64, 1) void ip_scan16_kernel(ScanArgs a) {
   // prologue: PD tiles in flight
 #pragma unroll
   for (int p = 0; p < C::PD; ++p)
-    if (p < my_tiles) issue_tile16<D, NW, (OPT & SOPT_NT) != 0>(a, ring + p * C::TILE_BYTES, t0 + p * tstep, wave, lane);
-  if ((OPT & SOPT_PRIO) && wave >= NW / 2) __builtin_amdgcn_s_setprio(1);
+    if (p < my_tiles) issue_tile16<D, NW>(a, ring + p * C::TILE_BYTES, t0 + p * tstep, wave, lane);
 
   // A-fragment address: chunk 4s + kq of row r, group s >> 1, position (4(s&1) + kq) ^ sw
   const int sw = (r >> 1) & 7;
@@ -499,36 +304,15 @@ __global__ __launch_bounds__(NW * 64, 1) void ip_scan16_kernel(ScanArgs a) {
     const char* tb = smem + buf_ * C::TILE_BYTES;
 #pragma unroll
     for (int b = 0; b < QB; ++b) acc[b] = (f32x4){0.f, 0.f, 0.f, 0.f};
-    if (ABL == 1) {
-      const bf16x8 af = *(const bf16x8*)(tb + aoff[0]);
-      asm volatile("" ::"v"(af));
-    } else if (ABL == 4) {
 #pragma unroll
-      for (int s = 0; s < C::KS; ++s) {
-        const bf16x8 af = *(const bf16x8*)(tb + (s >> 1) * (kT16 * 128) + aoff[s & 1]);
-        asm volatile("" ::"v"(af));
-      }
-    } else if (ABL == 2 || ABL == 5) {
-      const bf16x8 af = *(const bf16x8*)(tb + aoff[0]);
+    for (int s = 0; s < C::KS; ++s) {
+      const bf16x8 af = *(const bf16x8*)(tb + (s >> 1) * (kT16 * 128) + aoff[s & 1]);
 #pragma unroll
-      for (int s = 0; s < C::KS; ++s)
-#pragma unroll
-        for (int b = 0; b < QB; ++b) acc[b] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af, qf[s][b], acc[b], 0, 0, 0);
-    } else {
-#pragma unroll
-      for (int s = 0; s < C::KS; ++s) {
-        const bf16x8 af = *(const bf16x8*)(tb + (s >> 1) * (kT16 * 128) + aoff[s & 1]);
-#pragma unroll
-        for (int b = 0; b < QB; ++b) acc[b] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af, qf[s][b], acc[b], 0, 0, 0);
-      }
+      for (int b = 0; b < QB; ++b) acc[b] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af, qf[s][b], acc[b], 0, 0, 0);
     }
-
   };
   auto epilogue = [&](const f32x4 (&acc)[QB], int64_t rowbase) {
-    if (ABL == 1 || ABL == 3 || ABL == 4 || ABL == 5) {
-#pragma unroll
-      for (int b = 0; b < QB; ++b) asm volatile("" ::"v"(acc[b]));
-    } else if (MODE == SCAN_FILTER) {
+    if (MODE == SCAN_FILTER) {
       float mx = -__builtin_inff();
 #pragma unroll
       for (int b = 0; b < QB; ++b)
@@ -621,13 +405,10 @@ __global__ __launch_bounds__(NW * 64, 1) void ip_scan16_kernel(ScanArgs a) {
       }
     }
     if (it + C::PD < my_tiles)
-      issue_tile16<D, NW, (OPT & SOPT_NT) != 0>(a, ring + nslot * C::TILE_BYTES, tile + C::PD * tstep, wave, lane);
+      issue_tile16<D, NW>(a, ring + nslot * C::TILE_BYTES, tile + C::PD * tstep, wave, lane);
 
     const int64_t rowbase = tile * kT16 + 4 * kq;
-    if (OPT & SOPT_NOPIPE) {
-      mma_tile(accA, buf);
-      epilogue(accA, rowbase);
-    } else if ((it & 1) == 0) {
+    if ((it & 1) == 0) {
       mma_tile(accA, buf);
       if (it > 0) epilogue(accB, rbB);
       rbA = rowbase;
@@ -640,10 +421,8 @@ __global__ __launch_bounds__(NW * 64, 1) void ip_scan16_kernel(ScanArgs a) {
     nslot = (nslot + 1 == C::NBUF) ? 0 : nslot + 1;
   }
 
-  if (!(OPT & SOPT_NOPIPE)) {
-    if (my_tiles & 1) epilogue(accA, rbA);
-    else epilogue(accB, rbB);
-  }
+  if (my_tiles & 1) epilogue(accA, rbA);
+  else epilogue(accB, rbB);
 
   if (MODE == SCAN_FILTER) {
     lds_barrier();
@@ -1699,109 +1478,31 @@ __global__ __launch_bounds__(kTreeThreads) void merge_packed_tree_kernel(const u
   if (status && tid == 0) status[q] = (bad || (L[k - 1] == ~0ull && n_global >= (int64_t)k)) ? 1 : 0;
 }
 
-// Rank merge of packed per-shard lists (the N > 1 step's merge for nparts * k * 8 B <= 64 KiB):
-// one work-group per (query, part) instead of one per query (128 work-groups on 256 CUs in the
-// bench), every part of the query staged in LDS, and each key of the block's own part placed
-// directly at its merged rank = own index + #keys below it in every other part (binary
-// searches in LDS; keys are unique: (score key << 32) | global id).  Same output and status as
-// merge_packed_tree_kernel.  Padding keys (~0) are skipped; part 0's block writes the pad tail
-// (merged count T < k) and the status.
-constexpr int kRankThreads = 1024;
-constexpr int kRankMaxParts = 8;
-constexpr int kRankLds = 64 * 1024;
-__global__ __launch_bounds__(kRankThreads) void merge_packed_rank_kernel(const uint64_t* parts, int64_t nq,
-                                                                         int nparts, int k, int64_t n_global,
-                                                                         float* out_s, int64_t* out_i,
-                                                                         int32_t* status) {
-  extern __shared__ __attribute__((aligned(16))) uint64_t P[];   // [nparts][k]
-  __shared__ int cnt[kRankMaxParts];
-  __shared__ int bad;
-  const int tid = threadIdx.x;
-  const int64_t q = blockIdx.x / nparts;
-  const int me = (int)(blockIdx.x % nparts);
-  const int64_t ps = (int64_t)(k + 1);
-  if (tid == 0) bad = 0;
-  {
-    // all loads of the fill in flight at once (clamped addresses, then select; nparts * k <= 8192)
-    constexpr int E = kRankLds / 8 / kRankThreads;
-    uint64_t tmp[E];
-#pragma unroll
-    for (int t = 0; t < E; ++t) {
-      const int e = tid + t * kRankThreads;
-      const bool ok = e < nparts * k;
-      const int l = ok ? e / k : 0, i = ok ? e - l * k : 0;
-      tmp[t] = parts[((int64_t)l * nq + q) * ps + i];
-    }
-#pragma unroll
-    for (int t = 0; t < E; ++t) {
-      const int e = tid + t * kRankThreads;
-      if (e < nparts * k) P[e] = tmp[t];
-    }
-  }
-  __syncthreads();
-  // valid (non-pad) count of every part: first ~0 key (lists are sorted ascending)
-  if (tid < nparts) {
-    const uint64_t* L = P + tid * k;
-    int lo = 0, hi = k;
-    while (lo < hi) {
-      const int mid = (lo + hi) >> 1;
-      if (L[mid] != ~0ull) lo = mid + 1;
-      else hi = mid;
-    }
-    cnt[tid] = lo;
-    if (parts[((int64_t)tid * nq + q) * ps + k] & 1ull) atomicOr(&bad, 1);
-  }
-  __syncthreads();
-  int c[kRankMaxParts];
-#pragma unroll
-  for (int l = 0; l < kRankMaxParts; ++l) c[l] = (l < nparts && l != me) ? cnt[l] : 0;
-  const uint64_t* mine = P + me * k;
-  for (int i = tid; i < cnt[me]; i += kRankThreads) {
-    const uint64_t x = mine[i];
-    // branch-free lower bounds in all other parts at once: the kRankMaxParts searches
-    // advance in lock step, so their LDS reads overlap instead of forming one long chain
-    int base[kRankMaxParts], len[kRankMaxParts];
-#pragma unroll
-    for (int l = 0; l < kRankMaxParts; ++l) {
-      base[l] = 0;
-      len[l] = c[l];
-    }
-    for (int step = 0; step < 12; ++step) {
-#pragma unroll
-      for (int l = 0; l < kRankMaxParts; ++l) {
-        if (len[l] > 1) {
-          const int half = len[l] >> 1;
-          base[l] = P[l * k + base[l] + half - 1] < x ? base[l] + half : base[l];
-          len[l] -= half;
-        }
-      }
-    }
-    int rank = i;
-#pragma unroll
-    for (int l = 0; l < kRankMaxParts; ++l)
-      rank += base[l] + ((len[l] == 1 && P[l * k + base[l]] < x) ? 1 : 0);
-    if (rank < k) {
-      out_s[q * k + rank] = desc_key_to_score((uint32_t)(x >> 32));
-      out_i[q * k + rank] = (int64_t)(x & 0xFFFFFFFFull);
-    }
-  }
-  if (me == 0) {
-    int tot = 0;
-    for (int l = 0; l < nparts; ++l) tot += cnt[l];
-    for (int i = tot + tid; i < k; i += kRankThreads) {
-      out_s[q * k + i] = kPadScore;
-      out_i[q * k + i] = -1;
-    }
-    if (status && tid == 0) status[q] = (bad || (tot < k && n_global >= (int64_t)k)) ? 1 : 0;
-  }
-}
-
-// Count merge (round 2, the default where nparts <= 8 and nparts * k <= 8192): entry k of every
-// packed list carries its valid count in bits 32-63, so ONE work-group per query loads only the
-// valid keys of all parts (in the global-threshold regime ~1.3 k / world per part, not k) into
+// Count merge (round 2, the default where 2 <= nparts <= 8 and nparts * k <= 8192): entry k of
+// every packed list carries its valid count in bits 32-63, so ONE work-group per query loads only
+// the valid keys of all parts (in the global-threshold regime ~1.3 k / world per part, not k) into
 // LDS, then places every key at rank = its index in its part + its lower bounds in the other
-// parts (branch-free searches advancing in lock step, as in the rank merge).  The rank merge
-// loaded all nparts * k keys of a query in each of its nparts work-groups.
+// parts (branch-free searches advancing in lock step, so their LDS reads overlap).  The round-2
+// rank merge (one work-group per (query, part), all nparts * k keys loaded by each) measured
+// 13.4 vs 21.7 us at 128 queries and 57 vs 278 us at 2048 (profiles/r02f_merge_bench.log).
+// The count word is checked against the data: the key before it must be real and the key at it
+// a pad (~0); a list whose count disagrees (e.g. written by a producer that leaves entry k = flags
+// only) is measured instead by a binary search for its first pad key (lists are sorted ascending).
+__device__ __forceinline__ int packed_valid_count(const uint64_t* L, int k) {
+  const uint64_t w = L[k];
+  int c = (int)(w >> 32);
+  c = c < k ? c : k;
+  const bool ok_lo = c == 0 || L[c - 1] != ~0ull;
+  const bool ok_hi = c == k || L[c] == ~0ull;
+  if (ok_lo && ok_hi) return c;
+  int lo = 0, hi = k;
+  while (lo < hi) {
+    const int mid = (lo + hi) >> 1;
+    if (L[mid] != ~0ull) lo = mid + 1;
+    else hi = mid;
+  }
+  return lo;
+}
 constexpr int kCntThreads = 1024;
 constexpr int kCntMaxParts = 8;
 constexpr int kCntMaxKeys = 8192;
@@ -1817,10 +1518,9 @@ __global__ __launch_bounds__(kCntThreads) void merge_packed_count_kernel(const u
   if (tid < kCntMaxParts) {
     int c = 0, f = 0;
     if (tid < nparts) {
-      const uint64_t w = parts[((int64_t)tid * nq + q) * ps + k];
-      c = (int)(w >> 32);
-      c = c < k ? c : k;
-      f = (int)(w & 1ull);
+      const uint64_t* L = parts + ((int64_t)tid * nq + q) * ps;
+      c = packed_valid_count(L, k);
+      f = (int)(L[k] & 1ull);
     }
     cnt[tid] = c;
     flg[tid] = f;
@@ -1892,8 +1592,6 @@ __global__ __launch_bounds__(kCntThreads) void merge_packed_count_kernel(const u
     status[q] = (bad || (tot < k && n_global >= (int64_t)k)) ? 1 : 0;
   }
 }
-
-static int g_merge_variant = 0;   // 0 auto, 1 tree, 2 rank, 3 count (tests / benchmarks)
 
 // Merge of packed per-shard lists [nparts][nq][k + 1] (sorted u64 keys, entry k =
 // flags) into (score, id) [nq][k]; status[q] = 1 unless exact: the k-th merged
@@ -2182,81 +1880,27 @@ static int scan_grid_x(int64_t ntiles) {
   return (int)std::max<int64_t>(g, 1);
 }
 
-static int g_scan_variant = 0;  // testing/benchmark switch (drt_scan_variant)
-
 template <int D>
 static int launch_scan_d(const ScanArgs& a, int mode, hipStream_t s) {
   if (a.nq == 0 || a.nrows == 0) return DRT_OK;
-  const dim3 block(kScanThreads);
   const unsigned gy = (unsigned)((a.nq + kQueriesPerWG - 1) / kQueriesPerWG);
-  if (g_scan_variant == 0 || g_scan_variant >= 3) {
-    const int64_t ntiles = (a.nrows + kT16 - 1) / kT16;
-    dim3 grid(scan_grid_x(ntiles), gy);
-    if (mode == SCAN_FILTER && D == 768 && g_scan_variant == 3)
-      hipLaunchKernelGGL((ip_scan16_kernel<D, SCAN_FILTER, 1>), grid, block, 0, s, a);
-    else if (mode == SCAN_FILTER && D == 768 && g_scan_variant == 4)
-      hipLaunchKernelGGL((ip_scan16_kernel<D, SCAN_FILTER, 2>), grid, block, 0, s, a);
-    else if (mode == SCAN_FILTER && D == 768 && g_scan_variant == 5)
-      hipLaunchKernelGGL((ip_scan16_kernel<D, SCAN_FILTER, 3>), grid, block, 0, s, a);
-    else if (mode == SCAN_FILTER && g_scan_variant == 6)
-      hipLaunchKernelGGL((ip_scan16_kernel<D, SCAN_FILTER, 0, 4>), grid, block, 0, s, a);
-    else if (mode == SCAN_DENSE && g_scan_variant == 6)
-      hipLaunchKernelGGL((ip_scan16_kernel<D, SCAN_DENSE, 0, 4>), grid, block, 0, s, a);
-    else if (mode == SCAN_FILTER && D == 768 && g_scan_variant == 8)
-      hipLaunchKernelGGL((ip_scan16_kernel<D, SCAN_FILTER, 4, 8>), grid, dim3(512), 0, s, a);
-    else if (mode == SCAN_FILTER && D == 768 && g_scan_variant == 9)
-      hipLaunchKernelGGL((ip_scan16_kernel<D, SCAN_FILTER, 5, 8>), grid, dim3(512), 0, s, a);
-    else if (mode == SCAN_FILTER && D == 768 && g_scan_variant == 10)
-      hipLaunchKernelGGL((ip_scan16_kernel<D, SCAN_FILTER, 3, 8>), grid, dim3(512), 0, s, a);
-    else if (mode == SCAN_FILTER && D == 768 && g_scan_variant == 11)
-      hipLaunchKernelGGL((ip_scan16_kernel<D, SCAN_FILTER, 1, 8>), grid, dim3(512), 0, s, a);
-    else if (mode == SCAN_FILTER && g_scan_variant >= 12 && g_scan_variant <= 19) {
-      // production kernel with the OPT switches (variant 12 + OPT bits 0..2), sparse append
-      switch (g_scan_variant - 11) {
-        case 1: hipLaunchKernelGGL((ip_scan16_kernel<D, SCAN_FILTER, 0, 8, false, 1>), grid, dim3(512), 0, s, a); break;
-        case 2: hipLaunchKernelGGL((ip_scan16_kernel<D, SCAN_FILTER, 0, 8, false, 2>), grid, dim3(512), 0, s, a); break;
-        case 3: hipLaunchKernelGGL((ip_scan16_kernel<D, SCAN_FILTER, 0, 8, false, 3>), grid, dim3(512), 0, s, a); break;
-        case 4: hipLaunchKernelGGL((ip_scan16_kernel<D, SCAN_FILTER, 0, 8, false, 4>), grid, dim3(512), 0, s, a); break;
-        case 5: hipLaunchKernelGGL((ip_scan16_kernel<D, SCAN_FILTER, 0, 8, false, 5>), grid, dim3(512), 0, s, a); break;
-        case 6: hipLaunchKernelGGL((ip_scan16_kernel<D, SCAN_FILTER, 0, 8, false, 6>), grid, dim3(512), 0, s, a); break;
-        case 7: hipLaunchKernelGGL((ip_scan16_kernel<D, SCAN_FILTER, 0, 8, false, 7>), grid, dim3(512), 0, s, a); break;
-        default: hipLaunchKernelGGL((ip_scan16_kernel<D, SCAN_FILTER, 0, 8, false, 0>), grid, dim3(512), 0, s, a); break;
-      }
-    }
-    else if (mode == SCAN_FILTER && g_scan_variant >= 20 && g_scan_variant <= 22) {
-      // rolled fragment reads (ip_scan16r_kernel): 20 sparse append, 21 wave-aggregated append and
-      // flush, 22 sparse append + aggregated flush (one global atomic per (work-group, query))
-      if (g_scan_variant == 20) hipLaunchKernelGGL((ip_scan16r_kernel<D, false>), grid, dim3(512), 0, s, a);
-      else if (g_scan_variant == 21) hipLaunchKernelGGL((ip_scan16r_kernel<D, true>), grid, dim3(512), 0, s, a);
-      else hipLaunchKernelGGL((ip_scan16r_kernel<D, false, true>), grid, dim3(512), 0, s, a);
-    }
-    else if (mode == SCAN_FILTER && g_scan_variant == 7)
-      hipLaunchKernelGGL((ip_scan16_kernel<D, SCAN_FILTER, 0, 8, false>), grid, dim3(512), 0, s, a);
-    else if (mode == SCAN_FILTER) {
-      // production: 8 waves (2 per SIMD), 16 queries each.  Hit append: one LDS
-      // atomic per hit when hits are rare, one per wave-tile (popcount + wave scan)
-      // when they are dense.  Expected hits per 16x16 wave-tile = 256 * (cap/4) / n;
-      // measured crossover (profiles/r01_*): dense below ~3M rows at cap 16384.
-      const double eh = a.exp_hits > 0 ? (double)a.exp_hits : (double)a.cap / 4.0;
-      const bool dense_hits = eh * 256.0 / (double)a.nrows >= 0.35;
-      // ip_scan16r_kernel: fragment reads of the next tile rolled into this tile's MFMAs, non-temporal
-      // corpus loads, s_setprio 1 for waves 4-7 (r02 A/B, tools/scan_ab.py, profiles/r02e_scan_roll.log:
-      // 2.59-2.62 vs 2.93 ms per launch for the round-1 loop with the same options, ids identical)
-      // sparse flavour: per-hit LDS append, aggregated flush (one global atomic per (work-group,
-      // query); r02 A/B, profiles/r02g_scan_flush.log: -3 % per launch vs the per-hit flush)
-      if (dense_hits) hipLaunchKernelGGL((ip_scan16r_kernel<D, true>), grid, dim3(512), 0, s, a);
-      else hipLaunchKernelGGL((ip_scan16r_kernel<D, false, true>), grid, dim3(512), 0, s, a);
-    }
-    else
-      hipLaunchKernelGGL((ip_scan16_kernel<D, SCAN_DENSE, 0, 8>), grid, dim3(512), 0, s, a);
-    return hip_status(hipGetLastError());
+  const int64_t ntiles = (a.nrows + kT16 - 1) / kT16;
+  const dim3 grid(scan_grid_x(ntiles), gy);
+  if (mode == SCAN_FILTER) {
+    // 8 waves (2 per SIMD), 16 queries each; fragment reads of the next tile rolled into this
+    // tile's MFMAs, non-temporal corpus loads, s_setprio 1 for waves 4-7 (r02 A/B, tools/scan_ab.py,
+    // profiles/r02e_scan_roll.log: 2.59-2.62 vs 2.93 ms per launch for the round-1 loop, ids identical).
+    // Hit append: one LDS atomic per hit when hits are rare (+ aggregated flush, one global atomic per
+    // (work-group, query): profiles/r02g_scan_flush.log, -3 % per launch), one per wave-tile (popcount +
+    // wave scan) when they are dense.  Expected hits per 16x16 wave-tile = 256 * (cap/4) / n; measured
+    // crossover (profiles/r01_*): dense below ~3M rows at cap 16384.
+    const double eh = a.exp_hits > 0 ? (double)a.exp_hits : (double)a.cap / 4.0;
+    const bool dense_hits = eh * 256.0 / (double)a.nrows >= 0.35;
+    if (dense_hits) hipLaunchKernelGGL((ip_scan16r_kernel<D, true>), grid, dim3(512), 0, s, a);
+    else hipLaunchKernelGGL((ip_scan16r_kernel<D, false, true>), grid, dim3(512), 0, s, a);
+  } else {
+    hipLaunchKernelGGL((ip_scan16_kernel<D, SCAN_DENSE>), grid, dim3(512), 0, s, a);
   }
-  const int64_t ntiles = (a.nrows + kTileRows - 1) / kTileRows;
-  dim3 grid(scan_grid_x(ntiles), gy);
-  if (mode == SCAN_FILTER && g_scan_variant == 1 && D == 768)
-    hipLaunchKernelGGL((ip_scan_kernel<D, SCAN_FILTER, true>), grid, block, 0, s, a);
-  else if (mode == SCAN_FILTER) hipLaunchKernelGGL((ip_scan_kernel<D, SCAN_FILTER>), grid, block, 0, s, a);
-  else hipLaunchKernelGGL((ip_scan_kernel<D, SCAN_DENSE>), grid, block, 0, s, a);
   return hip_status(hipGetLastError());
 }
 
@@ -2321,22 +1965,8 @@ using namespace drt;
 
 extern "C" {
 
-const char* drt_version(void) { return "drt-mi355x 0.1 (gfx950)"; }
-
-// Testing/benchmark switch: 0 = production (16-row tiles, 6-slot ring, 8 waves),
-// 6 = the same with 4 waves,
-// 1 = 32-row FILTER scan without MFMA (memory-pipeline ceiling; results are
-// meaningless), 2 = previous 32-row / 3-slot kernel; 3/4/5 = 16-row kernel
-// ablations (no MFMA / no LDS fragment reads / no filter; d = 768 only); 8-11 = 8-wave
-// ablations (LDS fragment reads only / MFMA on register operands without filter / no filter /
-// no MFMA and no filter); 12-19 = the production filter scan (sparse append) with OPT bits
-// v - 12: 1 no deferred epilogue, 2 non-temporal corpus loads, 4 s_setprio for waves 4-7 (the
-// round-1 production loop is 18); 20 / 21 = the production rolled-read kernel, sparse / aggregated
-// append (0 picks between them by the expected hit density).
-int drt_scan_variant(int32_t v) {
-  if (v < 0 || v > 22) return DRT_EINVAL;
-  g_scan_variant = v;
-  return DRT_OK;
+const char* drt_version(void) {
+  return "drt-mi355x 0.3 (gfx950; packed top-k lists: entry k = valid count << 32 | flags)";
 }
 
 size_t drt_ip_topk_workspace(int64_t nq, int64_t n, int32_t d, int32_t k) {
@@ -2743,13 +2373,6 @@ int drt_ip_topk_dist_filter_lists_at(const void* Q, int64_t nq, const void* P, i
   return launch_select(sa, SEL_KEYS64, SEL_TOPK, s);
 }
 
-// Test / benchmark switch of drt_topk_merge_packed: 0 automatic, 1 tree merge, 2 rank merge (where it fits).
-int drt_topk_merge_packed_variant(int32_t v) {
-  if (v < 0 || v > 3) return DRT_EINVAL;
-  g_merge_variant = v;
-  return DRT_OK;
-}
-
 int drt_topk_merge_packed(const uint64_t* parts, int64_t nq, int32_t nparts, int32_t k, int64_t n_global,
                           float* out_scores, int64_t* out_ids, int32_t* status, void* stream) {
   DRT_REQUIRE(nq >= 0 && nparts >= 1 && nparts <= 4096 && k >= 1 && k <= kSelMaxK && n_global >= 0);
@@ -2763,28 +2386,18 @@ int drt_topk_merge_packed(const uint64_t* parts, int64_t nq, int32_t nparts, int
   while (kp < k) kp <<= 1;
   const size_t lds = (size_t)p2 * kp * 8;
   int rc = DRT_OK;
-  const size_t rank_lds = (size_t)nparts * k * 8;
-  const bool rank_ok = nparts <= kRankMaxParts && rank_lds <= (size_t)kRankLds;
+  const size_t cnt_lds = (size_t)nparts * k * 8;
   const bool count_ok = nparts <= kCntMaxParts && (int64_t)nparts * k <= kCntMaxKeys;
   // one part (one GPU): the plain per-query kernel (tools/merge_bench.py: 8 vs 23 us at 2048 queries)
-  if (count_ok && ((g_merge_variant == 0 && nparts > 1) || g_merge_variant == 3)) {
+  if (count_ok && nparts > 1) {
     static bool attr_set = false;
     if (!attr_set) {
       DRT_CHECK_HIP(hipFuncSetAttribute((const void*)merge_packed_count_kernel,
                                         hipFuncAttributeMaxDynamicSharedMemorySize, kCntMaxKeys * 8));
       attr_set = true;
     }
-    hipLaunchKernelGGL(merge_packed_count_kernel, dim3((unsigned)nq), dim3(kCntThreads), rank_lds, s, parts, nq,
+    hipLaunchKernelGGL(merge_packed_count_kernel, dim3((unsigned)nq), dim3(kCntThreads), cnt_lds, s, parts, nq,
                        (int)nparts, (int)k, n_global, out_scores, out_ids, status);
-  } else if (rank_ok && g_merge_variant != 1 && (g_merge_variant == 2 || nparts > 1)) {
-    static bool attr_set = false;
-    if (!attr_set) {
-      DRT_CHECK_HIP(hipFuncSetAttribute((const void*)merge_packed_rank_kernel,
-                                        hipFuncAttributeMaxDynamicSharedMemorySize, kRankLds));
-      attr_set = true;
-    }
-    hipLaunchKernelGGL(merge_packed_rank_kernel, dim3((unsigned)(nq * nparts)), dim3(kRankThreads), rank_lds, s,
-                       parts, nq, (int)nparts, (int)k, n_global, out_scores, out_ids, status);
   } else if (nparts > 1 && (p2 / 2) * kp <= kTreeMaxE * kTreeThreads && lds <= 128 * 1024) {
 #define DRT_TREE(KPV)                                                                                        \
   {                                                                                                          \

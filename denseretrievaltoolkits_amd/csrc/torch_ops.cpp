@@ -55,6 +55,23 @@ Tensor workspace(const Tensor& like, size_t bytes) {
 }
 
 // ---------------------------------------------------------------------------- search
+// The caller-provided result buffers of ip_topk.out / ip_topk_resolve: the kernels write through their
+// raw pointers, so shape, dtype, contiguity and device are checked before any launch.
+static void check_topk_outputs(const Tensor& q, int64_t nq, int64_t k, const Tensor& scores, const Tensor& ids,
+                               const Tensor& status) {
+  TORCH_CHECK_VALUE(scores.device() == q.device() && ids.device() == q.device() && status.device() == q.device(),
+                    "scores / ids / status must be on the queries' device ", q.device());
+  TORCH_CHECK_VALUE(scores.is_contiguous() && scores.scalar_type() == at::kFloat && scores.dim() == 2 &&
+                        scores.size(0) == nq && scores.size(1) == k,
+                    "scores: expected a contiguous float [", nq, ", ", k, "] tensor, got ", scores.sizes());
+  TORCH_CHECK_VALUE(ids.is_contiguous() && ids.scalar_type() == at::kLong && ids.dim() == 2 && ids.size(0) == nq &&
+                        ids.size(1) == k,
+                    "ids: expected a contiguous int64 [", nq, ", ", k, "] tensor, got ", ids.sizes());
+  TORCH_CHECK_VALUE(status.is_contiguous() && status.scalar_type() == at::kInt && status.dim() == 1 &&
+                        status.size(0) == nq,
+                    "status: expected a contiguous int32 [", nq, "] tensor, got ", status.sizes());
+}
+
 void ip_topk_out(const Tensor& q_, const Tensor& p_, int64_t k, int64_t id_offset, Tensor& scores, Tensor& ids,
                  Tensor& status) {
   need(q_, "q", at::kBFloat16, 2);
@@ -63,12 +80,7 @@ void ip_topk_out(const Tensor& q_, const Tensor& p_, int64_t k, int64_t id_offse
   const c10::DeviceGuard g(q_.device());
   const Tensor q = q_.contiguous(), p = p_.contiguous();
   const int64_t nq = q.size(0), n = p.size(0), d = q.size(1);
-  TORCH_CHECK(scores.is_contiguous() && scores.scalar_type() == at::kFloat && scores.numel() == nq * k,
-              "scores: expected a contiguous float [", nq, ", ", k, "] tensor");
-  TORCH_CHECK(ids.is_contiguous() && ids.scalar_type() == at::kLong && ids.numel() == nq * k,
-              "ids: expected a contiguous int64 [", nq, ", ", k, "] tensor");
-  TORCH_CHECK(status.is_contiguous() && status.scalar_type() == at::kInt && status.numel() == nq,
-              "status: expected a contiguous int32 [", nq, "] tensor");
+  check_topk_outputs(q, nq, k, scores, ids, status);
   const size_t wsb = drt_ip_topk_workspace(nq, n, (int32_t)d, (int32_t)k);
   TORCH_CHECK_VALUE(wsb > 0 || nq == 0, "unsupported ip_topk shape nq=", nq, " n=", n, " d=", d, " k=", k,
               " (d % 64 == 0, d <= 1024, 1 <= k <= 2048)");
@@ -95,7 +107,11 @@ int64_t ip_topk_resolve(const Tensor& q_, const Tensor& p_, int64_t k, int64_t i
   need(p_, "p", at::kBFloat16, 2);
   const c10::DeviceGuard g(q_.device());
   const Tensor q = q_.contiguous(), p = p_.contiguous();
+  TORCH_CHECK_VALUE(q.size(1) == p.size(1), "q and p differ in dimension: ", q.sizes(), " vs ", p.sizes());
+  TORCH_CHECK_VALUE(p.device() == q.device(), "q and p must be on the same device");
   const int64_t nq = q.size(0), n = p.size(0), d = q.size(1);
+  TORCH_CHECK_VALUE(k >= 1 && k <= 2048, "unsupported k=", k);
+  check_topk_outputs(q, nq, k, scores, ids, status);
   if (nq == 0) return 0;
   const int64_t nbad = status.ne(0).sum().item<int64_t>();   // synchronises, like the C entry
   if (nbad == 0) return 0;

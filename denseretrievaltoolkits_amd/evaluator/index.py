@@ -51,15 +51,16 @@ class BaseFaissIPRetriever:
         return self.index.search_device(q_reps, k)
 
     def batch_search(self, q_reps, k: int, batch_size: int, quiet: bool = False) -> np.ndarray:
-        """All query batches enqueued back to back (FlatIPIndex.search_batches: batch j + 1 is
-        on the GPU while batch j is certified), one host copy of the ids at the end."""
+        """All query batches enqueued back to back (FlatIPIndex.search_batches_iter: batch j + 1 is
+        on the GPU while batch j is certified and its results land in pinned host memory)."""
         n = q_reps.shape[0]
         if n == 0:
             return np.zeros((0, k), dtype=np.int64)
         qd = self.index._queries(q_reps)
-        res = self.index.search_batches([qd[a: a + batch_size] for a in range(0, n, batch_size)], k)
-        self.last_scores = torch.cat([r[0] for r in res]).cpu().numpy()
-        return torch.cat([r[1] for r in res]).cpu().numpy()
+        res = list(self.index.search_batches_iter([qd[a: a + batch_size] for a in range(0, n, batch_size)], k,
+                                                  to_host=True))
+        self.last_scores = np.concatenate([r[0] for r in res])
+        return np.concatenate([r[1] for r in res])
 
 
 class FaissRetriever(BaseFaissIPRetriever):

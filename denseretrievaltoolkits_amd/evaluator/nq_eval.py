@@ -18,6 +18,32 @@ def tokenize_uncased(text: str):
     return [m.group().lower() for m in _TOKEN_RE.finditer(text)]
 
 
+# the same pattern without capture groups: findall returns the token strings directly
+_TOKEN_FINDALL = regex.compile(r"[\p{L}\p{N}\p{M}]+|[^\p{Z}\p{C}]",
+                               flags=regex.IGNORECASE + regex.UNICODE + regex.MULTILINE)
+# passage separator of the bulk tokeniser: a punctuation character (one token of its own under
+# the pattern, never part of a word token); a batch whose texts contain it is tokenised per text
+_SEP = "\u2042"
+
+
+def tokenize_uncased_many(texts):
+    """[tokenize_uncased(NFD(t)) for t in texts] in one regex pass over the joined texts."""
+    if not texts:
+        return []
+    if any(_SEP in t for t in texts):
+        return [tokenize_uncased(unicodedata.normalize("NFD", t)) for t in texts]
+    toks = _TOKEN_FINDALL.findall(unicodedata.normalize("NFD", _SEP.join(texts)))
+    out, cur = [], []
+    for t in toks:
+        if t == _SEP:
+            out.append(cur)
+            cur = []
+        else:
+            cur.append(t.lower())
+    out.append(cur)
+    return out
+
+
 def regex_match(text, pattern):
     try:
         pat = re.compile(pattern, flags=re.IGNORECASE + re.UNICODE + re.MULTILINE)
@@ -104,4 +130,98 @@ class AnswerMatcher:
                 pos = pos[flat[pos + j] == ids[j]]
             if pos.size:
                 hit[np.searchsorted(starts, pos, side="right") - 1] = 1
+        return hit
+
+
+class RowAnswerMatcher:
+    """``has_answers`` for a whole query batch's retrieved ROWS at once (Trainer.evaluate).
+
+    Same result as ``has_answers(text_of(row), answers[i])`` for every (query i, rank j) with
+    ``row = rows[i, j] >= 0`` (pads get 0).  Every index row is tokenised once per evaluation
+    (NFD, the uncased SimpleTokenizer pattern, one regex pass over many passages) into int32
+    token ids stored as one row of a padded [rows, width] matrix (-1 pads, width grows with the
+    longest passage seen), so a query's k passages are ONE row gather, and an answer of n tokens
+    is found by n shifted vectorised comparisons (a match never spans two passages; an empty
+    answer matches every passage, as the reference's loop does).
+    """
+
+    def __init__(self, n_rows: int):
+        self.vocab = {}
+        self.n_rows = int(n_rows)
+        self.width = 16
+        self.tok = np.full((self.n_rows, self.width), -1, dtype=np.int32)
+        self.seen = np.zeros(self.n_rows, dtype=bool)
+
+    def ensure_rows(self, n_rows: int):
+        """Capacity for rows [0, n_rows) (geometric growth: called once per corpus batch)."""
+        if n_rows > self.n_rows:
+            n_rows = max(int(n_rows), self.n_rows + self.n_rows // 2)
+            t = np.full((n_rows, self.width), -1, dtype=np.int32)
+            t[: self.n_rows] = self.tok
+            sn = np.zeros(n_rows, dtype=bool)
+            sn[: self.n_rows] = self.seen
+            self.tok, self.seen, self.n_rows = t, sn, int(n_rows)
+
+    def rebase(self, offset: int, n_local: int, n_total: int):
+        """Move rows [0, n_local) (a shard tokenised by local row) to [offset, offset + n_local) of
+        an n_total-row matcher (global rows of the sharded index)."""
+        t = np.full((n_total, self.width), -1, dtype=np.int32)
+        sn = np.zeros(n_total, dtype=bool)
+        t[offset: offset + n_local] = self.tok[:n_local]
+        sn[offset: offset + n_local] = self.seen[:n_local]
+        self.tok, self.seen, self.n_rows = t, sn, int(n_total)
+
+    def _grow(self, width: int):
+        w = self.width
+        while w < width:
+            w *= 2
+        t = np.full((self.n_rows, w), -1, dtype=np.int32)
+        t[:, : self.width] = self.tok
+        self.tok, self.width = t, w
+
+    def fill(self, rows, text_of) -> int:
+        """Tokenise every row of ``rows`` not seen yet (``text_of(row)`` -> passage text)."""
+        rows = np.unique(rows[rows >= 0])
+        miss = rows[~self.seen[rows]]
+        if miss.size:
+            v = self.vocab
+            toks_list = tokenize_uncased_many([text_of(r) for r in miss.tolist()])
+            mx = max((len(t) for t in toks_list), default=0)
+            if mx > self.width:
+                self._grow(mx)
+            for r, toks in zip(miss.tolist(), toks_list):
+                if toks:
+                    self.tok[r, : len(toks)] = [v[t] if t in v else v.setdefault(t, len(v)) for t in toks]
+            self.seen[miss] = True
+        return int(miss.size)
+
+    def match_rows(self, rows: np.ndarray, text_of, answers) -> np.ndarray:
+        """int8 [B, k]: 1 where the passage at rows[i, j] contains any of answers[i]."""
+        B, k = rows.shape
+        hit = np.zeros((B, k), dtype=np.int8)
+        if B == 0 or k == 0:
+            return hit
+        self.fill(rows, text_of)
+        valid = rows >= 0
+        W = self.width
+        for i in range(B):
+            toks = None
+            for ans in answers[i]:
+                aw = tokenize_uncased(unicodedata.normalize("NFD", ans))
+                if not aw:
+                    hit[i] = 1
+                    break
+                ids = [self.vocab.get(w, -2) for w in aw]
+                if min(ids) < 0:
+                    continue   # a token no passage has
+                n = len(ids)
+                if n > W:
+                    continue
+                if toks is None:
+                    toks = self.tok[np.where(valid[i], rows[i], 0)]       # [k, W] row gather
+                m = toks[:, : W - n + 1] == ids[0]
+                for j in range(1, n):
+                    m &= toks[:, j: W - n + 1 + j] == ids[j]
+                hit[i] |= m.any(axis=1).astype(np.int8)
+        hit[~valid] = 0
         return hit

@@ -33,16 +33,28 @@ def _as_device_bf16(x, device) -> torch.Tensor:
     return x.detach().to(device=device, dtype=torch.bfloat16).contiguous()
 
 
+def _stage_host(*ts: torch.Tensor):
+    """Host copies of device tensors, staged without waiting: pinned non-blocking D2H copies on
+    the tensors' device stream plus one event behind them.  The host looks at them only when the
+    work is finished, after the next batch has been enqueued, so reading them never drains the
+    stream (the copies and the event go on the tensors' OWN device stream: an index may live on
+    a device other than the current one)."""
+    dev = ts[0].device
+    hs = [torch.empty(t.shape, dtype=t.dtype, pin_memory=True) for t in ts]
+    with torch.cuda.device(dev):
+        stream = torch.cuda.current_stream(dev)
+        for h, t in zip(hs, ts):
+            h.copy_(t, non_blocking=True)
+        ev = torch.cuda.Event()
+        ev.record(stream)
+    return hs, ev
+
+
 def _stage_status(st: torch.Tensor):
-    """Host copy of a device status vector, staged without waiting: a pinned non-blocking D2H
-    plus an event behind it.  The host looks at it only when the batch is finished, after the
-    next batch has been enqueued (search_batches), so the check never drains the stream."""
+    """Host copy of a device status vector (see _stage_host)."""
     if not st.is_cuda:
         return st, None
-    h = torch.empty(st.shape, dtype=st.dtype, pin_memory=True)
-    h.copy_(st, non_blocking=True)
-    ev = torch.cuda.Event()
-    ev.record()
+    (h,), ev = _stage_host(st)
     return h, ev
 
 
@@ -52,18 +64,31 @@ def _status_failed(h: torch.Tensor, ev) -> int:
     return int((h != 0).sum().item())
 
 
+class _HostResult:
+    """(scores, ids) of a batch copied to pinned host memory behind an event (to_host mode)."""
+    __slots__ = ("hs", "ev")
+
+    def __init__(self, s: torch.Tensor, i: torch.Tensor):
+        self.hs, self.ev = _stage_host(s, i)
+
+    def get(self, s: torch.Tensor, i: torch.Tensor, redone: bool):
+        """numpy (scores, ids); a batch that was redone after staging is copied again."""
+        if redone:
+            return s.cpu().numpy(), i.cpu().numpy()
+        self.ev.synchronize()
+        return self.hs[0].numpy(), self.hs[1].numpy()
+
+
 def _pipeline(batches, enqueue, finish):
-    """Enqueue batch j + 1 before finishing (certifying) batch j."""
-    res = []
+    """Enqueue batch j + 1 before finishing (certifying) batch j; yields finished results in order."""
     pend = None
     for j, q in enumerate(batches):
         cur = enqueue(j, q)
         if pend is not None:
-            res.append(finish(pend))
+            yield finish(pend)
         pend = cur
     if pend is not None:
-        res.append(finish(pend))
-    return res
+        yield finish(pend)
 
 
 # Batched search (search_batches): the per-batch fixed costs of the global-threshold protocol --
@@ -91,12 +116,13 @@ def _groups(batches, cap=GROUP_QUERIES):
         yield grp
 
 
-def _gtau_enqueue_group(local, qs, k: int, n_global: int, offset: int, gather):
+def _gtau_enqueue_group(local, qs, k: int, n_global: int, offset: int, gather, to_host: bool = False):
     """One group of query batches through the global-threshold protocol (see ShardedFlatIP):
     ONE sample launch for all of the group's queries, one exchange of the sample lists, one
     threshold launch, one filter scan (+ select) per batch writing its packed top-k into a group buffer,
     one exchange of that buffer and one merge that certifies every query.  ``gather(t)`` ->
-    [world, *t.shape] (identity stack on one GPU)."""
+    [world, *t.shape] (identity stack on one GPU).  ``to_host``: the merged group's results are
+    also staged to pinned host memory behind the merge."""
     sizes = [q.shape[0] for q in qs]
     qg = qs[0] if len(qs) == 1 else torch.cat(qs)
     best = local.dist_sample(qg, n_global, k)                       # [Qg, r]
@@ -109,22 +135,29 @@ def _gtau_enqueue_group(local, qs, k: int, n_global: int, offset: int, gather):
         o += nb
     s, i, st = kernels.merge_packed(gather(packed), k, n_global)
     h, ev = _stage_status(st)
-    return qs, sizes, s, i, h, ev
+    host = _HostResult(s, i) if to_host else None
+    return qs, sizes, s, i, h, ev, host
 
 
 def _gtau_finish_group(pend, redo):
     """Per-batch results of a group; a batch with an uncertified query is redone by ``redo(q)``
     (the exact path).  Every rank merged the same gathered lists, so all ranks redo the same
-    batches (their collectives stay matched)."""
-    qs, sizes, s, i, h, ev = pend
+    batches (their collectives stay matched).  With staged host copies the results are numpy."""
+    qs, sizes, s, i, h, ev, host = pend
     if ev is not None:
         ev.synchronize()
     bad = (h != 0)
     res, o, nredo = [], 0, 0
+    hs = hi = None
     for q, nb in zip(qs, sizes):
         if bool(bad[o:o + nb].any()):
-            res.append(redo(q))
+            rs, ri = redo(q)
+            res.append((rs.cpu().numpy(), ri.cpu().numpy()) if host is not None else (rs, ri))
             nredo += 1
+        elif host is not None:
+            if hs is None:
+                hs, hi = host.get(s, i, False)
+            res.append((hs[o:o + nb], hi[o:o + nb]))
         else:
             res.append((s[o:o + nb], i[o:o + nb]))
         o += nb
@@ -186,17 +219,20 @@ class FlatIPIndex:
     # certify (status != 0, ~1e-9 per query on real data) is redone by the exact dense rescan.
     resolved = 0   # queries redone by the exact rescan over this index's lifetime
 
-    def _enqueue(self, q, k: int, id_offset: int = 0, out=None):
+    def _enqueue(self, q, k: int, id_offset: int = 0, out=None, to_host: bool = False):
         qd = self._queries(q)
         s, i, st = kernels.ip_topk(qd, self.rows, k, id_offset=id_offset, resolve=False, out=out)
         h, ev = _stage_status(st)
-        return qd, s, i, st, h, ev, id_offset, k
+        host = _HostResult(s, i) if to_host else None
+        return qd, s, i, st, h, ev, id_offset, k, host
 
     def _finish(self, pend):
-        qd, s, i, st, h, ev, off, k = pend
+        qd, s, i, st, h, ev, off, k, host = pend
         nbad = _status_failed(h, ev)
         if nbad:
             self.resolved += kernels.resolve_failed(qd, self.rows, k, off, s, i, st, n_failed=nbad)
+        if host is not None:
+            return host.get(s, i, nbad > 0)
         return s, i
 
     def search_unresolved(self, q, k: int, id_offset: int = 0):
@@ -216,13 +252,21 @@ class FlatIPIndex:
         group, one filter scan per batch (_gtau_enqueue_group).  ``outs[j]`` = optional
         (scores, ids) output buffers of batch j (per-batch path).  This is the path
         BaseFaissIPRetriever.batch_search, Trainer.evaluate and bench.py time."""
+        return list(self.search_batches_iter(batches, k, id_offset, outs))
+
+    def search_batches_iter(self, batches, k: int, id_offset: int = 0, outs=None, to_host: bool = False):
+        """search_batches as a generator: batch j's result is yielded once batch j + 1 (or the next
+        group) is on the GPU, so the caller's host work on batch j overlaps the device work on
+        batch j + 1.  ``to_host``: yield numpy (scores, ids) from pinned copies staged behind each
+        batch (no stream-draining .cpu() per batch)."""
         batches = list(batches)
         if outs is None and self.ntotal >= GROUP_MIN_ROWS and self.ntotal < 0xFFFFFFFF:
-            return self._search_groups(batches, k, id_offset)
-        return _pipeline(batches, lambda j, q: self._enqueue(q, k, id_offset, outs[j] if outs else None),
-                         self._finish)
+            yield from self._search_groups(batches, k, id_offset, to_host)
+            return
+        yield from _pipeline(batches, lambda j, q: self._enqueue(q, k, id_offset, outs[j] if outs else None,
+                                                                 to_host), self._finish)
 
-    def _search_groups(self, batches, k: int, id_offset: int):
+    def _search_groups(self, batches, k: int, id_offset: int, to_host: bool = False):
         groups = [[self._queries(q) for q in g] for g in _groups(batches)]
 
         def fin(pend):
@@ -230,9 +274,9 @@ class FlatIPIndex:
             self.group_fallbacks += nredo
             return res
 
-        out = _pipeline(groups, lambda j, g: _gtau_enqueue_group(self, g, k, self.ntotal, id_offset,
-                                                                 lambda t: t.unsqueeze(0)), fin)
-        return [r for g in out for r in g]
+        for res in _pipeline(groups, lambda j, g: _gtau_enqueue_group(self, g, k, self.ntotal, id_offset,
+                                                                      lambda t: t.unsqueeze(0), to_host), fin):
+            yield from res
 
     def search(self, q, k: int) -> Tuple[np.ndarray, np.ndarray]:
         s, i = self.search_device(q, k)
@@ -333,12 +377,16 @@ class ShardedFlatIP:
         return self._finish(self._enqueue(q, k))
 
     def search_batches(self, batches, k: int):
-        """search_device over a sequence of query batches.  Global-threshold protocol on the
-        HIP shard: the batches run in groups of GROUP_QUERIES queries (_gtau_enqueue_group: one
-        sample launch, one sample-list all-gather, one packed all-gather and one merge per
-        group; one filter scan per batch), group g + 1 enqueued before the host checks group
-        g's certificates.  Otherwise batch j + 1 is enqueued (scan, exchange, merge) before
-        the host checks batch j's certificate (see FlatIPIndex.search_batches)."""
+        """search_device over a sequence of query batches (every rank passes the same batches)."""
+        return list(self.search_batches_iter(batches, k))
+
+    def search_batches_iter(self, batches, k: int, to_host: bool = False):
+        """Generator form of search_batches (see FlatIPIndex.search_batches_iter).  Global-threshold
+        protocol on the HIP shard: the batches run in groups of GROUP_QUERIES queries
+        (_gtau_enqueue_group: one sample launch, one sample-list all-gather, one packed all-gather
+        and one merge per group; one filter scan per batch), group g + 1 enqueued before the host
+        checks group g's certificates.  Otherwise batch j + 1 is enqueued (scan, exchange, merge)
+        before the host checks batch j's certificate."""
         batches = list(batches)
         if self.world > 1 and self.protocol == "global_tau" and self.ntotal < 0xFFFFFFFF \
                 and isinstance(self.local, FlatIPIndex):
@@ -350,19 +398,23 @@ class ShardedFlatIP:
                 self.fallbacks += nredo
                 return res
 
-            out = _pipeline(groups, lambda j, g: _gtau_enqueue_group(self.local, g, k, self.ntotal, self.offset,
-                                                                     self._all_gather), fin)
-            return [r for g in out for r in g]
-        return _pipeline(batches, lambda j, q: self._enqueue(q, k), self._finish)
+            for res in _pipeline(groups, lambda j, g: _gtau_enqueue_group(self.local, g, k, self.ntotal, self.offset,
+                                                                          self._all_gather, to_host), fin):
+                yield from res
+            return
+        for r in _pipeline(batches, lambda j, q: self._enqueue(q, k, to_host), self._finish):
+            if to_host and isinstance(r[0], torch.Tensor):
+                r = (r[0].cpu().numpy(), r[1].cpu().numpy())
+            yield r
 
     def _all_gather(self, t: torch.Tensor) -> torch.Tensor:
         """[world, *t.shape] all-gather (RCCL on device; host-staged under gloo, comm.py)."""
         return comm.all_gather_stacked(t, self.group)
 
-    def _enqueue(self, q, k: int):
+    def _enqueue(self, q, k: int, to_host: bool = False):
         if self.world == 1:
             if hasattr(self.local, "_enqueue"):
-                return ("local", self.local._enqueue(q, k, self.offset))
+                return ("local", self.local._enqueue(q, k, self.offset, to_host=to_host))
             return ("done", self.local.search_device(q, k, id_offset=self.offset))
         if self.protocol == "global_tau" and self.ntotal < 0xFFFFFFFF:
             best = self.local.dist_sample(q, self.ntotal, k)                 # [nq, r] u32 keys

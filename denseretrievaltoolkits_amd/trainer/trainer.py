@@ -34,7 +34,7 @@ from torch.nn.parallel import DistributedDataParallel as DDP
 
 from .. import comm
 from ..evaluator.metrics import get_metrics
-from ..evaluator.nq_eval import AnswerMatcher, has_answers
+from ..evaluator.nq_eval import AnswerMatcher, RowAnswerMatcher, has_answers
 from ..search import ShardedFlatIP
 from .losses import get_loss_function
 from .scheduler import ConstantScheduler, CosineScheduler, InverseSquareRootScheduler, LinearScheduler
@@ -147,14 +147,31 @@ class Trainer:
         dim = None
         ids_local: List = []
         self.index = None
+        # answers of evaluate are matched against the passages' tokens: the passages of this
+        # rank's shard are tokenised here, on the host, while the GPU encodes the next batches
+        ds = getattr(self.corpus_dataloader, "dataset", None)
+        self._matcher = RowAnswerMatcher(0) if (self.prefill_answer_tokens and ds is not None) else None
         for batch in self.corpus_dataloader:
-            data = {k: v.to(self.device) if v is not None else None for k, v in batch[1].items()}
+            data = {k: self._to_device(v) for k, v in batch[1].items()}
             reps = self._encode(passage=data).p_reps
             if self.index is None:
                 dim = reps.shape[1]
                 self.index = ShardedFlatIP(dim, device=self.device)
+                try:   # one allocation for the whole shard when the loader knows its length
+                    self.index.local.reserve(len(self.corpus_dataloader) * reps.shape[0])
+                except TypeError:
+                    pass
+            row0 = self.index.local.ntotal
             self.index.local.add(reps)
             ids_local.extend(list(batch[0]))
+            if self._matcher is not None:
+                try:
+                    dids = list(batch[0])
+                    self._matcher.ensure_rows(row0 + len(dids))
+                    self._matcher.fill(np.arange(row0, row0 + len(dids)),
+                                       lambda r, _d=dids, _o=row0: ds[_d[r - _o]]["original"])
+                except (KeyError, TypeError, IndexError):
+                    self._matcher = None   # no 'original' texts here: matched on demand in evaluate
         if self.index is None:
             raise ValueError("empty corpus")
         self._ids_local = ids_local
@@ -170,6 +187,8 @@ class Trainer:
     def _index_corpus(self, ep):
         """Agree on global row ids (shard offsets) and the row -> doc-id map."""
         self.index.sync_offsets()
+        if getattr(self, "_matcher", None) is not None and self.world > 1:
+            self._matcher.rebase(self.index.offset, self.index.local.ntotal, self.index.ntotal)
         if self.world > 1:
             gathered = [None] * self.world
             dist.all_gather_object(gathered, self._ids_local)
@@ -186,20 +205,117 @@ class Trainer:
         if dist.is_initialized():
             dist.barrier()
 
-    def _search(self, q_reps: torch.Tensor, k: int) -> np.ndarray:
-        """Global top-k ids for THIS rank's query batch (all ranks call it together).
+    # ------------------------------------------------------------------
+    # evaluate: query encode + search + answer matching, pipelined (reference trainer.py:269-346)
+    # ------------------------------------------------------------------
+    # Query batches are encoded in windows of up to ENCODE_WINDOW queries of one sequence length
+    # (one tower pass over thousands of queries runs the large-GEMM plans instead of a 128-query
+    # pass per loader batch), then searched in batches of SEARCH_BATCH through the certified,
+    # pipelined product path (search.FlatIPIndex / ShardedFlatIP.search_batches_iter): batch j + 1
+    # is on the GPU while the host matches answers for batch j, whose ids land in pinned memory
+    # behind an event.  Metrics stay per LOADER batch (get_metrics' NDCG is a batch-level ratio).
+    ENCODE_WINDOW = 4096
+    SEARCH_BATCH = 128
+    prefill_answer_tokens = True
 
-        The reference searches each rank's own queries against a full host index on every
-        rank (trainer.py:296-297).  Here the corpus is row-sharded, so the ranks' query
-        batches (ragged: the last batch may differ per rank) are all-gathered, every rank
-        scans its shard for all of them, and each keeps its own rows of the merged result."""
+    def _to_device(self, v):
+        if v is None or not isinstance(v, torch.Tensor):
+            return v
+        if v.is_cuda:
+            return v
+        return v.pin_memory().to(self.device, non_blocking=True)
+
+    def _query_windows(self, query_loader):
+        """Yields lists of loader batches (inputs on the device) of one sequence length, up to
+        ENCODE_WINDOW queries each."""
+        win, n, L = [], 0, None
+        for batch in query_loader:
+            data = {kk: self._to_device(v) for kk, v in batch[1].items()}
+            bl = data["input_ids"].shape[1]
+            nb = data["input_ids"].shape[0]
+            if win and (bl != L or n + nb > self.ENCODE_WINDOW):
+                yield win
+                win, n = [], 0
+            win.append((batch, data))
+            n += nb
+            L = bl
+        if win:
+            yield win
+
+    def _encode_window(self, win) -> torch.Tensor:
+        datas = [d for _, d in win]
+        if len(datas) == 1:
+            data = datas[0]
+        else:
+            data = {kk: (torch.cat([d[kk] for d in datas]) if datas[0][kk] is not None else None) for kk in datas[0]}
+        return self._encode(query=data).q_reps
+
+    def _search_rows(self, q_reps: torch.Tensor, k: int):
+        """Yields (row0, ids [n, k] host) for consecutive row ranges of this rank's query reps.
+
+        W = 1: the window's rows in SEARCH_BATCH batches.  W > 1: the corpus is row-sharded, so the
+        ranks' windows (ragged: a rank may have fewer or no queries left) are all-gathered, every
+        rank scans its shard for all of them (grouped global-threshold protocol), and each keeps
+        its own rows of the merged result (the reference searches each rank's own queries against
+        a full host index on every rank, trainer.py:296-297)."""
+        sb = self.SEARCH_BATCH
         if self.world == 1:
-            _, i = self.index.search_device(q_reps, k)
-            return i.cpu().numpy()
+            batches = [q_reps[a: a + sb] for a in range(0, q_reps.shape[0], sb)]
+            for j, (_, ids) in enumerate(self.index.local.search_batches_iter(batches, k, to_host=True)):
+                yield j * sb, ids
+            return
         allq, sizes = comm.all_gather_rows(q_reps.contiguous())
-        _, ids = self.index.search_device(allq, k)
         lo = sum(sizes[: self.rank])
-        return ids[lo: lo + sizes[self.rank]].cpu().numpy()
+        hi = lo + sizes[self.rank]
+        batches = [allq[a: a + sb] for a in range(0, allq.shape[0], sb)]
+        for j, (_, ids) in enumerate(self.index.search_batches_iter(batches, k, to_host=True)):
+            a, b = max(lo, j * sb), min(hi, (j + 1) * sb)
+            if a < b:
+                yield a - lo, ids[a - j * sb: b - j * sb]
+
+    def _search(self, q_reps: torch.Tensor, k: int) -> np.ndarray:
+        """Global top-k ids [n, k] (host) of THIS rank's query reps (all ranks call it together)."""
+        out = np.empty((q_reps.shape[0], k), dtype=np.int64)
+        for row0, ids in self._search_rows(q_reps, k):
+            out[row0: row0 + ids.shape[0]] = ids
+        return out
+
+    def _eval_results(self, query_loader, k: int):
+        """Yields (loader batch, ids [B, k] host) in loader order (all ranks call it together)."""
+        windows = self._query_windows(query_loader)
+        d = self.index.d
+        while True:
+            win = next(windows, None)
+            if self.world > 1:
+                # every rank takes part in every window's collectives until all are exhausted
+                n_local = 0 if win is None else sum(dd["input_ids"].shape[0] for _, dd in win)
+                if sum(comm.all_gather_sizes(n_local, self.device)) == 0:
+                    return
+            elif win is None:
+                return
+            if win is None:
+                q_reps = torch.empty((0, d), dtype=torch.float32, device=self.device)
+                win = []
+            else:
+                q_reps = self._encode_window(win)
+            n = q_reps.shape[0]
+            ids_all = np.empty((n, k), dtype=np.int64)
+            done, bi, b0 = 0, 0, 0
+            for row0, ids in self._search_rows(q_reps, k):
+                ids_all[row0: row0 + ids.shape[0]] = ids
+                done = row0 + ids.shape[0]
+                # hand out every loader batch whose rows are complete (host work overlaps the
+                # GPU's next search batch)
+                while bi < len(win) and b0 + win[bi][1]["input_ids"].shape[0] <= done:
+                    nb = win[bi][1]["input_ids"].shape[0]
+                    yield win[bi][0], ids_all[b0: b0 + nb]
+                    b0 += nb
+                    bi += 1
+            while bi < len(win):
+                nb = win[bi][1]["input_ids"].shape[0]
+                yield win[bi][0], ids_all[b0: b0 + nb]
+                b0 += nb
+                bi += 1
 
     def _doc_text(self, did_):
         t = self._doc_cache.get(did_)
@@ -207,11 +323,21 @@ class Trainer:
             t = self._doc_cache[did_] = self.corpus_dataloader.dataset[did_]["original"]
         return t
 
+    # stage timing of evaluate (bench.py's evaluate_c2 leg): synchronises the device once between
+    # the corpus stage and the query stage when on; off by default
+    profile_eval = False
+
     def evaluate(self, query_loader, ep):
+        import time
+        t0 = time.perf_counter()
         self.model.eval()
         self._encoding_corpus(ep)
         self._index_corpus(ep)
         self._load_index(ep)
+        if self.profile_eval:
+            torch.cuda.synchronize(self.device)
+        t1 = time.perf_counter()
+        t_host = 0.0
         a = self.training_args
         topk = a.topk if not isinstance(a.topk, str) else [int(x) for x in a.topk.split(",")]
         m_all = {f"{m}@{k}": 0.0 for m in ["MRR", "NDCG", "Recall"] for k in topk}
@@ -220,33 +346,35 @@ class Trainer:
             query_loader.sampler.set_epoch(0)
         documents, queries, answers, qid, did = [], [], [], [], []
         k = a.retrieve_num
-        matcher = AnswerMatcher()
+        rdir = getattr(a, "retrieve_dir", "")
         self._doc_cache = {}
-        for batch in query_loader:
-            data = {kk: v.to(self.device) if v is not None else None for kk, v in batch[1].items()}
-            q_reps = self._encode(query=data).q_reps
-            indices = self._search(q_reps, k)
-            pos_index = np.zeros([len(indices), k], dtype=np.int8)
-            docs, doc_ids = [], []
-            for i, indice in enumerate(indices):
-                eval_num += 1
-                cols = np.flatnonzero(indice >= 0)
-                doc_id = [self.idx[row] for row in indice[cols]]
-                doc = [self._doc_text(did_) for did_ in doc_id]
-                # has_answers over the whole list at once (nq_eval.AnswerMatcher: each passage
-                # tokenised once per evaluation, not once per retrieving query)
-                pos_index[i, cols] = matcher.match(doc_id, doc, batch[2][i])
-                docs.append(doc)
-                doc_ids.append(doc_id)
-            documents.extend(docs)
+        # vectorised has_answers over each batch's retrieved rows (nq_eval.RowAnswerMatcher: every
+        # passage tokenised once per evaluation -- this rank's shard already during the corpus encode)
+        matcher = getattr(self, "_matcher", None)
+        if matcher is None:
+            matcher = RowAnswerMatcher(len(self.idx))
+        matcher.ensure_rows(len(self.idx))
+
+        def text_of(row):
+            return self._doc_text(self.idx[row])
+
+        for batch, indices in self._eval_results(query_loader, k):
+            th = time.perf_counter()
+            pos_index = matcher.match_rows(indices, text_of, batch[2])
+            eval_num += len(indices)
+            if rdir:   # the retrieved documents are only needed for the retrieve/ output file
+                for indice in indices:
+                    doc_id = [self.idx[row] for row in indice[indice >= 0]]
+                    documents.append([self._doc_text(did_) for did_ in doc_id])
+                    did.append(doc_id)
             qid.extend(batch[0])
             answers.extend(batch[2])
             queries.extend(batch[3])
-            did.extend(doc_ids)
             metrics = get_metrics(pos_index, topk)
             for key in m_all:
                 m_all[key] += metrics[key]
-        rdir = getattr(a, "retrieve_dir", "")
+            t_host += time.perf_counter() - th
+        t2 = time.perf_counter()
         if rdir:
             os.makedirs(rdir, exist_ok=True)
             with open(os.path.join(rdir, f"{ep}.{self.local_rank}.json"), "w", encoding="utf-8") as f:
@@ -267,6 +395,8 @@ class Trainer:
         if dist.is_initialized():
             dist.barrier()
         self.last_metrics = m_all
+        self.last_eval_timing = {"corpus_s": t1 - t0, "queries_s": t2 - t1, "host_match_s": t_host,
+                                 "files_s": time.perf_counter() - t2}
         return m_all
 
     # ------------------------------------------------------------------

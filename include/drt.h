@@ -73,12 +73,6 @@ int drt_ip_topk_resolve(const void* Q, int64_t nq, const void* P, int64_t n, int
                         int32_t* status, void* workspace, size_t workspace_bytes,
                         int64_t* n_resolved, void* stream);
 
-/* Benchmark/test switch: 0 = production scan (16-row tiles, 6-slot ring),
- * 1 = filter scan WITHOUT its MFMA work (memory-pipeline ceiling; results are
- * meaningless), 2 = the previous 32-row / 3-slot scan kernel, 3/4/5 = 16-row
- * ablations (no MFMA / no LDS reads / no filter), 6 = 16-row with 4 waves.  */
-int drt_scan_variant(int32_t v);
-
 /* Merge `nparts` per-shard top-k lists into one global top-k.
  * scores/ids: [nparts, nq, k_in] (each part sorted score desc, id asc, as
  * drt_ip_topk_bf16 writes them); out: [nq, k_out], k_out <= k_in*nparts,
@@ -135,13 +129,6 @@ int drt_ip_topk_dist_filter_lists_at(const void* Q, int64_t nq, const void* P, i
 int drt_topk_merge_packed(const uint64_t* parts, int64_t nq, int32_t nparts, int32_t k,
                           int64_t n_global, float* out_scores, int64_t* out_ids, int32_t* status,
                           void* stream);
-/* Test / benchmark switch of drt_topk_merge_packed's kernel: 0 automatic (count merge, one
- * work-group per query over the valid entries only, when nparts <= 8 and nparts * k <= 8192;
- * else the rank merge, one work-group per (query, part), when nparts * k * 8 B <= 64 KiB; else the
- * per-query bitonic tree merge), 1 tree merge, 2 rank merge wherever it fits, 3 count merge
- * wherever it fits.  Same results for every setting.                                         */
-int drt_topk_merge_packed_variant(int32_t v);
-
 /* Dense score matrix C[m, n] = A[m, d] . B[n, d]^T with fp32 accumulation
  * (torch.matmul(q_reps, p_reps.T), biencoder.py:107).  A, B bf16; C fp32 with
  * leading dimension ldc.                                                     */
@@ -292,33 +279,6 @@ int drt_dropout_add_bf16(const void* y, const void* resid, int64_t n, float p, u
 int drt_pool_bf16(const void* hidden, const int64_t* mask, int64_t B, int64_t L, int32_t H,
                   int32_t mode, float* out, void* out_bf16, void* stream);
 int drt_l2_normalize_f32(float* x, int64_t B, int32_t H, void* out_bf16, void* stream);
-/* A/B switch for tests/bench: 0 automatic (ping-pong 256x256, 5-slot ring),
- * 1 forces the 128x128-tile GEMM, 2 half-K-ring 256x256,
- * 7/8 ping-pong 4/5-slot ring, 9 full-K 32x32x16 256x256; >= 16 diagnostic
- * builds (ablations / cycle stamps, need drt_gemm_debug_buffer).            */
-int drt_gemm_force_small(int32_t on);
-/* Benchmark / test switch: 1 keeps 4-wave attention-backward work-groups at every sequence
- * length; 0 (default) runs 8 waves per (sequence, head) for 5 blocks of 32 rows (L 129-160,
- * e.g. the recipe's 156-token passages).  Outputs are bit-identical either way.              */
-int drt_attention_force4(int32_t on);
-/* Benchmark switch: smallest grid, in 256x256 tiles, that takes the 256x256 kernel. */
-/* Benchmark switch of the split-K planning: the 256^2 kernel splits K >= large_min_k (default
- * 8192) into chunks of >= large_k_per_split (512); the 128^2 kernel keeps its fp32 partials <=
- * small_cap_bytes (16 MiB).  Non-positive arguments keep the current value.                 */
-int drt_gemm_split_config(int64_t large_min_k, int64_t large_k_per_split, int64_t small_cap_bytes);
-int drt_gemm_large_min_tiles(int64_t tiles);
-/* Benchmark switch of the mid-size GEMM plan: problems below the 256x256 threshold with
- * M >= min_m take the whole-line 256x256 kernel, K split over ~one block per CU (fp32 partials
- * <= cap_bytes, >= min_ktiles K-tiles of 64 per split) when drt_linear_bf16_ws gets scratch
- * (drt_linear_workspace sizes it).  Non-positive arguments keep the current value.          */
-int drt_gemm_mid_config(int64_t min_m, int64_t cap_bytes, int64_t min_ktiles);
-/* Diagnostic only: device buffer for the GEMM cycle-stamp variants (drt_gemm_force_small >= 16). */
-int drt_gemm_debug_buffer(void* buf);
-/* Benchmark switch: tile order of the 256x256 ping-pong GEMM inside each XCD's tile range
- * (-1 automatic, 0 row-major, 1 grouped by 8 m-panels, 2 column-major,
- * 3/4 grouped by 4/16).                                                     */
-int drt_gemm_tile_order(int32_t order);
-
 /* ------------------------------------------------------------------------
  * In-batch-negative training loss (DRModel.forward, biencoder.py:107-119;
  * SimpleContrastiveLoss, losses.py:11-17), fp32 like the reference.

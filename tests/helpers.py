@@ -59,3 +59,28 @@ def corpus_topk_golden():
     q = rng.integers(-lim, lim + 1, size=(int(z["nq"]), int(z["d"]))).astype(np.float32)
     p = rng.integers(-lim, lim + 1, size=(int(z["n"]), int(z["d"]))).astype(np.float32)
     return q, p, int(z["k"]), int(z["parts"]), z["ids"].astype(np.int64), z["scores"]
+
+
+def oracle_topk_streamed(q, p_dev, k, chunk=1 << 20, id_offset=0):
+    """oracle.ip_topk of host queries q [nq, d] over a DEVICE corpus p_dev [n, d] (bf16), streamed to
+    the host chunk by chunk (fp32 BLAS: exact for the integer-valued fixtures) and merged with the
+    oracle's partition merge -- the full-size reference answer without a full host copy."""
+    from oracle.search_oracle import ip_topk, merge_topk
+    es = ei = None
+    n = p_dev.shape[0]
+    for a in range(0, n, chunk):
+        pc = p_dev[a: a + chunk].float().cpu().numpy()
+        cs, ci = ip_topk(q, pc, k, id_offset=id_offset + a, dtype=np.float32)
+        es, ei = (cs, ci) if es is None else merge_topk(np.stack([es, cs]), np.stack([ei, ci]), k)
+    return es, ei
+
+
+def device_int_corpus(n, d, lo, hi, seed, device, chunk=1 << 20):
+    """[n, d] bf16 corpus of integers in [lo, hi] generated on the device chunk by chunk (seeded)."""
+    import torch
+    p = torch.empty((n, d), dtype=torch.bfloat16, device=device)
+    g = torch.Generator(device=device).manual_seed(seed)
+    for a in range(0, n, chunk):
+        b = min(n, a + chunk)
+        p[a:b] = torch.randint(lo, hi + 1, (b - a, d), generator=g, device=device, dtype=torch.int32).to(torch.bfloat16)
+    return p

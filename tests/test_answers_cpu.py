@@ -52,3 +52,44 @@ def test_answer_matcher_random_vs_has_answers():
         sel = rng.choice(200, size=50).tolist()
         got = m.match(sel, [docs[j] for j in sel], ans).tolist()
         assert got == [int(has_answers(docs[j], ans)) for j in sel]
+
+
+def test_row_matcher_matches_reference_golden():
+    """RowAnswerMatcher (Trainer.evaluate's batch matcher) on the reference-generated cases: each
+    case is one query row of retrieved passages (pads appended: -1 rows match nothing)."""
+    from denseretrievaltoolkits_amd.evaluator.nq_eval import RowAnswerMatcher
+    g = _gold()
+    m = RowAnswerMatcher(len(g["docs"]))
+    for c in g["cases"]:
+        rows = np.array([c["docs"] + [-1, -1]], dtype=np.int64)
+        got = m.match_rows(rows, lambda r: g["docs"][r], [c["answers"]])
+        assert got.dtype == np.int8 and got[0].tolist() == c["has"] + [0, 0], c
+
+
+def test_row_matcher_random_vs_has_answers():
+    from denseretrievaltoolkits_amd.evaluator.nq_eval import RowAnswerMatcher, tokenize_uncased, \
+        tokenize_uncased_many
+    import unicodedata
+    rng = np.random.default_rng(1)
+    vocab = ["a", "b", "c", "d", "A", "b.", "c-d", "e", "É", "naïve", "⁂", "日本"]
+    docs = [" ".join(rng.choice(vocab, size=int(rng.integers(0, 40)))) for _ in range(300)]
+    m = RowAnswerMatcher(0)
+    m.ensure_rows(300)
+    for _ in range(60):
+        B, k = 4, 30
+        rows = rng.integers(-1, 300, size=(B, k))
+        ans = [[" ".join(rng.choice(vocab, size=int(rng.integers(0, 4)))) for _ in range(int(rng.integers(1, 3)))]
+               for _ in range(B)]
+        got = m.match_rows(rows, lambda r: docs[r], ans)
+        ref = [[int(has_answers(docs[r], ans[i])) if r >= 0 else 0 for r in rows[i]] for i in range(B)]
+        assert got.tolist() == ref
+    # the bulk tokeniser equals the per-text one (also with the separator inside a text)
+    assert tokenize_uncased_many(docs[:50]) == [tokenize_uncased(unicodedata.normalize("NFD", t)) for t in docs[:50]]
+    # rebase: rows tokenised by local row land at the shard's global offset
+    m2 = RowAnswerMatcher(0)
+    m2.ensure_rows(10)
+    m2.fill(np.arange(10), lambda r: docs[r])
+    m2.rebase(100, 10, 200)
+    rows = np.arange(100, 110)[None, :]
+    got = m2.match_rows(rows, lambda r: (_ for _ in ()).throw(AssertionError("refilled")), [["a"]])
+    assert got[0].tolist() == [int(has_answers(docs[r], ["a"])) for r in range(10)]

@@ -129,14 +129,16 @@ def test_dist_shape_errors(dev):
 
 @pytest.mark.parametrize("nparts,nq,k,fill", [(8, 128, 1000, 0.5), (2, 5, 2048, 1.0), (3, 7, 100, 0.0),
                                               (5, 9, 10, 0.3), (9, 4, 1000, 0.4), (16, 3, 1000, 0.2),
-                                              (8, 2, 1000, 0.05), (1, 6, 64, 0.7)])
-def test_merge_packed_variants_vs_oracle(dev, nparts, nq, k, fill):
-    """drt_topk_merge_packed's count merge (one work-group per query, valid entries only), rank merge
-    (one work-group per (query, part)) and tree merge against the oracle on random packed lists:
-    unique keys, ragged fills, empty parts, overflow flags."""
+                                              (8, 2, 1000, 0.05), (1, 6, 64, 0.7), (5, 3, 2048, 0.6)])
+@pytest.mark.parametrize("count_word", [True, False])
+def test_merge_packed_vs_oracle(dev, nparts, nq, k, fill, count_word):
+    """drt_topk_merge_packed against the oracle on random packed lists (unique keys, ragged fills,
+    empty parts, overflow flags) for every kernel the shape selects: count merge (2-8 parts,
+    nparts * k <= 8192), tree merge (more parts or keys), plain per-query merge (one part).
+    count_word False: entry k carries the flags only (the pre-0.3 contract) -> the count merge
+    measures each list itself and must give the same result."""
     import torch
-    from denseretrievaltoolkits_amd import _native, kernels
-    lib = _native.load()
+    from denseretrievaltoolkits_amd import kernels
     rng = np.random.default_rng(nparts * 1000 + k)
     parts = np.full((nparts, nq, k + 1), np.iinfo(np.uint64).max, dtype=np.uint64)
     n_global = nparts * k * 4
@@ -147,13 +149,11 @@ def test_merge_packed_variants_vs_oracle(dev, nparts, nq, k, fill):
         for l in range(nparts):
             cnt = int(rng.binomial(k, fill)) if fill < 1.0 else k
             parts[l, q, :cnt] = np.sort(keys[l * k: l * k + cnt])
-            parts[l, q, k] = (np.uint64(cnt) << np.uint64(32)) | np.uint64(rng.random() < 0.1)  # count | overflow
+            cw = np.uint64(cnt) << np.uint64(32) if count_word else np.uint64(0)
+            parts[l, q, k] = cw | np.uint64(rng.random() < 0.1)  # count | overflow
     es, ei, est = orc.merge_packed(parts, k, n_global)
     pt = torch.from_numpy(parts.view(np.int64)).to(dev)
-    for v in (0, 1, 2, 3):
-        _native.check(lib.drt_topk_merge_packed_variant(v), "variant")
-        s, i, st = kernels.merge_packed(pt, k, n_global)
-        np.testing.assert_array_equal(i.cpu().numpy(), ei, err_msg=f"variant {v}")
-        np.testing.assert_array_equal(s.cpu().numpy(), es, err_msg=f"variant {v}")
-        np.testing.assert_array_equal(st.cpu().numpy(), est, err_msg=f"variant {v}")
-    lib.drt_topk_merge_packed_variant(0)
+    s, i, st = kernels.merge_packed(pt, k, n_global)
+    np.testing.assert_array_equal(i.cpu().numpy(), ei)
+    np.testing.assert_array_equal(s.cpu().numpy(), es)
+    np.testing.assert_array_equal(st.cpu().numpy(), est)

@@ -347,38 +347,3 @@ def test_layernorm_bwd_drop_output_equals_dropout_kernel(dev, M, H):
     torch.cuda.synchronize()
     assert torch.equal(dx, dx0) and torch.equal(dg, dg0) and torch.equal(db, db0)
     assert torch.equal(dxd, ref)
-
-
-@pytest.mark.parametrize("L,p", [(156, 0.0), (160, 0.1), (137, 0.1)])
-def test_attention_8_wave_workgroups_bit_identical(dev, L, p):
-    """L 129-160: the attention backward runs 8 waves per (sequence, head) (one 32-row block per
-    wave instead of wave 0 taking two); every block's arithmetic is unchanged, so dqkv is
-    bit-identical to the 4-wave kernel (drt_attention_force4), padding keys and dropout included."""
-    import torch
-    from denseretrievaltoolkits_amd import _native
-    lib = _native.load()
-    s = _native.stream_ptr(dev)
-    B, heads, H = 6, 12, 768
-    g = torch.Generator(device=dev).manual_seed(L)
-    qkv = (0.5 * torch.randn(B * L, 3 * H, generator=g, device=dev)).to(torch.bfloat16)
-    dctx = (0.1 * torch.randn(B * L, H, generator=g, device=dev)).to(torch.bfloat16)
-    mask = torch.ones(B, L, dtype=torch.int64, device=dev)
-    mask[1, L - 17:] = 0
-    mask[4, 40:] = 0
-    outs = {}
-    for f4 in (1, 0):
-        _native.check(lib.drt_attention_force4(f4), "force4")
-        ctx = torch.empty(B * L, H, dtype=torch.bfloat16, device=dev)
-        lse = torch.empty(B * heads * L, dtype=torch.float32, device=dev)
-        dqkv = torch.empty_like(qkv)
-        _native.check(lib.drt_attention_train_fwd_bf16(qkv.data_ptr(), mask.data_ptr(), ctx.data_ptr(), lse.data_ptr(),
-                                                       B, L, heads, 64, 0.125, p, 77, 3, s), "fwd")
-        _native.check(lib.drt_attention_train_bwd_bf16(qkv.data_ptr(), ctx.data_ptr(), dctx.data_ptr(), lse.data_ptr(),
-                                                       mask.data_ptr(), dqkv.data_ptr(), B, L, heads, 64, 0.125, p, 77,
-                                                       3, s), "bwd")
-        torch.cuda.synchronize()
-        outs[f4] = (ctx, lse, dqkv)
-    lib.drt_attention_force4(0)
-    for a, b in zip(outs[1], outs[0]):
-        assert torch.equal(a, b)
-    assert bool(torch.isfinite(outs[0][2].float()).all())

@@ -14,6 +14,8 @@ transformers 4.x's ``prepare_for_model`` (the reference's collator calls it; tra
 one installed, removed it).
 
 Reads the reference from /root/reference (skipped where it is absent, e.g. on the GPU box).
+Opt-in (DRT_RUN_REFERENCE_SCRIPT=1): the test executes the reference checkout's own Python in-process,
+and that checkout is untrusted third-party content, so a default pytest run never imports it.
 """
 import json
 import os
@@ -25,7 +27,11 @@ import pytest
 REF = "/root/reference"
 SCRIPT = os.path.join(REF, "run_random_sampling.py")
 
-pytestmark = pytest.mark.skipif(not os.path.exists(SCRIPT), reason="reference checkout not present")
+pytestmark = [
+    pytest.mark.skipif(not os.path.exists(SCRIPT), reason="reference checkout not present"),
+    pytest.mark.skipif(os.environ.get("DRT_RUN_REFERENCE_SCRIPT") != "1",
+                       reason="runs untrusted reference code in-process: opt in with DRT_RUN_REFERENCE_SCRIPT=1"),
+]
 
 WORDS = ["paris", "france", "capital", "tower", "river", "seine", "london", "england", "what", "is", "the",
          "of", "city", "big", "bridge"]

@@ -50,7 +50,12 @@ def _loaders(n_docs, n_q, L_p, L_q, bs):
     return _L(cbatches, ds), _L(qbatches), corpus, answers
 
 
-def test_evaluate_end_to_end_matches_oracle(dev, tmp_path):
+@pytest.mark.parametrize("layers,n_docs,n_q,k,L_p,L_q,bs", [
+    (1, 3000, 40, 50, 64, 16, 256),
+    # BASELINE config C1's shape (1k passages / 32 queries, BERT-base) at k = 1000 = every row
+    (12, 1000, 32, 1000, 128, 32, 128),
+])
+def test_evaluate_end_to_end_matches_oracle(dev, tmp_path, layers, n_docs, n_q, k, L_p, L_q, bs):
     import torch
     from transformers import BertModel
     from denseretrievaltoolkits_amd import shards
@@ -60,12 +65,13 @@ def test_evaluate_end_to_end_matches_oracle(dev, tmp_path):
     from denseretrievaltoolkits_amd.trainer.trainer import Trainer
 
     torch.manual_seed(0)
-    lm = BertModel(bw.bert_config(layers=1), add_pooling_layer=False).eval()
+    lm = BertModel(bw.bert_config(layers=layers), add_pooling_layer=False).eval()
     bw.init_model_(lm, 5)
     model = DRModel(lm_q=lm, lm_p=lm, pooling="first", normalize=True)
-    n_docs, n_q, k = 3000, 40, 50
-    cl, ql, corpus, answers = _loaders(n_docs, n_q, 64, 16, 256)
-    args = SimpleNamespace(loss_fn="SimpleContrastiveLoss", learning_rate=1e-5, optimizer="adamw", topk="1,5,20,50",
+    cl, ql, corpus, answers = _loaders(n_docs, n_q, L_p, L_q, bs)
+    topk = [1, 5, 20, k]
+    args = SimpleNamespace(loss_fn="SimpleContrastiveLoss", learning_rate=1e-5, optimizer="adamw",
+                           topk=",".join(map(str, topk)),
                            retrieve_num=k, retrieve_dir=str(tmp_path / "ret"), cache_train_dir=str(tmp_path / "cache"),
                            encode_corpus_dir=str(tmp_path / "emb"), index_order_dir=str(tmp_path / "idx"),
                            max_epochs=0, save_per_train=1, eval_per_train=1)
@@ -97,7 +103,7 @@ def test_evaluate_end_to_end_matches_oracle(dev, tmp_path):
                 s_true = float(q[qi] @ rows[g[j]])
                 assert abs(s_true - es[qi, j]) <= 1e-3, (qi, j, g[j], ei[qi, j])
             pos[qi, j] = has_answers(corpus[g[j]]["original"], answers[qi])
-    ref = get_metrics(pos, [1, 5, 20, 50])
+    ref = get_metrics(pos, topk)
     for key, v in ref.items():
         assert abs(m[key] - v / n_q) < 1e-9, (key, m[key], v / n_q)
     with open(tmp_path / "cache" / "0.0_metrics", encoding="utf-8") as f:

@@ -25,8 +25,7 @@ def main(reps=10):
         dctx = (0.1 * torch.randn(T, H, device=dev)).to(torch.bfloat16)
         dqkv = torch.empty_like(qkv)
         mask = torch.ones(B, L, dtype=torch.int64, device=dev)
-        for p, f4 in ((0.0, 0), (0.1, 0), (0.1, 1)):
-            lib.drt_attention_force4(f4)
+        for p in (0.0, 0.1):
             def fwd():
                 return lib.drt_attention_train_fwd_bf16(qkv.data_ptr(), mask.data_ptr(), ctx.data_ptr(), lse.data_ptr(),
                                                         B, L, heads, 64, 0.125, p, 123, 4, s)
@@ -43,8 +42,7 @@ def main(reps=10):
                     fn()
                 e1.record()
                 torch.cuda.synchronize()
-                res[f"B{B}_L{L}_{name}_p{p}" + ("_4w" if f4 else "")] = round(e0.elapsed_time(e1) / reps * 1e3, 1)
-        lib.drt_attention_force4(0)
+                res[f"B{B}_L{L}_{name}_p{p}"] = round(e0.elapsed_time(e1) / reps * 1e3, 1)
         fwd_bytes = T * 3 * H * 2 + T * H * 2
         bwd_bytes = T * 3 * H * 2 + 2 * T * H * 2 + T * 3 * H * 2
         res[f"B{B}_L{L}_floor_us"] = {"fwd": round(fwd_bytes / 6.3e12 * 1e6, 1), "bwd": round(bwd_bytes / 6.3e12 * 1e6, 1)}

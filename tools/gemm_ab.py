@@ -1,8 +1,7 @@
-"""Interleaved A/B of the 256^2 encoder-GEMM kernels on the encoder projection shapes with
-their production epilogues (HIP events, one process, rounds alternate the variants), plus
-torch's hipBLASLt bf16 GEMM (no epilogue) as a reference point and a bit-identity check of
-every variant's output against variant 0's.
-usage: python tools/gemm_ab.py [variants, default 0,10,11] [M, default 65536] [rounds]"""
+"""The encoder GEMMs (drt_linear_bf16 with their production epilogues) against torch's hipBLASLt
+bf16 GEMM without epilogue on the encoder projection shapes (HIP events, one process, rounds
+alternate the two).
+usage: python tools/gemm_ab.py [M, default 65536] [rounds]"""
 import json
 import os
 import sys
@@ -16,12 +15,13 @@ SHAPES = [("qkv", 2304, 768, 0, False), ("oproj", 768, 768, 0, True), ("ffn1", 3
           ("ffn2", 768, 3072, 0, True)]
 
 
-def main(variants=(0, 10, 11), M=65536, rounds=5, reps=10):
+def main(M=65536, rounds=5, reps=10):
+    variants = (0,)
     lib = _native.load()
     dev = torch.device("cuda", 0)
     s = _native.stream_ptr(dev)
     g = torch.Generator(device=dev).manual_seed(0)
-    res, same = {}, {}
+    res = {}
     for name, N, K, flags, resid in SHAPES:
         x = (torch.rand(M, K, generator=g, device=dev) * 2 - 1).to(torch.bfloat16)
         w = (0.05 * torch.randn(N, K, generator=g, device=dev)).to(torch.bfloat16)
@@ -30,15 +30,12 @@ def main(variants=(0, 10, 11), M=65536, rounds=5, reps=10):
         outs = {v: torch.empty(M, N, dtype=torch.bfloat16, device=dev) for v in variants}
 
         def call(v):
-            lib.drt_gemm_force_small(v)
             return lib.drt_linear_bf16(x.data_ptr(), w.data_ptr(), b.data_ptr(), r.data_ptr() if r is not None else None,
                                        outs[v].data_ptr(), M, N, K, flags, s)
 
         for v in variants:
             _native.check(call(v), f"{name} v{v}")
         torch.cuda.synchronize()
-        for v in variants:
-            same[f"{name}_v{v}"] = bool(torch.equal(outs[v], outs[variants[0]]))
         times = {v: [] for v in variants}
         times["torch"] = []
         for _ in range(rounds):
@@ -50,7 +47,6 @@ def main(variants=(0, 10, 11), M=65536, rounds=5, reps=10):
                         y = x @ w.T
                     e1.record()
                 else:
-                    lib.drt_gemm_force_small(v)
                     e0.record()
                     for _ in range(reps):
                         call(v)
@@ -61,12 +57,10 @@ def main(variants=(0, 10, 11), M=65536, rounds=5, reps=10):
             ts = sorted(ts)
             ms = ts[len(ts) // 2]
             res[f"{name}_{v}"] = {"us": round(ms * 1e3, 1), "tflops": round(2 * M * N * K / ms / 1e9, 1)}
-    lib.drt_gemm_force_small(0)
-    print(json.dumps({"M": M, "gemm": res, "bit_identical_to_first": same}))
+    print(json.dumps({"M": M, "gemm": res}))
 
 
 if __name__ == "__main__":
-    vs = tuple(int(v) for v in sys.argv[1].split(",")) if len(sys.argv) > 1 else (0, 10, 11)
-    M = int(sys.argv[2]) if len(sys.argv) > 2 else 65536
-    rounds = int(sys.argv[3]) if len(sys.argv) > 3 else 5
-    main(vs, M, rounds)
+    M = int(sys.argv[1]) if len(sys.argv) > 1 else 65536
+    rounds = int(sys.argv[2]) if len(sys.argv) > 2 else 5
+    main(M, rounds)

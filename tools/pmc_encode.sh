@@ -9,7 +9,7 @@ mkdir -p $OUT
 export TMPDIR=/tmp
 cd /tmp
 timeout -s KILL 120 rocprofv3 --kernel-trace --pmc SQ_VALU_MFMA_BUSY_CYCLES GRBM_GUI_ACTIVE SQ_BUSY_CYCLES --output-format csv \
-  -d $OUT -o run -- python3 -c "import sys, json, torch; sys.path.insert(0, '$R'); from denseretrievaltoolkits_amd import bench_encode; print(json.dumps(bench_encode.run(torch.device('cuda', 0), steps=2, warmup=1)))" \
+  -d $OUT -o run -- python3 -c "import sys, json, torch; sys.path.insert(0, '$R'); import bench_legs as bench_encode; print(json.dumps(bench_encode.run(torch.device('cuda', 0), steps=2, warmup=1)))" \
   > $OUT/run.log 2>&1
 rc=$?
 echo "pmc rc=$rc"

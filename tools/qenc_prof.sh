@@ -6,7 +6,7 @@ export TMPDIR=/tmp
 mkdir -p $R/gpurun_out
 cd /tmp
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $R/gpurun_out/prof_qenc -o run --output-format csv -- \
-  python3 -c "import sys, json, torch; sys.path.insert(0, '$R'); from denseretrievaltoolkits_amd import bench_encode; print(json.dumps(bench_encode.run_query_encode(torch.device('cuda', 0))))" \
+  python3 -c "import sys, json, torch; sys.path.insert(0, '$R'); import bench_legs as bench_encode; print(json.dumps(bench_encode.run_query_encode(torch.device('cuda', 0))))" \
   > $R/gpurun_out/prof_qenc.log 2>&1
 rc=$?
 tail -1 $R/gpurun_out/prof_qenc.log

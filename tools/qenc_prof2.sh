@@ -7,7 +7,7 @@ mkdir -p $R/gpurun_out
 cd /tmp
 for B in 8 128; do
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $R/gpurun_out/prof_q$B -o run --output-format csv -- \
-  python3 -c "import sys, json, torch; sys.path.insert(0, '$R'); from denseretrievaltoolkits_amd import bench_encode; print(json.dumps(bench_encode.run_query_encode(torch.device('cuda', 0), batches=($B,), steps=20)))" \
+  python3 -c "import sys, json, torch; sys.path.insert(0, '$R'); import bench_legs as bench_encode; print(json.dumps(bench_encode.run_query_encode(torch.device('cuda', 0), batches=($B,), steps=20)))" \
   > $R/gpurun_out/prof_q$B.log 2>&1 || exit $?
 tail -1 $R/gpurun_out/prof_q$B.log
 python3 - <<PY

@@ -7,7 +7,7 @@ import sys
 import torch
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
-from denseretrievaltoolkits_amd import bench_encode  # noqa: E402
+import bench_legs as bench_encode  # noqa: E402
 
 dev = torch.device("cuda", 0)
 print(json.dumps(bench_encode.run_train_step(dev)), flush=True)

@@ -6,7 +6,7 @@ export TMPDIR=/tmp
 mkdir -p $R/gpurun_out
 cd /tmp
 timeout -k 10 400 rocprofv3 --kernel-trace --stats -d $R/gpurun_out/prof_train -o run --output-format csv -- \
-  python3 -c "import sys, json, torch; sys.path.insert(0, '$R'); from denseretrievaltoolkits_amd import bench_encode; print(json.dumps(bench_encode.run_train_step(torch.device('cuda', 0))))" \
+  python3 -c "import sys, json, torch; sys.path.insert(0, '$R'); import bench_legs as bench_encode; print(json.dumps(bench_encode.run_train_step(torch.device('cuda', 0))))" \
   > $R/gpurun_out/prof_train.log 2>&1
 rc=$?
 tail -1 $R/gpurun_out/prof_train.log
