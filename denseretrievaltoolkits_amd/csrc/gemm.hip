@@ -96,6 +96,28 @@ __device__ __forceinline__ float gelu_fast(float x) {
   return 0.5f * x * (1.0f + erf_v);
 }
 
+// gelu_fast on two elements with packed fp32 math (v_pk_mul_f32 / v_pk_fma_f32: half the
+// VALU issue of two scalar calls; the transcendentals stay per element).  The same A&S
+// polynomial; 0.5 x (1 + sign(x) erf|.|) is evaluated as 0.5 x + 0.5 |x| erf|.| (one fma).
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ f32x2 gelu_fast2(f32x2 x) {
+  f32x2 z = {fabsf(x.x), fabsf(x.y)};
+  z = z * 0.70710678118654752f;
+  const f32x2 d = z * 0.3275911f + 1.0f;
+  const f32x2 t = {__builtin_amdgcn_rcpf(d.x), __builtin_amdgcn_rcpf(d.y)};
+  f32x2 p = t * 1.061405429f - 1.453152027f;
+  p = p * t + 1.421413741f;
+  p = p * t - 0.284496736f;
+  p = p * t + 0.254829592f;
+  p = p * t;
+  const f32x2 ar = -(z * z) * 1.4426950408889634f;
+  const f32x2 e = {__builtin_amdgcn_exp2f(ar.x), __builtin_amdgcn_exp2f(ar.y)};
+  const f32x2 ea = 1.0f - p * e;
+  const f32x2 hx = x * 0.5f;
+  const f32x2 ha = {fabsf(hx.x), fabsf(hx.y)};
+  return hx + ha * ea;
+}
+
 // EPI_DGELU: multiply by GELU'(R) (the dgrad of a GELU input: R = the bf16 pre-activation);
 // EPI_PRE: also store the pre-activation to C2 (the training forward keeps it for the backward);
 // EPI_DROP: dropout (counter hash of the flat output index, the mask drt_dropout_add_bf16 draws)
@@ -595,10 +617,11 @@ __device__ __forceinline__ void pp_epilogue_lds(const GemmArgs& a, f32x4 (&acc)[
         for (int j = 0; j < 4; ++j) {
           bf16x4 o;
 #pragma unroll
-          for (int u = 0; u < 4; ++u) {
-            float x = acc[i][j][u] * a.alpha + bv[j][u];
-            if ((EPI & EPI_GELU) && act) x = gelu_fast(x);
-            o[u] = (__bf16)x;
+          for (int u = 0; u < 4; u += 2) {   // element pairs: the GELU on packed fp32 math
+            f32x2 x = {acc[i][j][u] * a.alpha + bv[j][u], acc[i][j][u + 1] * a.alpha + bv[j][u + 1]};
+            if ((EPI & EPI_GELU) && act) x = gelu_fast2(x);
+            o[u] = (__bf16)x.x;
+            o[u + 1] = (__bf16)x.y;
           }
           const int chunk = (2 * j + (fc >> 1)) ^ (r & 7);
           *(bf16x4*)(lds_wave + r * 128 + chunk * 16 + (fc & 1) * 8) = o;

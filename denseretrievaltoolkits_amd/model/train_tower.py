@@ -2,8 +2,9 @@
 
 The reference differentiates HF ``BertModel`` under autograd in every training step
 (DRT/trainer/trainer.py:113-133 -> DRModel.forward, DRT/model/biencoder.py:88-125).  Here one
-``torch.autograd.Function`` runs the whole tower: the forward on the inference kernels plus the
-activations the backward needs (bf16: layer input, qkv, ctx, attention LSE, pre-LN sums,
+``torch.autograd.Function`` per BertLayer (plus one for the embeddings) runs the tower, so each
+layer's parameter gradients reach autograd -- and DDP's bucketed all-reduce -- as soon as that
+layer's backward is done: the forward on the inference kernels plus the activations the backward needs (bf16: layer input, qkv, ctx, attention LSE, pre-LN sums,
 post-LN1, FFN pre-/post-activation), and the backward entirely on HIP kernels:
 
     LN2 bwd -> FFN2 linear bwd -> GELU bwd -> FFN1 linear bwd (+ dx2 residual in the dgrad
@@ -129,152 +130,198 @@ def dropout_sites(layer: int):
     return 4 * layer + 1, 4 * layer + 2, 4 * layer + 3
 
 
-def tower_forward(model, W: _Weights, ids: torch.Tensor, mask: Optional[torch.Tensor], drop=(0.0, 0.0, 0)):
-    """last_hidden_state bf16 [B, L, H] and the saved activations; drop = (hidden p, attention p, seed)."""
+class _Step:
+    """What every node of one tower pass shares: weights, shape, masks' inputs, dropout."""
+
+    def __init__(self, model, W: _Weights, ids, mask, drop):
+        cfg = model.config
+        self.model, self.W, self.ids, self.mask, self.drop = model, W, ids, mask, drop
+        self.B, self.L = ids.shape
+        self.H, self.heads, self.eps = cfg.hidden_size, cfg.num_attention_heads, float(cfg.layer_norm_eps)
+        self.scale = 1.0 / (self.H // self.heads) ** 0.5
+        self.dev = ids.device
+
+
+def embed_forward(st: _Step):
+    """h0 = dropout(LN(word + pos + type)) bf16 [T, H] and the pre-LN sum the backward needs."""
     lib = _native.load()
-    dev = ids.device
-    s = _native.stream_ptr(dev)
-    cfg = model.config
-    B, L = ids.shape
-    if L > MAX_TRAIN_SEQ:
-        raise ValueError(f"HIP training tower: sequence length {L} > {MAX_TRAIN_SEQ}")
-    H, heads, eps = cfg.hidden_size, cfg.num_attention_heads, float(cfg.layer_norm_eps)
-    T = B * L
-    h = torch.empty((T, H), dtype=torch.bfloat16, device=dev)
+    s = _native.stream_ptr(st.dev)
+    W = st.W
+    T = st.B * st.L
+    h = torch.empty((T, st.H), dtype=torch.bfloat16, device=st.dev)
     emb_pre = torch.empty_like(h)
-    _native.check(lib.drt_embed_ln_pre(ids.data_ptr(), None, B, L, W.word.data_ptr(), W.pos.data_ptr(),
-                                       W.type.data_ptr(), W.emb_g.data_ptr(), W.emb_b.data_ptr(), eps, H,
+    _native.check(lib.drt_embed_ln_pre(st.ids.data_ptr(), None, st.B, st.L, W.word.data_ptr(), W.pos.data_ptr(),
+                                       W.type.data_ptr(), W.emb_g.data_ptr(), W.emb_b.data_ptr(), st.eps, st.H,
                                        h.data_ptr(), emb_pre.data_ptr(), s), "drt_embed_ln_pre")
-    ph, pa, seed = drop
+    ph, _, seed = st.drop
     if ph > 0:
         h = _dropout(lib, h, ph, seed, 0, s)
-    saved = []
-    scale = 1.0 / (H // heads) ** 0.5
-    for i, ly in enumerate(W.layers):
-        s_att, s_out1, s_out2 = dropout_sites(i)
-        qkv = _lin(lib, h, ly["wqkv"], ly["bqkv"], torch.empty((T, 3 * H), dtype=torch.bfloat16, device=dev),
-                   stream=s)
-        ctx = torch.empty((T, H), dtype=torch.bfloat16, device=dev)
-        lse = torch.empty((B, heads, L), dtype=torch.float32, device=dev)
-        _native.check(lib.drt_attention_train_fwd_bf16(qkv.data_ptr(), _ptr(mask), ctx.data_ptr(), lse.data_ptr(),
-                                                       B, L, heads, H // heads, scale, float(pa), seed, s_att, s),
-                      "drt_attention_train_fwd_bf16")
-        # x1 = dropout(ctx Wo^T + bo) + h, dropout in the GEMM epilogue
-        x1 = _lin(lib, ctx, ly["wo"], ly["bo"], torch.empty_like(h), resid=h, stream=s,
-                  drop=(ph, seed, s_out1) if ph > 0 else None)
-        h1 = _layernorm(lib, x1, ly["g1"], ly["b1"], eps, s)
-        # f = GELU(fpre), fpre = h1 Wi^T + bi: both from the one GEMM epilogue
-        fpre = torch.empty((T, ly["wi"].shape[0]), dtype=torch.bfloat16, device=dev)
-        f = _lin(lib, h1, ly["wi"], ly["bi"], torch.empty_like(fpre), gelu=True, stream=s, pre_out=fpre)
-        # x2 = dropout(f Wf^T + bf) + h1
-        x2 = _lin(lib, f, ly["wf"], ly["bf"], torch.empty_like(h), resid=h1, stream=s,
-                  drop=(ph, seed, s_out2) if ph > 0 else None)
-        saved.append((h, qkv, ctx, lse, x1, h1, fpre, f, x2))
-        h = _layernorm(lib, x2, ly["g2"], ly["b2"], eps, s)
-    return h.view(B, L, H), (emb_pre, saved)
+    return h, emb_pre
 
 
-def tower_backward(model, W: _Weights, ids, mask, saved, d_hidden: torch.Tensor, drop=(0.0, 0.0, 0)
-                   ) -> Dict[str, torch.Tensor]:
-    """fp32 gradients of every tower parameter (HF names) for d last_hidden_state."""
+def embed_backward(st: _Step, emb_pre, d) -> Dict[str, torch.Tensor]:
     lib = _native.load()
-    dev = ids.device
-    s = _native.stream_ptr(dev)
-    cfg = model.config
-    B, L = ids.shape
-    H, heads, eps = cfg.hidden_size, cfg.num_attention_heads, float(cfg.layer_norm_eps)
-    scale = 1.0 / (H // heads) ** 0.5
-    emb_pre, layers = saved
-    ph, pa, seed = drop
-    d = d_hidden.reshape(B * L, H).to(torch.bfloat16).contiguous()
-    grads: Dict[str, torch.Tensor] = {}
-    for i in reversed(range(len(layers))):
-        h, qkv, ctx, lse, x1, h1, fpre, f, x2 = layers[i]
-        ly = W.layers[i]
-        p = f"encoder.layer.{i}."
-        s_att, s_out1, s_out2 = dropout_sites(i)
-        # LN backward also emits the dropped gradient entering FFN2; FFN2's dgrad applies the GELU
-        # backward in its epilogue (-> d fpre)
-        if ph > 0:
-            dx2, dg2, db2, dy2 = layernorm_backward(d, x2, ly["g2"], eps, drop=(ph, seed, s_out2))
-        else:
-            dx2, dg2, db2 = layernorm_backward(d, x2, ly["g2"], eps)
-            dy2 = dx2
-        dfpre, dwf, dbf = linear_backward(dy2, f, ly["wf_t"], gelu_pre=fpre)
-        dh1, dwi, dbi = linear_backward(dfpre, h1, ly["wi_t"], resid=dx2)
-        if ph > 0:
-            dx1, dg1, db1, dy1 = layernorm_backward(dh1, x1, ly["g1"], eps, drop=(ph, seed, s_out1))
-        else:
-            dx1, dg1, db1 = layernorm_backward(dh1, x1, ly["g1"], eps)
-            dy1 = dx1
-        dctx, dwo, dbo = linear_backward(dy1, ctx, ly["wo_t"])
-        dqkv = torch.empty_like(qkv)
-        _native.check(lib.drt_attention_train_bwd_bf16(qkv.data_ptr(), ctx.data_ptr(), dctx.data_ptr(),
-                                                       lse.data_ptr(), _ptr(mask), dqkv.data_ptr(), B, L, heads,
-                                                       H // heads, scale, float(pa), seed, s_att, s),
-                      "drt_attention_train_bwd_bf16")
-        d, dwqkv, dbqkv = linear_backward(dqkv, h, ly["wqkv_t"], resid=dx1)
-        grads[p + "output.LayerNorm.weight"], grads[p + "output.LayerNorm.bias"] = dg2, db2
-        grads[p + "output.dense.weight"], grads[p + "output.dense.bias"] = dwf, dbf
-        grads[p + "intermediate.dense.weight"], grads[p + "intermediate.dense.bias"] = dwi, dbi
-        grads[p + "attention.output.LayerNorm.weight"], grads[p + "attention.output.LayerNorm.bias"] = dg1, db1
-        grads[p + "attention.output.dense.weight"], grads[p + "attention.output.dense.bias"] = dwo, dbo
-        for j, n in enumerate(("query", "key", "value")):
-            grads[p + f"attention.self.{n}.weight"] = dwqkv[j * H:(j + 1) * H]
-            grads[p + f"attention.self.{n}.bias"] = dbqkv[j * H:(j + 1) * H]
+    s = _native.stream_ptr(st.dev)
+    W = st.W
+    ph, _, seed = st.drop
     if ph > 0:
         d = _dropout(lib, d, ph, seed, 0, s)
-    demb, dge, dbe = layernorm_backward(d, emb_pre, W.emb_g, eps)
-    e = "embeddings."
+    demb, dge, dbe = layernorm_backward(d, emb_pre, W.emb_g, st.eps)
     dword = torch.zeros_like(W.word)
     dpos = torch.zeros_like(W.pos)
     dtype = torch.zeros_like(W.type)
-    pad = model.embeddings.word_embeddings.padding_idx
-    _native.check(lib.drt_embedding_bwd(ids.data_ptr(), None, demb.data_ptr(), B, L, H,
+    pad = st.model.embeddings.word_embeddings.padding_idx
+    _native.check(lib.drt_embedding_bwd(st.ids.data_ptr(), None, demb.data_ptr(), st.B, st.L, st.H,
                                         -1 if pad is None else int(pad), dword.data_ptr(), dpos.data_ptr(),
                                         dtype.data_ptr(), s), "drt_embedding_bwd")
-    grads[e + "word_embeddings.weight"] = dword
-    grads[e + "position_embeddings.weight"] = dpos
-    grads[e + "token_type_embeddings.weight"] = dtype
-    grads[e + "LayerNorm.weight"], grads[e + "LayerNorm.bias"] = dge, dbe
-    return grads
+    e = "embeddings."
+    return {e + "word_embeddings.weight": dword, e + "position_embeddings.weight": dpos,
+            e + "token_type_embeddings.weight": dtype, e + "LayerNorm.weight": dge, e + "LayerNorm.bias": dbe}
 
 
-class _TowerFn(torch.autograd.Function):
+def layer_forward(st: _Step, i: int, h):
+    """One BertLayer (train-mode dropout as HF) -> (h_out, saved activations)."""
+    lib = _native.load()
+    dev = st.dev
+    s = _native.stream_ptr(dev)
+    ly = st.W.layers[i]
+    B, L, H, heads = st.B, st.L, st.H, st.heads
+    T = B * L
+    ph, pa, seed = st.drop
+    s_att, s_out1, s_out2 = dropout_sites(i)
+    qkv = _lin(lib, h, ly["wqkv"], ly["bqkv"], torch.empty((T, 3 * H), dtype=torch.bfloat16, device=dev), stream=s)
+    ctx = torch.empty((T, H), dtype=torch.bfloat16, device=dev)
+    lse = torch.empty((B, heads, L), dtype=torch.float32, device=dev)
+    _native.check(lib.drt_attention_train_fwd_bf16(qkv.data_ptr(), _ptr(st.mask), ctx.data_ptr(), lse.data_ptr(),
+                                                   B, L, heads, H // heads, st.scale, float(pa), seed, s_att, s),
+                  "drt_attention_train_fwd_bf16")
+    # x1 = dropout(ctx Wo^T + bo) + h, dropout in the GEMM epilogue
+    x1 = _lin(lib, ctx, ly["wo"], ly["bo"], torch.empty_like(h), resid=h, stream=s,
+              drop=(ph, seed, s_out1) if ph > 0 else None)
+    h1 = _layernorm(lib, x1, ly["g1"], ly["b1"], st.eps, s)
+    # f = GELU(fpre), fpre = h1 Wi^T + bi: both from the one GEMM epilogue
+    fpre = torch.empty((T, ly["wi"].shape[0]), dtype=torch.bfloat16, device=dev)
+    f = _lin(lib, h1, ly["wi"], ly["bi"], torch.empty_like(fpre), gelu=True, stream=s, pre_out=fpre)
+    # x2 = dropout(f Wf^T + bf) + h1
+    x2 = _lin(lib, f, ly["wf"], ly["bf"], torch.empty_like(h), resid=h1, stream=s,
+              drop=(ph, seed, s_out2) if ph > 0 else None)
+    h2 = _layernorm(lib, x2, ly["g2"], ly["b2"], st.eps, s)
+    return h2, (h, qkv, ctx, lse, x1, h1, fpre, f, x2)
+
+
+def layer_backward(st: _Step, i: int, saved, d) -> Tuple[torch.Tensor, Dict[str, torch.Tensor]]:
+    """d h_in and the fp32 gradients of layer i's parameters (HF names) for d h_out."""
+    lib = _native.load()
+    s = _native.stream_ptr(st.dev)
+    h, qkv, ctx, lse, x1, h1, fpre, f, x2 = saved
+    ly = st.W.layers[i]
+    H, heads, eps = st.H, st.heads, st.eps
+    ph, pa, seed = st.drop
+    p = f"encoder.layer.{i}."
+    s_att, s_out1, s_out2 = dropout_sites(i)
+    # LN backward also emits the dropped gradient entering FFN2; FFN2's dgrad applies the GELU
+    # backward in its epilogue (-> d fpre)
+    if ph > 0:
+        dx2, dg2, db2, dy2 = layernorm_backward(d, x2, ly["g2"], eps, drop=(ph, seed, s_out2))
+    else:
+        dx2, dg2, db2 = layernorm_backward(d, x2, ly["g2"], eps)
+        dy2 = dx2
+    dfpre, dwf, dbf = linear_backward(dy2, f, ly["wf_t"], gelu_pre=fpre)
+    dh1, dwi, dbi = linear_backward(dfpre, h1, ly["wi_t"], resid=dx2)
+    if ph > 0:
+        dx1, dg1, db1, dy1 = layernorm_backward(dh1, x1, ly["g1"], eps, drop=(ph, seed, s_out1))
+    else:
+        dx1, dg1, db1 = layernorm_backward(dh1, x1, ly["g1"], eps)
+        dy1 = dx1
+    dctx, dwo, dbo = linear_backward(dy1, ctx, ly["wo_t"])
+    dqkv = torch.empty_like(qkv)
+    _native.check(lib.drt_attention_train_bwd_bf16(qkv.data_ptr(), ctx.data_ptr(), dctx.data_ptr(),
+                                                   lse.data_ptr(), _ptr(st.mask), dqkv.data_ptr(), st.B, st.L, heads,
+                                                   H // heads, st.scale, float(pa), seed, s_att, s),
+                  "drt_attention_train_bwd_bf16")
+    d_in, dwqkv, dbqkv = linear_backward(dqkv, h, ly["wqkv_t"], resid=dx1)
+    grads = {}
+    grads[p + "output.LayerNorm.weight"], grads[p + "output.LayerNorm.bias"] = dg2, db2
+    grads[p + "output.dense.weight"], grads[p + "output.dense.bias"] = dwf, dbf
+    grads[p + "intermediate.dense.weight"], grads[p + "intermediate.dense.bias"] = dwi, dbi
+    grads[p + "attention.output.LayerNorm.weight"], grads[p + "attention.output.LayerNorm.bias"] = dg1, db1
+    grads[p + "attention.output.dense.weight"], grads[p + "attention.output.dense.bias"] = dwo, dbo
+    for j, n in enumerate(("query", "key", "value")):
+        grads[p + f"attention.self.{n}.weight"] = dwqkv[j * H:(j + 1) * H]
+        grads[p + f"attention.self.{n}.bias"] = dbqkv[j * H:(j + 1) * H]
+    return d_in, grads
+
+
+# One autograd node per BertLayer (and one for the embeddings): each node's parameter gradients
+# are handed to autograd (AccumulateGrad, so DDP's bucket hooks) as soon as THAT layer's backward
+# is done, and DDP's gradient all-reduce of layer i overlaps the backward of layers i-1 .. 0
+# (trainer.py:47-63 wraps the model in DDP).  The activation between nodes is the bf16 hidden
+# state; all nodes of one pass share a _Step (weights snapshot, ids, mask, dropout seed).
+def _grads_out(names, grads):
+    return tuple(grads[n].to(torch.float32) if n in grads else None for n in names)
+
+
+class _EmbedFn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, ids, mask, model, drop, *params):
-        W = _Weights(model, ids.device)
-        hidden, saved = tower_forward(model, W, ids, mask, drop)
-        ctx.model, ctx.W, ctx.saved_acts, ctx.drop = model, W, saved, drop
-        ctx.ids, ctx.mask = ids, mask
-        ctx.param_names = [n for n, _ in model.named_parameters()]
-        return hidden.float()
+    def forward(ctx, ids, st, names, *params):
+        h, emb_pre = embed_forward(st)
+        ctx.st, ctx.emb_pre, ctx.names = st, emb_pre, names
+        return h
 
     @staticmethod
-    def backward(ctx, d_hidden):
-        grads = tower_backward(ctx.model, ctx.W, ctx.ids, ctx.mask, ctx.saved_acts, d_hidden.contiguous(), ctx.drop)
-        out: List[Optional[torch.Tensor]] = [None, None, None, None]
-        for n in ctx.param_names:
-            g = grads.get(n)
-            out.append(g.to(torch.float32) if g is not None else None)
+    def backward(ctx, d):
+        grads = embed_backward(ctx.st, ctx.emb_pre, d.contiguous())
+        ctx.emb_pre = None
+        return (None, None, None) + _grads_out(ctx.names, grads)
+
+
+class _LayerFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, h, st, i, names, *params):
+        h2, saved = layer_forward(st, i, h)
+        ctx.st, ctx.i, ctx.saved_acts, ctx.names = st, i, saved, names
+        return h2
+
+    @staticmethod
+    def backward(ctx, d):
+        d_in, grads = layer_backward(ctx.st, ctx.i, ctx.saved_acts, d.contiguous())
         ctx.saved_acts = None
-        return tuple(out)
+        return (d_in, None, None, None) + _grads_out(ctx.names, grads)
+
+
+def _param_groups(model):
+    """(embedding names/params, [per-layer names/params]) in the HF naming."""
+    named = dict(model.named_parameters())
+    emb = [n for n in named if n.startswith("embeddings.")]
+    layers = []
+    for i in range(model.config.num_hidden_layers):
+        pre = f"encoder.layer.{i}."
+        layers.append([n for n in named if n.startswith(pre)])
+    return named, emb, layers
 
 
 def train_hidden(model, input_ids: torch.Tensor, attention_mask: Optional[torch.Tensor],
                  seed: Optional[int] = None) -> torch.Tensor:
-    """last_hidden_state fp32 [B, L, H] of ``model`` with the HIP tower backward attached.
-    Dropout follows ``model.training`` and the config's probabilities (seed: torch CPU RNG)."""
+    """last_hidden_state fp32 [B, L, H] of ``model`` with the HIP tower backward attached (one autograd
+    node per layer).  Dropout follows ``model.training`` and the config's probabilities (seed: torch
+    CPU RNG)."""
     why = tower_supported(model)
     if why is not None:
         raise NotImplementedError(f"HIP training tower: {why}")
     dev = next(model.parameters()).device
     ids = input_ids.to(dev, torch.int64).contiguous()
     mask = attention_mask.to(dev, torch.int64).contiguous() if attention_mask is not None else None
-    params = [p for _, p in model.named_parameters()]
+    B, L = ids.shape
+    if L > MAX_TRAIN_SEQ:
+        raise ValueError(f"HIP training tower: sequence length {L} > {MAX_TRAIN_SEQ}")
     cfg = model.config
     ph = float(cfg.hidden_dropout_prob) if model.training else 0.0
     pa = float(cfg.attention_probs_dropout_prob) if model.training else 0.0
     if seed is None:
         seed = int(torch.randint(0, 2 ** 62, (1,)).item()) if (ph > 0 or pa > 0) else 0
-    return _TowerFn.apply(ids, mask, model, (ph, pa, seed), *params)
+    st = _Step(model, _Weights(model, dev), ids, mask, (ph, pa, seed))
+    named, emb, layers = _param_groups(model)
+    h = _EmbedFn.apply(ids, st, emb, *[named[n] for n in emb])
+    for i, names in enumerate(layers):
+        h = _LayerFn.apply(h, st, i, names, *[named[n] for n in names])
+    return h.view(B, L, cfg.hidden_size).float()
