@@ -80,6 +80,10 @@ _SIGNATURES = [
     ("drt_attention_train_bwd_bf16", c_i32, [c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_i64, c_i64, c_i32, c_i32, c_f32,
                                              c_f32, ctypes.c_uint64, ctypes.c_uint64, c_vp]),
     ("drt_dropout_add_bf16", c_i32, [c_vp, c_vp, c_i64, c_f32, ctypes.c_uint64, ctypes.c_uint64, c_vp, c_vp]),
+    ("drt_attention_train_fwd_bits_bf16", c_i32, [c_vp, c_vp, c_vp, c_vp, c_vp, c_i64, c_i64, c_i32, c_i32, c_f32,
+                                                  c_f32, c_u64, c_u64, c_vp]),
+    ("drt_attention_train_bwd_bits_bf16", c_i32, [c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_i64, c_i64, c_i32,
+                                                  c_i32, c_f32, c_f32, c_u64, c_u64, c_vp]),
     ("drt_attention_bwd_bf16", c_i32, [c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_i64, c_i64, c_i32, c_i32, c_f32, c_vp]),
     ("drt_layernorm_bf16", c_i32, [c_vp, c_i64, c_i32, c_vp, c_vp, c_f32, c_vp, c_vp]),
     ("drt_attention_bf16", c_i32, [c_vp, c_vp, c_vp, c_i64, c_i64, c_i32, c_i32, c_f32, c_vp]),

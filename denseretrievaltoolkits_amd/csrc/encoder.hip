@@ -172,6 +172,8 @@ struct AttnArgs {
                           // scores (what the attention backward needs to rebuild P)
   float drop_p;           // training: dropout of the attention probabilities (DROP kernels)
   uint64_t seed, site;    //   mask = drop_hash24(seed, site, ((b * heads + head) * L + q) * L + key)
+  uint32_t* drop_bits;    // optional [B][heads][L][ceil(L / 32)]: the keep mask, bit (key & 31) of word
+                          //   (query, key >> 5) -- the backward reads it instead of re-hashing
 };
 
 // NW = waves per work-group (the launcher uses 4; an 8-wave form for 5-8 query blocks measured
@@ -302,11 +304,18 @@ __global__ __launch_bounds__(NW * 64, NW == 4 ? 4 : 2) void attention_kernel(Att
         const uint32_t thr = drop_threshold(a.drop_p);
         const int qq = qb * 32 + r;
         const uint64_t base = (((uint64_t)b * a.heads + hd) * L + qq) * (uint64_t)L;
+        uint32_t m16 = 0;
 #pragma unroll
         for (int e = 0; e < 16; ++e) {
-          const int key = kt + (e & 3) + 8 * (e >> 2) + 4 * h;
+          const int kr = (e & 3) + 8 * (e >> 2) + 4 * h;
+          const int key = kt + kr;
           const bool keep = key < L && drop_hash24(a.seed, a.site, base + key) >= thr;
+          m16 |= keep ? 1u << kr : 0u;
           s[e] = keep ? s[e] * inv : 0.0f;
+        }
+        if (a.drop_bits) {   // this query's 32 keep bits of the key tile: the two lane halves' 16 each
+          const uint32_t word = m16 | __shfl_xor(m16, 32, 64);
+          if (h == 0 && qq < L) a.drop_bits[(((int64_t)b * a.heads + hd) * L + qq) * (Lp / 32) + kt / 32] = word;
         }
       }
 #pragma unroll
@@ -524,14 +533,29 @@ int drt_attention_fwd_lse_bf16(const void* qkv, const int64_t* mask, void* ctx, 
   return drt_attention_train_fwd_bf16(qkv, mask, ctx, lse, B, L, heads, head_dim, scale, 0.0f, 0, 0, stream);
 }
 
+int drt_attention_train_fwd_bits_bf16(const void* qkv, const int64_t* mask, void* ctx, float* lse,
+                                      uint32_t* drop_bits, int64_t B, int64_t L, int32_t heads, int32_t head_dim,
+                                      float scale, float drop_p, uint64_t seed, uint64_t site, void* stream);
+
 int drt_attention_train_fwd_bf16(const void* qkv, const int64_t* mask, void* ctx, float* lse, int64_t B, int64_t L,
                                  int32_t heads, int32_t head_dim, float scale, float drop_p, uint64_t seed,
                                  uint64_t site, void* stream) {
+  return drt_attention_train_fwd_bits_bf16(qkv, mask, ctx, lse, nullptr, B, L, heads, head_dim, scale, drop_p, seed,
+                                           site, stream);
+}
+
+// The training forward that also writes the attention-dropout keep mask as bits (drop_bits, when
+// drop_p > 0 and drop_bits != NULL): [B][heads][L][ceil(L / 32)] u32, bit (key & 31) of word
+// (query, key >> 5); drt_attention_train_bwd_bits_bf16 reads it instead of regenerating the hash.
+int drt_attention_train_fwd_bits_bf16(const void* qkv, const int64_t* mask, void* ctx, float* lse,
+                                      uint32_t* drop_bits, int64_t B, int64_t L, int32_t heads, int32_t head_dim,
+                                      float scale, float drop_p, uint64_t seed, uint64_t site, void* stream) {
   DRT_REQUIRE(B >= 0 && L > 0 && L <= kMaxSeq && heads > 0 && head_dim == kHeadDim);
   DRT_REQUIRE(drop_p >= 0.0f && drop_p < 1.0f);
   if (B == 0) return DRT_OK;
   DRT_REQUIRE(qkv && ctx);
-  AttnArgs a{(const __bf16*)qkv, mask, (__bf16*)ctx, B, L, heads, heads * head_dim, scale, lse, drop_p, seed, site};
+  AttnArgs a{(const __bf16*)qkv, mask, (__bf16*)ctx, B, L, heads, heads * head_dim, scale, lse, drop_p, seed, site,
+             drop_bits};
   const int Lp = ((int)L + 31) & ~31;
   const size_t lds = (size_t)Lp * 128 + (size_t)64 * (Lp * 2 + 8) + (size_t)Lp * 4;
   static bool attr_set = false;

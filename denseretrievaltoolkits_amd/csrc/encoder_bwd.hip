@@ -262,6 +262,8 @@ struct AttnBwdArgs {
   float scale;
   float drop_p;           // attention-probability dropout of the forward (0: none)
   uint64_t seed, site;
+  const uint32_t* drop_bits;  // optional keep bits written by the forward ([B][heads][L][ceil(L/32)]);
+                              // NULL: the masks are regenerated from the hash
 };
 
 __device__ __forceinline__ int ab_rc(int row, int chunk) { return row * kAbRow + ((chunk ^ ((row >> 1) & 7)) << 4); }
@@ -305,6 +307,7 @@ __global__ __launch_bounds__(NW * 64, NW == 4 ? 2 : 1) void attention_bwd_kernel
   float* lse = (float*)(scr + NW * 32 * kAbScr);     // [Lp]
   float* dv = lse + Lp;                              // [Lp]  Dv
   float* kb = dv + Lp;                               // [Lp]  key bias
+  uint32_t* kbits = (uint32_t*)(kb + Lp);            // [Lp / 32][Lp] keep bits (drop_bits staged)
 
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
   const int r = lane & 31, h = lane >> 5;
@@ -371,6 +374,15 @@ __global__ __launch_bounds__(NW * 64, NW == 4 ? 2 : 1) void attention_bwd_kernel
     kb[i] = bv;
     lse[i] = i < L ? a.lse[((int64_t)b * a.heads + hd) * a.L + i] : 0.0f;
   }
+  const bool bits = a.drop_bits != nullptr && a.drop_p > 0.0f;
+  if (bits) {   // [query][key block] words of the forward -> [key block][query] (both phases read rows)
+    const int nkb = Lp / 32;
+    const uint32_t* src = a.drop_bits + ((int64_t)b * a.heads + hd) * a.L * nkb;
+    for (int i = tid; i < nkb * Lp; i += NT) {
+      const int q = i / nkb, kbi = i - q * nkb;
+      kbits[kbi * Lp + q] = q < L ? src[(int64_t)q * nkb + kbi] : 0u;
+    }
+  }
   __syncthreads();
 
   const int nblk = Lp / 32;
@@ -412,6 +424,7 @@ __global__ __launch_bounds__(NW * 64, NW == 4 ? 2 : 1) void attention_bwd_kernel
       // O = Pd V where Pd = mask P / (1 - p): dV takes Pd, and dS = P (mask dPd / (1 - p) - Dv)
       const float lq = lse[qcol], dq = dv[qcol];
       const uint64_t dbase = (((uint64_t)b * a.heads + hd) * L + qcol) * (uint64_t)L;
+      const uint32_t wbits = bits ? kbits[kbk * Lp + qcol] : 0u;
       float ds[16];
 #pragma unroll
       for (int e = 0; e < 16; ++e) {
@@ -420,7 +433,8 @@ __global__ __launch_bounds__(NW * 64, NW == 4 ? 2 : 1) void attention_bwd_kernel
         float pd = p, dpe = dpt[e];
         if (drop) {
           const int key = kbk * 32 + kr;
-          const bool keep = key < L && qcol < L && drop_hash24(a.seed, a.site, dbase + key) >= thr;
+          const bool keep = bits ? ((wbits >> kr) & 1u) != 0u
+                                 : key < L && qcol < L && drop_hash24(a.seed, a.site, dbase + key) >= thr;
           pd = keep ? p * inv : 0.f;
           dpe = keep ? dpe * inv : 0.f;
         }
@@ -503,6 +517,12 @@ __global__ __launch_bounds__(NW * 64, NW == 4 ? 2 : 1) void attention_bwd_kernel
         dp = __builtin_amdgcn_mfma_f32_32x32x16_bf16(oa, vb, dp, 0, 0, 0);
       }
       const float kbias = kb[kcol];
+      // keep bits of this lane's key column for its 16 queries: 4 x 4 consecutive query words
+      u32x4 wq[4] = {};
+      if (bits) {
+#pragma unroll
+        for (int g = 0; g < 4; ++g) wq[g] = *(const u32x4*)(kbits + kbk * Lp + qbq * 32 + 8 * g + 4 * h);
+      }
 #pragma unroll
       for (int e = 0; e < 16; ++e) {
         const int qr = (e & 3) + 8 * (e >> 2) + 4 * h;
@@ -511,7 +531,8 @@ __global__ __launch_bounds__(NW * 64, NW == 4 ? 2 : 1) void attention_bwd_kernel
         float dpe = dp[e];
         if (drop) {
           const uint64_t idx = (((uint64_t)b * a.heads + hd) * L + q) * (uint64_t)L + kcol;
-          const bool keep = kcol < L && q < L && drop_hash24(a.seed, a.site, idx) >= thr;
+          const bool keep = bits ? ((wq[e >> 2][e & 3] >> r) & 1u) != 0u
+                                 : kcol < L && q < L && drop_hash24(a.seed, a.site, idx) >= thr;
           dpe = keep ? dpe * inv : 0.f;
         }
         if (!(ABL & 8)) *(__bf16*)(sT + qr * kAbScr + r * 2) = (__bf16)(p * (dpe - dv[q]));
@@ -701,20 +722,36 @@ int drt_attention_bwd_bf16(const void* qkv, const void* ctx, const void* dctx, c
 
 // The same with the forward's attention-probability dropout (drop_p, seed, site as passed to
 // drt_attention_train_fwd_bf16).
+int drt_attention_train_bwd_bits_bf16(const void* qkv, const void* ctx, const void* dctx, const float* lse,
+                                      const int64_t* mask, const uint32_t* drop_bits, void* dqkv, int64_t B, int64_t L,
+                                      int32_t heads, int32_t head_dim, float scale, float drop_p, uint64_t seed,
+                                      uint64_t site, void* stream);
+
 int drt_attention_train_bwd_bf16(const void* qkv, const void* ctx, const void* dctx, const float* lse,
                                  const int64_t* mask, void* dqkv, int64_t B, int64_t L, int32_t heads,
                                  int32_t head_dim, float scale, float drop_p, uint64_t seed, uint64_t site,
                                  void* stream) {
+  return drt_attention_train_bwd_bits_bf16(qkv, ctx, dctx, lse, mask, nullptr, dqkv, B, L, heads, head_dim, scale,
+                                           drop_p, seed, site, stream);
+}
+
+// The same reading the forward's keep bits (drt_attention_train_fwd_bits_bf16) instead of re-hashing
+// every (query, key) twice (dK / dV and dQ phases); NULL drop_bits = regenerate from the hash.
+int drt_attention_train_bwd_bits_bf16(const void* qkv, const void* ctx, const void* dctx, const float* lse,
+                                      const int64_t* mask, const uint32_t* drop_bits, void* dqkv, int64_t B, int64_t L,
+                                      int32_t heads, int32_t head_dim, float scale, float drop_p, uint64_t seed,
+                                      uint64_t site, void* stream) {
   DRT_REQUIRE(B >= 0 && L > 0 && L <= kAbMaxSeq && heads > 0 && head_dim == 64);
   DRT_REQUIRE(drop_p >= 0.0f && drop_p < 1.0f);
   if (B == 0) return DRT_OK;
   DRT_REQUIRE(qkv && ctx && dctx && lse && dqkv);
   AttnBwdArgs a{(const __bf16*)qkv, (const __bf16*)ctx, (const __bf16*)dctx, lse, mask, (__bf16*)dqkv, B, L,
-                heads, heads * 64, scale, drop_p, seed, site};
+                heads, heads * 64, scale, drop_p, seed, site, drop_bits};
   const int Lp = ((int)L + 31) & ~31;
   const bool w8 = Lp / 32 > 4;
   const int nw = w8 ? 8 : 4;
-  const size_t lds = (size_t)4 * Lp * kAbRow + (size_t)nw * 32 * kAbScr + (size_t)3 * Lp * 4;
+  const size_t lds = (size_t)4 * Lp * kAbRow + (size_t)nw * 32 * kAbScr + (size_t)3 * Lp * 4 +
+                     (drop_bits && drop_p > 0.0f ? (size_t)(Lp / 32) * Lp * 4 : 0);
   DRT_REQUIRE(lds <= 160 * 1024);
   static bool attr_set = false;
   if (!attr_set) {

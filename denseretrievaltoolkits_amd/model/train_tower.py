@@ -192,9 +192,12 @@ def layer_forward(st: _Step, i: int, h):
     qkv = _lin(lib, h, ly["wqkv"], ly["bqkv"], torch.empty((T, 3 * H), dtype=torch.bfloat16, device=dev), stream=s)
     ctx = torch.empty((T, H), dtype=torch.bfloat16, device=dev)
     lse = torch.empty((B, heads, L), dtype=torch.float32, device=dev)
-    _native.check(lib.drt_attention_train_fwd_bf16(qkv.data_ptr(), _ptr(st.mask), ctx.data_ptr(), lse.data_ptr(),
-                                                   B, L, heads, H // heads, st.scale, float(pa), seed, s_att, s),
-                  "drt_attention_train_fwd_bf16")
+    # attention-dropout keep mask as bits (B * heads * L * L / 8 bytes): the backward reads it
+    bits = torch.empty((B, heads, L, (L + 31) // 32), dtype=torch.int32, device=dev) if pa > 0 else None
+    _native.check(lib.drt_attention_train_fwd_bits_bf16(qkv.data_ptr(), _ptr(st.mask), ctx.data_ptr(),
+                                                        lse.data_ptr(), _ptr(bits), B, L, heads, H // heads, st.scale,
+                                                        float(pa), seed, s_att, s),
+                  "drt_attention_train_fwd_bits_bf16")
     # x1 = dropout(ctx Wo^T + bo) + h, dropout in the GEMM epilogue
     x1 = _lin(lib, ctx, ly["wo"], ly["bo"], torch.empty_like(h), resid=h, stream=s,
               drop=(ph, seed, s_out1) if ph > 0 else None)
@@ -206,14 +209,14 @@ def layer_forward(st: _Step, i: int, h):
     x2 = _lin(lib, f, ly["wf"], ly["bf"], torch.empty_like(h), resid=h1, stream=s,
               drop=(ph, seed, s_out2) if ph > 0 else None)
     h2 = _layernorm(lib, x2, ly["g2"], ly["b2"], st.eps, s)
-    return h2, (h, qkv, ctx, lse, x1, h1, fpre, f, x2)
+    return h2, (h, qkv, ctx, lse, bits, x1, h1, fpre, f, x2)
 
 
 def layer_backward(st: _Step, i: int, saved, d) -> Tuple[torch.Tensor, Dict[str, torch.Tensor]]:
     """d h_in and the fp32 gradients of layer i's parameters (HF names) for d h_out."""
     lib = _native.load()
     s = _native.stream_ptr(st.dev)
-    h, qkv, ctx, lse, x1, h1, fpre, f, x2 = saved
+    h, qkv, ctx, lse, bits, x1, h1, fpre, f, x2 = saved
     ly = st.W.layers[i]
     H, heads, eps = st.H, st.heads, st.eps
     ph, pa, seed = st.drop
@@ -235,10 +238,11 @@ def layer_backward(st: _Step, i: int, saved, d) -> Tuple[torch.Tensor, Dict[str,
         dy1 = dx1
     dctx, dwo, dbo = linear_backward(dy1, ctx, ly["wo_t"])
     dqkv = torch.empty_like(qkv)
-    _native.check(lib.drt_attention_train_bwd_bf16(qkv.data_ptr(), ctx.data_ptr(), dctx.data_ptr(),
-                                                   lse.data_ptr(), _ptr(st.mask), dqkv.data_ptr(), st.B, st.L, heads,
-                                                   H // heads, st.scale, float(pa), seed, s_att, s),
-                  "drt_attention_train_bwd_bf16")
+    _native.check(lib.drt_attention_train_bwd_bits_bf16(qkv.data_ptr(), ctx.data_ptr(), dctx.data_ptr(),
+                                                        lse.data_ptr(), _ptr(st.mask), _ptr(bits), dqkv.data_ptr(),
+                                                        st.B, st.L, heads, H // heads, st.scale, float(pa), seed,
+                                                        s_att, s),
+                  "drt_attention_train_bwd_bits_bf16")
     d_in, dwqkv, dbqkv = linear_backward(dqkv, h, ly["wqkv_t"], resid=dx1)
     grads = {}
     grads[p + "output.LayerNorm.weight"], grads[p + "output.LayerNorm.bias"] = dg2, db2

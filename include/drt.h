@@ -276,6 +276,18 @@ int drt_attention_train_bwd_bf16(const void* qkv, const void* ctx, const void* d
                                  void* stream);
 int drt_dropout_add_bf16(const void* y, const void* resid, int64_t n, float p, uint64_t seed, uint64_t site,
                          void* out, void* stream);
+/* The training attention pair with the dropout keep mask kept as bits: the forward writes
+ * drop_bits [B][heads][L][ceil(L / 32)] u32 (bit key & 31 of word (query, key >> 5); only when
+ * drop_p > 0 and drop_bits != NULL), the backward reads them instead of regenerating the hash
+ * twice per (query, key).  Same masks, same results as the hash-regenerating pair.             */
+int drt_attention_train_fwd_bits_bf16(const void* qkv, const int64_t* mask, void* ctx, float* lse,
+                                      uint32_t* drop_bits, int64_t B, int64_t L, int32_t heads,
+                                      int32_t head_dim, float scale, float drop_p, uint64_t seed,
+                                      uint64_t site, void* stream);
+int drt_attention_train_bwd_bits_bf16(const void* qkv, const void* ctx, const void* dctx, const float* lse,
+                                      const int64_t* mask, const uint32_t* drop_bits, void* dqkv, int64_t B,
+                                      int64_t L, int32_t heads, int32_t head_dim, float scale, float drop_p,
+                                      uint64_t seed, uint64_t site, void* stream);
 int drt_pool_bf16(const void* hidden, const int64_t* mask, int64_t B, int64_t L, int32_t H,
                   int32_t mode, float* out, void* out_bf16, void* stream);
 int drt_l2_normalize_f32(float* x, int64_t B, int32_t H, void* out_bf16, void* stream);

@@ -1,6 +1,7 @@
 """GPU: encoder backward building blocks against torch fp32 autograd of the
 same forward ops (HF BertModel's LayerNorm / GELU / Linear bias / attention softmax,
 transformers modeling_bert.py:164-204, 282-352) on the same bf16 inputs."""
+import numpy as np
 import pytest
 
 pytestmark = pytest.mark.gpu
@@ -347,3 +348,49 @@ def test_layernorm_bwd_drop_output_equals_dropout_kernel(dev, M, H):
     torch.cuda.synchronize()
     assert torch.equal(dx, dx0) and torch.equal(dg, dg0) and torch.equal(db, db0)
     assert torch.equal(dxd, ref)
+
+
+@pytest.mark.parametrize("L,B", [(128, 6), (156, 5), (37, 9), (32, 4)])
+def test_attention_dropout_bits_equal_hash_regeneration(dev, L, B):
+    """drt_attention_train_fwd_bits_bf16 writes the dropout keep mask as bits; the backward that reads
+    them (drt_attention_train_bwd_bits_bf16) is bit-identical to the one that regenerates the hash,
+    and the forward's outputs do not change; the bits are the hash's keep decisions."""
+    import torch
+    from denseretrievaltoolkits_amd import _native
+    lib = _native.load()
+    s = _native.stream_ptr(dev)
+    heads, H, p, seed, site = 12, 768, 0.1, 77, 3
+    g = torch.Generator(device=dev).manual_seed(L)
+    qkv = (0.5 * torch.randn(B * L, 3 * H, generator=g, device=dev)).to(torch.bfloat16)
+    dctx = (0.1 * torch.randn(B * L, H, generator=g, device=dev)).to(torch.bfloat16)
+    mask = torch.ones(B, L, dtype=torch.int64, device=dev)
+    mask[1, L - 5:] = 0
+    nkb = (L + 31) // 32
+    outs = {}
+    for use_bits in (False, True):
+        ctx = torch.empty(B * L, H, dtype=torch.bfloat16, device=dev)
+        lse = torch.empty(B * heads * L, dtype=torch.float32, device=dev)
+        bits = torch.full((B, heads, L, nkb), -1, dtype=torch.int32, device=dev) if use_bits else None
+        _native.check(lib.drt_attention_train_fwd_bits_bf16(qkv.data_ptr(), mask.data_ptr(), ctx.data_ptr(),
+                                                            lse.data_ptr(), bits.data_ptr() if use_bits else None,
+                                                            B, L, heads, 64, 0.125, p, seed, site, s), "fwd")
+        dqkv = torch.empty_like(qkv)
+        _native.check(lib.drt_attention_train_bwd_bits_bf16(qkv.data_ptr(), ctx.data_ptr(), dctx.data_ptr(),
+                                                            lse.data_ptr(), mask.data_ptr(),
+                                                            bits.data_ptr() if use_bits else None, dqkv.data_ptr(),
+                                                            B, L, heads, 64, 0.125, p, seed, site, s), "bwd")
+        torch.cuda.synchronize()
+        outs[use_bits] = (ctx, lse, dqkv, bits)
+    for a, b in zip(outs[False][:3], outs[True][:3]):
+        assert torch.equal(a, b)
+    # spot-check the bits against the host restatement of the hash for one (sequence, head)
+    from tests.test_train_tower_gpu import _hash24_py
+
+    def drop_keep(seed_, site_, idx, p_):
+        return _hash24_py(seed_, site_, idx) >= int(np.float32(p_) * np.float32(16777216.0))
+    bb, hd = B - 1, heads // 2
+    w = outs[True][3][bb, hd].cpu().numpy().astype(np.uint32)
+    for q in (0, L // 2, L - 1):
+        for key in range(L):
+            want = drop_keep(seed, site, ((bb * heads + hd) * L + q) * L + key, p)
+            assert bool((w[q, key >> 5] >> (key & 31)) & 1) == want, (q, key)

@@ -478,19 +478,25 @@ def _w_ddp(rank, world, dev):
         for nxt, _ in fn.next_functions:
             walk(nxt, seen)
     walk(loss.grad_fn, set())
-    out = {"loss": float(loss), "per_layer_nodes": sorted(x for x in names if "Fn" in x)}
+    out = {"loss": float(loss.detach()), "per_layer_nodes": sorted(x for x in names if "Fn" in x)}
     if rank == 0:
         # single process on the concatenated batch (in-batch negatives over all of it) = the
         # gradient DDP must reproduce: (1 / W) sum_r grad_r (W loss) with x-device gathering
+        # (each rank's half encoded separately, as the ranks did: identical GEMM plans, so identical
+        # bf16 reps; unnormalised BERT reps amplify any rounding difference into the scores)
+        from denseretrievaltoolkits_amd.score_ce import score_ce
         ref_model = _ddp_model(dev, False).to(dev).train()
-        ref_loss = ref_model(*_ddp_batch(None, world, Bq, n, dev)).loss
+        halves = [_ddp_batch(r, world, Bq, n, dev) for r in range(world)]
+        q = torch.cat([ref_model.encode_query(hq)[1] for hq, _ in halves])
+        p = torch.cat([ref_model.encode_passage(hp)[1] for _, hp in halves])
+        ref_loss, _ = score_ce(q, p, n, 1.0)
         ref_loss.backward()
         ref = {k: p.grad.detach().float().cpu() for k, p in ref_model.lm_q.named_parameters() if p.grad is not None}
         cos = {}
         for k, g in ref.items():
             a, b = got[k].reshape(-1).double(), g.reshape(-1).double()
             cos[k] = float((a @ b) / (a.norm() * b.norm() + 1e-30)) if b.norm() > 0 else float((a.norm() == 0))
-        out.update(ref_loss=float(ref_loss), min_cos=min(cos.values()), worst=min(cos, key=cos.get),
+        out.update(ref_loss=float(ref_loss.detach()), min_cos=min(cos.values()), worst=min(cos, key=cos.get),
                    n_params=len(ref), n_got=len(got))
     return out
 
@@ -499,11 +505,12 @@ def test_ddp_train_step_world2_matches_single_process():
     """Trainer wraps the model in DDP (find_unused_parameters=True, as the reference) at world 2;
     one train step with negatives_x_device on the HIP training tower: the loss equals the single-
     process loss on the concatenated batch (x W, the reference's scaling) and DDP's averaged
-    parameter gradients equal that single process's gradients (cos >= 0.999 per tensor)."""
+    parameter gradients equal that single process's gradients (cos >= 0.999 per tensor).  The single
+    process encodes the two halves separately (the ranks' batch shapes) and scores their concatenation."""
     res = _spawn(_w_ddp, 2)
     r0 = res[0]
     assert abs(res[1]["loss"] - r0["loss"]) <= 1e-6 * max(1.0, abs(r0["loss"]))
-    assert abs(r0["loss"] - 2 * r0["ref_loss"]) <= 2e-3 * abs(r0["ref_loss"]) + 1e-4, r0
+    assert abs(r0["loss"] - 2 * r0["ref_loss"]) <= 1e-5 * abs(r0["ref_loss"]) + 1e-6, r0
     assert r0["n_got"] == r0["n_params"], r0
     assert r0["min_cos"] >= 0.999, r0
     assert "_LayerFnBackward" in r0["per_layer_nodes"] and "_EmbedFnBackward" in r0["per_layer_nodes"], r0

@@ -50,4 +50,4 @@ def main(reps=10):
 
 
 if __name__ == "__main__":
-    main()
+    main(int(sys.argv[1]) if len(sys.argv) > 1 else 10)
