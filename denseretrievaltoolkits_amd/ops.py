@@ -55,6 +55,15 @@ def _register_python_parts():
         return (q.new_empty((nq, k), dtype=torch.float32), q.new_empty((nq, k), dtype=torch.int64),
                 q.new_empty((nq,), dtype=torch.int32))
 
+    @lib.register_fake("drt::ip_topk.out")
+    def _(q, p, k, id_offset, *, scores, ids, status):
+        return None
+
+    @lib.register_fake("drt::ip_topk_resolve")
+    def _(q, p, k, id_offset, scores, ids, status):
+        # the count of rescanned queries is data-dependent (it reads the status back)
+        return torch.library.get_ctx().new_dynamic_size()
+
     @lib.register_fake("drt::topk_merge")
     def _(scores, ids, k_out):
         nq = scores.shape[1]

@@ -29,6 +29,7 @@ def test_fake_shapes(drt):
         s, i, st = drt.ip_topk(q, p, 10, 0)
         assert (s.shape, s.dtype, i.dtype, st.shape, st.dtype) == ((5, 10), torch.float32, torch.int64, (5,),
                                                                    torch.int32)
+        assert drt.ip_topk.out(q, p, 10, 0, scores=s, ids=i, status=st) is None
         ms, mi = drt.topk_merge(torch.empty(3, 5, 10, device="cuda"), torch.empty(3, 5, 10, dtype=torch.int64,
                                                                                   device="cuda"), 7)
         assert ms.shape == (5, 7) and mi.dtype == torch.int64
