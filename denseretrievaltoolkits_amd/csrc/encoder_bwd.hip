@@ -564,6 +564,278 @@ __global__ __launch_bounds__(NW * 64, NW == 4 ? 2 : 1) void attention_bwd_kernel
   }
 }
 
+// ---------------------------------------------------------------------------
+// Attention backward, register-resident P / dS (round 3).  Same math and LDS images as
+// attention_bwd_kernel, but each phase computes its score tile in the orientation whose MFMA
+// output layout IS the A operand of the next product, so P / dS never go through LDS:
+//   phase 1 (wave = key block kbk, loop over query blocks):  S = Qs K^T and dP = dO V^T as
+//     [query rows (registers)][key (lane)] tiles; a lane then holds, for its key, 16 queries of the
+//     block -- exactly the A operand of dV = Pd^T dO and dK = dS^T Qs with the k (query) order
+//     permuted (8 (e >> 2) + 4 h + (e & 3)); the B operands are read in the same permuted row order
+//     with ds_read_b64_tr_b16 (rows base + 4 h .. + 3 and base + 8 + 4 h .. + 3).
+//   phase 2 (wave = query block, loop over key blocks): S^T = K Qs^T and dP^T = V dO^T as
+//     [key rows][query (lane)] tiles = the A operand of dQ = dS K (k = key, permuted likewise).
+// The key-block operands of phase 1 (K, V as B operands) and the query-block operands of phase 2
+// (Qs, dO) stay in registers for the whole phase.  Per-query values of phase 1 (lse, Dv, keep words)
+// are read as 16-B vectors, four queries at a time.  DROP: the forward's keep bits (drop_bits)
+// staged in LDS as [key block][query] words -- no hashing here at all.
+// 32x32x16 MFMA: A lane (m = l & 31, h = l >> 5) holds A[m][k = 8h .. 8h + 7]; B lane (n, h) holds
+// B[k = 8h ..][n]; D lane (n = l & 31, h) holds D[m = 8 (e >> 2) + 4 h + (e & 3)][n].
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ bf16x8 ab_tr8p(const char* img, int rowA, int rowB, int col0, int lane) {
+  const int i = lane & 15, q = i >> 2, p = i & 3;
+  const int chunk = (col0 + 16 * ((lane >> 4) & 1) + 4 * p) >> 3;
+  const int lo = (p & 1) * 8;
+  typedef __attribute__((address_space(3))) ab_v4i16 lds_v4;
+  const ab_v4i16 x = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4*)(img + ab_rc(rowA + q, chunk) + lo));
+  const ab_v4i16 y = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4*)(img + ab_rc(rowB + q, chunk) + lo));
+  bf16x8 v;
+  __builtin_memcpy(&v, &x, 8);
+  __builtin_memcpy((char*)&v + 8, &y, 8);
+  return v;
+}
+
+template <int NW, bool DROP>
+__global__ __launch_bounds__(NW * 64, NW == 4 ? 2 : 1) void attention_bwd_rk_kernel(AttnBwdArgs a) {
+  constexpr int NT = NW * 64;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int L = (int)a.L;
+  const int Lp = (L + 31) & ~31;
+  const int nblk = Lp / 32;
+  char* Qs = smem;                                   // [Lp][64] (scaled Q)
+  char* Ks = Qs + Lp * kAbRow;
+  char* Vs = Ks + Lp * kAbRow;
+  char* Os = Vs + Lp * kAbRow;                       // dO
+  float* lse = (float*)(Os + Lp * kAbRow);           // [Lp]
+  float* dv = lse + Lp;                              // [Lp]  Dv
+  float* kb = dv + Lp;                               // [Lp]  key bias
+  uint32_t* kbits = (uint32_t*)(kb + Lp);            // [nblk][Lp] keep words (DROP)
+
+  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+  const int r = lane & 31, h = lane >> 5;
+  const int64_t b = blockIdx.x / a.heads;
+  const int hd = blockIdx.x % a.heads;
+  const int64_t row0 = b * a.L;
+  const int64_t ld = 3 * (int64_t)a.H;
+  const __bf16* Qg = a.qkv + row0 * ld + hd * 64;
+  const __bf16* Kg = Qg + a.H;
+  const __bf16* Vg = Qg + 2 * a.H;
+  const __bf16* Og = a.ctx + row0 * a.H + hd * 64;
+  const __bf16* dOg = a.dctx + row0 * a.H + hd * 64;
+
+  // ---- staging (as attention_bwd_kernel): every global load of the work-group's rows in flight
+  // before the first LDS store
+  {
+    constexpr int MAXIT = (kAbMaxSeq * 8 + NT - 1) / NT;
+    bf16x8 q[MAXIT], k[MAXIT], v[MAXIT], o[MAXIT], oo[MAXIT];
+#pragma unroll
+    for (int it = 0; it < MAXIT; ++it) {
+      const int i = tid + it * NT;
+      const int row = i >> 3, c = i & 7;
+      q[it] = bf16x8{};
+      k[it] = bf16x8{};
+      v[it] = bf16x8{};
+      o[it] = bf16x8{};
+      oo[it] = bf16x8{};
+      if (i < Lp * 8 && row < L) {
+        q[it] = *(const bf16x8*)(Qg + (int64_t)row * ld + c * 8);
+        k[it] = *(const bf16x8*)(Kg + (int64_t)row * ld + c * 8);
+        v[it] = *(const bf16x8*)(Vg + (int64_t)row * ld + c * 8);
+        o[it] = *(const bf16x8*)(dOg + (int64_t)row * a.H + c * 8);
+        oo[it] = *(const bf16x8*)(Og + (int64_t)row * a.H + c * 8);
+      }
+    }
+#pragma unroll
+    for (int it = 0; it < MAXIT; ++it) {
+      const int i = tid + it * NT;
+      if (i >= Lp * 8) break;
+      const int row = i >> 3, c = i & 7;
+      float part = 0.f;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        q[it][j] = (__bf16)((float)q[it][j] * a.scale);
+        part += (float)o[it][j] * (float)oo[it][j];
+      }
+      *(bf16x8*)(Qs + ab_rc(row, c)) = q[it];
+      *(bf16x8*)(Ks + ab_rc(row, c)) = k[it];
+      *(bf16x8*)(Vs + ab_rc(row, c)) = v[it];
+      *(bf16x8*)(Os + ab_rc(row, c)) = o[it];
+      part += __shfl_xor(part, 1, 64);
+      part += __shfl_xor(part, 2, 64);
+      part += __shfl_xor(part, 4, 64);
+      if (c == 0) dv[row] = part;
+    }
+  }
+  for (int i = tid; i < Lp; i += NT) {
+    float bv = 0.0f;
+    if (i >= L) bv = -3.402823466e+38f;
+    else if (a.mask && a.mask[b * a.L + i] == 0) bv = -3.402823466e+38f;
+    kb[i] = bv;
+    lse[i] = i < L ? a.lse[((int64_t)b * a.heads + hd) * a.L + i] : 0.0f;
+  }
+  if (DROP) {   // [query][key block] words of the forward -> [key block][query]
+    const uint32_t* src = a.drop_bits + ((int64_t)b * a.heads + hd) * a.L * nblk;
+    for (int i = tid; i < nblk * Lp; i += NT) {
+      const int q = i / nblk, kbi = i - q * nblk;
+      kbits[kbi * Lp + q] = q < L ? src[(int64_t)q * nblk + kbi] : 0u;
+    }
+  }
+  __syncthreads();
+
+  const float inv = DROP ? 1.0f / (1.0f - a.drop_p) : 1.0f;
+
+  // ---- phase 1: dK, dV of key block kbk
+  for (int kbk = wave; kbk < nblk; kbk += NW) {
+    const int key = kbk * 32 + r;                     // this lane's key (D column / A row)
+    bf16x8 kf[4], vf[4];                              // B operands of S = Qs K^T, dP = dO V^T
+#pragma unroll
+    for (int k4 = 0; k4 < 4; ++k4) {
+      kf[k4] = *(const bf16x8*)(Ks + ab_rc(key, 2 * k4 + h));
+      vf[k4] = *(const bf16x8*)(Vs + ab_rc(key, 2 * k4 + h));
+    }
+    const float kbias = kb[key];
+    f32x16 dK[2], dV[2];
+#pragma unroll
+    for (int t = 0; t < 2; ++t)
+#pragma unroll
+      for (int e = 0; e < 16; ++e) {
+        dK[t][e] = 0.f;
+        dV[t][e] = 0.f;
+      }
+    for (int qb = 0; qb < nblk; ++qb) {
+      const int qrow = qb * 32 + r;                   // A-operand row (query) of this lane
+      f32x16 sv, dp;
+#pragma unroll
+      for (int e = 0; e < 16; ++e) {
+        sv[e] = 0.f;
+        dp[e] = 0.f;
+      }
+#pragma unroll
+      for (int k4 = 0; k4 < 4; ++k4) {
+        const bf16x8 qa = *(const bf16x8*)(Qs + ab_rc(qrow, 2 * k4 + h));
+        sv = __builtin_amdgcn_mfma_f32_32x32x16_bf16(qa, kf[k4], sv, 0, 0, 0);
+        const bf16x8 oa = *(const bf16x8*)(Os + ab_rc(qrow, 2 * k4 + h));
+        dp = __builtin_amdgcn_mfma_f32_32x32x16_bf16(oa, vf[k4], dp, 0, 0, 0);
+      }
+      // P, dS for this lane's key and its 16 queries (four groups of four consecutive queries)
+      bf16x8 pa[2], sa[2];
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        const int q0 = qb * 32 + 8 * g + 4 * h;
+        const f32x4 lq = *(const f32x4*)(lse + q0);
+        const f32x4 dq = *(const f32x4*)(dv + q0);
+        u32x4 wk = {};
+        if (DROP) wk = *(const u32x4*)(kbits + kbk * Lp + q0);
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          const int e = 4 * g + u;
+          const float p = __expf(sv[e] + kbias - lq[u]);
+          float pd = p, dpe = dp[e];
+          if (DROP) {
+            const bool keep = ((wk[u] >> r) & 1u) != 0u;
+            pd = keep ? p * inv : 0.f;
+            dpe = keep ? dpe * inv : 0.f;
+          }
+          pa[e >> 3][e & 7] = (__bf16)pd;
+          sa[e >> 3][e & 7] = (__bf16)(p * (dpe - dq[u]));
+        }
+      }
+      // dV += Pd^T dO, dK += dS^T Qs over the block's 32 queries (2 k-steps of 16, permuted rows)
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks) {
+        const int rA = qb * 32 + 16 * ks + 4 * h, rB = rA + 8;
+#pragma unroll
+        for (int t = 0; t < 2; ++t) {
+          const bf16x8 ob = ab_tr8p(Os, rA, rB, 32 * t, lane);
+          dV[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(pa[ks], ob, dV[t], 0, 0, 0);
+          const bf16x8 qb8 = ab_tr8p(Qs, rA, rB, 32 * t, lane);
+          dK[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(sa[ks], qb8, dK[t], 0, 0, 0);
+        }
+      }
+    }
+    // dK / dV [key][d]: row = key 8 (e >> 2) + 4 h + (e & 3) of the block (regs), column d = 32 t + r
+#pragma unroll
+    for (int e = 0; e < 16; ++e) {
+      const int kr = kbk * 32 + (e & 3) + 8 * (e >> 2) + 4 * h;
+      if (kr < L) {
+        __bf16* dst = a.dqkv + (row0 + kr) * ld + hd * 64;
+#pragma unroll
+        for (int t = 0; t < 2; ++t) {
+          dst[a.H + 32 * t + r] = (__bf16)dK[t][e];
+          dst[2 * a.H + 32 * t + r] = (__bf16)dV[t][e];
+        }
+      }
+    }
+  }
+
+  // ---- phase 2: dQ of query block qbq
+  for (int qbq = wave; qbq < nblk; qbq += NW) {
+    const int q = qbq * 32 + r;                        // this lane's query (D column)
+    bf16x8 qf[4], of[4];                               // B operands of S^T = K Qs^T, dP^T = V dO^T
+#pragma unroll
+    for (int k4 = 0; k4 < 4; ++k4) {
+      qf[k4] = *(const bf16x8*)(Qs + ab_rc(q, 2 * k4 + h));
+      of[k4] = *(const bf16x8*)(Os + ab_rc(q, 2 * k4 + h));
+    }
+    const float lq = lse[q], dq = dv[q];
+    f32x16 dQ[2];
+#pragma unroll
+    for (int t = 0; t < 2; ++t)
+#pragma unroll
+      for (int e = 0; e < 16; ++e) dQ[t][e] = 0.f;
+    for (int kbk = 0; kbk < nblk; ++kbk) {
+      const int krow = kbk * 32 + r;
+      f32x16 st, dpt;
+#pragma unroll
+      for (int e = 0; e < 16; ++e) {
+        st[e] = 0.f;
+        dpt[e] = 0.f;
+      }
+#pragma unroll
+      for (int k4 = 0; k4 < 4; ++k4) {
+        const bf16x8 ka = *(const bf16x8*)(Ks + ab_rc(krow, 2 * k4 + h));
+        st = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ka, qf[k4], st, 0, 0, 0);
+        const bf16x8 va = *(const bf16x8*)(Vs + ab_rc(krow, 2 * k4 + h));
+        dpt = __builtin_amdgcn_mfma_f32_32x32x16_bf16(va, of[k4], dpt, 0, 0, 0);
+      }
+      uint32_t wq = 0;
+      if (DROP) wq = kbits[kbk * Lp + q];
+      bf16x8 sa[2];
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        const f32x4 kbv = *(const f32x4*)(kb + kbk * 32 + 8 * g + 4 * h);
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          const int e = 4 * g + u;
+          const float p = __expf(st[e] + kbv[u] - lq);
+          float dpe = dpt[e];
+          if (DROP) dpe = ((wq >> (8 * g + 4 * h + u)) & 1u) != 0u ? dpe * inv : 0.f;
+          sa[e >> 3][e & 7] = (__bf16)(p * (dpe - dq));
+        }
+      }
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks) {
+        const int rA = kbk * 32 + 16 * ks + 4 * h, rB = rA + 8;
+#pragma unroll
+        for (int t = 0; t < 2; ++t) {
+          const bf16x8 kt = ab_tr8p(Ks, rA, rB, 32 * t, lane);
+          dQ[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(sa[ks], kt, dQ[t], 0, 0, 0);
+        }
+      }
+    }
+    // dQ [q][d]: row = query 8 (e >> 2) + 4 h + (e & 3) of the block (regs), column d = 32 t + r
+#pragma unroll
+    for (int e = 0; e < 16; ++e) {
+      const int qr = qbq * 32 + (e & 3) + 8 * (e >> 2) + 4 * h;
+      if (qr < L) {
+        __bf16* dst = a.dqkv + (row0 + qr) * ld + hd * 64;
+#pragma unroll
+        for (int t = 0; t < 2; ++t) dst[32 * t + r] = (__bf16)(dQ[t][e] * a.scale);
+      }
+    }
+  }
+}
+
 // out = dropout(y) (+ resid): keep iff drop_hash24(seed, site, i) >= p 2^24, kept values scaled
 // by 1 / (1 - p).  The same call on a gradient (resid = NULL) is the dropout backward.
 __global__ __launch_bounds__(256) void dropout_add_kernel(const __bf16* y, const __bf16* resid, int64_t n, float p,
@@ -750,8 +1022,28 @@ int drt_attention_train_bwd_bits_bf16(const void* qkv, const void* ctx, const vo
   const int Lp = ((int)L + 31) & ~31;
   const bool w8 = Lp / 32 > 4;
   const int nw = w8 ? 8 : 4;
-  const size_t lds = (size_t)4 * Lp * kAbRow + (size_t)nw * 32 * kAbScr + (size_t)3 * Lp * 4 +
-                     (drop_bits && drop_p > 0.0f ? (size_t)(Lp / 32) * Lp * 4 : 0);
+  const dim3 grid((unsigned)(B * heads));
+  const bool drop = drop_p > 0.0f;
+  if (!drop || drop_bits) {
+    // register-resident P / dS; dropout from the forward's keep bits
+    const size_t lds = (size_t)4 * Lp * kAbRow + (size_t)3 * Lp * 4 + (drop ? (size_t)(Lp / 32) * Lp * 4 : 0);
+    DRT_REQUIRE(lds <= 160 * 1024);
+    static bool rk_attr = false;
+    if (!rk_attr) {
+      const void* ks[] = {(const void*)attention_bwd_rk_kernel<4, false>, (const void*)attention_bwd_rk_kernel<4, true>,
+                          (const void*)attention_bwd_rk_kernel<8, false>, (const void*)attention_bwd_rk_kernel<8, true>};
+      for (const void* f : ks) DRT_CHECK_HIP(hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
+      rk_attr = true;
+    }
+    hipStream_t st = (hipStream_t)stream;
+    if (w8 && drop) hipLaunchKernelGGL((attention_bwd_rk_kernel<8, true>), grid, dim3(512), lds, st, a);
+    else if (w8) hipLaunchKernelGGL((attention_bwd_rk_kernel<8, false>), grid, dim3(512), lds, st, a);
+    else if (drop) hipLaunchKernelGGL((attention_bwd_rk_kernel<4, true>), grid, dim3(256), lds, st, a);
+    else hipLaunchKernelGGL((attention_bwd_rk_kernel<4, false>), grid, dim3(256), lds, st, a);
+    return hip_status(hipGetLastError());
+  }
+  // dropout masks regenerated from the hash (C-ABI callers without the forward's bits)
+  const size_t lds = (size_t)4 * Lp * kAbRow + (size_t)nw * 32 * kAbScr + (size_t)3 * Lp * 4;
   DRT_REQUIRE(lds <= 160 * 1024);
   static bool attr_set = false;
   if (!attr_set) {
@@ -761,7 +1053,6 @@ int drt_attention_train_bwd_bits_bf16(const void* qkv, const void* ctx, const vo
                                       hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
     attr_set = true;
   }
-  const dim3 grid((unsigned)(B * heads));
   if (w8) {
     hipLaunchKernelGGL((attention_bwd_kernel<8>), grid, dim3(512), lds, (hipStream_t)stream, a);
   } else {

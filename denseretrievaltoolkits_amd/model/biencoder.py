@@ -49,6 +49,18 @@ class DROutput(ModelOutput):
     scores: Tensor = None
 
 
+_FALLBACK_LOGGED = set()
+
+
+def _log_fallback(why: str):
+    """Once per reason: a differentiable encode that cannot take the HIP training tower runs the HF
+    module under torch autograd (the reference's own arithmetic) -- say so instead of silently."""
+    if why not in _FALLBACK_LOGGED:
+        _FALLBACK_LOGGED.add(why)
+        logger.warning("DRModel.encode with autograd: HF module under torch autograd, not the HIP training "
+                       "tower (%s)", why)
+
+
 def _torch_mean_pooling(h, mask):
     m = mask.unsqueeze(-1).expand(h.size()).float()
     return torch.sum(h * m, 1) / torch.clamp(m.sum(1), min=1e-9)
@@ -170,11 +182,23 @@ class DRModel(nn.Module):
         # forward with autograd: BERT towers up to MAX_TRAIN_SEQ tokens run the HIP training tower
         # (saved bf16 activations + backward on HIP kernels, HF dropout semantics in train mode,
         # model/train_tower.py); anything else keeps the HF module under autograd.
-        if (self.hip_train and self.feature == "last_hidden_state" and next(model.parameters()).is_cuda
-                and "token_type_ids" not in items and tower_supported(model) is None
-                and items["input_ids"].shape[1] <= MAX_TRAIN_SEQ):
+        why = None
+        if not self.hip_train:
+            why = "hip_train = False"
+        elif self.feature != "last_hidden_state":
+            why = f"feature {self.feature!r}"
+        elif not next(model.parameters()).is_cuda:
+            why = "tower on the CPU"
+        elif "token_type_ids" in items:
+            why = "token_type_ids given"
+        elif items["input_ids"].shape[1] > MAX_TRAIN_SEQ:
+            why = f"sequence length {items['input_ids'].shape[1]} > {MAX_TRAIN_SEQ}"
+        else:
+            why = tower_supported(model)
+        if why is None:
             hidden = train_hidden(model, items["input_ids"], items.get("attention_mask"))
         else:
+            _log_fallback(why)
             out = model(**items, return_dict=True)
             hidden = getattr(out, self.feature)
         if self.pooling == "first":

@@ -112,6 +112,9 @@ class RRModel(nn.Module):
             # pair forward + backward on the HIP training tower (model/train_tower.py)
             hidden = train_hidden(self.lm, items["input_ids"], items.get("attention_mask"))
         else:
+            from .biencoder import _log_fallback
+            _log_fallback("reranker: " + ("tower on the CPU" if dev.type != "cuda" else
+                                          tower_supported(self.lm) or "feature / token_type_ids / length"))
             out = self.lm(**items, return_dict=True)
             hidden = getattr(out, self.feature)
         if self.pooling == "first":

@@ -351,15 +351,19 @@ def test_layernorm_bwd_drop_output_equals_dropout_kernel(dev, M, H):
 
 
 @pytest.mark.parametrize("L,B", [(128, 6), (156, 5), (37, 9), (32, 4)])
-def test_attention_dropout_bits_equal_hash_regeneration(dev, L, B):
-    """drt_attention_train_fwd_bits_bf16 writes the dropout keep mask as bits; the backward that reads
-    them (drt_attention_train_bwd_bits_bf16) is bit-identical to the one that regenerates the hash,
-    and the forward's outputs do not change; the bits are the hash's keep decisions."""
+def test_attention_dropout_bits_vs_hash_and_torch(dev, L, B):
+    """drt_attention_train_fwd_bits_bf16 writes the attention-dropout keep mask as bits (the forward's
+    outputs do not change, the bits are the hash's keep decisions); the backward that reads them (the
+    register-resident kernel) and the one that regenerates the hash (C-ABI callers without bits) both
+    match torch fp32 autograd of the same dropped attention."""
     import torch
     from denseretrievaltoolkits_amd import _native
+    from tests.test_train_tower_gpu import _hash24_py, _keep_torch
     lib = _native.load()
     s = _native.stream_ptr(dev)
-    heads, H, p, seed, site = 12, 768, 0.1, 77, 3
+    heads, dh, p, seed, site = 12, 64, 0.1, 77, 3
+    H = heads * dh
+    scale = 1.0 / dh ** 0.5
     g = torch.Generator(device=dev).manual_seed(L)
     qkv = (0.5 * torch.randn(B * L, 3 * H, generator=g, device=dev)).to(torch.bfloat16)
     dctx = (0.1 * torch.randn(B * L, H, generator=g, device=dev)).to(torch.bfloat16)
@@ -373,24 +377,39 @@ def test_attention_dropout_bits_equal_hash_regeneration(dev, L, B):
         bits = torch.full((B, heads, L, nkb), -1, dtype=torch.int32, device=dev) if use_bits else None
         _native.check(lib.drt_attention_train_fwd_bits_bf16(qkv.data_ptr(), mask.data_ptr(), ctx.data_ptr(),
                                                             lse.data_ptr(), bits.data_ptr() if use_bits else None,
-                                                            B, L, heads, 64, 0.125, p, seed, site, s), "fwd")
+                                                            B, L, heads, dh, scale, p, seed, site, s), "fwd")
         dqkv = torch.empty_like(qkv)
         _native.check(lib.drt_attention_train_bwd_bits_bf16(qkv.data_ptr(), ctx.data_ptr(), dctx.data_ptr(),
                                                             lse.data_ptr(), mask.data_ptr(),
                                                             bits.data_ptr() if use_bits else None, dqkv.data_ptr(),
-                                                            B, L, heads, 64, 0.125, p, seed, site, s), "bwd")
+                                                            B, L, heads, dh, scale, p, seed, site, s), "bwd")
         torch.cuda.synchronize()
         outs[use_bits] = (ctx, lse, dqkv, bits)
-    for a, b in zip(outs[False][:3], outs[True][:3]):
-        assert torch.equal(a, b)
-    # spot-check the bits against the host restatement of the hash for one (sequence, head)
-    from tests.test_train_tower_gpu import _hash24_py
-
-    def drop_keep(seed_, site_, idx, p_):
-        return _hash24_py(seed_, site_, idx) >= int(np.float32(p_) * np.float32(16777216.0))
+    assert torch.equal(outs[False][0], outs[True][0]) and torch.equal(outs[False][1], outs[True][1])
+    # torch fp32 reference with the same keep mask (host restatement of drop_hash24)
+    idx = torch.arange(B * heads * L * L, device=dev, dtype=torch.int64)
+    keep = _keep_torch(seed, site, idx, p).view(B, heads, L, L).float()
+    x = qkv.float().requires_grad_(True)
+    q = x[:, :H].view(B, L, heads, dh).transpose(1, 2)
+    k = x[:, H:2 * H].view(B, L, heads, dh).transpose(1, 2)
+    v = x[:, 2 * H:].view(B, L, heads, dh).transpose(1, 2)
+    sc = (q * scale) @ k.transpose(-1, -2) + (1 - mask[:, None, None, :].float()) * torch.finfo(torch.float32).min
+    o = (torch.softmax(sc, -1) * keep / (1 - p)) @ v
+    o.transpose(1, 2).reshape(B * L, H).backward(dctx.float())
+    ref = x.grad
+    for use_bits in (False, True):
+        dq = outs[use_bits][2]
+        for name, sl in (("dQ", slice(0, H)), ("dK", slice(H, 2 * H)), ("dV", slice(2 * H, 3 * H))):
+            got, want = dq[:, sl].float(), ref[:, sl]
+            cos = torch.nn.functional.cosine_similarity(got.flatten(), want.flatten(), dim=0).item()
+            assert cos > 0.999, (use_bits, name, cos)
+            err = (got - want).abs().max().item()
+            assert err <= 2e-2 * max(1.0, want.abs().max().item()), (use_bits, name, err)
+    # the bits are the hash's keep decisions
     bb, hd = B - 1, heads // 2
     w = outs[True][3][bb, hd].cpu().numpy().astype(np.uint32)
-    for q in (0, L // 2, L - 1):
+    thr = int(np.float32(p) * np.float32(16777216.0))
+    for qq in (0, L // 2, L - 1):
         for key in range(L):
-            want = drop_keep(seed, site, ((bb * heads + hd) * L + q) * L + key, p)
-            assert bool((w[q, key >> 5] >> (key & 31)) & 1) == want, (q, key)
+            want = _hash24_py(seed, site, ((bb * heads + hd) * L + qq) * L + key) >= thr
+            assert bool((w[qq, key >> 5] >> (key & 31)) & 1) == want, (qq, key)

@@ -25,24 +25,30 @@ def main(reps=10):
         dctx = (0.1 * torch.randn(T, H, device=dev)).to(torch.bfloat16)
         dqkv = torch.empty_like(qkv)
         mask = torch.ones(B, L, dtype=torch.int64, device=dev)
-        for p in (0.0, 0.1):
+        bits = torch.empty((B, heads, L, (L + 31) // 32), dtype=torch.int32, device=dev)
+        for p, use_bits in ((0.0, False), (0.1, True), (0.1, False)):
+            bp = bits.data_ptr() if use_bits else None
+
             def fwd():
-                return lib.drt_attention_train_fwd_bf16(qkv.data_ptr(), mask.data_ptr(), ctx.data_ptr(), lse.data_ptr(),
-                                                        B, L, heads, 64, 0.125, p, 123, 4, s)
+                return lib.drt_attention_train_fwd_bits_bf16(qkv.data_ptr(), mask.data_ptr(), ctx.data_ptr(),
+                                                             lse.data_ptr(), bp, B, L, heads, 64, 0.125, p, 123, 4, s)
 
             def bwd():
-                return lib.drt_attention_train_bwd_bf16(qkv.data_ptr(), ctx.data_ptr(), dctx.data_ptr(), lse.data_ptr(),
-                                                        mask.data_ptr(), dqkv.data_ptr(), B, L, heads, 64, 0.125, p,
-                                                        123, 4, s)
+                return lib.drt_attention_train_bwd_bits_bf16(qkv.data_ptr(), ctx.data_ptr(), dctx.data_ptr(),
+                                                             lse.data_ptr(), mask.data_ptr(), bp, dqkv.data_ptr(), B,
+                                                             L, heads, 64, 0.125, p, 123, 4, s)
+            tag = "" if p == 0 else ("_bits" if use_bits else "_hash")
             for name, fn in (("fwd", fwd), ("bwd", bwd)):
                 _native.check(fn(), name)
+                _native.check(fn(), name)
+                torch.cuda.synchronize()
                 e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
                 e0.record()
                 for _ in range(reps):
                     fn()
                 e1.record()
                 torch.cuda.synchronize()
-                res[f"B{B}_L{L}_{name}_p{p}"] = round(e0.elapsed_time(e1) / reps * 1e3, 1)
+                res[f"B{B}_L{L}_{name}_p{p}{tag}"] = round(e0.elapsed_time(e1) / reps * 1e3, 1)
         fwd_bytes = T * 3 * H * 2 + T * H * 2
         bwd_bytes = T * 3 * H * 2 + 2 * T * H * 2 + T * 3 * H * 2
         res[f"B{B}_L{L}_floor_us"] = {"fwd": round(fwd_bytes / 6.3e12 * 1e6, 1), "bwd": round(bwd_bytes / 6.3e12 * 1e6, 1)}
