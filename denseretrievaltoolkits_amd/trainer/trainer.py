@@ -35,7 +35,7 @@ from torch.nn.parallel import DistributedDataParallel as DDP
 from .. import comm
 from ..evaluator.metrics import get_metrics
 from ..evaluator.nq_eval import AnswerMatcher, RowAnswerMatcher, has_answers
-from ..search import ShardedFlatIP
+from ..search import ShardedFlatIP, _stage_host
 from .losses import get_loss_function
 from .scheduler import ConstantScheduler, CosineScheduler, InverseSquareRootScheduler, LinearScheduler
 
@@ -435,16 +435,31 @@ class RRTrainer(Trainer):
         result = {}
         m = self.module
         matcher = AnswerMatcher()
-        for batch in pair_loader:
-            data = {k: v.to(self.device) if v is not None else None for k, v in batch[1].items()}
-            with torch.no_grad():
-                scores = m(pos_pairs=data, neg_pairs=None).detach().cpu().numpy()
-            for q, ans, d, s, did in zip(batch[0], batch[2], batch[3], scores, batch[4]):
+
+        def finish(pend):
+            # host work of a batch whose scores were staged behind an event: runs while the GPU
+            # scores the next batch (the reference copies each batch's scores back synchronously)
+            batch, (hs,), ev = pend
+            ev.synchronize()
+            scores = hs.numpy()
+            for q, ans, d, sc, did in zip(batch[0], batch[2], batch[3], scores, batch[4]):
                 r = result.setdefault(q, ([], [], [], []))
-                r[0].append(float(s[0]))
+                r[0].append(float(sc[0]))
                 r[1].append(int(matcher.match([did], [d], ans)[0]))
                 r[2].append(d)
                 r[3].append(did)
+
+        pend = None
+        for batch in pair_loader:
+            data = {k: self._to_device(v) for k, v in batch[1].items()}
+            with torch.no_grad():
+                scores = m(pos_pairs=data, neg_pairs=None).detach()
+            cur = (batch,) + _stage_host(scores.float())
+            if pend is not None:
+                finish(pend)
+            pend = cur
+        if pend is not None:
+            finish(pend)
         rdir = getattr(a, "rr_result_dir", "")
         if rdir:
             os.makedirs(rdir, exist_ok=True)
