@@ -179,8 +179,10 @@ struct AttnArgs {
 // NW = waves per work-group (the launcher uses 4; an 8-wave form for 5-8 query blocks measured
 // slower, see drt_attention_train_fwd_bf16).  Each block's arithmetic is the same whichever wave
 // runs it.
+// Occupancy: 4 work-groups per CU for the 4-wave inference kernel (<= 128 VGPRs); the dropout
+// kernels (hash + keep-bit words) need more registers, so 3 (<= 170 VGPRs: at 4 they spilled).
 template <bool DROP, int NW = 4>
-__global__ __launch_bounds__(NW * 64, NW == 4 ? 4 : 2) void attention_kernel(AttnArgs a) {
+__global__ __launch_bounds__(NW * 64, (NW == 4 && !DROP) ? 4 : (NW <= 5 ? 3 : 2)) void attention_kernel(AttnArgs a) {
   constexpr int NT = NW * 64;
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int L = (int)a.L;
@@ -560,19 +562,24 @@ int drt_attention_train_fwd_bits_bf16(const void* qkv, const int64_t* mask, void
   const size_t lds = (size_t)Lp * 128 + (size_t)64 * (Lp * 2 + 8) + (size_t)Lp * 4;
   static bool attr_set = false;
   if (!attr_set) {
-    DRT_CHECK_HIP(hipFuncSetAttribute((const void*)attention_kernel<false, 4>,
-                                      hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
-    DRT_CHECK_HIP(hipFuncSetAttribute((const void*)attention_kernel<true, 4>,
-                                      hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
+    const void* ks[] = {(const void*)attention_kernel<false, 4>, (const void*)attention_kernel<true, 4>,
+                        (const void*)attention_kernel<false, 5>, (const void*)attention_kernel<true, 5>};
+    for (const void* f : ks) DRT_CHECK_HIP(hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
     attr_set = true;
   }
-  // 4 waves at every length: the 8-wave form (NW = 8) measured slower at L = 156 (570 vs 390 us
-  // with dropout: 130 VGPRs -> one work-group per CU instead of four), unlike the backward
+  // 4 waves, except 5 query blocks (129 <= L <= 160: the recipe's 156-token passages, the reranker's
+  // 160-token pairs): 5 waves, one block each -- with 4, wave 0 ran two blocks while three idled.
+  // (An 8-wave form measured slower: 130 VGPRs -> one work-group per CU.)  Same per-block arithmetic.
   const dim3 grid((unsigned)(B * heads));
-  if (drop_p > 0.0f)
-    hipLaunchKernelGGL((attention_kernel<true, 4>), grid, dim3(256), lds, (hipStream_t)stream, a);
-  else
-    hipLaunchKernelGGL((attention_kernel<false, 4>), grid, dim3(256), lds, (hipStream_t)stream, a);
+  hipStream_t s = (hipStream_t)stream;
+  if (Lp / 32 == 5) {
+    if (drop_p > 0.0f) hipLaunchKernelGGL((attention_kernel<true, 5>), grid, dim3(320), lds, s, a);
+    else hipLaunchKernelGGL((attention_kernel<false, 5>), grid, dim3(320), lds, s, a);
+  } else if (drop_p > 0.0f) {
+    hipLaunchKernelGGL((attention_kernel<true, 4>), grid, dim3(256), lds, s, a);
+  } else {
+    hipLaunchKernelGGL((attention_kernel<false, 4>), grid, dim3(256), lds, s, a);
+  }
   return hip_status(hipGetLastError());
 }
 

@@ -1896,8 +1896,17 @@ static int launch_scan_d(const ScanArgs& a, int mode, hipStream_t s) {
     // crossover (profiles/r01_*): dense below ~3M rows at cap 16384.
     const double eh = a.exp_hits > 0 ? (double)a.exp_hits : (double)a.cap / 4.0;
     const bool dense_hits = eh * 256.0 / (double)a.nrows >= 0.35;
-    if (dense_hits) hipLaunchKernelGGL((ip_scan16r_kernel<D, true>), grid, dim3(512), 0, s, a);
-    else hipLaunchKernelGGL((ip_scan16r_kernel<D, false, true>), grid, dim3(512), 0, s, a);
+    // d > 768: the rolled reads hold two tiles' fragments beside the queries' (2 x d / 32 x 4 VGPRs +
+    // d / 32 x 4): that spills from d = 832, so wider rows take the same loop with the fragments read
+    // per k-step (ip_scan16_kernel: same MFMA order, identical results)
+    if (D > 768) {
+      if (dense_hits) hipLaunchKernelGGL((ip_scan16_kernel<D, SCAN_FILTER, 8, true>), grid, dim3(512), 0, s, a);
+      else hipLaunchKernelGGL((ip_scan16_kernel<D, SCAN_FILTER, 8, false>), grid, dim3(512), 0, s, a);
+    } else if (dense_hits) {
+      hipLaunchKernelGGL((ip_scan16r_kernel<D, true>), grid, dim3(512), 0, s, a);
+    } else {
+      hipLaunchKernelGGL((ip_scan16r_kernel<D, false, true>), grid, dim3(512), 0, s, a);
+    }
   } else {
     hipLaunchKernelGGL((ip_scan16_kernel<D, SCAN_DENSE>), grid, dim3(512), 0, s, a);
   }
