@@ -10,7 +10,8 @@ cd $R
 timeout -k 10 600 python -u -m pytest -m gpu -v -rfE --timeout 300 --timeout-method thread \
   tests/test_encoder_bwd_gpu.py tests/test_train_tower_gpu.py tests/test_golden_gpu.py \
   "tests/test_multirank_gpu.py::test_ddp_train_step_world2_matches_single_process" \
-  "tests/test_multirank_gpu.py::test_rrtrainer_evaluate_world2" tests/test_trainer_gpu.py > $OUT/b3_pytest.log 2>&1
+  "tests/test_multirank_gpu.py::test_rrtrainer_evaluate_world2" tests/test_trainer_gpu.py tests/test_encoder_gpu.py \
+  "tests/test_search_gpu.py::test_filter_scan_flavours_bit_exact" > $OUT/b3_pytest.log 2>&1
 rc=$?
 echo "pytest rc=$rc"; tail -4 $OUT/b3_pytest.log
 [ $rc -ne 0 ] && exit $rc
