@@ -57,6 +57,35 @@ __host__ __device__ __forceinline__ uint32_t drop_hash24(uint64_t seed, uint64_t
 }
 __host__ __device__ __forceinline__ uint32_t drop_threshold(float p) { return (uint32_t)(p * 16777216.0f); }
 
+// Attention-probability dropout (modeling_bert.py:195) is the one site with L x L decisions per
+// (sequence, head), so it draws two per hash and keeps the 64-bit arithmetic out of the per-element
+// path: row = (b * heads + head) * L + query gets a 32-bit row key from the 64-bit mixer above (once
+// per query row); key pair j = key >> 1 hashes to fmix32(row_key + j * 0x9E3779B9) (murmur3's
+// finaliser on a Weyl sequence: two 32-bit multiplies per pair); the low 16 bits decide the even key,
+// the high 16 the odd one; keep iff half >= p * 2^16.
+constexpr uint32_t kAttnPairStep = 0x9E3779B9u;
+__host__ __device__ __forceinline__ uint32_t attn_row_key(uint64_t seed, uint64_t site, uint64_t row) {
+  uint64_t x = row * 0x9E3779B97F4A7C15ull + seed + site * 0xBF58476D1CE4E5B9ull;
+  x ^= x >> 31;
+  x *= 0x94D049BB133111EBull;
+  x ^= x >> 29;
+  return (uint32_t)(x >> 32);
+}
+__host__ __device__ __forceinline__ uint32_t attn_mix(uint32_t h) {
+  h ^= h >> 16;
+  h *= 0x85EBCA6Bu;
+  h ^= h >> 13;
+  h *= 0xC2B2AE35u;
+  h ^= h >> 16;
+  return h;
+}
+__host__ __device__ __forceinline__ uint32_t attn_drop_threshold(float p) { return (uint32_t)(p * 65536.0f); }
+// keep decision of (row key, key) -- the per-element form of the pairwise draw
+__host__ __device__ __forceinline__ bool attn_keep(uint32_t row_key, int key, uint32_t thr16) {
+  const uint32_t hsh = attn_mix(row_key + (uint32_t)(key >> 1) * kAttnPairStep);
+  return ((key & 1) ? hsh >> 16 : hsh & 0xFFFFu) >= thr16;
+}
+
 // faiss pads rows that have fewer than k results with label -1 and the
 // lowest float (CMin<float>::neutral() == numeric_limits<float>::lowest()).
 constexpr float kPadScore = -3.402823466e+38f;

@@ -171,7 +171,7 @@ struct AttnArgs {
   float* lse;             // optional [B][heads][L]: log-sum-exp of each query's scaled, masked
                           // scores (what the attention backward needs to rebuild P)
   float drop_p;           // training: dropout of the attention probabilities (DROP kernels)
-  uint64_t seed, site;    //   mask = drop_hash24(seed, site, ((b * heads + head) * L + q) * L + key)
+  uint64_t seed, site;    //   keep = attn_keep(attn_row_key(seed, site, (b * heads + head) * L + q), key)
   uint32_t* drop_bits;    // optional [B][heads][L][ceil(L / 32)]: the keep mask, bit (key & 31) of word
                           //   (query, key >> 5) -- the backward reads it instead of re-hashing
 };
@@ -271,6 +271,8 @@ __global__ __launch_bounds__(NW * 64, (NW == 4 && !DROP) ? 4 : (NW <= 5 ? 3 : 2)
 #pragma unroll
       for (int e = 0; e < 16; ++e) o[t][e] = 0.0f;
     float m = -__builtin_inff(), l = 0.0f;
+    const uint32_t rowkey =
+        DROP ? attn_row_key(a.seed, a.site, ((uint64_t)b * a.heads + hd) * (uint64_t)L + (uint64_t)(qb * 32 + r)) : 0u;
 
     for (int kt = 0; kt < Lp; kt += 32) {
       // S^T tile: rows = keys kt.., cols = queries
@@ -303,18 +305,25 @@ __global__ __launch_bounds__(NW * 64, (NW == 4 && !DROP) ? 4 : (NW <= 5 ? 3 : 2)
       m = mn;
       if (DROP) {   // dropout of P after its normaliser: O = dropout(softmax) V
         const float inv = 1.0f / (1.0f - a.drop_p);
-        const uint32_t thr = drop_threshold(a.drop_p);
+        const uint32_t thr = attn_drop_threshold(a.drop_p);
         const int qq = qb * 32 + r;
-        const uint64_t base = (((uint64_t)b * a.heads + hd) * L + qq) * (uint64_t)L;
+        // this lane's keys kt + 8 g + 4 h + {0,1,2,3}: pairs kt / 2 + 4 g + 2 h + {0, 1}
+        const uint32_t pbase = rowkey + (uint32_t)((kt >> 1) + 2 * h) * kAttnPairStep;
         uint32_t m16 = 0;
 #pragma unroll
-        for (int e = 0; e < 16; ++e) {
-          const int kr = (e & 3) + 8 * (e >> 2) + 4 * h;
-          const int key = kt + kr;
-          const bool keep = key < L && drop_hash24(a.seed, a.site, base + key) >= thr;
-          m16 |= keep ? 1u << kr : 0u;
-          s[e] = keep ? s[e] * inv : 0.0f;
-        }
+        for (int g = 0; g < 4; ++g)
+#pragma unroll
+          for (int u2 = 0; u2 < 2; ++u2) {
+            const uint32_t hsh = attn_mix(pbase + (uint32_t)(4 * g + u2) * kAttnPairStep);
+#pragma unroll
+            for (int w = 0; w < 2; ++w) {
+              const int e = 4 * g + 2 * u2 + w;
+              const int kr = 8 * g + 4 * h + 2 * u2 + w;
+              const bool keep = kt + kr < L && (w ? hsh >> 16 : hsh & 0xFFFFu) >= thr;
+              m16 |= keep ? 1u << kr : 0u;
+              s[e] = keep ? s[e] * inv : 0.0f;
+            }
+          }
         if (a.drop_bits) {   // this query's 32 keep bits of the key tile: the two lane halves' 16 each
           const uint32_t word = m16 | __shfl_xor(m16, 32, 64);
           if (h == 0 && qq < L) a.drop_bits[(((int64_t)b * a.heads + hd) * L + qq) * (Lp / 32) + kt / 32] = word;

@@ -230,24 +230,34 @@ __global__ __launch_bounds__(256) void transpose_bf16_kernel(const __bf16* x, in
 
 // ---------------------------------------------------------------------------
 // Attention backward (BertSelfAttention, modeling_bert.py:164-204, under autograd), one
-// work-group (4 waves) per (sequence, head), L <= 160 (the reference recipe's p_max_len 156,
-// run.sh), head_dim 64.  With Qs = scale * Q (rounded to bf16 as the forward does),
-// S = Qs K^T + key bias, P = exp(S - lse):
+// work-group per (sequence, head), L <= 160 (the reference recipe's p_max_len 156, run.sh),
+// head_dim 64.  With Qs = scale * Q (rounded to bf16 as the forward does), S = Qs K^T + key bias,
+// P = exp(S - lse):
 //   Dv_q = sum_d dO[q][d] O[q][d];   dP = dO V^T;   dS = P (dP - Dv)
 //   dV = P^T dO;   dK = dS^T Qs;   dQ = scale * dS K.
-// LDS: Qs, K, V, dO row-major [Lp][64] (16-B chunk XOR (row >> 1) & 7, as the forward's
-// K image), read row-wise with ds_read_b128 (A / B operands along d) and column-wise with
-// ds_read_b64_tr_b16 (the B operands of dV = P^T dO, dK = dS^T Qs, dQ = dS K, along the
-// sequence: no transposed copies); one per-wave 32 x 32 scratch tile (80-B rows) turns the P
-// and then the dS accumulator (rows in registers) into A operands.  Phase 1: wave w owns key
-// blocks w, w + 4 (dK, dV over all query blocks); phase 2: wave w owns query blocks w, w + 4
-// (dQ over all key blocks, S and dP recomputed).  v_mfma_f32_32x32x16_bf16 throughout.
-// 76 KiB of LDS at L = 128 (two work-groups per CU), 92 KiB at L = 160.
+// With dropout, O = Pd V where Pd = mask P / (1 - p): dV takes Pd, and dS = P (mask dP / (1 - p) - Dv).
+// LDS: Qs, K, V, dO row-major [Lp][64] (16-B chunk XOR (row >> 1) & 7, as the forward's K image),
+// read row-wise with ds_read_b128 (operands along d) and column-wise with ds_read_b64_tr_b16 (the
+// B operands of dV, dK, dQ along the sequence: no transposed copies).  Each phase computes its
+// score tile in the orientation whose MFMA output layout IS the A operand of the next product,
+// so P / dS never go through LDS:
+//   phase 1 (wave = key block kbk, loop over query blocks):  S = Qs K^T and dP = dO V^T as
+//     [query rows (registers)][key (lane)] tiles; a lane then holds, for its key, 16 queries of the
+//     block -- exactly the A operand of dV = Pd^T dO and dK = dS^T Qs with the k (query) order
+//     permuted (8 (e >> 2) + 4 h + (e & 3)); the B operands are read in the same permuted row order
+//     with ds_read_b64_tr_b16 (rows base + 4 h .. + 3 and base + 8 + 4 h .. + 3).
+//   phase 2 (wave = query block, loop over key blocks): S^T = K Qs^T and dP^T = V dO^T as
+//     [key rows][query (lane)] tiles = the A operand of dQ = dS K (k = key, permuted likewise).
+// The key-block operands of phase 1 (K, V as B operands) and the query-block operands of phase 2
+// (Qs, dO) stay in registers for the whole phase.  Per-query values of phase 1 (lse, Dv, keep words)
+// are read as 16-B vectors, four queries at a time.  DROP: the forward's keep bits (drop_bits)
+// staged in LDS as [key block][query] words; C-ABI callers without them get the same words drawn
+// again from the pairwise hash (drt_common.h attn_row_key / attn_mix) while staging.
+// 32x32x16 MFMA: A lane (m = l & 31, h = l >> 5) holds A[m][k = 8h .. 8h + 7]; B lane (n, h) holds
+// B[k = 8h ..][n]; D lane (n = l & 31, h) holds D[m = 8 (e >> 2) + 4 h + (e & 3)][n].
 // ---------------------------------------------------------------------------
-constexpr int kAbThreads = 256;
 constexpr int kAbMaxSeq = 160;
 constexpr int kAbRow = 128;               // bytes per [.][64] bf16 row
-constexpr int kAbScr = 80;                // bytes per scratch row (32 bf16 + 16 B pad)
 
 
 struct AttnBwdArgs {
@@ -263,325 +273,13 @@ struct AttnBwdArgs {
   float drop_p;           // attention-probability dropout of the forward (0: none)
   uint64_t seed, site;
   const uint32_t* drop_bits;  // optional keep bits written by the forward ([B][heads][L][ceil(L/32)]);
-                              // NULL: the masks are regenerated from the hash
+                              // NULL: the same bits drawn again from the hash
 };
 
 __device__ __forceinline__ int ab_rc(int row, int chunk) { return row * kAbRow + ((chunk ^ ((row >> 1) & 7)) << 4); }
 
 typedef short ab_v4i16 __attribute__((ext_vector_type(4)));
 
-// 32x32x16 B operand along the SEQUENCE of a row-major [Lp][64] image: lane (c = lane & 31,
-// h = lane >> 5) gets rows row0 + 0..7 (row0 per lane: the caller's k block, 8 h apart) of
-// column col0 + c.  Two ds_read_b64_tr_b16 per operand: per 16-lane group, lane 4q + p
-// addresses row row0 + q (+ 4), columns col0 + 16 g + 4p .. + 3 of the swizzled image.
-__device__ __forceinline__ bf16x8 ab_tr8(const char* img, int row0, int col0, int lane) {
-  const int i = lane & 15, q = i >> 2, p = i & 3;
-  const int chunk = (col0 + 16 * ((lane >> 4) & 1) + 4 * p) >> 3;
-  const int lo = (p & 1) * 8;
-  const int r1 = row0 + q, r2 = r1 + 4;
-  typedef __attribute__((address_space(3))) ab_v4i16 lds_v4;
-  const ab_v4i16 x = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4*)(img + ab_rc(r1, chunk) + lo));
-  const ab_v4i16 y = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4*)(img + ab_rc(r2, chunk) + lo));
-  bf16x8 v;
-  __builtin_memcpy(&v, &x, 8);
-  __builtin_memcpy((char*)&v + 8, &y, 8);
-  return v;
-}
-
-// NW = waves per work-group: 4 for L <= 128 (one 32-row block per wave in each phase), 8 for
-// 129 <= L <= 160 (5 blocks: 4 waves ran wave 0 twice per phase while 3 waves idled); the LDS
-// (92-104 KiB at L = 160) allows one work-group per CU either way.  Bit-identical block math.
-// ABL (diagnostic builds only, drt_attention_force4(16 + ABL)): 1 skips phase 2, 2 skips phase 1,
-// 4 replaces the softmax exp by the raw score, 8 skips the P / dS stores to the wave's LDS scratch.
-template <int NW = 4, int ABL = 0>
-__global__ __launch_bounds__(NW * 64, NW == 4 ? 2 : 1) void attention_bwd_kernel(AttnBwdArgs a) {
-  constexpr int NT = NW * 64;
-  extern __shared__ __attribute__((aligned(16))) char smem[];
-  const int L = (int)a.L;
-  const int Lp = (L + 31) & ~31;
-  char* Qs = smem;                                   // [Lp][64]
-  char* Ks = Qs + Lp * kAbRow;
-  char* Vs = Ks + Lp * kAbRow;
-  char* Os = Vs + Lp * kAbRow;                       // dO
-  char* scr = Os + Lp * kAbRow;                      // [NW waves][32][80 B]
-  float* lse = (float*)(scr + NW * 32 * kAbScr);     // [Lp]
-  float* dv = lse + Lp;                              // [Lp]  Dv
-  float* kb = dv + Lp;                               // [Lp]  key bias
-  uint32_t* kbits = (uint32_t*)(kb + Lp);            // [Lp / 32][Lp] keep bits (drop_bits staged)
-
-  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
-  const int r = lane & 31, h = lane >> 5;
-  const int64_t b = blockIdx.x / a.heads;
-  const int hd = blockIdx.x % a.heads;
-  const int64_t row0 = b * a.L;
-  const int64_t ld = 3 * (int64_t)a.H;
-  const __bf16* Qg = a.qkv + row0 * ld + hd * 64;
-  const __bf16* Kg = Qg + a.H;
-  const __bf16* Vg = Qg + 2 * a.H;
-  const __bf16* Og = a.ctx + row0 * a.H + hd * 64;
-  const __bf16* dOg = a.dctx + row0 * a.H + hd * 64;
-
-  // ---- staging: row-major images (transposed operands are read with ds_read_b64_tr_b16).  All
-  // global loads of the work-group's rows are issued before the first LDS store (up to MAXIT
-  // 16-B chunks of each of Q, K, V, dO, O per thread), so the HBM latency is paid once, not once
-  // per pass.  Lp * 8 is a multiple of 256: the pass predicate is wave-uniform.
-  {
-    constexpr int MAXIT = (kAbMaxSeq * 8 + NT - 1) / NT;
-    bf16x8 q[MAXIT], k[MAXIT], v[MAXIT], o[MAXIT], oo[MAXIT];
-#pragma unroll
-    for (int it = 0; it < MAXIT; ++it) {
-      const int i = tid + it * NT;
-      const int row = i >> 3, c = i & 7;
-      q[it] = bf16x8{};
-      k[it] = bf16x8{};
-      v[it] = bf16x8{};
-      o[it] = bf16x8{};
-      oo[it] = bf16x8{};
-      if (i < Lp * 8 && row < L) {
-        q[it] = *(const bf16x8*)(Qg + (int64_t)row * ld + c * 8);
-        k[it] = *(const bf16x8*)(Kg + (int64_t)row * ld + c * 8);
-        v[it] = *(const bf16x8*)(Vg + (int64_t)row * ld + c * 8);
-        o[it] = *(const bf16x8*)(dOg + (int64_t)row * a.H + c * 8);
-        oo[it] = *(const bf16x8*)(Og + (int64_t)row * a.H + c * 8);
-      }
-    }
-#pragma unroll
-    for (int it = 0; it < MAXIT; ++it) {
-      const int i = tid + it * NT;
-      if (i >= Lp * 8) break;
-      const int row = i >> 3, c = i & 7;
-      float part = 0.f;
-#pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        q[it][j] = (__bf16)((float)q[it][j] * a.scale);
-        part += (float)o[it][j] * (float)oo[it][j];
-      }
-      *(bf16x8*)(Qs + ab_rc(row, c)) = q[it];
-      *(bf16x8*)(Ks + ab_rc(row, c)) = k[it];
-      *(bf16x8*)(Vs + ab_rc(row, c)) = v[it];
-      *(bf16x8*)(Os + ab_rc(row, c)) = o[it];
-      // Dv: the 8 chunk-partials of one row sit in 8 consecutive lanes
-      part += __shfl_xor(part, 1, 64);
-      part += __shfl_xor(part, 2, 64);
-      part += __shfl_xor(part, 4, 64);
-      if (c == 0) dv[row] = part;
-    }
-  }
-  for (int i = tid; i < Lp; i += NT) {
-    float bv = 0.0f;
-    if (i >= L) bv = -3.402823466e+38f;
-    else if (a.mask && a.mask[b * a.L + i] == 0) bv = -3.402823466e+38f;
-    kb[i] = bv;
-    lse[i] = i < L ? a.lse[((int64_t)b * a.heads + hd) * a.L + i] : 0.0f;
-  }
-  const bool bits = a.drop_bits != nullptr && a.drop_p > 0.0f;
-  if (bits) {   // [query][key block] words of the forward -> [key block][query] (both phases read rows)
-    const int nkb = Lp / 32;
-    const uint32_t* src = a.drop_bits + ((int64_t)b * a.heads + hd) * a.L * nkb;
-    for (int i = tid; i < nkb * Lp; i += NT) {
-      const int q = i / nkb, kbi = i - q * nkb;
-      kbits[kbi * Lp + q] = q < L ? src[(int64_t)q * nkb + kbi] : 0u;
-    }
-  }
-  __syncthreads();
-
-  const int nblk = Lp / 32;
-  const bool drop = a.drop_p > 0.0f;
-  const float inv = drop ? 1.0f / (1.0f - a.drop_p) : 1.0f;
-  const uint32_t thr = drop_threshold(a.drop_p);
-  char* sT = scr + wave * 32 * kAbScr;   // P, then dS (phase 1); dS (phase 2)
-
-  // ---- phase 1: dK, dV for key block kbk (rows = keys in the D layout, cols = q / d)
-  for (int kbk = wave; !(ABL & 2) && kbk < nblk; kbk += NW) {
-    f32x16 dK[2], dV[2];
-#pragma unroll
-    for (int t = 0; t < 2; ++t)
-#pragma unroll
-      for (int e = 0; e < 16; ++e) {
-        dK[t][e] = 0.f;
-        dV[t][e] = 0.f;
-      }
-    const int key = kbk * 32 + r;   // A-operand row of this lane
-    for (int qb = 0; qb < nblk; ++qb) {
-      const int qcol = qb * 32 + r; // B-operand column of this lane
-      f32x16 st = {}, dpt = {};
-#pragma unroll
-      for (int e = 0; e < 16; ++e) {
-        st[e] = 0.f;
-        dpt[e] = 0.f;
-      }
-#pragma unroll
-      for (int k4 = 0; k4 < 4; ++k4) {
-        const int c = 2 * k4 + h;
-        const bf16x8 ka = *(const bf16x8*)(Ks + ab_rc(key, c));
-        const bf16x8 qbv = *(const bf16x8*)(Qs + ab_rc(qcol, c));
-        st = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ka, qbv, st, 0, 0, 0);
-        const bf16x8 va = *(const bf16x8*)(Vs + ab_rc(key, c));
-        const bf16x8 ob = *(const bf16x8*)(Os + ab_rc(qcol, c));
-        dpt = __builtin_amdgcn_mfma_f32_32x32x16_bf16(va, ob, dpt, 0, 0, 0);
-      }
-      // P^T, dS^T: row = key kbk*32 + (e&3) + 8(e>>2) + 4h, column = query qcol.  With dropout,
-      // O = Pd V where Pd = mask P / (1 - p): dV takes Pd, and dS = P (mask dPd / (1 - p) - Dv)
-      const float lq = lse[qcol], dq = dv[qcol];
-      const uint64_t dbase = (((uint64_t)b * a.heads + hd) * L + qcol) * (uint64_t)L;
-      const uint32_t wbits = bits ? kbits[kbk * Lp + qcol] : 0u;
-      float ds[16];
-#pragma unroll
-      for (int e = 0; e < 16; ++e) {
-        const int kr = (e & 3) + 8 * (e >> 2) + 4 * h;
-        const float p = (ABL & 4) ? st[e] : __expf(st[e] + kb[kbk * 32 + kr] - lq);
-        float pd = p, dpe = dpt[e];
-        if (drop) {
-          const int key = kbk * 32 + kr;
-          const bool keep = bits ? ((wbits >> kr) & 1u) != 0u
-                                 : key < L && qcol < L && drop_hash24(a.seed, a.site, dbase + key) >= thr;
-          pd = keep ? p * inv : 0.f;
-          dpe = keep ? dpe * inv : 0.f;
-        }
-        ds[e] = p * (dpe - dq);
-        if (!(ABL & 8)) *(__bf16*)(sT + kr * kAbScr + r * 2) = (__bf16)pd;
-      }
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-      __builtin_amdgcn_wave_barrier();
-#pragma unroll
-      for (int ks = 0; ks < 2; ++ks) {
-        const bf16x8 pa = *(const bf16x8*)(sT + r * kAbScr + (2 * ks + h) * 16);
-        const int qc = qb * 32 + 16 * ks + 8 * h;
-#pragma unroll
-        for (int t = 0; t < 2; ++t) {
-          const bf16x8 ob = ab_tr8(Os, qc, 32 * t, lane);
-          dV[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(pa, ob, dV[t], 0, 0, 0);
-        }
-      }
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-      __builtin_amdgcn_wave_barrier();
-#pragma unroll
-      for (int e = 0; e < 16; ++e) {
-        const int kr = (e & 3) + 8 * (e >> 2) + 4 * h;
-        if (!(ABL & 8)) *(__bf16*)(sT + kr * kAbScr + r * 2) = (__bf16)ds[e];
-      }
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-      __builtin_amdgcn_wave_barrier();
-#pragma unroll
-      for (int ks = 0; ks < 2; ++ks) {
-        const bf16x8 sa = *(const bf16x8*)(sT + r * kAbScr + (2 * ks + h) * 16);
-        const int qc = qb * 32 + 16 * ks + 8 * h;
-#pragma unroll
-        for (int t = 0; t < 2; ++t) {
-          const bf16x8 qbt = ab_tr8(Qs, qc, 32 * t, lane);
-          dK[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(sa, qbt, dK[t], 0, 0, 0);
-        }
-      }
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-      __builtin_amdgcn_wave_barrier();
-    }
-    // dK / dV [key][d]: row = key (regs), column d = 32 t + r (lanes)
-#pragma unroll
-    for (int e = 0; e < 16; ++e) {
-      const int kr = kbk * 32 + (e & 3) + 8 * (e >> 2) + 4 * h;
-      if (kr < L) {
-        __bf16* dst = a.dqkv + (row0 + kr) * ld + hd * 64;
-#pragma unroll
-        for (int t = 0; t < 2; ++t) {
-          dst[a.H + 32 * t + r] = (__bf16)dK[t][e];
-          dst[2 * a.H + 32 * t + r] = (__bf16)dV[t][e];
-        }
-      }
-    }
-  }
-
-  // ---- phase 2: dQ for query block qbq (rows = queries, cols = keys / d)
-  for (int qbq = wave; !(ABL & 1) && qbq < nblk; qbq += NW) {
-    f32x16 dQ[2];
-#pragma unroll
-    for (int t = 0; t < 2; ++t)
-#pragma unroll
-      for (int e = 0; e < 16; ++e) dQ[t][e] = 0.f;
-    const int qrow = qbq * 32 + r;
-    for (int kbk = 0; kbk < nblk; ++kbk) {
-      const int kcol = kbk * 32 + r;
-      f32x16 sv = {}, dp = {};
-#pragma unroll
-      for (int e = 0; e < 16; ++e) {
-        sv[e] = 0.f;
-        dp[e] = 0.f;
-      }
-#pragma unroll
-      for (int k4 = 0; k4 < 4; ++k4) {
-        const int c = 2 * k4 + h;
-        const bf16x8 qa = *(const bf16x8*)(Qs + ab_rc(qrow, c));
-        const bf16x8 kbv = *(const bf16x8*)(Ks + ab_rc(kcol, c));
-        sv = __builtin_amdgcn_mfma_f32_32x32x16_bf16(qa, kbv, sv, 0, 0, 0);
-        const bf16x8 oa = *(const bf16x8*)(Os + ab_rc(qrow, c));
-        const bf16x8 vb = *(const bf16x8*)(Vs + ab_rc(kcol, c));
-        dp = __builtin_amdgcn_mfma_f32_32x32x16_bf16(oa, vb, dp, 0, 0, 0);
-      }
-      const float kbias = kb[kcol];
-      // keep bits of this lane's key column for its 16 queries: 4 x 4 consecutive query words
-      u32x4 wq[4] = {};
-      if (bits) {
-#pragma unroll
-        for (int g = 0; g < 4; ++g) wq[g] = *(const u32x4*)(kbits + kbk * Lp + qbq * 32 + 8 * g + 4 * h);
-      }
-#pragma unroll
-      for (int e = 0; e < 16; ++e) {
-        const int qr = (e & 3) + 8 * (e >> 2) + 4 * h;
-        const int q = qbq * 32 + qr;
-        const float p = (ABL & 4) ? sv[e] : __expf(sv[e] + kbias - lse[q]);
-        float dpe = dp[e];
-        if (drop) {
-          const uint64_t idx = (((uint64_t)b * a.heads + hd) * L + q) * (uint64_t)L + kcol;
-          const bool keep = bits ? ((wq[e >> 2][e & 3] >> r) & 1u) != 0u
-                                 : kcol < L && q < L && drop_hash24(a.seed, a.site, idx) >= thr;
-          dpe = keep ? dpe * inv : 0.f;
-        }
-        if (!(ABL & 8)) *(__bf16*)(sT + qr * kAbScr + r * 2) = (__bf16)(p * (dpe - dv[q]));
-      }
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-      __builtin_amdgcn_wave_barrier();
-#pragma unroll
-      for (int ks = 0; ks < 2; ++ks) {
-        const bf16x8 sa = *(const bf16x8*)(sT + r * kAbScr + (2 * ks + h) * 16);
-        const int kc = kbk * 32 + 16 * ks + 8 * h;
-#pragma unroll
-        for (int t = 0; t < 2; ++t) {
-          const bf16x8 kt = ab_tr8(Ks, kc, 32 * t, lane);
-          dQ[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(sa, kt, dQ[t], 0, 0, 0);
-        }
-      }
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-      __builtin_amdgcn_wave_barrier();
-    }
-#pragma unroll
-    for (int e = 0; e < 16; ++e) {
-      const int qr = qbq * 32 + (e & 3) + 8 * (e >> 2) + 4 * h;
-      if (qr < L) {
-        __bf16* dst = a.dqkv + (row0 + qr) * ld + hd * 64;
-#pragma unroll
-        for (int t = 0; t < 2; ++t) dst[32 * t + r] = (__bf16)(dQ[t][e] * a.scale);
-      }
-    }
-  }
-}
-
-// ---------------------------------------------------------------------------
-// Attention backward, register-resident P / dS (round 3).  Same math and LDS images as
-// attention_bwd_kernel, but each phase computes its score tile in the orientation whose MFMA
-// output layout IS the A operand of the next product, so P / dS never go through LDS:
-//   phase 1 (wave = key block kbk, loop over query blocks):  S = Qs K^T and dP = dO V^T as
-//     [query rows (registers)][key (lane)] tiles; a lane then holds, for its key, 16 queries of the
-//     block -- exactly the A operand of dV = Pd^T dO and dK = dS^T Qs with the k (query) order
-//     permuted (8 (e >> 2) + 4 h + (e & 3)); the B operands are read in the same permuted row order
-//     with ds_read_b64_tr_b16 (rows base + 4 h .. + 3 and base + 8 + 4 h .. + 3).
-//   phase 2 (wave = query block, loop over key blocks): S^T = K Qs^T and dP^T = V dO^T as
-//     [key rows][query (lane)] tiles = the A operand of dQ = dS K (k = key, permuted likewise).
-// The key-block operands of phase 1 (K, V as B operands) and the query-block operands of phase 2
-// (Qs, dO) stay in registers for the whole phase.  Per-query values of phase 1 (lse, Dv, keep words)
-// are read as 16-B vectors, four queries at a time.  DROP: the forward's keep bits (drop_bits)
-// staged in LDS as [key block][query] words -- no hashing here at all.
-// 32x32x16 MFMA: A lane (m = l & 31, h = l >> 5) holds A[m][k = 8h .. 8h + 7]; B lane (n, h) holds
-// B[k = 8h ..][n]; D lane (n = l & 31, h) holds D[m = 8 (e >> 2) + 4 h + (e & 3)][n].
-// ---------------------------------------------------------------------------
 __device__ __forceinline__ bf16x8 ab_tr8p(const char* img, int rowA, int rowB, int col0, int lane) {
   const int i = lane & 15, q = i >> 2, p = i & 3;
   const int chunk = (col0 + 16 * ((lane >> 4) & 1) + 4 * p) >> 3;
@@ -623,11 +321,18 @@ __global__ __launch_bounds__(NW * 64, NW == 4 ? 2 : 1) void attention_bwd_rk_ker
   const __bf16* Og = a.ctx + row0 * a.H + hd * 64;
   const __bf16* dOg = a.dctx + row0 * a.H + hd * 64;
 
-  // ---- staging (as attention_bwd_kernel): every global load of the work-group's rows in flight
-  // before the first LDS store
+  // ---- staging: every global load of the work-group (the rows of Q, K, V, dO, O, and the per-row
+  // lse, mask and keep words) in flight before the first LDS store -- one latency round, which is
+  // exposed whenever one work-group holds the CU (L > 128)
   {
     constexpr int MAXIT = (kAbMaxSeq * 8 + NT - 1) / NT;
+    constexpr int MAXS = (kAbMaxSeq + NT - 1) / NT;                 // per-row values per thread
+    constexpr int MAXW = DROP ? (kAbMaxSeq / 32 * kAbMaxSeq + NT - 1) / NT : 1;   // keep words
+    const int64_t hrow = ((int64_t)b * a.heads + hd) * a.L;
     bf16x8 q[MAXIT], k[MAXIT], v[MAXIT], o[MAXIT], oo[MAXIT];
+    float lsev[MAXS];
+    int64_t mk[MAXS];
+    uint32_t wd[MAXW];
 #pragma unroll
     for (int it = 0; it < MAXIT; ++it) {
       const int i = tid + it * NT;
@@ -644,6 +349,24 @@ __global__ __launch_bounds__(NW * 64, NW == 4 ? 2 : 1) void attention_bwd_rk_ker
         o[it] = *(const bf16x8*)(dOg + (int64_t)row * a.H + c * 8);
         oo[it] = *(const bf16x8*)(Og + (int64_t)row * a.H + c * 8);
       }
+    }
+#pragma unroll
+    for (int j = 0; j < MAXS; ++j) {
+      const int i = tid + j * NT;
+      lsev[j] = 0.0f;
+      mk[j] = 1;
+      if (i < L) {
+        lsev[j] = a.lse[hrow + i];
+        if (a.mask) mk[j] = a.mask[b * a.L + i];
+      }
+    }
+    // [query][key block] words of the forward, read in their own order (coalesced)
+    const uint32_t* src = DROP && a.drop_bits ? a.drop_bits + hrow * nblk : nullptr;
+#pragma unroll
+    for (int j = 0; j < MAXW; ++j) {
+      const int i = tid + j * NT;
+      wd[j] = 0u;
+      if (src && i < L * nblk) wd[j] = src[i];
     }
 #pragma unroll
     for (int it = 0; it < MAXIT; ++it) {
@@ -665,19 +388,34 @@ __global__ __launch_bounds__(NW * 64, NW == 4 ? 2 : 1) void attention_bwd_rk_ker
       part += __shfl_xor(part, 4, 64);
       if (c == 0) dv[row] = part;
     }
-  }
-  for (int i = tid; i < Lp; i += NT) {
-    float bv = 0.0f;
-    if (i >= L) bv = -3.402823466e+38f;
-    else if (a.mask && a.mask[b * a.L + i] == 0) bv = -3.402823466e+38f;
-    kb[i] = bv;
-    lse[i] = i < L ? a.lse[((int64_t)b * a.heads + hd) * a.L + i] : 0.0f;
-  }
-  if (DROP) {   // [query][key block] words of the forward -> [key block][query]
-    const uint32_t* src = a.drop_bits + ((int64_t)b * a.heads + hd) * a.L * nblk;
-    for (int i = tid; i < nblk * Lp; i += NT) {
-      const int q = i / nblk, kbi = i - q * nblk;
-      kbits[kbi * Lp + q] = q < L ? src[(int64_t)q * nblk + kbi] : 0u;
+#pragma unroll
+    for (int j = 0; j < MAXS; ++j) {
+      const int i = tid + j * NT;
+      if (i < Lp) {
+        kb[i] = (i >= L || mk[j] == 0) ? -3.402823466e+38f : 0.0f;   // (1 - mask) * finfo.min
+        lse[i] = lsev[j];
+      }
+    }
+    if (DROP) {   // -> [key block][query]; without the forward's words (drop_bits NULL) the same
+                  // words are drawn again from the pairwise hash
+      const uint32_t thr = attn_drop_threshold(a.drop_p);
+#pragma unroll
+      for (int j = 0; j < MAXW; ++j) {
+        const int i = tid + j * NT;
+        if (i >= nblk * Lp) break;
+        const int qq = i / nblk, kbi = i - qq * nblk;
+        uint32_t w = wd[j];
+        if (!src && qq < L) {
+          const uint32_t rk = attn_row_key(a.seed, a.site, (uint64_t)(hrow + qq));
+          for (int jj = 0; jj < 16; ++jj) {
+            const uint32_t hsh = attn_mix(rk + (uint32_t)(kbi * 16 + jj) * kAttnPairStep);
+            const int key = kbi * 32 + 2 * jj;
+            w |= (key < L && (hsh & 0xFFFFu) >= thr) ? 1u << (2 * jj) : 0u;
+            w |= (key + 1 < L && (hsh >> 16) >= thr) ? 2u << (2 * jj) : 0u;
+          }
+        }
+        kbits[kbi * Lp + qq] = qq < L ? w : 0u;
+      }
     }
   }
   __syncthreads();
@@ -1021,43 +759,23 @@ int drt_attention_train_bwd_bits_bf16(const void* qkv, const void* ctx, const vo
                 heads, heads * 64, scale, drop_p, seed, site, drop_bits};
   const int Lp = ((int)L + 31) & ~31;
   const bool w8 = Lp / 32 > 4;
-  const int nw = w8 ? 8 : 4;
   const dim3 grid((unsigned)(B * heads));
   const bool drop = drop_p > 0.0f;
-  if (!drop || drop_bits) {
-    // register-resident P / dS; dropout from the forward's keep bits
-    const size_t lds = (size_t)4 * Lp * kAbRow + (size_t)3 * Lp * 4 + (drop ? (size_t)(Lp / 32) * Lp * 4 : 0);
-    DRT_REQUIRE(lds <= 160 * 1024);
-    static bool rk_attr = false;
-    if (!rk_attr) {
-      const void* ks[] = {(const void*)attention_bwd_rk_kernel<4, false>, (const void*)attention_bwd_rk_kernel<4, true>,
-                          (const void*)attention_bwd_rk_kernel<8, false>, (const void*)attention_bwd_rk_kernel<8, true>};
-      for (const void* f : ks) DRT_CHECK_HIP(hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
-      rk_attr = true;
-    }
-    hipStream_t st = (hipStream_t)stream;
-    if (w8 && drop) hipLaunchKernelGGL((attention_bwd_rk_kernel<8, true>), grid, dim3(512), lds, st, a);
-    else if (w8) hipLaunchKernelGGL((attention_bwd_rk_kernel<8, false>), grid, dim3(512), lds, st, a);
-    else if (drop) hipLaunchKernelGGL((attention_bwd_rk_kernel<4, true>), grid, dim3(256), lds, st, a);
-    else hipLaunchKernelGGL((attention_bwd_rk_kernel<4, false>), grid, dim3(256), lds, st, a);
-    return hip_status(hipGetLastError());
-  }
-  // dropout masks regenerated from the hash (C-ABI callers without the forward's bits)
-  const size_t lds = (size_t)4 * Lp * kAbRow + (size_t)nw * 32 * kAbScr + (size_t)3 * Lp * 4;
+  // register-resident P / dS; dropout from the forward's keep bits (or the same bits drawn again)
+  const size_t lds = (size_t)4 * Lp * kAbRow + (size_t)3 * Lp * 4 + (drop ? (size_t)(Lp / 32) * Lp * 4 : 0);
   DRT_REQUIRE(lds <= 160 * 1024);
-  static bool attr_set = false;
-  if (!attr_set) {
-    DRT_CHECK_HIP(hipFuncSetAttribute((const void*)attention_bwd_kernel<4>,
-                                      hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
-    DRT_CHECK_HIP(hipFuncSetAttribute((const void*)attention_bwd_kernel<8>,
-                                      hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
-    attr_set = true;
+  static bool rk_attr = false;
+  if (!rk_attr) {
+    const void* ks[] = {(const void*)attention_bwd_rk_kernel<4, false>, (const void*)attention_bwd_rk_kernel<4, true>,
+                        (const void*)attention_bwd_rk_kernel<8, false>, (const void*)attention_bwd_rk_kernel<8, true>};
+    for (const void* f : ks) DRT_CHECK_HIP(hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
+    rk_attr = true;
   }
-  if (w8) {
-    hipLaunchKernelGGL((attention_bwd_kernel<8>), grid, dim3(512), lds, (hipStream_t)stream, a);
-  } else {
-    hipLaunchKernelGGL((attention_bwd_kernel<4>), grid, dim3(256), lds, (hipStream_t)stream, a);
-  }
+  hipStream_t st = (hipStream_t)stream;
+  if (w8 && drop) hipLaunchKernelGGL((attention_bwd_rk_kernel<8, true>), grid, dim3(512), lds, st, a);
+  else if (w8) hipLaunchKernelGGL((attention_bwd_rk_kernel<8, false>), grid, dim3(512), lds, st, a);
+  else if (drop) hipLaunchKernelGGL((attention_bwd_rk_kernel<4, true>), grid, dim3(256), lds, st, a);
+  else hipLaunchKernelGGL((attention_bwd_rk_kernel<4, false>), grid, dim3(256), lds, st, a);
   return hip_status(hipGetLastError());
 }
 

@@ -15,8 +15,9 @@ producing fp32 gradients for every HF parameter (QKV split back into query/key/v
 Dropout as HF applies it in train mode (embeddings output, attention probabilities, both
 sublayer outputs before their residual add; hidden_dropout_prob / attention_probs_dropout_prob):
 each keep is a counter-based hash of (per-call seed, site, element index) (csrc/drt_common.h
-drop_hash24), so the backward regenerates the forward's masks instead of storing them; the
-seed comes from torch's CPU generator (``torch.manual_seed`` makes a step reproducible).  The
+drop_hash24; the attention probabilities draw two keeps per 32-bit hash of (row key, key pair),
+attn_row_key / attn_mix), so the backward regenerates the hidden-site masks instead of storing them
+and reads the attention keep bits the forward wrote (1 bit per probability); the seed comes from torch's CPU generator (``torch.manual_seed`` makes a step reproducible).  The
 masks are not HF's Philox stream: same distribution and semantics, different draws.
 Scope: L <= 160 (the reference recipe's p_max_len is 156, run.sh), erf GELU, head_dim 64; anything else
 raises.

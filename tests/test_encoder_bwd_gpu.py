@@ -353,12 +353,13 @@ def test_layernorm_bwd_drop_output_equals_dropout_kernel(dev, M, H):
 @pytest.mark.parametrize("L,B", [(128, 6), (156, 5), (37, 9), (32, 4)])
 def test_attention_dropout_bits_vs_hash_and_torch(dev, L, B):
     """drt_attention_train_fwd_bits_bf16 writes the attention-dropout keep mask as bits (the forward's
-    outputs do not change, the bits are the hash's keep decisions); the backward that reads them (the
-    register-resident kernel) and the one that regenerates the hash (C-ABI callers without bits) both
-    match torch fp32 autograd of the same dropped attention."""
+    outputs do not change, the bits are the hash's keep decisions); the backward that reads them and
+    the one that draws the same bits again from the hash (C-ABI callers without bits) both
+    match torch fp32 autograd of the same dropped attention (the mask from the host restatement of the
+    pairwise attention hash)."""
     import torch
     from denseretrievaltoolkits_amd import _native
-    from tests.test_train_tower_gpu import _hash24_py, _keep_torch
+    from tests.test_train_tower_gpu import _attn_keep_py, _attn_keep_torch
     lib = _native.load()
     s = _native.stream_ptr(dev)
     heads, dh, p, seed, site = 12, 64, 0.1, 77, 3
@@ -386,9 +387,8 @@ def test_attention_dropout_bits_vs_hash_and_torch(dev, L, B):
         torch.cuda.synchronize()
         outs[use_bits] = (ctx, lse, dqkv, bits)
     assert torch.equal(outs[False][0], outs[True][0]) and torch.equal(outs[False][1], outs[True][1])
-    # torch fp32 reference with the same keep mask (host restatement of drop_hash24)
-    idx = torch.arange(B * heads * L * L, device=dev, dtype=torch.int64)
-    keep = _keep_torch(seed, site, idx, p).view(B, heads, L, L).float()
+    # torch fp32 reference with the same keep mask (host restatement of the attention hash)
+    keep = _attn_keep_torch(seed, site, B, heads, L, p, dev).float()
     x = qkv.float().requires_grad_(True)
     q = x[:, :H].view(B, L, heads, dh).transpose(1, 2)
     k = x[:, H:2 * H].view(B, L, heads, dh).transpose(1, 2)
@@ -408,8 +408,7 @@ def test_attention_dropout_bits_vs_hash_and_torch(dev, L, B):
     # the bits are the hash's keep decisions
     bb, hd = B - 1, heads // 2
     w = outs[True][3][bb, hd].cpu().numpy().astype(np.uint32)
-    thr = int(np.float32(p) * np.float32(16777216.0))
     for qq in (0, L // 2, L - 1):
         for key in range(L):
-            want = _hash24_py(seed, site, ((bb * heads + hd) * L + qq) * L + key) >= thr
+            want = _attn_keep_py(seed, site, (bb * heads + hd) * L + qq, key, p)
             assert bool((w[qq, key >> 5] >> (key & 31)) & 1) == want, (qq, key)

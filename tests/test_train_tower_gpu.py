@@ -113,6 +113,47 @@ def _keep_torch(seed, site, idx, p):
     return h >= int(np.float32(p) * np.float32(16777216.0))
 
 
+# attention-probability dropout (csrc/drt_common.h attn_row_key / attn_mix): two keep decisions per
+# 32-bit hash of (row key, key pair), 16-bit thresholds
+_G32, _F1, _F2 = 0x9E3779B9, 0x85EBCA6B, 0xC2B2AE35
+_M32 = (1 << 32) - 1
+
+
+def _attn_keep_py(seed, site, row, key, p):
+    x = (row * _C1 + seed + site * _C2) & _M64
+    x ^= x >> 31
+    x = (x * _C3) & _M64
+    x ^= x >> 29
+    h = ((x >> 32) + (key >> 1) * _G32) & _M32
+    h ^= h >> 16
+    h = (h * _F1) & _M32
+    h ^= h >> 13
+    h = (h * _F2) & _M32
+    h ^= h >> 16
+    half = (h >> 16) if key & 1 else (h & 0xFFFF)
+    return half >= int(np.float32(p) * np.float32(65536.0))
+
+
+def _attn_keep_torch(seed, site, B, heads, L, p, device):
+    """[B][heads][L query][L key] keep mask of the attention-probability dropout."""
+    import torch
+    row = torch.arange(B * heads * L, device=device, dtype=torch.int64)
+    x = row * _s64(_C1) + _s64(seed + site * _C2)
+    x = x ^ ((x >> 31) & ((1 << 33) - 1))
+    x = x * _s64(_C3)
+    x = x ^ ((x >> 29) & ((1 << 35) - 1))
+    rk = (x >> 32) & _M32
+    key = torch.arange(L, device=device, dtype=torch.int64)
+    h = (rk[:, None] + (key >> 1)[None, :] * _G32) & _M32
+    h = h ^ (h >> 16)
+    h = (h * _F1) & _M32
+    h = h ^ (h >> 13)
+    h = (h * _F2) & _M32
+    h = h ^ (h >> 16)
+    half = torch.where((key & 1).bool()[None, :], h >> 16, h & 0xFFFF)
+    return (half >= int(np.float32(p) * np.float32(65536.0))).view(B, heads, L, L)
+
+
 def test_dropout_kernel_mask_matches_restatement(dev):
     import torch
     from denseretrievaltoolkits_amd import _native
@@ -149,12 +190,15 @@ def _ref_forward_with_masks(m, ids, mask, ph, pa, seed):
     def drop(x, site, p, idx):
         return torch.where(_keep_torch(seed, site, idx, p), x / (1 - p), torch.zeros_like(x)) if p > 0 else x
 
+    def drop_probs(x, site, p):
+        keep = _attn_keep_torch(seed, site, B, nh, L, p, dev)
+        return torch.where(keep, x / (1 - p), torch.zeros_like(x)) if p > 0 else x
+
     e = m.embeddings
     x = e.word_embeddings(ids) + e.token_type_embeddings(torch.zeros_like(ids)) + \
         e.position_embeddings(torch.arange(L, device=dev))[None]
     x = drop(F.layer_norm(x, (H,), e.LayerNorm.weight, e.LayerNorm.bias, eps), 0, ph, flat)
     bias = (1 - mask[:, None, None, :].float()) * torch.finfo(torch.float32).min
-    pidx = torch.arange(B * nh * L * L, device=dev, dtype=torch.int64).view(B, nh, L, L)
     for i, layer in enumerate(m.encoder.layer):
         s_att, s1, s2 = dropout_sites(i)
         sa = layer.attention.self
@@ -162,7 +206,7 @@ def _ref_forward_with_masks(m, ids, mask, ph, pa, seed):
         k = sa.key(x).view(B, L, nh, dh).transpose(1, 2)
         v = sa.value(x).view(B, L, nh, dh).transpose(1, 2)
         probs = torch.softmax(q @ k.transpose(-1, -2) / dh ** 0.5 + bias, -1)
-        ctx = (drop(probs, s_att, pa, pidx) @ v).transpose(1, 2).reshape(B, L, H)
+        ctx = (drop_probs(probs, s_att, pa) @ v).transpose(1, 2).reshape(B, L, H)
         ao = layer.attention.output
         x1 = F.layer_norm(drop(ao.dense(ctx), s1, ph, flat) + x, (H,), ao.LayerNorm.weight, ao.LayerNorm.bias, eps)
         f = F.gelu(layer.intermediate.dense(x1))
