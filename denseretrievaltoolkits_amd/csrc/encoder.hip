@@ -179,10 +179,17 @@ struct AttnArgs {
 // NW = waves per work-group (the launcher uses 4; an 8-wave form for 5-8 query blocks measured
 // slower, see drt_attention_train_fwd_bf16).  Each block's arithmetic is the same whichever wave
 // runs it.
-// Occupancy: 4 work-groups per CU for the 4-wave inference kernel (<= 128 VGPRs); the dropout
-// kernels (hash + keep-bit words) need more registers, so 3 (<= 170 VGPRs: at 4 they spilled).
+// Occupancy: 4 work-groups per CU for the 4-wave inference kernel (<= 128 VGPRs); the 4-wave
+// dropout kernel (hash + keep-bit words) needs more registers, so 3 (<= 170 VGPRs: at 4 it spilled).
+// The 5-wave dropout kernel (L 129-160) at 4 work-groups per CU, i.e. <= 128 VGPRs with a few
+// spills, beat its spill-free 156-VGPR build (2 work-groups of 5 waves per CU) by 11 % at L 156
+// (467 -> 417 us, profiles/r03e_attn_probe_minb4.log); the 4-wave one at 4 lost 19 % at L 128.
+#ifndef DRT_ATTN_DROP5_MINB   // tools/build_variant.sh A/B
+#define DRT_ATTN_DROP5_MINB 4
+#endif
 template <bool DROP, int NW = 4>
-__global__ __launch_bounds__(NW * 64, (NW == 4 && !DROP) ? 4 : (NW <= 5 ? 3 : 2)) void attention_kernel(AttnArgs a) {
+__global__ __launch_bounds__(NW * 64, !DROP ? (NW == 4 ? 4 : (NW <= 5 ? 3 : 2)) : (NW == 5 ? DRT_ATTN_DROP5_MINB : 3))
+void attention_kernel(AttnArgs a) {
   constexpr int NT = NW * 64;
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int L = (int)a.L;

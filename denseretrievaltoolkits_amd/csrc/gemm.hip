@@ -159,9 +159,14 @@ __device__ __forceinline__ float epi_post(const GemmArgs& a, float v, int64_t ro
 constexpr int64_t kLargeMinTiles = 128;
 __host__ __device__ constexpr int auto_tile_order(int64_t k) { return k <= 1024 ? 1 : 0; }
 
-template <bool OUT_BF16, int EPI, bool PART = false>
-__global__ __launch_bounds__(kGemmThreads, 2) void gemm_nt_kernel(GemmArgs a) {
-  __shared__ __attribute__((aligned(16))) char smem[kGemmLds];
+// NS = LDS stages of 32 KiB (A + B K-tile): 2 = double buffer, 2 work-groups per CU (grids of
+// more than one round); 4 = a ring with two K-tiles in flight across each barrier (counted vmcnt,
+// raw s_barrier), one work-group per CU -- for grids of at most one round (query-sized batches),
+// where the double buffer's one-K-tile prefetch left every K-step waiting on an L2 round trip.
+template <bool OUT_BF16, int EPI, bool PART = false, int NS = 2>
+__global__ __launch_bounds__(kGemmThreads, NS == 2 ? 2 : 1) void gemm_nt_kernel(GemmArgs a) {
+  static_assert(NS == 2 || NS == 4, "stage counts with vmcnt immediates below");
+  __shared__ __attribute__((aligned(16))) char smem[NS * kStage];
   const int tid = threadIdx.x;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int lane = tid & 63;
@@ -197,21 +202,34 @@ __global__ __launch_bounds__(kGemmThreads, 2) void gemm_nt_kernel(GemmArgs a) {
 #pragma unroll
   for (int s = 0; s < 4; ++s) aoff[s] = r * 128 + ((((2 * s) | h) ^ sw) << 4);
 
-  stage_panel(a.A, a.lda, m0, a.m, kbeg, lds0, wave, lane);
-  stage_panel(a.B, a.ldb, n0, a.n, kbeg, lds0 + kTileA, wave, lane);
+  // one K-tile = 8 LDS-DMA wave-instructions per wave (4 of A, 4 of B)
+  auto stage_k = [&](int kt, int slot) {
+    const uint32_t nb = lds0 + slot * kStage;
+    stage_panel(a.A, a.lda, m0, a.m, kbeg + (int64_t)kt * kBK, nb, wave, lane);
+    stage_panel(a.B, a.ldb, n0, a.n, kbeg + (int64_t)kt * kBK, nb + kTileA, wave, lane);
+  };
+#pragma unroll
+  for (int st = 0; st < NS - 1; ++st)
+    if (st < ksteps) stage_k(st, st);
 
+  int slot = 0;
   for (int kt = 0; kt < ksteps; ++kt) {
-    const int slot = kt & 1;
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    if (NS == 2) {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    } else {   // K-tile kt landed; the (at most NS - 2) tiles issued after it may stay in flight
+      const int after = ksteps - 1 - kt;
+      if (after >= 2) asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
+      else if (after == 1) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+      else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
-    if (kt + 1 < ksteps) {
-      const uint32_t nb = lds0 + (slot ^ 1) * kStage;
-      stage_panel(a.A, a.lda, m0, a.m, kbeg + (int64_t)(kt + 1) * kBK, nb, wave, lane);
-      stage_panel(a.B, a.ldb, n0, a.n, kbeg + (int64_t)(kt + 1) * kBK, nb + kTileA, wave, lane);
-    }
+    // WAR: the slot staged here was last read in iteration kt - 1, whose reads every wave retired
+    // (lgkmcnt(0)) before the barrier above
+    if (kt + NS - 1 < ksteps) stage_k(kt + NS - 1, slot == 0 ? NS - 1 : slot - 1);
     const char* As = smem + slot * kStage + wm * 64 * 128;
     const char* Bs = smem + slot * kStage + kTileA + wn * 64 * 128;
+    slot = slot + 1 == NS ? 0 : slot + 1;
 #pragma unroll
     for (int s = 0; s < 4; ++s) {
       bf16x8 af[2], bfr[2];
@@ -241,6 +259,40 @@ __global__ __launch_bounds__(kGemmThreads, 2) void gemm_nt_kernel(GemmArgs a) {
         for (int e = 0; e < 16; ++e) {
           const int64_t row = m0 + wm * 64 + i * 32 + (e & 3) + 8 * (e >> 2) + 4 * h;
           if (row < a.m) wz[row * a.n + col] = acc[i][j][e];
+        }
+    }
+    return;
+  }
+  if (m0 + kBM <= a.m && n0 + kBN <= a.n) {
+    // full tile: every residual / GELU-input value is loaded before the first store and no element
+    // is guarded -- a guarded load per element made hipcc branch around each one and wait for its
+    // round trip (64 serial L2 / HBM round trips per thread in the epilogue)
+    float aux[2][2][16];
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int e = 0; e < 16; ++e) {
+          const int64_t row = m0 + wm * 64 + i * 32 + (e & 3) + 8 * (e >> 2) + 4 * h;
+          const int64_t col = n0 + wn * 64 + j * 32 + r;
+          aux[j][i][e] = (EPI & EPI_AUX) ? (float)a.R[row * a.ldr + col] : 0.f;
+        }
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const int64_t col = n0 + wn * 64 + j * 32 + r;
+      const float bv = (EPI & EPI_BIAS) ? a.bias[col] : 0.0f;
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int e = 0; e < 16; ++e) {
+          const int64_t row = m0 + wm * 64 + i * 32 + (e & 3) + 8 * (e >> 2) + 4 * h;
+          float v = acc[i][j][e] * a.alpha + bv;
+          if (EPI & EPI_PRE) ((__bf16*)a.C2)[row * a.ldc + col] = (__bf16)v;
+          if (EPI & EPI_GELU) v = gelu_erf(v);
+          v = epi_post<EPI>(a, v, row, col, aux[j][i][e]);
+          if (OUT_BF16) ((__bf16*)a.C)[row * a.ldc + col] = (__bf16)v;
+          else ((float*)a.C)[row * a.ldc + col] = v;
         }
     }
     return;
@@ -372,6 +424,9 @@ __global__ __launch_bounds__(256) void splitk_ln_kernel(const float* ws, int spl
 //   SMALL        everything else (and any split plan whose scratch the caller did not give)
 // ---------------------------------------------------------------------------
 constexpr int64_t kLSplitMinK = 8192, kLSplitKPer = 512, kSSplitCap = 16 << 20;
+#ifndef DRT_SMALL_SPLIT_BLOCKS   // blocks a SMALL_SPLIT grid aims at (tools/build_variant.sh A/B)
+#define DRT_SMALL_SPLIT_BLOCKS 512
+#endif
 enum GemmPath { GP_LARGE, GP_LARGE_SPLIT, GP_SMALL_SPLIT, GP_SMALL };
 struct GemmPlan {
   int path = GP_SMALL;
@@ -417,7 +472,7 @@ static int large_splits(int64_t m, int64_t n, int64_t k, int64_t* kchunk) {
 static int small_splits(int64_t m, int64_t n, int64_t k, int64_t* kchunk) {
   const int64_t tiles = ((m + kBM - 1) / kBM) * ((n + kBN - 1) / kBN);
   if (tiles >= 384 || k < 256) return 0;
-  int64_t splits = (512 + tiles - 1) / tiles;
+  int64_t splits = (DRT_SMALL_SPLIT_BLOCKS + tiles - 1) / tiles;
   if (splits > k / 128) splits = k / 128;
   const int64_t cap = kSSplitCap / (m * n * 4);
   if (splits > cap) splits = cap;
@@ -995,6 +1050,17 @@ static void launch_splitk_epi(const GemmArgs& a, int splits, hipStream_t s) {
   hipLaunchKernelGGL((splitk_epi_kernel<OUT_BF16, EPI>), dim3((unsigned)blocks), dim3(256), 0, s, a, splits);
 }
 
+// The 128^2 kernel: the 4-stage ring when the grid fits in one round of CUs (one block per CU),
+// the double buffer otherwise.  Same K order and MFMA sequence: bit-identical outputs.
+template <bool OUT_BF16, int EPI, bool PART>
+static void launch_small(const GemmArgs& a, int64_t tiles, int splits, hipStream_t s) {
+  const dim3 grid((unsigned)tiles, 1, (unsigned)splits);
+  if (tiles * splits <= gemm_cus())
+    hipLaunchKernelGGL((gemm_nt_kernel<OUT_BF16, EPI, PART, 4>), grid, dim3(kGemmThreads), 0, s, a);
+  else
+    hipLaunchKernelGGL((gemm_nt_kernel<OUT_BF16, EPI, PART, 2>), grid, dim3(kGemmThreads), 0, s, a);
+}
+
 template <bool OUT_BF16, int EPI>
 static int launch_gemm_t(const GemmArgs& a0, size_t ws_bytes, hipStream_t s) {
   GemmArgs a = a0;
@@ -1027,13 +1093,12 @@ static int launch_gemm_t(const GemmArgs& a0, size_t ws_bytes, hipStream_t s) {
     case GP_SMALL_SPLIT: {
       GemmArgs b = a;
       b.kchunk = p.kchunk;
-      hipLaunchKernelGGL((gemm_nt_kernel<OUT_BF16, EPI, true>), dim3((unsigned)tiles, 1, (unsigned)p.splits),
-                         dim3(kGemmThreads), 0, s, b);
+      launch_small<OUT_BF16, EPI, true>(b, tiles, p.splits, s);
       launch_splitk_epi<OUT_BF16, EPI>(b, p.splits, s);
       break;
     }
     default:
-      hipLaunchKernelGGL((gemm_nt_kernel<OUT_BF16, EPI>), dim3((unsigned)tiles), dim3(kGemmThreads), 0, s, a);
+      launch_small<OUT_BF16, EPI, false>(a, tiles, 1, s);
       break;
   }
   prof_end(pp, s);
@@ -1174,8 +1239,7 @@ extern "C" int drt_linear_ln_bf16_ws(const void* X, const void* W, const float* 
   b.order = auto_tile_order(K);
   const int64_t tiles = ceil_div(M, kBM) * ceil_div(N, kBN);
   const ProfPair pp = prof_begin(PROF_GEMM, s);
-  hipLaunchKernelGGL((gemm_nt_kernel<true, EPI_BIAS | EPI_RESID, true>), dim3((unsigned)tiles, 1, (unsigned)p.splits),
-                     dim3(kGemmThreads), 0, s, b);
+  launch_small<true, EPI_BIAS | EPI_RESID, true>(b, tiles, p.splits, s);
   const dim3 grid((unsigned)((M + 3) / 4));
   const int splits = p.splits;
   switch (N / 64) {

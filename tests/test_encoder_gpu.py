@@ -96,10 +96,13 @@ def test_linear_epilogues_vs_torch(dev):
 
 @pytest.mark.parametrize("M,N,K,flags", [(16384, 2304, 768, 0), (32768, 768, 3072, 2), (20000, 3072, 768, 1),
                                           (131072, 768, 768, 2), (65536, 768, 768, 4), (30000, 768, 3072, 4),
-                                          (4096, 768, 768, 4), (1000, 3072, 768, 1)])
+                                          (4096, 768, 768, 4), (1000, 3072, 768, 1), (8192, 768, 768, 4),
+                                          (4096, 768, 3072, 8)])
 def test_gemm_plans_vs_torch(dev, M, N, K, flags):
     """Every GEMM plan the shape selects (plan_gemm: whole-line 256^2 kernel from 128 tiles up,
-    128^2 kernel below) against torch fp32, with bias / GELU / fp32 or bf16 output / residual."""
+    128^2 kernel below -- its 4-stage ring for one-round grids, 4096 x 768, and its double buffer
+    beyond, 8192 x 768) against torch fp32, with bias / GELU / fp32 or bf16 output / residual
+    (flags 8, test-local: fp32 output + residual, no bias)."""
     import torch
     from denseretrievaltoolkits_amd import _native
     lib = _native.load()
@@ -108,15 +111,18 @@ def test_gemm_plans_vs_torch(dev, M, N, K, flags):
     w = (0.05 * torch.randn(N, K, generator=g, device=dev)).to(torch.bfloat16)
     b = torch.randn(N, generator=g, device=dev)
     # flags 4 (test-local): bf16 output + residual, the encoder's pre-LayerNorm sums
-    r = torch.randn(M, N, generator=g, device=dev).to(torch.bfloat16) if flags in (2, 4) else None
-    ref = x.float() @ w.float().T + b
+    r = torch.randn(M, N, generator=g, device=dev).to(torch.bfloat16) if flags in (2, 4, 8) else None
+    if flags == 8:
+        b = None
+        flags = 2
+    ref = x.float() @ w.float().T + (b if b is not None else 0.0)
     if flags == 1:
         ref = torch.nn.functional.gelu(ref)
     if r is not None:
         ref = ref + r.float()
     dt = torch.float32 if flags & 2 else torch.bfloat16
     out = torch.empty(M, N, dtype=dt, device=dev)
-    _native.check(lib.drt_linear_bf16(x.data_ptr(), w.data_ptr(), b.data_ptr(),
+    _native.check(lib.drt_linear_bf16(x.data_ptr(), w.data_ptr(), b.data_ptr() if b is not None else None,
                                       r.data_ptr() if r is not None else None, out.data_ptr(), M, N, K, flags & 3,
                                       _native.stream_ptr(dev)), "linear")
     tol = dict(atol=2e-3, rtol=1e-4) if dt == torch.float32 else dict(atol=3e-2, rtol=1e-2)
@@ -192,7 +198,7 @@ def test_split_k_linear_vs_unsplit_and_torch(dev, M, N, K, flags, resid):
     rp = r.data_ptr() if r is not None else None
     _native.check(lib.drt_linear_bf16_ws(x.data_ptr(), w.data_ptr(), b.data_ptr(), rp, o1.data_ptr(), M, N, K, flags,
                                          ws.data_ptr(), nb, s), "split")
-    _native.check(lib.drt_linear_bf16(x.data_ptr(), w.data_ptr(), b.data_ptr(), rp, o0.data_ptr(), M, N, K, flags, s),
+    _native.check(lib.drt_linear_bf16(x.data_ptr(), w.data_ptr(), b.data_ptr() if b is not None else None, rp, o0.data_ptr(), M, N, K, flags, s),
                   "unsplit")
     # too-small workspace: silently the unsplit kernel, same result as o0
     o2 = torch.empty(M, N, dtype=dt, device=dev)
