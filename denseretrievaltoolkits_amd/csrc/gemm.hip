@@ -418,14 +418,19 @@ __global__ __launch_bounds__(256) void splitk_ln_kernel(const float* ws, int spl
 //                ONE round of blocks (floor(CUs / tiles) splits; a ceiling put e.g. 9 tiles x 29
 //                splits = 261 blocks on 256 CUs and the launch took ~2x its one-round time),
 //                >= kLSplitKPer per split, fp32 partials <= 256 MiB, fixed-order reduction
-//   SMALL_SPLIT  query-sized problems (< 384 tiles of 128^2, K >= 256): 128^2 kernel, ~2 blocks
-//                per CU, >= 128 K per split, partials <= 16 MiB (at 4096 x 768 -- a 128-query
-//                batch -- 3 splits = 38 MB of partials measured slower than unsplit)
+//   SMALL_SPLIT  query-sized problems (< 384 tiles of 128^2, K >= 256): 128^2 kernel, splits to
+//                about DRT_SMALL_SPLIT_BLOCKS blocks, >= 128 K per split, partials <= 16 MiB (at
+//                4096 x 768 -- a 128-query batch -- 3 splits = 38 MB of partials measured slower
+//                than unsplit)
 //   SMALL        everything else (and any split plan whose scratch the caller did not give)
 // ---------------------------------------------------------------------------
 constexpr int64_t kLSplitMinK = 8192, kLSplitKPer = 512, kSSplitCap = 16 << 20;
-#ifndef DRT_SMALL_SPLIT_BLOCKS   // blocks a SMALL_SPLIT grid aims at (tools/build_variant.sh A/B)
-#define DRT_SMALL_SPLIT_BLOCKS 512
+// Blocks a SMALL_SPLIT grid aims at.  With the 4-stage ring kernel a block streams its K range
+// without waiting on each K-tile, so fewer, longer splits win: query tower at batch 8 (256 tokens)
+// 0.827 ms at 512, 0.756 at 32, 0.738 at 64, 0.753 at 96, 0.772 at 128, 0.943 unsplit
+// (profiles/r03f_query_encode_*, r03g_query_encode_*); batch 128 unchanged.  tools/build_variant.sh for A/B builds.
+#ifndef DRT_SMALL_SPLIT_BLOCKS
+#define DRT_SMALL_SPLIT_BLOCKS 64
 #endif
 enum GemmPath { GP_LARGE, GP_LARGE_SPLIT, GP_SMALL_SPLIT, GP_SMALL };
 struct GemmPlan {
