@@ -280,34 +280,64 @@ __device__ __forceinline__ int ab_rc(int row, int chunk) { return row * kAbRow +
 
 typedef short ab_v4i16 __attribute__((ext_vector_type(4)));
 
-__device__ __forceinline__ bf16x8 ab_tr8p(const char* img, int rowA, int rowB, int col0, int lane) {
-  const int i = lane & 15, q = i >> 2, p = i & 3;
-  const int chunk = (col0 + 16 * ((lane >> 4) & 1) + 4 * p) >> 3;
-  const int lo = (p & 1) * 8;
+// Per-lane LDS offsets of the fragment reads, fixed for the kernel: every row block starts at a
+// multiple of 32 rows, so the swizzle term (row >> 1) & 7 of a block's row never depends on the
+// block (16 blk = 0 mod 8).  A-operand rows (blk * 32 + r, chunk 2 k4 + h): offA[k4]; column-wise
+// B operands (ab_tr8p rows blk * 32 + 16 ks + 4 h + q and + 8, col0 = 32 t): offT[t][0 / 1].
+// A read of block blk is then img + blk * 4096 (+ ks * 2048) + offset: with NB a template
+// argument and the block loops unrolled, one VGPR + an immediate per read.
+struct AbOffsets {
+  int offA[4];
+  int offT[2][2];
+};
+__device__ __forceinline__ AbOffsets ab_offsets(int lane) {
+  AbOffsets o;
+  const int r = lane & 31, h = lane >> 5, sw = (r >> 1) & 7;
+#pragma unroll
+  for (int k4 = 0; k4 < 4; ++k4) o.offA[k4] = r * kAbRow + (((2 * k4 + h) ^ sw) << 4);
+  const int i = lane & 15, q = i >> 2, p = i & 3, b4 = (lane >> 4) & 1;
+  const int sx = 2 * h + (q >> 1), lo = (p & 1) * 8;
+#pragma unroll
+  for (int t = 0; t < 2; ++t) {
+    const int c = 4 * t + 2 * b4 + (p >> 1);
+    o.offT[t][0] = (q + 4 * h) * kAbRow + ((c ^ sx) << 4) + lo;
+    o.offT[t][1] = (q + 4 * h + 8) * kAbRow + ((c ^ (sx + 4)) << 4) + lo;
+  }
+  return o;
+}
+
+__device__ __forceinline__ bf16x8 ab_tr8o(const char* img, int off0, int off1) {
   typedef __attribute__((address_space(3))) ab_v4i16 lds_v4;
-  const ab_v4i16 x = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4*)(img + ab_rc(rowA + q, chunk) + lo));
-  const ab_v4i16 y = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4*)(img + ab_rc(rowB + q, chunk) + lo));
+  const ab_v4i16 x = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4*)(img + off0));
+  const ab_v4i16 y = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4*)(img + off1));
   bf16x8 v;
   __builtin_memcpy(&v, &x, 8);
   __builtin_memcpy((char*)&v + 8, &y, 8);
   return v;
 }
 
-template <int NW, bool DROP>
-__global__ __launch_bounds__(NW * 64, NW == 4 ? 2 : 1) void attention_bwd_rk_kernel(AttnBwdArgs a) {
+constexpr float kLog2e = 1.4426950408889634f;
+
+// NB = row blocks of 32 (Lp = 32 NB), NW = waves: one work-group per (sequence, head).
+// Exponentials as exp2(s log2e + kb2 - lse2) with the key bias and lse pre-scaled by log2e in
+// staging (one fma + one sub + v_exp per score); the dropout scale 1 / (1 - p) leaves the
+// per-element path: dS = P (keep ? dP : 0) / (1 - p) - P Dv is one fma on the kept dP, and
+// dV = (1 / (1 - p)) sum_q (keep P)^T dO scales the accumulator once at the store.
+template <int NB, bool DROP>
+__global__ __launch_bounds__((NB == 5 ? 8 : 4) * 64, NB == 5 ? 1 : 2) void attention_bwd_rk_kernel(AttnBwdArgs a) {
+  constexpr int NW = NB == 5 ? 8 : 4;
   constexpr int NT = NW * 64;
+  constexpr int Lp = NB * 32;
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int L = (int)a.L;
-  const int Lp = (L + 31) & ~31;
-  const int nblk = Lp / 32;
   char* Qs = smem;                                   // [Lp][64] (scaled Q)
   char* Ks = Qs + Lp * kAbRow;
   char* Vs = Ks + Lp * kAbRow;
   char* Os = Vs + Lp * kAbRow;                       // dO
-  float* lse = (float*)(Os + Lp * kAbRow);           // [Lp]
-  float* dv = lse + Lp;                              // [Lp]  Dv
-  float* kb = dv + Lp;                               // [Lp]  key bias
-  uint32_t* kbits = (uint32_t*)(kb + Lp);            // [nblk][Lp] keep words (DROP)
+  float* lse2 = (float*)(Os + Lp * kAbRow);          // [Lp]  lse * log2e
+  float* dv = lse2 + Lp;                             // [Lp]  Dv
+  float* kb2 = dv + Lp;                              // [Lp]  key bias * log2e
+  uint32_t* kbits = (uint32_t*)(kb2 + Lp);           // [NB][Lp] keep words (DROP)
 
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
   const int r = lane & 31, h = lane >> 5;
@@ -325,9 +355,9 @@ __global__ __launch_bounds__(NW * 64, NW == 4 ? 2 : 1) void attention_bwd_rk_ker
   // lse, mask and keep words) in flight before the first LDS store -- one latency round, which is
   // exposed whenever one work-group holds the CU (L > 128)
   {
-    constexpr int MAXIT = (kAbMaxSeq * 8 + NT - 1) / NT;
-    constexpr int MAXS = (kAbMaxSeq + NT - 1) / NT;                 // per-row values per thread
-    constexpr int MAXW = DROP ? (kAbMaxSeq / 32 * kAbMaxSeq + NT - 1) / NT : 1;   // keep words
+    constexpr int MAXIT = (Lp * 8 + NT - 1) / NT;
+    constexpr int MAXS = (Lp + NT - 1) / NT;                        // per-row values per thread
+    constexpr int MAXW = DROP ? (NB * Lp + NT - 1) / NT : 1;        // keep words
     const int64_t hrow = ((int64_t)b * a.heads + hd) * a.L;
     bf16x8 q[MAXIT], k[MAXIT], v[MAXIT], o[MAXIT], oo[MAXIT];
     float lsev[MAXS];
@@ -342,7 +372,20 @@ __global__ __launch_bounds__(NW * 64, NW == 4 ? 2 : 1) void attention_bwd_rk_ker
       v[it] = bf16x8{};
       o[it] = bf16x8{};
       oo[it] = bf16x8{};
+#ifdef DRT_AB_ABL_NOLOAD   // ablation builds (tools/build_variant.sh): staging without global reads
       if (i < Lp * 8 && row < L) {
+        for (int j = 0; j < 8; ++j) {
+          q[it][j] = (__bf16)(0.01f * ((row + j) % 7));
+          k[it][j] = (__bf16)(0.02f * ((row + 3 * j) % 5));
+          v[it][j] = (__bf16)(0.01f * ((row * j) % 9));
+          o[it][j] = (__bf16)(0.001f * ((row + j) % 3));
+          oo[it][j] = (__bf16)(0.01f * ((row + 2 * j) % 11));
+        }
+      }
+      if (false) {
+#else
+      if (i < Lp * 8 && row < L) {
+#endif
         q[it] = *(const bf16x8*)(Qg + (int64_t)row * ld + c * 8);
         k[it] = *(const bf16x8*)(Kg + (int64_t)row * ld + c * 8);
         v[it] = *(const bf16x8*)(Vg + (int64_t)row * ld + c * 8);
@@ -361,12 +404,12 @@ __global__ __launch_bounds__(NW * 64, NW == 4 ? 2 : 1) void attention_bwd_rk_ker
       }
     }
     // [query][key block] words of the forward, read in their own order (coalesced)
-    const uint32_t* src = DROP && a.drop_bits ? a.drop_bits + hrow * nblk : nullptr;
+    const uint32_t* src = DROP && a.drop_bits ? a.drop_bits + hrow * NB : nullptr;
 #pragma unroll
     for (int j = 0; j < MAXW; ++j) {
       const int i = tid + j * NT;
       wd[j] = 0u;
-      if (src && i < L * nblk) wd[j] = src[i];
+      if (src && i < L * NB) wd[j] = src[i];
     }
 #pragma unroll
     for (int it = 0; it < MAXIT; ++it) {
@@ -392,8 +435,8 @@ __global__ __launch_bounds__(NW * 64, NW == 4 ? 2 : 1) void attention_bwd_rk_ker
     for (int j = 0; j < MAXS; ++j) {
       const int i = tid + j * NT;
       if (i < Lp) {
-        kb[i] = (i >= L || mk[j] == 0) ? -3.402823466e+38f : 0.0f;   // (1 - mask) * finfo.min
-        lse[i] = lsev[j];
+        kb2[i] = (i >= L || mk[j] == 0) ? -3.402823466e+38f * kLog2e : 0.0f;   // (1 - mask) * finfo.min
+        lse2[i] = lsev[j] * kLog2e;
       }
     }
     if (DROP) {   // -> [key block][query]; without the forward's words (drop_bits NULL) the same
@@ -402,8 +445,8 @@ __global__ __launch_bounds__(NW * 64, NW == 4 ? 2 : 1) void attention_bwd_rk_ker
 #pragma unroll
       for (int j = 0; j < MAXW; ++j) {
         const int i = tid + j * NT;
-        if (i >= nblk * Lp) break;
-        const int qq = i / nblk, kbi = i - qq * nblk;
+        if (i >= NB * Lp) break;
+        const int qq = i / NB, kbi = i - qq * NB;
         uint32_t w = wd[j];
         if (!src && qq < L) {
           const uint32_t rk = attn_row_key(a.seed, a.site, (uint64_t)(hrow + qq));
@@ -421,17 +464,31 @@ __global__ __launch_bounds__(NW * 64, NW == 4 ? 2 : 1) void attention_bwd_rk_ker
   __syncthreads();
 
   const float inv = DROP ? 1.0f / (1.0f - a.drop_p) : 1.0f;
+  const AbOffsets off = ab_offsets(lane);
+  const uint32_t lanebit = 1u << r;
+  // NW >= NB: each wave owns at most one key block (phase 1) and one query block (phase 2).
+  // Outputs leave through LDS: dK / dV stay in registers (bf16) until every wave holds its phase-2
+  // operands, then go into the Qs / dO images (dead from there on); dQ goes into the K image once
+  // phase 2 is done; the work-group then writes whole 128-B rows with 16-B stores (12 per thread
+  // at L 128 instead of 96 two-byte stores per wave: the store issue, not the bytes, was the cost).
+#ifdef DRT_AB_ABL_NOPHASE
+  const bool act = false;
+#else
+  const bool act = wave < NB;
+#endif
+  const int blk = act ? wave : 0;
+  bf16x8 dKo[2][2], dVo[2][2];                        // [t][e >> 3]: element e of column 32 t + r
 
-  // ---- phase 1: dK, dV of key block kbk
-  for (int kbk = wave; kbk < nblk; kbk += NW) {
-    const int key = kbk * 32 + r;                     // this lane's key (D column / A row)
+  // ---- phase 1: dK, dV of key block blk
+  if (act) {
+    const int key = blk * 32 + r;                     // this lane's key (D column / A row)
     bf16x8 kf[4], vf[4];                              // B operands of S = Qs K^T, dP = dO V^T
 #pragma unroll
     for (int k4 = 0; k4 < 4; ++k4) {
-      kf[k4] = *(const bf16x8*)(Ks + ab_rc(key, 2 * k4 + h));
-      vf[k4] = *(const bf16x8*)(Vs + ab_rc(key, 2 * k4 + h));
+      kf[k4] = *(const bf16x8*)(Ks + blk * 4096 + off.offA[k4]);
+      vf[k4] = *(const bf16x8*)(Vs + blk * 4096 + off.offA[k4]);
     }
-    const float kbias = kb[key];
+    const float kbias = kb2[key];
     f32x16 dK[2], dV[2];
 #pragma unroll
     for (int t = 0; t < 2; ++t)
@@ -440,8 +497,8 @@ __global__ __launch_bounds__(NW * 64, NW == 4 ? 2 : 1) void attention_bwd_rk_ker
         dK[t][e] = 0.f;
         dV[t][e] = 0.f;
       }
-    for (int qb = 0; qb < nblk; ++qb) {
-      const int qrow = qb * 32 + r;                   // A-operand row (query) of this lane
+#pragma unroll
+    for (int qb = 0; qb < NB; ++qb) {
       f32x16 sv, dp;
 #pragma unroll
       for (int e = 0; e < 16; ++e) {
@@ -450,9 +507,9 @@ __global__ __launch_bounds__(NW * 64, NW == 4 ? 2 : 1) void attention_bwd_rk_ker
       }
 #pragma unroll
       for (int k4 = 0; k4 < 4; ++k4) {
-        const bf16x8 qa = *(const bf16x8*)(Qs + ab_rc(qrow, 2 * k4 + h));
+        const bf16x8 qa = *(const bf16x8*)(Qs + qb * 4096 + off.offA[k4]);
         sv = __builtin_amdgcn_mfma_f32_32x32x16_bf16(qa, kf[k4], sv, 0, 0, 0);
-        const bf16x8 oa = *(const bf16x8*)(Os + ab_rc(qrow, 2 * k4 + h));
+        const bf16x8 oa = *(const bf16x8*)(Os + qb * 4096 + off.offA[k4]);
         dp = __builtin_amdgcn_mfma_f32_32x32x16_bf16(oa, vf[k4], dp, 0, 0, 0);
       }
       // P, dS for this lane's key and its 16 queries (four groups of four consecutive queries)
@@ -460,69 +517,82 @@ __global__ __launch_bounds__(NW * 64, NW == 4 ? 2 : 1) void attention_bwd_rk_ker
 #pragma unroll
       for (int g = 0; g < 4; ++g) {
         const int q0 = qb * 32 + 8 * g + 4 * h;
-        const f32x4 lq = *(const f32x4*)(lse + q0);
+        const f32x4 lq = *(const f32x4*)(lse2 + q0);
         const f32x4 dq = *(const f32x4*)(dv + q0);
         u32x4 wk = {};
-        if (DROP) wk = *(const u32x4*)(kbits + kbk * Lp + q0);
+        if (DROP) wk = *(const u32x4*)(kbits + blk * Lp + q0);
 #pragma unroll
         for (int u = 0; u < 4; ++u) {
           const int e = 4 * g + u;
-          const float p = __expf(sv[e] + kbias - lq[u]);
-          float pd = p, dpe = dp[e];
+          const float p = __builtin_amdgcn_exp2f(__builtin_fmaf(sv[e], kLog2e, kbias) - lq[u]);
+          float pd = p, ds;
           if (DROP) {
-            const bool keep = ((wk[u] >> r) & 1u) != 0u;
-            pd = keep ? p * inv : 0.f;
-            dpe = keep ? dpe * inv : 0.f;
+            const bool keep = (wk[u] & lanebit) != 0u;
+            pd = keep ? p : 0.f;
+            ds = p * __builtin_fmaf(keep ? dp[e] : 0.f, inv, -dq[u]);
+          } else {
+            ds = p * (dp[e] - dq[u]);
           }
           pa[e >> 3][e & 7] = (__bf16)pd;
-          sa[e >> 3][e & 7] = (__bf16)(p * (dpe - dq[u]));
+          sa[e >> 3][e & 7] = (__bf16)ds;
         }
       }
       // dV += Pd^T dO, dK += dS^T Qs over the block's 32 queries (2 k-steps of 16, permuted rows)
 #pragma unroll
       for (int ks = 0; ks < 2; ++ks) {
-        const int rA = qb * 32 + 16 * ks + 4 * h, rB = rA + 8;
 #pragma unroll
         for (int t = 0; t < 2; ++t) {
-          const bf16x8 ob = ab_tr8p(Os, rA, rB, 32 * t, lane);
+          const int base = qb * 4096 + ks * 2048;
+          const bf16x8 ob = ab_tr8o(Os + base, off.offT[t][0], off.offT[t][1]);
           dV[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(pa[ks], ob, dV[t], 0, 0, 0);
-          const bf16x8 qb8 = ab_tr8p(Qs, rA, rB, 32 * t, lane);
+          const bf16x8 qb8 = ab_tr8o(Qs + base, off.offT[t][0], off.offT[t][1]);
           dK[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(sa[ks], qb8, dK[t], 0, 0, 0);
         }
       }
     }
-    // dK / dV [key][d]: row = key 8 (e >> 2) + 4 h + (e & 3) of the block (regs), column d = 32 t + r
 #pragma unroll
-    for (int e = 0; e < 16; ++e) {
-      const int kr = kbk * 32 + (e & 3) + 8 * (e >> 2) + 4 * h;
-      if (kr < L) {
-        __bf16* dst = a.dqkv + (row0 + kr) * ld + hd * 64;
+    for (int t = 0; t < 2; ++t)
 #pragma unroll
-        for (int t = 0; t < 2; ++t) {
-          dst[a.H + 32 * t + r] = (__bf16)dK[t][e];
-          dst[2 * a.H + 32 * t + r] = (__bf16)dV[t][e];
-        }
+      for (int e = 0; e < 16; ++e) {
+        dKo[t][e >> 3][e & 7] = (__bf16)dK[t][e];
+        dVo[t][e >> 3][e & 7] = (__bf16)(DROP ? dV[t][e] * inv : dV[t][e]);
       }
-    }
   }
 
-  // ---- phase 2: dQ of query block qbq
-  for (int qbq = wave; qbq < nblk; qbq += NW) {
-    const int q = qbq * 32 + r;                        // this lane's query (D column)
-    bf16x8 qf[4], of[4];                               // B operands of S^T = K Qs^T, dP^T = V dO^T
+  // ---- phase 2: dQ of query block blk (operands read before the images are reused)
+  bf16x8 qf[4], of[4];                                 // B operands of S^T = K Qs^T, dP^T = V dO^T
+  float lq = 0.f, dq = 0.f;
+  const int q = blk * 32 + r;                          // this lane's query (D column)
+  if (act) {
 #pragma unroll
     for (int k4 = 0; k4 < 4; ++k4) {
-      qf[k4] = *(const bf16x8*)(Qs + ab_rc(q, 2 * k4 + h));
-      of[k4] = *(const bf16x8*)(Os + ab_rc(q, 2 * k4 + h));
+      qf[k4] = *(const bf16x8*)(Qs + blk * 4096 + off.offA[k4]);
+      of[k4] = *(const bf16x8*)(Os + blk * 4096 + off.offA[k4]);
     }
-    const float lq = lse[q], dq = dv[q];
+    lq = lse2[q];
+    dq = dv[q];
+  }
+  __syncthreads();
+  // element (row 8 (e >> 2) + 4 h + (e & 3) of the block, column 32 t + r) into a [Lp][64] image
+  auto put = [&](char* img, const bf16x8 (&v)[2][2]) {
+#pragma unroll
+    for (int t = 0; t < 2; ++t)
+#pragma unroll
+      for (int e = 0; e < 16; ++e) {
+        const int row = blk * 32 + 8 * (e >> 2) + 4 * h + (e & 3), col = 32 * t + r;
+        *(__bf16*)(img + ab_rc(row, col >> 3) + (col & 7) * 2) = v[t][e >> 3][e & 7];
+      }
+  };
+  if (act) {
+    put(Qs, dKo);
+    put(Os, dVo);
     f32x16 dQ[2];
 #pragma unroll
     for (int t = 0; t < 2; ++t)
 #pragma unroll
       for (int e = 0; e < 16; ++e) dQ[t][e] = 0.f;
-    for (int kbk = 0; kbk < nblk; ++kbk) {
-      const int krow = kbk * 32 + r;
+#pragma unroll
+    for (int kbk = 0; kbk < NB; ++kbk) {
       f32x16 st, dpt;
 #pragma unroll
       for (int e = 0; e < 16; ++e) {
@@ -531,45 +601,53 @@ __global__ __launch_bounds__(NW * 64, NW == 4 ? 2 : 1) void attention_bwd_rk_ker
       }
 #pragma unroll
       for (int k4 = 0; k4 < 4; ++k4) {
-        const bf16x8 ka = *(const bf16x8*)(Ks + ab_rc(krow, 2 * k4 + h));
+        const bf16x8 ka = *(const bf16x8*)(Ks + kbk * 4096 + off.offA[k4]);
         st = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ka, qf[k4], st, 0, 0, 0);
-        const bf16x8 va = *(const bf16x8*)(Vs + ab_rc(krow, 2 * k4 + h));
+        const bf16x8 va = *(const bf16x8*)(Vs + kbk * 4096 + off.offA[k4]);
         dpt = __builtin_amdgcn_mfma_f32_32x32x16_bf16(va, of[k4], dpt, 0, 0, 0);
       }
       uint32_t wq = 0;
-      if (DROP) wq = kbits[kbk * Lp + q];
+      if (DROP) wq = kbits[kbk * Lp + q] >> (4 * h);   // bit 8 g + u: key 8 g + 4 h + u of the block
       bf16x8 sa[2];
 #pragma unroll
       for (int g = 0; g < 4; ++g) {
-        const f32x4 kbv = *(const f32x4*)(kb + kbk * 32 + 8 * g + 4 * h);
+        const f32x4 kbv = *(const f32x4*)(kb2 + kbk * 32 + 8 * g + 4 * h);
 #pragma unroll
         for (int u = 0; u < 4; ++u) {
           const int e = 4 * g + u;
-          const float p = __expf(st[e] + kbv[u] - lq);
-          float dpe = dpt[e];
-          if (DROP) dpe = ((wq >> (8 * g + 4 * h + u)) & 1u) != 0u ? dpe * inv : 0.f;
-          sa[e >> 3][e & 7] = (__bf16)(p * (dpe - dq));
+          const float p = __builtin_amdgcn_exp2f(__builtin_fmaf(st[e], kLog2e, kbv[u]) - lq);
+          float ds;
+          if (DROP) ds = p * __builtin_fmaf((wq & (1u << (8 * g + u))) != 0u ? dpt[e] : 0.f, inv, -dq);
+          else ds = p * (dpt[e] - dq);
+          sa[e >> 3][e & 7] = (__bf16)ds;
         }
       }
 #pragma unroll
       for (int ks = 0; ks < 2; ++ks) {
-        const int rA = kbk * 32 + 16 * ks + 4 * h, rB = rA + 8;
 #pragma unroll
         for (int t = 0; t < 2; ++t) {
-          const bf16x8 kt = ab_tr8p(Ks, rA, rB, 32 * t, lane);
+          const bf16x8 kt = ab_tr8o(Ks + kbk * 4096 + ks * 2048, off.offT[t][0], off.offT[t][1]);
           dQ[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(sa[ks], kt, dQ[t], 0, 0, 0);
         }
       }
     }
-    // dQ [q][d]: row = query 8 (e >> 2) + 4 h + (e & 3) of the block (regs), column d = 32 t + r
 #pragma unroll
-    for (int e = 0; e < 16; ++e) {
-      const int qr = qbq * 32 + (e & 3) + 8 * (e >> 2) + 4 * h;
-      if (qr < L) {
-        __bf16* dst = a.dqkv + (row0 + qr) * ld + hd * 64;
+    for (int t = 0; t < 2; ++t)
 #pragma unroll
-        for (int t = 0; t < 2; ++t) dst[32 * t + r] = (__bf16)(dQ[t][e] * a.scale);
-      }
+      for (int e = 0; e < 16; ++e) dKo[t][e >> 3][e & 7] = (__bf16)(dQ[t][e] * a.scale);
+  }
+  __syncthreads();
+  if (act) put(Ks, dKo);
+  __syncthreads();
+  // ---- rows out: dQ (K image), dK (Qs image), dV (dO image), 16 B per lane, 8 lanes per row
+#pragma unroll
+  for (int it = 0; it < (3 * Lp * 8 + NT - 1) / NT; ++it) {
+    const int i = tid + it * NT;
+    const int m = i / (Lp * 8), rem = i - m * (Lp * 8);   // m: 0 dQ, 1 dK, 2 dV
+    const int row = rem >> 3, c = rem & 7;
+    if (m < 3 && row < L) {
+      const char* img = m == 0 ? Ks : (m == 1 ? Qs : Os);
+      *(bf16x8*)(a.dqkv + (row0 + row) * ld + m * a.H + hd * 64 + c * 8) = *(const bf16x8*)(img + ab_rc(row, c));
     }
   }
 }
@@ -758,24 +836,35 @@ int drt_attention_train_bwd_bits_bf16(const void* qkv, const void* ctx, const vo
   AttnBwdArgs a{(const __bf16*)qkv, (const __bf16*)ctx, (const __bf16*)dctx, lse, mask, (__bf16*)dqkv, B, L,
                 heads, heads * 64, scale, drop_p, seed, site, drop_bits};
   const int Lp = ((int)L + 31) & ~31;
-  const bool w8 = Lp / 32 > 4;
+  const int nb = Lp / 32;
   const dim3 grid((unsigned)(B * heads));
   const bool drop = drop_p > 0.0f;
   // register-resident P / dS; dropout from the forward's keep bits (or the same bits drawn again)
-  const size_t lds = (size_t)4 * Lp * kAbRow + (size_t)3 * Lp * 4 + (drop ? (size_t)(Lp / 32) * Lp * 4 : 0);
+  const size_t lds = (size_t)4 * Lp * kAbRow + (size_t)3 * Lp * 4 + (drop ? (size_t)nb * Lp * 4 : 0);
   DRT_REQUIRE(lds <= 160 * 1024);
   static bool rk_attr = false;
   if (!rk_attr) {
     const void* ks[] = {(const void*)attention_bwd_rk_kernel<4, false>, (const void*)attention_bwd_rk_kernel<4, true>,
-                        (const void*)attention_bwd_rk_kernel<8, false>, (const void*)attention_bwd_rk_kernel<8, true>};
+                        (const void*)attention_bwd_rk_kernel<5, false>, (const void*)attention_bwd_rk_kernel<5, true>};
     for (const void* f : ks) DRT_CHECK_HIP(hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
     rk_attr = true;
   }
   hipStream_t st = (hipStream_t)stream;
-  if (w8 && drop) hipLaunchKernelGGL((attention_bwd_rk_kernel<8, true>), grid, dim3(512), lds, st, a);
-  else if (w8) hipLaunchKernelGGL((attention_bwd_rk_kernel<8, false>), grid, dim3(512), lds, st, a);
-  else if (drop) hipLaunchKernelGGL((attention_bwd_rk_kernel<4, true>), grid, dim3(256), lds, st, a);
-  else hipLaunchKernelGGL((attention_bwd_rk_kernel<4, false>), grid, dim3(256), lds, st, a);
+  const dim3 blk(nb == 5 ? 512 : 256);
+#define DRT_AB_LAUNCH(NB_)                                                                              \
+  case NB_:                                                                                             \
+    if (drop) hipLaunchKernelGGL((attention_bwd_rk_kernel<NB_, true>), grid, blk, lds, st, a);         \
+    else hipLaunchKernelGGL((attention_bwd_rk_kernel<NB_, false>), grid, blk, lds, st, a);             \
+    break;
+  switch (nb) {
+    DRT_AB_LAUNCH(1)
+    DRT_AB_LAUNCH(2)
+    DRT_AB_LAUNCH(3)
+    DRT_AB_LAUNCH(4)
+    DRT_AB_LAUNCH(5)
+    default: return DRT_EINVAL;
+  }
+#undef DRT_AB_LAUNCH
   return hip_status(hipGetLastError());
 }
 

@@ -16,6 +16,7 @@ def main(reps=10):
     dev = torch.device("cuda", 0)
     s = _native.stream_ptr(dev)
     res = {}
+    torch.manual_seed(0)
     for B, L in ((1024, 128), (1024, 156), (512, 32)):
         H, heads = 768, 12
         T = B * L
@@ -49,6 +50,11 @@ def main(reps=10):
                 e1.record()
                 torch.cuda.synchronize()
                 res[f"B{B}_L{L}_{name}_p{p}{tag}"] = round(e0.elapsed_time(e1) / reps * 1e3, 1)
+                if name == "bwd":   # position-weighted checksum of dQKV: variants compare bitwise
+                    v = dqkv.view(torch.int16).view(-1).long()
+                    w = torch.arange(v.numel(), device=dev) % 1009 + 1
+                    res[f"B{B}_L{L}_bwd_p{p}{tag}_sum"] = int((v * w).sum())
+                    del v, w
         fwd_bytes = T * 3 * H * 2 + T * H * 2
         bwd_bytes = T * 3 * H * 2 + 2 * T * H * 2 + T * 3 * H * 2
         res[f"B{B}_L{L}_floor_us"] = {"fwd": round(fwd_bytes / 6.3e12 * 1e6, 1), "bwd": round(bwd_bytes / 6.3e12 * 1e6, 1)}
