@@ -466,21 +466,36 @@ __global__ __launch_bounds__((NB == 5 ? 8 : 4) * 64, NB == 5 ? 1 : 2) void atten
   const float inv = DROP ? 1.0f / (1.0f - a.drop_p) : 1.0f;
   const AbOffsets off = ab_offsets(lane);
   const uint32_t lanebit = 1u << r;
-  // NW >= NB: each wave owns at most one key block (phase 1) and one query block (phase 2).
-  // Outputs leave through LDS: dK / dV stay in registers (bf16) until every wave holds its phase-2
-  // operands, then go into the Qs / dO images (dead from there on); dQ goes into the K image once
-  // phase 2 is done; the work-group then writes whole 128-B rows with 16-B stores (12 per thread
-  // at L 128 instead of 96 two-byte stores per wave: the store issue, not the bytes, was the cost).
-#ifdef DRT_AB_ABL_NOPHASE
-  const bool act = false;
-#else
-  const bool act = wave < NB;
-#endif
-  const int blk = act ? wave : 0;
-  bf16x8 dKo[2][2], dVo[2][2];                        // [t][e >> 3]: element e of column 32 t + r
 
-  // ---- phase 1: dK, dV of key block blk
-  if (act) {
+  // Work units: P1(k) = dK, dV of key block k (loop over the query blocks), P2(q) = dQ of query
+  // block q (loop over the key blocks).  After staging the LDS images are read-only, so the two
+  // kinds run concurrently, each wave through its own list:
+  //   NB <= 4 (4 waves): wave w runs P1(w) then P2(w) -- every SIMD the same load;
+  //   NB = 5 (8 waves; wave w on SIMD w % 4): w0 P1(0) | w1 P1(1) P2(3) | w2 P1(2) P2(4) |
+  //     w3 P1(3) | w4 P1(4) | w5 P2(0) | w6 P2(1) | w7 P2(2): SIMD loads (16 MFMA per P1 step,
+  //     12 per P2 step) 32 / 40 / 40 / 28 against 56 on SIMD 0 for phase 1 on waves 0-4 followed
+  //     by phase 2 on waves 0-4.
+  // Outputs stay in registers (bf16) until every unit is done, then leave through LDS (dK into
+  // the Qs image, dV into the dO image, dQ into the K image) as whole 128-B rows of 16-B stores
+  // (12 per thread at L 128 instead of 96 two-byte stores per wave).
+#ifdef DRT_AB_ABL_NOPHASE
+  constexpr bool kRun = false;
+#else
+  constexpr bool kRun = true;
+#endif
+  int p1 = -1, p2 = -1;
+  if (NB <= 4) {
+    if (wave < NB) p1 = p2 = wave;
+  } else {
+    p1 = wave < 5 ? wave : -1;
+    p2 = wave >= 5 ? wave - 5 : (wave == 1 ? 3 : (wave == 2 ? 4 : -1));
+  }
+  if (!kRun) p1 = p2 = -1;
+  bf16x8 dKo[2][2], dVo[2][2], dQo[2][2];             // [t][e >> 3]: element e of column 32 t + r
+
+  // ---- P1: dK, dV of key block p1
+  if (p1 >= 0) {
+    const int blk = p1;
     const int key = blk * 32 + r;                     // this lane's key (D column / A row)
     bf16x8 kf[4], vf[4];                              // B operands of S = Qs K^T, dP = dO V^T
 #pragma unroll
@@ -559,33 +574,17 @@ __global__ __launch_bounds__((NB == 5 ? 8 : 4) * 64, NB == 5 ? 1 : 2) void atten
       }
   }
 
-  // ---- phase 2: dQ of query block blk (operands read before the images are reused)
-  bf16x8 qf[4], of[4];                                 // B operands of S^T = K Qs^T, dP^T = V dO^T
-  float lq = 0.f, dq = 0.f;
-  const int q = blk * 32 + r;                          // this lane's query (D column)
-  if (act) {
+  // ---- P2: dQ of query block p2
+  if (p2 >= 0) {
+    const int blk = p2;
+    const int q = blk * 32 + r;                        // this lane's query (D column)
+    bf16x8 qf[4], of[4];                               // B operands of S^T = K Qs^T, dP^T = V dO^T
 #pragma unroll
     for (int k4 = 0; k4 < 4; ++k4) {
       qf[k4] = *(const bf16x8*)(Qs + blk * 4096 + off.offA[k4]);
       of[k4] = *(const bf16x8*)(Os + blk * 4096 + off.offA[k4]);
     }
-    lq = lse2[q];
-    dq = dv[q];
-  }
-  __syncthreads();
-  // element (row 8 (e >> 2) + 4 h + (e & 3) of the block, column 32 t + r) into a [Lp][64] image
-  auto put = [&](char* img, const bf16x8 (&v)[2][2]) {
-#pragma unroll
-    for (int t = 0; t < 2; ++t)
-#pragma unroll
-      for (int e = 0; e < 16; ++e) {
-        const int row = blk * 32 + 8 * (e >> 2) + 4 * h + (e & 3), col = 32 * t + r;
-        *(__bf16*)(img + ab_rc(row, col >> 3) + (col & 7) * 2) = v[t][e >> 3][e & 7];
-      }
-  };
-  if (act) {
-    put(Qs, dKo);
-    put(Os, dVo);
+    const float lq = lse2[q], dq = dv[q];
     f32x16 dQ[2];
 #pragma unroll
     for (int t = 0; t < 2; ++t)
@@ -634,10 +633,24 @@ __global__ __launch_bounds__((NB == 5 ? 8 : 4) * 64, NB == 5 ? 1 : 2) void atten
 #pragma unroll
     for (int t = 0; t < 2; ++t)
 #pragma unroll
-      for (int e = 0; e < 16; ++e) dKo[t][e >> 3][e & 7] = (__bf16)(dQ[t][e] * a.scale);
+      for (int e = 0; e < 16; ++e) dQo[t][e >> 3][e & 7] = (__bf16)(dQ[t][e] * a.scale);
   }
   __syncthreads();
-  if (act) put(Ks, dKo);
+  // element (row 8 (e >> 2) + 4 h + (e & 3) of block blk, column 32 t + r) into a [Lp][64] image
+  auto put = [&](char* img, int blk, const bf16x8 (&v)[2][2]) {
+#pragma unroll
+    for (int t = 0; t < 2; ++t)
+#pragma unroll
+      for (int e = 0; e < 16; ++e) {
+        const int row = blk * 32 + 8 * (e >> 2) + 4 * h + (e & 3), col = 32 * t + r;
+        *(__bf16*)(img + ab_rc(row, col >> 3) + (col & 7) * 2) = v[t][e >> 3][e & 7];
+      }
+  };
+  if (p1 >= 0) {
+    put(Qs, p1, dKo);
+    put(Os, p1, dVo);
+  }
+  if (p2 >= 0) put(Ks, p2, dQo);
   __syncthreads();
   // ---- rows out: dQ (K image), dK (Qs image), dV (dO image), 16 B per lane, 8 lanes per row
 #pragma unroll
