@@ -86,6 +86,8 @@ __host__ __device__ __forceinline__ bool attn_keep(uint32_t row_key, int key, ui
   return ((key & 1) ? hsh >> 16 : hsh & 0xFFFFu) >= thr16;
 }
 
+constexpr float kLog2e = 1.4426950408889634f;   // softmax in exp2 form (attention kernels)
+
 // faiss pads rows that have fewer than k results with label -1 and the
 // lowest float (CMin<float>::neutral() == numeric_limits<float>::lowest()).
 constexpr float kPadScore = -3.402823466e+38f;

@@ -176,28 +176,41 @@ struct AttnArgs {
                           //   (query, key >> 5) -- the backward reads it instead of re-hashing
 };
 
-// NW = waves per work-group (the launcher uses 4; an 8-wave form for 5-8 query blocks measured
-// slower, see drt_attention_train_fwd_bf16).  Each block's arithmetic is the same whichever wave
-// runs it.
-// Occupancy: 4 work-groups per CU for the 4-wave inference kernel (<= 128 VGPRs); the 4-wave
-// dropout kernel (hash + keep-bit words) needs more registers, so 3 (<= 170 VGPRs: at 4 it spilled).
-// The 5-wave dropout kernel (L 129-160) at 4 work-groups per CU, i.e. <= 128 VGPRs with a few
-// spills, beat its spill-free 156-VGPR build (2 work-groups of 5 waves per CU) by 11 % at L 156
-// (467 -> 417 us, profiles/r03e_attn_probe_minb4.log); the 4-wave one at 4 lost 19 % at L 128.
-#ifndef DRT_ATTN_DROP5_MINB   // tools/build_variant.sh A/B
-#define DRT_ATTN_DROP5_MINB 4
-#endif
-template <bool DROP, int NW = 4>
-__global__ __launch_bounds__(NW * 64, !DROP ? (NW == 4 ? 4 : (NW <= 5 ? 3 : 2)) : (NW == 5 ? DRT_ATTN_DROP5_MINB : 3))
-void attention_kernel(AttnArgs a) {
+// Attention forward, one work-group per (sequence, head): K (swizzled rows), V^T and the key bias
+// in LDS, one 32-query block per wave (S^T tiles of 32 keys: rows = keys, lane = query), online
+// softmax in registers, P as the B operand of O^T += V^T P^T.  NB = blocks of 32 (Lp = 32 NB) as a
+// template argument for L <= 160 (every LDS offset a per-lane constant + an immediate, key loop
+// unrolled, O leaves through LDS as whole-row 16-B stores); NB = 0: any L <= 512 (inference), a
+// wave loops over its query blocks and stores directly.
+// Round 3: scores in log2 units, s2 = fma(s, log2e, kb) with the key bias kb = 0 / -FLT_MAX (finite:
+// a row with every key masked gets HF's uniform softmax, no NaN); the running max moves only when a
+// tile's max exceeds it by more than kLazy (= 8, P <= 2^8 in bf16 / fp32 is exact to the same
+// relative precision), so the O rescale is a rare wave-uniform branch instead of 32 multiplies per
+// tile; dropout draws the keep decisions from the pairwise hash (drt_common.h), zeroes dropped P,
+// writes the keep words for the backward when asked (drop_bits), and moves 1 / (1 - p) into the
+// final 1 / l.  (Drawing the words in a separate one-thread-per-word pass for the forward to read
+// measured slower: 272 vs 178 us at 1024 x 128, profiles/r03r_attn_probe.log "bits" vs "hash".)
+// lse = (m + log2 l) ln 2 (natural log, what the backward rebuilds P from).
+// NW waves: 4, or 5 for 5 query blocks (129 <= L <= 160: the recipe's 156-token passages, the
+// reranker's 160-token pairs; with 4, wave 0 ran two blocks while three idled).
+constexpr float kLazy = 8.0f;
+constexpr float kLn2 = 0.6931471805599453f;
+
+// Register budget: 4 waves per SIMD (<= 128 VGPRs) -- at 5 query blocks the LDS (42 KiB) admits 3
+// work-groups of 5 waves per CU, i.e. 4 waves on three of the SIMDs.
+template <int NB, bool DROP>
+__global__ __launch_bounds__(NB == 5 ? 320 : 256) __attribute__((amdgpu_waves_per_eu(4, 8)))
+void attention_fwd_kernel(AttnArgs a) {
+  constexpr int NW = NB == 5 ? 5 : 4;
   constexpr int NT = NW * 64;
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int L = (int)a.L;
-  const int Lp = (L + 31) & ~31;           // keys padded to the 32-key tile
+  const int Lp = NB ? NB * 32 : (L + 31) & ~31;  // keys padded to the 32-key tile
+  const int nqb = Lp / 32;
   const int vts = Lp * 2 + 8;              // Vt row stride (bytes): conflict-free ds_read_b64
   char* Ks = smem;                          // Lp * 128 B
   char* Vt = smem + Lp * 128;               // 64 * vts B
-  float* kbias = (float*)(Vt + 64 * vts);   // Lp floats
+  float* kb = (float*)(Vt + 64 * vts);      // Lp floats
 
   const int tid = threadIdx.x;
   const int wave = tid >> 6, lane = tid & 63;
@@ -205,6 +218,7 @@ void attention_kernel(AttnArgs a) {
   const int64_t b = blockIdx.x / a.heads;
   const int hd = blockIdx.x % a.heads;
   const int64_t row0 = b * a.L;
+  const int64_t hrow = ((int64_t)b * a.heads + hd) * L;
   const int64_t ld = 3 * (int64_t)a.H;
   const __bf16* Qg = a.qkv + row0 * ld + hd * kHeadDim;
   const __bf16* Kg = Qg + a.H;
@@ -254,16 +268,25 @@ void attention_kernel(AttnArgs a) {
     float bv = 0.0f;
     if (i >= L) bv = -3.402823466e+38f;
     else if (a.mask && a.mask[b * a.L + i] == 0) bv = -3.402823466e+38f;  // (1 - mask) * finfo.min
-    kbias[i] = bv;
+    kb[i] = bv;
   }
   __syncthreads();
 
+  // per-lane LDS offsets (a 32-key tile starts at a multiple of 32 rows: its swizzle term never
+  // depends on the tile)
   const int sw = (r >> 1) & 7;
-  const int nqb = Lp / 32;
+  int offK[4];
+#pragma unroll
+  for (int st = 0; st < 4; ++st) offK[st] = r * 128 + ((((2 * st) | h) ^ sw) << 4);
+  const int offV0 = r * vts + 8 * h, offV1 = (32 + r) * vts + 8 * h;
+  const float inv = DROP ? 1.0f / (1.0f - a.drop_p) : 1.0f;
+  const uint32_t thr = DROP ? attn_drop_threshold(a.drop_p) : 0u;
+  bf16x8 oo[2][2];                           // NB: this wave's O block, [t][g / 2] (bf16)
+
   for (int qb = wave; qb < nqb; qb += NW) {
     // Q fragment (B operand, B[k=d][col=q] = Q[q][d]) scaled by 1/sqrt(dh)
-    int qrow = qb * 32 + r;
-    qrow = qrow < L ? qrow : L - 1;
+    const int qq = qb * 32 + r;
+    const int qrow = qq < L ? qq : L - 1;
     bf16x8 qf[4];
 #pragma unroll
     for (int s = 0; s < 4; ++s) {
@@ -272,49 +295,54 @@ void attention_kernel(AttnArgs a) {
       for (int j = 0; j < 8; ++j) v[j] = (__bf16)((float)v[j] * a.scale);
       qf[s] = v;
     }
+    const uint32_t rowkey = DROP ? attn_row_key(a.seed, a.site, (uint64_t)(hrow + qq)) : 0u;
+    uint32_t words[NB ? NB : 1];               // keep words of this query (stored once, after the last tile)
     f32x16 o[2];
 #pragma unroll
     for (int t = 0; t < 2; ++t)
 #pragma unroll
       for (int e = 0; e < 16; ++e) o[t][e] = 0.0f;
     float m = -__builtin_inff(), l = 0.0f;
-    const uint32_t rowkey =
-        DROP ? attn_row_key(a.seed, a.site, ((uint64_t)b * a.heads + hd) * (uint64_t)L + (uint64_t)(qb * 32 + r)) : 0u;
 
-    for (int kt = 0; kt < Lp; kt += 32) {
+    auto tile = [&](int kt) {
       // S^T tile: rows = keys kt.., cols = queries
       f32x16 s;
 #pragma unroll
       for (int e = 0; e < 16; ++e) s[e] = 0.0f;
 #pragma unroll
       for (int st = 0; st < 4; ++st) {
-        const int key = kt + r;
-        const bf16x8 kf = *(const bf16x8*)(Ks + key * 128 + ((((2 * st) | h) ^ sw) << 4));
+        const bf16x8 kf = *(const bf16x8*)(Ks + kt * 128 + offK[st]);
         s = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kf, qf[st], s, 0, 0, 0);
       }
       float mt = -__builtin_inff();
 #pragma unroll
-      for (int e = 0; e < 16; ++e) {
-        s[e] += kbias[kt + (e & 3) + 8 * (e >> 2) + 4 * h];
-        mt = fmaxf(mt, s[e]);
+      for (int g = 0; g < 4; ++g) {
+        const f32x4 kbv = *(const f32x4*)(kb + kt + 8 * g + 4 * h);
+#pragma unroll
+        for (int u = 0; u < 4; ++u) s[4 * g + u] = __builtin_fmaf(s[4 * g + u], kLog2e, kbv[u]);
+        mt = fmaxf(fmaxf(mt, fmaxf(s[4 * g], s[4 * g + 1])), fmaxf(s[4 * g + 2], s[4 * g + 3]));
       }
       mt = fmaxf(mt, __shfl_xor(mt, 32, 64));
-      const float mn = fmaxf(m, mt);
-      const float alpha = __expf(m - mn);
+      const bool grow = mt > m + kLazy;
+      if (__builtin_amdgcn_ballot_w64(grow) != 0ull) {   // rare after the first tile
+        const float mn = grow ? mt : m;
+        const float alpha = __builtin_amdgcn_exp2f(m - mn);
+#pragma unroll
+        for (int t = 0; t < 2; ++t)
+#pragma unroll
+          for (int e = 0; e < 16; ++e) o[t][e] *= alpha;
+        l *= alpha;
+        m = mn;
+      }
       float ps = 0.0f;
 #pragma unroll
       for (int e = 0; e < 16; ++e) {
-        s[e] = __expf(s[e] - mn);
+        s[e] = __builtin_amdgcn_exp2f(s[e] - m);
         ps += s[e];
       }
       ps += __shfl_xor(ps, 32, 64);
-      l = l * alpha + ps;
-      m = mn;
-      if (DROP) {   // dropout of P after its normaliser: O = dropout(softmax) V
-        const float inv = 1.0f / (1.0f - a.drop_p);
-        const uint32_t thr = attn_drop_threshold(a.drop_p);
-        const int qq = qb * 32 + r;
-        // this lane's keys kt + 8 g + 4 h + {0,1,2,3}: pairs kt / 2 + 4 g + 2 h + {0, 1}
+      l += ps;
+      if (DROP) {   // this lane's keys kt + 8 g + 4 h + {0,1,2,3}: pairs kt / 2 + 4 g + 2 h + {0, 1}
         const uint32_t pbase = rowkey + (uint32_t)((kt >> 1) + 2 * h) * kAttnPairStep;
         uint32_t m16 = 0;
 #pragma unroll
@@ -328,18 +356,15 @@ void attention_kernel(AttnArgs a) {
               const int kr = 8 * g + 4 * h + 2 * u2 + w;
               const bool keep = kt + kr < L && (w ? hsh >> 16 : hsh & 0xFFFFu) >= thr;
               m16 |= keep ? 1u << kr : 0u;
-              s[e] = keep ? s[e] * inv : 0.0f;
+              s[e] = keep ? s[e] : 0.0f;
             }
           }
         if (a.drop_bits) {   // this query's 32 keep bits of the key tile: the two lane halves' 16 each
           const uint32_t word = m16 | __shfl_xor(m16, 32, 64);
-          if (h == 0 && qq < L) a.drop_bits[(((int64_t)b * a.heads + hd) * L + qq) * (Lp / 32) + kt / 32] = word;
+          if (NB) words[NB ? (kt / 32) % NB : 0] = word;
+          else if (h == 0 && qq < L) a.drop_bits[(hrow + qq) * nqb + kt / 32] = word;
         }
       }
-#pragma unroll
-      for (int t = 0; t < 2; ++t)
-#pragma unroll
-        for (int e = 0; e < 16; ++e) o[t][e] *= alpha;
       // O^T += V^T P^T over the 32 keys (2 k-steps of 16)
 #pragma unroll
       for (int ks = 0; ks < 2; ++ks) {
@@ -348,7 +373,7 @@ void attention_kernel(AttnArgs a) {
         for (int j = 0; j < 8; ++j) pf[j] = (__bf16)s[8 * ks + j];
 #pragma unroll
         for (int t = 0; t < 2; ++t) {
-          const char* vrow = Vt + (32 * t + r) * vts + (kt + 16 * ks + 4 * h) * 2;
+          const char* vrow = Vt + (t ? offV1 : offV0) + (kt + 16 * ks) * 2;
           const bf16x4 v0 = *(const bf16x4*)(vrow);
           const bf16x4 v1 = *(const bf16x4*)(vrow + 16);
           bf16x8 vf;
@@ -360,25 +385,70 @@ void attention_kernel(AttnArgs a) {
           o[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vf, pf, o[t], 0, 0, 0);
         }
       }
+    };
+    if (NB) {
+#pragma unroll
+      for (int j = 0; j < (NB ? NB : 1); ++j) tile(32 * j);
+      if (DROP && a.drop_bits && h == 0 && qq < L) {   // the row's words: contiguous over the wave's queries
+        uint32_t* dst = a.drop_bits + (hrow + qq) * nqb;
+        if (NB == 4) {
+          *(u32x4*)dst = u32x4{words[0], words[NB > 1 ? 1 : 0], words[NB > 2 ? 2 : 0], words[NB > 3 ? 3 : 0]};
+        } else {
+#pragma unroll
+          for (int j = 0; j < (NB ? NB : 1); ++j) dst[j] = words[j];
+        }
+      }
+    } else {
+      for (int kt = 0; kt < Lp; kt += 32) tile(kt);
     }
     // O^T[d][q]: lane holds query r; d = 32t + (e&3) + 8(e>>2) + 4h
-    const int q = qb * 32 + r;
-    if (q < L && a.lse && h == 0) a.lse[((int64_t)b * a.heads + hd) * L + q] = m + __logf(l);
-    if (q < L) {
-      const float inv = 1.0f / l;
-      __bf16* orow = a.ctx + (row0 + q) * a.H + hd * kHeadDim;
+    if (qq < L && a.lse && h == 0) a.lse[hrow + qq] = (m + __log2f(l)) * kLn2;
+    const float sc = inv / l;
+    if (NB) {
+#pragma unroll
+      for (int t = 0; t < 2; ++t)
+#pragma unroll
+        for (int e = 0; e < 16; ++e) oo[t][e >> 3][e & 7] = (__bf16)(o[t][e] * sc);
+    } else if (qq < L) {
+      __bf16* orow = a.ctx + (row0 + qq) * a.H + hd * kHeadDim;
 #pragma unroll
       for (int t = 0; t < 2; ++t)
 #pragma unroll
         for (int g = 0; g < 4; ++g) {
           bf16x4 v;
 #pragma unroll
-          for (int u = 0; u < 4; ++u) v[u] = (__bf16)(o[t][4 * g + u] * inv);
+          for (int u = 0; u < 4; ++u) v[u] = (__bf16)(o[t][4 * g + u] * sc);
           *(bf16x4*)(orow + 32 * t + 8 * g + 4 * h) = v;
         }
     }
   }
+  if (NB) {
+    // O through LDS (the K image, dead once every wave is past its last tile): rows of 128 B
+    __syncthreads();
+    if (wave < nqb) {
+#pragma unroll
+      for (int t = 0; t < 2; ++t)
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+          bf16x4 v;
+#pragma unroll
+          for (int u = 0; u < 4; ++u) v[u] = oo[t][g >> 1][(g & 1) * 4 + u];
+          const int qr = wave * 32 + r, d0 = 32 * t + 8 * g + 4 * h;   // 4 consecutive d of row qr
+          *(bf16x4*)(Ks + qr * 128 + (((d0 >> 3) ^ ((qr >> 1) & 7)) << 4) + (d0 & 7) * 2) = v;
+        }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int it = 0; it < (Lp * 8 + NT - 1) / NT; ++it) {
+      const int i = tid + it * NT;
+      const int row = i >> 3, c = i & 7;
+      if (i < Lp * 8 && row < L)
+        *(bf16x8*)(a.ctx + (row0 + row) * a.H + hd * kHeadDim + c * 8) =
+            *(const bf16x8*)(Ks + row * 128 + ((c ^ ((row >> 1) & 7)) << 4));
+    }
+  }
 }
+
 
 // ---------------------------------------------------------------------------
 // Pooling (utils.py:233-240, biencoder.py:139-146) and L2 normalisation.
@@ -575,27 +645,36 @@ int drt_attention_train_fwd_bits_bf16(const void* qkv, const int64_t* mask, void
   AttnArgs a{(const __bf16*)qkv, mask, (__bf16*)ctx, B, L, heads, heads * head_dim, scale, lse, drop_p, seed, site,
              drop_bits};
   const int Lp = ((int)L + 31) & ~31;
+  const int nb = Lp / 32;
   const size_t lds = (size_t)Lp * 128 + (size_t)64 * (Lp * 2 + 8) + (size_t)Lp * 4;
   static bool attr_set = false;
   if (!attr_set) {
-    const void* ks[] = {(const void*)attention_kernel<false, 4>, (const void*)attention_kernel<true, 4>,
-                        (const void*)attention_kernel<false, 5>, (const void*)attention_kernel<true, 5>};
+    const void* ks[] = {(const void*)attention_fwd_kernel<0, false>, (const void*)attention_fwd_kernel<4, false>,
+                        (const void*)attention_fwd_kernel<5, false>, (const void*)attention_fwd_kernel<4, true>,
+                        (const void*)attention_fwd_kernel<5, true>};
     for (const void* f : ks) DRT_CHECK_HIP(hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
     attr_set = true;
   }
-  // 4 waves, except 5 query blocks (129 <= L <= 160: the recipe's 156-token passages, the reranker's
-  // 160-token pairs): 5 waves, one block each -- with 4, wave 0 ran two blocks while three idled.
-  // (An 8-wave form measured slower: 130 VGPRs -> one work-group per CU.)  Same per-block arithmetic.
   const dim3 grid((unsigned)(B * heads));
   hipStream_t s = (hipStream_t)stream;
-  if (Lp / 32 == 5) {
-    if (drop_p > 0.0f) hipLaunchKernelGGL((attention_kernel<true, 5>), grid, dim3(320), lds, s, a);
-    else hipLaunchKernelGGL((attention_kernel<false, 5>), grid, dim3(320), lds, s, a);
-  } else if (drop_p > 0.0f) {
-    hipLaunchKernelGGL((attention_kernel<true, 4>), grid, dim3(256), lds, s, a);
-  } else {
-    hipLaunchKernelGGL((attention_kernel<false, 4>), grid, dim3(256), lds, s, a);
+  const bool drop = drop_p > 0.0f;
+  DRT_REQUIRE(!drop || nb <= 5);   // training shapes (the backward's L <= 160)
+#define DRT_AF_LAUNCH(NB_)                                                                              \
+  case NB_: {                                                                                           \
+    const dim3 blk(NB_ == 5 ? 320 : 256);                                                               \
+    if (drop) hipLaunchKernelGGL((attention_fwd_kernel<NB_, true>), grid, blk, lds, s, a);             \
+    else hipLaunchKernelGGL((attention_fwd_kernel<NB_, false>), grid, blk, lds, s, a);                 \
+    break;                                                                                              \
   }
+  switch (nb) {
+    DRT_AF_LAUNCH(1)
+    DRT_AF_LAUNCH(2)
+    DRT_AF_LAUNCH(3)
+    DRT_AF_LAUNCH(4)
+    DRT_AF_LAUNCH(5)
+    default: hipLaunchKernelGGL((attention_fwd_kernel<0, false>), grid, dim3(256), lds, s, a); break;
+  }
+#undef DRT_AF_LAUNCH
   return hip_status(hipGetLastError());
 }
 

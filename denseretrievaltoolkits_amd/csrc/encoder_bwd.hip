@@ -316,8 +316,6 @@ __device__ __forceinline__ bf16x8 ab_tr8o(const char* img, int off0, int off1) {
   return v;
 }
 
-constexpr float kLog2e = 1.4426950408889634f;
-
 // NB = row blocks of 32 (Lp = 32 NB), NW = waves: one work-group per (sequence, head).
 // Exponentials as exp2(s log2e + kb2 - lse2) with the key bias and lse pre-scaled by log2e in
 // staging (one fma + one sub + v_exp per score); the dropout scale 1 / (1 - p) leaves the
@@ -336,7 +334,7 @@ __global__ __launch_bounds__((NB == 5 ? 8 : 4) * 64, NB == 5 ? 1 : 2) void atten
   char* Os = Vs + Lp * kAbRow;                       // dO
   float* lse2 = (float*)(Os + Lp * kAbRow);          // [Lp]  lse * log2e
   float* dv = lse2 + Lp;                             // [Lp]  Dv
-  float* kb2 = dv + Lp;                              // [Lp]  key bias * log2e
+  float* kb2 = dv + Lp;                              // [Lp]  key bias (0 / -FLT_MAX)
   uint32_t* kbits = (uint32_t*)(kb2 + Lp);           // [NB][Lp] keep words (DROP)
 
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
@@ -435,7 +433,7 @@ __global__ __launch_bounds__((NB == 5 ? 8 : 4) * 64, NB == 5 ? 1 : 2) void atten
     for (int j = 0; j < MAXS; ++j) {
       const int i = tid + j * NT;
       if (i < Lp) {
-        kb2[i] = (i >= L || mk[j] == 0) ? -3.402823466e+38f * kLog2e : 0.0f;   // (1 - mask) * finfo.min
+        kb2[i] = (i >= L || mk[j] == 0) ? -3.402823466e+38f : 0.0f;   // (1 - mask) * finfo.min (finite)
         lse2[i] = lsev[j] * kLog2e;
       }
     }
