@@ -60,6 +60,8 @@ _SIGNATURES = [
     ("drt_layernorm_bwd_workspace", c_sz, [c_i64, c_i32]),
     ("drt_layernorm_bwd_drop_bf16", c_i32, [c_vp, c_vp, c_vp, c_f32, c_i64, c_i32, c_vp, c_vp, c_vp, c_f32, c_u64,
                                             c_u64, c_vp, c_vp, c_vp, c_sz, c_vp]),
+    ("drt_layernorm_bwd_sum_bf16", c_i32, [c_vp, c_vp, c_vp, c_f32, c_i64, c_i32, c_vp, c_vp, c_vp, c_f32, c_u64,
+                                           c_u64, c_vp, c_vp, c_vp, c_vp, c_sz, c_vp]),
     ("drt_linear_bf16_ex", c_i32, [c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_i64, c_i64, c_i64, c_i32, c_f32, c_u64,
                                    c_u64, c_vp, c_sz, c_vp]),
     ("drt_layernorm_bwd_bf16", c_i32, [c_vp, c_vp, c_vp, c_f32, c_i64, c_i32, c_vp, c_vp, c_vp, c_vp, c_vp, c_sz,
@@ -84,6 +86,9 @@ _SIGNATURES = [
                                                   c_f32, c_u64, c_u64, c_vp]),
     ("drt_attention_train_bwd_bits_bf16", c_i32, [c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_i64, c_i64, c_i32,
                                                   c_i32, c_f32, c_f32, c_u64, c_u64, c_vp]),
+    ("drt_attention_train_bwd_bias_workspace", c_sz, [c_i64, c_i32, c_i32]),
+    ("drt_attention_train_bwd_bias_bf16", c_i32, [c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_i64, c_i64, c_i32,
+                                                  c_i32, c_f32, c_f32, c_u64, c_u64, c_vp, c_vp, c_sz, c_vp]),
     ("drt_attention_bwd_bf16", c_i32, [c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_i64, c_i64, c_i32, c_i32, c_f32, c_vp]),
     ("drt_layernorm_bf16", c_i32, [c_vp, c_i64, c_i32, c_vp, c_vp, c_f32, c_vp, c_vp]),
     ("drt_attention_bf16", c_i32, [c_vp, c_vp, c_vp, c_i64, c_i64, c_i32, c_i32, c_f32, c_vp]),

@@ -26,32 +26,41 @@ constexpr int kLnBwdBlocks = 1024;   // grid of the row pass = rows of the param
 // One wave per row (grid-stride over rows), H = 64 * EPL; lane owns columns
 // (e / 4) * 256 + lane * 4 + e % 4.  Statistics recomputed from the stored bf16 pre-LN sums
 // exactly as layernorm_bf16_kernel computed them.  Each block leaves its dgamma / dbeta
-// partial sums in part[blockIdx.x][0..H) and part[gridDim.x + blockIdx.x][0..H).
-template <int EPL>
-__global__ __launch_bounds__(256) void layernorm_bwd_kernel(const __bf16* dy, const __bf16* x, const float* gamma,
+// partial sums in part[blockIdx.x][0..H) and part[gridDim.x + blockIdx.x][0..H); SUM: also the
+// column sums of the gradient handed down (dxd when dropping, else dx, as stored in bf16) in
+// part[2 gridDim.x + blockIdx.x] -- the bias gradient of the linear below, without a pass
+// that reads that gradient again.
+template <int EPL, bool SUM>
+__global__ __launch_bounds__(256, EPL <= 12 ? 4 : 1) void layernorm_bwd_kernel(const __bf16* dy, const __bf16* x, const float* gamma,
                                                             float eps, int64_t M, int H, const __bf16* dres,
                                                             __bf16* dx, float* part, __bf16* dxd, float drop_p,
                                                             uint64_t seed, uint64_t site) {
-  __shared__ float red[4][2][EPL * 64];
+  __shared__ float red[4][SUM ? 3 : 2][EPL * 64];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  float dg[EPL], db[EPL], gm[EPL];
+  // SUM keeps 4 wave-wide partial sums per column: gamma is re-read per row there (an L1 hit)
+  // instead of held in registers, so the kernel keeps 4 waves per SIMD without spilling
+  float dg[EPL], db[EPL], gm[SUM ? 1 : EPL], ds[SUM ? EPL : 1];
 #pragma unroll
   for (int e = 0; e < EPL; ++e) {
     dg[e] = 0.f;
     db[e] = 0.f;
-    gm[e] = gamma[(e >> 2) * 256 + lane * 4 + (e & 3)];
+    if (SUM) ds[SUM ? e : 0] = 0.f;
+    else gm[SUM ? 0 : e] = gamma[(e >> 2) * 256 + lane * 4 + (e & 3)];
   }
   for (int64_t t = (int64_t)blockIdx.x * 4 + wave; t < M; t += (int64_t)gridDim.x * 4) {
-    float xv[EPL], gv[EPL], dyv[EPL];
+    float xv[EPL], gv[EPL], dyv[EPL], gmr[SUM ? EPL : 1];
 #pragma unroll
     for (int e4 = 0; e4 < EPL / 4; ++e4) {
       const int c = e4 * 256 + lane * 4;
       const bf16x4 a = *(const bf16x4*)(x + t * H + c);
       const bf16x4 b = *(const bf16x4*)(dy + t * H + c);
+      f32x4 g4 = {};
+      if (SUM) g4 = *(const f32x4*)(gamma + c);
 #pragma unroll
       for (int u = 0; u < 4; ++u) {
         xv[e4 * 4 + u] = (float)a[u];
         dyv[e4 * 4 + u] = (float)b[u];
+        if (SUM) gmr[SUM ? e4 * 4 + u : 0] = g4[u];
       }
     }
     float s = 0.f;
@@ -69,7 +78,7 @@ __global__ __launch_bounds__(256) void layernorm_bwd_kernel(const __bf16* dy, co
 #pragma unroll
     for (int e = 0; e < EPL; ++e) {
       xv[e] = (xv[e] - mean) * rstd;   // xhat
-      gv[e] = dyv[e] * gm[e];
+      gv[e] = dyv[e] * (SUM ? gmr[SUM ? e : 0] : gm[SUM ? 0 : e]);
       sg += gv[e];
       sgx += gv[e] * xv[e];
       dg[e] += dyv[e] * xv[e];
@@ -96,8 +105,12 @@ __global__ __launch_bounds__(256) void layernorm_bwd_kernel(const __bf16* dy, co
         for (int u = 0; u < 4; ++u) {
           const bool keep = drop_hash24(seed, site, (uint64_t)(t * H + c + u)) >= thr;
           od[u] = (__bf16)(keep ? (float)o[u] * inv : 0.0f);
+          if (SUM) ds[SUM ? e4 * 4 + u : 0] += (float)od[u];
         }
         *(bf16x4*)(dxd + t * H + c) = od;
+      } else if (SUM) {
+#pragma unroll
+        for (int u = 0; u < 4; ++u) ds[SUM ? e4 * 4 + u : 0] += (float)o[u];
       }
     }
   }
@@ -106,6 +119,7 @@ __global__ __launch_bounds__(256) void layernorm_bwd_kernel(const __bf16* dy, co
   for (int e = 0; e < EPL; ++e) {
     red[wave][0][e * 64 + lane] = dg[e];
     red[wave][1][e * 64 + lane] = db[e];
+    if (SUM) red[wave][SUM ? 2 : 0][e * 64 + lane] = ds[SUM ? e : 0];
   }
   __syncthreads();
   for (int i = threadIdx.x; i < EPL * 64; i += 256) {
@@ -113,6 +127,10 @@ __global__ __launch_bounds__(256) void layernorm_bwd_kernel(const __bf16* dy, co
     const int col = (e >> 2) * 256 + ln * 4 + (e & 3);
     part[(int64_t)blockIdx.x * H + col] = ((red[0][0][i] + red[1][0][i]) + red[2][0][i]) + red[3][0][i];
     part[(int64_t)(gridDim.x + blockIdx.x) * H + col] = ((red[0][1][i] + red[1][1][i]) + red[2][1][i]) + red[3][1][i];
+    if (SUM) {
+      constexpr int k = SUM ? 2 : 0;
+      part[(int64_t)(2 * gridDim.x + blockIdx.x) * H + col] = ((red[0][k][i] + red[1][k][i]) + red[2][k][i]) + red[3][k][i];
+    }
   }
 }
 
@@ -274,6 +292,7 @@ struct AttnBwdArgs {
   uint64_t seed, site;
   const uint32_t* drop_bits;  // optional keep bits written by the forward ([B][heads][L][ceil(L/32)]);
                               // NULL: the same bits drawn again from the hash
+  float* dsum;                // optional [B][3H]: per-sequence column sums of dQKV (bias gradients)
 };
 
 __device__ __forceinline__ int ab_rc(int row, int chunk) { return row * kAbRow + ((chunk ^ ((row >> 1) & 7)) << 4); }
@@ -644,11 +663,31 @@ __global__ __launch_bounds__((NB == 5 ? 8 : 4) * 64, NB == 5 ? 1 : 2) void atten
         *(__bf16*)(img + ab_rc(row, col >> 3) + (col & 7) * 2) = v[t][e >> 3][e & 7];
       }
   };
+  // dsum: each unit's column sums over its 32 rows (of the values as stored; rows past L are
+  // exactly 0) into the V image, dead from here on: [NB][3 (dQ, dK, dV)][64]
+  float* csum = (float*)Vs;
+  auto colsum32 = [&](int blk, int m, const bf16x8 (&v)[2][2]) {
+#pragma unroll
+    for (int t = 0; t < 2; ++t) {
+      float x = 0.f;
+#pragma unroll
+      for (int e = 0; e < 16; ++e) x += (float)v[t][e >> 3][e & 7];
+      x += __shfl_xor(x, 32, 64);
+      if (h == 0) csum[(blk * 3 + m) * 64 + 32 * t + r] = x;
+    }
+  };
   if (p1 >= 0) {
     put(Qs, p1, dKo);
     put(Os, p1, dVo);
+    if (a.dsum) {
+      colsum32(p1, 1, dKo);
+      colsum32(p1, 2, dVo);
+    }
   }
-  if (p2 >= 0) put(Ks, p2, dQo);
+  if (p2 >= 0) {
+    put(Ks, p2, dQo);
+    if (a.dsum) colsum32(p2, 0, dQo);
+  }
   __syncthreads();
   // ---- rows out: dQ (K image), dK (Qs image), dV (dO image), 16 B per lane, 8 lanes per row
 #pragma unroll
@@ -660,6 +699,13 @@ __global__ __launch_bounds__((NB == 5 ? 8 : 4) * 64, NB == 5 ? 1 : 2) void atten
       const char* img = m == 0 ? Ks : (m == 1 ? Qs : Os);
       *(bf16x8*)(a.dqkv + (row0 + row) * ld + m * a.H + hd * 64 + c * 8) = *(const bf16x8*)(img + ab_rc(row, c));
     }
+  }
+  if (a.dsum && tid < 192) {   // the blocks' column sums in block order -> dsum[b][3H]
+    const int m = tid >> 6, col = tid & 63;
+    float t = 0.f;
+#pragma unroll
+    for (int k = 0; k < NB; ++k) t += csum[(k * 3 + m) * 64 + col];
+    a.dsum[b * 3 * (int64_t)a.H + m * a.H + hd * 64 + col] = t;
   }
 }
 
@@ -751,7 +797,7 @@ int drt_colsum_bf16(const void* x, int64_t M, int64_t N, float* out, void* ws, s
 
 size_t drt_layernorm_bwd_workspace(int64_t M, int32_t H) {
   if (M <= 0 || H <= 0) return 0;
-  return (size_t)2 * kLnBwdBlocks * (size_t)H * sizeof(float) + drt_colsum_workspace(kLnBwdBlocks, 2 * H);
+  return (size_t)3 * kLnBwdBlocks * (size_t)H * sizeof(float) + drt_colsum_workspace(kLnBwdBlocks, 2 * H);
 }
 
 // dx = LN backward of dy through out = LN(x) (gamma; x = the bf16 pre-LN sums the forward
@@ -767,32 +813,51 @@ int drt_layernorm_bwd_bf16(const void* dy, const void* x, const float* gamma, fl
                                      ws_bytes, stream);
 }
 
+int drt_layernorm_bwd_sum_bf16(const void* dy, const void* x, const float* gamma, float eps, int64_t M, int32_t H,
+                               const void* dres, void* dx, void* dx_drop, float drop_p, uint64_t seed, uint64_t site,
+                               float* dgamma, float* dbeta, float* dsum, void* ws, size_t ws_bytes, void* stream);
+
 // The same, also writing dx_drop = dropout(dx) with drt_dropout_add_bf16's mask of (drop_p, seed, site)
 // (the gradient entering the linear whose output HF dropped before this LayerNorm's residual add).
 int drt_layernorm_bwd_drop_bf16(const void* dy, const void* x, const float* gamma, float eps, int64_t M, int32_t H,
                                 const void* dres, void* dx, void* dx_drop, float drop_p, uint64_t seed, uint64_t site,
                                 float* dgamma, float* dbeta, void* ws, size_t ws_bytes, void* stream) {
+  return drt_layernorm_bwd_sum_bf16(dy, x, gamma, eps, M, H, dres, dx, dx_drop, drop_p, seed, site, dgamma, dbeta,
+                                    nullptr, ws, ws_bytes, stream);
+}
+
+// The same, also writing dsum [H] fp32 = the column sums of the gradient it hands down (dx_drop,
+// or dx without dropout) -- the bias gradient of the linear feeding this LayerNorm.
+int drt_layernorm_bwd_sum_bf16(const void* dy, const void* x, const float* gamma, float eps, int64_t M, int32_t H,
+                               const void* dres, void* dx, void* dx_drop, float drop_p, uint64_t seed, uint64_t site,
+                               float* dgamma, float* dbeta, float* dsum, void* ws, size_t ws_bytes, void* stream) {
   DRT_REQUIRE(M > 0 && H > 0 && H % 256 == 0 && H <= 1024);
   DRT_REQUIRE(!dx_drop || (drop_p >= 0.f && drop_p < 1.f));
   DRT_REQUIRE(dy && x && gamma && dx && dgamma && dbeta && ws && ws_bytes >= drt_layernorm_bwd_workspace(M, H));
   hipStream_t s = (hipStream_t)stream;
-  float* part = (float*)ws;   // [2 * blocks][H]: dgamma rows then dbeta rows
+  float* part = (float*)ws;   // [3 * blocks][H]: dgamma rows, dbeta rows, dsum rows
   const dim3 grid(kLnBwdBlocks);
-#define LNB(E) hipLaunchKernelGGL(layernorm_bwd_kernel<E>, grid, dim3(256), 0, s, (const __bf16*)dy, (const __bf16*)x, \
-                                  gamma, eps, M, (int)H, (const __bf16*)dres, (__bf16*)dx, part, (__bf16*)dx_drop, \
-                                  drop_p, seed, site)
+#define LNB(E, S)                                                                                                   \
+  hipLaunchKernelGGL((layernorm_bwd_kernel<E, S>), grid, dim3(256), 0, s, (const __bf16*)dy, (const __bf16*)x, gamma, \
+                     eps, M, (int)H, (const __bf16*)dres, (__bf16*)dx, part, (__bf16*)dx_drop, drop_p, seed, site)
+#define LNB2(E) \
+  if (dsum) LNB(E, true); \
+  else LNB(E, false);
   switch (H / 64) {
-    case 4: LNB(4); break;
-    case 8: LNB(8); break;
-    case 12: LNB(12); break;
-    case 16: LNB(16); break;
+    case 4: LNB2(4); break;
+    case 8: LNB2(8); break;
+    case 12: LNB2(12); break;
+    case 16: LNB2(16); break;
     default: return DRT_EINVAL;
   }
+#undef LNB2
 #undef LNB
-  float* ws2 = part + (size_t)2 * kLnBwdBlocks * H;
+  float* ws2 = part + (size_t)3 * kLnBwdBlocks * H;
   int rc = colsum_launch<float>(part, kLnBwdBlocks, H, dgamma, ws2, s);
   if (rc) return rc;
-  return colsum_launch<float>(part + (size_t)kLnBwdBlocks * H, kLnBwdBlocks, H, dbeta, ws2, s);
+  rc = colsum_launch<float>(part + (size_t)kLnBwdBlocks * H, kLnBwdBlocks, H, dbeta, ws2, s);
+  if (rc || !dsum) return rc;
+  return colsum_launch<float>(part + (size_t)2 * kLnBwdBlocks * H, kLnBwdBlocks, H, dsum, ws2, s);
 }
 
 int drt_gelu_bwd_bf16(const void* dy, const void* pre, int64_t n, void* dx, void* stream) {
@@ -836,22 +901,56 @@ int drt_attention_train_bwd_bf16(const void* qkv, const void* ctx, const void* d
 
 // The same reading the forward's keep bits (drt_attention_train_fwd_bits_bf16) instead of re-hashing
 // every (query, key) twice (dK / dV and dQ phases); NULL drop_bits = regenerate from the hash.
+static int attention_bwd_launch(const void* qkv, const void* ctx, const void* dctx, const float* lse,
+                                const int64_t* mask, const uint32_t* drop_bits, void* dqkv, int64_t B, int64_t L,
+                                int32_t heads, int32_t head_dim, float scale, float drop_p, uint64_t seed,
+                                uint64_t site, float* dsum_part, void* stream);
+
 int drt_attention_train_bwd_bits_bf16(const void* qkv, const void* ctx, const void* dctx, const float* lse,
                                       const int64_t* mask, const uint32_t* drop_bits, void* dqkv, int64_t B, int64_t L,
                                       int32_t heads, int32_t head_dim, float scale, float drop_p, uint64_t seed,
                                       uint64_t site, void* stream) {
+  return attention_bwd_launch(qkv, ctx, dctx, lse, mask, drop_bits, dqkv, B, L, heads, head_dim, scale, drop_p, seed,
+                              site, nullptr, stream);
+}
+
+size_t drt_attention_train_bwd_bias_workspace(int64_t B, int32_t heads, int32_t head_dim) {
+  if (B <= 0 || heads <= 0 || head_dim <= 0) return 0;
+  const int64_t n = 3 * (int64_t)heads * head_dim;
+  return (size_t)B * n * sizeof(float) + drt_colsum_workspace(B, n);
+}
+
+// The same, also writing dbias [3H] fp32 = the column sums of dQKV (the query / key / value
+// bias gradients) from per-sequence partials the kernel leaves in ws -- no pass over dQKV.
+int drt_attention_train_bwd_bias_bf16(const void* qkv, const void* ctx, const void* dctx, const float* lse,
+                                      const int64_t* mask, const uint32_t* drop_bits, void* dqkv, int64_t B, int64_t L,
+                                      int32_t heads, int32_t head_dim, float scale, float drop_p, uint64_t seed,
+                                      uint64_t site, float* dbias, void* ws, size_t ws_bytes, void* stream) {
+  DRT_REQUIRE(dbias && B > 0 && ws && ws_bytes >= drt_attention_train_bwd_bias_workspace(B, heads, head_dim));
+  float* part = (float*)ws;
+  int rc = attention_bwd_launch(qkv, ctx, dctx, lse, mask, drop_bits, dqkv, B, L, heads, head_dim, scale, drop_p,
+                                seed, site, part, stream);
+  if (rc) return rc;
+  const int64_t n = 3 * (int64_t)heads * head_dim;
+  return colsum_launch<float>(part, B, n, dbias, part + (size_t)B * n, (hipStream_t)stream);
+}
+
+static int attention_bwd_launch(const void* qkv, const void* ctx, const void* dctx, const float* lse,
+                                const int64_t* mask, const uint32_t* drop_bits, void* dqkv, int64_t B, int64_t L,
+                                int32_t heads, int32_t head_dim, float scale, float drop_p, uint64_t seed,
+                                uint64_t site, float* dsum_part, void* stream) {
   DRT_REQUIRE(B >= 0 && L > 0 && L <= kAbMaxSeq && heads > 0 && head_dim == 64);
   DRT_REQUIRE(drop_p >= 0.0f && drop_p < 1.0f);
   if (B == 0) return DRT_OK;
   DRT_REQUIRE(qkv && ctx && dctx && lse && dqkv);
   AttnBwdArgs a{(const __bf16*)qkv, (const __bf16*)ctx, (const __bf16*)dctx, lse, mask, (__bf16*)dqkv, B, L,
-                heads, heads * 64, scale, drop_p, seed, site, drop_bits};
+                heads, heads * 64, scale, drop_p, seed, site, drop_bits, dsum_part};
   const int Lp = ((int)L + 31) & ~31;
   const int nb = Lp / 32;
   const dim3 grid((unsigned)(B * heads));
   const bool drop = drop_p > 0.0f;
   // register-resident P / dS; dropout from the forward's keep bits (or the same bits drawn again)
-  const size_t lds = (size_t)4 * Lp * kAbRow + (size_t)3 * Lp * 4 + (drop ? (size_t)nb * Lp * 4 : 0);
+  size_t lds = (size_t)4 * Lp * kAbRow + (size_t)3 * Lp * 4 + (drop ? (size_t)nb * Lp * 4 : 0);
   DRT_REQUIRE(lds <= 160 * 1024);
   static bool rk_attr = false;
   if (!rk_attr) {

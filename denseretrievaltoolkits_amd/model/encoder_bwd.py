@@ -53,13 +53,16 @@ def colsum(x: torch.Tensor) -> torch.Tensor:
 
 
 def linear_backward(dy: torch.Tensor, x: torch.Tensor, w_t: torch.Tensor, want_dx: bool = True,
-                    resid: Optional[torch.Tensor] = None, gelu_pre: Optional[torch.Tensor] = None
+                    resid: Optional[torch.Tensor] = None, gelu_pre: Optional[torch.Tensor] = None,
+                    db: Optional[torch.Tensor] = None
                     ) -> Tuple[Optional[torch.Tensor], torch.Tensor, torch.Tensor]:
     """Gradients of y = x W^T + b (nn.Linear, W [N, K]) for dy [T, N], x [T, K] (bf16 CUDA),
     given w_t = W^T [K, N] bf16.  Returns (dx bf16 [T, K] or None, dW fp32 [N, K], db fp32 [N]);
     ``resid`` [T, K] bf16 is added to dx in the dgrad GEMM's epilogue (a residual branch);
     ``gelu_pre`` [T, K] (x = GELU(gelu_pre)) makes dx the gradient of gelu_pre instead, the GELU
-    backward applied in the same epilogue (drt_linear_bf16_ex)."""
+    backward applied in the same epilogue (drt_linear_bf16_ex); ``db``: the bias gradient already
+    produced by dy's producer (the LayerNorm / attention backward), returned as is instead of a
+    column-sum pass over dy."""
     lib = _native.load()
     dev = dy.device
     s = _native.stream_ptr(dev)
@@ -82,7 +85,7 @@ def linear_backward(dy: torch.Tensor, x: torch.Tensor, w_t: torch.Tensor, want_d
             _native.check(lib.drt_linear_bf16_ws(dy.data_ptr(), w_t.data_ptr(), None, _ptr(resid), dx.data_ptr(), T, K,
                                                  N, 0, _ptr(ws), nb, s), "dgrad")
     dW = wgrad(dy, x)
-    return dx, dW, colsum(dy)
+    return dx, dW, (db if db is not None else colsum(dy))
 
 
 WGRAD_TN = True   # A/B switch: False = transposed operand copies + NT GEMM (the round-1 path)
@@ -116,10 +119,12 @@ def wgrad(dy: torch.Tensor, x: torch.Tensor) -> torch.Tensor:
 
 
 def layernorm_backward(dy: torch.Tensor, x: torch.Tensor, gamma: torch.Tensor, eps: float,
-                       dres: Optional[torch.Tensor] = None, drop=None):
+                       dres: Optional[torch.Tensor] = None, drop=None, want_sum: bool = False):
     """(dx bf16 [M, H], dgamma fp32 [H], dbeta fp32 [H]) of out = LN(x) (x = the bf16 pre-LN sums).
     ``drop`` = (p, seed, site): also return dropout(dx) with that mask (drt_layernorm_bwd_drop_bf16)
-    as a fourth value."""
+    as a fourth value.  ``want_sum``: also return (last) the column sums of the gradient handed
+    down -- dropout(dx), or dx -- i.e. the bias gradient of the linear below
+    (drt_layernorm_bwd_sum_bf16)."""
     lib = _native.load()
     M, H = x.shape
     dev = x.device
@@ -130,13 +135,13 @@ def layernorm_backward(dy: torch.Tensor, x: torch.Tensor, gamma: torch.Tensor, e
     ws = _ws(nb, dev)
     dxd = torch.empty_like(dx) if drop is not None else None
     p, seed, site = drop if drop is not None else (0.0, 0, 0)
-    _native.check(lib.drt_layernorm_bwd_drop_bf16(dy.data_ptr(), x.data_ptr(), gamma.data_ptr(), float(eps), M, H,
-                                                  _ptr(dres), dx.data_ptr(), _ptr(dxd), float(p), seed, site,
-                                                  dg.data_ptr(), db.data_ptr(), _ptr(ws), nb,
-                                                  _native.stream_ptr(dev)), "drt_layernorm_bwd_drop_bf16")
-    if drop is not None:
-        return dx, dg, db, dxd
-    return dx, dg, db
+    dsum = torch.empty(H, dtype=torch.float32, device=dev) if want_sum else None
+    _native.check(lib.drt_layernorm_bwd_sum_bf16(dy.data_ptr(), x.data_ptr(), gamma.data_ptr(), float(eps), M, H,
+                                                 _ptr(dres), dx.data_ptr(), _ptr(dxd), float(p), seed, site,
+                                                 dg.data_ptr(), db.data_ptr(), _ptr(dsum), _ptr(ws), nb,
+                                                 _native.stream_ptr(dev)), "drt_layernorm_bwd_sum_bf16")
+    out = (dx, dg, db) + ((dxd,) if drop is not None else ()) + ((dsum,) if want_sum else ())
+    return out
 
 
 def gelu_backward(dy: torch.Tensor, pre: torch.Tensor) -> torch.Tensor:

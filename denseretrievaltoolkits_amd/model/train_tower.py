@@ -225,26 +225,33 @@ def layer_backward(st: _Step, i: int, saved, d) -> Tuple[torch.Tensor, Dict[str,
     s_att, s_out1, s_out2 = dropout_sites(i)
     # LN backward also emits the dropped gradient entering FFN2; FFN2's dgrad applies the GELU
     # backward in its epilogue (-> d fpre)
+    # (the LayerNorm backwards also return the column sums of what they hand down: the dense
+    # biases' gradients, without a pass over dy2 / dy1)
     if ph > 0:
-        dx2, dg2, db2, dy2 = layernorm_backward(d, x2, ly["g2"], eps, drop=(ph, seed, s_out2))
+        dx2, dg2, db2, dy2, sum2 = layernorm_backward(d, x2, ly["g2"], eps, drop=(ph, seed, s_out2), want_sum=True)
     else:
-        dx2, dg2, db2 = layernorm_backward(d, x2, ly["g2"], eps)
+        dx2, dg2, db2, sum2 = layernorm_backward(d, x2, ly["g2"], eps, want_sum=True)
         dy2 = dx2
-    dfpre, dwf, dbf = linear_backward(dy2, f, ly["wf_t"], gelu_pre=fpre)
+    dfpre, dwf, dbf = linear_backward(dy2, f, ly["wf_t"], gelu_pre=fpre, db=sum2)
     dh1, dwi, dbi = linear_backward(dfpre, h1, ly["wi_t"], resid=dx2)
     if ph > 0:
-        dx1, dg1, db1, dy1 = layernorm_backward(dh1, x1, ly["g1"], eps, drop=(ph, seed, s_out1))
+        dx1, dg1, db1, dy1, sum1 = layernorm_backward(dh1, x1, ly["g1"], eps, drop=(ph, seed, s_out1), want_sum=True)
     else:
-        dx1, dg1, db1 = layernorm_backward(dh1, x1, ly["g1"], eps)
+        dx1, dg1, db1, sum1 = layernorm_backward(dh1, x1, ly["g1"], eps, want_sum=True)
         dy1 = dx1
-    dctx, dwo, dbo = linear_backward(dy1, ctx, ly["wo_t"])
+    dctx, dwo, dbo = linear_backward(dy1, ctx, ly["wo_t"], db=sum1)
     dqkv = torch.empty_like(qkv)
-    _native.check(lib.drt_attention_train_bwd_bits_bf16(qkv.data_ptr(), ctx.data_ptr(), dctx.data_ptr(),
+    # the attention backward also leaves per-sequence column sums of dQKV: the q / k / v bias
+    # gradients without a pass over dQKV
+    dbqkv = torch.empty(3 * H, dtype=torch.float32, device=st.dev)
+    nb = int(lib.drt_attention_train_bwd_bias_workspace(st.B, heads, H // heads))
+    ws = torch.empty((nb + 3) // 4, dtype=torch.float32, device=st.dev)
+    _native.check(lib.drt_attention_train_bwd_bias_bf16(qkv.data_ptr(), ctx.data_ptr(), dctx.data_ptr(),
                                                         lse.data_ptr(), _ptr(st.mask), _ptr(bits), dqkv.data_ptr(),
                                                         st.B, st.L, heads, H // heads, st.scale, float(pa), seed,
-                                                        s_att, s),
-                  "drt_attention_train_bwd_bits_bf16")
-    d_in, dwqkv, dbqkv = linear_backward(dqkv, h, ly["wqkv_t"], resid=dx1)
+                                                        s_att, dbqkv.data_ptr(), ws.data_ptr(), nb, s),
+                  "drt_attention_train_bwd_bias_bf16")
+    d_in, dwqkv, dbqkv = linear_backward(dqkv, h, ly["wqkv_t"], resid=dx1, db=dbqkv)
     grads = {}
     grads[p + "output.LayerNorm.weight"], grads[p + "output.LayerNorm.bias"] = dg2, db2
     grads[p + "output.dense.weight"], grads[p + "output.dense.bias"] = dwf, dbf

@@ -227,6 +227,13 @@ int drt_layernorm_bwd_drop_bf16(const void* dy, const void* x, const float* gamm
                                 int64_t M, int32_t H, const void* dres, void* dx, void* dx_drop,
                                 float drop_p, uint64_t seed, uint64_t site, float* dgamma,
                                 float* dbeta, void* ws, size_t ws_bytes, void* stream);
+/* The same, also writing dsum [H] fp32 = the column sums of the gradient it hands down (dx_drop,
+ * or dx when dx_drop is NULL): the bias gradient of the linear feeding this LayerNorm
+ * (BertSelfOutput / BertOutput dense.bias) without a separate pass over that gradient.   */
+int drt_layernorm_bwd_sum_bf16(const void* dy, const void* x, const float* gamma, float eps,
+                               int64_t M, int32_t H, const void* dres, void* dx, void* dx_drop,
+                               float drop_p, uint64_t seed, uint64_t site, float* dgamma,
+                               float* dbeta, float* dsum, void* ws, size_t ws_bytes, void* stream);
 size_t drt_colsum_workspace(int64_t M, int64_t N);
 int drt_colsum_bf16(const void* x, int64_t M, int64_t N, float* out, void* ws, size_t ws_bytes,
                     void* stream);
@@ -288,6 +295,15 @@ int drt_attention_train_bwd_bits_bf16(const void* qkv, const void* ctx, const vo
                                       const int64_t* mask, const uint32_t* drop_bits, void* dqkv, int64_t B,
                                       int64_t L, int32_t heads, int32_t head_dim, float scale, float drop_p,
                                       uint64_t seed, uint64_t site, void* stream);
+/* drt_attention_train_bwd_bias_bf16: the same, also writing dbias [3H] fp32 = the column sums of
+ * dQKV (the query / key / value bias gradients of BertSelfAttention) from per-sequence partials
+ * left in ws (drt_attention_train_bwd_bias_workspace bytes), without a pass over dQKV.        */
+size_t drt_attention_train_bwd_bias_workspace(int64_t B, int32_t heads, int32_t head_dim);
+int drt_attention_train_bwd_bias_bf16(const void* qkv, const void* ctx, const void* dctx, const float* lse,
+                                      const int64_t* mask, const uint32_t* drop_bits, void* dqkv, int64_t B,
+                                      int64_t L, int32_t heads, int32_t head_dim, float scale, float drop_p,
+                                      uint64_t seed, uint64_t site, float* dbias, void* ws, size_t ws_bytes,
+                                      void* stream);
 int drt_pool_bf16(const void* hidden, const int64_t* mask, int64_t B, int64_t L, int32_t H,
                   int32_t mode, float* out, void* out_bf16, void* stream);
 int drt_l2_normalize_f32(float* x, int64_t B, int32_t H, void* out_bf16, void* stream);

@@ -174,6 +174,20 @@ def test_attention_bwd_vs_torch(dev, B, L):
         assert err <= 2e-2 * max(1.0, want.abs().max().item()), (name, err, want.abs().max().item())
         cos = torch.nn.functional.cosine_similarity(got.flatten(), want.flatten(), dim=0).item()
         assert cos > 0.999, (name, cos)
+    # drt_attention_train_bwd_bias_bf16: the same dQKV bit for bit plus its column sums (the q / k / v
+    # bias gradients) = fp64 sums of the stored bf16 dQKV, to fp32 summation
+    dqkv2 = torch.zeros_like(dqkv)
+    dbias = torch.empty(3 * H, device=dev)
+    nb = int(lib.drt_attention_train_bwd_bias_workspace(B, heads, dh))
+    ws = torch.empty((nb + 3) // 4, device=dev)
+    _native.check(lib.drt_attention_train_bwd_bias_bf16(qkv.data_ptr(), ctx.data_ptr(), dctx.data_ptr(),
+                                                        lse.data_ptr(), mask.data_ptr(), None, dqkv2.data_ptr(), B,
+                                                        L, heads, dh, scale, 0.0, 0, 0, dbias.data_ptr(),
+                                                        ws.data_ptr(), nb, s), "bwd+bias")
+    torch.cuda.synchronize()
+    assert torch.equal(dqkv2, dqkv)
+    ref_b = dqkv.double().sum(0)
+    assert bool(((dbias.double() - ref_b).abs() <= 1e-5 * dqkv.double().abs().sum(0) + 1e-6).all())
 
 
 @pytest.mark.parametrize("R,C,pad", [(1000, 768, 24), (65536, 3072, 0), (77, 130, 3)])
@@ -348,6 +362,15 @@ def test_layernorm_bwd_drop_output_equals_dropout_kernel(dev, M, H):
     torch.cuda.synchronize()
     assert torch.equal(dx, dx0) and torch.equal(dg, dg0) and torch.equal(db, db0)
     assert torch.equal(dxd, ref)
+    # drt_layernorm_bwd_sum_bf16: the same outputs plus the column sums of what it hands down
+    # (the linear-bias gradient) = fp64 column sums of the stored bf16 gradient, to fp32 summation
+    dx_s, dg_s, db_s, dxd_s, sd = layernorm_backward(dy, x, gamma, 1e-12, drop=(0.1, 99, 5), want_sum=True)
+    dx_n, _, _, sn = layernorm_backward(dy, x, gamma, 1e-12, want_sum=True)
+    assert torch.equal(dx_s, dx) and torch.equal(dxd_s, dxd) and torch.equal(dg_s, dg) and torch.equal(db_s, db)
+    for s_, t_ in ((sd, dxd), (sn, dx_n)):
+        ref_s = t_.double().sum(0)
+        tol = 1e-5 * t_.double().abs().sum(0) + 1e-6
+        assert bool(((s_.double() - ref_s).abs() <= tol).all())
 
 
 @pytest.mark.parametrize("L,B", [(128, 6), (156, 5), (37, 9), (32, 4)])
