@@ -68,6 +68,9 @@ _SIGNATURES = [
                                        c_vp]),
     ("drt_colsum_workspace", c_sz, [c_i64, c_i64]),
     ("drt_colsum_bf16", c_i32, [c_vp, c_i64, c_i64, c_vp, c_vp, c_sz, c_vp]),
+    ("drt_colsum_f32", c_i32, [c_vp, c_i64, c_i64, c_vp, c_vp, c_sz, c_vp]),
+    ("drt_linear_dgelu_bias_workspace", c_sz, [c_i64, c_i64, c_i64]),
+    ("drt_linear_dgelu_bias_bf16", c_i32, [c_vp, c_vp, c_vp, c_vp, c_i64, c_i64, c_i64, c_vp, c_vp, c_sz, c_vp]),
     ("drt_gelu_bwd_bf16", c_i32, [c_vp, c_vp, c_i64, c_vp, c_vp]),
     ("drt_linear_wgrad_workspace", c_sz, [c_i64, c_i64, c_i64]),
     ("drt_linear_wgrad_bf16", c_i32, [c_vp, c_vp, c_vp, c_i64, c_i64, c_i64, c_vp, c_sz, c_vp]),

@@ -785,6 +785,16 @@ size_t drt_colsum_workspace(int64_t M, int64_t N) {
   return slabs > 1 ? (size_t)slabs * (size_t)N * sizeof(float) : 0;
 }
 
+int drt_colsum_f32(const float* x, int64_t M, int64_t N, float* out, void* ws, size_t ws_bytes, void* stream) {
+  DRT_REQUIRE(M >= 0 && N >= 0);
+  if (N == 0) return DRT_OK;
+  DRT_REQUIRE(out);
+  hipStream_t s = (hipStream_t)stream;
+  if (M == 0) return hip_status(hipMemsetAsync(out, 0, N * sizeof(float), s));
+  DRT_REQUIRE(x && ws_bytes >= drt_colsum_workspace(M, N) && (ws || drt_colsum_workspace(M, N) == 0));
+  return colsum_launch<float>(x, M, N, out, (float*)ws, s);
+}
+
 int drt_colsum_bf16(const void* x, int64_t M, int64_t N, float* out, void* ws, size_t ws_bytes, void* stream) {
   DRT_REQUIRE(M >= 0 && N >= 0);
   if (N == 0) return DRT_OK;

@@ -40,6 +40,8 @@ struct GemmArgs {
   void* C2;                 // EPI_PRE: bf16 [m][ldc] pre-activation (bias added, before GELU)
   float drop_p;             // EPI_DROP: dropout probability, hash seed and site (drt_common.h)
   uint64_t seed, site;
+  float* csum;              // optional (whole-line kernel, fp32-staged epilogue): column sums of the
+                            // stored output per 128-row half tile, [2 * ceil(m / 256)][n]
 };
 
 __device__ __forceinline__ void g_glds16(const void* gsrc, uint32_t lds_addr) {
@@ -706,6 +708,7 @@ __device__ __forceinline__ void pp_epilogue_lds(const GemmArgs& a, f32x4 (&acc)[
     // with a residual (pre-LayerNorm sums) stages fp32, so the sum is rounded once, at the store.
     // Residual rows of pass 1 are requested once pass 0 is staged (its accumulators are dead).
     const int c8 = lane & 7;
+    float cs[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};   // csum: this lane's 8 columns
     bf16x8 rq[2][8];
     auto load_rq = [&](int h) {
 #pragma unroll
@@ -761,6 +764,10 @@ __device__ __forceinline__ void pp_epilogue_lds(const GemmArgs& a, f32x4 (&acc)[
 #pragma unroll
             for (int u = 0; u < 8; ++u) o[u] = (__bf16)v[u];
             *(bf16x8*)((__bf16*)a.C + row * a.ldc + colw + c8 * 8) = o;
+            if (a.csum) {
+#pragma unroll
+              for (int u = 0; u < 8; ++u) cs[u] += (float)o[u];
+            }
           } else {
             *(f32x4*)((float*)a.C + row * a.ldc + colw + c8 * 8) = f32x4{v[0], v[1], v[2], v[3]};
             *(f32x4*)((float*)a.C + row * a.ldc + colw + c8 * 8 + 4) = f32x4{v[4], v[5], v[6], v[7]};
@@ -768,6 +775,21 @@ __device__ __forceinline__ void pp_epilogue_lds(const GemmArgs& a, f32x4 (&acc)[
         }
       }
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    }
+    if (OUT_BF16 && a.csum) {   // the 8 lanes of each column group hold 16 rows each: xor 8 / 16 / 32
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        float x = cs[u];
+        x += __shfl_xor(x, 8, 64);
+        x += __shfl_xor(x, 16, 64);
+        x += __shfl_xor(x, 32, 64);
+        cs[u] = x;
+      }
+      if (lane < 8) {
+        float* dst = a.csum + ((m0 / 256) * 2 + grp) * a.n + colw + c8 * 8;
+        *(f32x4*)dst = f32x4{cs[0], cs[1], cs[2], cs[3]};
+        *(f32x4*)(dst + 4) = f32x4{cs[4], cs[5], cs[6], cs[7]};
+      }
     }
   }
 }
@@ -1301,6 +1323,59 @@ extern "C" int drt_linear_bf16_ex(const void* X, const void* W, const float* bia
   const int epi = (bias ? EPI_BIAS : 0) | (gelu ? EPI_GELU : 0) | (residual ? EPI_RESID : 0) |
                   (gelu_pre ? EPI_DGELU : 0) | (Y_pre ? EPI_PRE : 0) | (drop ? EPI_DROP : 0);
   return launch_gemm(a, !f32, epi, ws ? ws_bytes : 0, (hipStream_t)stream);
+}
+
+// FFN1 dgrad with the GELU backward AND its bias gradient: dX = (dY W^T) * GELU'(pre) (bf16, as
+// drt_linear_bf16_ex with gelu_pre), dbias[N] = column sums of the stored dX.  On the whole-line
+// plan with full column tiles the GEMM epilogue leaves per-half-tile column sums (no pass over dX);
+// otherwise dX is summed after the GEMM.  ws: the GEMM's split partials, then the column-sum
+// partials and their reduction scratch.
+static bool dgelu_fused(int64_t M, int64_t N, int64_t K) {
+  return plan_gemm(M, N, K).path == GP_LARGE && N % kL == 0;
+}
+extern "C" size_t drt_linear_dgelu_bias_workspace(int64_t M, int64_t N, int64_t K) {
+  if (M <= 0 || N <= 0 || K <= 0 || K % 64) return 0;
+  const size_t g = (plan_gemm(M, N, K).ws_bytes + 255) & ~(size_t)255;
+  if (dgelu_fused(M, N, K)) {
+    const int64_t rows = 2 * ceil_div(M, kL);
+    return g + (size_t)rows * N * sizeof(float) + drt_colsum_workspace(rows, N);
+  }
+  return g + drt_colsum_workspace(M, N);
+}
+
+extern "C" int drt_linear_dgelu_bias_bf16(const void* dY, const void* Wt, const void* gelu_pre, void* dX, int64_t M,
+                                          int64_t N, int64_t K, float* dbias, void* ws, size_t ws_bytes,
+                                          void* stream) {
+  DRT_REQUIRE(M > 0 && N > 0 && K > 0 && K % 64 == 0 && dY && Wt && gelu_pre && dX && dbias);
+  DRT_REQUIRE(ws_bytes >= drt_linear_dgelu_bias_workspace(M, N, K) && (ws || ws_bytes == 0));
+  hipStream_t s = (hipStream_t)stream;
+  const size_t g = (plan_gemm(M, N, K).ws_bytes + 255) & ~(size_t)255;
+  char* rest = (char*)ws + g;
+  GemmArgs a{};
+  a.A = (const __bf16*)dY;
+  a.B = (const __bf16*)Wt;
+  a.C = dX;
+  a.R = (const __bf16*)gelu_pre;
+  a.m = M;
+  a.n = N;
+  a.k = K;
+  a.lda = K;
+  a.ldb = K;
+  a.ldc = N;
+  a.ldr = N;
+  a.alpha = 1.0f;
+  a.ws = (float*)ws;
+  if (dgelu_fused(M, N, K)) {
+    const int64_t rows = 2 * ceil_div(M, kL);
+    a.csum = (float*)rest;
+    int rc = launch_gemm(a, true, EPI_DGELU, g, s);
+    if (rc) return rc;
+    return drt_colsum_f32(a.csum, rows, N, dbias, rest + (size_t)rows * N * sizeof(float),
+                          drt_colsum_workspace(rows, N), stream);
+  }
+  int rc = launch_gemm(a, true, EPI_DGELU, g, s);
+  if (rc) return rc;
+  return drt_colsum_bf16(dX, M, N, dbias, rest, drt_colsum_workspace(M, N), stream);
 }
 
 // Weight gradient of nn.Linear without transposed operand copies: dW[N][K] fp32 = dY[T][N]^T . X[T][K]

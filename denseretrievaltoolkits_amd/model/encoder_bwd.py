@@ -54,7 +54,7 @@ def colsum(x: torch.Tensor) -> torch.Tensor:
 
 def linear_backward(dy: torch.Tensor, x: torch.Tensor, w_t: torch.Tensor, want_dx: bool = True,
                     resid: Optional[torch.Tensor] = None, gelu_pre: Optional[torch.Tensor] = None,
-                    db: Optional[torch.Tensor] = None
+                    db: Optional[torch.Tensor] = None, dx_colsum: Optional[torch.Tensor] = None
                     ) -> Tuple[Optional[torch.Tensor], torch.Tensor, torch.Tensor]:
     """Gradients of y = x W^T + b (nn.Linear, W [N, K]) for dy [T, N], x [T, K] (bf16 CUDA),
     given w_t = W^T [K, N] bf16.  Returns (dx bf16 [T, K] or None, dW fp32 [N, K], db fp32 [N]);
@@ -62,7 +62,9 @@ def linear_backward(dy: torch.Tensor, x: torch.Tensor, w_t: torch.Tensor, want_d
     ``gelu_pre`` [T, K] (x = GELU(gelu_pre)) makes dx the gradient of gelu_pre instead, the GELU
     backward applied in the same epilogue (drt_linear_bf16_ex); ``db``: the bias gradient already
     produced by dy's producer (the LayerNorm / attention backward), returned as is instead of a
-    column-sum pass over dy."""
+    column-sum pass over dy.  ``dx_colsum`` [K] fp32 (with ``gelu_pre``): also filled with the column
+    sums of dx -- the bias gradient of the GELU's linear -- from the dgrad GEMM's epilogue
+    (drt_linear_dgelu_bias_bf16)."""
     lib = _native.load()
     dev = dy.device
     s = _native.stream_ptr(dev)
@@ -75,7 +77,15 @@ def linear_backward(dy: torch.Tensor, x: torch.Tensor, w_t: torch.Tensor, want_d
         dx = torch.empty((T, K), dtype=torch.bfloat16, device=dev)
         nb = int(lib.drt_linear_workspace(T, K, N))
         ws = _ws(nb, dev)
-        if gelu_pre is not None:
+        if gelu_pre is not None and dx_colsum is not None:
+            if resid is not None:
+                raise ValueError("linear_backward: gelu_pre and resid are exclusive")
+            nb = int(lib.drt_linear_dgelu_bias_workspace(T, K, N))
+            ws = _ws(nb, dev)
+            _native.check(lib.drt_linear_dgelu_bias_bf16(dy.data_ptr(), w_t.data_ptr(), gelu_pre.data_ptr(),
+                                                         dx.data_ptr(), T, K, N, dx_colsum.data_ptr(), _ptr(ws), nb,
+                                                         s), "dgrad (GELU backward + bias gradient epilogue)")
+        elif gelu_pre is not None:
             if resid is not None:
                 raise ValueError("linear_backward: gelu_pre and resid are exclusive")
             _native.check(lib.drt_linear_bf16_ex(dy.data_ptr(), w_t.data_ptr(), None, None, gelu_pre.data_ptr(),

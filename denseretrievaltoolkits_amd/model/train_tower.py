@@ -232,8 +232,9 @@ def layer_backward(st: _Step, i: int, saved, d) -> Tuple[torch.Tensor, Dict[str,
     else:
         dx2, dg2, db2, sum2 = layernorm_backward(d, x2, ly["g2"], eps, want_sum=True)
         dy2 = dx2
-    dfpre, dwf, dbf = linear_backward(dy2, f, ly["wf_t"], gelu_pre=fpre, db=sum2)
-    dh1, dwi, dbi = linear_backward(dfpre, h1, ly["wi_t"], resid=dx2)
+    dbi = torch.empty(fpre.shape[1], dtype=torch.float32, device=st.dev)   # from FFN2's dgrad epilogue
+    dfpre, dwf, dbf = linear_backward(dy2, f, ly["wf_t"], gelu_pre=fpre, db=sum2, dx_colsum=dbi)
+    dh1, dwi, dbi = linear_backward(dfpre, h1, ly["wi_t"], resid=dx2, db=dbi)
     if ph > 0:
         dx1, dg1, db1, dy1, sum1 = layernorm_backward(dh1, x1, ly["g1"], eps, drop=(ph, seed, s_out1), want_sum=True)
     else:

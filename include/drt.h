@@ -187,6 +187,14 @@ int drt_linear_ln_bf16_ws(const void* X, const void* W, const float* bias, const
  *     (drop_p, seed, site) at the flat index m * N + n.
  * Replaces linear -> drt_gelu_bf16, dgrad -> drt_gelu_bwd_bf16 and linear -> drt_dropout_add_bf16
  * pairs of the training tower (BertIntermediate / BertOutput / BertSelfOutput under autograd). */
+/* drt_linear_dgelu_bias_bf16: the FFN1 dgrad with its GELU backward and bias gradient:
+ *   dX [M,N] bf16 = (dY[M,K] . Wt[N,K]^T) * GELU'(pre[M,N]) (as drt_linear_bf16_ex with gelu_pre),
+ *   dbias [N] fp32 = column sums of the stored dX -- from the GEMM epilogue when the whole-line
+ *   plan applies with N % 256 == 0 (no pass over dX), else summed after it.  ws of
+ *   drt_linear_dgelu_bias_workspace(M, N, K) bytes.  (BertIntermediate, modeling_bert.py:325-337.) */
+size_t drt_linear_dgelu_bias_workspace(int64_t M, int64_t N, int64_t K);
+int drt_linear_dgelu_bias_bf16(const void* dY, const void* Wt, const void* gelu_pre, void* dX, int64_t M,
+                               int64_t N, int64_t K, float* dbias, void* ws, size_t ws_bytes, void* stream);
 int drt_linear_bf16_ex(const void* X, const void* W, const float* bias, const void* residual,
                        const void* gelu_pre, void* Y, void* Y_pre, int64_t M, int64_t N, int64_t K,
                        int32_t flags, float drop_p, uint64_t seed, uint64_t site, void* ws,
@@ -237,6 +245,9 @@ int drt_layernorm_bwd_sum_bf16(const void* dy, const void* x, const float* gamma
 size_t drt_colsum_workspace(int64_t M, int64_t N);
 int drt_colsum_bf16(const void* x, int64_t M, int64_t N, float* out, void* ws, size_t ws_bytes,
                     void* stream);
+/* drt_colsum_f32: the same over an fp32 matrix (partial sums of the fused bias gradients).  */
+int drt_colsum_f32(const float* x, int64_t M, int64_t N, float* out, void* ws, size_t ws_bytes,
+                   void* stream);
 int drt_gelu_bwd_bf16(const void* dy, const void* pre, int64_t n, void* dx, void* stream);
 int drt_transpose_bf16(const void* x, int64_t R, int64_t C, void* y, void* stream);
 /* drt_transpose_bf16_ld: the same into y with row stride ldy >= R (padded GEMM operands). */

@@ -311,6 +311,20 @@ def test_linear_ex_dgelu_vs_fp32(dev, M, N, K):
     scale = ref.abs().max().item()
     assert err_f <= 1.05 * err_u + 1e-3 * scale, (err_f, err_u, scale)
     assert err_f <= 1e-2 * scale
+    # drt_linear_dgelu_bias_bf16: the same dX bit for bit, plus its column sums (the FFN1 bias
+    # gradient) -- from the epilogue on the whole-line plan (M 131072, 4096), after the GEMM
+    # otherwise -- = fp64 column sums of the stored dX to fp32 summation
+    dx2 = torch.empty_like(fused)
+    dbias = torch.empty(N, device=dev)
+    nb = int(lib.drt_linear_dgelu_bias_workspace(M, N, K))
+    ws = torch.empty(max(1, (nb + 3) // 4), dtype=torch.float32, device=dev)
+    _native.check(lib.drt_linear_dgelu_bias_bf16(dy.data_ptr(), wt.data_ptr(), pre.data_ptr(), dx2.data_ptr(), M, N, K,
+                                                 dbias.data_ptr(), ws.data_ptr(), nb, _native.stream_ptr(dev)),
+                  "drt_linear_dgelu_bias_bf16")
+    torch.cuda.synchronize()
+    assert torch.equal(dx2, fused)
+    ref_b = fused.double().sum(0)
+    assert bool(((dbias.double() - ref_b).abs() <= 1e-5 * fused.double().abs().sum(0) + 1e-6).all())
 
 
 @pytest.mark.parametrize("M,N,K,p", [(131072, 768, 3072, 0.1), (16384, 768, 768, 0.1), (300, 768, 64, 0.5)])
