@@ -225,3 +225,95 @@ class RowAnswerMatcher:
                 hit[i] |= m.any(axis=1).astype(np.int8)
         hit[~valid] = 0
         return hit
+
+
+class DeviceRowMatcher:
+    """RowAnswerMatcher with the token matrix resident in HBM: a query batch's k retrieved rows are
+    gathered and compared on the GPU (the host only tokenises the batch's answers), on a stream of
+    its own so the matching of batch j runs beside the search of batch j + 1.  Same result as
+    ``RowAnswerMatcher.match_rows`` (the host matcher also owns the vocabulary and the passage
+    tokenisation); tests/test_answers_gpu.py compares the two on random and golden cases.
+
+    Per batch: toks = tok[rows] -> [B, k, W]; every answer a of query i as token ids padded to the
+    longest answer; a window start s matches answer a iff toks[i, :, s + j] == ids[a][j] for every
+    j < len(a) (and s + len(a) <= W) -- n_max broadcast compares over [B, A, k, W]."""
+
+    def __init__(self, host: "RowAnswerMatcher", device):
+        import torch
+        self.h = host
+        self.device = torch.device(device)
+        self.tok = None
+        self._key = None
+        self.stream = torch.cuda.Stream(self.device)
+
+    def _upload(self, miss: np.ndarray):
+        """Mirror the host token matrix: whole when it was reallocated (growth, rebase), else only
+        the rows ``fill`` just tokenised."""
+        import torch
+        h = self.h
+        key = (id(h.tok), h.tok.shape)
+        with torch.cuda.stream(self.stream):
+            if key != self._key:
+                self.tok = torch.from_numpy(np.ascontiguousarray(h.tok)).to(self.device)
+                self._key = key
+            elif miss.size:
+                mt = torch.from_numpy(miss).to(self.device)
+                self.tok[mt] = torch.from_numpy(np.ascontiguousarray(h.tok[miss])).to(self.device)
+
+    def match_rows(self, rows: np.ndarray, text_of, answers) -> np.ndarray:
+        import torch
+        B, k = rows.shape
+        if B == 0 or k == 0:
+            return np.zeros((B, k), dtype=np.int8)
+        h = self.h
+        flat = np.unique(rows[rows >= 0])
+        miss = flat[~h.seen[flat]] if flat.size and flat.max() < h.n_rows else flat
+        h.fill(rows, text_of)
+        self._upload(miss)
+        W = h.width
+        # the batch's answers as token ids (host): unknown tokens / longer than W never match,
+        # an empty answer matches every passage of its query
+        lists, every = [], np.zeros(B, dtype=bool)
+        for i in range(B):
+            ids_i = []
+            for ans in answers[i]:
+                aw = tokenize_uncased(unicodedata.normalize("NFD", ans))
+                if not aw:
+                    every[i] = True
+                    break
+                ids = [h.vocab.get(w, -2) for w in aw]
+                if min(ids) < 0 or len(ids) > W:
+                    continue
+                ids_i.append(ids)
+            lists.append(ids_i)
+        A = max(1, max(len(x) for x in lists))
+        n_max = max([1] + [len(a) for x in lists for a in x])
+        ans = np.full((B, A, n_max), -3, dtype=np.int32)
+        alen = np.zeros((B, A), dtype=np.int64)
+        for i, x in enumerate(lists):
+            for a, ids in enumerate(x):
+                ans[i, a, : len(ids)] = ids
+                alen[i, a] = len(ids)
+        with torch.cuda.stream(self.stream):
+            dev = self.device
+            r = torch.from_numpy(np.ascontiguousarray(rows)).pin_memory().to(dev, non_blocking=True)
+            at = torch.from_numpy(ans).pin_memory().to(dev, non_blocking=True)
+            lt = torch.from_numpy(alen).pin_memory().to(dev, non_blocking=True)
+            ev = torch.from_numpy(every).pin_memory().to(dev, non_blocking=True)
+            valid = r >= 0
+            toks = self.tok[r.clamp(min=0)]                                    # [B, k, W]
+            m = torch.ones((B, A, k, W), dtype=torch.bool, device=dev)          # window starts s
+            for j in range(n_max):
+                use = (lt > j)[:, :, None, None]                               # answer has token j
+                eq = toks[:, None, :, j:] == at[:, :, j][:, :, None, None]     # [B, A, k, W - j]
+                m[..., : W - j] &= eq | ~use
+                if j:
+                    m[..., W - j:] &= ~use                                     # s + j past the row
+            hit = (m.any(-1) & (lt > 0)[:, :, None]).any(1) | ev[:, None]
+            hit &= valid
+            out = torch.empty((B, k), dtype=torch.int8, pin_memory=True)
+            out.copy_(hit.to(torch.int8), non_blocking=True)
+            done = torch.cuda.Event()
+            done.record(self.stream)
+        done.synchronize()
+        return out.numpy().copy()

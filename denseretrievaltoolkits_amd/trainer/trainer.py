@@ -34,7 +34,7 @@ from torch.nn.parallel import DistributedDataParallel as DDP
 
 from .. import comm
 from ..evaluator.metrics import get_metrics
-from ..evaluator.nq_eval import AnswerMatcher, RowAnswerMatcher, has_answers
+from ..evaluator.nq_eval import AnswerMatcher, DeviceRowMatcher, RowAnswerMatcher, has_answers
 from ..search import ShardedFlatIP, _stage_host
 from .losses import get_loss_function
 from .scheduler import ConstantScheduler, CosineScheduler, InverseSquareRootScheduler, LinearScheduler
@@ -354,6 +354,8 @@ class Trainer:
         if matcher is None:
             matcher = RowAnswerMatcher(len(self.idx))
         matcher.ensure_rows(len(self.idx))
+        if self.device.type == "cuda":   # the token matrix in HBM: rows gathered / compared on the GPU
+            matcher = DeviceRowMatcher(matcher, self.device)
 
         def text_of(row):
             return self._doc_text(self.idx[row])

@@ -1,0 +1,47 @@
+"""GPU: DeviceRowMatcher (Trainer.evaluate's answer matching with the token matrix in HBM) equals
+the host RowAnswerMatcher -- itself pinned to the reference's has_answers (tests/test_answers_cpu.py)
+-- on random cases (pads, unknown tokens, empty answers, multi-token answers, growing widths)
+and on the reference-generated golden cases."""
+import json
+import os
+
+import numpy as np
+import pytest
+
+from conftest import REPO
+
+pytestmark = pytest.mark.gpu
+
+
+def test_device_matcher_equals_host_random(dev):
+    from denseretrievaltoolkits_amd.evaluator.nq_eval import DeviceRowMatcher, RowAnswerMatcher, has_answers
+    rng = np.random.default_rng(7)
+    vocab = ["a", "b", "c", "d", "A", "b.", "c-d", "e", "É", "naïve", "⁂", "日本"]
+    docs = [" ".join(rng.choice(vocab, size=int(rng.integers(0, 40)))) for _ in range(500)]
+    host = RowAnswerMatcher(0)
+    host.ensure_rows(500)
+    dm = DeviceRowMatcher(host, dev)
+    ref_m = RowAnswerMatcher(0)
+    ref_m.ensure_rows(500)
+    for it in range(40):
+        B, k = int(rng.integers(1, 9)), int(rng.integers(1, 60))
+        rows = rng.integers(-1, 500, size=(B, k))
+        ans = [[" ".join(rng.choice(vocab + ["zzz"], size=int(rng.integers(0, 5))))
+                for _ in range(int(rng.integers(1, 4)))] for _ in range(B)]
+        got = dm.match_rows(rows, lambda r: docs[r], ans)
+        want = ref_m.match_rows(rows, lambda r: docs[r], ans)
+        assert got.dtype == np.int8 and np.array_equal(got, want), it
+        if it % 10 == 0:
+            ref = [[int(has_answers(docs[r], ans[i])) if r >= 0 else 0 for r in rows[i]] for i in range(B)]
+            assert got.tolist() == ref
+
+
+def test_device_matcher_reference_golden(dev):
+    from denseretrievaltoolkits_amd.evaluator.nq_eval import DeviceRowMatcher, RowAnswerMatcher
+    with open(os.path.join(REPO, "tests", "golden", "answers.json"), encoding="utf-8") as f:
+        g = json.load(f)
+    dm = DeviceRowMatcher(RowAnswerMatcher(len(g["docs"])), dev)
+    for c in g["cases"]:
+        rows = np.array([c["docs"] + [-1, -1]], dtype=np.int64)
+        got = dm.match_rows(rows, lambda r: g["docs"][r], [c["answers"]])
+        assert got[0].tolist() == c["has"] + [0, 0], c
