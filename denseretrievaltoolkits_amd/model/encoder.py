@@ -79,7 +79,9 @@ class HipBertEncoder:
         self._graph_cache = {}
         self.split_streams = True       # two halves on two streams from split_min_tokens up
         self.fuse_ln = True             # dense + residual + LayerNorm in one call (_lin_ln)
-        self.split_min_tokens = 65536
+        # from 8192 tokens: 256 x 32-token queries 2.47 -> 2.06 ms, 512 x 32 3.81 -> 3.74 (4096 tokens:
+        # slower, 1.36 -> 1.50; tools/qenc_split_ab.py, profiles/r03zc_qenc_split_ab.log)
+        self.split_min_tokens = 8192
         self._streams = None
         self._ws_plan = {}
         self._ws = None
