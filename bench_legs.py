@@ -55,6 +55,21 @@ def run(device, batch=512, L=128, steps=10, warmup=2):
     # two-stream split (HipBertEncoder.split_streams) they overlap the other half's kernels
     split = enc.split_streams and batch >= 2 and batch * L >= enc.split_min_tokens
     gemm_tf = gemm_flops / (tot.value * 1e-3) / 1e12 if tot.value > 0 and not split else None
+    # like-for-like library baseline on the same GPU: the HF module in bf16 (hipBLASLt GEMMs, sdpa
+    # attention) under torch, same batch and [CLS] pooling
+    del enc
+    torch.manual_seed(0)
+    tm = BertModel(BertConfig(), add_pooling_layer=False).eval().to(device=device, dtype=torch.bfloat16)
+    with torch.no_grad():
+        for _ in range(warmup):
+            tm(input_ids=ids, attention_mask=mask).last_hidden_state[:, 0].float()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(steps):
+            tm(input_ids=ids, attention_mask=mask).last_hidden_state[:, 0].float()
+        torch.cuda.synchronize()
+    torch_pps = steps * batch / (time.perf_counter() - t0)
+    del tm
     return {
         "metric": "passages encoded/sec (bf16 BERT-base, 128-token passages)",
         "value": round(pps, 1),
@@ -71,6 +86,9 @@ def run(device, batch=512, L=128, steps=10, warmup=2):
             "gemm_only_tflops": round(gemm_tf, 1) if gemm_tf else None,
             "streams": 2 if split else 1,
         },
+        "torch_bf16": {"value": round(torch_pps, 1), "unit": "passages/s",
+                       "what": "HF BertModel in bf16 under torch (hipBLASLt + sdpa), same GPU and batch",
+                       "speedup": round(pps / torch_pps, 2)},
     }
 
 
