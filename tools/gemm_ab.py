@@ -37,14 +37,26 @@ def main(M=65536, rounds=5, reps=10):
             _native.check(call(v), f"{name} v{v}")
         torch.cuda.synchronize()
         times = {v: [] for v in variants}
-        times["torch"] = []
+        tv = ["torch", "torch_bias"] + (["torch_resid_c"] if r is not None else [])
+        for t in tv:
+            times[t] = []
         for _ in range(rounds):
-            for v in list(variants) + ["torch"]:
+            for v in list(variants) + tv:
                 e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
                 if v == "torch":
                     e0.record()
                     for _ in range(reps):
                         y = x @ w.T
+                    e1.record()
+                elif v == "torch_bias":   # hipBLASLt with its bias epilogue
+                    e0.record()
+                    for _ in range(reps):
+                        y = torch.nn.functional.linear(x, w, b.to(torch.bfloat16))
+                    e1.record()
+                elif v == "torch_resid_c":   # hipBLASLt with the residual as C (beta = 1)
+                    e0.record()
+                    for _ in range(reps):
+                        y = torch.addmm(r, x, w.T)
                     e1.record()
                 else:
                     e0.record()
