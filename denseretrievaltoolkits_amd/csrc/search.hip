@@ -199,7 +199,8 @@ __device__ __forceinline__ void issue_tile16(const ScanArgs& a, uint32_t buf_lds
 #pragma unroll
   for (int j = 0; j < C::GLDS_PER_WAVE; ++j) {
     int J = j * NW + wave;                   // wave-instruction index in the tile
-    if (C::GLDS_PER_TILE % NW != 0 && J >= C::GLDS_PER_TILE) J -= C::GLDS_PER_TILE;
+    // (modulo, not one subtraction: at d = 64 a tile is 2 instructions for 8 waves)
+    if (C::GLDS_PER_TILE % NW != 0) J %= C::GLDS_PER_TILE;
     const int g = J >> 1;                    // chunk group (2 instructions each)
     const int row = ((J & 1) << 3) + rsub;   // 0..15
     int64_t li = tile * kT16 + row;

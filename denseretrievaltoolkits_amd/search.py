@@ -165,14 +165,20 @@ def _gtau_finish_group(pend, redo):
 
 
 class FlatIPIndex:
-    """Exact IP index over bf16 rows resident on one GPU (IndexFlatIP semantics)."""
+    """Exact IP index over bf16 rows resident on one GPU (IndexFlatIP semantics).
+
+    Any d <= 1024 (the scan keeps a query block's d values on chip; faiss's GPU flat index has the
+    same kind of bound on k, none on d): rows and queries of a d that is not a multiple of 64 are
+    stored zero-padded to the next multiple (``dp``), which leaves every inner product exactly
+    unchanged.  ``rows`` is the padded [ntotal, dp] view the kernels scan."""
 
     def __init__(self, d: int, device=None, capacity: int = 0):
-        if d <= 0 or d % 64 or d > 1024:
-            raise ValueError(f"dimension {d} unsupported: the HIP scan needs d % 64 == 0 and d <= 1024")
+        if d <= 0 or d > 1024:
+            raise ValueError(f"dimension {d} unsupported: the HIP scan needs 0 < d <= 1024")
         self.d = int(d)
+        self.dp = (self.d + 63) // 64 * 64
         self.device = torch.device(device) if device is not None else torch.device("cuda", torch.cuda.current_device())
-        self._buf = torch.empty((max(0, capacity), self.d), dtype=torch.bfloat16, device=self.device)
+        self._buf = torch.zeros((max(0, capacity), self.dp), dtype=torch.bfloat16, device=self.device)
         self.ntotal = 0
         self.metric = "inner_product"
 
@@ -186,7 +192,7 @@ class FlatIPIndex:
 
     def reserve(self, n: int):
         if n > self._buf.shape[0]:
-            nb = torch.empty((n, self.d), dtype=torch.bfloat16, device=self.device)
+            nb = torch.zeros((n, self.dp), dtype=torch.bfloat16, device=self.device)
             if self.ntotal:
                 nb[: self.ntotal] = self._buf[: self.ntotal]
             self._buf = nb
@@ -198,7 +204,9 @@ class FlatIPIndex:
         n = x.shape[0]
         if self.ntotal + n > self._buf.shape[0]:
             self.reserve(max(self.ntotal + n, int(self._buf.shape[0] * 1.5) + 1))
-        self._buf[self.ntotal: self.ntotal + n] = x
+        self._buf[self.ntotal: self.ntotal + n, : self.d] = x
+        if self.dp != self.d:   # (the buffer may hold rows of an earlier, reset() index)
+            self._buf[self.ntotal: self.ntotal + n, self.d:] = 0
         self.ntotal += n
 
     @property
@@ -211,7 +219,7 @@ class FlatIPIndex:
         if rows.dtype != torch.bfloat16 or rows.dim() != 2 or not rows.is_cuda:
             raise ValueError("from_rows expects a [n, d] bf16 device tensor")
         idx = cls(rows.shape[1], device=rows.device, capacity=0)
-        idx._buf = rows.contiguous()
+        idx._buf = idx._pad(rows).contiguous()
         idx.ntotal = rows.shape[0]
         return idx
 
@@ -283,11 +291,14 @@ class FlatIPIndex:
         return s.cpu().numpy(), i.cpu().numpy()
 
     # global-threshold protocol steps (ShardedFlatIP) ---------------------
+    def _pad(self, x: torch.Tensor) -> torch.Tensor:
+        return x if self.dp == self.d else torch.nn.functional.pad(x, (0, self.dp - self.d))
+
     def _queries(self, q):
         qd = _as_device_bf16(q, self.device)
-        if qd.dim() != 2 or qd.shape[1] != self.d:
+        if qd.dim() != 2 or qd.shape[1] not in (self.d, self.dp):
             raise ValueError(f"search: expected [nq, {self.d}] queries, got {tuple(qd.shape)}")
-        return qd
+        return self._pad(qd) if qd.shape[1] == self.d else qd
 
     def dist_sample(self, q, n_global: int, k: int) -> torch.Tensor:
         return kernels.dist_sample(self._queries(q), self.rows, n_global, k)
@@ -304,7 +315,7 @@ class FlatIPIndex:
     # persistence (replaces faiss.write_index / read_index, trainer.py:245,257): a
     # memory-mapped bf16 shard file streamed chunk by chunk (shards.py)
     def save(self, path: str) -> None:
-        shards.save_rows(self.rows, path)
+        shards.save_rows(self.rows if self.dp == self.d else self.rows[:, : self.d].contiguous(), path)
 
     @classmethod
     def load(cls, path: str, device=None) -> "FlatIPIndex":
@@ -317,7 +328,7 @@ class FlatIPIndex:
         start = 0 if start is None else int(start)
         stop = sum(sizes) if stop is None else int(stop)
         idx = cls(d, device=device, capacity=0)
-        idx._buf = shards.load_rows(paths, start, stop, idx.device)
+        idx._buf = idx._pad(shards.load_rows(paths, start, stop, idx.device))
         idx.ntotal = stop - start
         return idx
 

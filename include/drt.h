@@ -49,7 +49,7 @@ const char* drt_version(void);
  * Brute-force inner-product top-k over one row shard  (index.py:16-33)
  * ------------------------------------------------------------------------
  * Q: [nq, d] bf16 queries.  P: [n, d] bf16 corpus shard (row i has global id
- * id_offset + i).  d must be a multiple of 64 and <= 1024; 1 <= k <= 2048.
+ * id_offset + i).  d must be a multiple of 64 and <= 1024 (FlatIPIndex zero-pads any other d <= 1024); 1 <= k <= 2048.
  * Writes out_scores [nq, k] fp32 and out_ids [nq, k] int64, and status [nq]
  * int32: 0 = exact result, 1 = the fast threshold path could not certify the
  * query and drt_ip_topk_resolve must be called for it (probability ~1e-9 per

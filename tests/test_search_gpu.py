@@ -37,6 +37,10 @@ def _run(dev, q, p, k, id_offset=0, resolve=True):
     (64, 70000, 1024, 1000),   # 2-slot LDS ring (d = 1024)
     (40, 30000, 832, 2048),    # k at its maximum, 2-slot ring
     (7, 40000, 384, 1),        # k = 1
+    (37, 20011, 64, 50),       # d = 64: a tile is 2 LDS-DMA instructions for 8 waves
+    (16, 100000, 64, 1000),
+    (9, 50000, 192, 100),      # 6 instructions per tile, 8 waves
+    (5, 30000, 320, 20),       # 10 per tile: 2 per wave, 6 duplicates
 ])
 def test_ip_topk_integer_bit_exact(dev, nq, n, d, k):
     rng = np.random.default_rng(1000 + nq + n + d + k)
@@ -55,6 +59,8 @@ def test_ip_topk_integer_bit_exact(dev, nq, n, d, k):
     (1, 200003, 768, 1000),    # ragged tail tile
     (64, 70000, 1024, 1000),   # 4-slot ring at d = 1024
     (16, 4_000_003, 768, 1000),  # sparse hits: the per-hit append + aggregated flush flavour
+    (128, 50000, 64, 1000),    # d = 64
+    (16, 4_000_003, 64, 1000),   # d = 64, sparse flavour
 ])
 def test_filter_scan_flavours_bit_exact(dev, nq, n, d, k):
     """The production filter scan picks its hit-append flavour by the expected hit density
@@ -280,6 +286,48 @@ def test_shard_file_roundtrip_through_hbm(dev, tmp_path):
     s1, i1 = back.search(q, 100)
     es, ei = orc.ip_topk(q, p, 100)
     assert np.array_equal(i1, ei) and np.array_equal(s1, es) and np.array_equal(i0, i1)
+
+
+@pytest.mark.parametrize("d", [100, 8, 1000])
+def test_flat_index_any_dimension_bit_exact(dev, d, tmp_path):
+    """d not a multiple of 64 (faiss IndexFlatIP takes any d): rows and queries zero-padded to the
+    next multiple of 64 inside FlatIPIndex -- ids and scores bit-exact vs the oracle on the
+    unpadded data, through search, search_batches (grouped path included), the retriever's
+    batch_search and a shard-file round trip (which stores the unpadded d columns)."""
+    import torch
+    from denseretrievaltoolkits_amd import search as S
+    from denseretrievaltoolkits_amd.evaluator.index import BaseFaissIPRetriever
+    from denseretrievaltoolkits_amd.search import FlatIPIndex
+    rng = np.random.default_rng(d)
+    p = int_bf16(rng, (20011, d), -3, 3)
+    q = int_bf16(rng, (37, d), -3, 3)
+    es, ei = orc.ip_topk(q, p, 50)
+    idx = FlatIPIndex(d, device=dev)
+    idx.add(p[:7000])
+    idx.add(p[7000:])
+    assert idx.rows.shape == (20011, (d + 63) // 64 * 64)
+    s, i = idx.search(q, 50)
+    assert np.array_equal(i, ei) and np.array_equal(s, es)
+    old = S.GROUP_MIN_ROWS
+    try:
+        for gmin in (old, 1):   # per-batch pipeline and the grouped global-threshold path
+            S.GROUP_MIN_ROWS = gmin
+            res = idx.search_batches([torch.from_numpy(q[a: a + 10]).to(dev) for a in range(0, 37, 10)], 50)
+            assert np.array_equal(torch.cat([r[1] for r in res]).cpu().numpy(), ei)
+            assert np.array_equal(torch.cat([r[0] for r in res]).cpu().numpy(), es)
+    finally:
+        S.GROUP_MIN_ROWS = old
+    ret = BaseFaissIPRetriever(p[:1], device=dev)
+    ret.add(p)
+    assert np.array_equal(ret.batch_search(q, 50, 16), ei)
+    path = str(tmp_path / "0.0.bf16.npy")
+    idx.save(path)
+    back = FlatIPIndex.load(path, device=dev)
+    assert back.d == d and torch.equal(back.rows.view(torch.int16), idx.rows.view(torch.int16))
+    s2, i2 = back.search(q, 50)
+    assert np.array_equal(i2, ei) and np.array_equal(s2, es)
+    with pytest.raises(ValueError):
+        FlatIPIndex(1025, device=dev)
 
 
 def test_hip_topk_matches_reference_corpus_golden(dev):
