@@ -210,6 +210,62 @@ def test_split_k_linear_vs_unsplit_and_torch(dev, M, N, K, flags, resid):
     torch.testing.assert_close(o0.float(), ref, **tol)
 
 
+@pytest.mark.parametrize("M,N,K,flags,resid", [(256, 2304, 768, 0, False), (8, 768, 3072, 0, True),
+                                               (256, 3072, 768, 1, False), (200, 98, 1024, 2, True)])
+def test_split_k_scratch_contents_and_graph_replay(dev, M, N, K, flags, resid):
+    """The split-K plan (fp32 partials in the caller's scratch, fixed-order reduction) is a pure
+    function of its inputs: whatever the scratch held (random bits, all ones), repeated launches
+    and a hipGraph replayed several times give the same bits as the first eager launch, and that
+    matches torch fp32."""
+    import torch
+    from denseretrievaltoolkits_amd import _native
+    lib = _native.load()
+    nb = int(lib.drt_linear_workspace(M, N, K))
+    assert nb > 0
+    g = torch.Generator(device=dev).manual_seed(M * 3 + N + K)
+    x = torch.randn(M, K, generator=g, device=dev).to(torch.bfloat16)
+    w = (0.05 * torch.randn(N, K, generator=g, device=dev)).to(torch.bfloat16)
+    b = torch.randn(N, generator=g, device=dev)
+    r = torch.randn(M, N, generator=g, device=dev).to(torch.bfloat16) if resid else None
+    rp = r.data_ptr() if r is not None else None
+    dt = torch.float32 if flags & 2 else torch.bfloat16
+    ws = torch.randint(-2 ** 31, 2 ** 31 - 1, ((nb + 3) // 4,), dtype=torch.int32, device=dev, generator=g)
+
+    def run(out, stream=None):
+        s = _native.stream_ptr(dev) if stream is None else stream.cuda_stream
+        _native.check(lib.drt_linear_bf16_ws(x.data_ptr(), w.data_ptr(), b.data_ptr(), rp, out.data_ptr(), M, N, K,
+                                             flags, ws.data_ptr(), nb, s), "split")
+
+    first = torch.empty(M, N, dtype=dt, device=dev)
+    run(first)
+    for fill in (None, -1):
+        if fill is not None:
+            ws.fill_(fill)
+        o = torch.empty(M, N, dtype=dt, device=dev)
+        for _ in range(3):
+            o.zero_()
+            run(o)
+            torch.cuda.synchronize()
+            assert torch.equal(o, first)
+    og = torch.zeros(M, N, dtype=dt, device=dev)
+    side = torch.cuda.Stream(dev)
+    graph = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(graph, stream=side):
+        run(og, side)
+    for _ in range(3):
+        og.zero_()
+        graph.replay()
+        torch.cuda.synchronize()
+        assert torch.equal(og, first)
+    ref = x.float() @ w.float().T + b
+    if flags & 1:
+        ref = torch.nn.functional.gelu(ref)
+    if r is not None:
+        ref = ref + r.float()
+    tol = dict(atol=2e-3, rtol=1e-4) if dt == torch.float32 else dict(atol=3e-2, rtol=1e-2)
+    torch.testing.assert_close(first.float(), ref, **tol)
+
+
 def test_gemm_gelu_epilogue_value_sweep(dev):
     """The 256^2 kernel's GELU epilogue (packed, one exp per element) on exact pre-activations:
     X rows are unit vectors, so every output is exactly W[n, m % 64] + bias; 16384 distinct values in
