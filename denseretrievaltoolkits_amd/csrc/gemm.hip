@@ -158,7 +158,10 @@ __device__ __forceinline__ float epi_post(const GemmArgs& a, float v, int64_t ro
 // 256^2 kernel from this many 256^2 tiles up (tools/qsweep.py: 128 beats 512 by 16-22 % on 4k-16k-token
 // batches); tile order inside an XCD's range: grouped-8 for K <= 1024 (small panels), row-major otherwise
 // (profiles/r02o_gemm_tile_order.log: orders within noise).
-constexpr int64_t kLargeMinTiles = 128;
+#ifndef DRT_LARGE_MIN_TILES
+#define DRT_LARGE_MIN_TILES 128
+#endif
+constexpr int64_t kLargeMinTiles = DRT_LARGE_MIN_TILES;
 __host__ __device__ constexpr int auto_tile_order(int64_t k) { return k <= 1024 ? 1 : 0; }
 
 // NS = LDS stages of 32 KiB (A + B K-tile): 2 = double buffer, 2 work-groups per CU (grids of
