@@ -1344,6 +1344,156 @@ __global__ __launch_bounds__(kKthThreads) void kth_final_kernel(const uint32_t* 
     for (int i = threadIdx.x; i < r; i += kKthThreads) best[q * r + i] = buf[i];
 }
 
+// Sample threshold in ONE launch (one-GPU search, samples up to kRankThreads * kRankPer keys --
+// 70,801 at 10M rows and k = 1000): one 1024-thread work-group per query holds the whole sample
+// row in registers, a 1024-bin histogram linear in the score finds the bin holding rank r, the
+// keys of the bins up to it (~r + that bin) are sorted in LDS and tau = the r-th best -- the same
+// key kth_partial + kth_final pick (both exact), without the 2,304-work-group chunk pass, its
+// survivor lists and the second launch.  More than kRankBuf candidates (ties / a degenerate score
+// range) fall back to an exact MSD radix select over the candidates.  Also zeroes the hit counter.
+constexpr int kRankThreads = 1024;
+constexpr int kRankPer = 80;
+constexpr int kRankBins = 1024;
+constexpr int kRankBuf = 2048;
+constexpr int64_t kRankMaxKeys = (int64_t)kRankThreads * kRankPer;
+
+__global__ __launch_bounds__(kRankThreads) void kth_rank_kernel(const uint32_t* in, int64_t stride, int64_t n, int r,
+                                                                float* tau, uint32_t* zero) {
+  __shared__ uint32_t hist[kRankBins];
+  __shared__ __attribute__((aligned(16))) uint32_t buf[kRankBuf];
+  __shared__ float red[2][kRankThreads / 64];
+  __shared__ uint32_t wsum[kRankThreads / 64];
+  __shared__ uint32_t sh_n, sh_rem, sh_prefix;
+  __shared__ int sh_bin;
+  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+  const int64_t q = blockIdx.x;
+  if (zero && tid == 0) zero[q * kCntStride] = 0;
+  const uint32_t* src = in + q * stride;
+  constexpr uint32_t kPad = 0xFFFFFFFFu;
+  // thread t holds keys j * 4096 + 4t + [0, 4), j < kRankPer / 4 (coalesced 16-B loads; stride % 4 == 0)
+  uint32_t key[kRankPer];
+#pragma unroll
+  for (int j = 0; j < kRankPer / 4; ++j) {
+    const int64_t base = (int64_t)j * (4 * kRankThreads) + 4 * tid;
+    if (base + 3 < n) {
+      const u32x4 x = *(const u32x4*)(src + base);
+#pragma unroll
+      for (int u = 0; u < 4; ++u) key[4 * j + u] = x[u];
+    } else {
+#pragma unroll
+      for (int u = 0; u < 4; ++u) key[4 * j + u] = base + u < n ? src[base + u] : kPad;
+    }
+  }
+  float hi = -__builtin_inff(), lo = __builtin_inff();
+#pragma unroll
+  for (int e = 0; e < kRankPer; ++e) {
+    if (key[e] != kPad) {
+      const float sc = desc_key_to_score(key[e]);
+      hi = fmaxf(hi, sc);
+      lo = fminf(lo, sc);
+    }
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    hi = fmaxf(hi, __shfl_xor(hi, o, 64));
+    lo = fminf(lo, __shfl_xor(lo, o, 64));
+  }
+  if (lane == 0) {
+    red[0][wave] = hi;
+    red[1][wave] = lo;
+  }
+  hist[tid] = 0;
+  __syncthreads();
+#pragma unroll
+  for (int w = 0; w < kRankThreads / 64; ++w) {
+    hi = fmaxf(hi, red[0][w]);
+    lo = fminf(lo, red[1][w]);
+  }
+  const float range = hi - lo;
+  const float scale = (range > 0.0f && range < __builtin_inff()) ? (float)kRankBins / range : 0.0f;
+  // bin 0 = best scores; monotone in the key, so the keys of bins <= b are the smallest keys
+  auto bin_of = [&](uint32_t kk) {
+    const float f = (hi - desc_key_to_score(kk)) * scale;
+    int bb = (int)f;
+    return bb < 0 ? 0 : (bb > kRankBins - 1 ? kRankBins - 1 : bb);
+  };
+#pragma unroll
+  for (int e = 0; e < kRankPer; ++e)
+    if (key[e] != kPad) atomicAdd(&hist[bin_of(key[e])], 1u);
+  __syncthreads();
+  {
+    const uint32_t v = hist[tid];
+    uint32_t incl = v;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const uint32_t t = __shfl_up(incl, o, 64);
+      if (lane >= o) incl += t;
+    }
+    if (lane == 63) wsum[wave] = incl;
+    if (tid == 0) sh_n = 0;
+    __syncthreads();
+    uint32_t off = 0;
+    for (int w = 0; w < wave; ++w) off += wsum[w];
+    incl += off;
+    const uint32_t excl = incl - v;
+    if (excl < (uint32_t)r && (uint32_t)r <= incl) sh_bin = tid;
+    if (tid == kRankThreads - 1 && incl < (uint32_t)r) sh_bin = kRankBins - 1;   // fewer than r real keys
+  }
+  __syncthreads();
+  const int b = sh_bin;
+#pragma unroll
+  for (int e = 0; e < kRankPer; ++e) {
+    if (key[e] != kPad && bin_of(key[e]) <= b) {
+      const uint32_t pos = atomicAdd(&sh_n, 1u);
+      if (pos < (uint32_t)kRankBuf) buf[pos] = key[e];
+    }
+  }
+  __syncthreads();
+  const int nsel = (int)sh_n;
+  uint32_t kth;
+  if (nsel <= kRankBuf) {
+    int n2 = 1;
+    while (n2 < nsel) n2 <<= 1;
+    for (int i = nsel + tid; i < n2; i += kRankThreads) buf[i] = kPad;
+    __syncthreads();
+    block_sort<uint32_t, kRankThreads>(buf, n2);
+    kth = r <= nsel ? buf[r - 1] : kPad;
+  } else {
+    // exact MSD radix select (8 bits per pass) of the r-th smallest candidate key
+    if (tid == 0) {
+      sh_rem = (uint32_t)r;
+      sh_prefix = 0;
+    }
+    uint32_t mask = 0;
+    for (int shift = 24; shift >= 0; shift -= 8) {
+      if (tid < 256) hist[tid] = 0;
+      __syncthreads();
+      const uint32_t prefix = sh_prefix;
+#pragma unroll
+      for (int e = 0; e < kRankPer; ++e)
+        if (key[e] != kPad && bin_of(key[e]) <= b && (key[e] & mask) == prefix)
+          atomicAdd(&hist[(key[e] >> shift) & 255u], 1u);
+      __syncthreads();
+      if (tid == 0) {
+        uint32_t rem = sh_rem, dgt = 255;
+        for (uint32_t dd = 0; dd < 256; ++dd) {
+          if (hist[dd] >= rem) {
+            dgt = dd;
+            break;
+          }
+          rem -= hist[dd];
+        }
+        sh_rem = rem;
+        sh_prefix = prefix | (dgt << shift);
+      }
+      mask |= 255u << shift;
+      __syncthreads();
+    }
+    kth = sh_prefix;
+  }
+  if (tau && tid == 0) tau[q] = (kth == kPad) ? -__builtin_inff() : desc_key_to_score(kth);
+}
+
 // Tree merge of packed per-shard lists by bitonic networks: all P2 =
 // pow2ceil(nparts) lists, padded to KP = pow2ceil(k) keys, sit in LDS.  Each
 // round merges list pairs (A, B): the half-cleaner min(A[i], B[KP-1-i]) keeps
@@ -2055,12 +2205,17 @@ int drt_ip_topk_bf16(const void* Q, int64_t nq, const void* P, int64_t n, int32_
   if (rc) return rc;
   {
     const ProfPair pp = prof_begin(PROF_SELECT, s);
-    hipLaunchKernelGGL(kth_partial_kernel, dim3((unsigned)p.nchunk, (unsigned)nq), dim3(kKthThreads), 0, s,
-                       (const uint32_t*)(w + p.off_sample), (int64_t)align_up(p.m, 4), p.m, (int)p.r,
-                       (uint32_t*)(w + p.off_part));
-    hipLaunchKernelGGL(kth_final_kernel, dim3((unsigned)nq), dim3(kKthThreads), 0, s,
-                       (const uint32_t*)(w + p.off_part), (int)p.nchunk, (int)p.r, (int64_t)p.r,
-                       (int64_t)(p.nchunk * p.r), tau, (uint32_t*)nullptr, cnt);   // also zeroes the hit counters
+    if (p.m <= kRankMaxKeys && p.r <= kRankBuf) {   // one launch: the whole sample row per work-group
+      hipLaunchKernelGGL(kth_rank_kernel, dim3((unsigned)nq), dim3(kRankThreads), 0, s,
+                         (const uint32_t*)(w + p.off_sample), (int64_t)align_up(p.m, 4), p.m, (int)p.r, tau, cnt);
+    } else {
+      hipLaunchKernelGGL(kth_partial_kernel, dim3((unsigned)p.nchunk, (unsigned)nq), dim3(kKthThreads), 0, s,
+                         (const uint32_t*)(w + p.off_sample), (int64_t)align_up(p.m, 4), p.m, (int)p.r,
+                         (uint32_t*)(w + p.off_part));
+      hipLaunchKernelGGL(kth_final_kernel, dim3((unsigned)nq), dim3(kKthThreads), 0, s,
+                         (const uint32_t*)(w + p.off_part), (int)p.nchunk, (int)p.r, (int64_t)p.r,
+                         (int64_t)(p.nchunk * p.r), tau, (uint32_t*)nullptr, cnt);   // also zeroes the hit counters
+    }
     prof_end(pp, s);
     DRT_CHECK_HIP(hipGetLastError());
   }

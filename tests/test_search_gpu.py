@@ -157,6 +157,43 @@ def test_ties_all_rows_identical(dev):
     assert (st == 0).all()  # resolved
 
 
+@pytest.mark.parametrize("n,d,nq,ties", [(200_003, 128, 7, False), (2_400_000, 64, 5, False),
+                                         (10_000_000, 64, 3, False), (2_400_000, 64, 2, True)])
+def test_sample_threshold_is_rth_best_sampled_score(dev, n, d, nq, ties):
+    """White-box: the sample threshold tau_q (the first nq floats of the drt_ip_topk_bf16 workspace)
+    is exactly the r-th best score among the plan's sampled rows -- at 10M rows (70,801 sampled keys,
+    the one-launch kth_rank_kernel near its register capacity), smaller samples, and a row of all-equal
+    scores (every sampled key a candidate: the exact radix-select fallback).  A wrong tau would still
+    give exact results through the rescan, only slower, so the other tests cannot see it."""
+    import torch
+    from denseretrievaltoolkits_amd import _native
+    lib = _native.load()
+    k = 1000
+    plan = sample_plan(n, k)
+    assert plan is not None
+    rng = np.random.default_rng(n + nq)
+    q = int_bf16(rng, (nq, d))
+    if ties:
+        p = torch.ones((n, d), dtype=torch.bfloat16, device=dev)
+    else:
+        p = device_int_corpus(n, d, -8, 8, seed=n, device=dev)
+    qt = to_dev_bf16(q, dev)
+    nb = int(lib.drt_ip_topk_workspace(nq, n, d, k))
+    ws = torch.empty((nb + 3) // 4, dtype=torch.float32, device=dev)
+    s = torch.empty((nq, k), dtype=torch.float32, device=dev)
+    i = torch.empty((nq, k), dtype=torch.int64, device=dev)
+    st = torch.empty((nq,), dtype=torch.int32, device=dev)
+    _native.check(lib.drt_ip_topk_bf16(qt.data_ptr(), nq, p.data_ptr(), n, d, k, 0, s.data_ptr(), i.data_ptr(),
+                                       st.data_ptr(), ws.data_ptr(), nb, _native.stream_ptr(dev)), "ip_topk")
+    torch.cuda.synchronize()
+    tau = ws[:nq].cpu().numpy()
+    rows = torch.from_numpy(plan["rows"]).to(dev)
+    sampled = p[rows].double().cpu().numpy() @ q.astype(np.float64).T          # [m, nq], exact integers
+    want = -np.sort(-sampled, axis=0)[plan["r"] - 1]
+    np.testing.assert_array_equal(tau, want.astype(np.float32))
+    assert (st.cpu().numpy() == 0).all() or ties   # all-equal rows overflow the filter (resolved elsewhere)
+
+
 def test_resolve_when_sample_threshold_too_high(dev):
     """Sampled rows are the only strong matches -> fast path under-collects; resolve must be exact."""
     import torch
