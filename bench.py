@@ -19,8 +19,11 @@ per-shard top-k (u64 score-key|id) and a device merge that certifies
 exactness; an uncertified batch is redone with the per-shard exact path
 inside the timed region.  The corpus is fixed as N grows ("scaling": "strong").
 
-Launch: python bench.py [--gpus N --steps K --warmup W]; for N > 1 under
-torch.distributed.run (one process per GPU, RCCL).
+Launch: python bench.py [--gpus N --steps K --warmup W].  For N > 1 either
+under torch.distributed.run (WORLD_SIZE must then equal N) or directly: with
+WORLD_SIZE unset, `python bench.py --gpus N` starts the N ranks itself (one
+process per GPU, RCCL over xGMI) through a torch.distributed.run child launched
+BEFORE anything touches the GPU, and exits with its status (launch()).
 """
 from __future__ import annotations
 
@@ -56,7 +59,61 @@ def parse():
                          "search.GROUP_QUERIES)")
     ap.add_argument("--protocol", choices=["global_tau", "per_shard"], default="global_tau",
                     help="N > 1 exchange protocol (per_shard = exact top-k per shard + merge)")
+    ap.add_argument("--launch-check", action="store_true",
+                    help="start the ranks, join the process group, report n_gpus and exit without touching "
+                         "the GPU (tests/test_bench_launch_cpu.py)")
     return ap.parse_args()
+
+
+def _free_port():
+    import socket
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def launch(args):
+    """Start one rank per GPU when asked for N > 1 GPUs outside a launcher.
+
+    Returns when this process IS a rank (WORLD_SIZE set by torch.distributed.run, the driver's form
+    for N > 1) or N = 1; otherwise runs `python -m torch.distributed.run --nproc-per-node N bench.py
+    ...` as a child and exits with its status.  This process has not initialised the GPU (no HIP
+    call has been made yet), and the ranks are a child process, not an exec."""
+    ws = os.environ.get("WORLD_SIZE")
+    if ws is not None:
+        if int(ws) != args.gpus:
+            sys.stderr.write(f"bench.py: WORLD_SIZE={ws} but --gpus {args.gpus}; launch one rank per GPU\n")
+            sys.exit(2)
+        return
+    if args.gpus <= 1:
+        return
+    import subprocess
+    env = dict(os.environ)
+    env.setdefault("MASTER_ADDR", "127.0.0.1")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={args.gpus}",
+           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()),
+           os.path.abspath(__file__)] + sys.argv[1:]
+    rc = subprocess.call(cmd, env=env)
+    sys.exit(rc)
+
+
+def launch_check(args):
+    """--launch-check: every rank joins the process group (gloo, no GPU) and rank 0 reports how many
+    ranks the launch produced."""
+    import torch
+    import torch.distributed as dist
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    seen = world
+    if world > 1:
+        dist.init_process_group("gloo")
+        t = torch.ones(1)
+        dist.all_reduce(t)
+        seen = int(t.item())
+        dist.destroy_process_group()
+    if rank == 0:
+        print(json.dumps({"launch_check": True, "n_gpus": world, "ranks_joined": seen,
+                          "backend": os.environ.get("DRT_BENCH_BACKEND", "nccl")}), flush=True)
 
 
 def init_dist(n_gpus):
@@ -232,6 +289,10 @@ def encode_leg(args, device):
 
 def main():
     args = parse()
+    launch(args)
+    if args.launch_check:
+        launch_check(args)
+        return
     import torch
     import torch.distributed as dist
     rank, world, local = init_dist(args.gpus)

@@ -26,6 +26,24 @@ def world_rank(group=None):
     return dist.get_world_size(group), dist.get_rank(group)
 
 
+# Test-only switch: take the collective code path even in a world-1 group, so a one-GPU box
+# drives the device-tensor branch of every collective below through a real RCCL communicator
+# (tests/test_rccl_gpu.py).  Production never sets it: a world-1 collective is a copy.
+_FORCE = False
+
+
+def force_collectives(on: bool) -> None:
+    global _FORCE
+    _FORCE = bool(on)
+
+
+def collective(group=None) -> bool:
+    """True when a call must go through torch.distributed: world > 1, or forced at world 1."""
+    if not dist.is_initialized():
+        return False
+    return _FORCE or dist.get_world_size(group) > 1
+
+
 def is_gloo(group=None) -> bool:
     return dist.is_initialized() and dist.get_backend(group) == "gloo"
 
@@ -38,7 +56,7 @@ def comm_device(t: torch.Tensor, group=None) -> torch.device:
 def all_gather_stacked(t: torch.Tensor, group=None) -> torch.Tensor:
     """[world, *t.shape] on t.device: every rank's (same-shaped) tensor, in rank order."""
     world, _ = world_rank(group)
-    if world == 1:
+    if not collective(group):
         return t.unsqueeze(0)
     cd = comm_device(t, group)
     src = t.detach().contiguous().to(cd)
@@ -53,8 +71,7 @@ def all_gather_list(t: torch.Tensor, group=None) -> List[torch.Tensor]:
 
 
 def all_gather_sizes(n: int, device: Optional[torch.device] = None, group=None) -> List[int]:
-    world, _ = world_rank(group)
-    if world == 1:
+    if not collective(group):
         return [int(n)]
     dev = torch.device("cpu") if is_gloo(group) or device is None else device
     v = torch.tensor([int(n)], dtype=torch.int64, device=dev)
@@ -66,7 +83,7 @@ def all_gather_rows(t: torch.Tensor, group=None):
     Rows are padded to the largest rank's count for the collective and the padding dropped."""
     world, _ = world_rank(group)
     sizes = all_gather_sizes(t.shape[0], t.device, group)
-    if world == 1:
+    if not collective(group):
         return t, sizes
     mx = max(sizes)
     pad = torch.zeros((mx,) + tuple(t.shape[1:]), dtype=t.dtype, device=t.device)
@@ -77,7 +94,7 @@ def all_gather_rows(t: torch.Tensor, group=None):
 
 def all_reduce_max_(t: torch.Tensor, group=None) -> torch.Tensor:
     """In-place MAX all-reduce (staged through host under gloo)."""
-    if world_rank(group)[0] == 1:
+    if not collective(group):
         return t
     if is_gloo(group) and t.is_cuda:
         h = t.cpu()

@@ -43,6 +43,22 @@ __host__ __device__ __forceinline__ float desc_key_to_score(uint32_t k) {
   return __builtin_bit_cast(float, u);
 }
 
+// Score histograms of the select / threshold kernels.  hist_scale: bins per unit score, 0 when the
+// range is degenerate (empty, subnormal-small so that nbins / range overflows, infinite or NaN) --
+// every key then falls in one bin and the callers' exact fallbacks take over.  hist_bin: the bin
+// of f = distance * scale, clamped to [0, nbins) without an out-of-range or NaN float -> int
+// conversion; a NaN distance (a NaN score) goes to `nan_bin`, the end of the histogram its key
+// sorts to (desc_key: a positive NaN above +inf, a negative one below -inf).
+__device__ __forceinline__ float hist_scale(float nbins, float range) {
+  const float s = nbins / range;
+  return (range > 0.0f && __builtin_isfinite(s)) ? s : 0.0f;
+}
+__device__ __forceinline__ int hist_bin(float f, int nbins, int nan_bin) {
+  if (f != f) return nan_bin;
+  if (!(f < (float)(nbins - 1))) return nbins - 1;
+  return f < 1.0f ? 0 : (int)f;
+}
+
 // Training dropout (HF BertModel in train mode: embeddings, attention probabilities, and the
 // two sublayer outputs, modeling_bert.py:107,195,296,348): a counter-based hash of (seed, site,
 // element index) decides each keep, so forward and backward regenerate the same mask without

@@ -389,20 +389,7 @@ __global__ __launch_bounds__((NB == 5 ? 8 : 4) * 64, NB == 5 ? 1 : 2) void atten
       v[it] = bf16x8{};
       o[it] = bf16x8{};
       oo[it] = bf16x8{};
-#ifdef DRT_AB_ABL_NOLOAD   // ablation builds (tools/build_variant.sh): staging without global reads
       if (i < Lp * 8 && row < L) {
-        for (int j = 0; j < 8; ++j) {
-          q[it][j] = (__bf16)(0.01f * ((row + j) % 7));
-          k[it][j] = (__bf16)(0.02f * ((row + 3 * j) % 5));
-          v[it][j] = (__bf16)(0.01f * ((row * j) % 9));
-          o[it][j] = (__bf16)(0.001f * ((row + j) % 3));
-          oo[it][j] = (__bf16)(0.01f * ((row + 2 * j) % 11));
-        }
-      }
-      if (false) {
-#else
-      if (i < Lp * 8 && row < L) {
-#endif
         q[it] = *(const bf16x8*)(Qg + (int64_t)row * ld + c * 8);
         k[it] = *(const bf16x8*)(Kg + (int64_t)row * ld + c * 8);
         v[it] = *(const bf16x8*)(Vg + (int64_t)row * ld + c * 8);
@@ -495,11 +482,6 @@ __global__ __launch_bounds__((NB == 5 ? 8 : 4) * 64, NB == 5 ? 1 : 2) void atten
   // Outputs stay in registers (bf16) until every unit is done, then leave through LDS (dK into
   // the Qs image, dV into the dO image, dQ into the K image) as whole 128-B rows of 16-B stores
   // (12 per thread at L 128 instead of 96 two-byte stores per wave).
-#ifdef DRT_AB_ABL_NOPHASE
-  constexpr bool kRun = false;
-#else
-  constexpr bool kRun = true;
-#endif
   int p1 = -1, p2 = -1;
   if (NB <= 4) {
     if (wave < NB) p1 = p2 = wave;
@@ -507,7 +489,6 @@ __global__ __launch_bounds__((NB == 5 ? 8 : 4) * 64, NB == 5 ? 1 : 2) void atten
     p1 = wave < 5 ? wave : -1;
     p2 = wave >= 5 ? wave - 5 : (wave == 1 ? 3 : (wave == 2 ? 4 : -1));
   }
-  if (!kRun) p1 = p2 = -1;
   bf16x8 dKo[2][2], dVo[2][2], dQo[2][2];             // [t][e >> 3]: element e of column 32 t + r
 
   // ---- P1: dK, dV of key block p1

@@ -158,10 +158,7 @@ __device__ __forceinline__ float epi_post(const GemmArgs& a, float v, int64_t ro
 // 256^2 kernel from this many 256^2 tiles up (tools/qsweep.py: 128 beats 512 by 16-22 % on 4k-16k-token
 // batches); tile order inside an XCD's range: grouped-8 for K <= 1024 (small panels), row-major otherwise
 // (profiles/r02o_gemm_tile_order.log: orders within noise).
-#ifndef DRT_LARGE_MIN_TILES
-#define DRT_LARGE_MIN_TILES 128
-#endif
-constexpr int64_t kLargeMinTiles = DRT_LARGE_MIN_TILES;
+constexpr int64_t kLargeMinTiles = 128;
 __host__ __device__ constexpr int auto_tile_order(int64_t k) { return k <= 1024 ? 1 : 0; }
 
 // NS = LDS stages of 32 KiB (A + B K-tile): 2 = double buffer, 2 work-groups per CU (grids of
@@ -424,7 +421,7 @@ __global__ __launch_bounds__(256) void splitk_ln_kernel(const float* ws, int spl
 //                splits = 261 blocks on 256 CUs and the launch took ~2x its one-round time),
 //                >= kLSplitKPer per split, fp32 partials <= 256 MiB, fixed-order reduction
 //   SMALL_SPLIT  query-sized problems (< 384 tiles of 128^2, K >= 256): 128^2 kernel, splits to
-//                about DRT_SMALL_SPLIT_BLOCKS blocks, >= 128 K per split, partials <= 16 MiB (at
+//                about kSmallSplitBlocks blocks, >= 128 K per split, partials <= 16 MiB (at
 //                4096 x 768 -- a 128-query batch -- 3 splits = 38 MB of partials measured slower
 //                than unsplit)
 //   SMALL        everything else (and any split plan whose scratch the caller did not give)
@@ -433,10 +430,8 @@ constexpr int64_t kLSplitMinK = 8192, kLSplitKPer = 512, kSSplitCap = 16 << 20;
 // Blocks a SMALL_SPLIT grid aims at.  With the 4-stage ring kernel a block streams its K range
 // without waiting on each K-tile, so fewer, longer splits win: query tower at batch 8 (256 tokens)
 // 0.827 ms at 512, 0.756 at 32, 0.738 at 64, 0.753 at 96, 0.772 at 128, 0.943 unsplit
-// (profiles/r03f_query_encode_*, r03g_query_encode_*); batch 128 unchanged.  tools/build_variant.sh for A/B builds.
-#ifndef DRT_SMALL_SPLIT_BLOCKS
-#define DRT_SMALL_SPLIT_BLOCKS 64
-#endif
+// (profiles/r03f_query_encode_*, r03g_query_encode_*); batch 128 unchanged.
+constexpr int64_t kSmallSplitBlocks = 64;
 enum GemmPath { GP_LARGE, GP_LARGE_SPLIT, GP_SMALL_SPLIT, GP_SMALL };
 struct GemmPlan {
   int path = GP_SMALL;
@@ -482,7 +477,7 @@ static int large_splits(int64_t m, int64_t n, int64_t k, int64_t* kchunk) {
 static int small_splits(int64_t m, int64_t n, int64_t k, int64_t* kchunk) {
   const int64_t tiles = ((m + kBM - 1) / kBM) * ((n + kBN - 1) / kBN);
   if (tiles >= 384 || k < 256) return 0;
-  int64_t splits = (DRT_SMALL_SPLIT_BLOCKS + tiles - 1) / tiles;
+  int64_t splits = (kSmallSplitBlocks + tiles - 1) / tiles;
   if (splits > k / 128) splits = k / 128;
   const int64_t cap = kSSplitCap / (m * n * 4);
   if (splits > cap) splits = cap;

@@ -683,11 +683,10 @@ __device__ __forceinline__ uint64_t sel_load(const SelectArgs& a, int64_t q, int
 
 __device__ __forceinline__ float key_score(uint64_t x) { return desc_key_to_score((uint32_t)(x >> 32)); }
 
+// bin kSelBins - 1 = best scores
 __device__ __forceinline__ int score_bin(float s, float smin, float scale) {
-  float f = (s - smin) * scale;
-  int b = (int)f;
-  b = b < 0 ? 0 : b;
-  return b > kSelBins - 1 ? kSelBins - 1 : b;
+  if (scale == 0.0f) return 0;
+  return hist_bin((s - smin) * scale, kSelBins, __builtin_signbit(s) ? 0 : kSelBins - 1);
 }
 
 template <typename T, typename Op>
@@ -844,7 +843,7 @@ __global__ __launch_bounds__(kSelThreads) void select_kernel(SelectArgs a) {
     lo = block_reduce(lo, fscr, [](float x, float y) { return fminf(x, y); });
     hi = block_reduce(hi, fscr, [](float x, float y) { return fmaxf(x, y); });
     const float range = hi - lo;
-    const float scale = (range > 0.0f && range < __builtin_inff()) ? (float)kSelBins / range : 0.0f;
+    const float scale = hist_scale((float)kSelBins, range);
     for (int i = tid; i < kSelWaves * kSelBins; i += kSelThreads) (&hist[0][0])[i] = 0;
     __syncthreads();
     int bn[kSelKPT];
@@ -942,7 +941,7 @@ __global__ __launch_bounds__(kSelThreads) void select_kernel(SelectArgs a) {
     lo = block_reduce(lo, fscr, [](float x, float y) { return fminf(x, y); });
     hi = block_reduce(hi, fscr, [](float x, float y) { return fmaxf(x, y); });
     const float range = hi - lo;
-    const float scale = (range > 0.0f && range < __builtin_inff()) ? (float)kSelBins / range : 0.0f;
+    const float scale = hist_scale((float)kSelBins, range);
     // ---- B: per-wave histograms
     for (int i = tid; i < kSelWaves * kSelBins; i += kSelThreads) (&hist[0][0])[i] = 0;
     __syncthreads();
@@ -1233,16 +1232,15 @@ __global__ __launch_bounds__(kKthThreads) void kth_partial_kernel(const uint32_t
     lo = fminf(lo, red[1][w]);
   }
   const float range = hi - lo;
-  const float scale = (range > 0.0f && range < __builtin_inff()) ? (float)kKthBins / range : 0.0f;
+  const float scale = hist_scale((float)kKthBins, range);
   // bin 0 = best scores
   int bins[kKthPer];
 #pragma unroll
   for (int e = 0; e < kKthPer; ++e) {
     int bb = kKthBins;  // padding
     if (key[e] != 0xFFFFFFFFu) {
-      const float f = (hi - desc_key_to_score(key[e])) * scale;
-      bb = (int)f;
-      bb = bb < 0 ? 0 : (bb > kKthBins - 1 ? kKthBins - 1 : bb);
+      const float sc = desc_key_to_score(key[e]);
+      bb = scale == 0.0f ? 0 : hist_bin((hi - sc) * scale, kKthBins, __builtin_signbit(sc) ? kKthBins - 1 : 0);
       atomicAdd(&hist[wave][bb], 1u);
     }
     bins[e] = bb;
@@ -1410,12 +1408,12 @@ __global__ __launch_bounds__(kRankThreads) void kth_rank_kernel(const uint32_t* 
     lo = fminf(lo, red[1][w]);
   }
   const float range = hi - lo;
-  const float scale = (range > 0.0f && range < __builtin_inff()) ? (float)kRankBins / range : 0.0f;
+  const float scale = hist_scale((float)kRankBins, range);
   // bin 0 = best scores; monotone in the key, so the keys of bins <= b are the smallest keys
   auto bin_of = [&](uint32_t kk) {
-    const float f = (hi - desc_key_to_score(kk)) * scale;
-    int bb = (int)f;
-    return bb < 0 ? 0 : (bb > kRankBins - 1 ? kRankBins - 1 : bb);
+    if (scale == 0.0f) return 0;
+    const float sc = desc_key_to_score(kk);
+    return hist_bin((hi - sc) * scale, kRankBins, __builtin_signbit(sc) ? kRankBins - 1 : 0);
   };
 #pragma unroll
   for (int e = 0; e < kRankPer; ++e)

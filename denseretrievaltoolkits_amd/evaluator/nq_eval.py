@@ -137,63 +137,91 @@ class RowAnswerMatcher:
     """``has_answers`` for a whole query batch's retrieved ROWS at once (Trainer.evaluate).
 
     Same result as ``has_answers(text_of(row), answers[i])`` for every (query i, rank j) with
-    ``row = rows[i, j] >= 0`` (pads get 0).  Every index row is tokenised once per evaluation
-    (NFD, the uncased SimpleTokenizer pattern, one regex pass over many passages) into int32
-    token ids stored as one row of a padded [rows, width] matrix (-1 pads, width grows with the
-    longest passage seen), so a query's k passages are ONE row gather, and an answer of n tokens
-    is found by n shifted vectorised comparisons (a match never spans two passages; an empty
-    answer matches every passage, as the reference's loop does).
-    """
+    ``row = rows[i, j] >= 0`` (pads get 0).  A row is tokenised at most once per evaluation (NFD,
+    the uncased SimpleTokenizer pattern, one regex pass over many passages) into int32 token ids
+    stored in a compact SLOT of a padded [slots, width] matrix (-1 pads, width grows with the
+    longest passage seen); ``slot[row]`` maps an index row to its slot (-1 = not tokenised yet).
+    Memory therefore follows the rows actually tokenised -- the corpus rows prefilled during the
+    encode (up to the caller's budget) plus the rows queries retrieve -- not the corpus size.  A
+    query's k passages are ONE slot gather, and an answer of n tokens is found by n shifted
+    vectorised comparisons (a match never spans two passages; an empty answer matches every
+    passage, as the reference's loop does).  ``version`` changes whenever ``tok`` is reallocated
+    (the device mirror re-uploads on a change)."""
 
     def __init__(self, n_rows: int):
         self.vocab = {}
         self.n_rows = int(n_rows)
         self.width = 16
-        self.tok = np.full((self.n_rows, self.width), -1, dtype=np.int32)
-        self.seen = np.zeros(self.n_rows, dtype=bool)
+        self.slot = np.full(self.n_rows, -1, dtype=np.int64)
+        self.tok = np.full((0, self.width), -1, dtype=np.int32)
+        self.n_slots = 0
+        self.version = 0
+
+    @property
+    def seen(self) -> np.ndarray:
+        return self.slot >= 0
+
+    @property
+    def token_bytes(self) -> int:
+        return int(self.n_slots) * self.width * 4
 
     def ensure_rows(self, n_rows: int):
-        """Capacity for rows [0, n_rows) (geometric growth: called once per corpus batch)."""
+        """Rows [0, n_rows) addressable (geometric growth: called once per corpus batch)."""
         if n_rows > self.n_rows:
             n_rows = max(int(n_rows), self.n_rows + self.n_rows // 2)
-            t = np.full((n_rows, self.width), -1, dtype=np.int32)
-            t[: self.n_rows] = self.tok
-            sn = np.zeros(n_rows, dtype=bool)
-            sn[: self.n_rows] = self.seen
-            self.tok, self.seen, self.n_rows = t, sn, int(n_rows)
+            sl = np.full(n_rows, -1, dtype=np.int64)
+            sl[: self.n_rows] = self.slot
+            self.slot, self.n_rows = sl, int(n_rows)
 
     def rebase(self, offset: int, n_local: int, n_total: int):
         """Move rows [0, n_local) (a shard tokenised by local row) to [offset, offset + n_local) of
-        an n_total-row matcher (global rows of the sharded index)."""
-        t = np.full((n_total, self.width), -1, dtype=np.int32)
-        sn = np.zeros(n_total, dtype=bool)
-        t[offset: offset + n_local] = self.tok[:n_local]
-        sn[offset: offset + n_local] = self.seen[:n_local]
-        self.tok, self.seen, self.n_rows = t, sn, int(n_total)
+        an n_total-row matcher (global rows of the sharded index).  The token slots stay put."""
+        sl = np.full(n_total, -1, dtype=np.int64)
+        sl[offset: offset + n_local] = self.slot[:n_local]
+        self.slot, self.n_rows = sl, int(n_total)
 
-    def _grow(self, width: int):
-        w = self.width
+    def _reserve(self, n_slots: int, width: int):
+        cap, w = self.tok.shape[0], self.width
         while w < width:
             w *= 2
-        t = np.full((self.n_rows, w), -1, dtype=np.int32)
-        t[:, : self.width] = self.tok
+        if n_slots <= cap and w == self.width:
+            return
+        cap = max(n_slots, cap + cap // 2, 1024)
+        t = np.full((cap, w), -1, dtype=np.int32)
+        t[: self.n_slots, : self.width] = self.tok[: self.n_slots]
         self.tok, self.width = t, w
+        self.version += 1
 
     def fill(self, rows, text_of) -> int:
-        """Tokenise every row of ``rows`` not seen yet (``text_of(row)`` -> passage text)."""
-        rows = np.unique(rows[rows >= 0])
-        miss = rows[~self.seen[rows]]
+        """Tokenise every row of ``rows`` not tokenised yet (``text_of(row)`` -> passage text)."""
+        rows = np.unique(np.asarray(rows)[np.asarray(rows) >= 0])
+        miss = rows[self.slot[rows] < 0]
         if miss.size:
             v = self.vocab
             toks_list = tokenize_uncased_many([text_of(r) for r in miss.tolist()])
             mx = max((len(t) for t in toks_list), default=0)
-            if mx > self.width:
-                self._grow(mx)
-            for r, toks in zip(miss.tolist(), toks_list):
+            s0 = self.n_slots
+            self._reserve(s0 + miss.size, mx)
+            for j, toks in enumerate(toks_list):
                 if toks:
-                    self.tok[r, : len(toks)] = [v[t] if t in v else v.setdefault(t, len(v)) for t in toks]
-            self.seen[miss] = True
+                    self.tok[s0 + j, : len(toks)] = [v[t] if t in v else v.setdefault(t, len(v)) for t in toks]
+            self.slot[miss] = np.arange(s0, s0 + miss.size)
+            self.n_slots = s0 + int(miss.size)
         return int(miss.size)
+
+    def _answer_ids(self, answers_i):
+        """(token-id lists of the answers that can match, every): unknown tokens or answers longer
+        than the width never match; an empty answer matches every passage."""
+        out = []
+        for ans in answers_i:
+            aw = tokenize_uncased(unicodedata.normalize("NFD", ans))
+            if not aw:
+                return [], True
+            ids = [self.vocab.get(w, -2) for w in aw]
+            if min(ids) < 0 or len(ids) > self.width:
+                continue
+            out.append(ids)
+        return out, False
 
     def match_rows(self, rows: np.ndarray, text_of, answers) -> np.ndarray:
         """int8 [B, k]: 1 where the passage at rows[i, j] contains any of answers[i]."""
@@ -205,20 +233,16 @@ class RowAnswerMatcher:
         valid = rows >= 0
         W = self.width
         for i in range(B):
+            lists, every = self._answer_ids(answers[i])
+            if every:
+                hit[i] = 1
+                continue
             toks = None
-            for ans in answers[i]:
-                aw = tokenize_uncased(unicodedata.normalize("NFD", ans))
-                if not aw:
-                    hit[i] = 1
-                    break
-                ids = [self.vocab.get(w, -2) for w in aw]
-                if min(ids) < 0:
-                    continue   # a token no passage has
+            for ids in lists:
                 n = len(ids)
-                if n > W:
-                    continue
                 if toks is None:
-                    toks = self.tok[np.where(valid[i], rows[i], 0)]       # [k, W] row gather
+                    toks = self.tok[self.slot[np.where(valid[i], rows[i], 0)]] if valid[i].any() \
+                        else np.full((k, W), -1, np.int32)                        # [k, W] slot gather
                 m = toks[:, : W - n + 1] == ids[0]
                 for j in range(1, n):
                     m &= toks[:, j: W - n + 1 + j] == ids[j]
@@ -228,37 +252,42 @@ class RowAnswerMatcher:
 
 
 class DeviceRowMatcher:
-    """RowAnswerMatcher with the token matrix resident in HBM: a query batch's k retrieved rows are
-    gathered and compared on the GPU (the host only tokenises the batch's answers), on a stream of
-    its own so the matching of batch j runs beside the search of batch j + 1.  Same result as
-    ``RowAnswerMatcher.match_rows`` (the host matcher also owns the vocabulary and the passage
-    tokenisation); tests/test_answers_gpu.py compares the two on random and golden cases.
+    """RowAnswerMatcher with the token slots resident in HBM: a query batch's k retrieved rows are
+    gathered and compared on the GPU (the host only tokenises the batch's answers and any row not
+    tokenised yet), on a stream of its own so the matching of batch j runs beside the search of
+    batch j + 1.  Same result as ``RowAnswerMatcher.match_rows`` (the host matcher owns the
+    vocabulary, the slots and the passage tokenisation); tests/test_answers_gpu.py compares the two.
 
-    Per batch: toks = tok[rows] -> [B, k, W]; every answer a of query i as token ids padded to the
-    longest answer; a window start s matches answer a iff toks[i, :, s + j] == ids[a][j] for every
-    j < len(a) (and s + len(a) <= W) -- n_max broadcast compares over [B, A, k, W]."""
+    Per batch: toks = tok[slot[rows]] -> [B, k, W]; every answer a of query i as token ids padded
+    to the longest answer; a window start s matches answer a iff toks[i, :, s + j] == ids[a][j] for
+    every j < len(a) (and s + len(a) <= W).  The [B, a, k, W] window masks are evaluated in answer
+    chunks of at most MASK_ELEMS elements, so alias-heavy answer sets and long passages stay
+    bounded in memory."""
+
+    MASK_ELEMS = 1 << 26
 
     def __init__(self, host: "RowAnswerMatcher", device):
         import torch
         self.h = host
         self.device = torch.device(device)
         self.tok = None
-        self._key = None
+        self._version = None
+        self._slots = 0
         self.stream = torch.cuda.Stream(self.device)
 
-    def _upload(self, miss: np.ndarray):
-        """Mirror the host token matrix: whole when it was reallocated (growth, rebase), else only
-        the rows ``fill`` just tokenised."""
+    def _upload(self):
+        """Mirror the host slots: whole after a reallocation (version change), else only the slots
+        tokenised since the last upload."""
         import torch
         h = self.h
-        key = (id(h.tok), h.tok.shape)
         with torch.cuda.stream(self.stream):
-            if key != self._key:
+            if h.version != self._version or self.tok is None:
                 self.tok = torch.from_numpy(np.ascontiguousarray(h.tok)).to(self.device)
-                self._key = key
-            elif miss.size:
-                mt = torch.from_numpy(miss).to(self.device)
-                self.tok[mt] = torch.from_numpy(np.ascontiguousarray(h.tok[miss])).to(self.device)
+                self._version = h.version
+            elif h.n_slots > self._slots:
+                a, b = self._slots, h.n_slots
+                self.tok[a:b] = torch.from_numpy(np.ascontiguousarray(h.tok[a:b])).to(self.device)
+        self._slots = h.n_slots
 
     def match_rows(self, rows: np.ndarray, text_of, answers) -> np.ndarray:
         import torch
@@ -266,25 +295,12 @@ class DeviceRowMatcher:
         if B == 0 or k == 0:
             return np.zeros((B, k), dtype=np.int8)
         h = self.h
-        flat = np.unique(rows[rows >= 0])
-        miss = flat[~h.seen[flat]] if flat.size and flat.max() < h.n_rows else flat
         h.fill(rows, text_of)
-        self._upload(miss)
+        self._upload()
         W = h.width
-        # the batch's answers as token ids (host): unknown tokens / longer than W never match,
-        # an empty answer matches every passage of its query
         lists, every = [], np.zeros(B, dtype=bool)
         for i in range(B):
-            ids_i = []
-            for ans in answers[i]:
-                aw = tokenize_uncased(unicodedata.normalize("NFD", ans))
-                if not aw:
-                    every[i] = True
-                    break
-                ids = [h.vocab.get(w, -2) for w in aw]
-                if min(ids) < 0 or len(ids) > W:
-                    continue
-                ids_i.append(ids)
+            ids_i, every[i] = h._answer_ids(answers[i])
             lists.append(ids_i)
         A = max(1, max(len(x) for x in lists))
         n_max = max([1] + [len(a) for x in lists for a in x])
@@ -294,22 +310,27 @@ class DeviceRowMatcher:
             for a, ids in enumerate(x):
                 ans[i, a, : len(ids)] = ids
                 alen[i, a] = len(ids)
+        slots = np.where(rows >= 0, h.slot[np.maximum(rows, 0)], -1)
+        ac = max(1, min(A, self.MASK_ELEMS // max(1, B * k * W)))       # answers per chunk
         with torch.cuda.stream(self.stream):
             dev = self.device
-            r = torch.from_numpy(np.ascontiguousarray(rows)).pin_memory().to(dev, non_blocking=True)
-            at = torch.from_numpy(ans).pin_memory().to(dev, non_blocking=True)
-            lt = torch.from_numpy(alen).pin_memory().to(dev, non_blocking=True)
+            r = torch.from_numpy(np.ascontiguousarray(slots)).pin_memory().to(dev, non_blocking=True)
+            at_all = torch.from_numpy(ans).pin_memory().to(dev, non_blocking=True)
+            lt_all = torch.from_numpy(alen).pin_memory().to(dev, non_blocking=True)
             ev = torch.from_numpy(every).pin_memory().to(dev, non_blocking=True)
             valid = r >= 0
             toks = self.tok[r.clamp(min=0)]                                    # [B, k, W]
-            m = torch.ones((B, A, k, W), dtype=torch.bool, device=dev)          # window starts s
-            for j in range(n_max):
-                use = (lt > j)[:, :, None, None]                               # answer has token j
-                eq = toks[:, None, :, j:] == at[:, :, j][:, :, None, None]     # [B, A, k, W - j]
-                m[..., : W - j] &= eq | ~use
-                if j:
-                    m[..., W - j:] &= ~use                                     # s + j past the row
-            hit = (m.any(-1) & (lt > 0)[:, :, None]).any(1) | ev[:, None]
+            hit = ev[:, None].expand(B, k).clone()
+            for a0 in range(0, A, ac):
+                at, lt = at_all[:, a0: a0 + ac], lt_all[:, a0: a0 + ac]
+                m = torch.ones((B, at.shape[1], k, W), dtype=torch.bool, device=dev)   # window starts s
+                for j in range(n_max):
+                    use = (lt > j)[:, :, None, None]                           # answer has token j
+                    m[..., : W - j] &= (toks[:, None, :, j:] == at[:, :, j][:, :, None, None]) | ~use
+                    if j:
+                        m[..., W - j:] &= ~use                                 # s + j past the row
+                hit |= (m.any(-1) & (lt > 0)[:, :, None]).any(1)
+                del m
             hit &= valid
             out = torch.empty((B, k), dtype=torch.int8, pin_memory=True)
             out.copy_(hit.to(torch.int8), non_blocking=True)

@@ -377,7 +377,7 @@ class ShardedFlatIP:
         self.sync_offsets()
 
     def sync_offsets(self):
-        counts = comm.all_gather_sizes(self.local.ntotal, self.local.device, self.group) if self.world > 1 \
+        counts = comm.all_gather_sizes(self.local.ntotal, self.local.device, self.group) if self._multi() \
             else [int(self.local.ntotal)]
         self.offset = sum(counts[: self.rank])
         self.ntotal = sum(counts)
@@ -399,7 +399,7 @@ class ShardedFlatIP:
         checks group g's certificates.  Otherwise batch j + 1 is enqueued (scan, exchange, merge)
         before the host checks batch j's certificate."""
         batches = list(batches)
-        if self.world > 1 and self.protocol == "global_tau" and self.ntotal < 0xFFFFFFFF \
+        if self._multi() and self.protocol == "global_tau" and self.ntotal < 0xFFFFFFFF \
                 and isinstance(self.local, FlatIPIndex):
             groups = [[self.local._queries(q) for q in g] for g in _groups(batches)]
 
@@ -422,8 +422,12 @@ class ShardedFlatIP:
         """[world, *t.shape] all-gather (RCCL on device; host-staged under gloo, comm.py)."""
         return comm.all_gather_stacked(t, self.group)
 
+    def _multi(self) -> bool:
+        """Exchange through collectives: world > 1 (or the test-only world-1 forcing, comm.py)."""
+        return self.world > 1 or comm.collective(self.group)
+
     def _enqueue(self, q, k: int, to_host: bool = False):
-        if self.world == 1:
+        if not self._multi():
             if hasattr(self.local, "_enqueue"):
                 return ("local", self.local._enqueue(q, k, self.offset, to_host=to_host))
             return ("done", self.local.search_device(q, k, id_offset=self.offset))

@@ -37,7 +37,6 @@ from ..evaluator.metrics import get_metrics
 from ..evaluator.nq_eval import AnswerMatcher, DeviceRowMatcher, RowAnswerMatcher, has_answers
 from ..search import ShardedFlatIP, _stage_host
 from .losses import get_loss_function
-from .scheduler import ConstantScheduler, CosineScheduler, InverseSquareRootScheduler, LinearScheduler
 
 logger = logging.getLogger(__name__)
 
@@ -100,10 +99,14 @@ class Trainer:
             opt = transformers.Adafactor(params=params, **kw)
         else:
             opt = classes[name](params=params, **kw)
-        sched = {"inverse": InverseSquareRootScheduler, "cosine": CosineScheduler, "linear": LinearScheduler,
-                 "constant": ConstantScheduler}
         sname = getattr(a, "scheduler", None)
-        if sname is not None and sname in sched:
+        if sname is not None and sname in ("inverse", "cosine", "linear", "constant"):
+            # the LR schedulers are off the hot path (scalar lr arithmetic): the user's own
+            # DRT.trainer.scheduler classes wrap the optimizer, as the reference does (trainer.py:85-112)
+            import importlib
+            us = importlib.import_module("DRT.trainer.scheduler")
+            sched = {"inverse": us.InverseSquareRootScheduler, "cosine": us.CosineScheduler,
+                     "linear": us.LinearScheduler, "constant": us.ConstantScheduler}
             skw = dict(getattr(a, "scheduler_kwargs", {}) or {})
             skw.setdefault("max_lr", a.learning_rate)
             opt = sched[sname](base_optimizer=opt, **skw)
@@ -151,6 +154,7 @@ class Trainer:
         # rank's shard are tokenised here, on the host, while the GPU encodes the next batches
         ds = getattr(self.corpus_dataloader, "dataset", None)
         self._matcher = RowAnswerMatcher(0) if (self.prefill_answer_tokens and ds is not None) else None
+        prefill = self._matcher is not None
         for batch in self.corpus_dataloader:
             data = {k: self._to_device(v) for k, v in batch[1].items()}
             reps = self._encode(passage=data).p_reps
@@ -165,13 +169,18 @@ class Trainer:
             self.index.local.add(reps)
             ids_local.extend(list(batch[0]))
             if self._matcher is not None:
-                try:
-                    dids = list(batch[0])
-                    self._matcher.ensure_rows(row0 + len(dids))
-                    self._matcher.fill(np.arange(row0, row0 + len(dids)),
-                                       lambda r, _d=dids, _o=row0: ds[_d[r - _o]]["original"])
-                except (KeyError, TypeError, IndexError):
-                    self._matcher = None   # no 'original' texts here: matched on demand in evaluate
+                dids = list(batch[0])
+                self._matcher.ensure_rows(row0 + len(dids))
+                if prefill:
+                    try:
+                        self._matcher.fill(np.arange(row0, row0 + len(dids)),
+                                           lambda r, _d=dids, _o=row0: ds[_d[r - _o]]["original"])
+                    except (KeyError, TypeError, IndexError):
+                        self._matcher = None   # no 'original' texts here: matched on demand in evaluate
+                        continue
+                    # bounded: past the budget the remaining rows are tokenised only if a query
+                    # retrieves them (the matcher's slots grow with the rows actually tokenised)
+                    prefill = self._matcher.token_bytes < self.prefill_answer_max_bytes
         if self.index is None:
             raise ValueError("empty corpus")
         self._ids_local = ids_local
@@ -217,6 +226,8 @@ class Trainer:
     ENCODE_WINDOW = 4096
     SEARCH_BATCH = 128
     prefill_answer_tokens = True
+    # host (and, mirrored, HBM) bytes of passage tokens prefilled during the corpus encode
+    prefill_answer_max_bytes = 1 << 30
 
     def _to_device(self, v):
         if v is None or not isinstance(v, torch.Tensor):
@@ -264,7 +275,9 @@ class Trainer:
             for j, (_, ids) in enumerate(self.index.local.search_batches_iter(batches, k, to_host=True)):
                 yield j * sb, ids
             return
-        allq, sizes = comm.all_gather_rows(q_reps.contiguous())
+        # every rank hands the collective the same dtype (a rank with no queries left sends an
+        # empty fp32 tensor)
+        allq, sizes = comm.all_gather_rows(q_reps.float().contiguous())
         lo = sum(sizes[: self.rank])
         hi = lo + sizes[self.rank]
         batches = [allq[a: a + sb] for a in range(0, allq.shape[0], sb)]

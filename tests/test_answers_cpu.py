@@ -93,3 +93,18 @@ def test_row_matcher_random_vs_has_answers():
     rows = np.arange(100, 110)[None, :]
     got = m2.match_rows(rows, lambda r: (_ for _ in ()).throw(AssertionError("refilled")), [["a"]])
     assert got[0].tolist() == [int(has_answers(docs[r], ["a"])) for r in range(10)]
+
+
+def test_row_matcher_memory_follows_tokenised_rows():
+    """The token matrix holds only rows that were tokenised: a 5M-row index with 3 retrieved rows
+    keeps a few KiB of tokens (the dense [rows, W] matrix did not scale to 21M)."""
+    from denseretrievaltoolkits_amd.evaluator.nq_eval import RowAnswerMatcher
+    m = RowAnswerMatcher(5_000_000)
+    texts = {7: "the eiffel tower in paris", 4_999_999: "tokyo tower", 123: " ".join(["w"] * 40)}
+    rows = np.array([[7, 4_999_999, 123, -1]])
+    got = m.match_rows(rows, lambda r: texts[r], [["tower"]])
+    assert got.tolist() == [[1, 1, 0, 0]]
+    assert m.n_slots == 3 and m.width == 64 and m.tok.nbytes <= 1024 * 64 * 4
+    v = m.version
+    m.fill(np.array([8]), lambda r: " ".join(["x"] * 100))     # wider passage: reallocation
+    assert m.version > v and m.width == 128 and m.match_rows(rows, None, [["tower"]]).tolist() == [[1, 1, 0, 0]]

@@ -13,7 +13,9 @@ from conftest import REPO
 pytestmark = pytest.mark.gpu
 
 
-def test_device_matcher_equals_host_random(dev):
+@pytest.mark.parametrize("mask_elems", [None, 64])
+def test_device_matcher_equals_host_random(dev, mask_elems):
+    """mask_elems 64: the window masks evaluated one answer at a time (the memory-bounded chunking)."""
     from denseretrievaltoolkits_amd.evaluator.nq_eval import DeviceRowMatcher, RowAnswerMatcher, has_answers
     rng = np.random.default_rng(7)
     vocab = ["a", "b", "c", "d", "A", "b.", "c-d", "e", "É", "naïve", "⁂", "日本"]
@@ -21,6 +23,8 @@ def test_device_matcher_equals_host_random(dev):
     host = RowAnswerMatcher(0)
     host.ensure_rows(500)
     dm = DeviceRowMatcher(host, dev)
+    if mask_elems:
+        dm.MASK_ELEMS = mask_elems
     ref_m = RowAnswerMatcher(0)
     ref_m.ensure_rows(500)
     for it in range(40):
