@@ -48,6 +48,16 @@ _SIGNATURES = [
     ("drt_ip_topk_dist_filter_lists_at", c_i32, [c_vp, c_i64, c_vp, c_i64, c_i64, c_i32, c_i32, c_i64, c_vp,
                                                  c_i32, c_i64, c_vp, c_vp, c_vp, c_sz, c_vp]),
     ("drt_topk_merge_packed", c_i32, [c_vp, c_i64, c_i32, c_i32, c_i64, c_vp, c_vp, c_vp, c_vp]),
+    ("drt_topk_merge_packed_cert", c_i32, [c_vp, c_i64, c_i32, c_i32, c_i32, c_i64, c_vp, c_vp, c_vp, c_vp]),
+    ("drt_row_stats_bf16", c_i32, [c_vp, c_i64, c_i32, c_vp, c_i32, c_vp]),
+    ("drt_refine_width", c_i32, [c_i32]),
+    ("drt_ip_topk_exact_bf16", c_i32, [c_vp, c_i64, c_vp, c_i64, c_i32, c_i32, c_i64, c_vp, c_vp, c_vp, c_vp, c_vp,
+                                       c_sz, c_vp]),
+    ("drt_ip_topk_resolve_exact", c_i32, [c_vp, c_i64, c_vp, c_i64, c_i32, c_i32, c_i64, c_vp, c_vp, c_vp, c_vp,
+                                          c_vp, c_sz, c_vp, c_vp]),
+    ("drt_refine_delta_bf16", c_i32, [c_vp, c_i64, c_i32, c_vp, c_i64, c_i64, c_vp, c_vp, c_i32, c_i32, c_vp, c_vp,
+                                      c_vp, c_vp, c_vp, c_vp]),
+    ("drt_refine_sort", c_i32, [c_vp, c_vp, c_vp, c_vp, c_i64, c_i32, c_i32, c_vp, c_vp, c_vp]),
     ("drt_gemm_nt_bf16_f32", c_i32, [c_vp, c_vp, c_vp, c_i64, c_i64, c_i32, c_i64, c_vp]),
     ("drt_embed_ln", c_i32, [c_vp, c_vp, c_i64, c_i64, c_vp, c_vp, c_vp, c_vp, c_vp, c_f32, c_i32, c_vp, c_vp]),
     ("drt_linear_bf16", c_i32, [c_vp, c_vp, c_vp, c_vp, c_vp, c_i64, c_i64, c_i64, c_i32, c_vp]),

@@ -103,3 +103,16 @@ def all_reduce_max_(t: torch.Tensor, group=None) -> torch.Tensor:
     else:
         dist.all_reduce(t, op=dist.ReduceOp.MAX, group=group)
     return t
+
+
+def all_reduce_sum_(t: torch.Tensor, group=None) -> torch.Tensor:
+    """In-place SUM all-reduce (staged through host under gloo)."""
+    if not collective(group):
+        return t
+    if is_gloo(group) and t.is_cuda:
+        h = t.cpu()
+        dist.all_reduce(h, op=dist.ReduceOp.SUM, group=group)
+        t.copy_(h)
+    else:
+        dist.all_reduce(t, op=dist.ReduceOp.SUM, group=group)
+    return t

@@ -672,6 +672,7 @@ struct SelectArgs {
   // entry k = flags (bit 0: overflow); with a global tau a short local list is not a failure
   uint64_t* out_packed;
   bool global_tau;
+  int k_cert;               // k of the certification (0: k); the refine stage selects kc >= k entries
 };
 
 template <int INPUT>
@@ -1150,7 +1151,8 @@ __global__ __launch_bounds__(kSelThreads) void select_kernel(SelectArgs a) {
     int st = 0;
     if (INPUT == SEL_KEYS64) {
       if (c_raw > a.cap) st = 1;                                                       // overflow
-      if (!a.global_tau && c_raw < (int64_t)a.k && c_raw < a.n_total) st = 1;          // threshold too high
+      const int64_t kq = a.k_cert > 0 ? a.k_cert : a.k;
+      if (!a.global_tau && c_raw < kq && c_raw < a.n_total) st = 1;                    // threshold too high
     }
     a.status[orow] = st;
   }
@@ -1519,7 +1521,8 @@ template <int KP>
 __global__ __launch_bounds__(kTreeThreads) void merge_packed_tree_kernel(const uint64_t* parts, int64_t nq,
                                                                          int nparts, int p2, int k,
                                                                          int64_t n_global, float* out_s,
-                                                                         int64_t* out_i, int32_t* status) {
+                                                                         int64_t* out_i, int32_t* status,
+                                                                         int kcert) {
   extern __shared__ __attribute__((aligned(16))) uint64_t L[];  // [p2][KP]
   constexpr int NT = kTreeThreads;
   __shared__ int bad;
@@ -1624,7 +1627,7 @@ __global__ __launch_bounds__(kTreeThreads) void merge_packed_tree_kernel(const u
       out_i[q * k + i] = (int64_t)(x & 0xFFFFFFFFull);
     }
   }
-  if (status && tid == 0) status[q] = (bad || (L[k - 1] == ~0ull && n_global >= (int64_t)k)) ? 1 : 0;
+  if (status && tid == 0) status[q] = (bad || (L[kcert - 1] == ~0ull && n_global >= (int64_t)kcert)) ? 1 : 0;
 }
 
 // Count merge (round 2, the default where 2 <= nparts <= 8 and nparts * k <= 8192): entry k of
@@ -1654,11 +1657,11 @@ __device__ __forceinline__ int packed_valid_count(const uint64_t* L, int k) {
 }
 constexpr int kCntThreads = 1024;
 constexpr int kCntMaxParts = 8;
-constexpr int kCntMaxKeys = 8192;
+constexpr int kCntMaxKeys = 16384;   // 128 KiB of LDS
 __global__ __launch_bounds__(kCntThreads) void merge_packed_count_kernel(const uint64_t* parts, int64_t nq,
                                                                          int nparts, int k, int64_t n_global,
                                                                          float* out_s, int64_t* out_i,
-                                                                         int32_t* status) {
+                                                                         int32_t* status, int kcert) {
   extern __shared__ __attribute__((aligned(16))) uint64_t P[];   // valid prefixes of all parts, concatenated
   __shared__ int cnt[kCntMaxParts], off[kCntMaxParts + 1], flg[kCntMaxParts];
   const int tid = threadIdx.x;
@@ -1738,7 +1741,7 @@ __global__ __launch_bounds__(kCntThreads) void merge_packed_count_kernel(const u
   if (status && tid == 0) {
     int bad = 0;
     for (int l = 0; l < kCntMaxParts; ++l) bad |= flg[l];
-    status[q] = (bad || (tot < k && n_global >= (int64_t)k)) ? 1 : 0;
+    status[q] = (bad || (tot < kcert && n_global >= (int64_t)kcert)) ? 1 : 0;
   }
 }
 
@@ -1748,7 +1751,7 @@ __global__ __launch_bounds__(kCntThreads) void merge_packed_count_kernel(const u
 // k-th score) and no shard overflowed.
 __global__ __launch_bounds__(512) void merge_packed_kernel(const uint64_t* parts, int64_t nq, int nparts, int k,
                                                            int64_t n_global, float* out_s, int64_t* out_i,
-                                                           int32_t* status) {
+                                                           int32_t* status, int kcert) {
   __shared__ uint64_t A[kSelMaxK], B[kSelMaxK], Cb[kSelMaxK];
   __shared__ int bad;
   const int tid = threadIdx.x;
@@ -1793,7 +1796,7 @@ __global__ __launch_bounds__(512) void merge_packed_kernel(const uint64_t* parts
       out_i[q * k + i] = (int64_t)(x & 0xFFFFFFFFull);
     }
   }
-  if (status && tid == 0) status[q] = (bad || (A[k - 1] == ~0ull && n_global >= (int64_t)k)) ? 1 : 0;
+  if (status && tid == 0) status[q] = (bad || (A[kcert - 1] == ~0ull && n_global >= (int64_t)kcert)) ? 1 : 0;
 }
 
 // ---------------------------------------------------------------------------
@@ -1899,6 +1902,282 @@ __global__ __launch_bounds__(kMergeThreads) void merge_kernel(const float* score
 }
 
 // ---------------------------------------------------------------------------
+// Canonical order: exact re-ranking of a top-k candidate list.
+//
+// The filter scan scores in fp32 on the MFMA (bf16 products are exact in fp32; the sum of d of
+// them is rounded), so rows whose exact inner products differ by less than the fp32 summation
+// error may come out in either order -- and a row just outside the fp32 top-k may belong inside
+// it.  The reference evaluator's answer is defined by the exact products (faiss sums in fp32 too,
+// in yet another order); this stage makes the result canonical: the order of the EXACT scores
+// (fp64 sums of the bf16 products), ties by ascending id -- what an fp64 CPU evaluator returns.
+//
+// Error bound (any fp32 summation order, each addition rounded to nearest): |fl(s) - s| <=
+// gamma_d sum_i |q_i p_i| <= d u ||q||_2 ||p||_2 (u = 2^-24); eps = 2.5 d u ||q|| max_row ||p||
+// leaves a factor 2.5 of slack (faithful rather than nearest rounding inside the MFMA, the fp32
+// norms' own rounding).  With s_k the k-th candidate's fp32 score, every row of the exact top-k
+// has fp32 score >= B = s_k - 2 eps, so the candidates are exactly the entries >= B of a list
+// that (a) holds every hit >= B -- its last entry is < B, or the hits ended -- and (b) saw every
+// row >= B -- the filter threshold tau <= B.  (a) fails: status bit 1 (the window is wider than
+// the list: more than kc - k near-ties; the fp32 order is kept).  (b) fails: status bit 0 (the
+// caller's exact rescan).  Integer-valued rows and queries whose |partial sums| stay below 2^23
+// are scored exactly in fp32: eps = 0 and the fp32 order IS the exact order.
+//
+// refine_delta_kernel  grid (nq, kc / kRefSlice): exact sum for each candidate this rank owns
+//   (global id in [row_offset, row_offset + n_local)) -> delta = exact - fp32 score (0 where not
+//   owned or past the window: shards add their deltas with one all-reduce SUM); cnt[q] = window
+//   size (-1 when eps = 0).
+// refine_sort_kernel   grid nq: the window by (fp32 score + delta desc, id asc) -> top-k.
+// ---------------------------------------------------------------------------
+constexpr int kRefThreads = 256;
+constexpr int kRefSlice = 128;
+constexpr int kRefSortThreads = 512;
+constexpr int kRefMax = kSelMaxK;
+
+struct RefineArgs {
+  const __bf16* Q;
+  int64_t nq;
+  int32_t d;
+  const __bf16* P;
+  int64_t n_local;
+  int64_t row_offset;
+  const float* cs;      // [nq][kc] fp32 scores, sorted desc (pads -FLT_MAX)
+  const int64_t* ci;    // [nq][kc] global ids (pads -1)
+  int32_t kc, k;
+  const float* stats;   // row statistics (drt_row_stats_bf16)
+  const float* tau;     // [nq] filter thresholds or NULL (every row was scored)
+  float* delta;         // [nq][kc]
+  int32_t* cnt;         // [nq]
+  int32_t* status;      // [nq] (indexed through qmap) or NULL
+  const int32_t* qmap;  // output row of query q, or NULL
+  bool set_status;      // status[row] = this stage's bits (the exact rescan clears it) instead of |=
+  float* out_s;         // refine_sort: [*, k]
+  int64_t* out_i;
+};
+
+__device__ __forceinline__ uint64_t desc_key64(double x) {
+  x = x + 0.0;
+  const uint64_t u = __builtin_bit_cast(uint64_t, x);
+  const uint64_t ord = (u >> 63) ? ~u : (u | 0x8000000000000000ull);
+  return ~ord;
+}
+
+template <typename T>
+__device__ __forceinline__ T ref_block_sum(T v, T* scr) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  __syncthreads();
+  if ((threadIdx.x & 63) == 0) scr[threadIdx.x >> 6] = v;
+  __syncthreads();
+  T r = 0;
+  for (int w = 0; w < (int)(blockDim.x >> 6); ++w) r += scr[w];
+  return r;
+}
+
+// eps of query q (0: exact in fp32).  Every work-group of q computes the same value.
+__device__ __forceinline__ float refine_eps(const RefineArgs& a, int64_t q, float* fscr, int* iscr) {
+  const __bf16* qr = a.Q + q * (int64_t)a.d;
+  float ss = 0.0f;
+  int nonint = 0;
+  for (int i = threadIdx.x; i < a.d; i += blockDim.x) {
+    const float v = (float)qr[i];
+    ss += v * v;
+    nonint |= (v != __builtin_rintf(v)) ? 1 : 0;
+  }
+  ss = ref_block_sum(ss, fscr);
+  nonint = ref_block_sum(nonint, iscr);
+  const float qn = __builtin_sqrtf(ss) * 1.0001f;
+  const float pmax = __builtin_sqrtf(a.stats[0]) * 1.0001f;
+  const bool pint = a.stats[1] != 0.0f;
+  if (pint && nonint == 0 && qn * pmax < 8388608.0f) return 0.0f;
+  return 2.5f * (float)a.d * 5.9604645e-8f * qn * pmax + 1e-30f;
+}
+
+__global__ __launch_bounds__(kRefThreads) void refine_delta_kernel(RefineArgs a) {
+  __shared__ float fscr[kRefThreads / 64];
+  __shared__ int iscr[kRefThreads / 64];
+  const int64_t q = blockIdx.x;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const float eps = refine_eps(a, q, fscr, iscr);
+  const float* cs = a.cs + q * (int64_t)a.kc;
+  const int64_t* ci = a.ci + q * (int64_t)a.kc;
+  int nval = 0;
+  for (int j = tid; j < a.kc; j += kRefThreads) nval += ci[j] >= 0 ? 1 : 0;
+  nval = ref_block_sum(nval, iscr);
+  const float B = nval < a.k ? -__builtin_inff() : cs[a.k - 1] - 2.0f * eps;
+  int C = 0;
+  for (int j = tid; j < nval; j += kRefThreads) C += cs[j] >= B ? 1 : 0;
+  C = ref_block_sum(C, iscr);
+  const bool wide = eps != 0.0f && C == a.kc && nval == a.kc;               // window wider than the list
+  if (blockIdx.y == 0 && tid == 0) {
+    a.cnt[q] = eps == 0.0f ? -1 : (wide ? -2 : C);
+    if (a.status) {
+      int st = wide ? 2 : 0;
+      if (eps != 0.0f && a.tau && nval >= a.k && a.tau[q] > B) st |= 1;     // rows in [B, tau) unseen
+      const int64_t orow = a.qmap ? (int64_t)a.qmap[q] : q;
+      if (a.set_status) a.status[orow] = st;
+      else if (st) a.status[orow] |= st;
+    }
+  }
+  const int j0 = blockIdx.y * kRefSlice;
+  const int j1 = j0 + kRefSlice < a.kc ? j0 + kRefSlice : a.kc;
+  float* dq = a.delta + q * (int64_t)a.kc;
+  // this lane's query elements: 4-element chunks c = lane + 64 t of the row, in fp64
+  constexpr int kMaxT = 4;   // d <= 1024
+  const int nch = a.d >> 2;
+  double qv[kMaxT][4];
+  const __bf16* qr = a.Q + q * (int64_t)a.d;
+#pragma unroll
+  for (int t = 0; t < kMaxT; ++t) {
+    const int c = lane + 64 * t;
+    const bf16x4 x = c < nch ? *(const bf16x4*)(qr + 4 * c) : bf16x4{};
+#pragma unroll
+    for (int u = 0; u < 4; ++u) qv[t][u] = (double)(float)x[u];
+  }
+  for (int j = j0 + wave; j < j1; j += kRefThreads / 64) {
+    const int64_t id = ci[j];
+    const int64_t row = id - a.row_offset;
+    const bool own = eps != 0.0f && !wide && j < C && id >= 0 && row >= 0 && row < a.n_local;   // wave-uniform
+    double acc = 0.0;
+    if (own) {
+      const __bf16* pr = a.P + row * (int64_t)a.d;
+#pragma unroll
+      for (int t = 0; t < kMaxT; ++t) {
+        const int c = lane + 64 * t;
+        if (c < nch) {
+          const bf16x4 x = *(const bf16x4*)(pr + 4 * c);
+#pragma unroll
+          for (int u = 0; u < 4; ++u) acc = __builtin_fma(qv[t][u], (double)(float)x[u], acc);
+        }
+      }
+#pragma unroll
+      for (int o = 32; o > 0; o >>= 1) acc += __shfl_xor(acc, o, 64);
+    }
+    if (lane == 0) dq[j] = own ? (float)(acc - (double)cs[j]) : 0.0f;
+  }
+}
+
+__global__ __launch_bounds__(kRefSortThreads) void refine_sort_kernel(RefineArgs a) {
+  __shared__ uint64_t key[kRefMax];
+  __shared__ int64_t idv[kRefMax];
+  __shared__ float sco[kRefMax];
+  const int64_t q = blockIdx.x;
+  const int tid = threadIdx.x;
+  const int64_t orow = a.qmap ? (int64_t)a.qmap[q] : q;
+  const float* cs = a.cs + q * (int64_t)a.kc;
+  const int64_t* ci = a.ci + q * (int64_t)a.kc;
+  float* os = a.out_s + orow * (int64_t)a.k;
+  int64_t* oi = a.out_i + orow * (int64_t)a.k;
+  const int C = a.cnt[q];
+  if (C < 0) {   // exact in fp32 (or the window did not fit the list: status bit 1): the fp32 order
+    for (int j = tid; j < a.k; j += kRefSortThreads) {
+      os[j] = cs[j];
+      oi[j] = ci[j];
+    }
+    return;
+  }
+  const float* dq = a.delta + q * (int64_t)a.kc;
+  int n2 = 1;
+  while (n2 < C) n2 <<= 1;
+  for (int j = tid; j < n2; j += kRefSortThreads) {
+    if (j < C) {
+      const double ex = (double)cs[j] + (double)dq[j];
+      key[j] = desc_key64(ex);
+      idv[j] = ci[j];
+      sco[j] = (float)ex;
+    } else {
+      key[j] = ~0ull;
+      idv[j] = INT64_MAX;
+      sco[j] = kPadScore;
+    }
+  }
+  __syncthreads();
+  // bitonic sort of (key asc, id asc); the score rides along
+  for (int size = 2; size <= n2; size <<= 1) {
+    for (int stride = size >> 1; stride > 0; stride >>= 1) {
+      for (int i = tid; i < n2; i += kRefSortThreads) {
+        const int j = i ^ stride;
+        if (j > i) {
+          const bool up = (i & size) == 0;
+          const uint64_t ki = key[i], kj = key[j];
+          const int64_t ii = idv[i], ij = idv[j];
+          const bool gt = ki > kj || (ki == kj && ii > ij);
+          if (gt == up) {
+            key[i] = kj;
+            key[j] = ki;
+            idv[i] = ij;
+            idv[j] = ii;
+            const float t = sco[i];
+            sco[i] = sco[j];
+            sco[j] = t;
+          }
+        }
+      }
+      __syncthreads();
+    }
+  }
+  for (int j = tid; j < a.k; j += kRefSortThreads) {
+    if (j < C) {
+      os[j] = sco[j];
+      oi[j] = idv[j];
+    } else {
+      os[j] = kPadScore;
+      oi[j] = -1;
+    }
+  }
+}
+
+// Row statistics for the refine bound: stats[0] = max over rows of the fp32 sum of squares
+// (as a non-negative float, combined by an integer max of its bits), stats[1] = 1.0f while every
+// element seen is an integer (combined by AND of the bits of 1.0f / 0.0f).
+__global__ __launch_bounds__(256) void row_stats_kernel(const __bf16* P, int64_t n, int32_t d, uint32_t* stats) {
+  __shared__ float fm[4];
+  __shared__ int fi[4];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int64_t gw = (int64_t)blockIdx.x * 4 + wave, nw = (int64_t)gridDim.x * 4;
+  const int nch = d >> 2;
+  float mx = 0.0f;
+  int nonint = 0;
+  for (int64_t r = gw; r < n; r += nw) {
+    const __bf16* pr = P + r * (int64_t)d;
+    float ss = 0.0f;
+    for (int c = lane; c < nch; c += 64) {
+      const bf16x4 x = *(const bf16x4*)(pr + 4 * c);
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const float v = (float)x[u];
+        ss += v * v;
+        nonint |= (v != __builtin_rintf(v)) ? 1 : 0;
+      }
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) ss += __shfl_xor(ss, o, 64);
+    mx = fmaxf(mx, ss);
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) nonint |= __shfl_xor(nonint, o, 64);
+  if (lane == 0) {
+    fm[wave] = mx;
+    fi[wave] = nonint;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    float m = 0.0f;
+    int ni = 0;
+    for (int w = 0; w < 4; ++w) {
+      m = fmaxf(m, fm[w]);
+      ni |= fi[w];
+    }
+    atomicMax(stats, __builtin_bit_cast(uint32_t, m));
+    if (ni) atomicAnd(stats + 1, 0u);
+  }
+}
+
+__global__ void row_stats_init_kernel(uint32_t* stats) {
+  stats[0] = 0u;
+  stats[1] = __builtin_bit_cast(uint32_t, 1.0f);
+}
+
+// ---------------------------------------------------------------------------
 // Host-side planning and launch helpers.
 // ---------------------------------------------------------------------------
 struct TopkPlan {
@@ -1909,9 +2188,29 @@ struct TopkPlan {
   int64_t stride;     // sample stride
   int64_t r;          // rank of the sampled score used as tau
   int64_t nchunk;     // kth_partial chunks per query
+  int64_t kc;         // refine: candidates selected per query (>= k)
   // workspace offsets (bytes)
-  size_t off_tau, off_cnt, off_keys, off_sample, off_part, total;
+  size_t off_tau, off_cnt, off_keys, off_sample, off_part, off_cs, off_ci, off_delta, off_rcnt, total;
 };
+
+static size_t align_up(size_t x, size_t a) { return (x + a - 1) / a * a; }
+
+// Candidates the canonical-order stage selects per query: k plus a window for the entries within
+// 2 eps of the k-th score (a few dozen on real-valued data; up to 2048 in all).
+static int64_t refine_width(int64_t k) { return std::min<int64_t>(kSelMaxK, k + std::max<int64_t>(256, k / 4)); }
+
+static size_t plan_refine_tail(TopkPlan& p, size_t o) {
+  p.kc = refine_width(p.k);
+  p.off_cs = o;
+  o = align_up(o + (size_t)p.nq_pad * p.kc * 4, 256);
+  p.off_ci = o;
+  o = align_up(o + (size_t)p.nq_pad * p.kc * 8, 256);
+  p.off_delta = o;
+  o = align_up(o + (size_t)p.nq_pad * p.kc * 4, 256);
+  p.off_rcnt = o;
+  o = align_up(o + (size_t)p.nq_pad * 4, 256);
+  return o;
+}
 
 static double poisson_tail_ge(double lam, int64_t r) {
   // P[X >= r], X ~ Poisson(lam), by summing the pmf from r upward.
@@ -1925,7 +2224,6 @@ static double poisson_tail_ge(double lam, int64_t r) {
   return s;
 }
 
-static size_t align_up(size_t x, size_t a) { return (x + a - 1) / a * a; }
 
 static TopkPlan make_plan(int64_t nq, int64_t n, int64_t k) {
   TopkPlan p{};
@@ -1971,7 +2269,7 @@ static TopkPlan make_plan(int64_t nq, int64_t n, int64_t k) {
   if (p.sample) o = align_up(o + (size_t)p.nq_pad * align_up(p.m, 4) * 4, 256);
   p.off_part = o;
   if (p.sample) o = align_up(o + (size_t)p.nq_pad * p.nchunk * p.r * 4, 256);
-  p.total = o;
+  p.total = plan_refine_tail(p, o);
   return p;
 }
 
@@ -2132,32 +2430,74 @@ size_t drt_ip_topk_workspace(int64_t nq, int64_t n, int32_t d, int32_t k) {
   return make_plan(nq, n, k).total;
 }
 
-int drt_ip_topk_bf16(const void* Q, int64_t nq, const void* P, int64_t n, int32_t d, int32_t k,
-                     int64_t id_offset, float* out_scores, int64_t* out_ids, int32_t* status,
-                     void* ws, size_t ws_bytes, void* stream) {
+}  // extern "C"
+
+namespace drt {
+
+static int launch_refine(RefineArgs& ra, hipStream_t s) {
+  if (ra.nq == 0) return DRT_OK;
+  const ProfPair pp = prof_begin(PROF_SELECT, s);
+  hipLaunchKernelGGL(refine_delta_kernel, dim3((unsigned)ra.nq, (unsigned)((ra.kc + kRefSlice - 1) / kRefSlice)),
+                     dim3(kRefThreads), 0, s, ra);
+  hipLaunchKernelGGL(refine_sort_kernel, dim3((unsigned)ra.nq), dim3(kRefSortThreads), 0, s, ra);
+  prof_end(pp, s);
+  return hip_status(hipGetLastError());
+}
+
+// One shard's top-k (drt_ip_topk_bf16); with row statistics (stats != NULL) the result is put in
+// the canonical exact-score order (refine stage above): the select keeps kc >= k candidates in the
+// workspace and the refine kernels write the k outputs.
+static int ip_topk_impl(const void* Q, int64_t nq, const void* P, int64_t n, int32_t d, int32_t k,
+                        int64_t id_offset, float* out_scores, int64_t* out_ids, int32_t* status, void* ws,
+                        size_t ws_bytes, const float* stats, hipStream_t s) {
   DRT_REQUIRE(valid_dims(nq, n, d, k));
   if (nq == 0) return DRT_OK;
   DRT_REQUIRE(Q && out_scores && out_ids && ws);
   const TopkPlan p = make_plan(nq, n, k);
   DRT_REQUIRE(ws_bytes >= p.total);
-  hipStream_t s = (hipStream_t)stream;
   char* w = (char*)ws;
   float* tau = (float*)(w + p.off_tau);
   uint32_t* cnt = (uint32_t*)(w + p.off_cnt);
+  const bool refine = stats != nullptr && n > 0;
+
+  SelectArgs sa{};
+  sa.k = k;
+  sa.nq = nq;
+  sa.out_scores = out_scores;
+  sa.out_ids = out_ids;
+  sa.ldo = k;
+  sa.id_offset = id_offset;
+  sa.status = status;
+  if (refine) {   // kc candidates into the workspace, certified at k
+    sa.k = (int)p.kc;
+    sa.k_cert = k;
+    sa.out_scores = (float*)(w + p.off_cs);
+    sa.out_ids = (int64_t*)(w + p.off_ci);
+    sa.ldo = p.kc;
+  }
+  RefineArgs ra{};
+  ra.Q = (const __bf16*)Q;
+  ra.nq = nq;
+  ra.d = d;
+  ra.P = (const __bf16*)P;
+  ra.n_local = n;
+  ra.row_offset = id_offset;
+  ra.cs = (const float*)(w + p.off_cs);
+  ra.ci = (const int64_t*)(w + p.off_ci);
+  ra.kc = (int32_t)p.kc;
+  ra.k = k;
+  ra.stats = stats;
+  ra.delta = (float*)(w + p.off_delta);
+  ra.cnt = (int32_t*)(w + p.off_rcnt);
+  ra.status = status;
+  ra.out_s = out_scores;
+  ra.out_i = out_ids;
 
   if (n == 0) {
-    SelectArgs sa{};
     sa.in = w + p.off_keys;
     sa.in_stride = p.cap;
     sa.n_in = 0;
     sa.n_total = 0;
-    sa.k = k;
-    sa.nq = nq;
-    sa.out_scores = out_scores;
-    sa.out_ids = out_ids;
-    sa.ldo = k;
-    sa.id_offset = id_offset;
-    sa.status = status;
     return launch_select(sa, SEL_DENSE32, SEL_TOPK, s);
   }
   DRT_REQUIRE(P != nullptr);
@@ -2178,19 +2518,14 @@ int drt_ip_topk_bf16(const void* Q, int64_t nq, const void* P, int64_t n, int32_
     a.cap = p.cap;
     int rc = launch_scan(a, d, SCAN_DENSE, s, PROF_SCAN);
     if (rc) return rc;
-    SelectArgs sa{};
     sa.in = w + p.off_keys;
     sa.in_stride = p.cap;
     sa.n_in = n;
     sa.n_total = n;
-    sa.k = k;
-    sa.nq = nq;
-    sa.out_scores = out_scores;
-    sa.out_ids = out_ids;
-    sa.ldo = k;
-    sa.id_offset = id_offset;
-    sa.status = status;
-    return launch_select(sa, SEL_DENSE32, SEL_TOPK, s);
+    rc = launch_select(sa, SEL_DENSE32, SEL_TOPK, s);
+    if (rc || !refine) return rc;
+    ra.tau = nullptr;   // every row was scored
+    return launch_refine(ra, s);
   }
 
   // 1. sample pass -> tau
@@ -2218,7 +2553,7 @@ int drt_ip_topk_bf16(const void* Q, int64_t nq, const void* P, int64_t n, int32_
     DRT_CHECK_HIP(hipGetLastError());
   }
 
-  // 2. filter pass (counters zeroed by kth_final above: one launch fewer than a memset)
+  // 2. filter pass (counters zeroed by the threshold kernel above: one launch fewer than a memset)
   a.row0 = 0;
   a.nrows = n;
   a.rstride = 1;
@@ -2229,21 +2564,100 @@ int drt_ip_topk_bf16(const void* Q, int64_t nq, const void* P, int64_t n, int32_
   rc = launch_scan(a, d, SCAN_FILTER, s, PROF_SCAN);
   if (rc) return rc;
 
-  // 3. select + certify
-  SelectArgs sa{};
+  // 3. select + certify (4. canonical order)
   sa.in = w + p.off_keys;
   sa.in_stride = p.cap;
   sa.counts = cnt;
   sa.cap = p.cap;
   sa.n_total = n;
-  sa.k = k;
-  sa.nq = nq;
-  sa.out_scores = out_scores;
-  sa.out_ids = out_ids;
-  sa.ldo = k;
-  sa.id_offset = id_offset;
-  sa.status = status;
-  return launch_select(sa, SEL_KEYS64, SEL_TOPK, s);
+  rc = launch_select(sa, SEL_KEYS64, SEL_TOPK, s);
+  if (rc || !refine) return rc;
+  ra.tau = tau;
+  return launch_refine(ra, s);
+}
+
+}  // namespace drt
+
+extern "C" {
+
+int drt_ip_topk_bf16(const void* Q, int64_t nq, const void* P, int64_t n, int32_t d, int32_t k,
+                     int64_t id_offset, float* out_scores, int64_t* out_ids, int32_t* status,
+                     void* ws, size_t ws_bytes, void* stream) {
+  return ip_topk_impl(Q, nq, P, n, d, k, id_offset, out_scores, out_ids, status, ws, ws_bytes, nullptr,
+                      (hipStream_t)stream);
+}
+
+int drt_ip_topk_exact_bf16(const void* Q, int64_t nq, const void* P, int64_t n, int32_t d, int32_t k,
+                           int64_t id_offset, const float* stats, float* out_scores, int64_t* out_ids,
+                           int32_t* status, void* ws, size_t ws_bytes, void* stream) {
+  DRT_REQUIRE(stats != nullptr);
+  return ip_topk_impl(Q, nq, P, n, d, k, id_offset, out_scores, out_ids, status, ws, ws_bytes, stats,
+                      (hipStream_t)stream);
+}
+
+int drt_row_stats_bf16(const void* P, int64_t n, int32_t d, float* stats, int32_t accumulate, void* stream) {
+  DRT_REQUIRE(n >= 0 && d > 0 && d % 4 == 0 && stats != nullptr);
+  hipStream_t s = (hipStream_t)stream;
+  if (!accumulate) hipLaunchKernelGGL(row_stats_init_kernel, dim3(1), dim3(1), 0, s, (uint32_t*)stats);
+  if (n > 0) {
+    DRT_REQUIRE(P != nullptr);
+    const int64_t blocks = std::min<int64_t>((n + 3) / 4, 4096);
+    hipLaunchKernelGGL(row_stats_kernel, dim3((unsigned)blocks), dim3(256), 0, s, (const __bf16*)P, n, d,
+                       (uint32_t*)stats);
+  }
+  return hip_status(hipGetLastError());
+}
+
+int32_t drt_refine_width(int32_t k) {
+  if (k < 1 || k > kSelMaxK) return -1;
+  return (int32_t)refine_width(k);
+}
+
+int drt_refine_delta_bf16(const void* Q, int64_t nq, int32_t d, const void* P, int64_t n_local, int64_t row_offset,
+                          const float* cand_s, const int64_t* cand_i, int32_t kc, int32_t k, const float* stats,
+                          const float* tau, float* delta, int32_t* cnt, int32_t* status, void* stream) {
+  DRT_REQUIRE(nq >= 0 && d > 0 && d % 64 == 0 && d <= 1024 && k >= 1 && kc >= k && kc <= kSelMaxK && n_local >= 0);
+  if (nq == 0) return DRT_OK;
+  DRT_REQUIRE(Q && cand_s && cand_i && stats && delta && cnt && (P || n_local == 0));
+  RefineArgs ra{};
+  ra.Q = (const __bf16*)Q;
+  ra.nq = nq;
+  ra.d = d;
+  ra.P = (const __bf16*)P;
+  ra.n_local = n_local;
+  ra.row_offset = row_offset;
+  ra.cs = cand_s;
+  ra.ci = cand_i;
+  ra.kc = kc;
+  ra.k = k;
+  ra.stats = stats;
+  ra.tau = tau;
+  ra.delta = delta;
+  ra.cnt = cnt;
+  ra.status = status;
+  hipStream_t s = (hipStream_t)stream;
+  hipLaunchKernelGGL(refine_delta_kernel, dim3((unsigned)nq, (unsigned)((kc + kRefSlice - 1) / kRefSlice)),
+                     dim3(kRefThreads), 0, s, ra);
+  return hip_status(hipGetLastError());
+}
+
+int drt_refine_sort(const float* cand_s, const int64_t* cand_i, const float* delta, const int32_t* cnt, int64_t nq,
+                    int32_t kc, int32_t k, float* out_scores, int64_t* out_ids, void* stream) {
+  DRT_REQUIRE(nq >= 0 && k >= 1 && kc >= k && kc <= kSelMaxK);
+  if (nq == 0) return DRT_OK;
+  DRT_REQUIRE(cand_s && cand_i && delta && cnt && out_scores && out_ids);
+  RefineArgs ra{};
+  ra.nq = nq;
+  ra.cs = cand_s;
+  ra.ci = cand_i;
+  ra.kc = kc;
+  ra.k = k;
+  ra.delta = (float*)delta;
+  ra.cnt = (int32_t*)cnt;
+  ra.out_s = out_scores;
+  ra.out_i = out_ids;
+  hipLaunchKernelGGL(refine_sort_kernel, dim3((unsigned)nq), dim3(kRefSortThreads), 0, (hipStream_t)stream, ra);
+  return hip_status(hipGetLastError());
 }
 
 static int64_t resolve_width(int64_t n) { return align_up(std::max<int64_t>(n, 4), 4); }
@@ -2257,7 +2671,7 @@ static int64_t resolve_chunk(int64_t nbad, int64_t n) {
 
 static size_t resolve_ws_bytes(int64_t chunk, int64_t n, int32_t d) {
   return (size_t)(align_up(chunk * (int64_t)d * 2, 256) + align_up(chunk * resolve_width(n) * 4, 256) +
-                  align_up(chunk * 4, 256));
+                  align_up(chunk * 4, 256) + align_up(chunk * kSelMaxK * 16 + chunk * 4, 256));
 }
 
 size_t drt_ip_topk_resolve_workspace(int64_t nbad, int64_t n, int32_t d) {
@@ -2265,19 +2679,22 @@ size_t drt_ip_topk_resolve_workspace(int64_t nbad, int64_t n, int32_t d) {
   return resolve_ws_bytes(resolve_chunk(nbad, n), n, d);
 }
 
-int drt_ip_topk_resolve(const void* Q, int64_t nq, const void* P, int64_t n, int32_t d, int32_t k,
-                        int64_t id_offset, float* out_scores, int64_t* out_ids, int32_t* status,
-                        void* ws, size_t ws_bytes, int64_t* n_resolved, void* stream) {
+}  // extern "C"
+
+namespace drt {
+
+static int resolve_impl(const void* Q, int64_t nq, const void* P, int64_t n, int32_t d, int32_t k, int64_t id_offset,
+                        float* out_scores, int64_t* out_ids, int32_t* status, void* ws, size_t ws_bytes,
+                        int64_t* n_resolved, const float* stats, hipStream_t s) {
   DRT_REQUIRE(valid_dims(nq, n, d, k));
   if (n_resolved) *n_resolved = 0;
   if (nq == 0 || status == nullptr) return DRT_OK;
-  hipStream_t s = (hipStream_t)stream;
   std::vector<int32_t> st(nq);
   DRT_CHECK_HIP(hipMemcpyAsync(st.data(), status, nq * 4, hipMemcpyDeviceToHost, s));
   DRT_CHECK_HIP(hipStreamSynchronize(s));
   std::vector<int32_t> bad;
   for (int64_t i = 0; i < nq; ++i)
-    if (st[i] != 0) bad.push_back((int32_t)i);
+    if (st[i] & 1) bad.push_back((int32_t)i);
   if (bad.empty()) return DRT_OK;
   if (n_resolved) *n_resolved = (int64_t)bad.size();
 
@@ -2287,10 +2704,17 @@ int drt_ip_topk_resolve(const void* Q, int64_t nq, const void* P, int64_t n, int
   int64_t chunk = resolve_chunk((int64_t)bad.size(), n);
   while (chunk > 1 && resolve_ws_bytes(chunk, n, d) > ws_bytes) chunk >>= 1;
   DRT_REQUIRE(ws != nullptr && resolve_ws_bytes(chunk, n, d) <= ws_bytes);
+  const bool refine = stats != nullptr && n > 0;
+  const int64_t kc = refine_width(k);
   char* wp = (char*)ws;
   void* qbuf = wp;
   void* sbuf = wp + align_up(chunk * (int64_t)d * 2, 256);
   void* mbuf = (char*)sbuf + align_up(chunk * width * 4, 256);
+  char* rbuf = (char*)mbuf + align_up(chunk * 4, 256);   // refine: [chunk][kc] scores, ids, deltas; [chunk] cnt
+  float* rcs = (float*)rbuf;
+  int64_t* rci = (int64_t*)(rbuf + chunk * kc * 4);
+  float* rdl = (float*)(rbuf + chunk * kc * 12);
+  int32_t* rcn = (int32_t*)(rbuf + chunk * kc * 16);
   int rc = DRT_OK;
   hipError_t e;
   for (size_t b0 = 0; b0 < bad.size() && rc == DRT_OK; b0 += chunk) {
@@ -2331,12 +2755,64 @@ int drt_ip_topk_resolve(const void* Q, int64_t nq, const void* P, int64_t n, int
     sa.id_offset = id_offset;
     sa.status = status;
     sa.qmap = (const int32_t*)mbuf;
+    if (refine) {   // kc candidates of the chunk, then the canonical order into the caller's rows
+      sa.k = (int)kc;
+      sa.k_cert = k;
+      sa.out_scores = rcs;
+      sa.out_ids = rci;
+      sa.ldo = kc;
+      sa.status = nullptr;
+      sa.qmap = nullptr;
+    }
     rc = launch_select(sa, SEL_DENSE32, SEL_TOPK, s);
     if (rc) break;
+    if (refine) {
+      RefineArgs ra{};
+      ra.Q = (const __bf16*)qbuf;
+      ra.nq = nb;
+      ra.d = d;
+      ra.P = (const __bf16*)P;
+      ra.n_local = n;
+      ra.row_offset = id_offset;
+      ra.cs = rcs;
+      ra.ci = rci;
+      ra.kc = (int32_t)kc;
+      ra.k = k;
+      ra.stats = stats;
+      ra.tau = nullptr;
+      ra.delta = rdl;
+      ra.cnt = rcn;
+      ra.status = status;
+      ra.qmap = (const int32_t*)mbuf;
+      ra.set_status = true;
+      ra.out_s = out_scores;
+      ra.out_i = out_ids;
+      rc = launch_refine(ra, s);
+      if (rc) break;
+    }
     if ((e = hipStreamSynchronize(s)) != hipSuccess) { rc = (int)e; break; }
   }
   const hipError_t se = hipStreamSynchronize(s);
   return rc != DRT_OK ? rc : (se == hipSuccess ? DRT_OK : (int)se);
+}
+
+}  // namespace drt
+
+extern "C" {
+
+int drt_ip_topk_resolve(const void* Q, int64_t nq, const void* P, int64_t n, int32_t d, int32_t k,
+                        int64_t id_offset, float* out_scores, int64_t* out_ids, int32_t* status,
+                        void* ws, size_t ws_bytes, int64_t* n_resolved, void* stream) {
+  return resolve_impl(Q, nq, P, n, d, k, id_offset, out_scores, out_ids, status, ws, ws_bytes, n_resolved, nullptr,
+                      (hipStream_t)stream);
+}
+
+int drt_ip_topk_resolve_exact(const void* Q, int64_t nq, const void* P, int64_t n, int32_t d, int32_t k,
+                              int64_t id_offset, const float* stats, float* out_scores, int64_t* out_ids,
+                              int32_t* status, void* ws, size_t ws_bytes, int64_t* n_resolved, void* stream) {
+  DRT_REQUIRE(stats != nullptr);
+  return resolve_impl(Q, nq, P, n, d, k, id_offset, out_scores, out_ids, status, ws, ws_bytes, n_resolved, stats,
+                      (hipStream_t)stream);
 }
 
 int drt_topk_merge(const float* scores, const int64_t* ids, int64_t nq, int32_t nparts, int32_t k_in,
@@ -2538,7 +3014,14 @@ int drt_ip_topk_dist_filter_lists_at(const void* Q, int64_t nq, const void* P, i
 
 int drt_topk_merge_packed(const uint64_t* parts, int64_t nq, int32_t nparts, int32_t k, int64_t n_global,
                           float* out_scores, int64_t* out_ids, int32_t* status, void* stream) {
-  DRT_REQUIRE(nq >= 0 && nparts >= 1 && nparts <= 4096 && k >= 1 && k <= kSelMaxK && n_global >= 0);
+  return drt_topk_merge_packed_cert(parts, nq, nparts, k, k, n_global, out_scores, out_ids, status, stream);
+}
+
+int drt_topk_merge_packed_cert(const uint64_t* parts, int64_t nq, int32_t nparts, int32_t k, int32_t k_cert,
+                               int64_t n_global, float* out_scores, int64_t* out_ids, int32_t* status,
+                               void* stream) {
+  DRT_REQUIRE(nq >= 0 && nparts >= 1 && nparts <= 4096 && k >= 1 && k <= kSelMaxK && n_global >= 0 &&
+              k_cert >= 1 && k_cert <= k);
   if (nq == 0) return DRT_OK;
   DRT_REQUIRE(parts && out_scores && out_ids);
   hipStream_t s = (hipStream_t)stream;
@@ -2560,7 +3043,7 @@ int drt_topk_merge_packed(const uint64_t* parts, int64_t nq, int32_t nparts, int
       attr_set = true;
     }
     hipLaunchKernelGGL(merge_packed_count_kernel, dim3((unsigned)nq), dim3(kCntThreads), cnt_lds, s, parts, nq,
-                       (int)nparts, (int)k, n_global, out_scores, out_ids, status);
+                       (int)nparts, (int)k, n_global, out_scores, out_ids, status, (int)k_cert);
   } else if (nparts > 1 && (p2 / 2) * kp <= kTreeMaxE * kTreeThreads && lds <= 128 * 1024) {
 #define DRT_TREE(KPV)                                                                                        \
   {                                                                                                          \
@@ -2571,7 +3054,7 @@ int drt_topk_merge_packed(const uint64_t* parts, int64_t nq, int32_t nparts, int
       attr_set = true;                                                                                       \
     }                                                                                                        \
     hipLaunchKernelGGL(merge_packed_tree_kernel<KPV>, dim3((unsigned)nq), dim3(kTreeThreads), lds, s, parts,   \
-                       nq, (int)nparts, p2, (int)k, n_global, out_scores, out_ids, status);                  \
+                       nq, (int)nparts, p2, (int)k, n_global, out_scores, out_ids, status, (int)k_cert);     \
   }
     switch (kp) {
       case 64: DRT_TREE(64) break;
@@ -2584,7 +3067,7 @@ int drt_topk_merge_packed(const uint64_t* parts, int64_t nq, int32_t nparts, int
 #undef DRT_TREE
   } else {
     hipLaunchKernelGGL(merge_packed_kernel, dim3((unsigned)nq), dim3(512), 0, s, parts, nq, (int)nparts, (int)k,
-                       n_global, out_scores, out_ids, status);
+                       n_global, out_scores, out_ids, status, (int)k_cert);
   }
   prof_end(pp, s);
   rc = hip_status(hipGetLastError());

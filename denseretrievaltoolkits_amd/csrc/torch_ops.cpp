@@ -72,8 +72,17 @@ static void check_topk_outputs(const Tensor& q, int64_t nq, int64_t k, const Ten
                     "status: expected a contiguous int32 [", nq, "] tensor, got ", status.sizes());
 }
 
-void ip_topk_out(const Tensor& q_, const Tensor& p_, int64_t k, int64_t id_offset, Tensor& scores, Tensor& ids,
-                 Tensor& status) {
+// row statistics of the canonical-order stage: a [2] float tensor on p's device (drt_row_stats_bf16)
+static const float* stats_ptr(const c10::optional<Tensor>& stats, const Tensor& q) {
+  if (!stats.has_value()) return nullptr;
+  TORCH_CHECK_VALUE(stats->device() == q.device() && stats->scalar_type() == at::kFloat && stats->numel() == 2 &&
+                        stats->is_contiguous(),
+                    "stats: expected a contiguous float [2] tensor on ", q.device());
+  return stats->data_ptr<float>();
+}
+
+void ip_topk_out(const Tensor& q_, const Tensor& p_, int64_t k, int64_t id_offset, const c10::optional<Tensor>& stats,
+                 Tensor& scores, Tensor& ids, Tensor& status) {
   need(q_, "q", at::kBFloat16, 2);
   need(p_, "p", at::kBFloat16, 2);
   TORCH_CHECK_VALUE(q_.size(1) == p_.size(1), "q and p differ in dimension: ", q_.sizes(), " vs ", p_.sizes());
@@ -85,24 +94,33 @@ void ip_topk_out(const Tensor& q_, const Tensor& p_, int64_t k, int64_t id_offse
   TORCH_CHECK_VALUE(wsb > 0 || nq == 0, "unsupported ip_topk shape nq=", nq, " n=", n, " d=", d, " k=", k,
               " (d % 64 == 0, d <= 1024, 1 <= k <= 2048)");
   Tensor ws = workspace(q, wsb);
-  check_rc(drt_ip_topk_bf16(q.data_ptr(), nq, n ? p.data_ptr() : nullptr, n, (int32_t)d, (int32_t)k, id_offset,
-                            scores.data_ptr<float>(), ids.data_ptr<int64_t>(), status.data_ptr<int32_t>(),
-                            ws.data_ptr(), wsb, stream_of(q)),
-           "drt_ip_topk_bf16");
+  const float* sp = stats_ptr(stats, q);
+  if (sp) {
+    check_rc(drt_ip_topk_exact_bf16(q.data_ptr(), nq, n ? p.data_ptr() : nullptr, n, (int32_t)d, (int32_t)k,
+                                    id_offset, sp, scores.data_ptr<float>(), ids.data_ptr<int64_t>(),
+                                    status.data_ptr<int32_t>(), ws.data_ptr(), wsb, stream_of(q)),
+             "drt_ip_topk_exact_bf16");
+  } else {
+    check_rc(drt_ip_topk_bf16(q.data_ptr(), nq, n ? p.data_ptr() : nullptr, n, (int32_t)d, (int32_t)k, id_offset,
+                              scores.data_ptr<float>(), ids.data_ptr<int64_t>(), status.data_ptr<int32_t>(),
+                              ws.data_ptr(), wsb, stream_of(q)),
+             "drt_ip_topk_bf16");
+  }
 }
 
-std::tuple<Tensor, Tensor, Tensor> ip_topk(const Tensor& q, const Tensor& p, int64_t k, int64_t id_offset) {
+std::tuple<Tensor, Tensor, Tensor> ip_topk(const Tensor& q, const Tensor& p, int64_t k, int64_t id_offset,
+                                           const c10::optional<Tensor>& stats) {
   need_gpu(q, "q");
   const int64_t nq = q.size(0);
   Tensor s = at::empty({nq, k}, q.options().dtype(at::kFloat));
   Tensor i = at::empty({nq, k}, q.options().dtype(at::kLong));
   Tensor st = at::empty({nq}, q.options().dtype(at::kInt));
-  ip_topk_out(q, p, k, id_offset, s, i, st);
+  ip_topk_out(q, p, k, id_offset, stats, s, i, st);
   return {s, i, st};
 }
 
 int64_t ip_topk_resolve(const Tensor& q_, const Tensor& p_, int64_t k, int64_t id_offset, Tensor& scores,
-                        Tensor& ids, Tensor& status) {
+                        Tensor& ids, Tensor& status, const c10::optional<Tensor>& stats) {
   need(q_, "q", at::kBFloat16, 2);
   need(p_, "p", at::kBFloat16, 2);
   const c10::DeviceGuard g(q_.device());
@@ -113,16 +131,94 @@ int64_t ip_topk_resolve(const Tensor& q_, const Tensor& p_, int64_t k, int64_t i
   TORCH_CHECK_VALUE(k >= 1 && k <= 2048, "unsupported k=", k);
   check_topk_outputs(q, nq, k, scores, ids, status);
   if (nq == 0) return 0;
-  const int64_t nbad = status.ne(0).sum().item<int64_t>();   // synchronises, like the C entry
+  // bit 0 = not certified (bit 1, order not certified, cannot be improved by a rescan)
+  const int64_t nbad = status.bitwise_and(1).ne(0).sum().item<int64_t>();   // synchronises, like the C entry
   if (nbad == 0) return 0;
   const size_t wsb = drt_ip_topk_resolve_workspace(nbad, n, (int32_t)d);
   Tensor ws = workspace(q, wsb);
   int64_t nres = 0;
-  check_rc(drt_ip_topk_resolve(q.data_ptr(), nq, n ? p.data_ptr() : nullptr, n, (int32_t)d, (int32_t)k, id_offset,
-                               scores.data_ptr<float>(), ids.data_ptr<int64_t>(), status.data_ptr<int32_t>(),
-                               ws.data_ptr(), wsb, &nres, stream_of(q)),
-           "drt_ip_topk_resolve");
+  const float* sp = stats_ptr(stats, q);
+  if (sp) {
+    check_rc(drt_ip_topk_resolve_exact(q.data_ptr(), nq, n ? p.data_ptr() : nullptr, n, (int32_t)d, (int32_t)k,
+                                       id_offset, sp, scores.data_ptr<float>(), ids.data_ptr<int64_t>(),
+                                       status.data_ptr<int32_t>(), ws.data_ptr(), wsb, &nres, stream_of(q)),
+             "drt_ip_topk_resolve_exact");
+  } else {
+    check_rc(drt_ip_topk_resolve(q.data_ptr(), nq, n ? p.data_ptr() : nullptr, n, (int32_t)d, (int32_t)k,
+                                 id_offset, scores.data_ptr<float>(), ids.data_ptr<int64_t>(),
+                                 status.data_ptr<int32_t>(), ws.data_ptr(), wsb, &nres, stream_of(q)),
+             "drt_ip_topk_resolve");
+  }
   return nres;
+}
+
+// row statistics of p (+ those of earlier rows in `prev`, appended rows)
+Tensor row_stats(const Tensor& p_, const c10::optional<Tensor>& prev) {
+  need(p_, "p", at::kBFloat16, 2);
+  const c10::DeviceGuard g(p_.device());
+  const Tensor p = p_.contiguous();
+  Tensor st;
+  if (prev.has_value()) {
+    stats_ptr(prev, p);
+    st = prev->clone();
+  } else {
+    st = at::empty({2}, p.options().dtype(at::kFloat));
+  }
+  check_rc(drt_row_stats_bf16(p.size(0) ? p.data_ptr() : nullptr, p.size(0), (int32_t)p.size(1),
+                              st.data_ptr<float>(), prev.has_value() ? 1 : 0, stream_of(p)),
+           "drt_row_stats_bf16");
+  return st;
+}
+
+// canonical-order stage on a candidate list [nq, kc] (drt_refine_delta_bf16); status updated in place
+std::tuple<Tensor, Tensor> refine_delta(const Tensor& q_, const Tensor& p_, int64_t row_offset, const Tensor& cs_,
+                                        const Tensor& ci_, int64_t k, const Tensor& stats,
+                                        const c10::optional<Tensor>& tau_, Tensor& status) {
+  need(q_, "q", at::kBFloat16, 2);
+  need(p_, "p", at::kBFloat16, 2);
+  need(cs_, "cand_scores", at::kFloat, 2);
+  need(ci_, "cand_ids", at::kLong, 2);
+  need(status, "status", at::kInt, 1);
+  const c10::DeviceGuard g(q_.device());
+  const Tensor q = q_.contiguous(), p = p_.contiguous(), cs = cs_.contiguous(), ci = ci_.contiguous();
+  const int64_t nq = q.size(0), kc = cs.size(1);
+  TORCH_CHECK_VALUE(ci.sizes() == cs.sizes() && cs.size(0) == nq, "candidates must be [nq, kc] like q");
+  TORCH_CHECK_VALUE(status.is_contiguous() && status.size(0) == nq, "status must be a contiguous [nq] tensor");
+  Tensor tau;
+  if (tau_.has_value()) {
+    need(*tau_, "tau", at::kFloat, 1);
+    tau = tau_->contiguous();
+    TORCH_CHECK_VALUE(tau.size(0) == nq, "tau must hold one threshold per query");
+  }
+  Tensor delta = at::empty({nq, kc}, cs.options());
+  Tensor cnt = at::empty({nq}, cs.options().dtype(at::kInt));
+  check_rc(drt_refine_delta_bf16(q.data_ptr(), nq, (int32_t)q.size(1), p.size(0) ? p.data_ptr() : nullptr, p.size(0),
+                                 row_offset, cs.data_ptr<float>(), ci.data_ptr<int64_t>(), (int32_t)kc, (int32_t)k,
+                                 stats_ptr(stats, q), tau.defined() ? tau.data_ptr<float>() : nullptr,
+                                 delta.data_ptr<float>(), cnt.data_ptr<int32_t>(), status.data_ptr<int32_t>(),
+                                 stream_of(q)),
+           "drt_refine_delta_bf16");
+  return {delta, cnt};
+}
+
+std::tuple<Tensor, Tensor> refine_sort(const Tensor& cs_, const Tensor& ci_, const Tensor& delta_, const Tensor& cnt_,
+                                       int64_t k) {
+  need(cs_, "cand_scores", at::kFloat, 2);
+  need(ci_, "cand_ids", at::kLong, 2);
+  need(delta_, "delta", at::kFloat, 2);
+  need(cnt_, "cnt", at::kInt, 1);
+  const c10::DeviceGuard g(cs_.device());
+  const Tensor cs = cs_.contiguous(), ci = ci_.contiguous(), delta = delta_.contiguous(), cnt = cnt_.contiguous();
+  const int64_t nq = cs.size(0), kc = cs.size(1);
+  TORCH_CHECK_VALUE(ci.sizes() == cs.sizes() && delta.sizes() == cs.sizes() && cnt.size(0) == nq,
+                    "refine_sort: candidate, delta and cnt shapes disagree");
+  Tensor os = at::empty({nq, k}, cs.options());
+  Tensor oi = at::empty({nq, k}, ci.options());
+  check_rc(drt_refine_sort(cs.data_ptr<float>(), ci.data_ptr<int64_t>(), delta.data_ptr<float>(),
+                           cnt.data_ptr<int32_t>(), nq, (int32_t)kc, (int32_t)k, os.data_ptr<float>(),
+                           oi.data_ptr<int64_t>(), stream_of(cs)),
+           "drt_refine_sort");
+  return {os, oi};
 }
 
 std::tuple<Tensor, Tensor> topk_merge(const Tensor& scores_, const Tensor& ids_, int64_t k_out) {
@@ -260,7 +356,7 @@ void dist_filter_lists_into(const Tensor& q_, const Tensor& p_, int64_t n_global
            "drt_ip_topk_dist_filter_lists_at");
 }
 
-std::tuple<Tensor, Tensor, Tensor> merge_packed(const Tensor& parts_, int64_t k, int64_t n_global) {
+std::tuple<Tensor, Tensor, Tensor> merge_packed(const Tensor& parts_, int64_t k, int64_t n_global, int64_t k_cert) {
   need(parts_, "parts", at::kLong, 3);
   TORCH_CHECK_VALUE(parts_.size(2) == k + 1, "merge_packed expects [nparts, nq, k + 1]");
   const c10::DeviceGuard g(parts_.device());
@@ -269,10 +365,10 @@ std::tuple<Tensor, Tensor, Tensor> merge_packed(const Tensor& parts_, int64_t k,
   Tensor s = at::empty({nq, k}, parts.options().dtype(at::kFloat));
   Tensor i = at::empty({nq, k}, parts.options().dtype(at::kLong));
   Tensor st = at::empty({nq}, parts.options().dtype(at::kInt));
-  check_rc(drt_topk_merge_packed((const uint64_t*)parts.data_ptr<int64_t>(), nq, (int32_t)parts.size(0), (int32_t)k,
-                                 n_global, s.data_ptr<float>(), i.data_ptr<int64_t>(), st.data_ptr<int32_t>(),
-                                 stream_of(parts)),
-           "drt_topk_merge_packed");
+  check_rc(drt_topk_merge_packed_cert((const uint64_t*)parts.data_ptr<int64_t>(), nq, (int32_t)parts.size(0),
+                                      (int32_t)k, (int32_t)(k_cert > 0 ? k_cert : k), n_global, s.data_ptr<float>(),
+                                      i.data_ptr<int64_t>(), st.data_ptr<int32_t>(), stream_of(parts)),
+           "drt_topk_merge_packed_cert");
   return {s, i, st};
 }
 
@@ -425,11 +521,15 @@ Tensor l2_normalize(const Tensor& x_) {
 }  // namespace
 
 TORCH_LIBRARY(drt, m) {
-  m.def("ip_topk(Tensor q, Tensor p, int k, int id_offset=0) -> (Tensor, Tensor, Tensor)");
-  m.def("ip_topk.out(Tensor q, Tensor p, int k, int id_offset, *, Tensor(a!) scores, Tensor(b!) ids, "
-        "Tensor(c!) status) -> ()");
+  m.def("ip_topk(Tensor q, Tensor p, int k, int id_offset=0, Tensor? stats=None) -> (Tensor, Tensor, Tensor)");
+  m.def("ip_topk.out(Tensor q, Tensor p, int k, int id_offset, Tensor? stats=None, *, Tensor(a!) scores, "
+        "Tensor(b!) ids, Tensor(c!) status) -> ()");
   m.def("ip_topk_resolve(Tensor q, Tensor p, int k, int id_offset, Tensor(a!) scores, Tensor(b!) ids, "
-        "Tensor(c!) status) -> int");
+        "Tensor(c!) status, Tensor? stats=None) -> int");
+  m.def("row_stats(Tensor p, Tensor? prev=None) -> Tensor");
+  m.def("refine_delta(Tensor q, Tensor p, int row_offset, Tensor cand_scores, Tensor cand_ids, int k, Tensor stats, "
+        "Tensor? tau, Tensor(a!) status) -> (Tensor, Tensor)");
+  m.def("refine_sort(Tensor cand_scores, Tensor cand_ids, Tensor delta, Tensor cnt, int k) -> (Tensor, Tensor)");
   m.def("topk_merge(Tensor scores, Tensor ids, int k_out) -> (Tensor, Tensor)");
   m.def("dist_sample(Tensor q, Tensor p, int n_global, int k) -> Tensor");
   m.def("dist_tau(Tensor lists, int k) -> Tensor");
@@ -438,7 +538,7 @@ TORCH_LIBRARY(drt, m) {
   m.def("dist_filter_lists_into(Tensor q, Tensor p, int n_global, int k, int id_offset, Tensor lists, int q0, "
         "Tensor(a!) packed) -> ()");
   m.def("dist_filter_into(Tensor q, Tensor p, int n_global, int k, int id_offset, Tensor tau, Tensor(a!) packed) -> ()");
-  m.def("merge_packed(Tensor parts, int k, int n_global) -> (Tensor, Tensor, Tensor)");
+  m.def("merge_packed(Tensor parts, int k, int n_global, int k_cert=-1) -> (Tensor, Tensor, Tensor)");
   m.def("score_ce_fwd(Tensor q, Tensor p, int target_stride, float scale) -> (Tensor, Tensor, Tensor)");
   m.def("score_ce_bwd(Tensor grad, Tensor q, Tensor p, Tensor scores, Tensor lse, int target_stride, "
         "float scale) -> (Tensor, Tensor)");
@@ -455,6 +555,9 @@ TORCH_LIBRARY_IMPL(drt, CUDA, m) {   // the GPU dispatch key of torch-ROCm
   m.impl("ip_topk", &ip_topk);
   m.impl("ip_topk.out", &ip_topk_out);
   m.impl("ip_topk_resolve", &ip_topk_resolve);
+  m.impl("row_stats", &row_stats);
+  m.impl("refine_delta", &refine_delta);
+  m.impl("refine_sort", &refine_sort);
   m.impl("topk_merge", &topk_merge);
   m.impl("dist_sample", &dist_sample);
   m.impl("dist_tau", &dist_tau);

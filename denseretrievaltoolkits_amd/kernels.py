@@ -26,13 +26,17 @@ def ip_topk_workspace_bytes(nq: int, n: int, d: int, k: int) -> int:
 
 def ip_topk(q: torch.Tensor, p: torch.Tensor, k: int, id_offset: int = 0, resolve: bool = True,
             out: Optional[Tuple[torch.Tensor, torch.Tensor]] = None,
-            status: Optional[torch.Tensor] = None) -> Tuple[torch.Tensor, torch.Tensor, torch.Tensor]:
+            status: Optional[torch.Tensor] = None,
+            stats: Optional[torch.Tensor] = None) -> Tuple[torch.Tensor, torch.Tensor, torch.Tensor]:
     """Exact inner-product top-k of `q` [nq, d] against corpus shard `p` [n, d] (bf16).
 
     Returns (scores fp32 [nq, k], ids int64 [nq, k], status int32 [nq]) ordered by
-    (score desc, id asc); ids are ``id_offset + row``.  With ``resolve`` the
-    (rare) uncertified queries are recomputed exactly before returning (this
-    synchronises the stream); without it the caller must inspect ``status``.
+    (score desc, id asc); ids are ``id_offset + row``.  With ``stats`` (row_stats(p)) the order
+    is the canonical one of the EXACT scores (fp64 sums of the bf16 products, what an fp64
+    evaluator returns; scores = those sums rounded to fp32); without it, the fp32 scan's.
+    status bit 0: not certified -- with ``resolve`` such queries are recomputed exactly before
+    returning (this synchronises the stream), without it the caller must; bit 1: the exact order
+    could not be certified (massive near-ties; that query keeps the fp32 order).
     """
     drt = ops.load()
     _require_device(q, p)
@@ -45,28 +49,60 @@ def ip_topk(q: torch.Tensor, p: torch.Tensor, k: int, id_offset: int = 0, resolv
         raise ValueError(f"unsupported ip_topk shape nq={nq} n={p.shape[0]} d={d} k={k} "
                          "(d % 64 == 0, d <= 1024, 1 <= k <= 2048)")
     if out is None and status is None:
-        scores, ids, status = drt.ip_topk(q, p, k, id_offset)
+        scores, ids, status = drt.ip_topk(q, p, k, id_offset, stats)
     else:
         dev = q.device
         scores, ids = out if out is not None else (torch.empty((nq, k), dtype=torch.float32, device=dev),
                                                    torch.empty((nq, k), dtype=torch.int64, device=dev))
         if status is None:
             status = torch.empty((nq,), dtype=torch.int32, device=dev)
-        drt.ip_topk.out(q, p, k, id_offset, scores=scores, ids=ids, status=status)
+        drt.ip_topk.out(q, p, k, id_offset, stats, scores=scores, ids=ids, status=status)
     if resolve:
-        resolve_failed(q, p, k, id_offset, scores, ids, status)
+        resolve_failed(q, p, k, id_offset, scores, ids, status, stats=stats)
     return scores, ids, status
 
 
-def resolve_failed(q, p, k, id_offset, scores, ids, status, n_failed: Optional[int] = None) -> int:
-    """Exact dense rescan of every query whose status is non-zero (synchronous).
+def resolve_failed(q, p, k, id_offset, scores, ids, status, n_failed: Optional[int] = None,
+                   stats: Optional[torch.Tensor] = None) -> int:
+    """Exact dense rescan of every query whose status bit 0 is set (synchronous), in the canonical
+    order when ``stats`` is given.
 
     ``n_failed``: the caller's count of failed queries if it already read ``status`` back
     (then a zero count returns without touching the device); the dense-score workspace
     (up to ~2 GB per chunk) comes from torch's caching allocator inside the op."""
     if n_failed == 0 or q.shape[0] == 0:
         return 0
-    return int(ops.load().ip_topk_resolve(q, p, k, id_offset, scores, ids, status))
+    return int(ops.load().ip_topk_resolve(q, p, k, id_offset, scores, ids, status, stats))
+
+
+def row_stats(p: torch.Tensor, prev: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """[2] fp32 device tensor: (max squared row norm, 1.0 if every element is an integer) of the
+    bf16 rows p [n, d], combined with ``prev`` (the stats of earlier rows) when given."""
+    _require_device(p)
+    return ops.load().row_stats(p, prev)
+
+
+def refine_width(k: int) -> int:
+    """Candidates per query the canonical-order stage works on (k plus its near-tie window)."""
+    w = int(_native.load().drt_refine_width(k))
+    if w <= 0:
+        raise ValueError(f"unsupported k={k}")
+    return w
+
+
+def refine(q: torch.Tensor, p: torch.Tensor, row_offset: int, cand_s: torch.Tensor, cand_i: torch.Tensor, k: int,
+           stats: torch.Tensor, tau: Optional[torch.Tensor], status: torch.Tensor, all_reduce_sum=None):
+    """Canonical exact-score order of candidate lists [nq, kc] (scores desc, global ids): exact
+    sums for the candidates whose rows this shard holds (global ids [row_offset, row_offset +
+    len(p))), combined across shards by ``all_reduce_sum`` (in place; None on one GPU), then the
+    top-k by (exact score desc, id asc).  ``status`` [nq] gains bit 0 (candidates below ``tau``
+    missing: redo exactly) / bit 1 (near-tie window wider than the list) in place."""
+    _require_device(q, p, cand_s, cand_i, stats, status)
+    drt = ops.load()
+    delta, cnt = drt.refine_delta(q, p, row_offset, cand_s, cand_i, k, stats, tau, status)
+    if all_reduce_sum is not None:
+        all_reduce_sum(delta)
+    return drt.refine_sort(cand_s, cand_i, delta, cnt, k)
 
 
 def topk_merge(scores: torch.Tensor, ids: torch.Tensor, k_out: int) -> Tuple[torch.Tensor, torch.Tensor]:
@@ -131,12 +167,13 @@ def dist_filter_lists_into(q: torch.Tensor, p: torch.Tensor, n_global: int, k: i
     ops.load().dist_filter_lists_into(q, p, n_global, k, id_offset, lists, q0, packed)
 
 
-def merge_packed(parts: torch.Tensor, k: int, n_global: int):
-    """[nparts, nq, k + 1] packed lists -> (scores [nq,k], ids [nq,k], status [nq] int32; 0 = exact)."""
+def merge_packed(parts: torch.Tensor, k: int, n_global: int, k_cert: int = -1):
+    """[nparts, nq, k + 1] packed lists -> (scores [nq,k], ids [nq,k], status [nq] int32; 0 = exact);
+    certified at ``k_cert`` <= k entries when given (the canonical-order stage merges wider lists)."""
     _require_device(parts)
     if parts.dim() != 3 or parts.shape[2] != k + 1:
         raise ValueError("merge_packed expects [nparts, nq, k + 1]")
-    return ops.load().merge_packed(parts, k, n_global)
+    return ops.load().merge_packed(parts, k, n_global, k_cert)
 
 
 def gemm_nt_f32(a: torch.Tensor, b: torch.Tensor, out: Optional[torch.Tensor] = None) -> torch.Tensor:

@@ -6,8 +6,9 @@ loads that library (no fallback: a missing library raises) and registers, per op
 fake (meta) implementation that torch.compile / FakeTensor tracing need, plus the autograd
 formula of the fused score + cross-entropy op.
 
-    torch.ops.drt.ip_topk(q, p, k, id_offset)          -> (scores, ids, status)   index.py:31-33
-    torch.ops.drt.ip_topk_resolve(q, p, k, off, s, i, st) -> n_resolved  (in place, synchronous)
+    torch.ops.drt.ip_topk(q, p, k, id_offset, stats)   -> (scores, ids, status)   index.py:31-33
+    torch.ops.drt.ip_topk_resolve(q, p, k, off, s, i, st, stats) -> n_resolved  (in place, synchronous)
+    torch.ops.drt.row_stats / refine_delta / refine_sort  (canonical exact-score order, include/drt.h)
     torch.ops.drt.topk_merge(scores, ids, k_out)        -> (scores, ids)           utils.py:215-229
     torch.ops.drt.dist_sample / dist_tau / dist_filter / dist_filter_lists / merge_packed  (sharded, §8e)
     torch.ops.drt.score_ce_fwd(q, p, stride, scale)     -> (loss, scores, lse)     biencoder.py:107-119
@@ -50,19 +51,33 @@ def _register_python_parts():
     lib = torch.library
 
     @lib.register_fake("drt::ip_topk")
-    def _(q, p, k, id_offset=0):
+    def _(q, p, k, id_offset=0, stats=None):
         nq = q.shape[0]
         return (q.new_empty((nq, k), dtype=torch.float32), q.new_empty((nq, k), dtype=torch.int64),
                 q.new_empty((nq,), dtype=torch.int32))
 
     @lib.register_fake("drt::ip_topk.out")
-    def _(q, p, k, id_offset, *, scores, ids, status):
+    def _(q, p, k, id_offset, stats=None, *, scores, ids, status):
         return None
 
     @lib.register_fake("drt::ip_topk_resolve")
-    def _(q, p, k, id_offset, scores, ids, status):
+    def _(q, p, k, id_offset, scores, ids, status, stats=None):
         # the count of rescanned queries is data-dependent (it reads the status back)
         return torch.library.get_ctx().new_dynamic_size()
+
+    @lib.register_fake("drt::row_stats")
+    def _(p, prev=None):
+        return p.new_empty((2,), dtype=torch.float32)
+
+    @lib.register_fake("drt::refine_delta")
+    def _(q, p, row_offset, cand_scores, cand_ids, k, stats, tau, status):
+        return cand_scores.new_empty(cand_scores.shape), cand_scores.new_empty((cand_scores.shape[0],),
+                                                                                 dtype=torch.int32)
+
+    @lib.register_fake("drt::refine_sort")
+    def _(cand_scores, cand_ids, delta, cnt, k):
+        nq = cand_scores.shape[0]
+        return cand_scores.new_empty((nq, k)), cand_ids.new_empty((nq, k))
 
     @lib.register_fake("drt::topk_merge")
     def _(scores, ids, k_out):
@@ -95,7 +110,7 @@ def _register_python_parts():
         return None
 
     @lib.register_fake("drt::merge_packed")
-    def _(parts, k, n_global):
+    def _(parts, k, n_global, k_cert=-1):
         nq = parts.shape[1]
         return (parts.new_empty((nq, k), dtype=torch.float32), parts.new_empty((nq, k), dtype=torch.int64),
                 parts.new_empty((nq,), dtype=torch.int32))

@@ -59,9 +59,22 @@ def _stage_status(st: torch.Tensor):
 
 
 def _status_failed(h: torch.Tensor, ev) -> int:
+    """Queries whose status bit 0 is set (not certified: redo exactly)."""
     if ev is not None:
         ev.synchronize()
-    return int((h != 0).sum().item())
+    return int(((h & 1) != 0).sum().item())
+
+
+def _order_uncertified(h: torch.Tensor) -> int:
+    """Queries whose status bit 1 is set (canonical order not certified: fp32 order kept)."""
+    return int(((h & 2) != 0).sum().item())
+
+
+# Canonical order (kernels.refine): results ranked by the EXACT inner products (fp64 sums of the
+# bf16 products, ties by ascending id) -- what an fp64 evaluator returns -- instead of by the
+# scan's fp32 sums.  Costs one gather of the ~k candidate rows per query (~1.3 % of a 10M-row
+# step).  False: the fp32 scan order (the bf16-product sums faiss-style, near-ties in MFMA order).
+EXACT_ORDER = True
 
 
 class _HostResult:
@@ -104,7 +117,8 @@ GROUP_QUERIES = 2048
 GROUP_MIN_ROWS = 1 << 62
 
 
-def _groups(batches, cap=GROUP_QUERIES):
+def _groups(batches, cap=None):
+    cap = GROUP_QUERIES if cap is None else cap
     grp, n = [], 0
     for q in batches:
         if grp and n + q.shape[0] > cap:
@@ -116,24 +130,30 @@ def _groups(batches, cap=GROUP_QUERIES):
         yield grp
 
 
-def _gtau_enqueue_group(local, qs, k: int, n_global: int, offset: int, gather, to_host: bool = False):
+def _gtau_enqueue_group(local, qs, k: int, n_global: int, offset: int, gather, to_host: bool = False,
+                        stats=None, all_reduce_sum=None):
     """One group of query batches through the global-threshold protocol (see ShardedFlatIP):
     ONE sample launch for all of the group's queries, one exchange of the sample lists, one
     threshold launch, one filter scan (+ select) per batch writing its packed top-k into a group buffer,
     one exchange of that buffer and one merge that certifies every query.  ``gather(t)`` ->
     [world, *t.shape] (identity stack on one GPU).  ``to_host``: the merged group's results are
-    also staged to pinned host memory behind the merge."""
+    also staged to pinned host memory behind the merge.  ``stats`` (the GLOBAL row statistics):
+    the shards keep kc = refine_width(k) candidates each, the merge keeps kc, and the canonical
+    stage (kernels.refine, deltas summed across shards by ``all_reduce_sum``) orders the top-k."""
     sizes = [q.shape[0] for q in qs]
     qg = qs[0] if len(qs) == 1 else torch.cat(qs)
     best = local.dist_sample(qg, n_global, k)                       # [Qg, r]
     lists = gather(best).contiguous()                               # [world, Qg, r]
     tau = kernels.dist_tau(lists, k)                                # [Qg]: one launch for the group
-    packed = torch.empty((qg.shape[0], k + 1), dtype=torch.int64, device=qg.device)
+    kc = kernels.refine_width(k) if stats is not None else k
+    packed = torch.empty((qg.shape[0], kc + 1), dtype=torch.int64, device=qg.device)
     o = 0
     for q, nb in zip(qs, sizes):
-        kernels.dist_filter_into(q, local.rows, n_global, k, offset, tau[o:o + nb], packed[o:o + nb])
+        kernels.dist_filter_into(q, local.rows, n_global, kc, offset, tau[o:o + nb], packed[o:o + nb])
         o += nb
-    s, i, st = kernels.merge_packed(gather(packed), k, n_global)
+    s, i, st = kernels.merge_packed(gather(packed), kc, n_global, k_cert=k)
+    if stats is not None:
+        s, i = kernels.refine(qg, local.rows, offset, s, i, k, stats, tau, st, all_reduce_sum)
     h, ev = _stage_status(st)
     host = _HostResult(s, i) if to_host else None
     return qs, sizes, s, i, h, ev, host
@@ -146,7 +166,7 @@ def _gtau_finish_group(pend, redo):
     qs, sizes, s, i, h, ev, host = pend
     if ev is not None:
         ev.synchronize()
-    bad = (h != 0)
+    bad = (h & 1) != 0
     res, o, nredo = [], 0, 0
     hs = hi = None
     for q, nb in zip(qs, sizes):
@@ -161,7 +181,7 @@ def _gtau_finish_group(pend, redo):
         else:
             res.append((s[o:o + nb], i[o:o + nb]))
         o += nb
-    return res, nredo
+    return res, nredo, _order_uncertified(h)
 
 
 class FlatIPIndex:
@@ -181,6 +201,9 @@ class FlatIPIndex:
         self._buf = torch.zeros((max(0, capacity), self.dp), dtype=torch.bfloat16, device=self.device)
         self.ntotal = 0
         self.metric = "inner_product"
+        self.exact_order = EXACT_ORDER
+        self._stats = None     # row statistics of rows [0, _stats_n) (kernels.row_stats)
+        self._stats_n = 0
 
     # faiss-compatible surface -----------------------------------------
     @property
@@ -213,6 +236,20 @@ class FlatIPIndex:
     def rows(self) -> torch.Tensor:
         return self._buf[: self.ntotal]
 
+    def row_stats(self) -> torch.Tensor:
+        """Row statistics of the canonical-order stage (one pass over rows added since the last call)."""
+        if self._stats is None or self._stats_n > self.ntotal:
+            self._stats = kernels.row_stats(self.rows)
+        elif self._stats_n < self.ntotal:
+            self._stats = kernels.row_stats(self.rows[self._stats_n:], prev=self._stats)
+        self._stats_n = self.ntotal
+        return self._stats
+
+    def _stats_arg(self):
+        return self.row_stats() if self.exact_order and self.ntotal > 0 else None
+
+    order_uncertified = 0   # queries whose canonical order could not be certified (fp32 order kept)
+
     @classmethod
     def from_rows(cls, rows: torch.Tensor) -> "FlatIPIndex":
         """Wrap an existing bf16 [n, d] device tensor as the index rows (no copy)."""
@@ -229,22 +266,25 @@ class FlatIPIndex:
 
     def _enqueue(self, q, k: int, id_offset: int = 0, out=None, to_host: bool = False):
         qd = self._queries(q)
-        s, i, st = kernels.ip_topk(qd, self.rows, k, id_offset=id_offset, resolve=False, out=out)
+        stats = self._stats_arg()
+        s, i, st = kernels.ip_topk(qd, self.rows, k, id_offset=id_offset, resolve=False, out=out, stats=stats)
         h, ev = _stage_status(st)
         host = _HostResult(s, i) if to_host else None
-        return qd, s, i, st, h, ev, id_offset, k, host
+        return qd, s, i, st, h, ev, id_offset, k, host, stats
 
     def _finish(self, pend):
-        qd, s, i, st, h, ev, off, k, host = pend
+        qd, s, i, st, h, ev, off, k, host, stats = pend
         nbad = _status_failed(h, ev)
+        self.order_uncertified += _order_uncertified(h)
         if nbad:
-            self.resolved += kernels.resolve_failed(qd, self.rows, k, off, s, i, st, n_failed=nbad)
+            self.resolved += kernels.resolve_failed(qd, self.rows, k, off, s, i, st, n_failed=nbad, stats=stats)
         if host is not None:
             return host.get(s, i, nbad > 0)
         return s, i
 
     def search_unresolved(self, q, k: int, id_offset: int = 0):
-        """(scores, ids, status) with status still on device (the per-shard protocol gathers it)."""
+        """(scores, ids, status) with status still on device (the per-shard protocol gathers it);
+        the fp32 scan order (the per-shard lists are merged by their fp32 scores)."""
         return kernels.ip_topk(self._queries(q), self.rows, k, id_offset=id_offset, resolve=False)
 
     def search_device(self, q, k: int, id_offset: int = 0) -> Tuple[torch.Tensor, torch.Tensor]:
@@ -278,12 +318,15 @@ class FlatIPIndex:
         groups = [[self._queries(q) for q in g] for g in _groups(batches)]
 
         def fin(pend):
-            res, nredo = _gtau_finish_group(pend, lambda q: self.search_device(q, k, id_offset))
+            res, nredo, nunc = _gtau_finish_group(pend, lambda q: self.search_device(q, k, id_offset))
             self.group_fallbacks += nredo
+            self.order_uncertified += nunc
             return res
 
+        stats = self._stats_arg()
         for res in _pipeline(groups, lambda j, g: _gtau_enqueue_group(self, g, k, self.ntotal, id_offset,
-                                                                      lambda t: t.unsqueeze(0), to_host), fin):
+                                                                      lambda t: t.unsqueeze(0), to_host,
+                                                                      stats=stats), fin):
             yield from res
 
     def search(self, q, k: int) -> Tuple[np.ndarray, np.ndarray]:
@@ -367,9 +410,11 @@ class ShardedFlatIP:
             raise ValueError(f"unknown protocol {protocol!r}")
         self.protocol = protocol
         self.fallbacks = 0   # batches the global-tau protocol could not certify
+        self.order_uncertified = 0   # queries left in the fp32 order (massive near-ties, per-shard path)
         self.d = d
         self.offset = 0      # global id of this shard's first row
         self.ntotal = 0      # rows over all shards
+        self.stats = None    # GLOBAL row statistics (max over shards), set by sync_offsets
 
     def add_shard(self, x) -> None:
         """Append rows to THIS rank's shard, then agree on the global id offsets (collective)."""
@@ -377,10 +422,22 @@ class ShardedFlatIP:
         self.sync_offsets()
 
     def sync_offsets(self):
+        """Agree on the shard offsets and the corpus-wide row statistics (collective)."""
         counts = comm.all_gather_sizes(self.local.ntotal, self.local.device, self.group) if self._multi() \
             else [int(self.local.ntotal)]
         self.offset = sum(counts[: self.rank])
         self.ntotal = sum(counts)
+        self.stats = None
+        if isinstance(self.local, FlatIPIndex) and self.local.exact_order:
+            st = self.local.row_stats() if self.local.ntotal > 0 else \
+                torch.tensor([0.0, 1.0], dtype=torch.float32, device=self.local.device)
+            if self._multi():
+                # max of the squared norms, AND of the integer flags (as a max of their negations)
+                st = st.clone()
+                st[1] = -st[1]
+                comm.all_reduce_max_(st, self.group)
+                st[1] = -st[1]
+            self.stats = st
         return counts
 
     def search_device(self, q, k: int) -> Tuple[torch.Tensor, torch.Tensor]:
@@ -403,14 +460,20 @@ class ShardedFlatIP:
                 and isinstance(self.local, FlatIPIndex):
             groups = [[self.local._queries(q) for q in g] for g in _groups(batches)]
 
+            def redo(q):
+                if self.stats is not None:   # the per-shard redo merges by fp32 scores
+                    self.order_uncertified += int(q.shape[0])
+                return self._finish(("pshard", q, k) + self._per_shard_enqueue(q, k))
+
             def fin(pend):
-                res, nredo = _gtau_finish_group(pend, lambda q: self._finish(
-                    ("pshard", q, k) + self._per_shard_enqueue(q, k)))
+                res, nredo, nunc = _gtau_finish_group(pend, redo)
                 self.fallbacks += nredo
+                self.order_uncertified += nunc
                 return res
 
-            for res in _pipeline(groups, lambda j, g: _gtau_enqueue_group(self.local, g, k, self.ntotal, self.offset,
-                                                                          self._all_gather, to_host), fin):
+            for res in _pipeline(groups, lambda j, g: _gtau_enqueue_group(
+                    self.local, g, k, self.ntotal, self.offset, self._all_gather, to_host, stats=self.stats,
+                    all_reduce_sum=lambda t: comm.all_reduce_sum_(t, self.group)), fin):
                 yield from res
             return
         for r in _pipeline(batches, lambda j, q: self._enqueue(q, k, to_host), self._finish):
@@ -432,6 +495,13 @@ class ShardedFlatIP:
                 return ("local", self.local._enqueue(q, k, self.offset, to_host=to_host))
             return ("done", self.local.search_device(q, k, id_offset=self.offset))
         if self.protocol == "global_tau" and self.ntotal < 0xFFFFFFFF:
+            if isinstance(self.local, FlatIPIndex):
+                # the HIP shard: one batch as a group of one (canonical order included)
+                qd = self.local._queries(q)
+                _, _, s, i, h, ev, _ = _gtau_enqueue_group(
+                    self.local, [qd], k, self.ntotal, self.offset, self._all_gather, stats=self.stats,
+                    all_reduce_sum=lambda t: comm.all_reduce_sum_(t, self.group))
+                return ("gtau", qd, k, s, i, h, ev)
             best = self.local.dist_sample(q, self.ntotal, k)                 # [nq, r] u32 keys
             lists = self._all_gather(best)                                   # [world, nq, r]
             if hasattr(self.local, "dist_filter_lists"):                     # tau + filter fused
@@ -465,8 +535,11 @@ class ShardedFlatIP:
         if kind == "gtau":
             _, q, k, s, i, h, ev = pend
             if _status_failed(h, ev) == 0:
+                self.order_uncertified += _order_uncertified(h)
                 return s, i
             self.fallbacks += 1
+            if self.stats is not None:   # the per-shard redo merges by fp32 scores
+                self.order_uncertified += int(q.shape[0])
             pend = ("pshard", q, k) + self._per_shard_enqueue(q, k)
         _, q, k, ms, mi, h, ev, s, i, st = pend
         if _status_failed(h, ev) == 0:

@@ -73,6 +73,44 @@ int drt_ip_topk_resolve(const void* Q, int64_t nq, const void* P, int64_t n, int
                         int32_t* status, void* workspace, size_t workspace_bytes,
                         int64_t* n_resolved, void* stream);
 
+/* ------------------------------------------------------------------------
+ * Canonical (exact-score) order  (the fp64 evaluator's answer)
+ * ------------------------------------------------------------------------
+ * The scan ranks rows by fp32 sums of the bf16 products; rows whose exact inner products lie
+ * within the fp32 summation error of each other (or of the k-th score) may come out in either
+ * order.  These entry points put a result in the order of the EXACT products (fp64 sums of the
+ * bf16 products, ties by ascending id), as an fp64 CPU evaluator (faiss's semantics without its
+ * rounding) ranks them, with scores = the exact sums rounded to fp32.
+ * drt_row_stats_bf16: stats[2] (device floats) = (max squared L2 norm over the rows, 1.0f while
+ *   every element is an integer); accumulate = 0 (re)initialises, 1 combines with the stats
+ *   already there (appended rows).  Across shards combine by max / min.  Reads every row once.
+ * drt_ip_topk_exact_bf16: drt_ip_topk_bf16 in the canonical order (same workspace).  status bit 0
+ *   as drt_ip_topk_bf16 (call drt_ip_topk_resolve_exact); bit 1 = more than
+ *   drt_refine_width(k) - k rows within the fp32 error of the k-th score (massive near-ties;
+ *   that query keeps the fp32 order).
+ * drt_ip_topk_resolve_exact: drt_ip_topk_resolve in the canonical order (status bit 0 only).
+ * drt_refine_delta_bf16 / drt_refine_sort: the stage alone, on a candidate list cand [nq][kc]
+ *   (scores desc, global ids, kc = drt_refine_width(k), e.g. a merged sharded result): delta =
+ *   exact - fp32 score for the candidates whose rows this shard holds (row_offset = global id of
+ *   its row 0; 0 elsewhere, so shards combine their deltas with one SUM all-reduce), cnt [nq] the
+ *   window per query; then the sort writes the top-k.  tau [nq] = the filter thresholds the
+ *   candidate list was collected with (NULL: every row was scored).                           */
+int drt_row_stats_bf16(const void* P, int64_t n, int32_t d, float* stats, int32_t accumulate, void* stream);
+int32_t drt_refine_width(int32_t k);
+int drt_ip_topk_exact_bf16(const void* Q, int64_t nq, const void* P, int64_t n, int32_t d, int32_t k,
+                           int64_t id_offset, const float* stats, float* out_scores, int64_t* out_ids,
+                           int32_t* status, void* workspace, size_t workspace_bytes, void* stream);
+int drt_ip_topk_resolve_exact(const void* Q, int64_t nq, const void* P, int64_t n, int32_t d, int32_t k,
+                              int64_t id_offset, const float* stats, float* out_scores, int64_t* out_ids,
+                              int32_t* status, void* workspace, size_t workspace_bytes, int64_t* n_resolved,
+                              void* stream);
+int drt_refine_delta_bf16(const void* Q, int64_t nq, int32_t d, const void* P, int64_t n_local,
+                          int64_t row_offset, const float* cand_s, const int64_t* cand_i, int32_t kc,
+                          int32_t k, const float* stats, const float* tau, float* delta, int32_t* cnt,
+                          int32_t* status, void* stream);
+int drt_refine_sort(const float* cand_s, const int64_t* cand_i, const float* delta, const int32_t* cnt,
+                    int64_t nq, int32_t kc, int32_t k, float* out_scores, int64_t* out_ids, void* stream);
+
 /* Merge `nparts` per-shard top-k lists into one global top-k.
  * scores/ids: [nparts, nq, k_in] (each part sorted score desc, id asc, as
  * drt_ip_topk_bf16 writes them); out: [nq, k_out], k_out <= k_in*nparts,
@@ -129,6 +167,12 @@ int drt_ip_topk_dist_filter_lists_at(const void* Q, int64_t nq, const void* P, i
 int drt_topk_merge_packed(const uint64_t* parts, int64_t nq, int32_t nparts, int32_t k,
                           int64_t n_global, float* out_scores, int64_t* out_ids, int32_t* status,
                           void* stream);
+/* The same merge of lists of k entries certified at k_cert <= k (status 1 when fewer than k_cert
+ * candidates exist overall or a shard overflowed): the canonical-order stage merges
+ * drt_refine_width(k_cert) entries per shard.                                                  */
+int drt_topk_merge_packed_cert(const uint64_t* parts, int64_t nq, int32_t nparts, int32_t k,
+                               int32_t k_cert, int64_t n_global, float* out_scores, int64_t* out_ids,
+                               int32_t* status, void* stream);
 /* Dense score matrix C[m, n] = A[m, d] . B[n, d]^T with fp32 accumulation
  * (torch.matmul(q_reps, p_reps.T), biencoder.py:107).  A, B bf16; C fp32 with
  * leading dimension ldc.                                                     */
