@@ -59,6 +59,9 @@ def parse():
                          "search.GROUP_QUERIES)")
     ap.add_argument("--protocol", choices=["global_tau", "per_shard"], default="global_tau",
                     help="N > 1 exchange protocol (per_shard = exact top-k per shard + merge)")
+    ap.add_argument("--order", choices=["exact", "fp32"], default="exact",
+                    help="exact: the canonical exact-score order (search.EXACT_ORDER, the product default); "
+                         "fp32: the scan's fp32 order (A/B of the refine stage's cost)")
     ap.add_argument("--launch-check", action="store_true",
                     help="start the ranks, join the process group, report n_gpus and exit without touching "
                          "the GPU (tests/test_bench_launch_cpu.py)")
@@ -216,6 +219,16 @@ def cpu_baseline(args, shard, queries, gpu_result):
     gs = gs.cpu().numpy()
     same = float((gi == best_i).mean())
     n_mis, gap = _tie_check(q, shard, gi, best_i)
+    # parity against the fp64 evaluator (exact products; the canonical order's definition), untimed
+    b64_s = b64_i = None
+    for a in range(0, n, chunk):
+        pc = shard[a: a + chunk].double().cpu().numpy()
+        cs, ci = ip_topk(q, pc, args.k, id_offset=a, chunk=pc.shape[0], dtype=np.float64, out_dtype=np.float64)
+        if b64_s is None:
+            b64_s, b64_i = cs, ci
+        else:
+            b64_s, b64_i = merge_topk(np.stack([b64_s, cs]), np.stack([b64_i, ci]), args.k)
+    same64 = float((gi == b64_i).mean())
     cores = int(thr["blas_threads"] or thr["torch_threads"])
     value = q.shape[0] / t_comp
     return {
@@ -236,6 +249,11 @@ def cpu_baseline(args, shard, queries, gpu_result):
                           "n_mismatch": n_mis,
                           "max_tie_gap_fp64": gap,
                           "all_mismatches_near_ties": bool(gap <= 1e-3)},
+        # the same batch against the fp64 evaluator (oracle ip_topk in float64 over the full corpus)
+        "parity_vs_gpu_fp64": {"ids_equal_frac": round(same64, 6),
+                               "n_mismatch": int((gi != b64_i).sum()),
+                               "max_abs_score_diff": float(np.abs(gs.astype(np.float64) - b64_s).max()),
+                               "scores_equal_fp32_frac": round(float((gs == b64_s.astype(np.float32)).mean()), 6)},
     }
 
 
@@ -310,6 +328,7 @@ def main():
 
     gloo = world > 1 and dist.get_backend() == "gloo"
     from denseretrievaltoolkits_amd import search as srch
+    srch.EXACT_ORDER = args.order == "exact"
     if args.group_queries == 0:
         srch.GROUP_MIN_ROWS = 1 << 62          # one-GPU: per-batch path
         srch.GROUP_QUERIES = qb                 # several GPUs: one batch per group
@@ -343,6 +362,7 @@ def main():
     def fallbacks():
         return index.group_fallbacks if world == 1 else index.fallbacks
     fb0 = fallbacks()
+    unc0 = index.order_uncertified
 
     lib.drt_profile_enable(_native.PROF_SCAN, 1)
     if world > 1:
@@ -357,6 +377,7 @@ def main():
     lib.drt_profile_enable(_native.PROF_SCAN, 0)
     n_resolved = local_index.resolved - res0
     n_fallback = fallbacks() - fb0
+    n_unc = index.order_uncertified - unc0
     tot_ms = _native.ctypes.c_double(0.0)
     cnt = _native.c_i64(0)
     _native.check(lib.drt_profile_read(_native.PROF_SCAN, _native.ctypes.byref(tot_ms), _native.ctypes.byref(cnt)),
@@ -422,6 +443,10 @@ def main():
                 "launches": int(cnt.value),
                 "alg_bytes_per_launch": alg_bytes,
             },
+            "order": ("canonical: exact-score re-rank of each query's near-tie window (fp64 sums of the bf16 "
+                      "products, ties by id), the product default" if args.order == "exact" else
+                      "fp32 scan order (A/B leg)"),
+            "order_uncertified_queries": int(n_unc),
             "uncertified_queries_resolved": int(n_resolved),
             "global_tau_fallback_batches": int(n_fallback),
             "query_group": srch.GROUP_QUERIES if use_global else qb,

@@ -1352,11 +1352,12 @@ __global__ __launch_bounds__(kKthThreads) void kth_final_kernel(const uint32_t* 
 // survivor lists and the second launch.  More than kRankBuf candidates (ties / a degenerate score
 // range) fall back to an exact MSD radix select over the candidates.  Also zeroes the hit counter.
 constexpr int kRankThreads = 1024;
-constexpr int kRankPer = 80;
+constexpr int kRankPerMax = 80;   // keys per thread (register-resident); smaller samples take 8 / 24
 constexpr int kRankBins = 1024;
 constexpr int kRankBuf = 2048;
-constexpr int64_t kRankMaxKeys = (int64_t)kRankThreads * kRankPer;
+constexpr int64_t kRankMaxKeys = (int64_t)kRankThreads * kRankPerMax;
 
+template <int kRankPer>
 __global__ __launch_bounds__(kRankThreads) void kth_rank_kernel(const uint32_t* in, int64_t stride, int64_t n, int r,
                                                                 float* tau, uint32_t* zero) {
   __shared__ uint32_t hist[kRankBins];
@@ -1929,7 +1930,7 @@ __global__ __launch_bounds__(kMergeThreads) void merge_kernel(const float* score
 // refine_sort_kernel   grid nq: the window by (fp32 score + delta desc, id asc) -> top-k.
 // ---------------------------------------------------------------------------
 constexpr int kRefThreads = 256;
-constexpr int kRefSlice = 128;
+constexpr int kRefSlice = 64;   // candidates per work-group of refine_delta (16 per wave)
 constexpr int kRefSortThreads = 512;
 constexpr int kRefMax = kSelMaxK;
 
@@ -1946,7 +1947,7 @@ struct RefineArgs {
   const float* stats;   // row statistics (drt_row_stats_bf16)
   const float* tau;     // [nq] filter thresholds or NULL (every row was scored)
   float* delta;         // [nq][kc]
-  int32_t* cnt;         // [nq]
+  int32_t* cnt;         // [nq][2]: window size C (-1: exact in fp32, -2: window wider than the list), eps bits
   int32_t* status;      // [nq] (indexed through qmap) or NULL
   const int32_t* qmap;  // output row of query q, or NULL
   bool set_status;      // status[row] = this stage's bits (the exact rescan clears it) instead of |=
@@ -1992,11 +1993,12 @@ __device__ __forceinline__ float refine_eps(const RefineArgs& a, int64_t q, floa
   return 2.5f * (float)a.d * 5.9604645e-8f * qn * pmax + 1e-30f;
 }
 
-__global__ __launch_bounds__(kRefThreads) void refine_delta_kernel(RefineArgs a) {
+// per query: eps, the window C (entries >= B = s_k - 2 eps) and the certificate bits -> cnt[q]
+__global__ __launch_bounds__(kRefThreads) void refine_prep_kernel(RefineArgs a) {
   __shared__ float fscr[kRefThreads / 64];
   __shared__ int iscr[kRefThreads / 64];
   const int64_t q = blockIdx.x;
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int tid = threadIdx.x;
   const float eps = refine_eps(a, q, fscr, iscr);
   const float* cs = a.cs + q * (int64_t)a.kc;
   const int64_t* ci = a.ci + q * (int64_t)a.kc;
@@ -2008,8 +2010,9 @@ __global__ __launch_bounds__(kRefThreads) void refine_delta_kernel(RefineArgs a)
   for (int j = tid; j < nval; j += kRefThreads) C += cs[j] >= B ? 1 : 0;
   C = ref_block_sum(C, iscr);
   const bool wide = eps != 0.0f && C == a.kc && nval == a.kc;               // window wider than the list
-  if (blockIdx.y == 0 && tid == 0) {
-    a.cnt[q] = eps == 0.0f ? -1 : (wide ? -2 : C);
+  if (tid == 0) {
+    a.cnt[2 * q] = eps == 0.0f ? -1 : (wide ? -2 : C);
+    a.cnt[2 * q + 1] = __builtin_bit_cast(int32_t, eps);
     if (a.status) {
       int st = wide ? 2 : 0;
       if (eps != 0.0f && a.tau && nval >= a.k && a.tau[q] > B) st |= 1;     // rows in [B, tau) unseen
@@ -2018,8 +2021,21 @@ __global__ __launch_bounds__(kRefThreads) void refine_delta_kernel(RefineArgs a)
       else if (st) a.status[orow] |= st;
     }
   }
-  const int j0 = blockIdx.y * kRefSlice;
-  const int j1 = j0 + kRefSlice < a.kc ? j0 + kRefSlice : a.kc;
+}
+
+// exact sums of the window's candidates this shard owns: each wave takes kRefSlice / 4 of them,
+// kRefUnroll at a time with every row load of the group in flight together (one HBM round trip
+// per group instead of one per candidate)
+constexpr int kRefUnroll = 8;
+__global__ __launch_bounds__(kRefThreads) void refine_delta_kernel(RefineArgs a) {
+  const int64_t q = blockIdx.x;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int C = a.cnt[2 * q];
+  const int j0 = blockIdx.y * kRefSlice + wave * (kRefSlice / 4);
+  if (C <= j0) return;   // also: exact in fp32 (-1) or window too wide (-2)
+  const int j1 = j0 + kRefSlice / 4 < C ? j0 + kRefSlice / 4 : C;
+  const float* cs = a.cs + q * (int64_t)a.kc;
+  const int64_t* ci = a.ci + q * (int64_t)a.kc;
   float* dq = a.delta + q * (int64_t)a.kc;
   // this lane's query elements: 4-element chunks c = lane + 64 t of the row, in fp64
   constexpr int kMaxT = 4;   // d <= 1024
@@ -2033,33 +2049,57 @@ __global__ __launch_bounds__(kRefThreads) void refine_delta_kernel(RefineArgs a)
 #pragma unroll
     for (int u = 0; u < 4; ++u) qv[t][u] = (double)(float)x[u];
   }
-  for (int j = j0 + wave; j < j1; j += kRefThreads / 64) {
-    const int64_t id = ci[j];
-    const int64_t row = id - a.row_offset;
-    const bool own = eps != 0.0f && !wide && j < C && id >= 0 && row >= 0 && row < a.n_local;   // wave-uniform
-    double acc = 0.0;
-    if (own) {
-      const __bf16* pr = a.P + row * (int64_t)a.d;
+  for (int jb = j0; jb < j1; jb += kRefUnroll) {
+    bool own[kRefUnroll];
+    int64_t row[kRefUnroll];
+#pragma unroll
+    for (int u = 0; u < kRefUnroll; ++u) {
+      const int j = jb + u;
+      const int64_t id = j < j1 ? ci[j] : -1;
+      row[u] = id - a.row_offset;
+      own[u] = j < j1 && id >= 0 && row[u] >= 0 && row[u] < a.n_local;   // wave-uniform
+    }
+    bf16x4 x[kRefUnroll][kMaxT];
+#pragma unroll
+    for (int u = 0; u < kRefUnroll; ++u) {
+      const __bf16* pr = a.P + (own[u] ? row[u] : 0) * (int64_t)a.d;
 #pragma unroll
       for (int t = 0; t < kMaxT; ++t) {
         const int c = lane + 64 * t;
-        if (c < nch) {
-          const bf16x4 x = *(const bf16x4*)(pr + 4 * c);
-#pragma unroll
-          for (int u = 0; u < 4; ++u) acc = __builtin_fma(qv[t][u], (double)(float)x[u], acc);
-        }
+        x[u][t] = (own[u] && c < nch) ? *(const bf16x4*)(pr + 4 * c) : bf16x4{};
       }
-#pragma unroll
-      for (int o = 32; o > 0; o >>= 1) acc += __shfl_xor(acc, o, 64);
     }
-    if (lane == 0) dq[j] = own ? (float)(acc - (double)cs[j]) : 0.0f;
+    double acc[kRefUnroll];
+#pragma unroll
+    for (int u = 0; u < kRefUnroll; ++u) {
+      acc[u] = 0.0;
+#pragma unroll
+      for (int t = 0; t < kMaxT; ++t)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) acc[u] = __builtin_fma(qv[t][e], (double)(float)x[u][t][e], acc[u]);
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1)
+#pragma unroll
+      for (int u = 0; u < kRefUnroll; ++u) acc[u] += __shfl_xor(acc[u], o, 64);
+    if (lane == 0) {
+#pragma unroll
+      for (int u = 0; u < kRefUnroll; ++u)
+        if (jb + u < j1) dq[jb + u] = own[u] ? (float)(acc[u] - (double)cs[jb + u]) : 0.0f;
+    }
   }
 }
 
+// The window ranked by (exact score desc, id asc) without a sort network: the candidates arrive
+// sorted by fp32 score and every row's fp32 score is within eps of its exact one, so candidate i
+// follows every j with s_j > s_i + 2 eps and precedes every j with s_j < s_i - 2 eps; its rank is
+// the count of the former plus the exact comparisons inside the band |s_j - s_i| <= 2 eps (two
+// binary searches and ~ band-width compares per candidate; the band is a few dozen entries on
+// real-valued data).  Each candidate then writes itself at its rank.
 __global__ __launch_bounds__(kRefSortThreads) void refine_sort_kernel(RefineArgs a) {
   __shared__ uint64_t key[kRefMax];
   __shared__ int64_t idv[kRefMax];
-  __shared__ float sco[kRefMax];
+  __shared__ float sf[kRefMax];
   const int64_t q = blockIdx.x;
   const int tid = threadIdx.x;
   const int64_t orow = a.qmap ? (int64_t)a.qmap[q] : q;
@@ -2067,7 +2107,7 @@ __global__ __launch_bounds__(kRefSortThreads) void refine_sort_kernel(RefineArgs
   const int64_t* ci = a.ci + q * (int64_t)a.kc;
   float* os = a.out_s + orow * (int64_t)a.k;
   int64_t* oi = a.out_i + orow * (int64_t)a.k;
-  const int C = a.cnt[q];
+  const int C = a.cnt[2 * q];
   if (C < 0) {   // exact in fp32 (or the window did not fit the list: status bit 1): the fp32 order
     for (int j = tid; j < a.k; j += kRefSortThreads) {
       os[j] = cs[j];
@@ -2075,53 +2115,47 @@ __global__ __launch_bounds__(kRefSortThreads) void refine_sort_kernel(RefineArgs
     }
     return;
   }
+  const double two_eps = 2.0 * (double)__builtin_bit_cast(float, a.cnt[2 * q + 1]);
   const float* dq = a.delta + q * (int64_t)a.kc;
-  int n2 = 1;
-  while (n2 < C) n2 <<= 1;
-  for (int j = tid; j < n2; j += kRefSortThreads) {
-    if (j < C) {
-      const double ex = (double)cs[j] + (double)dq[j];
-      key[j] = desc_key64(ex);
-      idv[j] = ci[j];
-      sco[j] = (float)ex;
-    } else {
-      key[j] = ~0ull;
-      idv[j] = INT64_MAX;
-      sco[j] = kPadScore;
-    }
+  for (int j = tid; j < C; j += kRefSortThreads) {
+    const float s = cs[j];
+    sf[j] = s;
+    key[j] = desc_key64((double)s + (double)dq[j]);
+    idv[j] = ci[j];
+  }
+  for (int j = C + tid; j < a.k; j += kRefSortThreads) {   // fewer candidates than k: pads
+    os[j] = kPadScore;
+    oi[j] = -1;
   }
   __syncthreads();
-  // bitonic sort of (key asc, id asc); the score rides along
-  for (int size = 2; size <= n2; size <<= 1) {
-    for (int stride = size >> 1; stride > 0; stride >>= 1) {
-      for (int i = tid; i < n2; i += kRefSortThreads) {
-        const int j = i ^ stride;
-        if (j > i) {
-          const bool up = (i & size) == 0;
-          const uint64_t ki = key[i], kj = key[j];
-          const int64_t ii = idv[i], ij = idv[j];
-          const bool gt = ki > kj || (ki == kj && ii > ij);
-          if (gt == up) {
-            key[i] = kj;
-            key[j] = ki;
-            idv[i] = ij;
-            idv[j] = ii;
-            const float t = sco[i];
-            sco[i] = sco[j];
-            sco[j] = t;
-          }
-        }
-      }
-      __syncthreads();
+  for (int i = tid; i < C; i += kRefSortThreads) {
+    const double si = (double)sf[i];
+    const double up = si + two_eps, dn = si - two_eps;
+    int lo = 0, hi = i;   // lo = #{j : s_j > si + 2 eps} (a prefix: sf is non-increasing)
+    while (lo < hi) {
+      const int mid = (lo + hi) >> 1;
+      if ((double)sf[mid] > up) lo = mid + 1;
+      else hi = mid;
     }
-  }
-  for (int j = tid; j < a.k; j += kRefSortThreads) {
-    if (j < C) {
-      os[j] = sco[j];
-      oi[j] = idv[j];
-    } else {
-      os[j] = kPadScore;
-      oi[j] = -1;
+    int lo2 = i, hi2 = C;  // hi2 = #{j : s_j >= si - 2 eps}
+    while (lo2 < hi2) {
+      const int mid = (lo2 + hi2) >> 1;
+      if ((double)sf[mid] >= dn) lo2 = mid + 1;
+      else hi2 = mid;
+    }
+    const uint64_t ki = key[i];
+    const int64_t ii = idv[i];
+    int rank = lo;
+    for (int j = lo; j < lo2; ++j) {
+      const uint64_t kj = key[j];
+      rank += (kj < ki || (kj == ki && idv[j] < ii)) ? 1 : 0;
+    }
+    if (rank < a.k) {
+      // the exact score from its order key (desc_key64 is a bijection)
+      const uint64_t ord = ~ki;
+      const uint64_t u = (ord >> 63) ? (ord & 0x7FFFFFFFFFFFFFFFull) : ~ord;
+      os[rank] = (float)__builtin_bit_cast(double, u);
+      oi[rank] = ii;
     }
   }
 }
@@ -2208,7 +2242,7 @@ static size_t plan_refine_tail(TopkPlan& p, size_t o) {
   p.off_delta = o;
   o = align_up(o + (size_t)p.nq_pad * p.kc * 4, 256);
   p.off_rcnt = o;
-  o = align_up(o + (size_t)p.nq_pad * 4, 256);
+  o = align_up(o + (size_t)p.nq_pad * 8, 256);
   return o;
 }
 
@@ -2437,6 +2471,7 @@ namespace drt {
 static int launch_refine(RefineArgs& ra, hipStream_t s) {
   if (ra.nq == 0) return DRT_OK;
   const ProfPair pp = prof_begin(PROF_SELECT, s);
+  hipLaunchKernelGGL(refine_prep_kernel, dim3((unsigned)ra.nq), dim3(kRefThreads), 0, s, ra);
   hipLaunchKernelGGL(refine_delta_kernel, dim3((unsigned)ra.nq, (unsigned)((ra.kc + kRefSlice - 1) / kRefSlice)),
                      dim3(kRefThreads), 0, s, ra);
   hipLaunchKernelGGL(refine_sort_kernel, dim3((unsigned)ra.nq), dim3(kRefSortThreads), 0, s, ra);
@@ -2539,8 +2574,18 @@ static int ip_topk_impl(const void* Q, int64_t nq, const void* P, int64_t n, int
   {
     const ProfPair pp = prof_begin(PROF_SELECT, s);
     if (p.m <= kRankMaxKeys && p.r <= kRankBuf) {   // one launch: the whole sample row per work-group
-      hipLaunchKernelGGL(kth_rank_kernel, dim3((unsigned)nq), dim3(kRankThreads), 0, s,
-                         (const uint32_t*)(w + p.off_sample), (int64_t)align_up(p.m, 4), p.m, (int)p.r, tau, cnt);
+      // keys per thread sized to the sample (a sample of ~7k keys at 1M rows needs 8, not 80)
+      const uint32_t* smp = (const uint32_t*)(w + p.off_sample);
+      const int64_t ld = (int64_t)align_up(p.m, 4);
+      if (p.m <= (int64_t)kRankThreads * 8)
+        hipLaunchKernelGGL(kth_rank_kernel<8>, dim3((unsigned)nq), dim3(kRankThreads), 0, s, smp, ld, p.m, (int)p.r,
+                           tau, cnt);
+      else if (p.m <= (int64_t)kRankThreads * 24)
+        hipLaunchKernelGGL(kth_rank_kernel<24>, dim3((unsigned)nq), dim3(kRankThreads), 0, s, smp, ld, p.m, (int)p.r,
+                           tau, cnt);
+      else
+        hipLaunchKernelGGL(kth_rank_kernel<kRankPerMax>, dim3((unsigned)nq), dim3(kRankThreads), 0, s, smp, ld, p.m,
+                           (int)p.r, tau, cnt);
     } else {
       hipLaunchKernelGGL(kth_partial_kernel, dim3((unsigned)p.nchunk, (unsigned)nq), dim3(kKthThreads), 0, s,
                          (const uint32_t*)(w + p.off_sample), (int64_t)align_up(p.m, 4), p.m, (int)p.r,
@@ -2636,6 +2681,7 @@ int drt_refine_delta_bf16(const void* Q, int64_t nq, int32_t d, const void* P, i
   ra.cnt = cnt;
   ra.status = status;
   hipStream_t s = (hipStream_t)stream;
+  hipLaunchKernelGGL(refine_prep_kernel, dim3((unsigned)nq), dim3(kRefThreads), 0, s, ra);
   hipLaunchKernelGGL(refine_delta_kernel, dim3((unsigned)nq, (unsigned)((kc + kRefSlice - 1) / kRefSlice)),
                      dim3(kRefThreads), 0, s, ra);
   return hip_status(hipGetLastError());
@@ -2671,7 +2717,7 @@ static int64_t resolve_chunk(int64_t nbad, int64_t n) {
 
 static size_t resolve_ws_bytes(int64_t chunk, int64_t n, int32_t d) {
   return (size_t)(align_up(chunk * (int64_t)d * 2, 256) + align_up(chunk * resolve_width(n) * 4, 256) +
-                  align_up(chunk * 4, 256) + align_up(chunk * kSelMaxK * 16 + chunk * 4, 256));
+                  align_up(chunk * 4, 256) + align_up(chunk * kSelMaxK * 16 + chunk * 8, 256));
 }
 
 size_t drt_ip_topk_resolve_workspace(int64_t nbad, int64_t n, int32_t d) {

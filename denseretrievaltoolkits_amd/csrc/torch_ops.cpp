@@ -191,7 +191,7 @@ std::tuple<Tensor, Tensor> refine_delta(const Tensor& q_, const Tensor& p_, int6
     TORCH_CHECK_VALUE(tau.size(0) == nq, "tau must hold one threshold per query");
   }
   Tensor delta = at::empty({nq, kc}, cs.options());
-  Tensor cnt = at::empty({nq}, cs.options().dtype(at::kInt));
+  Tensor cnt = at::empty({nq, 2}, cs.options().dtype(at::kInt));
   check_rc(drt_refine_delta_bf16(q.data_ptr(), nq, (int32_t)q.size(1), p.size(0) ? p.data_ptr() : nullptr, p.size(0),
                                  row_offset, cs.data_ptr<float>(), ci.data_ptr<int64_t>(), (int32_t)kc, (int32_t)k,
                                  stats_ptr(stats, q), tau.defined() ? tau.data_ptr<float>() : nullptr,
@@ -206,7 +206,7 @@ std::tuple<Tensor, Tensor> refine_sort(const Tensor& cs_, const Tensor& ci_, con
   need(cs_, "cand_scores", at::kFloat, 2);
   need(ci_, "cand_ids", at::kLong, 2);
   need(delta_, "delta", at::kFloat, 2);
-  need(cnt_, "cnt", at::kInt, 1);
+  need(cnt_, "cnt", at::kInt, 2);
   const c10::DeviceGuard g(cs_.device());
   const Tensor cs = cs_.contiguous(), ci = ci_.contiguous(), delta = delta_.contiguous(), cnt = cnt_.contiguous();
   const int64_t nq = cs.size(0), kc = cs.size(1);

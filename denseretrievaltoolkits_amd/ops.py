@@ -71,7 +71,7 @@ def _register_python_parts():
 
     @lib.register_fake("drt::refine_delta")
     def _(q, p, row_offset, cand_scores, cand_ids, k, stats, tau, status):
-        return cand_scores.new_empty(cand_scores.shape), cand_scores.new_empty((cand_scores.shape[0],),
+        return cand_scores.new_empty(cand_scores.shape), cand_scores.new_empty((cand_scores.shape[0], 2),
                                                                                  dtype=torch.int32)
 
     @lib.register_fake("drt::refine_sort")

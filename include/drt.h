@@ -92,8 +92,8 @@ int drt_ip_topk_resolve(const void* Q, int64_t nq, const void* P, int64_t n, int
  * drt_refine_delta_bf16 / drt_refine_sort: the stage alone, on a candidate list cand [nq][kc]
  *   (scores desc, global ids, kc = drt_refine_width(k), e.g. a merged sharded result): delta =
  *   exact - fp32 score for the candidates whose rows this shard holds (row_offset = global id of
- *   its row 0; 0 elsewhere, so shards combine their deltas with one SUM all-reduce), cnt [nq] the
- *   window per query; then the sort writes the top-k.  tau [nq] = the filter thresholds the
+ *   its row 0; 0 elsewhere, so shards combine their deltas with one SUM all-reduce), cnt [nq][2]
+ *   (window size, eps) per query; then the sort writes the top-k.  tau [nq] = the filter thresholds the
  *   candidate list was collected with (NULL: every row was scored).                           */
 int drt_row_stats_bf16(const void* P, int64_t n, int32_t d, float* stats, int32_t accumulate, void* stream);
 int32_t drt_refine_width(int32_t k);

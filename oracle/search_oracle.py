@@ -68,13 +68,14 @@ def _order(scores: np.ndarray, ids: np.ndarray) -> np.ndarray:
 
 
 def ip_topk(q: np.ndarray, p: np.ndarray, k: int, id_offset: int = 0, chunk: int = 262144,
-            dtype=np.float64):
-    """Exact IP top-k of q [nq, d] over p [n, d].  Returns (scores f32 [nq,k], ids i64 [nq,k])."""
+            dtype=np.float64, out_dtype=np.float32):
+    """Exact IP top-k of q [nq, d] over p [n, d].  Returns (scores [nq,k] in out_dtype (fp32: the
+    faiss output type; fp64 keeps the ranking precision for a later partition merge), ids i64)."""
     q = np.asarray(q)
     p = np.asarray(p)
     nq = q.shape[0]
     n = p.shape[0]
-    out_s = np.full((nq, k), PAD_SCORE, dtype=np.float32)
+    out_s = np.full((nq, k), PAD_SCORE, dtype=out_dtype)
     out_i = np.full((nq, k), PAD_ID, dtype=np.int64)
     if nq == 0 or n == 0:
         return out_s, out_i
@@ -108,7 +109,7 @@ def ip_topk(q: np.ndarray, p: np.ndarray, k: int, id_offset: int = 0, chunk: int
             best_s[r, :len(new_s[r])] = new_s[r]
             best_i[r, :len(new_i[r])] = new_i[r]
     kk = min(k, n)
-    out_s[:, :kk] = best_s[:, :kk].astype(np.float32)
+    out_s[:, :kk] = best_s[:, :kk].astype(out_dtype)
     out_i[:, :kk] = best_i[:, :kk] + id_offset
     return out_s, out_i
 
@@ -119,12 +120,14 @@ def search_ids(q: np.ndarray, p: np.ndarray, k: int) -> np.ndarray:
 
 
 def merge_topk(scores: np.ndarray, ids: np.ndarray, k_out: int):
-    """Merge per-part sorted lists [nparts, nq, k_in] into the top-k_out (score desc, id asc)."""
+    """Merge per-part sorted lists [nparts, nq, k_in] into the top-k_out (score desc, id asc).
+    fp64 scores are merged (and returned) in fp64, anything else in fp32."""
     nparts, nq, k_in = scores.shape
-    out_s = np.full((nq, k_out), PAD_SCORE, dtype=np.float32)
+    sdt = np.float64 if scores.dtype == np.float64 else np.float32
+    out_s = np.full((nq, k_out), PAD_SCORE, dtype=sdt)
     out_i = np.full((nq, k_out), PAD_ID, dtype=np.int64)
     for r in range(nq):
-        ss = scores[:, r, :].reshape(-1).astype(np.float32)
+        ss = scores[:, r, :].reshape(-1).astype(sdt)
         ii = ids[:, r, :].reshape(-1).astype(np.int64)
         o = _order(ss.astype(np.float64), ii)[:k_out]
         out_s[r, :len(o)] = ss[o]

@@ -19,6 +19,7 @@ def main():
     ap.add_argument("--steps", type=int, default=32)
     ap.add_argument("--n", type=int, default=10_000_000)
     ap.add_argument("--groups", default="2048,0")
+    ap.add_argument("--order", choices=["exact", "fp32"], default="exact")
     args = ap.parse_args()
     import torch
     from bench import gen_shard
@@ -28,6 +29,7 @@ def main():
     g = torch.Generator(device=dev)
     g.manual_seed(5678)
     qs = torch.randn((args.steps, 128, 768), generator=g, device=dev).to(torch.bfloat16)
+    srch.EXACT_ORDER = args.order == "exact"
     idx = srch.FlatIPIndex.from_rows(shard)
     batches = [qs[j] for j in range(args.steps)]
     variants = [int(v) for v in args.groups.split(",")]
