@@ -434,43 +434,53 @@ __global__ __launch_bounds__(NW * 64, 1) void ip_scan16_kernel(ScanArgs a) {
 }
 
 // ---------------------------------------------------------------------------
-// Production filter scan, round 2: the 16-row / 8-wave kernel above with the LDS
-// fragment reads of tile t+1 rolled into tile t's MFMA sequence.  Fragment s of
-// tile t+1 is read into the register that held fragment s of tile t right after
-// that fragment's MFMA, so no LDS latency sits between the per-tile barrier and
-// the matrix work (the r02 ablation, tools/scan_ab.py: DMA alone 2.44 ms, DMA +
-// fragment reads 2.39, DMA + MFMA on registers 2.47, reads + MFMA 2.80 -> the
-// read-to-MFMA latency after every barrier, in lock step on both waves of a SIMD,
-// was the cost).  Same registers as the 8-wave kernel (the fragments were already
-// held for a whole tile).
-// Ring: NBUF slots, all in use: at iteration t tile t+1 has landed (it is read
-// during t), tiles t+2 .. t+NBUF are in flight, and slot(t) is refilled with tile
-// t+NBUF right after the barrier (its fragments were read in t-1 and drained by
-// that barrier's lgkmcnt(0)).
-// RAW: every wave waits (vmcnt) for its own share of tile t+1 before the barrier
-// of iteration t; reads of t+1 follow that barrier.  WAR: slot(t) is re-issued
-// after the barrier that follows the drain of its last reads.
-// The hit-count check that may flush the LDS hit list runs every 8th tile in the
-// sparse flavour (a full list spills straight to the global lists, so the check
-// only keeps appends cheap; it cost an exposed LDS round trip per tile).
+// Production filter scan: the 16-row / 8-wave kernel above with the LDS fragment reads of tile
+// t+1 rolled into tile t's MFMA sequence (round 2) and, round 4, PER-WAVE hit lists.
+// Fragment s of tile t+1 is read into the register that held fragment s of tile t right after
+// that fragment's MFMA, so no LDS latency sits between the per-tile barrier and the matrix work
+// (the r02 ablation, tools/scan_ab.py: DMA alone 2.44 ms, DMA + fragment reads 2.39, DMA + MFMA
+// on registers 2.47, reads + MFMA 2.80 -> the read-to-MFMA latency after every barrier, in lock
+// step on both waves of a SIMD, was the cost).
+// Ring: NBUF slots, all in use: at iteration t tile t+1 has landed (it is read during t), tiles
+// t+2 .. t+NBUF are in flight, and slot(t) is refilled with tile t+NBUF right after the barrier
+// (its fragments were read in t-1 and drained by that barrier's lgkmcnt(0)).
+// RAW: every wave waits (vmcnt) for its own share of tile t+1 before the barrier of iteration t;
+// reads of t+1 follow that barrier.  WAR: slot(t) is re-issued after the barrier that follows the
+// drain of its last reads.
+// Hits (round 4): each wave owns a private segment of the LDS hit list and appends with
+// ballot + mbcnt (no LDS atomic, no read-back latency in the epilogue); a full segment is flushed
+// by its own wave to the global per-query lists (one global atomic per hit, no block barrier).
+// The round-2/3 shared list needed an LDS atomic per hit (or per wave-tile) and a block-wide
+// flush every 512 hits; with ~4k hits per query that cost 20-35 % of the launch at 1M rows
+// (tools/scan_probe.py, profiles/r04b_probe*).
 // ---------------------------------------------------------------------------
-template <int D, bool AGG, bool FAGG = AGG>
+constexpr int kWaveSeg = kHitCap / 8;   // hit entries per wave segment
+
+__device__ __forceinline__ void wave_flush_hits(const ScanArgs& a, int64_t qw, const uint64_t* hk,
+                                                const uint8_t* hq, int n, int lane) {
+  for (int i = lane; i < n; i += 64) {
+    const uint64_t key = hk[i];
+    const int64_t q = qw + hq[i];
+    const uint32_t g = atomicAdd(a.counts + q * kCntStride, 1u);
+    if (g < (uint64_t)a.cap) ((uint64_t*)a.out)[q * a.cap + g] = key;
+  }
+}
+
+template <int D>
 __global__ __launch_bounds__(512, 1) void ip_scan16r_kernel(ScanArgs a) {
   constexpr int NW = 8;
   using C = Scan16Cfg<D, NW>;
   constexpr int PD = C::NBUF;   // issue distance: every slot in use
   __shared__ __attribute__((aligned(16))) char smem[C::LDS_BYTES];
-  uint64_t* hk = (uint64_t*)(smem + C::HIT_KEY_OFF);
-  uint16_t* hq = (uint16_t*)(smem + C::HIT_Q_OFF);
-  uint32_t* hit_n = (uint32_t*)(smem + C::HIT_N_OFF);
-  uint32_t* qcnt = (uint32_t*)(smem + C::QCNT_OFF);
-  uint32_t* qoff = qcnt + kQueriesPerWG;
 
   const int tid = threadIdx.x;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int lane = tid & 63;
   const int r = lane & 15;
   const int kq = lane >> 4;
+  // this wave's hit segment: kWaveSeg keys + kWaveSeg query indices (within the wave's 16)
+  uint64_t* hk = (uint64_t*)(smem + C::HIT_KEY_OFF) + wave * kWaveSeg;
+  uint8_t* hq = (uint8_t*)(smem + C::HIT_Q_OFF) + wave * kWaveSeg;
 
   const int64_t qbase = (int64_t)blockIdx.y * kQueriesPerWG;
   const int64_t ntiles = (a.nrows + kT16 - 1) / kT16;
@@ -478,12 +488,11 @@ __global__ __launch_bounds__(512, 1) void ip_scan16r_kernel(ScanArgs a) {
   const int64_t tstep = gridDim.x;
   const int64_t my_tiles = t0 < ntiles ? (ntiles - 1 - t0) / tstep + 1 : 0;
   if (my_tiles == 0) return;
-  if (tid == 0) *hit_n = 0;
   const uint32_t ring = lds_addr_of(smem);
 
   // 16 queries per wave: qbase + 16 * wave + r
-  const int qloc = wave * 16 + r;
-  const int64_t qg = qbase + qloc;
+  const int64_t qw = qbase + wave * 16;
+  const int64_t qg = qw + r;
   const bool qok = qg < a.nq;
   const int64_t qs = qok ? qg : 0;
   bf16x8 qf[C::KS];
@@ -536,47 +545,27 @@ __global__ __launch_bounds__(512, 1) void ip_scan16r_kernel(ScanArgs a) {
       __builtin_amdgcn_sched_barrier(0);
     }
   };
+  int wcnt = 0;   // entries in this wave's segment (wave-uniform)
   auto epilogue = [&](const f32x4& acc, int64_t rowbase) {
     const float mx = fmaxf(fmaxf(acc[0], acc[1]), fmaxf(acc[2], acc[3])) - tau;
     if (__ballot(mx >= 0.0f) == 0ull) return;
-    if (AGG) {
-      uint32_t m = 0;
 #pragma unroll
-      for (int j = 0; j < 4; ++j)
-        if (acc[j] >= tau && rowbase + j < a.nrows) m |= 1u << j;
-      const uint32_t c = __builtin_popcount(m);
-      uint32_t incl = c;
-#pragma unroll
-      for (int o = 1; o < 64; o <<= 1) {
-        const uint32_t v = __shfl_up(incl, o, 64);
-        if (lane >= o) incl += v;
+    for (int j = 0; j < 4; ++j) {
+      const bool hit = acc[j] >= tau && rowbase + j < a.nrows;
+      const uint64_t m = __ballot(hit);
+      if (m == 0ull) continue;
+      const int c = __builtin_popcountll(m);
+      if (wcnt + c > kWaveSeg) {
+        wave_flush_hits(a, qw, hk, hq, wcnt, lane);
+        wcnt = 0;
       }
-      const uint32_t tot = __shfl(incl, 63, 64);
-      uint32_t base = 0;
-      if (lane == 0) base = atomicAdd(hit_n, tot);
-      base = __shfl(base, 0, 64) + incl - c;
-      while (m) {
-        const int j = __builtin_ctz(m);
-        m &= m - 1;
-        const uint64_t key = ((uint64_t)desc_key(acc[j]) << 32) | (uint64_t)(uint32_t)(rowbase + j);
-        if (base < (uint32_t)kHitCap) {
-          hk[base] = key;
-          hq[base] = (uint16_t)qloc;
-        } else {
-          const uint32_t g = atomicAdd(a.counts + qg * kCntStride, 1u);
-          if (g < (uint64_t)a.cap) ((uint64_t*)a.out)[qg * a.cap + g] = key;
-        }
-        ++base;
+      if (hit) {
+        const int pos = wcnt + (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32),
+                                                              __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+        hk[pos] = ((uint64_t)desc_key(acc[j]) << 32) | (uint64_t)(uint32_t)(rowbase + j);
+        hq[pos] = (uint8_t)r;
       }
-    } else {
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const int64_t row = rowbase + j;
-        if (acc[j] >= tau && row < a.nrows) {
-          const uint64_t key = ((uint64_t)desc_key(acc[j]) << 32) | (uint64_t)(uint32_t)row;
-          push_hit(a, qloc, qg, key, hit_n, hk, hq);
-        }
-      }
+      wcnt += c;
     }
   };
 
@@ -593,17 +582,6 @@ __global__ __launch_bounds__(512, 1) void ip_scan16r_kernel(ScanArgs a) {
       wait_tiles_younger<C::GLDS_PER_WAVE>((int)(last - it - 1));
     }
     lds_barrier();   // tile it+1 landed (every wave's share); slot(it) fully read
-
-    if (AGG || (it & 7) == 0) {
-      const uint32_t n = *hit_n;
-      if (n >= (uint32_t)(kHitCap / 2)) {
-        if (FAGG) flush_hits_agg<NW * 64>(a, qbase, n, hk, hq, qcnt, qoff);
-        else flush_hits<NW * 64>(a, qbase, n, hk, hq);
-        lds_barrier();
-        if (tid == 0) *hit_n = 0;
-        lds_barrier();
-      }
-    }
     if (it + PD < my_tiles) issue_tile16<D, NW, true>(a, ring + buf * C::TILE_BYTES, tile + PD * tstep, wave, lane);
     const int nslot = buf + 1 == C::NBUF ? 0 : buf + 1;
     mma_roll(acc, nslot);
@@ -617,11 +595,7 @@ __global__ __launch_bounds__(512, 1) void ip_scan16r_kernel(ScanArgs a) {
   }
   if (my_tiles & 1) epilogue(accA, rbA);
   else epilogue(accB, rbB);
-
-  lds_barrier();
-  const uint32_t nf = *hit_n;
-  if (FAGG) flush_hits_agg<NW * 64>(a, qbase, nf, hk, hq, qcnt, qoff);
-  else flush_hits<NW * 64>(a, qbase, nf, hk, hq);
+  if (wcnt) wave_flush_hits(a, qw, hk, hq, wcnt, lane);
 }
 
 // ---------------------------------------------------------------------------
@@ -2383,10 +2357,8 @@ static int launch_scan_d(const ScanArgs& a, int mode, hipStream_t s) {
     if (D > 768) {
       if (dense_hits) hipLaunchKernelGGL((ip_scan16_kernel<D, SCAN_FILTER, 8, true>), grid, dim3(512), 0, s, a);
       else hipLaunchKernelGGL((ip_scan16_kernel<D, SCAN_FILTER, 8, false>), grid, dim3(512), 0, s, a);
-    } else if (dense_hits) {
-      hipLaunchKernelGGL((ip_scan16r_kernel<D, true>), grid, dim3(512), 0, s, a);
     } else {
-      hipLaunchKernelGGL((ip_scan16r_kernel<D, false, true>), grid, dim3(512), 0, s, a);
+      hipLaunchKernelGGL((ip_scan16r_kernel<D>), grid, dim3(512), 0, s, a);
     }
   } else {
     hipLaunchKernelGGL((ip_scan16_kernel<D, SCAN_DENSE>), grid, dim3(512), 0, s, a);
