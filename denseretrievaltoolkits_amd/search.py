@@ -147,10 +147,9 @@ def _gtau_enqueue_group(local, qs, k: int, n_global: int, offset: int, gather, t
     tau = kernels.dist_tau(lists, k)                                # [Qg]: one launch for the group
     kc = kernels.refine_width(k) if stats is not None else k
     packed = torch.empty((qg.shape[0], kc + 1), dtype=torch.int64, device=qg.device)
-    o = 0
-    for q, nb in zip(qs, sizes):
-        kernels.dist_filter_into(q, local.rows, n_global, kc, offset, tau[o:o + nb], packed[o:o + nb])
-        o += nb
+    # ONE filter launch for the whole group (grid: corpus tiles x 128-query blocks; every block still
+    # streams the shard once) and one select over all of its queries
+    kernels.dist_filter_into(qg, local.rows, n_global, kc, offset, tau, packed)
     s, i, st = kernels.merge_packed(gather(packed), kc, n_global, k_cert=k)
     if stats is not None:
         s, i = kernels.refine(qg, local.rows, offset, s, i, k, stats, tau, st, all_reduce_sum)
