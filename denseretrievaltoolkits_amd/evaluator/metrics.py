@@ -43,17 +43,43 @@ def ndcg(indices, topk: Sequence[int]):
     disc = 1.0 / np.log(np.arange(max(ncol, 1)) + 2.0)
     out = []
     cnt = hits.sum(axis=1) if nrow else np.zeros(0, dtype=np.int64)
+    # ideal DCG of a row with c hits = cumdisc[min(c, k) - 1]: one gather per k instead of a Python loop
+    # over the rows (that loop was ~1 ms of host time per 128-query batch at k = 1000)
+    cumdisc = np.concatenate([[0.0], np.cumsum(disc)])
+    cmax = np.maximum(cnt, 1)
     for k in topk:
         dcg = float((hits[:, :k] * disc[:k]).sum()) if nrow else 0.0
-        idcg = 0.0
-        for c in np.maximum(cnt, 1):
-            idcg += float(disc[: min(int(c), k)].sum()) if k > 0 else 0.0
+        idcg = float(cumdisc[np.minimum(cmax, max(k, 0))].sum()) if nrow else 0.0
         out.append(dcg / idcg if idcg else math.nan)
     return out
 
 
+def _metrics_fast(indices, topk: Sequence[int]):
+    """recall / mrr / ndcg from ONE pass over the hit matrix (the Trainer calls this per query
+    batch at k = 1000: hits, first hits, per-position DCG column sums and row counts computed once)."""
+    hits = np.asarray(indices) != 0
+    if hits.ndim != 2 or hits.shape[0] == 0:
+        return recall(indices, topk), mrr(indices, topk), ndcg(indices, topk)
+    nrow, ncol = hits.shape
+    first = _first_hit(hits)
+    disc = 1.0 / np.log(np.arange(ncol) + 2.0)
+    cumdcg = np.concatenate([[0.0], np.cumsum(np.count_nonzero(hits, axis=0) * disc)])
+    cumdisc = np.concatenate([[0.0], np.cumsum(disc)])
+    cmax = np.maximum(np.count_nonzero(hits, axis=1), 1)
+    r, m, n = [], [], []
+    for k in topk:
+        sel = first < k
+        r.append(int(sel.sum()))
+        m.append(float(np.sum(1.0 / (first[sel] + 1))) if sel.any() else 0)
+        kk = min(max(k, 0), ncol)
+        dcg = float(cumdcg[kk])
+        idcg = float(cumdisc[np.minimum(cmax, max(k, 0))].sum()) if k > 0 else 0.0
+        n.append(dcg / idcg if idcg else math.nan)
+    return r, m, n
+
+
 def get_metrics(indices, topk: Sequence[int]) -> Dict[str, float]:
-    r, m, n = recall(indices, topk), mrr(indices, topk), ndcg(indices, topk)
+    r, m, n = _metrics_fast(indices, topk)
     res = {}
     for name, vals in zip(["Recall@", "MRR@", "NDCG@"], [r, m, n]):
         for k, v in zip(topk, vals):

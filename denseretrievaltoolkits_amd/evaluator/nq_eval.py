@@ -194,9 +194,11 @@ class RowAnswerMatcher:
 
     def fill(self, rows, text_of) -> int:
         """Tokenise every row of ``rows`` not tokenised yet (``text_of(row)`` -> passage text)."""
-        rows = np.unique(np.asarray(rows)[np.asarray(rows) >= 0])
-        miss = rows[self.slot[rows] < 0]
+        r = np.asarray(rows).reshape(-1)
+        r = r[r >= 0]
+        miss = r[self.slot[r] < 0]          # a gather; np.unique only over the (usually no) misses
         if miss.size:
+            miss = np.unique(miss)
             v = self.vocab
             toks_list = tokenize_uncased_many([text_of(r) for r in miss.tolist()])
             mx = max((len(t) for t in toks_list), default=0)
@@ -213,8 +215,13 @@ class RowAnswerMatcher:
         """(token-id lists of the answers that can match, every): unknown tokens or answers longer
         than the width never match; an empty answer matches every passage."""
         out = []
+        cache = self.__dict__.setdefault("_ans_words", {})
+        if len(cache) > 1 << 20:
+            cache.clear()
         for ans in answers_i:
-            aw = tokenize_uncased(unicodedata.normalize("NFD", ans))
+            aw = cache.get(ans)
+            if aw is None:   # tokenised once per distinct answer string (the vocabulary lookup is not
+                aw = cache[ans] = tokenize_uncased(unicodedata.normalize("NFD", ans))   # cached: it grows)
             if not aw:
                 return [], True
             ids = [self.vocab.get(w, -2) for w in aw]
