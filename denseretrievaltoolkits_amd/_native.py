@@ -90,6 +90,8 @@ _SIGNATURES = [
                                  c_vp]),
     ("drt_gelu_bf16", c_i32, [c_vp, c_i64, c_vp, c_vp]),
     ("drt_embedding_bwd", c_i32, [c_vp, c_vp, c_vp, c_i64, c_i64, c_i32, c_i64, c_vp, c_vp, c_vp, c_vp]),
+    ("drt_embedding_bwd_types", c_i32, [c_vp, c_vp, c_i32, c_vp, c_i64, c_i64, c_i32, c_i64, c_vp, c_vp, c_vp,
+                                         c_vp]),
     ("drt_attention_train_fwd_bf16", c_i32, [c_vp, c_vp, c_vp, c_vp, c_i64, c_i64, c_i32, c_i32, c_f32, c_f32,
                                              ctypes.c_uint64, ctypes.c_uint64, c_vp]),
     ("drt_attention_train_bwd_bf16", c_i32, [c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_i64, c_i64, c_i32, c_i32, c_f32,

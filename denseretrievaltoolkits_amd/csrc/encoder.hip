@@ -73,19 +73,36 @@ __global__ __launch_bounds__(256) void gelu_kernel(const __bf16* x, int64_t n, _
 
 // Embedding backward (BertEmbeddings, modeling_bert.py:68-108): the gradient of the pre-LN sum
 // goes to the word / position / token-type tables (fp32, caller zeroes them).
-// Word rows: one block per token, fp32 atomics (the row ids are spread over the vocabulary);
-// token-type rows the same way when type ids are given.
-__global__ __launch_bounds__(256) void embedding_bwd_word_kernel(const int64_t* ids, const int64_t* type_ids,
-                                                                 const __bf16* d, int H, int64_t padding_idx,
-                                                                 float* dword, float* dtype) {
+// Word rows: one block per token, fp32 atomics (the row ids are spread over the vocabulary).
+__global__ __launch_bounds__(256) void embedding_bwd_word_kernel(const int64_t* ids, const __bf16* d, int H,
+                                                                 int64_t padding_idx, float* dword) {
   const int64_t t = (int64_t)blockIdx.x;
   const int64_t id = ids[t];
-  const int64_t tt = type_ids ? type_ids[t] : 0;
-  for (int c = threadIdx.x; c < H; c += 256) {
+  if (id == padding_idx) return;   // nn.Embedding(padding_idx): the row stays 0
+  for (int c = threadIdx.x; c < H; c += 256) atomicAdd(dword + id * H + c, (float)d[t * H + c]);
+}
+
+// Token-type rows with type ids (BERT: 2 rows, every token adds to one of them -- per-token atomics
+// were T-way contended): a block sums one column slab over a chunk of kTypeChunk tokens per type
+// in registers and adds once per (chunk, element).  Grid (column slabs, token chunks).
+constexpr int kTypeChunk = 1024;
+constexpr int kMaxTypes = 4;
+__global__ __launch_bounds__(256) void embedding_bwd_type_kernel(const int64_t* type_ids, const __bf16* d, int64_t T,
+                                                                 int H, int ntypes, float* dtype) {
+  const int c = blockIdx.x * 256 + threadIdx.x;
+  if (c >= H) return;
+  const int64_t t0 = (int64_t)blockIdx.y * kTypeChunk;
+  const int64_t t1 = t0 + kTypeChunk < T ? t0 + kTypeChunk : T;
+  float s[kMaxTypes] = {0.f, 0.f, 0.f, 0.f};
+  for (int64_t t = t0; t < t1; ++t) {
+    const int64_t tt = type_ids[t];
     const float g = (float)d[t * H + c];
-    if (id != padding_idx) atomicAdd(dword + id * H + c, g);   // nn.Embedding(padding_idx): row stays 0
-    if (type_ids) atomicAdd(dtype + tt * H + c, g);
+#pragma unroll
+    for (int y = 0; y < kMaxTypes; ++y) s[y] += tt == y ? g : 0.0f;
   }
+#pragma unroll
+  for (int y = 0; y < kMaxTypes; ++y)
+    if (y < ntypes && s[y] != 0.0f) atomicAdd(dtype + (int64_t)y * H + c, s[y]);
 }
 
 // Position rows: every sequence adds to rows 0..L-1, so per-element atomics from every token were
@@ -522,20 +539,31 @@ int drt_gelu_bf16(const void* x, int64_t n, void* y, void* stream) {
   return hip_status(hipGetLastError());
 }
 
-int drt_embedding_bwd(const int64_t* ids, const int64_t* type_ids, const void* d, int64_t B, int64_t L, int32_t H,
-                      int64_t padding_idx, float* dword, float* dpos, float* dtype, void* stream) {
-  DRT_REQUIRE(B >= 0 && L > 0 && H > 0);
+int drt_embedding_bwd_types(const int64_t* ids, const int64_t* type_ids, int32_t ntypes, const void* d, int64_t B,
+                            int64_t L, int32_t H, int64_t padding_idx, float* dword, float* dpos, float* dtype,
+                            void* stream) {
+  DRT_REQUIRE(B >= 0 && L > 0 && H > 0 && ntypes >= 1 && (type_ids == nullptr || ntypes <= kMaxTypes));
   if (B == 0) return DRT_OK;
   DRT_REQUIRE(ids && d && dword && dpos && dtype);
   hipStream_t s = (hipStream_t)stream;
-  hipLaunchKernelGGL(embedding_bwd_word_kernel, dim3((unsigned)(B * L)), dim3(256), 0, s, ids, type_ids,
-                     (const __bf16*)d, (int)H, padding_idx, dword, dtype);
+  hipLaunchKernelGGL(embedding_bwd_word_kernel, dim3((unsigned)(B * L)), dim3(256), 0, s, ids, (const __bf16*)d,
+                     (int)H, padding_idx, dword);
   const unsigned cy = (unsigned)((H + 255) / 256), cz = (unsigned)((B + kPosChunk - 1) / kPosChunk);
   hipLaunchKernelGGL(embedding_bwd_pos_kernel, dim3((unsigned)L, cy, cz), dim3(256), 0, s, (const __bf16*)d, B, L,
                      (int)H, dpos);
-  if (!type_ids)
+  if (!type_ids) {
     hipLaunchKernelGGL(embedding_bwd_type0_kernel, dim3(cy), dim3(256), 0, s, (const float*)dpos, L, (int)H, dtype);
+  } else {
+    const int64_t T = B * L;
+    hipLaunchKernelGGL(embedding_bwd_type_kernel, dim3(cy, (unsigned)((T + kTypeChunk - 1) / kTypeChunk)), dim3(256),
+                       0, s, type_ids, (const __bf16*)d, T, (int)H, (int)ntypes, dtype);
+  }
   return hip_status(hipGetLastError());
+}
+
+int drt_embedding_bwd(const int64_t* ids, const int64_t* type_ids, const void* d, int64_t B, int64_t L, int32_t H,
+                      int64_t padding_idx, float* dword, float* dpos, float* dtype, void* stream) {
+  return drt_embedding_bwd_types(ids, type_ids, type_ids ? 2 : 1, d, B, L, H, padding_idx, dword, dpos, dtype, stream);
 }
 
 int drt_embed_ln(const int64_t* ids, const int64_t* type_ids, int64_t B, int64_t L, const float* word_emb,

@@ -189,14 +189,13 @@ class DRModel(nn.Module):
             why = f"feature {self.feature!r}"
         elif not next(model.parameters()).is_cuda:
             why = "tower on the CPU"
-        elif "token_type_ids" in items:
-            why = "token_type_ids given"
         elif items["input_ids"].shape[1] > MAX_TRAIN_SEQ:
             why = f"sequence length {items['input_ids'].shape[1]} > {MAX_TRAIN_SEQ}"
         else:
             why = tower_supported(model)
         if why is None:
-            hidden = train_hidden(model, items["input_ids"], items.get("attention_mask"))
+            hidden = train_hidden(model, items["input_ids"], items.get("attention_mask"),
+                                  token_type_ids=items.get("token_type_ids"))
         else:
             _log_fallback(why)
             out = model(**items, return_dict=True)

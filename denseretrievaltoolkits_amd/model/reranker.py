@@ -107,14 +107,15 @@ class RRModel(nn.Module):
             hidden = enc(items["input_ids"], mask, items.get("token_type_ids"))
             _, rb = enc.pool(hidden, mask, self.pooling, want_bf16=True)
             return linear_head(rb, w)  # [B, 1] fp32
-        if (dev.type == "cuda" and self.feature == "last_hidden_state" and "token_type_ids" not in items
+        if (dev.type == "cuda" and self.feature == "last_hidden_state"
                 and tower_supported(self.lm) is None and items["input_ids"].shape[1] <= MAX_TRAIN_SEQ):
             # pair forward + backward on the HIP training tower (model/train_tower.py)
-            hidden = train_hidden(self.lm, items["input_ids"], items.get("attention_mask"))
+            hidden = train_hidden(self.lm, items["input_ids"], items.get("attention_mask"),
+                                  token_type_ids=items.get("token_type_ids"))
         else:
             from .biencoder import _log_fallback
             _log_fallback("reranker: " + ("tower on the CPU" if dev.type != "cuda" else
-                                          tower_supported(self.lm) or "feature / token_type_ids / length"))
+                                          tower_supported(self.lm) or "feature / length"))
             out = self.lm(**items, return_dict=True)
             hidden = getattr(out, self.feature)
         if self.pooling == "first":

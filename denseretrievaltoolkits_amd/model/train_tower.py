@@ -134,9 +134,10 @@ def dropout_sites(layer: int):
 class _Step:
     """What every node of one tower pass shares: weights, shape, masks' inputs, dropout."""
 
-    def __init__(self, model, W: _Weights, ids, mask, drop):
+    def __init__(self, model, W: _Weights, ids, mask, drop, types=None):
         cfg = model.config
         self.model, self.W, self.ids, self.mask, self.drop = model, W, ids, mask, drop
+        self.types = types   # token_type_ids [B, L] int64 or None (all type 0)
         self.B, self.L = ids.shape
         self.H, self.heads, self.eps = cfg.hidden_size, cfg.num_attention_heads, float(cfg.layer_norm_eps)
         self.scale = 1.0 / (self.H // self.heads) ** 0.5
@@ -151,7 +152,8 @@ def embed_forward(st: _Step):
     T = st.B * st.L
     h = torch.empty((T, st.H), dtype=torch.bfloat16, device=st.dev)
     emb_pre = torch.empty_like(h)
-    _native.check(lib.drt_embed_ln_pre(st.ids.data_ptr(), None, st.B, st.L, W.word.data_ptr(), W.pos.data_ptr(),
+    _native.check(lib.drt_embed_ln_pre(st.ids.data_ptr(), _ptr(st.types), st.B, st.L, W.word.data_ptr(),
+                                       W.pos.data_ptr(),
                                        W.type.data_ptr(), W.emb_g.data_ptr(), W.emb_b.data_ptr(), st.eps, st.H,
                                        h.data_ptr(), emb_pre.data_ptr(), s), "drt_embed_ln_pre")
     ph, _, seed = st.drop
@@ -172,9 +174,10 @@ def embed_backward(st: _Step, emb_pre, d) -> Dict[str, torch.Tensor]:
     dpos = torch.zeros_like(W.pos)
     dtype = torch.zeros_like(W.type)
     pad = st.model.embeddings.word_embeddings.padding_idx
-    _native.check(lib.drt_embedding_bwd(st.ids.data_ptr(), None, demb.data_ptr(), st.B, st.L, st.H,
-                                        -1 if pad is None else int(pad), dword.data_ptr(), dpos.data_ptr(),
-                                        dtype.data_ptr(), s), "drt_embedding_bwd")
+    _native.check(lib.drt_embedding_bwd_types(st.ids.data_ptr(), _ptr(st.types), int(W.type.shape[0]),
+                                              demb.data_ptr(), st.B, st.L, st.H, -1 if pad is None else int(pad),
+                                              dword.data_ptr(), dpos.data_ptr(), dtype.data_ptr(), s),
+                  "drt_embedding_bwd_types")
     e = "embeddings."
     return {e + "word_embeddings.weight": dword, e + "position_embeddings.weight": dpos,
             e + "token_type_embeddings.weight": dtype, e + "LayerNorm.weight": dge, e + "LayerNorm.bias": dbe}
@@ -314,7 +317,7 @@ def _param_groups(model):
 
 
 def train_hidden(model, input_ids: torch.Tensor, attention_mask: Optional[torch.Tensor],
-                 seed: Optional[int] = None) -> torch.Tensor:
+                 seed: Optional[int] = None, token_type_ids: Optional[torch.Tensor] = None) -> torch.Tensor:
     """last_hidden_state fp32 [B, L, H] of ``model`` with the HIP tower backward attached (one autograd
     node per layer).  Dropout follows ``model.training`` and the config's probabilities (seed: torch
     CPU RNG)."""
@@ -324,6 +327,9 @@ def train_hidden(model, input_ids: torch.Tensor, attention_mask: Optional[torch.
     dev = next(model.parameters()).device
     ids = input_ids.to(dev, torch.int64).contiguous()
     mask = attention_mask.to(dev, torch.int64).contiguous() if attention_mask is not None else None
+    types = token_type_ids.to(dev, torch.int64).contiguous() if token_type_ids is not None else None
+    if types is not None and (types.shape != ids.shape or model.config.type_vocab_size > 4):
+        raise ValueError("HIP training tower: token_type_ids must match input_ids, type_vocab_size <= 4")
     B, L = ids.shape
     if L > MAX_TRAIN_SEQ:
         raise ValueError(f"HIP training tower: sequence length {L} > {MAX_TRAIN_SEQ}")
@@ -332,7 +338,7 @@ def train_hidden(model, input_ids: torch.Tensor, attention_mask: Optional[torch.
     pa = float(cfg.attention_probs_dropout_prob) if model.training else 0.0
     if seed is None:
         seed = int(torch.randint(0, 2 ** 62, (1,)).item()) if (ph > 0 or pa > 0) else 0
-    st = _Step(model, _Weights(model, dev), ids, mask, (ph, pa, seed))
+    st = _Step(model, _Weights(model, dev), ids, mask, (ph, pa, seed), types)
     named, emb, layers = _param_groups(model)
     h = _EmbedFn.apply(ids, st, emb, *[named[n] for n in emb])
     for i, names in enumerate(layers):

@@ -320,6 +320,12 @@ int drt_gelu_bf16(const void* x, int64_t n, void* y, void* stream);
 int drt_embedding_bwd(const int64_t* ids, const int64_t* type_ids, const void* d, int64_t B, int64_t L,
                       int32_t H, int64_t padding_idx, float* dword, float* dpos, float* dtype,
                       void* stream);
+/* drt_embedding_bwd with the token-type table's row count (type_vocab_size <= 4 when type_ids is
+ * given; BERT: 2): the type rows' gradients are per-type column sums over token chunks (drt_embedding_bwd
+ * assumes 2 rows).                                                                            */
+int drt_embedding_bwd_types(const int64_t* ids, const int64_t* type_ids, int32_t ntypes, const void* d,
+                            int64_t B, int64_t L, int32_t H, int64_t padding_idx, float* dword, float* dpos,
+                            float* dtype, void* stream);
 int drt_attention_bwd_bf16(const void* qkv, const void* ctx, const void* dctx, const float* lse,
                            const int64_t* mask, void* dqkv, int64_t B, int64_t L, int32_t heads,
                            int32_t head_dim, float scale, void* stream);

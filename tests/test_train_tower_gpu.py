@@ -23,17 +23,33 @@ def _bert(layers, seed, dev):
 
 @pytest.mark.parametrize("layers,B,L", [(2, 4, 64), (1, 8, 128), (2, 6, 32), (1, 4, 156)])
 def test_tower_grads_vs_hf_autograd(dev, layers, B, L):
+    _grads_vs_hf(dev, layers, B, L, types=False)
+
+
+@pytest.mark.parametrize("layers,B,L", [(1, 6, 64), (2, 4, 156)])
+def test_tower_grads_with_token_types_vs_hf_autograd(dev, layers, B, L):
+    """token_type_ids given (segment A = 0, segment B = 1, as a pair encoder would): the type
+    embeddings enter the forward and the type-row gradients come from per-type column sums."""
+    _grads_vs_hf(dev, layers, B, L, types=True)
+
+
+def _grads_vs_hf(dev, layers, B, L, types):
     import torch
     from denseretrievaltoolkits_amd.model.train_tower import train_hidden
     m_ref = _bert(layers, 11, dev).train()
     m_hip = _bert(layers, 11, dev).train()
     ids, mask = bw.token_batch(B, L, seed=L + B)
     ids_t, mask_t = torch.from_numpy(ids).to(dev), torch.from_numpy(mask).to(dev)
+    tt = None
+    if types:
+        rng = np.random.default_rng(L)
+        cut = rng.integers(1, L, size=(B, 1))
+        tt = torch.from_numpy((np.arange(L)[None, :] >= cut).astype(np.int64)).to(dev)
     g = torch.Generator(device=dev).manual_seed(5)
     R = torch.randn(B, L, 768, generator=g, device=dev)
-    ref = m_ref(input_ids=ids_t, attention_mask=mask_t).last_hidden_state
+    ref = m_ref(input_ids=ids_t, attention_mask=mask_t, token_type_ids=tt).last_hidden_state
     (ref * R).sum().backward()
-    hid = train_hidden(m_hip, ids_t, mask_t)
+    hid = train_hidden(m_hip, ids_t, mask_t, token_type_ids=tt)
     (hid * R).sum().backward()
     cos_h = torch.nn.functional.cosine_similarity(hid.flatten(), ref.detach().flatten(), dim=0).item()
     assert cos_h > 0.9999, cos_h
