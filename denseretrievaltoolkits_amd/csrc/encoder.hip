@@ -679,14 +679,13 @@ int drt_attention_train_fwd_bits_bf16(const void* qkv, const int64_t* mask, void
   if (!attr_set) {
     const void* ks[] = {(const void*)attention_fwd_kernel<0, false>, (const void*)attention_fwd_kernel<4, false>,
                         (const void*)attention_fwd_kernel<5, false>, (const void*)attention_fwd_kernel<4, true>,
-                        (const void*)attention_fwd_kernel<5, true>};
+                        (const void*)attention_fwd_kernel<5, true>, (const void*)attention_fwd_kernel<0, true>};
     for (const void* f : ks) DRT_CHECK_HIP(hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
     attr_set = true;
   }
   const dim3 grid((unsigned)(B * heads));
   hipStream_t s = (hipStream_t)stream;
   const bool drop = drop_p > 0.0f;
-  DRT_REQUIRE(!drop || nb <= 5);   // training shapes (the backward's L <= 160)
 #define DRT_AF_LAUNCH(NB_)                                                                              \
   case NB_: {                                                                                           \
     const dim3 blk(NB_ == 5 ? 320 : 256);                                                               \
@@ -700,7 +699,10 @@ int drt_attention_train_fwd_bits_bf16(const void* qkv, const int64_t* mask, void
     DRT_AF_LAUNCH(3)
     DRT_AF_LAUNCH(4)
     DRT_AF_LAUNCH(5)
-    default: hipLaunchKernelGGL((attention_fwd_kernel<0, false>), grid, dim3(256), lds, s, a); break;
+    default:   // 161 <= L <= 512 (the backward's streamed kernels)
+      if (drop) hipLaunchKernelGGL((attention_fwd_kernel<0, true>), grid, dim3(256), lds, s, a);
+      else hipLaunchKernelGGL((attention_fwd_kernel<0, false>), grid, dim3(256), lds, s, a);
+      break;
   }
 #undef DRT_AF_LAUNCH
   return hip_status(hipGetLastError());

@@ -292,7 +292,7 @@ struct AttnBwdArgs {
   uint64_t seed, site;
   const uint32_t* drop_bits;  // optional keep bits written by the forward ([B][heads][L][ceil(L/32)]);
                               // NULL: the same bits drawn again from the hash
-  float* dsum;                // optional [B][3H]: per-sequence column sums of dQKV (bias gradients)
+  float* dsum;                // optional [B][3H] (L > 160: [B][ceil(L / 128)][3H]): column sums of dQKV
 };
 
 __device__ __forceinline__ int ab_rc(int row, int chunk) { return row * kAbRow + ((chunk ^ ((row >> 1) & 7)) << 4); }
@@ -690,6 +690,353 @@ __global__ __launch_bounds__((NB == 5 ? 8 : 4) * 64, NB == 5 ? 1 : 2) void atten
   }
 }
 
+// ---------------------------------------------------------------------------
+// Attention backward for 160 < L <= 512 (BERT's max_position_embeddings; the whole-sequence kernel
+// above holds Qs, K, V, dO of the sequence in LDS, which stops at 160 rows): the same two phases,
+// each as its own kernel over 128-row groups, with the OTHER side streamed through LDS 32 rows at
+// a time (FlashAttention-2 style):
+//   dkdv: work-group = (sequence, head, 128 keys), wave = 32 keys (K, V fragments in registers);
+//         loop over the query blocks: Qs, dO rows (+ Dv from O, lse, keep words) staged in LDS;
+//   dq:   work-group = (sequence, head, 128 queries), wave = 32 queries (Qs, dO in registers);
+//         loop over the key blocks: K, V rows and the key bias staged in LDS.
+// Every score product, exponential and MFMA operand layout is the phase's of
+// attention_bwd_rk_kernel (same arithmetic per element).  The next block's global loads are issued
+// before the current block's matrix work (one barrier pair per block).  Dropout needs the forward's
+// keep bits (drt_attention_train_fwd_bits_bf16).  dsum: column sums per (sequence, 128-row group)
+// [B][G][3H], reduced in a fixed order by the caller (deterministic).
+// ---------------------------------------------------------------------------
+constexpr int kAblMaxSeq = 512;
+constexpr int kAblGroup = 128;   // rows per work-group (4 waves x 32)
+
+template <bool DROP>
+__global__ __launch_bounds__(256, 2) void attention_bwd_long_dkdv_kernel(AttnBwdArgs a) {
+  __shared__ __attribute__((aligned(16))) char Qs[32 * kAbRow];
+  __shared__ __attribute__((aligned(16))) char Os[32 * kAbRow];
+  __shared__ __attribute__((aligned(16))) float lse2[32];
+  __shared__ __attribute__((aligned(16))) float dvs[32];
+  __shared__ __attribute__((aligned(16))) uint32_t kw[4][32];
+  __shared__ __attribute__((aligned(16))) char Out[2][kAblGroup * kAbRow];   // dK, dV rows out
+  __shared__ float csum[4][2][64];
+  const int L = (int)a.L;
+  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+  const int r = lane & 31, h = lane >> 5;
+  const int64_t b = blockIdx.x / a.heads;
+  const int hd = blockIdx.x % a.heads;
+  const int grp = blockIdx.y;
+  const int64_t row0 = b * a.L;
+  const int64_t hrow = ((int64_t)b * a.heads + hd) * a.L;
+  const int64_t ld = 3 * (int64_t)a.H;
+  const int nkw = (L + 31) >> 5;                     // keep words per query row
+  const int nqb = nkw;                               // query blocks
+  const __bf16* Qg = a.qkv + row0 * ld + hd * 64;
+  const __bf16* Kg = Qg + a.H;
+  const __bf16* Vg = Qg + 2 * a.H;
+  const __bf16* Og = a.ctx + row0 * a.H + hd * 64;
+  const __bf16* dOg = a.dctx + row0 * a.H + hd * 64;
+  const int blk = grp * 4 + wave;                    // this wave's key block
+  const int key = blk * 32 + r;
+  const bool active = blk * 32 < L;                  // wave-uniform
+  const int keyc = key < L ? key : L - 1;
+  bf16x8 kf[4], vf[4];                               // B operands of S = Qs K^T, dP = dO V^T
+#pragma unroll
+  for (int k4 = 0; k4 < 4; ++k4) {
+    kf[k4] = *(const bf16x8*)(Kg + (int64_t)keyc * ld + (2 * k4 + h) * 8);
+    vf[k4] = *(const bf16x8*)(Vg + (int64_t)keyc * ld + (2 * k4 + h) * 8);
+    if (key >= L) {
+      kf[k4] = bf16x8{};
+      vf[k4] = bf16x8{};
+    }
+  }
+  const float kbias = (key >= L || (a.mask && a.mask[b * a.L + key] == 0)) ? -3.402823466e+38f : 0.0f;
+  const float inv = DROP ? 1.0f / (1.0f - a.drop_p) : 1.0f;
+  const AbOffsets off = ab_offsets(lane);
+  const uint32_t lanebit = 1u << r;
+
+  // staging of query block qb: thread (row = tid >> 3, chunk c = tid & 7)
+  const int srow = tid >> 3, sc = tid & 7;
+  bf16x8 gq, go, goo;
+  float glse = 0.f;
+  uint32_t gw = 0u;
+  auto load = [&](int qb) {
+    const int q = qb * 32 + srow;
+    gq = go = goo = bf16x8{};
+    if (q < L) {
+      gq = *(const bf16x8*)(Qg + (int64_t)q * ld + sc * 8);
+      go = *(const bf16x8*)(dOg + (int64_t)q * a.H + sc * 8);
+      goo = *(const bf16x8*)(Og + (int64_t)q * a.H + sc * 8);
+    }
+    if (tid < 32) glse = qb * 32 + tid < L ? a.lse[hrow + qb * 32 + tid] : 0.f;
+    if (DROP && tid < 128) {
+      const int w = tid >> 5, qq = qb * 32 + (tid & 31), kb = grp * 4 + w;
+      gw = (qq < L && kb < nkw) ? a.drop_bits[(hrow + qq) * nkw + kb] : 0u;
+    }
+  };
+  auto store = [&](int qb) {
+    float part = 0.f;
+    bf16x8 qv = gq;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      qv[j] = (__bf16)((float)qv[j] * a.scale);
+      part += (float)go[j] * (float)goo[j];
+    }
+    *(bf16x8*)(Qs + ab_rc(srow, sc)) = qv;
+    *(bf16x8*)(Os + ab_rc(srow, sc)) = go;
+    part += __shfl_xor(part, 1, 64);
+    part += __shfl_xor(part, 2, 64);
+    part += __shfl_xor(part, 4, 64);
+    if (sc == 0) dvs[srow] = part;
+    // rows past L: lse2 = +inf makes P = 0 (their dO is 0 too)
+    if (tid < 32) lse2[tid] = qb * 32 + tid < L ? glse * kLog2e : __builtin_inff();
+    if (DROP && tid < 128) kw[tid >> 5][tid & 31] = gw;
+  };
+
+  f32x16 dK[2], dV[2];
+#pragma unroll
+  for (int t = 0; t < 2; ++t)
+#pragma unroll
+    for (int e = 0; e < 16; ++e) {
+      dK[t][e] = 0.f;
+      dV[t][e] = 0.f;
+    }
+  load(0);
+  for (int qb = 0; qb < nqb; ++qb) {
+    store(qb);
+    __syncthreads();
+    if (qb + 1 < nqb) load(qb + 1);   // in flight during this block's matrix work
+    if (active) {
+      f32x16 sv, dp;
+#pragma unroll
+      for (int e = 0; e < 16; ++e) {
+        sv[e] = 0.f;
+        dp[e] = 0.f;
+      }
+#pragma unroll
+      for (int k4 = 0; k4 < 4; ++k4) {
+        const bf16x8 qa = *(const bf16x8*)(Qs + off.offA[k4]);
+        sv = __builtin_amdgcn_mfma_f32_32x32x16_bf16(qa, kf[k4], sv, 0, 0, 0);
+        const bf16x8 oa = *(const bf16x8*)(Os + off.offA[k4]);
+        dp = __builtin_amdgcn_mfma_f32_32x32x16_bf16(oa, vf[k4], dp, 0, 0, 0);
+      }
+      bf16x8 pa[2], sa[2];
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        const int q0 = 8 * g + 4 * h;
+        const f32x4 lq = *(const f32x4*)(lse2 + q0);
+        const f32x4 dq = *(const f32x4*)(dvs + q0);
+        u32x4 wk = {};
+        if (DROP) wk = *(const u32x4*)(&kw[wave][q0]);
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          const int e = 4 * g + u;
+          const float p = __builtin_amdgcn_exp2f(__builtin_fmaf(sv[e], kLog2e, kbias) - lq[u]);
+          float pd = p, ds;
+          if (DROP) {
+            const bool keep = (wk[u] & lanebit) != 0u;
+            pd = keep ? p : 0.f;
+            ds = p * __builtin_fmaf(keep ? dp[e] : 0.f, inv, -dq[u]);
+          } else {
+            ds = p * (dp[e] - dq[u]);
+          }
+          pa[e >> 3][e & 7] = (__bf16)pd;
+          sa[e >> 3][e & 7] = (__bf16)ds;
+        }
+      }
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks) {
+#pragma unroll
+        for (int t = 0; t < 2; ++t) {
+          const bf16x8 ob = ab_tr8o(Os + ks * 2048, off.offT[t][0], off.offT[t][1]);
+          dV[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(pa[ks], ob, dV[t], 0, 0, 0);
+          const bf16x8 qb8 = ab_tr8o(Qs + ks * 2048, off.offT[t][0], off.offT[t][1]);
+          dK[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(sa[ks], qb8, dK[t], 0, 0, 0);
+        }
+      }
+    }
+    __syncthreads();
+  }
+  // rows out through LDS: element (key row 8 (e >> 2) + 4 h + (e & 3) of the wave's block, column
+  // 32 t + r); dsum: the wave's column sums of the stored values, then the 4 waves in order
+#pragma unroll
+  for (int t = 0; t < 2; ++t) {
+    float sk = 0.f, sv2 = 0.f;
+#pragma unroll
+    for (int e = 0; e < 16; ++e) {
+      const int row = wave * 32 + 8 * (e >> 2) + 4 * h + (e & 3), col = 32 * t + r;
+      const __bf16 vk = (__bf16)dK[t][e];
+      const __bf16 vv = (__bf16)(DROP ? dV[t][e] * inv : dV[t][e]);
+      *(__bf16*)(Out[0] + ab_rc(row, col >> 3) + (col & 7) * 2) = vk;
+      *(__bf16*)(Out[1] + ab_rc(row, col >> 3) + (col & 7) * 2) = vv;
+      sk += (float)vk;
+      sv2 += (float)vv;
+    }
+    sk += __shfl_xor(sk, 32, 64);
+    sv2 += __shfl_xor(sv2, 32, 64);
+    if (h == 0) {
+      csum[wave][0][32 * t + r] = sk;
+      csum[wave][1][32 * t + r] = sv2;
+    }
+  }
+  __syncthreads();
+  for (int i = tid; i < kAblGroup * 8; i += 256) {   // 16 B per lane, 8 lanes per row
+    const int row = i >> 3, c = i & 7, kk = grp * kAblGroup + row;
+    if (kk < L) {
+      *(bf16x8*)(a.dqkv + (row0 + kk) * ld + a.H + hd * 64 + c * 8) = *(const bf16x8*)(Out[0] + ab_rc(row, c));
+      *(bf16x8*)(a.dqkv + (row0 + kk) * ld + 2 * a.H + hd * 64 + c * 8) = *(const bf16x8*)(Out[1] + ab_rc(row, c));
+    }
+  }
+  if (a.dsum && tid < 128) {   // [B][G][3H]
+    const int G = (L + kAblGroup - 1) / kAblGroup;
+    const int m = tid >> 6, col = tid & 63;   // m: 0 dK, 1 dV
+    a.dsum[((int64_t)b * G + grp) * 3 * a.H + (1 + m) * a.H + hd * 64 + col] =
+        csum[0][m][col] + csum[1][m][col] + csum[2][m][col] + csum[3][m][col];
+  }
+}
+
+template <bool DROP>
+__global__ __launch_bounds__(256, 2) void attention_bwd_long_dq_kernel(AttnBwdArgs a) {
+  __shared__ __attribute__((aligned(16))) char Ks[32 * kAbRow];
+  __shared__ __attribute__((aligned(16))) char Vs[32 * kAbRow];
+  __shared__ __attribute__((aligned(16))) float kb2[32];
+  __shared__ __attribute__((aligned(16))) char Out[kAblGroup * kAbRow];
+  __shared__ float csum[4][64];
+  const int L = (int)a.L;
+  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+  const int r = lane & 31, h = lane >> 5;
+  const int64_t b = blockIdx.x / a.heads;
+  const int hd = blockIdx.x % a.heads;
+  const int grp = blockIdx.y;
+  const int64_t row0 = b * a.L;
+  const int64_t hrow = ((int64_t)b * a.heads + hd) * a.L;
+  const int64_t ld = 3 * (int64_t)a.H;
+  const int nkw = (L + 31) >> 5;
+  const int nkb = nkw;
+  const __bf16* Qg = a.qkv + row0 * ld + hd * 64;
+  const __bf16* Kg = Qg + a.H;
+  const __bf16* Vg = Qg + 2 * a.H;
+  const __bf16* Og = a.ctx + row0 * a.H + hd * 64;
+  const __bf16* dOg = a.dctx + row0 * a.H + hd * 64;
+  const int blk = grp * 4 + wave;
+  const int q = blk * 32 + r;                        // this lane's query (D column)
+  const bool active = blk * 32 < L;
+  const int qc = q < L ? q : L - 1;
+  bf16x8 qf[4], of[4];                               // B operands of S^T = K Qs^T, dP^T = V dO^T
+  float part = 0.f;
+#pragma unroll
+  for (int k4 = 0; k4 < 4; ++k4) {
+    bf16x8 x = *(const bf16x8*)(Qg + (int64_t)qc * ld + (2 * k4 + h) * 8);
+    const bf16x8 o = *(const bf16x8*)(dOg + (int64_t)qc * a.H + (2 * k4 + h) * 8);
+    const bf16x8 oo = *(const bf16x8*)(Og + (int64_t)qc * a.H + (2 * k4 + h) * 8);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      x[j] = (__bf16)((float)x[j] * a.scale);
+      part += (float)o[j] * (float)oo[j];
+    }
+    qf[k4] = q < L ? x : bf16x8{};
+    of[k4] = q < L ? o : bf16x8{};
+  }
+  part += __shfl_xor(part, 32, 64);                 // Dv over the 64 d (the two lane halves)
+  const float dq = part;
+  const float lq = q < L ? a.lse[hrow + q] * kLog2e : __builtin_inff();
+  const float inv = DROP ? 1.0f / (1.0f - a.drop_p) : 1.0f;
+  const AbOffsets off = ab_offsets(lane);
+
+  const int srow = tid >> 3, sc = tid & 7;
+  bf16x8 gk, gv;
+  float gkb = 0.f;
+  uint32_t gw = 0u;
+  auto load = [&](int kb) {
+    const int kk = kb * 32 + srow;
+    gk = gv = bf16x8{};
+    if (kk < L) {
+      gk = *(const bf16x8*)(Kg + (int64_t)kk * ld + sc * 8);
+      gv = *(const bf16x8*)(Vg + (int64_t)kk * ld + sc * 8);
+    }
+    if (tid < 32) {
+      const int k2 = kb * 32 + tid;
+      gkb = (k2 >= L || (a.mask && a.mask[b * a.L + k2] == 0)) ? -3.402823466e+38f : 0.0f;
+    }
+    if (DROP) gw = q < L ? a.drop_bits[(hrow + q) * nkw + kb] : 0u;
+  };
+  auto store = [&]() {
+    *(bf16x8*)(Ks + ab_rc(srow, sc)) = gk;
+    *(bf16x8*)(Vs + ab_rc(srow, sc)) = gv;
+    if (tid < 32) kb2[tid] = gkb;
+  };
+  f32x16 dQ[2];
+#pragma unroll
+  for (int t = 0; t < 2; ++t)
+#pragma unroll
+    for (int e = 0; e < 16; ++e) dQ[t][e] = 0.f;
+  load(0);
+  for (int kb = 0; kb < nkb; ++kb) {
+    store();
+    const uint32_t wq0 = DROP ? gw >> (4 * h) : 0u;   // bit 8 g + u: key 8 g + 4 h + u of the block
+    __syncthreads();
+    if (kb + 1 < nkb) load(kb + 1);
+    if (active) {
+      f32x16 st, dpt;
+#pragma unroll
+      for (int e = 0; e < 16; ++e) {
+        st[e] = 0.f;
+        dpt[e] = 0.f;
+      }
+#pragma unroll
+      for (int k4 = 0; k4 < 4; ++k4) {
+        const bf16x8 ka = *(const bf16x8*)(Ks + off.offA[k4]);
+        st = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ka, qf[k4], st, 0, 0, 0);
+        const bf16x8 va = *(const bf16x8*)(Vs + off.offA[k4]);
+        dpt = __builtin_amdgcn_mfma_f32_32x32x16_bf16(va, of[k4], dpt, 0, 0, 0);
+      }
+      bf16x8 sa[2];
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        const f32x4 kbv = *(const f32x4*)(kb2 + 8 * g + 4 * h);
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          const int e = 4 * g + u;
+          const float p = __builtin_amdgcn_exp2f(__builtin_fmaf(st[e], kLog2e, kbv[u]) - lq);
+          float ds;
+          if (DROP) ds = p * __builtin_fmaf((wq0 & (1u << (8 * g + u))) != 0u ? dpt[e] : 0.f, inv, -dq);
+          else ds = p * (dpt[e] - dq);
+          sa[e >> 3][e & 7] = (__bf16)ds;
+        }
+      }
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks) {
+#pragma unroll
+        for (int t = 0; t < 2; ++t) {
+          const bf16x8 kt = ab_tr8o(Ks + ks * 2048, off.offT[t][0], off.offT[t][1]);
+          dQ[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(sa[ks], kt, dQ[t], 0, 0, 0);
+        }
+      }
+    }
+    __syncthreads();
+  }
+  // rows out: element (query row 8 (e >> 2) + 4 h + (e & 3) of the wave's block, column 32 t + r)
+#pragma unroll
+  for (int t = 0; t < 2; ++t) {
+    float sq = 0.f;
+#pragma unroll
+    for (int e = 0; e < 16; ++e) {
+      const int row = wave * 32 + 8 * (e >> 2) + 4 * h + (e & 3), col = 32 * t + r;
+      const __bf16 v = (__bf16)(dQ[t][e] * a.scale);
+      *(__bf16*)(Out + ab_rc(row, col >> 3) + (col & 7) * 2) = v;
+      sq += (float)v;
+    }
+    sq += __shfl_xor(sq, 32, 64);
+    if (h == 0) csum[wave][32 * t + r] = sq;
+  }
+  __syncthreads();
+  for (int i = tid; i < kAblGroup * 8; i += 256) {
+    const int row = i >> 3, c = i & 7, qq = grp * kAblGroup + row;
+    if (qq < L) *(bf16x8*)(a.dqkv + (row0 + qq) * ld + hd * 64 + c * 8) = *(const bf16x8*)(Out + ab_rc(row, c));
+  }
+  if (a.dsum && tid < 64) {
+    const int G = (L + kAblGroup - 1) / kAblGroup;
+    a.dsum[((int64_t)b * G + grp) * 3 * a.H + hd * 64 + tid] = csum[0][tid] + csum[1][tid] + csum[2][tid] + csum[3][tid];
+  }
+}
+
 // out = dropout(y) (+ resid): keep iff drop_hash24(seed, site, i) >= p 2^24, kept values scaled
 // by 1 / (1 - p).  The same call on a gradient (resid = NULL) is the dropout backward.
 __global__ __launch_bounds__(256) void dropout_add_kernel(const __bf16* y, const __bf16* resid, int64_t n, float p,
@@ -905,14 +1252,17 @@ int drt_attention_train_bwd_bits_bf16(const void* qkv, const void* ctx, const vo
                               site, nullptr, stream);
 }
 
+// Sized for any L <= 512: per-(sequence, 128-row group) partials [B][G <= 4][3H] + the colsum's own.
 size_t drt_attention_train_bwd_bias_workspace(int64_t B, int32_t heads, int32_t head_dim) {
   if (B <= 0 || heads <= 0 || head_dim <= 0) return 0;
   const int64_t n = 3 * (int64_t)heads * head_dim;
-  return (size_t)B * n * sizeof(float) + drt_colsum_workspace(B, n);
+  const int64_t gmax = kAblMaxSeq / kAblGroup;
+  return (size_t)B * gmax * n * sizeof(float) + drt_colsum_workspace(B * gmax, n);
 }
 
 // The same, also writing dbias [3H] fp32 = the column sums of dQKV (the query / key / value
-// bias gradients) from per-sequence partials the kernel leaves in ws -- no pass over dQKV.
+// bias gradients) from per-sequence (L > 160: per 128-row group) partials the kernels leave in ws,
+// reduced in a fixed order -- no pass over dQKV.
 int drt_attention_train_bwd_bias_bf16(const void* qkv, const void* ctx, const void* dctx, const float* lse,
                                       const int64_t* mask, const uint32_t* drop_bits, void* dqkv, int64_t B, int64_t L,
                                       int32_t heads, int32_t head_dim, float scale, float drop_p, uint64_t seed,
@@ -923,19 +1273,35 @@ int drt_attention_train_bwd_bias_bf16(const void* qkv, const void* ctx, const vo
                                 seed, site, part, stream);
   if (rc) return rc;
   const int64_t n = 3 * (int64_t)heads * head_dim;
-  return colsum_launch<float>(part, B, n, dbias, part + (size_t)B * n, (hipStream_t)stream);
+  const int64_t rows = L > kAbMaxSeq ? B * ((L + kAblGroup - 1) / kAblGroup) : B;
+  const int64_t gmax = kAblMaxSeq / kAblGroup;
+  return colsum_launch<float>(part, rows, n, dbias, part + (size_t)B * gmax * n, (hipStream_t)stream);
 }
 
 static int attention_bwd_launch(const void* qkv, const void* ctx, const void* dctx, const float* lse,
                                 const int64_t* mask, const uint32_t* drop_bits, void* dqkv, int64_t B, int64_t L,
                                 int32_t heads, int32_t head_dim, float scale, float drop_p, uint64_t seed,
                                 uint64_t site, float* dsum_part, void* stream) {
-  DRT_REQUIRE(B >= 0 && L > 0 && L <= kAbMaxSeq && heads > 0 && head_dim == 64);
+  DRT_REQUIRE(B >= 0 && L > 0 && L <= kAblMaxSeq && heads > 0 && head_dim == 64);
   DRT_REQUIRE(drop_p >= 0.0f && drop_p < 1.0f);
   if (B == 0) return DRT_OK;
   DRT_REQUIRE(qkv && ctx && dctx && lse && dqkv);
   AttnBwdArgs a{(const __bf16*)qkv, (const __bf16*)ctx, (const __bf16*)dctx, lse, mask, (__bf16*)dqkv, B, L,
                 heads, heads * 64, scale, drop_p, seed, site, drop_bits, dsum_part};
+  if (L > kAbMaxSeq) {   // streamed kernels: dK / dV over key groups, dQ over query groups
+    const bool drop = drop_p > 0.0f;
+    DRT_REQUIRE(!drop || drop_bits);   // the forward's keep bits (drt_attention_train_fwd_bits_bf16)
+    const dim3 grid((unsigned)(B * heads), (unsigned)((L + kAblGroup - 1) / kAblGroup));
+    hipStream_t st = (hipStream_t)stream;
+    if (drop) {
+      hipLaunchKernelGGL((attention_bwd_long_dkdv_kernel<true>), grid, dim3(256), 0, st, a);
+      hipLaunchKernelGGL((attention_bwd_long_dq_kernel<true>), grid, dim3(256), 0, st, a);
+    } else {
+      hipLaunchKernelGGL((attention_bwd_long_dkdv_kernel<false>), grid, dim3(256), 0, st, a);
+      hipLaunchKernelGGL((attention_bwd_long_dq_kernel<false>), grid, dim3(256), 0, st, a);
+    }
+    return hip_status(hipGetLastError());
+  }
   const int Lp = ((int)L + 31) & ~31;
   const int nb = Lp / 32;
   const dim3 grid((unsigned)(B * heads));

@@ -10,7 +10,7 @@ biencoder.py:159-241).  What changes is where the arithmetic runs:
   LayerNorm statistics, pooling / head / L2-normalise kernels.  ``hidden`` is
   returned in bf16, ``reps`` in fp32.
 * encode with autograd (training, or eval mode with grad on, where the reference
-  returns differentiable reps) runs BERT towers up to L = 160 on the HIP training
+  returns differentiable reps) runs BERT towers up to L = 512 on the HIP training
   tower (model/train_tower.py: forward with saved bf16 activations + backward on
   HIP kernels, HF train-mode dropout regenerated from a counter hash; dropout is
   off in eval mode); other towers stay on the HF module under autograd.
@@ -85,7 +85,7 @@ class DRModel(nn.Module):
         self.loss_fn = nn.CrossEntropyLoss(reduction="mean")
         self.feature = feature
         self.pooling = pooling
-        self.hip_train = True   # HIP training tower for BERT towers with L <= 160 (set False: HF autograd)
+        self.hip_train = True   # HIP training tower for BERT towers with L <= 512 (set False: HF autograd)
         self.normalize = normalize
         self.model_args = model_args
         self.train_args = train_args

@@ -5,7 +5,7 @@ L = q_max_len + p_max_len = 160) -> pooling -> LinearHead(768 -> 1) score.  When
 no gradient can be asked for (grad mode off or a frozen tower) the whole pair
 tower runs on the HIP inference kernels (the same bf16 MFMA GEMMs + fused
 attention as the bi-encoder) and the 768 -> 1 head on the HIP GEMM; with grad on
-(training, or eval mode with grad) BERT pair towers up to L = 160 run on the HIP
+(training, or eval mode with grad) BERT pair towers up to L = 512 run on the HIP
 training tower (model/train_tower.py, forward + backward on HIP kernels, HF
 train-mode dropout), other towers on the HF module under autograd.  T5
 rerankers (logits of pos/neg tokens, :115-119) are outside the MI355X path.

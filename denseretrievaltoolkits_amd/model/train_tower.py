@@ -19,7 +19,8 @@ drop_hash24; the attention probabilities draw two keeps per 32-bit hash of (row 
 attn_row_key / attn_mix), so the backward regenerates the hidden-site masks instead of storing them
 and reads the attention keep bits the forward wrote (1 bit per probability); the seed comes from torch's CPU generator (``torch.manual_seed`` makes a step reproducible).  The
 masks are not HF's Philox stream: same distribution and semantics, different draws.
-Scope: L <= 160 (the reference recipe's p_max_len is 156, run.sh), erf GELU, head_dim 64; anything else
+Scope: L <= 512 (BERT max_position_embeddings; L <= 160 -- the recipe, p_max_len 156 -- runs the whole-sequence
+attention backward, longer sequences the streamed one), erf GELU, head_dim 64; anything else
 raises.
 """
 from __future__ import annotations
@@ -32,7 +33,7 @@ from .. import _native
 from .encoder import BertShape, _check_supported
 from .encoder_bwd import _ptr, layernorm_backward, linear_backward
 
-MAX_TRAIN_SEQ = 160
+MAX_TRAIN_SEQ = 512
 
 
 def tower_supported(model) -> Optional[str]:
@@ -331,9 +332,10 @@ def train_hidden(model, input_ids: torch.Tensor, attention_mask: Optional[torch.
     if types is not None and (types.shape != ids.shape or model.config.type_vocab_size > 4):
         raise ValueError("HIP training tower: token_type_ids must match input_ids, type_vocab_size <= 4")
     B, L = ids.shape
-    if L > MAX_TRAIN_SEQ:
-        raise ValueError(f"HIP training tower: sequence length {L} > {MAX_TRAIN_SEQ}")
     cfg = model.config
+    lmax = min(MAX_TRAIN_SEQ, int(cfg.max_position_embeddings))
+    if L > lmax:
+        raise ValueError(f"HIP training tower: sequence length {L} > {lmax}")
     ph = float(cfg.hidden_dropout_prob) if model.training else 0.0
     pa = float(cfg.attention_probs_dropout_prob) if model.training else 0.0
     if seed is None:

@@ -304,7 +304,9 @@ int drt_linear_wgrad_bf16(const void* dY, const void* X, float* dW, int64_t T, i
                           size_t ws_bytes, void* stream);
 /* drt_attention_bwd_bf16: dqkv [B*L, 3H] (dQ | dK | dV in qkv's packed layout) of the
  * attention forward, from qkv, its ctx = O, dctx = dO, the forward's lse and the key mask;
- * L <= 160, head_dim 64 (BertSelfAttention under autograd, modeling_bert.py:164-204).   */
+ * L <= 512, head_dim 64 (BertSelfAttention under autograd, modeling_bert.py:164-204);
+ * L <= 160: one work-group per (sequence, head) holding the sequence in LDS; 160 < L <= 512:
+ * streamed dK/dV and dQ kernels over 128-row groups (dropout there needs the forward's bits). */
 /* drt_embed_ln_pre: drt_embed_ln that also writes the bf16 pre-LN sum (word + type + pos).
  * drt_gelu_bf16: y = GELU(x) elementwise (erf form).
  * drt_embedding_bwd: scatter-add of d [B*L, H] (gradient of the pre-LN embedding sum) into
@@ -347,7 +349,8 @@ int drt_dropout_add_bf16(const void* y, const void* resid, int64_t n, float p, u
 /* The training attention pair with the dropout keep mask kept as bits: the forward writes
  * drop_bits [B][heads][L][ceil(L / 32)] u32 (bit key & 31 of word (query, key >> 5); only when
  * drop_p > 0 and drop_bits != NULL), the backward reads them instead of regenerating the hash
- * twice per (query, key).  Same masks, same results as the hash-regenerating pair.             */
+ * twice per (query, key).  Same masks, same results as the hash-regenerating pair.  For
+ * L > 160 with drop_p > 0 the backward requires drop_bits (DRT_EINVAL without).              */
 int drt_attention_train_fwd_bits_bf16(const void* qkv, const int64_t* mask, void* ctx, float* lse,
                                       uint32_t* drop_bits, int64_t B, int64_t L, int32_t heads,
                                       int32_t head_dim, float scale, float drop_p, uint64_t seed,
@@ -357,8 +360,9 @@ int drt_attention_train_bwd_bits_bf16(const void* qkv, const void* ctx, const vo
                                       int64_t L, int32_t heads, int32_t head_dim, float scale, float drop_p,
                                       uint64_t seed, uint64_t site, void* stream);
 /* drt_attention_train_bwd_bias_bf16: the same, also writing dbias [3H] fp32 = the column sums of
- * dQKV (the query / key / value bias gradients of BertSelfAttention) from per-sequence partials
- * left in ws (drt_attention_train_bwd_bias_workspace bytes), without a pass over dQKV.        */
+ * dQKV (the query / key / value bias gradients of BertSelfAttention) from per-sequence (L > 160:
+ * per 128-row group) partials left in ws (drt_attention_train_bwd_bias_workspace bytes, sized for
+ * any L <= 512), reduced in a fixed order, without a pass over dQKV.                          */
 size_t drt_attention_train_bwd_bias_workspace(int64_t B, int32_t heads, int32_t head_dim);
 int drt_attention_train_bwd_bias_bf16(const void* qkv, const void* ctx, const void* dctx, const float* lse,
                                       const int64_t* mask, const uint32_t* drop_bits, void* dqkv, int64_t B,

@@ -136,10 +136,12 @@ def test_linear_backward_vs_torch(dev, T, N, K):
     torch.testing.assert_close(db, bf.grad, atol=tol, rtol=1e-4)
 
 
-@pytest.mark.parametrize("B,L", [(4, 128), (3, 50), (6, 32), (2, 100), (3, 156), (2, 160), (2, 129)])
+@pytest.mark.parametrize("B,L", [(4, 128), (3, 50), (6, 32), (2, 100), (3, 156), (2, 160), (2, 129),
+                                 (3, 161), (2, 256), (3, 300), (2, 512)])
 def test_attention_bwd_vs_torch(dev, B, L):
     """drt_attention_bwd_bf16 (dQ | dK | dV) against torch fp32 autograd of the same attention
-    (scaled scores + HF key mask, softmax, P V) on the same bf16 qkv, with padded sequences."""
+    (scaled scores + HF key mask, softmax, P V) on the same bf16 qkv, with padded sequences;
+    L > 160 runs the streamed dK/dV + dQ kernels (128-row groups, ragged last group at 161, 300)."""
     import torch
     from denseretrievaltoolkits_amd import _native
     lib = _native.load()
@@ -387,13 +389,14 @@ def test_layernorm_bwd_drop_output_equals_dropout_kernel(dev, M, H):
         assert bool(((s_.double() - ref_s).abs() <= tol).all())
 
 
-@pytest.mark.parametrize("L,B", [(128, 6), (156, 5), (37, 9), (32, 4)])
+@pytest.mark.parametrize("L,B", [(128, 6), (156, 5), (37, 9), (32, 4), (200, 3), (512, 2)])
 def test_attention_dropout_bits_vs_hash_and_torch(dev, L, B):
     """drt_attention_train_fwd_bits_bf16 writes the attention-dropout keep mask as bits (the forward's
     outputs do not change, the bits are the hash's keep decisions); the backward that reads them and
     the one that draws the same bits again from the hash (C-ABI callers without bits) both
     match torch fp32 autograd of the same dropped attention (the mask from the host restatement of the
-    pairwise attention hash)."""
+    pairwise attention hash).  L > 160 (streamed backward): the bits are required -- a backward
+    without them is refused."""
     import torch
     from denseretrievaltoolkits_amd import _native
     from tests.test_train_tower_gpu import _attn_keep_py, _attn_keep_torch
@@ -417,10 +420,14 @@ def test_attention_dropout_bits_vs_hash_and_torch(dev, L, B):
                                                             lse.data_ptr(), bits.data_ptr() if use_bits else None,
                                                             B, L, heads, dh, scale, p, seed, site, s), "fwd")
         dqkv = torch.empty_like(qkv)
-        _native.check(lib.drt_attention_train_bwd_bits_bf16(qkv.data_ptr(), ctx.data_ptr(), dctx.data_ptr(),
-                                                            lse.data_ptr(), mask.data_ptr(),
-                                                            bits.data_ptr() if use_bits else None, dqkv.data_ptr(),
-                                                            B, L, heads, dh, scale, p, seed, site, s), "bwd")
+        rc = lib.drt_attention_train_bwd_bits_bf16(qkv.data_ptr(), ctx.data_ptr(), dctx.data_ptr(), lse.data_ptr(),
+                                                   mask.data_ptr(), bits.data_ptr() if use_bits else None,
+                                                   dqkv.data_ptr(), B, L, heads, dh, scale, p, seed, site, s)
+        if L > 160 and not use_bits:
+            assert rc != 0
+            dqkv = None
+        else:
+            _native.check(rc, "bwd")
         torch.cuda.synchronize()
         outs[use_bits] = (ctx, lse, dqkv, bits)
     assert torch.equal(outs[False][0], outs[True][0]) and torch.equal(outs[False][1], outs[True][1])
@@ -436,6 +443,8 @@ def test_attention_dropout_bits_vs_hash_and_torch(dev, L, B):
     ref = x.grad
     for use_bits in (False, True):
         dq = outs[use_bits][2]
+        if dq is None:
+            continue
         for name, sl in (("dQ", slice(0, H)), ("dK", slice(H, 2 * H)), ("dV", slice(2 * H, 3 * H))):
             got, want = dq[:, sl].float(), ref[:, sl]
             cos = torch.nn.functional.cosine_similarity(got.flatten(), want.flatten(), dim=0).item()

@@ -26,7 +26,7 @@ def test_tower_grads_vs_hf_autograd(dev, layers, B, L):
     _grads_vs_hf(dev, layers, B, L, types=False)
 
 
-@pytest.mark.parametrize("layers,B,L", [(1, 6, 64), (2, 4, 156)])
+@pytest.mark.parametrize("layers,B,L", [(1, 6, 64), (2, 4, 156), (1, 3, 256), (1, 2, 512)])
 def test_tower_grads_with_token_types_vs_hf_autograd(dev, layers, B, L):
     """token_type_ids given (segment A = 0, segment B = 1, as a pair encoder would): the type
     embeddings enter the forward and the type-row gradients come from per-type column sums."""
@@ -86,8 +86,8 @@ def test_tower_rejects_unsupported(dev):
     from transformers import BertModel
     from denseretrievaltoolkits_amd.model.train_tower import train_hidden
     m = BertModel(bw.bert_config(layers=1), add_pooling_layer=False).to(dev)
-    with pytest.raises(ValueError):                      # attention backward holds L <= 160 in LDS
-        train_hidden(m, torch.ones((1, 161), dtype=torch.int64, device=dev), None)
+    with pytest.raises(ValueError):                      # past max_position_embeddings
+        train_hidden(m, torch.ones((1, 513), dtype=torch.int64, device=dev), None)
 
 
 def test_gelu_forward_vs_torch(dev):
@@ -231,7 +231,7 @@ def _ref_forward_with_masks(m, ids, mask, ph, pa, seed):
     return x
 
 
-@pytest.mark.parametrize("layers,B,L", [(2, 4, 64), (1, 6, 128), (1, 3, 156)])
+@pytest.mark.parametrize("layers,B,L", [(2, 4, 64), (1, 6, 128), (1, 3, 156), (1, 2, 384)])
 def test_tower_with_dropout_vs_masked_fp32_reference(dev, layers, B, L):
     """Train-mode tower with HF's default dropout (0.1 / 0.1) against a functional fp32 BERT under
     autograd that applies the SAME hash masks: hidden states and every parameter gradient."""
