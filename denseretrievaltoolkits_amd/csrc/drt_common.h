@@ -15,6 +15,7 @@ typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef float f32x2 __attribute__((ext_vector_type(2)));   // v_pk_{fma,mul,add}_f32 operand pair
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 
 typedef __attribute__((address_space(3))) void lds_void;

@@ -331,12 +331,18 @@ void attention_fwd_kernel(AttnArgs a) {
         const bf16x8 kf = *(const bf16x8*)(Ks + kt * 128 + offK[st]);
         s = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kf, qf[st], s, 0, 0, 0);
       }
+      // element pairs on the packed FP32 path (v_pk_fma_f32 / v_pk_add_f32: two elements per issue)
       float mt = -__builtin_inff();
+      const f32x2 l2e = {kLog2e, kLog2e};
 #pragma unroll
       for (int g = 0; g < 4; ++g) {
         const f32x4 kbv = *(const f32x4*)(kb + kt + 8 * g + 4 * h);
-#pragma unroll
-        for (int u = 0; u < 4; ++u) s[4 * g + u] = __builtin_fmaf(s[4 * g + u], kLog2e, kbv[u]);
+        const f32x2 lo = __builtin_elementwise_fma(f32x2{s[4 * g], s[4 * g + 1]}, l2e, f32x2{kbv[0], kbv[1]});
+        const f32x2 hi = __builtin_elementwise_fma(f32x2{s[4 * g + 2], s[4 * g + 3]}, l2e, f32x2{kbv[2], kbv[3]});
+        s[4 * g] = lo[0];
+        s[4 * g + 1] = lo[1];
+        s[4 * g + 2] = hi[0];
+        s[4 * g + 3] = hi[1];
         mt = fmaxf(fmaxf(mt, fmaxf(s[4 * g], s[4 * g + 1])), fmaxf(s[4 * g + 2], s[4 * g + 3]));
       }
       mt = fmaxf(mt, __shfl_xor(mt, 32, 64));
@@ -351,12 +357,18 @@ void attention_fwd_kernel(AttnArgs a) {
         l *= alpha;
         m = mn;
       }
-      float ps = 0.0f;
+      const f32x2 mm = {m, m};
+      f32x2 psum = {0.0f, 0.0f};
 #pragma unroll
-      for (int e = 0; e < 16; ++e) {
-        s[e] = __builtin_amdgcn_exp2f(s[e] - m);
-        ps += s[e];
+      for (int e = 0; e < 16; e += 2) {
+        f32x2 v = f32x2{s[e], s[e + 1]} - mm;
+        v[0] = __builtin_amdgcn_exp2f(v[0]);
+        v[1] = __builtin_amdgcn_exp2f(v[1]);
+        psum += v;
+        s[e] = v[0];
+        s[e + 1] = v[1];
       }
+      float ps = psum[0] + psum[1];
       ps += __shfl_xor(ps, 32, 64);
       l += ps;
       if (DROP) {   // this lane's keys kt + 8 g + 4 h + {0,1,2,3}: pairs kt / 2 + 4 g + 2 h + {0, 1}

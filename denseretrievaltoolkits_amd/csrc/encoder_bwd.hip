@@ -335,6 +335,62 @@ __device__ __forceinline__ bf16x8 ab_tr8o(const char* img, int off0, int off1) {
   return v;
 }
 
+// Per-score-element work of the two phases on element PAIRS (v_pk_fma_f32 / v_pk_add_f32 /
+// v_pk_mul_f32 issue two fp32 lanes each; exp2 stays per element):
+//   P1 (lane = key, 4 queries e0..e0+3): P = exp2(S log2e + (kbias - lse2)), dS = P (keep dP / (1-p) - Dv)
+//   P2 (lane = query, 4 keys e0..e0+3):  P = exp2(S log2e + (kb2 - lse2)),   dS = P (keep dP / (1-p) - Dv)
+// Same roundings as the per-element form: fma(S, log2e, kbias - lse2) vs fma(S, log2e, kbias) - lse2 can
+// differ in the last bit of the exponent argument (checked against torch fp32, not bitwise).
+template <bool DROP>
+__device__ __forceinline__ void ab_p1_pairs(const f32x16& sv, const f32x16& dp, int e0, const f32x4& lq,
+                                            const f32x4& dq, float kbias, const u32x4& wk, uint32_t lanebit,
+                                            float inv, bf16x8 (&pa)[2], bf16x8 (&sa)[2]) {
+  const f32x2 l2e = {kLog2e, kLog2e}, kb = {kbias, kbias}, iv = {inv, inv};
+#pragma unroll
+  for (int u = 0; u < 4; u += 2) {
+    const int e = e0 + u;
+    const f32x2 c = kb - f32x2{lq[u], lq[u + 1]};
+    f32x2 x = __builtin_elementwise_fma(f32x2{sv[e], sv[e + 1]}, l2e, c);
+    f32x2 p = {__builtin_amdgcn_exp2f(x[0]), __builtin_amdgcn_exp2f(x[1])};
+    f32x2 ds, pd = p;
+    const f32x2 nd = -f32x2{dq[u], dq[u + 1]};
+    if (DROP) {
+      const bool k0 = (wk[u] & lanebit) != 0u, k1 = (wk[u + 1] & lanebit) != 0u;
+      pd = f32x2{k0 ? p[0] : 0.f, k1 ? p[1] : 0.f};
+      ds = p * __builtin_elementwise_fma(f32x2{k0 ? dp[e] : 0.f, k1 ? dp[e + 1] : 0.f}, iv, nd);
+    } else {
+      ds = p * (f32x2{dp[e], dp[e + 1]} + nd);
+    }
+    pa[e >> 3][e & 7] = (__bf16)pd[0];
+    pa[e >> 3][(e & 7) + 1] = (__bf16)pd[1];
+    sa[e >> 3][e & 7] = (__bf16)ds[0];
+    sa[e >> 3][(e & 7) + 1] = (__bf16)ds[1];
+  }
+}
+
+// wbits: bit u (u < 4) = keep of key e0 + u's pair element for this lane's query
+template <bool DROP>
+__device__ __forceinline__ void ab_p2_pairs(const f32x16& st, const f32x16& dpt, int e0, const f32x4& kbv, float lq,
+                                            float dq, uint32_t wbits, float inv, bf16x8 (&sa)[2]) {
+  const f32x2 l2e = {kLog2e, kLog2e}, lq2 = {lq, lq}, nd = {-dq, -dq}, iv = {inv, inv};
+#pragma unroll
+  for (int u = 0; u < 4; u += 2) {
+    const int e = e0 + u;
+    const f32x2 c = f32x2{kbv[u], kbv[u + 1]} - lq2;
+    const f32x2 x = __builtin_elementwise_fma(f32x2{st[e], st[e + 1]}, l2e, c);
+    const f32x2 p = {__builtin_amdgcn_exp2f(x[0]), __builtin_amdgcn_exp2f(x[1])};
+    f32x2 ds;
+    if (DROP) {
+      const f32x2 kd = {(wbits >> u) & 1u ? dpt[e] : 0.f, (wbits >> (u + 1)) & 1u ? dpt[e + 1] : 0.f};
+      ds = p * __builtin_elementwise_fma(kd, iv, nd);
+    } else {
+      ds = p * (f32x2{dpt[e], dpt[e + 1]} + nd);
+    }
+    sa[e >> 3][e & 7] = (__bf16)ds[0];
+    sa[e >> 3][(e & 7) + 1] = (__bf16)ds[1];
+  }
+}
+
 // NB = row blocks of 32 (Lp = 32 NB), NW = waves: one work-group per (sequence, head).
 // Exponentials as exp2(s log2e + kb2 - lse2) with the key bias and lse pre-scaled by log2e in
 // staging (one fma + one sub + v_exp per score); the dropout scale 1 / (1 - p) leaves the
@@ -534,21 +590,7 @@ __global__ __launch_bounds__((NB == 5 ? 8 : 4) * 64, NB == 5 ? 1 : 2) void atten
         const f32x4 dq = *(const f32x4*)(dv + q0);
         u32x4 wk = {};
         if (DROP) wk = *(const u32x4*)(kbits + blk * Lp + q0);
-#pragma unroll
-        for (int u = 0; u < 4; ++u) {
-          const int e = 4 * g + u;
-          const float p = __builtin_amdgcn_exp2f(__builtin_fmaf(sv[e], kLog2e, kbias) - lq[u]);
-          float pd = p, ds;
-          if (DROP) {
-            const bool keep = (wk[u] & lanebit) != 0u;
-            pd = keep ? p : 0.f;
-            ds = p * __builtin_fmaf(keep ? dp[e] : 0.f, inv, -dq[u]);
-          } else {
-            ds = p * (dp[e] - dq[u]);
-          }
-          pa[e >> 3][e & 7] = (__bf16)pd;
-          sa[e >> 3][e & 7] = (__bf16)ds;
-        }
+        ab_p1_pairs<DROP>(sv, dp, 4 * g, lq, dq, kbias, wk, lanebit, inv, pa, sa);
       }
       // dV += Pd^T dO, dK += dS^T Qs over the block's 32 queries (2 k-steps of 16, permuted rows)
 #pragma unroll
@@ -609,15 +651,7 @@ __global__ __launch_bounds__((NB == 5 ? 8 : 4) * 64, NB == 5 ? 1 : 2) void atten
 #pragma unroll
       for (int g = 0; g < 4; ++g) {
         const f32x4 kbv = *(const f32x4*)(kb2 + kbk * 32 + 8 * g + 4 * h);
-#pragma unroll
-        for (int u = 0; u < 4; ++u) {
-          const int e = 4 * g + u;
-          const float p = __builtin_amdgcn_exp2f(__builtin_fmaf(st[e], kLog2e, kbv[u]) - lq);
-          float ds;
-          if (DROP) ds = p * __builtin_fmaf((wq & (1u << (8 * g + u))) != 0u ? dpt[e] : 0.f, inv, -dq);
-          else ds = p * (dpt[e] - dq);
-          sa[e >> 3][e & 7] = (__bf16)ds;
-        }
+        ab_p2_pairs<DROP>(st, dpt, 4 * g, kbv, lq, dq, wq >> (8 * g), inv, sa);
       }
 #pragma unroll
       for (int ks = 0; ks < 2; ++ks) {
@@ -825,21 +859,7 @@ __global__ __launch_bounds__(256, 2) void attention_bwd_long_dkdv_kernel(AttnBwd
         const f32x4 dq = *(const f32x4*)(dvs + q0);
         u32x4 wk = {};
         if (DROP) wk = *(const u32x4*)(&kw[wave][q0]);
-#pragma unroll
-        for (int u = 0; u < 4; ++u) {
-          const int e = 4 * g + u;
-          const float p = __builtin_amdgcn_exp2f(__builtin_fmaf(sv[e], kLog2e, kbias) - lq[u]);
-          float pd = p, ds;
-          if (DROP) {
-            const bool keep = (wk[u] & lanebit) != 0u;
-            pd = keep ? p : 0.f;
-            ds = p * __builtin_fmaf(keep ? dp[e] : 0.f, inv, -dq[u]);
-          } else {
-            ds = p * (dp[e] - dq[u]);
-          }
-          pa[e >> 3][e & 7] = (__bf16)pd;
-          sa[e >> 3][e & 7] = (__bf16)ds;
-        }
+        ab_p1_pairs<DROP>(sv, dp, 4 * g, lq, dq, kbias, wk, lanebit, inv, pa, sa);
       }
 #pragma unroll
       for (int ks = 0; ks < 2; ++ks) {
@@ -991,15 +1011,7 @@ __global__ __launch_bounds__(256, 2) void attention_bwd_long_dq_kernel(AttnBwdAr
 #pragma unroll
       for (int g = 0; g < 4; ++g) {
         const f32x4 kbv = *(const f32x4*)(kb2 + 8 * g + 4 * h);
-#pragma unroll
-        for (int u = 0; u < 4; ++u) {
-          const int e = 4 * g + u;
-          const float p = __builtin_amdgcn_exp2f(__builtin_fmaf(st[e], kLog2e, kbv[u]) - lq);
-          float ds;
-          if (DROP) ds = p * __builtin_fmaf((wq0 & (1u << (8 * g + u))) != 0u ? dpt[e] : 0.f, inv, -dq);
-          else ds = p * (dpt[e] - dq);
-          sa[e >> 3][e & 7] = (__bf16)ds;
-        }
+        ab_p2_pairs<DROP>(st, dpt, 4 * g, kbv, lq, dq, wq0 >> (8 * g), inv, sa);
       }
 #pragma unroll
       for (int ks = 0; ks < 2; ++ks) {

@@ -11,13 +11,13 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from denseretrievaltoolkits_amd import _native  # noqa: E402
 
 
-def main(reps=10):
+def main(reps=10, shapes=((1024, 128), (1024, 156), (512, 32))):
     lib = _native.load()
     dev = torch.device("cuda", 0)
     s = _native.stream_ptr(dev)
     res = {}
     torch.manual_seed(0)
-    for B, L in ((1024, 128), (1024, 156), (512, 32)):
+    for B, L in shapes:
         H, heads = 768, 12
         T = B * L
         qkv = (0.5 * torch.randn(T, 3 * H, device=dev)).to(torch.bfloat16)
@@ -27,7 +27,8 @@ def main(reps=10):
         dqkv = torch.empty_like(qkv)
         mask = torch.ones(B, L, dtype=torch.int64, device=dev)
         bits = torch.empty((B, heads, L, (L + 31) // 32), dtype=torch.int32, device=dev)
-        for p, use_bits in ((0.0, False), (0.1, True), (0.1, False)):
+        # L > 160 (streamed backward): dropout needs the forward's bits, no hash variant
+        for p, use_bits in ((0.0, False), (0.1, True)) + (((0.1, False),) if L <= 160 else ()):
             bp = bits.data_ptr() if use_bits else None
 
             def fwd():
@@ -58,8 +59,14 @@ def main(reps=10):
         fwd_bytes = T * 3 * H * 2 + T * H * 2
         bwd_bytes = T * 3 * H * 2 + 2 * T * H * 2 + T * 3 * H * 2
         res[f"B{B}_L{L}_floor_us"] = {"fwd": round(fwd_bytes / 6.3e12 * 1e6, 1), "bwd": round(bwd_bytes / 6.3e12 * 1e6, 1)}
+        # matrix flops: forward S, PV; backward S, dP, dV, dK, dQ (the streamed L > 160 kernels recompute
+        # S and dP in the dQ pass: 7 products)
+        per = 2 * L * L * 64 * heads * B
+        res[f"B{B}_L{L}_gflop"] = {"fwd": round(2 * per / 1e9, 1), "bwd": round((5 if L <= 160 else 7) * per / 1e9, 1)}
     print(json.dumps(res))
 
 
 if __name__ == "__main__":
-    main(int(sys.argv[1]) if len(sys.argv) > 1 else 10)
+    # usage: attn_bwd_probe.py [reps] [BxL,BxL,...]
+    shp = tuple(tuple(int(v) for v in x.split("x")) for x in sys.argv[2].split(",")) if len(sys.argv) > 2 else None
+    main(int(sys.argv[1]) if len(sys.argv) > 1 else 10, *((shp,) if shp else ()))
