@@ -297,10 +297,16 @@ class DeviceRowMatcher:
         self._slots = h.n_slots
 
     def match_rows(self, rows: np.ndarray, text_of, answers) -> np.ndarray:
+        return self.match_rows_async(rows, text_of, answers).get()
+
+    def match_rows_async(self, rows: np.ndarray, text_of, answers) -> "_PendingMatch":
+        """match_rows enqueued on the matcher's stream; ``.get()`` waits for it (Trainer.evaluate
+        reads batch j's matches after enqueueing batch j + 1's, so the host never waits for the
+        comparison kernels of the batch it just handed over)."""
         import torch
         B, k = rows.shape
         if B == 0 or k == 0:
-            return np.zeros((B, k), dtype=np.int8)
+            return _PendingMatch(np.zeros((B, k), dtype=np.int8), None)
         h = self.h
         h.fill(rows, text_of)
         self._upload()
@@ -343,5 +349,18 @@ class DeviceRowMatcher:
             out.copy_(hit.to(torch.int8), non_blocking=True)
             done = torch.cuda.Event()
             done.record(self.stream)
-        done.synchronize()
-        return out.numpy().copy()
+        return _PendingMatch(out, done)
+
+
+class _PendingMatch:
+    """pos_index of one batch behind an event (DeviceRowMatcher.match_rows_async)."""
+    __slots__ = ("out", "done")
+
+    def __init__(self, out, done):
+        self.out, self.done = out, done
+
+    def get(self) -> np.ndarray:
+        if self.done is None:
+            return self.out
+        self.done.synchronize()
+        return self.out.numpy().copy()

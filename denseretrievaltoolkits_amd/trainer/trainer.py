@@ -297,8 +297,15 @@ class Trainer:
         """Yields (loader batch, ids [B, k] host) in loader order (all ranks call it together)."""
         windows = self._query_windows(query_loader)
         d = self.index.d
+
+        def encode_next():
+            w = next(windows, None)
+            return w, (self._encode_window(w) if w is not None else None)
+
+        nxt = encode_next()
         while True:
-            win = next(windows, None)
+            win, q_reps = nxt
+            nxt = None
             if self.world > 1:
                 # every rank takes part in every window's collectives until all are exhausted
                 n_local = 0 if win is None else sum(dd["input_ids"].shape[0] for _, dd in win)
@@ -309,12 +316,14 @@ class Trainer:
             if win is None:
                 q_reps = torch.empty((0, d), dtype=torch.float32, device=self.device)
                 win = []
-            else:
-                q_reps = self._encode_window(win)
             n = q_reps.shape[0]
             ids_all = np.empty((n, k), dtype=np.int64)
             done, bi, b0 = 0, 0, 0
             for row0, ids in self._search_rows(q_reps, k):
+                if nxt is None:
+                    # the next window's tower pass goes on the GPU behind this window's first search
+                    # runs, so it runs while the host matches this window's batches
+                    nxt = encode_next()
                 ids_all[row0: row0 + ids.shape[0]] = ids
                 done = row0 + ids.shape[0]
                 # hand out every loader batch whose rows are complete (host work overlaps the
@@ -329,6 +338,8 @@ class Trainer:
                 yield win[bi][0], ids_all[b0: b0 + nb]
                 b0 += nb
                 bi += 1
+            if nxt is None:
+                nxt = encode_next()
 
     def _doc_text(self, did_):
         t = self._doc_cache.get(did_)
@@ -373,10 +384,10 @@ class Trainer:
         def text_of(row):
             return self._doc_text(self.idx[row])
 
-        for batch, indices in self._eval_results(query_loader, k):
-            th = time.perf_counter()
-            pos_index = matcher.match_rows(indices, text_of, batch[2])
-            eval_num += len(indices)
+        def finish(pend):
+            # batch j's matches are read (and its metrics taken) after batch j + 1's are enqueued
+            batch, indices, match = pend
+            pos_index = match.get()
             if rdir:   # the retrieved documents are only needed for the retrieve/ output file
                 for indice in indices:
                     doc_id = [self.idx[row] for row in indice[indice >= 0]]
@@ -388,6 +399,22 @@ class Trainer:
             metrics = get_metrics(pos_index, topk)
             for key in m_all:
                 m_all[key] += metrics[key]
+
+        pend = None
+        for batch, indices in self._eval_results(query_loader, k):
+            th = time.perf_counter()
+            if hasattr(matcher, "match_rows_async"):
+                cur = (batch, indices, matcher.match_rows_async(indices, text_of, batch[2]))
+            else:
+                cur = (batch, indices, _Ready(matcher.match_rows(indices, text_of, batch[2])))
+            eval_num += len(indices)
+            if pend is not None:
+                finish(pend)
+            pend = cur
+            t_host += time.perf_counter() - th
+        if pend is not None:
+            th = time.perf_counter()
+            finish(pend)
             t_host += time.perf_counter() - th
         t2 = time.perf_counter()
         if rdir:
@@ -431,6 +458,17 @@ class Trainer:
             self.start_epoch = checkpoint["epoch"] + 1
             self.module.load(checkpoint["state_dict"])
             self.optimizer.load_state_dict(checkpoint["optimizer"])
+
+
+class _Ready:
+    """An already computed match result with the pending-match interface."""
+    __slots__ = ("v",)
+
+    def __init__(self, v):
+        self.v = v
+
+    def get(self):
+        return self.v
 
 
 class RRTrainer(Trainer):
