@@ -466,31 +466,12 @@ __device__ __forceinline__ void wave_flush_hits(const ScanArgs& a, int64_t qw, c
   }
 }
 
-// Round 4, DYN: tiles from a per-launch queue instead of the static grid stride.  Work-group g
-// scans chunk g (kChunkTiles tiles) first, then chunks taken from a counter (counts[qbase *
-// kCntStride + 1], zeroed with the hit counters): a work-group that starts late -- its CU still
-// busy with another stream's kernel (the previous batch's select / canonical-order tail,
-// drt_ip_topk_batches_bf16) -- takes fewer chunks instead of finishing its fixed share late.
-// The chunk indices sit in a 4-entry LDS ring; the take for chunk m+1 is issued (one lane, inline
-// asm, so hipcc inserts no vmcnt(0) drain for its result) when the DMA issue enters chunk m, and its
-// value is published NBUF + 2 tiles later: by then the wave has waited (vmcnt, in-order return) for
-// a tile issued after the take.  Same tiles, same per-tile arithmetic and hit order per row ->
-// identical keys; only which work-group scans a tile changes (the select sorts the hits).
-constexpr int kChunkTiles = 32;
-
-__device__ __forceinline__ uint32_t queue_take_async(uint32_t* ctr) {
-  uint32_t old;
-  asm volatile("global_atomic_add %0, %1, %2, off sc0" : "=v"(old) : "v"(ctr), "v"(1u) : "memory");
-  return old;
-}
-
-template <int D, bool DYN>
+template <int D>
 __global__ __launch_bounds__(512, 1) void ip_scan16r_kernel(ScanArgs a) {
   constexpr int NW = 8;
   using C = Scan16Cfg<D, NW>;
   constexpr int PD = C::NBUF;   // issue distance: every slot in use
   __shared__ __attribute__((aligned(16))) char smem[C::LDS_BYTES];
-  __shared__ int32_t chunk_ring[4];
 
   const int tid = threadIdx.x;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -505,29 +486,8 @@ __global__ __launch_bounds__(512, 1) void ip_scan16r_kernel(ScanArgs a) {
   const int64_t ntiles = (a.nrows + kT16 - 1) / kT16;
   const int64_t t0 = blockIdx.x;
   const int64_t tstep = gridDim.x;
-  const int64_t nchunk = (ntiles + kChunkTiles - 1) / kChunkTiles;
-  uint32_t* qctr = a.counts + qbase * kCntStride + 1;
-  int64_t my_tiles = 0;   // static schedule only
-  if (DYN) {
-    if (t0 >= nchunk) return;
-    if (tid == 0) {
-      chunk_ring[0] = (int32_t)t0;
-      chunk_ring[1] = (int32_t)(tstep + atomicAdd(qctr, 1u));
-    }
-  } else {
-    my_tiles = t0 < ntiles ? (ntiles - 1 - t0) / tstep + 1 : 0;
-    if (my_tiles == 0) return;
-  }
-  // tile at sequence position p (wave-uniform; DYN: from the chunk ring)
-  auto tile_at = [&](int64_t p, int64_t& tile) -> bool {
-    if (!DYN) {
-      tile = t0 + p * tstep;
-      return p < my_tiles;
-    }
-    const int32_t c = chunk_ring[(p / kChunkTiles) & 3];
-    tile = (int64_t)c * kChunkTiles + (p % kChunkTiles);
-    return c < nchunk && tile < ntiles;
-  };
+  const int64_t my_tiles = t0 < ntiles ? (ntiles - 1 - t0) / tstep + 1 : 0;
+  if (my_tiles == 0) return;
   const uint32_t ring = lds_addr_of(smem);
 
   // 16 queries per wave: qbase + 16 * wave + r
@@ -551,20 +511,16 @@ __global__ __launch_bounds__(512, 1) void ip_scan16r_kernel(ScanArgs a) {
   for (int s = 0; s < C::KS; ++s) asm volatile("" ::"v"(qf[s]));
   asm volatile("" ::"v"(tau));
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  if (DYN) lds_barrier();   // chunk_ring[0..1] visible
 
-  // prologue: positions 0 .. PD-1 in flight, position 0 landed and read into registers
-  int64_t issued = 0;   // positions issued (a prefix of the sequence)
+  // prologue: tiles 0 .. PD-1 in flight, tile 0 landed and read into registers
 #pragma unroll
-  for (int p = 0; p < PD; ++p) {
-    int64_t tile;
-    if (tile_at(p, tile)) {
-      issue_tile16<D, NW, true>(a, ring + p * C::TILE_BYTES, tile, wave, lane);
-      issued = p + 1;
-    }
-  }
+  for (int p = 0; p < PD; ++p)
+    if (p < my_tiles) issue_tile16<D, NW, true>(a, ring + p * C::TILE_BYTES, t0 + p * tstep, wave, lane);
   if (wave >= NW / 2) __builtin_amdgcn_s_setprio(1);
-  wait_tiles_younger<C::GLDS_PER_WAVE>((int)(issued - 1));
+  {
+    const int64_t last = my_tiles - 1 < PD - 1 ? my_tiles - 1 : PD - 1;
+    wait_tiles_younger<C::GLDS_PER_WAVE>((int)last);
+  }
   lds_barrier();
 
   const int sw = (r >> 1) & 7;
@@ -615,55 +571,29 @@ __global__ __launch_bounds__(512, 1) void ip_scan16r_kernel(ScanArgs a) {
 
   f32x4 accA, accB;
   int64_t rbA = 0, rbB = 0;
-  int buf = 0;   // slot of position it (its fragments are in af[])
-  uint32_t take = 0;        // DYN: pending queue take (lane 0 of wave 0)
-  int64_t take_pub = -1;    // DYN: iteration at which it is published to the chunk ring
-  int take_slot = 0;
+  int buf = 0;   // slot of tile it (its fragments are in af[])
   // one tile: barrier, ring refill, MFMAs (+ reads of the next tile), deferred epilogue of the
   // previous tile; the loop body runs two of them in sequence (accA / accB) so the fragment
-  // registers flow straight through and the accumulators are never selected at run time.
-  // Returns false when position it + 1 does not exist (the loop ends after this tile).
-  // total: the sequence length once known (static: my_tiles; DYN: set when the issue side meets the
-  // first invalid position -- PD ahead of the consumer, so always before the loop needs it)
-  int64_t total = DYN ? INT64_MAX : my_tiles;
-  if (DYN && issued < PD) total = issued;
+  // registers flow straight through and the accumulators are never selected at run time
   auto iter = [&](int64_t it, f32x4& acc, int64_t& rb, const f32x4& prev, int64_t rb_prev) {
-    int64_t tile;
-    tile_at(it, tile);
-    if (it + 1 < total) wait_tiles_younger<C::GLDS_PER_WAVE>((int)(issued - it - 2));
-    if (DYN && it == take_pub && tid == 0) chunk_ring[take_slot] = (int32_t)(tstep + take);
+    const int64_t tile = t0 + it * tstep;
+    if (it + 1 < my_tiles) {
+      const int64_t last = it + PD - 1 < my_tiles - 1 ? it + PD - 1 : my_tiles - 1;
+      wait_tiles_younger<C::GLDS_PER_WAVE>((int)(last - it - 1));
+    }
     lds_barrier();   // tile it+1 landed (every wave's share); slot(it) fully read
-    const int64_t p = it + PD;
-    if (DYN && p % kChunkTiles == 0 && p < total) {
-      // the issue enters chunk m = p / kChunkTiles: take chunk m + 1 (if chunk m is real)
-      const int64_t m = p / kChunkTiles;
-      if (chunk_ring[m & 3] < nchunk) {
-        if (tid == 0) take = queue_take_async(qctr);
-        take_pub = it + PD + 2;
-        take_slot = (int)((m + 1) & 3);
-      }
-    }
-    if (p < total) {
-      int64_t ntile;
-      if (tile_at(p, ntile)) {
-        issue_tile16<D, NW, true>(a, ring + buf * C::TILE_BYTES, ntile, wave, lane);
-        issued = p + 1;
-      } else {
-        total = p;
-      }
-    }
+    if (it + PD < my_tiles) issue_tile16<D, NW, true>(a, ring + buf * C::TILE_BYTES, tile + PD * tstep, wave, lane);
     const int nslot = buf + 1 == C::NBUF ? 0 : buf + 1;
     mma_roll(acc, nslot);
     if (it > 0) epilogue(prev, rb_prev);
     rb = tile * kT16 + 4 * kq;
     buf = nslot;
   };
-  int64_t it = 0;
-  for (; it < total; it += 2) {
+  for (int64_t it = 0; it < my_tiles; it += 2) {
     iter(it, accA, rbA, accB, rbB);
-    if (it + 1 < total) iter(it + 1, accB, rbB, accA, rbA);
+    if (it + 1 < my_tiles) iter(it + 1, accB, rbB, accA, rbA);
   }
-  if (total & 1) epilogue(accA, rbA);
+  if (my_tiles & 1) epilogue(accA, rbA);
   else epilogue(accB, rbB);
   if (wcnt) wave_flush_hits(a, qw, hk, hq, wcnt, lane);
 }
@@ -1362,10 +1292,7 @@ __global__ __launch_bounds__(kKthThreads) void kth_final_kernel(const uint32_t* 
                                                                 uint32_t* best, uint32_t* zero) {
   __shared__ uint32_t buf[kKthChunk];
   const int64_t q = blockIdx.x;
-  if (zero && threadIdx.x == 0) {   // the hit counter (+ the scan's tile queue counter)
-    zero[q * kCntStride] = 0;
-    zero[q * kCntStride + 1] = 0;
-  }
+  if (zero && threadIdx.x == 0) zero[q * kCntStride] = 0;
   const int tot = nlists * r;
   {
     uint32_t tmp[kKthChunk / kKthThreads];
@@ -1415,10 +1342,7 @@ __global__ __launch_bounds__(kRankThreads) void kth_rank_kernel(const uint32_t* 
   __shared__ int sh_bin;
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
   const int64_t q = blockIdx.x;
-  if (zero && tid == 0) {   // the hit counter (+ the scan's tile queue counter)
-    zero[q * kCntStride] = 0;
-    zero[q * kCntStride + 1] = 0;
-  }
+  if (zero && tid == 0) zero[q * kCntStride] = 0;
   const uint32_t* src = in + q * stride;
   constexpr uint32_t kPad = 0xFFFFFFFFu;
   // thread t holds keys j * 4096 + 4t + [0, 4), j < kRankPer / 4 (coalesced 16-B loads; stride % 4 == 0)
@@ -2434,8 +2358,7 @@ static int launch_scan_d(const ScanArgs& a, int mode, hipStream_t s) {
       if (dense_hits) hipLaunchKernelGGL((ip_scan16_kernel<D, SCAN_FILTER, 8, true>), grid, dim3(512), 0, s, a);
       else hipLaunchKernelGGL((ip_scan16_kernel<D, SCAN_FILTER, 8, false>), grid, dim3(512), 0, s, a);
     } else {
-      // tiles from the per-launch queue (zeroed with the hit counters; every filter caller zeroes them)
-      hipLaunchKernelGGL((ip_scan16r_kernel<D, true>), grid, dim3(512), 0, s, a);
+      hipLaunchKernelGGL((ip_scan16r_kernel<D>), grid, dim3(512), 0, s, a);
     }
   } else {
     hipLaunchKernelGGL((ip_scan16_kernel<D, SCAN_DENSE>), grid, dim3(512), 0, s, a);
@@ -2738,14 +2661,10 @@ int drt_ip_topk_exact_bf16(const void* Q, int64_t nq, const void* P, int64_t n, 
 
 // Consecutive query batches of one shard with the per-batch fixed work off the critical path: batch
 // b's tail (select + refine, latency-bound launches of one work-group per query) runs on side_stream
-// while batch b + 1's threshold stage (sample scan + k-th) and filter scan run on stream.  Two
-// workspace halves alternate between batches.  Outputs complete in stream order on return (stream
-// waits for the last tail).
-// false: batch b + 1's filter scan runs beside batch b's tail -- the scan takes its tiles from a
-// queue (ip_scan16r_kernel<D, true>), so work-groups delayed behind the tail's work-groups just
-// take fewer tiles.
-constexpr bool kBatchesScanWaitsTail = false;
-
+// while batch b + 1's threshold stage (sample scan + k-th) runs on stream; batch b + 1's filter scan
+// waits for batch b's tail (its persistent work-groups take every CU, and a work-group delayed behind
+// a tail kernel would finish its fixed tile share late).  Two workspace halves alternate between
+// batches.  Outputs complete in stream order on return (stream waits for the last tail).
 size_t drt_ip_topk_batches_workspace(int64_t batch, int64_t n, int32_t d, int32_t k) {
   if (batch <= 0 || !valid_dims(batch, n, d, k)) return 0;
   return 2 * align_up(make_plan(batch, n, k).total, 256);
@@ -2792,18 +2711,13 @@ int drt_ip_topk_batches_bf16(const void* Q, int64_t nq, int64_t batch, const voi
   for (int64_t b = 0; b < nb && rc == DRT_OK; ++b) {
     const TopkCall c = call(b);
     const int j = (int)(b & 1);
-    if (kBatchesScanWaitsTail && b > 0 && !ok(hipStreamWaitEvent(s, ev_tail[j ^ 1], 0))) break;
+    if (b > 0 && !ok(hipStreamWaitEvent(s, ev_tail[j ^ 1], 0))) break;
     if ((rc = topk_scan_stage(c, s)) != DRT_OK) break;
     if (!ok(hipEventRecord(ev_scan[j], s)) || !ok(hipStreamWaitEvent(side, ev_scan[j], 0))) break;
     if ((rc = topk_tail_stage(c, side)) != DRT_OK) break;
     if (!ok(hipEventRecord(ev_tail[j], side))) break;
     last_tail = b;
-    if (b + 1 < nb) {
-      // batch b + 1 reuses batch b - 1's workspace half: its threshold stage (which zeroes the
-      // hit / tile-queue counters) waits for that batch's tail
-      if (b > 0 && !ok(hipStreamWaitEvent(s, ev_tail[j ^ 1], 0))) break;
-      rc = topk_tau_stage(call(b + 1), s);   // overlaps batch b's tail
-    }
+    if (b + 1 < nb) rc = topk_tau_stage(call(b + 1), s);   // overlaps batch b's tail
   }
   // outputs complete in stream order (also after an error: nothing enqueued on side is left behind)
   if (last_tail >= 0) {
