@@ -2451,148 +2451,6 @@ static int launch_refine(RefineArgs& ra, hipStream_t s) {
   return hip_status(hipGetLastError());
 }
 
-// One query batch of ip_topk: its pointers and plan, so the three stages of the sampled path --
-// threshold (sample scan + k-th), filter scan, tail (select + refine) -- can be enqueued on
-// different streams (drt_ip_topk_batches_bf16) as well as back to back (ip_topk_impl).
-struct TopkCall {
-  const void* Q;
-  int64_t nq;
-  const void* P;
-  int64_t n;
-  int32_t d, k;
-  int64_t id_offset;
-  float* out_scores;
-  int64_t* out_ids;
-  int32_t* status;
-  char* w;
-  const float* stats;
-  TopkPlan p;
-  bool refine() const { return stats != nullptr && n > 0; }
-  float* tau() const { return (float*)(w + p.off_tau); }
-  uint32_t* cnt() const { return (uint32_t*)(w + p.off_cnt); }
-};
-
-static ScanArgs topk_scan_args(const TopkCall& c) {
-  ScanArgs a{};
-  a.Q = (const __bf16*)c.Q;
-  a.nq = c.nq;
-  a.ldq = c.d;
-  a.P = (const __bf16*)c.P;
-  a.ldp = c.d;
-  return a;
-}
-
-static SelectArgs topk_select_args(const TopkCall& c) {
-  SelectArgs sa{};
-  sa.k = c.k;
-  sa.nq = c.nq;
-  sa.out_scores = c.out_scores;
-  sa.out_ids = c.out_ids;
-  sa.ldo = c.k;
-  sa.id_offset = c.id_offset;
-  sa.status = c.status;
-  if (c.refine()) {   // kc candidates into the workspace, certified at k
-    sa.k = (int)c.p.kc;
-    sa.k_cert = c.k;
-    sa.out_scores = (float*)(c.w + c.p.off_cs);
-    sa.out_ids = (int64_t*)(c.w + c.p.off_ci);
-    sa.ldo = c.p.kc;
-  }
-  return sa;
-}
-
-static int topk_refine(const TopkCall& c, const float* tau, hipStream_t s) {
-  RefineArgs ra{};
-  ra.Q = (const __bf16*)c.Q;
-  ra.nq = c.nq;
-  ra.d = c.d;
-  ra.P = (const __bf16*)c.P;
-  ra.n_local = c.n;
-  ra.row_offset = c.id_offset;
-  ra.cs = (const float*)(c.w + c.p.off_cs);
-  ra.ci = (const int64_t*)(c.w + c.p.off_ci);
-  ra.kc = (int32_t)c.p.kc;
-  ra.k = c.k;
-  ra.stats = c.stats;
-  ra.delta = (float*)(c.w + c.p.off_delta);
-  ra.cnt = (int32_t*)(c.w + c.p.off_rcnt);
-  ra.status = c.status;
-  ra.out_s = c.out_scores;
-  ra.out_i = c.out_ids;
-  ra.tau = tau;
-  return launch_refine(ra, s);
-}
-
-// stage 1 (sampled plans): sample scan -> tau; the threshold kernel also zeroes the hit counters
-static int topk_tau_stage(const TopkCall& c, hipStream_t s) {
-  const TopkPlan& p = c.p;
-  ScanArgs a = topk_scan_args(c);
-  a.row0 = p.stride / 2;
-  a.nrows = p.m;
-  a.rstride = p.stride;
-  a.out = c.w + p.off_sample;
-  a.cap = align_up(p.m, 4);
-  int rc = launch_scan(a, c.d, SCAN_DENSE, s, PROF_SAMPLE);
-  if (rc) return rc;
-  float* tau = c.tau();
-  uint32_t* cnt = c.cnt();
-  const ProfPair pp = prof_begin(PROF_SELECT, s);
-  if (p.m <= kRankMaxKeys && p.r <= kRankBuf) {   // one launch: the whole sample row per work-group
-    // keys per thread sized to the sample (a sample of ~7k keys at 1M rows needs 8, not 80)
-    const uint32_t* smp = (const uint32_t*)(c.w + p.off_sample);
-    const int64_t ld = (int64_t)align_up(p.m, 4);
-    const unsigned nq = (unsigned)c.nq;
-    if (p.m <= (int64_t)kRankThreads * 8)
-      hipLaunchKernelGGL(kth_rank_kernel<8>, dim3(nq), dim3(kRankThreads), 0, s, smp, ld, p.m, (int)p.r, tau, cnt);
-    else if (p.m <= (int64_t)kRankThreads * 24)
-      hipLaunchKernelGGL(kth_rank_kernel<24>, dim3(nq), dim3(kRankThreads), 0, s, smp, ld, p.m, (int)p.r, tau, cnt);
-    else
-      hipLaunchKernelGGL(kth_rank_kernel<kRankPerMax>, dim3(nq), dim3(kRankThreads), 0, s, smp, ld, p.m, (int)p.r,
-                         tau, cnt);
-  } else {
-    hipLaunchKernelGGL(kth_partial_kernel, dim3((unsigned)p.nchunk, (unsigned)c.nq), dim3(kKthThreads), 0, s,
-                       (const uint32_t*)(c.w + p.off_sample), (int64_t)align_up(p.m, 4), p.m, (int)p.r,
-                       (uint32_t*)(c.w + p.off_part));
-    hipLaunchKernelGGL(kth_final_kernel, dim3((unsigned)c.nq), dim3(kKthThreads), 0, s,
-                       (const uint32_t*)(c.w + p.off_part), (int)p.nchunk, (int)p.r, (int64_t)p.r,
-                       (int64_t)(p.nchunk * p.r), tau, (uint32_t*)nullptr, cnt);   // also zeroes the hit counters
-  }
-  prof_end(pp, s);
-  return hip_status(hipGetLastError());
-}
-
-// stage 2: the filter scan against tau (hit counters zeroed by stage 1: one launch fewer than a memset)
-static int topk_scan_stage(const TopkCall& c, hipStream_t s) {
-  ScanArgs a = topk_scan_args(c);
-  a.row0 = 0;
-  a.nrows = c.n;
-  a.rstride = 1;
-  a.tau = c.tau();
-  a.counts = c.cnt();
-  a.out = c.w + c.p.off_keys;
-  a.cap = c.p.cap;
-  return launch_scan(a, c.d, SCAN_FILTER, s, PROF_SCAN);
-}
-
-// stage 3: select + certify (+ canonical order)
-static int topk_tail_stage(const TopkCall& c, hipStream_t s) {
-  SelectArgs sa = topk_select_args(c);
-  sa.in = c.w + c.p.off_keys;
-  sa.in_stride = c.p.cap;
-  sa.counts = c.cnt();
-  sa.cap = c.p.cap;
-  sa.n_total = c.n;
-  int rc = launch_select(sa, SEL_KEYS64, SEL_TOPK, s);
-  if (rc || !c.refine()) return rc;
-  return topk_refine(c, c.tau(), s);
-}
-
-static TopkCall topk_call(const void* Q, int64_t nq, const void* P, int64_t n, int32_t d, int32_t k,
-                          int64_t id_offset, float* out_scores, int64_t* out_ids, int32_t* status, void* ws,
-                          const float* stats) {
-  return TopkCall{Q, nq, P, n, d, k, id_offset, out_scores, out_ids, status, (char*)ws, stats, make_plan(nq, n, k)};
-}
-
 // One shard's top-k (drt_ip_topk_bf16); with row statistics (stats != NULL) the result is put in
 // the canonical exact-score order (refine stage above): the select keeps kc >= k candidates in the
 // workspace and the refine kernels write the k outputs.
@@ -2602,42 +2460,137 @@ static int ip_topk_impl(const void* Q, int64_t nq, const void* P, int64_t n, int
   DRT_REQUIRE(valid_dims(nq, n, d, k));
   if (nq == 0) return DRT_OK;
   DRT_REQUIRE(Q && out_scores && out_ids && ws);
-  const TopkCall c = topk_call(Q, nq, P, n, d, k, id_offset, out_scores, out_ids, status, ws, stats);
-  const TopkPlan& p = c.p;
+  const TopkPlan p = make_plan(nq, n, k);
   DRT_REQUIRE(ws_bytes >= p.total);
+  char* w = (char*)ws;
+  float* tau = (float*)(w + p.off_tau);
+  uint32_t* cnt = (uint32_t*)(w + p.off_cnt);
+  const bool refine = stats != nullptr && n > 0;
+
+  SelectArgs sa{};
+  sa.k = k;
+  sa.nq = nq;
+  sa.out_scores = out_scores;
+  sa.out_ids = out_ids;
+  sa.ldo = k;
+  sa.id_offset = id_offset;
+  sa.status = status;
+  if (refine) {   // kc candidates into the workspace, certified at k
+    sa.k = (int)p.kc;
+    sa.k_cert = k;
+    sa.out_scores = (float*)(w + p.off_cs);
+    sa.out_ids = (int64_t*)(w + p.off_ci);
+    sa.ldo = p.kc;
+  }
+  RefineArgs ra{};
+  ra.Q = (const __bf16*)Q;
+  ra.nq = nq;
+  ra.d = d;
+  ra.P = (const __bf16*)P;
+  ra.n_local = n;
+  ra.row_offset = id_offset;
+  ra.cs = (const float*)(w + p.off_cs);
+  ra.ci = (const int64_t*)(w + p.off_ci);
+  ra.kc = (int32_t)p.kc;
+  ra.k = k;
+  ra.stats = stats;
+  ra.delta = (float*)(w + p.off_delta);
+  ra.cnt = (int32_t*)(w + p.off_rcnt);
+  ra.status = status;
+  ra.out_s = out_scores;
+  ra.out_i = out_ids;
+
   if (n == 0) {
-    SelectArgs sa = topk_select_args(c);
-    sa.in = c.w + p.off_keys;
+    sa.in = w + p.off_keys;
     sa.in_stride = p.cap;
     sa.n_in = 0;
     sa.n_total = 0;
     return launch_select(sa, SEL_DENSE32, SEL_TOPK, s);
   }
   DRT_REQUIRE(P != nullptr);
+
+  ScanArgs a{};
+  a.Q = (const __bf16*)Q;
+  a.nq = nq;
+  a.ldq = d;
+  a.P = (const __bf16*)P;
+  a.ldp = d;
+
   if (!p.sample) {
     // Small shard: score every row densely, select directly.
-    ScanArgs a = topk_scan_args(c);
     a.row0 = 0;
     a.nrows = n;
     a.rstride = 1;
-    a.out = c.w + p.off_keys;
+    a.out = w + p.off_keys;
     a.cap = p.cap;
     int rc = launch_scan(a, d, SCAN_DENSE, s, PROF_SCAN);
     if (rc) return rc;
-    SelectArgs sa = topk_select_args(c);
-    sa.in = c.w + p.off_keys;
+    sa.in = w + p.off_keys;
     sa.in_stride = p.cap;
     sa.n_in = n;
     sa.n_total = n;
     rc = launch_select(sa, SEL_DENSE32, SEL_TOPK, s);
-    if (rc || !c.refine()) return rc;
-    return topk_refine(c, nullptr, s);   // every row was scored
+    if (rc || !refine) return rc;
+    ra.tau = nullptr;   // every row was scored
+    return launch_refine(ra, s);
   }
-  int rc = topk_tau_stage(c, s);
+
+  // 1. sample pass -> tau
+  a.row0 = p.stride / 2;
+  a.nrows = p.m;
+  a.rstride = p.stride;
+  a.out = w + p.off_sample;
+  a.cap = align_up(p.m, 4);
+  int rc = launch_scan(a, d, SCAN_DENSE, s, PROF_SAMPLE);
   if (rc) return rc;
-  rc = topk_scan_stage(c, s);
+  {
+    const ProfPair pp = prof_begin(PROF_SELECT, s);
+    if (p.m <= kRankMaxKeys && p.r <= kRankBuf) {   // one launch: the whole sample row per work-group
+      // keys per thread sized to the sample (a sample of ~7k keys at 1M rows needs 8, not 80)
+      const uint32_t* smp = (const uint32_t*)(w + p.off_sample);
+      const int64_t ld = (int64_t)align_up(p.m, 4);
+      if (p.m <= (int64_t)kRankThreads * 8)
+        hipLaunchKernelGGL(kth_rank_kernel<8>, dim3((unsigned)nq), dim3(kRankThreads), 0, s, smp, ld, p.m, (int)p.r,
+                           tau, cnt);
+      else if (p.m <= (int64_t)kRankThreads * 24)
+        hipLaunchKernelGGL(kth_rank_kernel<24>, dim3((unsigned)nq), dim3(kRankThreads), 0, s, smp, ld, p.m, (int)p.r,
+                           tau, cnt);
+      else
+        hipLaunchKernelGGL(kth_rank_kernel<kRankPerMax>, dim3((unsigned)nq), dim3(kRankThreads), 0, s, smp, ld, p.m,
+                           (int)p.r, tau, cnt);
+    } else {
+      hipLaunchKernelGGL(kth_partial_kernel, dim3((unsigned)p.nchunk, (unsigned)nq), dim3(kKthThreads), 0, s,
+                         (const uint32_t*)(w + p.off_sample), (int64_t)align_up(p.m, 4), p.m, (int)p.r,
+                         (uint32_t*)(w + p.off_part));
+      hipLaunchKernelGGL(kth_final_kernel, dim3((unsigned)nq), dim3(kKthThreads), 0, s,
+                         (const uint32_t*)(w + p.off_part), (int)p.nchunk, (int)p.r, (int64_t)p.r,
+                         (int64_t)(p.nchunk * p.r), tau, (uint32_t*)nullptr, cnt);   // also zeroes the hit counters
+    }
+    prof_end(pp, s);
+    DRT_CHECK_HIP(hipGetLastError());
+  }
+
+  // 2. filter pass (counters zeroed by the threshold kernel above: one launch fewer than a memset)
+  a.row0 = 0;
+  a.nrows = n;
+  a.rstride = 1;
+  a.tau = tau;
+  a.counts = cnt;
+  a.out = w + p.off_keys;
+  a.cap = p.cap;
+  rc = launch_scan(a, d, SCAN_FILTER, s, PROF_SCAN);
   if (rc) return rc;
-  return topk_tail_stage(c, s);
+
+  // 3. select + certify (4. canonical order)
+  sa.in = w + p.off_keys;
+  sa.in_stride = p.cap;
+  sa.counts = cnt;
+  sa.cap = p.cap;
+  sa.n_total = n;
+  rc = launch_select(sa, SEL_KEYS64, SEL_TOPK, s);
+  if (rc || !refine) return rc;
+  ra.tau = tau;
+  return launch_refine(ra, s);
 }
 
 }  // namespace drt
@@ -2657,78 +2610,6 @@ int drt_ip_topk_exact_bf16(const void* Q, int64_t nq, const void* P, int64_t n, 
   DRT_REQUIRE(stats != nullptr);
   return ip_topk_impl(Q, nq, P, n, d, k, id_offset, out_scores, out_ids, status, ws, ws_bytes, stats,
                       (hipStream_t)stream);
-}
-
-// Consecutive query batches of one shard with the per-batch fixed work off the critical path: batch
-// b's tail (select + refine, latency-bound launches of one work-group per query) runs on side_stream
-// while batch b + 1's threshold stage (sample scan + k-th) runs on stream; batch b + 1's filter scan
-// waits for batch b's tail (its persistent work-groups take every CU, and a work-group delayed behind
-// a tail kernel would finish its fixed tile share late).  Two workspace halves alternate between
-// batches.  Outputs complete in stream order on return (stream waits for the last tail).
-size_t drt_ip_topk_batches_workspace(int64_t batch, int64_t n, int32_t d, int32_t k) {
-  if (batch <= 0 || !valid_dims(batch, n, d, k)) return 0;
-  return 2 * align_up(make_plan(batch, n, k).total, 256);
-}
-
-int drt_ip_topk_batches_bf16(const void* Q, int64_t nq, int64_t batch, const void* P, int64_t n, int32_t d,
-                             int32_t k, int64_t id_offset, const float* stats, float* out_scores, int64_t* out_ids,
-                             int32_t* status, void* ws, size_t ws_bytes, void* stream, void* side_stream) {
-  DRT_REQUIRE(batch > 0 && valid_dims(nq, n, d, k) && valid_dims(batch, n, d, k));
-  if (nq == 0) return DRT_OK;
-  DRT_REQUIRE(Q && out_scores && out_ids && status && ws);
-  const size_t half = align_up(make_plan(batch, n, k).total, 256);
-  DRT_REQUIRE(ws_bytes >= 2 * half);
-  hipStream_t s = (hipStream_t)stream;
-  hipStream_t side = (hipStream_t)side_stream;
-  const int64_t nb = (nq + batch - 1) / batch;
-  auto call = [&](int64_t b) {
-    const int64_t q0 = b * batch, m = std::min<int64_t>(batch, nq - q0);
-    return topk_call((const __bf16*)Q + q0 * d, m, P, n, d, k, id_offset, out_scores + q0 * k, out_ids + q0 * k,
-                     status + q0, (char*)ws + (b & 1) * half, stats);
-  };
-  if (n == 0 || !make_plan(batch, n, k).sample || nb == 1 || side == nullptr || side == s) {
-    for (int64_t b = 0; b < nb; ++b) {
-      const TopkCall c = call(b);
-      const int rc = ip_topk_impl(c.Q, c.nq, P, n, d, k, id_offset, c.out_scores, c.out_ids, c.status, c.w, half,
-                                  stats, s);
-      if (rc) return rc;
-    }
-    return DRT_OK;
-  }
-  DRT_REQUIRE(P != nullptr);
-  hipEvent_t ev_scan[2] = {}, ev_tail[2] = {};
-  int rc = DRT_OK;
-  auto ok = [&](hipError_t e) {
-    if (rc == DRT_OK) rc = hip_status(e);
-    return rc == DRT_OK;
-  };
-  for (int j = 0; j < 2; ++j)
-    if (ok(hipEventCreateWithFlags(&ev_scan[j], hipEventDisableTiming))) ok(hipEventCreateWithFlags(&ev_tail[j], hipEventDisableTiming));
-  // the side stream starts behind everything already enqueued on stream (queries, outputs)
-  if (ok(hipEventRecord(ev_scan[1], s))) ok(hipStreamWaitEvent(side, ev_scan[1], 0));
-  if (rc == DRT_OK) rc = topk_tau_stage(call(0), s);
-  int64_t last_tail = -1;
-  for (int64_t b = 0; b < nb && rc == DRT_OK; ++b) {
-    const TopkCall c = call(b);
-    const int j = (int)(b & 1);
-    if (b > 0 && !ok(hipStreamWaitEvent(s, ev_tail[j ^ 1], 0))) break;
-    if ((rc = topk_scan_stage(c, s)) != DRT_OK) break;
-    if (!ok(hipEventRecord(ev_scan[j], s)) || !ok(hipStreamWaitEvent(side, ev_scan[j], 0))) break;
-    if ((rc = topk_tail_stage(c, side)) != DRT_OK) break;
-    if (!ok(hipEventRecord(ev_tail[j], side))) break;
-    last_tail = b;
-    if (b + 1 < nb) rc = topk_tau_stage(call(b + 1), s);   // overlaps batch b's tail
-  }
-  // outputs complete in stream order (also after an error: nothing enqueued on side is left behind)
-  if (last_tail >= 0) {
-    const hipError_t e = hipStreamWaitEvent(s, ev_tail[last_tail & 1], 0);
-    if (rc == DRT_OK) rc = hip_status(e);
-  }
-  for (int j = 0; j < 2; ++j) {
-    if (ev_scan[j]) (void)hipEventDestroy(ev_scan[j]);
-    if (ev_tail[j]) (void)hipEventDestroy(ev_tail[j]);
-  }
-  return rc;
 }
 
 int drt_row_stats_bf16(const void* P, int64_t n, int32_t d, float* stats, int32_t accumulate, void* stream) {

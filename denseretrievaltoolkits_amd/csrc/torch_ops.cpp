@@ -119,34 +119,6 @@ std::tuple<Tensor, Tensor, Tensor> ip_topk(const Tensor& q, const Tensor& p, int
   return {s, i, st};
 }
 
-// consecutive query batches of `batch` rows, the per-batch tails on a pool stream of q's device
-// (drt_ip_topk_batches_bf16); results complete in the current stream's order
-std::tuple<Tensor, Tensor, Tensor> ip_topk_batches(const Tensor& q_, const Tensor& p_, int64_t k, int64_t batch,
-                                                   int64_t id_offset, const c10::optional<Tensor>& stats) {
-  need(q_, "q", at::kBFloat16, 2);
-  need(p_, "p", at::kBFloat16, 2);
-  TORCH_CHECK_VALUE(q_.size(1) == p_.size(1), "q and p differ in dimension: ", q_.sizes(), " vs ", p_.sizes());
-  TORCH_CHECK_VALUE(batch > 0, "batch must be positive, got ", batch);
-  const c10::DeviceGuard g(q_.device());
-  const Tensor q = q_.contiguous(), p = p_.contiguous();
-  const int64_t nq = q.size(0), n = p.size(0), d = q.size(1);
-  Tensor s = at::empty({nq, k}, q.options().dtype(at::kFloat));
-  Tensor i = at::empty({nq, k}, q.options().dtype(at::kLong));
-  Tensor st = at::empty({nq}, q.options().dtype(at::kInt));
-  if (nq == 0) return {s, i, st};
-  const int64_t b = std::min<int64_t>(batch, nq);
-  const size_t wsb = drt_ip_topk_batches_workspace(b, n, (int32_t)d, (int32_t)k);
-  TORCH_CHECK_VALUE(wsb > 0, "unsupported ip_topk shape batch=", b, " n=", n, " d=", d, " k=", k,
-                    " (d % 64 == 0, d <= 1024, 1 <= k <= 2048)");
-  Tensor ws = workspace(q, wsb);
-  void* side = (void*)at::hip::getStreamFromPoolMasqueradingAsCUDA(false, q.device().index()).stream();
-  check_rc(drt_ip_topk_batches_bf16(q.data_ptr(), nq, b, n ? p.data_ptr() : nullptr, n, (int32_t)d, (int32_t)k,
-                                    id_offset, stats_ptr(stats, q), s.data_ptr<float>(), i.data_ptr<int64_t>(),
-                                    st.data_ptr<int32_t>(), ws.data_ptr(), wsb, stream_of(q), side),
-           "drt_ip_topk_batches_bf16");
-  return {s, i, st};
-}
-
 int64_t ip_topk_resolve(const Tensor& q_, const Tensor& p_, int64_t k, int64_t id_offset, Tensor& scores,
                         Tensor& ids, Tensor& status, const c10::optional<Tensor>& stats) {
   need(q_, "q", at::kBFloat16, 2);
@@ -552,8 +524,6 @@ TORCH_LIBRARY(drt, m) {
   m.def("ip_topk(Tensor q, Tensor p, int k, int id_offset=0, Tensor? stats=None) -> (Tensor, Tensor, Tensor)");
   m.def("ip_topk.out(Tensor q, Tensor p, int k, int id_offset, Tensor? stats=None, *, Tensor(a!) scores, "
         "Tensor(b!) ids, Tensor(c!) status) -> ()");
-  m.def("ip_topk_batches(Tensor q, Tensor p, int k, int batch, int id_offset=0, Tensor? stats=None) -> "
-        "(Tensor, Tensor, Tensor)");
   m.def("ip_topk_resolve(Tensor q, Tensor p, int k, int id_offset, Tensor(a!) scores, Tensor(b!) ids, "
         "Tensor(c!) status, Tensor? stats=None) -> int");
   m.def("row_stats(Tensor p, Tensor? prev=None) -> Tensor");
@@ -584,7 +554,6 @@ TORCH_LIBRARY(drt, m) {
 TORCH_LIBRARY_IMPL(drt, CUDA, m) {   // the GPU dispatch key of torch-ROCm
   m.impl("ip_topk", &ip_topk);
   m.impl("ip_topk.out", &ip_topk_out);
-  m.impl("ip_topk_batches", &ip_topk_batches);
   m.impl("ip_topk_resolve", &ip_topk_resolve);
   m.impl("row_stats", &row_stats);
   m.impl("refine_delta", &refine_delta);

@@ -62,20 +62,6 @@ def ip_topk(q: torch.Tensor, p: torch.Tensor, k: int, id_offset: int = 0, resolv
     return scores, ids, status
 
 
-def ip_topk_batches(q: torch.Tensor, p: torch.Tensor, k: int, batch: int, id_offset: int = 0,
-                    stats: Optional[torch.Tensor] = None) -> Tuple[torch.Tensor, torch.Tensor, torch.Tensor]:
-    """ip_topk (resolve=False) of the consecutive batches q[j*batch:(j+1)*batch] in one call: batch
-    j's select + canonical-order stage overlaps batch j+1's sample phase on a second stream
-    (drt_ip_topk_batches_bf16).  Bit-identical to one ip_topk call per batch."""
-    drt = ops.load()
-    _require_device(q, p)
-    if q.dtype != torch.bfloat16 or p.dtype != torch.bfloat16:
-        raise ValueError("ip_topk_batches expects bf16 queries and corpus")
-    if q.dim() != 2 or p.dim() != 2 or q.shape[1] != p.shape[1]:
-        raise ValueError(f"shape mismatch: q {tuple(q.shape)} vs p {tuple(p.shape)}")
-    return drt.ip_topk_batches(q, p, k, batch, id_offset, stats)
-
-
 def resolve_failed(q, p, k, id_offset, scores, ids, status, n_failed: Optional[int] = None,
                    stats: Optional[torch.Tensor] = None) -> int:
     """Exact dense rescan of every query whose status bit 0 is set (synchronous), in the canonical

@@ -7,8 +7,6 @@ fake (meta) implementation that torch.compile / FakeTensor tracing need, plus th
 formula of the fused score + cross-entropy op.
 
     torch.ops.drt.ip_topk(q, p, k, id_offset, stats)   -> (scores, ids, status)   index.py:31-33
-    torch.ops.drt.ip_topk_batches(q, p, k, batch, id_offset, stats) -> (scores, ids, status)  (batch loop,
-        per-batch tails on a second stream)
     torch.ops.drt.ip_topk_resolve(q, p, k, off, s, i, st, stats) -> n_resolved  (in place, synchronous)
     torch.ops.drt.row_stats / refine_delta / refine_sort  (canonical exact-score order, include/drt.h)
     torch.ops.drt.topk_merge(scores, ids, k_out)        -> (scores, ids)           utils.py:215-229
@@ -54,12 +52,6 @@ def _register_python_parts():
 
     @lib.register_fake("drt::ip_topk")
     def _(q, p, k, id_offset=0, stats=None):
-        nq = q.shape[0]
-        return (q.new_empty((nq, k), dtype=torch.float32), q.new_empty((nq, k), dtype=torch.int64),
-                q.new_empty((nq,), dtype=torch.int32))
-
-    @lib.register_fake("drt::ip_topk_batches")
-    def _(q, p, k, batch, id_offset=0, stats=None):
         nq = q.shape[0]
         return (q.new_empty((nq, k), dtype=torch.float32), q.new_empty((nq, k), dtype=torch.int64),
                 q.new_empty((nq,), dtype=torch.int32))

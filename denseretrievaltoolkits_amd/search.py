@@ -117,24 +117,6 @@ GROUP_QUERIES = 2048
 GROUP_MIN_ROWS = 1 << 62
 
 
-# Query batches per drt_ip_topk_batches call on one GPU (FlatIPIndex.search_batches): inside a call
-# batch b's select + canonical-order tail runs on a second stream under batch b + 1's sample phase;
-# the host certifies once per call.  0: one ip_topk call per batch.
-BATCH_RUN = 16
-
-
-def _batch_runs(batches, cap: int):
-    """Runs of consecutive batches of one size b (the last of a run may be shorter), <= cap each."""
-    run = []
-    for q in batches:
-        if run and (len(run) >= cap or q.shape[0] > run[0].shape[0] or run[-1].shape[0] < run[0].shape[0]):
-            yield run
-            run = []
-        run.append(q)
-    if run:
-        yield run
-
-
 def _groups(batches, cap=None):
     cap = GROUP_QUERIES if cap is None else cap
     grp, n = [], 0
@@ -308,31 +290,6 @@ class FlatIPIndex:
         return self._finish(self._enqueue(q, k, id_offset))
 
     group_fallbacks = 0   # batches of grouped searches redone by the exact per-batch path
-    batch_run = None      # batches per drt_ip_topk_batches call (None: BATCH_RUN; 0: per-batch calls)
-
-    def _enqueue_run(self, run, k: int, id_offset: int, to_host: bool):
-        qs = [self._queries(q) for q in run]
-        sizes = [q.shape[0] for q in qs]
-        qg = qs[0] if len(qs) == 1 else torch.cat(qs)
-        stats = self._stats_arg()
-        s, i, st = kernels.ip_topk_batches(qg, self.rows, k, sizes[0], id_offset=id_offset, stats=stats)
-        h, ev = _stage_status(st)
-        host = _HostResult(s, i) if to_host else None
-        return qg, sizes, s, i, st, h, ev, id_offset, k, host, stats
-
-    def _finish_run(self, pend):
-        qg, sizes, s, i, st, h, ev, off, k, host, stats = pend
-        nbad = _status_failed(h, ev)
-        self.order_uncertified += _order_uncertified(h)
-        if nbad:
-            self.resolved += kernels.resolve_failed(qg, self.rows, k, off, s, i, st, n_failed=nbad, stats=stats)
-        if host is not None:
-            s, i = host.get(s, i, nbad > 0)
-        res, o = [], 0
-        for nb in sizes:
-            res.append((s[o:o + nb], i[o:o + nb]))
-            o += nb
-        return res
 
     def search_batches(self, batches, k: int, id_offset: int = 0, outs=None):
         """Certified top-k of every query batch (device tensors), pipelined: the next batch (or
@@ -352,12 +309,6 @@ class FlatIPIndex:
         batches = list(batches)
         if outs is None and self.ntotal >= GROUP_MIN_ROWS and self.ntotal < 0xFFFFFFFF:
             yield from self._search_groups(batches, k, id_offset, to_host)
-            return
-        cap = BATCH_RUN if self.batch_run is None else self.batch_run
-        if outs is None and cap > 1 and len(batches) > 1:
-            for res in _pipeline(list(_batch_runs(batches, cap)),
-                                 lambda j, run: self._enqueue_run(run, k, id_offset, to_host), self._finish_run):
-                yield from res
             return
         yield from _pipeline(batches, lambda j, q: self._enqueue(q, k, id_offset, outs[j] if outs else None,
                                                                  to_host), self._finish)

@@ -111,22 +111,6 @@ int drt_refine_delta_bf16(const void* Q, int64_t nq, int32_t d, const void* P, i
 int drt_refine_sort(const float* cand_s, const int64_t* cand_i, const float* delta, const int32_t* cnt,
                     int64_t nq, int32_t kc, int32_t k, float* out_scores, int64_t* out_ids, void* stream);
 
-/* drt_ip_topk_batches_bf16: drt_ip_topk_bf16 (stats == NULL) / drt_ip_topk_exact_bf16 (stats
- * given) over the consecutive query batches [b*batch, (b+1)*batch) of Q [nq, d] (the last may be
- * shorter), with the per-batch fixed work off the critical path: batch b's select + canonical-order
- * stage runs on side_stream while batch b+1's sample scan + threshold run on stream, and batch b+1's
- * filter scan starts once batch b's tail is done.  Same outputs bit for bit as one drt_ip_topk_*
- * call per batch; status as there (resolve with drt_ip_topk_resolve[_exact]).  Workspace:
- * drt_ip_topk_batches_workspace(batch, n, d, k) bytes (two batch workspaces, alternating).  Every
- * output is complete in `stream` order on return; side_stream NULL (or == stream) runs the batches
- * back to back on stream.  (Replaces the per-batch index.search loop of
- * DRT/evaluator/index.py:31-33 / trainer.py:287-297 batch_search.)                          */
-size_t drt_ip_topk_batches_workspace(int64_t batch, int64_t n, int32_t d, int32_t k);
-int drt_ip_topk_batches_bf16(const void* Q, int64_t nq, int64_t batch, const void* P, int64_t n, int32_t d,
-                             int32_t k, int64_t id_offset, const float* stats, float* out_scores,
-                             int64_t* out_ids, int32_t* status, void* workspace, size_t workspace_bytes,
-                             void* stream, void* side_stream);
-
 /* Merge `nparts` per-shard top-k lists into one global top-k.
  * scores/ids: [nparts, nq, k_in] (each part sorted score desc, id asc, as
  * drt_ip_topk_bf16 writes them); out: [nq, k_out], k_out <= k_in*nparts,

@@ -120,58 +120,6 @@ def test_flat_index_search_batches_grouped(dev, case, monkeypatch):
         assert idx.group_fallbacks == (0 if case == "int" else 3)
 
 
-@pytest.mark.parametrize("case,exact", [("int", False), ("gauss", True), ("gauss", False), ("ties", True),
-                                        ("small", True)])
-def test_ip_topk_batches_equals_per_batch_calls(dev, case, exact):
-    """drt_ip_topk_batches_bf16 (batch j's tail on a second stream under batch j+1's sample phase,
-    alternating workspace halves) writes exactly what one ip_topk call per batch writes -- scores,
-    ids and status bits -- for a ragged last batch; the same entry with no side stream too; and
-    FlatIPIndex.search_batches (runs of batches through it) certifies against the oracle."""
-    import torch
-    from denseretrievaltoolkits_amd import _native, kernels
-    from denseretrievaltoolkits_amd import search as srch
-    rng = np.random.default_rng(31)
-    if case == "int":
-        q, p, k, b = int_bf16(rng, (300, 768), -4, 4), int_bf16(rng, (150001, 768), -4, 4), 1000, 128
-    elif case == "gauss":
-        q, p, k, b = gauss_bf16(rng, (200, 768)), gauss_bf16(rng, (120000, 768)), 100, 64
-    elif case == "ties":   # every query uncertified (status bit 0 / 1 set) in every batch
-        q, p, k, b = int_bf16(rng, (12, 256), -3, 3), np.repeat(int_bf16(rng, (1, 256), -3, 3), 40000, axis=0), 100, 5
-    else:                  # dense small-shard plan: the batches run back to back
-        q, p, k, b = gauss_bf16(rng, (70, 128)), gauss_bf16(rng, (5000, 128)), 50, 32
-    qd, pd = to_dev_bf16(q, dev), to_dev_bf16(p, dev)
-    stats = kernels.row_stats(pd) if exact else None
-    s, i, st = kernels.ip_topk_batches(qd, pd, k, b, id_offset=7, stats=stats)
-    parts = [kernels.ip_topk(qd[a:a + b], pd, k, id_offset=7, resolve=False, stats=stats) for a in range(0, len(q), b)]
-    torch.cuda.synchronize()
-    assert torch.equal(s, torch.cat([x[0] for x in parts]))
-    assert torch.equal(i, torch.cat([x[1] for x in parts]))
-    assert torch.equal(st, torch.cat([x[2] for x in parts]))
-    # C ABI, no side stream: batches back to back on one stream, same outputs
-    lib = _native.load()
-    nq, d = qd.shape
-    wsb = int(lib.drt_ip_topk_batches_workspace(b, pd.shape[0], d, k))
-    assert wsb > 0
-    ws = torch.empty(wsb, dtype=torch.uint8, device=dev)
-    s2, i2, st2 = torch.empty_like(s), torch.empty_like(i), torch.empty_like(st)
-    _native.check(lib.drt_ip_topk_batches_bf16(qd.data_ptr(), nq, b, pd.data_ptr(), pd.shape[0], d, k, 7,
-                                               stats.data_ptr() if stats is not None else None, s2.data_ptr(),
-                                               i2.data_ptr(), st2.data_ptr(), ws.data_ptr(), wsb,
-                                               _native.stream_ptr(dev), None), "drt_ip_topk_batches_bf16")
-    torch.cuda.synchronize()
-    assert torch.equal(s2, s) and torch.equal(i2, i) and torch.equal(st2, st)
-    # the index path: runs of batches, certified (uncertified queries redone exactly)
-    idx = srch.FlatIPIndex.from_rows(pd)
-    idx.exact_order = exact
-    res = idx.search_batches([qd[a:a + b] for a in range(0, len(q), b)], k)
-    gi = torch.cat([r[1] for r in res]).cpu().numpy()
-    es, ei = orc.ip_topk(q, p, k, dtype=np.float64 if exact else np.float32)
-    if case == "gauss" and not exact:
-        assert (gi == ei).mean() > 0.99   # fp32 order: near-tie swaps only (test_ip_topk_gaussian_tolerance)
-    else:
-        np.testing.assert_array_equal(gi, ei)
-
-
 def test_ip_topk_gaussian_tolerance(dev):
     rng = np.random.default_rng(7)
     nq, n, d, k = 128, 120000, 768, 1000

@@ -59,16 +59,3 @@ def test_pipeline_enqueues_next_before_finishing():
                                 lambda j: (log.append(("fin", j)), j)[1]))
     assert out == [0, 1, 2]
     assert log == [("enq", 0), ("enq", 1), ("fin", 0), ("enq", 2), ("fin", 1), ("fin", 2)]
-
-
-def test_batch_runs_split_at_size_changes_and_cap():
-    """FlatIPIndex.search_batches hands drt_ip_topk_batches runs of equal-size batches whose last
-    member may be shorter (the C entry's layout), at most `cap` per run, in order."""
-    sizes = [128, 128, 128, 40, 128, 128, 200, 7, 7, 7, 3, 9]
-    runs = list(search._batch_runs([torch.empty((n, 1)) for n in sizes], cap=2))
-    got = [[q.shape[0] for q in r] for r in runs]
-    assert got == [[128, 128], [128, 40], [128, 128], [200, 7], [7, 7], [3], [9]]
-    for r in got:
-        assert all(n == r[0] for n in r[:-1]) and r[-1] <= r[0] and len(r) <= 2
-    assert sum(sum(r) for r in got) == sum(sizes)
-    assert [[q.shape[0] for q in r] for r in search._batch_runs([torch.empty((5, 1))] * 5, cap=16)] == [[5] * 5]

@@ -1,8 +1,7 @@
 #!/usr/bin/env python3
 """Interleaved A/B of FlatIPIndex.search_batches paths on the bench workload (10M x 768 bf16,
-Qb 128, k 1000), one process.  Variants: gN = grouped (GROUP_QUERIES N per group), bN = runs of N
-batches through drt_ip_topk_batches (b0: one ip_topk call per batch).
-usage: python tools/search_ab.py [--rounds 3] [--steps 32] [--variants b16,b0,g2048]"""
+Qb 128, k 1000), one process: grouped (search.GROUP_QUERIES per group) vs per-batch.
+usage: python tools/search_ab.py [--rounds 3] [--steps 32] [--groups 2048,0]"""
 from __future__ import annotations
 
 import argparse
@@ -19,7 +18,7 @@ def main():
     ap.add_argument("--rounds", type=int, default=3)
     ap.add_argument("--steps", type=int, default=32)
     ap.add_argument("--n", type=int, default=10_000_000)
-    ap.add_argument("--variants", default="b16,b0")
+    ap.add_argument("--groups", default="2048,0")
     ap.add_argument("--order", choices=["exact", "fp32"], default="exact")
     args = ap.parse_args()
     import torch
@@ -33,17 +32,16 @@ def main():
     srch.EXACT_ORDER = args.order == "exact"
     idx = srch.FlatIPIndex.from_rows(shard)
     batches = [qs[j] for j in range(args.steps)]
-    variants = args.variants.split(",")
+    variants = [int(v) for v in args.groups.split(",")]
     times = {v: [] for v in variants}
     ref = None
     for rnd in range(args.rounds):
         for v in variants:
-            if v[0] == "b":
+            if v == 0:
                 srch.GROUP_MIN_ROWS = 1 << 62
-                idx.batch_run = int(v[1:])
             else:
                 srch.GROUP_MIN_ROWS = 0
-                srch.GROUP_QUERIES = int(v[1:])
+                srch.GROUP_QUERIES = v
             idx.search_batches(batches[:2], 1000)
             torch.cuda.synchronize()
             t0 = time.perf_counter()
