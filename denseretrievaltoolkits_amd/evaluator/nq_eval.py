@@ -10,6 +10,8 @@ import unicodedata
 import numpy as np
 import regex
 
+from .. import _native
+
 _TOKEN_RE = regex.compile(r"([\p{L}\p{N}\p{M}]+)|([^\p{Z}\p{C}])",
                           flags=regex.IGNORECASE + regex.UNICODE + regex.MULTILINE)
 
@@ -265,13 +267,12 @@ class DeviceRowMatcher:
     batch j + 1.  Same result as ``RowAnswerMatcher.match_rows`` (the host matcher owns the
     vocabulary, the slots and the passage tokenisation); tests/test_answers_gpu.py compares the two.
 
-    Per batch: toks = tok[slot[rows]] -> [B, k, W]; every answer a of query i as token ids padded
-    to the longest answer; a window start s matches answer a iff toks[i, :, s + j] == ids[a][j] for
-    every j < len(a) (and s + len(a) <= W).  The [B, a, k, W] window masks are evaluated in answer
-    chunks of at most MASK_ELEMS elements, so alias-heavy answer sets and long passages stay
-    bounded in memory."""
-
-    MASK_ELEMS = 1 << 26
+    Per batch ONE kernel (drt_answer_match_i32, csrc/match.hip): wave (i, j) takes the token slot of
+    retrieved row j of query i, its lanes take window starts s, and the row matches when some answer
+    a of query i has toks[s + t] == ids[a][t] for every t < len(a) (s + len(a) <= W).  The host
+    builds the batch's [B, A, n_max] answer ids (cached per answer string) and the slot array.
+    (Round 3 evaluated [B, a, k, W] window masks with ~5 torch ops per answer token; the host cost of
+    issuing them bounded the C2 query stage.)"""
 
     def __init__(self, host: "RowAnswerMatcher", device):
         import torch
@@ -324,29 +325,22 @@ class DeviceRowMatcher:
                 ans[i, a, : len(ids)] = ids
                 alen[i, a] = len(ids)
         slots = np.where(rows >= 0, h.slot[np.maximum(rows, 0)], -1)
-        ac = max(1, min(A, self.MASK_ELEMS // max(1, B * k * W)))       # answers per chunk
+        if h.n_slots == 0:   # no row tokenised: every retrieved row is a pad
+            return _PendingMatch(np.zeros((B, k), dtype=np.int8), None)
+        lib = _native.load()
         with torch.cuda.stream(self.stream):
             dev = self.device
-            r = torch.from_numpy(np.ascontiguousarray(slots)).pin_memory().to(dev, non_blocking=True)
-            at_all = torch.from_numpy(ans).pin_memory().to(dev, non_blocking=True)
-            lt_all = torch.from_numpy(alen).pin_memory().to(dev, non_blocking=True)
-            ev = torch.from_numpy(every).pin_memory().to(dev, non_blocking=True)
-            valid = r >= 0
-            toks = self.tok[r.clamp(min=0)]                                    # [B, k, W]
-            hit = ev[:, None].expand(B, k).clone()
-            for a0 in range(0, A, ac):
-                at, lt = at_all[:, a0: a0 + ac], lt_all[:, a0: a0 + ac]
-                m = torch.ones((B, at.shape[1], k, W), dtype=torch.bool, device=dev)   # window starts s
-                for j in range(n_max):
-                    use = (lt > j)[:, :, None, None]                           # answer has token j
-                    m[..., : W - j] &= (toks[:, None, :, j:] == at[:, :, j][:, :, None, None]) | ~use
-                    if j:
-                        m[..., W - j:] &= ~use                                 # s + j past the row
-                hit |= (m.any(-1) & (lt > 0)[:, :, None]).any(1)
-                del m
-            hit &= valid
+            r = torch.from_numpy(np.ascontiguousarray(slots, dtype=np.int64)).pin_memory().to(dev, non_blocking=True)
+            at = torch.from_numpy(ans).pin_memory().to(dev, non_blocking=True)
+            lt = torch.from_numpy(alen.astype(np.int32)).pin_memory().to(dev, non_blocking=True)
+            ev = torch.from_numpy(every.astype(np.uint8)).pin_memory().to(dev, non_blocking=True)
+            hit = torch.empty((B, k), dtype=torch.int8, device=dev)
+            # one launch: wave (i, j) scans retrieved row j of query i for every answer of query i
+            _native.check(lib.drt_answer_match_i32(self.tok.data_ptr(), W, r.data_ptr(), B, k, at.data_ptr(),
+                                                   lt.data_ptr(), A, n_max, ev.data_ptr(), hit.data_ptr(),
+                                                   self.stream.cuda_stream), "drt_answer_match_i32")
             out = torch.empty((B, k), dtype=torch.int8, pin_memory=True)
-            out.copy_(hit.to(torch.int8), non_blocking=True)
+            out.copy_(hit, non_blocking=True)
             done = torch.cuda.Event()
             done.record(self.stream)
         return _PendingMatch(out, done)

@@ -13,18 +13,16 @@ from conftest import REPO
 pytestmark = pytest.mark.gpu
 
 
-@pytest.mark.parametrize("mask_elems", [None, 64])
-def test_device_matcher_equals_host_random(dev, mask_elems):
-    """mask_elems 64: the window masks evaluated one answer at a time (the memory-bounded chunking)."""
+@pytest.mark.parametrize("max_words", [40, 300])
+def test_device_matcher_equals_host_random(dev, max_words):
+    """max_words 300: token rows wider than a wave (several window starts per lane)."""
     from denseretrievaltoolkits_amd.evaluator.nq_eval import DeviceRowMatcher, RowAnswerMatcher, has_answers
     rng = np.random.default_rng(7)
     vocab = ["a", "b", "c", "d", "A", "b.", "c-d", "e", "É", "naïve", "⁂", "日本"]
-    docs = [" ".join(rng.choice(vocab, size=int(rng.integers(0, 40)))) for _ in range(500)]
+    docs = [" ".join(rng.choice(vocab, size=int(rng.integers(0, max_words)))) for _ in range(500)]
     host = RowAnswerMatcher(0)
     host.ensure_rows(500)
     dm = DeviceRowMatcher(host, dev)
-    if mask_elems:
-        dm.MASK_ELEMS = mask_elems
     ref_m = RowAnswerMatcher(0)
     ref_m.ensure_rows(500)
     for it in range(40):
