@@ -389,9 +389,12 @@ def run_evaluate_c2(device, n_passages=1_000_000, n_queries=10_000, k=1000, p_le
     reps = torch.cat([tr._encode_window(w) for w in wins])
     torch.cuda.synchronize()
     t2 = time.perf_counter()
-    res = tr.index.local.search_batches([reps[a: a + q_batch] for a in range(0, reps.shape[0], q_batch)], k)
+    loc = tr.index.local
+    r0, u0 = loc.resolved, loc.order_uncertified
+    res = loc.search_batches([reps[a: a + q_batch] for a in range(0, reps.shape[0], q_batch)], k)
     torch.cuda.synchronize()
     t3 = time.perf_counter()
+    n_res, n_unc = loc.resolved - r0, loc.order_uncertified - u0
     del res
     qps_e2e = n_queries / tm["queries_s"]
     return {
@@ -409,6 +412,10 @@ def run_evaluate_c2(device, n_passages=1_000_000, n_queries=10_000, k=1000, p_le
             "query_encode_qps": round(n_queries / (t2 - t1), 1),
             "search_s": round(t3 - t2, 4),
             "search_qps": round(n_queries / (t3 - t2), 1),
+            # queries rescanned densely / kept in the fp32 order (canonical order not certifiable:
+            # the random-init tower's embeddings are near-ties within the fp32 error)
+            "search_resolved_queries": int(n_res),
+            "search_order_uncertified_queries": int(n_unc),
         },
         "query_num": m["query_num"],
         "recall@1000": m.get("Recall@1000"),

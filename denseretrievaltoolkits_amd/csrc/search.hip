@@ -1984,12 +1984,17 @@ __global__ __launch_bounds__(kRefThreads) void refine_prep_kernel(RefineArgs a) 
   for (int j = tid; j < nval; j += kRefThreads) C += cs[j] >= B ? 1 : 0;
   C = ref_block_sum(C, iscr);
   const bool wide = eps != 0.0f && C == a.kc && nval == a.kc;               // window wider than the list
+  // the window reaches below the filter threshold: rows in [B, tau) were never collected, so the
+  // exact order of the window cannot be certified from the list.  The fp32 top-k itself is exact
+  // (every row >= tau was collected; the select certified k <= hits): keep it in the fp32 order
+  // (faiss's semantics) rather than rescanning the shard densely -- degenerate embeddings (e.g. an
+  // untrained tower, every score within the fp32 error of the k-th) hit this for every query.
+  const bool below = eps != 0.0f && a.tau && nval >= a.k && a.tau[q] > B;
   if (tid == 0) {
-    a.cnt[2 * q] = eps == 0.0f ? -1 : (wide ? -2 : C);
+    a.cnt[2 * q] = eps == 0.0f ? -1 : ((wide || below) ? -2 : C);
     a.cnt[2 * q + 1] = __builtin_bit_cast(int32_t, eps);
     if (a.status) {
-      int st = wide ? 2 : 0;
-      if (eps != 0.0f && a.tau && nval >= a.k && a.tau[q] > B) st |= 1;     // rows in [B, tau) unseen
+      const int st = (wide || below) ? 2 : 0;
       const int64_t orow = a.qmap ? (int64_t)a.qmap[q] : q;
       if (a.set_status) a.status[orow] = st;
       else if (st) a.status[orow] |= st;

@@ -95,8 +95,9 @@ def refine(q: torch.Tensor, p: torch.Tensor, row_offset: int, cand_s: torch.Tens
     """Canonical exact-score order of candidate lists [nq, kc] (scores desc, global ids): exact
     sums for the candidates whose rows this shard holds (global ids [row_offset, row_offset +
     len(p))), combined across shards by ``all_reduce_sum`` (in place; None on one GPU), then the
-    top-k by (exact score desc, id asc).  ``status`` [nq] gains bit 0 (candidates below ``tau``
-    missing: redo exactly) / bit 1 (near-tie window wider than the list) in place."""
+    top-k by (exact score desc, id asc).  ``status`` [nq] gains bit 1 in place where the order cannot
+    be certified (near-tie window wider than the list, or reaching below ``tau``): that query keeps
+    the fp32 top-k in the fp32 order."""
     _require_device(q, p, cand_s, cand_i, stats, status)
     drt = ops.load()
     delta, cnt = drt.refine_delta(q, p, row_offset, cand_s, cand_i, k, stats, tau, status)

@@ -85,9 +85,10 @@ int drt_ip_topk_resolve(const void* Q, int64_t nq, const void* P, int64_t n, int
  *   every element is an integer); accumulate = 0 (re)initialises, 1 combines with the stats
  *   already there (appended rows).  Across shards combine by max / min.  Reads every row once.
  * drt_ip_topk_exact_bf16: drt_ip_topk_bf16 in the canonical order (same workspace).  status bit 0
- *   as drt_ip_topk_bf16 (call drt_ip_topk_resolve_exact); bit 1 = more than
- *   drt_refine_width(k) - k rows within the fp32 error of the k-th score (massive near-ties;
- *   that query keeps the fp32 order).
+ *   as drt_ip_topk_bf16 (call drt_ip_topk_resolve_exact); bit 1 = the exact order could not be
+ *   certified and the query keeps the (exact) fp32 top-k in the fp32 order: more than
+ *   drt_refine_width(k) - k rows within the fp32 error of the k-th score, or that window reaching
+ *   below the filter threshold (massive near-ties, e.g. an untrained tower's embeddings).
  * drt_ip_topk_resolve_exact: drt_ip_topk_resolve in the canonical order (status bit 0 only).
  * drt_refine_delta_bf16 / drt_refine_sort: the stage alone, on a candidate list cand [nq][kc]
  *   (scores desc, global ids, kc = drt_refine_width(k), e.g. a merged sharded result): delta =
