@@ -431,7 +431,7 @@ def main():
                           "filter scan per batch)" if use_global else ")")),
             },
             "roofline": {
-                "kernel": "ip_scan16r_kernel<768,false,true> (csrc/search.hip)",
+                "kernel": "ip_scan16r_kernel<768> (csrc/search.hip)",
                 "bound": "hbm",
                 "achieved": round(achieved, 1),
                 "peak": HBM_PEAK_GBS,
@@ -453,6 +453,12 @@ def main():
         }
         if world == 1 and not args.no_cpu_baseline:
             out["cpu_baseline"] = cpu_baseline(args, shard, queries[args.warmup], results[0])
+    # the search leg's 15 GB corpus, index and results leave HBM before the model legs: the training
+    # legs' torch baselines reserve ~140 GB, and with the corpus still cached the recipe leg's
+    # allocations ran into the pool's limit (169 vs 119 ms per step in one process, r04s vs r04v)
+    del shard, queries, results, index, local_index
+    torch.cuda.synchronize()
+    torch.cuda.empty_cache()
     enc = None if args.no_encode else encode_leg(args, dev)
     if enc is not None:
         if world > 1:
@@ -471,14 +477,19 @@ def main():
         import bench_legs as bench_encode
         if not args.no_cpu_baseline:
             out["encode"]["cpu_baseline"] = encode_cpu_baseline()
-        out["rerank"] = bench_encode.run_rerank(dev)
-        out["query_encode"] = bench_encode.run_query_encode(dev)
-        out["train_scores"] = bench_encode.run_train_scores(dev)
-        out["train_step"] = bench_encode.run_train_step(dev)
+        def leg(fn, *a, **kw):   # each leg starts from an empty cache (no pool pressure from the last)
+            r = fn(*a, **kw)
+            torch.cuda.synchronize()
+            torch.cuda.empty_cache()
+            return r
+        out["rerank"] = leg(bench_encode.run_rerank, dev)
+        out["query_encode"] = leg(bench_encode.run_query_encode, dev)
+        out["train_scores"] = leg(bench_encode.run_train_scores, dev)
+        out["train_step"] = leg(bench_encode.run_train_step, dev)
         # the reference recipe's shapes (run.sh:16-19: train_n_passages 8, p_max_len 156) at batch 128
-        out["train_step_recipe"] = bench_encode.run_train_step(dev, bq=128, n=8, p_len=156)
+        out["train_step_recipe"] = leg(bench_encode.run_train_step, dev, bq=128, n=8, p_len=156)
         if not args.no_evaluate:
-            out["evaluate_c2"] = bench_encode.run_evaluate_c2(dev, n_passages=args.c2_passages)
+            out["evaluate_c2"] = leg(bench_encode.run_evaluate_c2, dev, n_passages=args.c2_passages)
     if rank == 0:
         print(json.dumps(out), flush=True)
     if world > 1:
