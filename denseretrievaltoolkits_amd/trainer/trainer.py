@@ -319,18 +319,7 @@ class Trainer:
             n = q_reps.shape[0]
             ids_all = np.empty((n, k), dtype=np.int64)
             done, bi, b0 = 0, 0, 0
-            if self.world == 1:
-                # the whole window's searches go on the GPU first, then the next window's tower
-                # pass; the host certifies and matches this window's batches while the GPU runs
-                # that pass (one rank: no collective order to keep)
-                sb = self.SEARCH_BATCH
-                loc = self.index.local
-                pend = loc.enqueue_batches([q_reps[a: a + sb] for a in range(0, n, sb)], k, to_host=True)
-                nxt = encode_next()
-                rows_iter = ((j * sb, loc.finish_batch(p_)[1]) for j, p_ in enumerate(pend))
-            else:
-                rows_iter = self._search_rows(q_reps, k)
-            for row0, ids in rows_iter:
+            for row0, ids in self._search_rows(q_reps, k):
                 if nxt is None:
                     # the next window's tower pass goes on the GPU behind this window's first search
                     # runs, so it runs while the host matches this window's batches
