@@ -1320,11 +1320,13 @@ __global__ __launch_bounds__(kKthThreads) void kth_final_kernel(const uint32_t* 
 
 // Sample threshold in ONE launch (one-GPU search, samples up to kRankThreads * kRankPer keys --
 // 70,801 at 10M rows and k = 1000): one 1024-thread work-group per query holds the whole sample
-// row in registers, a 1024-bin histogram linear in the score finds the bin holding rank r, the
-// keys of the bins up to it (~r + that bin) are sorted in LDS and tau = the r-th best -- the same
-// key kth_partial + kth_final pick (both exact), without the 2,304-work-group chunk pass, its
-// survivor lists and the second launch.  More than kRankBuf candidates (ties / a degenerate score
-// range) fall back to an exact MSD radix select over the candidates.  Also zeroes the hit counter.
+// row in registers; round 4: the r-th best of the 1024 per-thread best keys bounds the answer, so only
+// those 1024 keys go through the 1024-bin histogram (not every sampled key: 70k LDS atomics per query,
+// mostly on the crowded middle bins), the keys no worse than that bound (~r of them) are sorted in
+// LDS and tau = the r-th best -- the same key kth_partial + kth_final pick (both exact), without the
+// chunk pass, its survivor lists and the second launch.  More than kRankBuf candidates (ties / a
+// degenerate score range) fall back to an exact MSD radix select over the candidates.  Also zeroes
+// the hit counter.
 constexpr int kRankThreads = 1024;
 constexpr int kRankPerMax = 80;   // keys per thread (register-resident); smaller samples take 8 / 24
 constexpr int kRankBins = 1024;
@@ -1359,14 +1361,20 @@ __global__ __launch_bounds__(kRankThreads) void kth_rank_kernel(const uint32_t* 
       for (int u = 0; u < 4; ++u) key[4 * j + u] = base + u < n ? src[base + u] : kPad;
     }
   }
-  float hi = -__builtin_inff(), lo = __builtin_inff();
+  // Candidates without a histogram of every key: the r best of the 1024 per-thread best keys are r
+  // distinct keys, so the r-th best key overall is no worse than the r-th best thread-best, K_r.
+  // A 1024-bin histogram of the thread-bests (1024 LDS atomics instead of one per sampled key)
+  // brackets K_r by bin b; T = the worst thread-best in bins <= b (>= K_r); every key <= T is a
+  // candidate -- the r best keys are among them, typically with few others (the thread-bests of
+  // those bins plus the rare second top key of one thread).
+  uint32_t best = kPad;
 #pragma unroll
-  for (int e = 0; e < kRankPer; ++e) {
-    if (key[e] != kPad) {
-      const float sc = desc_key_to_score(key[e]);
-      hi = fmaxf(hi, sc);
-      lo = fminf(lo, sc);
-    }
+  for (int e = 0; e < kRankPer; ++e) best = key[e] < best ? key[e] : best;   // kPad = the largest key
+  float hi = -__builtin_inff(), lo = __builtin_inff();
+  if (best != kPad) {
+    const float sc = desc_key_to_score(best);
+    hi = sc;
+    lo = sc;
   }
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) {
@@ -1386,15 +1394,13 @@ __global__ __launch_bounds__(kRankThreads) void kth_rank_kernel(const uint32_t* 
   }
   const float range = hi - lo;
   const float scale = hist_scale((float)kRankBins, range);
-  // bin 0 = best scores; monotone in the key, so the keys of bins <= b are the smallest keys
+  // bin 0 = best scores; monotone in the key
   auto bin_of = [&](uint32_t kk) {
     if (scale == 0.0f) return 0;
     const float sc = desc_key_to_score(kk);
     return hist_bin((hi - sc) * scale, kRankBins, __builtin_signbit(sc) ? kRankBins - 1 : 0);
   };
-#pragma unroll
-  for (int e = 0; e < kRankPer; ++e)
-    if (key[e] != kPad) atomicAdd(&hist[bin_of(key[e])], 1u);
+  if (best != kPad) atomicAdd(&hist[bin_of(best)], 1u);
   __syncthreads();
   {
     const uint32_t v = hist[tid];
@@ -1405,20 +1411,37 @@ __global__ __launch_bounds__(kRankThreads) void kth_rank_kernel(const uint32_t* 
       if (lane >= o) incl += t;
     }
     if (lane == 63) wsum[wave] = incl;
-    if (tid == 0) sh_n = 0;
+    if (tid == 0) {
+      sh_n = 0;
+      sh_prefix = 0;   // T below (max over the selected thread-bests)
+    }
     __syncthreads();
     uint32_t off = 0;
     for (int w = 0; w < wave; ++w) off += wsum[w];
     incl += off;
     const uint32_t excl = incl - v;
     if (excl < (uint32_t)r && (uint32_t)r <= incl) sh_bin = tid;
-    if (tid == kRankThreads - 1 && incl < (uint32_t)r) sh_bin = kRankBins - 1;   // fewer than r real keys
+    // fewer than r thread-bests: every real key is a candidate
+    if (tid == kRankThreads - 1 && incl < (uint32_t)r) sh_bin = -1;
   }
   __syncthreads();
   const int b = sh_bin;
+  if (b >= 0) {
+    // T = the worst (largest) thread-best key in bins <= b
+    uint32_t t = (best != kPad && bin_of(best) <= b) ? best : 0u;
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+      const uint32_t u = __shfl_xor(t, o, 64);
+      t = u > t ? u : t;
+    }
+    if (lane == 0) atomicMax(&sh_prefix, t);
+  }
+  __syncthreads();
+  const uint32_t T = b >= 0 ? sh_prefix : kPad - 1u;
+  __syncthreads();
 #pragma unroll
   for (int e = 0; e < kRankPer; ++e) {
-    if (key[e] != kPad && bin_of(key[e]) <= b) {
+    if (key[e] <= T) {
       const uint32_t pos = atomicAdd(&sh_n, 1u);
       if (pos < (uint32_t)kRankBuf) buf[pos] = key[e];
     }
@@ -1446,7 +1469,7 @@ __global__ __launch_bounds__(kRankThreads) void kth_rank_kernel(const uint32_t* 
       const uint32_t prefix = sh_prefix;
 #pragma unroll
       for (int e = 0; e < kRankPer; ++e)
-        if (key[e] != kPad && bin_of(key[e]) <= b && (key[e] & mask) == prefix)
+        if (key[e] <= T && (key[e] & mask) == prefix)
           atomicAdd(&hist[(key[e] >> shift) & 255u], 1u);
       __syncthreads();
       if (tid == 0) {
