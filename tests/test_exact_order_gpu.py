@@ -161,3 +161,28 @@ def test_flat_index_exact_order_default_and_counter(dev):
         np.testing.assert_array_equal(torch.cat([r[1] for r in res]).cpu().numpy(), ei)
         _assert_scores(torch.cat([r[0] for r in res]).cpu().numpy(), es)
     assert idx.order_uncertified == 0 and idx.group_fallbacks == 0
+
+
+def test_exact_order_degenerate_near_ties_keep_fp32_result_without_rescan(dev):
+    """Sampled path, every score within the fp32 error bound of every other (a common large
+    component + 1e-4-scale rest: the untrained-tower case of the C2 leg): the near-tie window
+    reaches below the filter threshold, so the canonical order cannot be certified from the list.
+    Status bit 1 is set, bit 0 is NOT (no dense rescan), and the result is exactly the fp32 path's
+    (ip_topk without row statistics): the certified fp32 top-k in the fp32 order."""
+    import torch
+    from denseretrievaltoolkits_amd import kernels
+    rng = np.random.default_rng(21)
+    n, d, k, nq = 60000, 128, 1000, 4
+    p = orc.bf16_round(1e-4 * rng.standard_normal((n, d)))
+    p[:, 0] = 8.0
+    q = orc.bf16_round(rng.standard_normal((nq, d)))
+    q[:, 0] = 8.0
+    qt, pt = to_dev_bf16(q, dev), to_dev_bf16(p, dev)
+    stats = kernels.row_stats(pt)
+    s, i, st = kernels.ip_topk(qt, pt, k, resolve=False, stats=stats)
+    s32, i32, st32 = kernels.ip_topk(qt, pt, k, resolve=False)
+    torch.cuda.synchronize()
+    st = st.cpu().numpy()
+    assert ((st & 2) != 0).all() and ((st & 1) == 0).all(), st
+    assert (st32.cpu().numpy() == 0).all()
+    assert torch.equal(i, i32) and torch.equal(s, s32)

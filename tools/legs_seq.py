@@ -33,7 +33,27 @@ def main():
         print(json.dumps({"recipe_" + tag: r["hip_ms"], "torch_bf16": r["torch_bf16_autocast_ms"],
                           "leg_s": round(time.perf_counter() - t0, 1)}), flush=True)
 
-    legs = {"encode": lambda: bl.run(dev), "rerank": lambda: bl.run_rerank(dev),
+    def search_leg():   # bench.py's search leg + its CPU baseline, corpus dropped afterwards
+        import types
+        import bench
+        from denseretrievaltoolkits_amd.search import FlatIPIndex
+        shard, _, _ = bench.gen_shard(10_000_000, 1, 0, 768, dev)
+        g = torch.Generator(device=dev)
+        g.manual_seed(1234)
+        qs = [torch.randn((128, 768), generator=g, device=dev).to(torch.bfloat16) for _ in range(20)]
+        idx = FlatIPIndex.from_rows(shard)
+        res = idx.search_batches(qs, 1000)
+        torch.cuda.synchronize()
+        a = types.SimpleNamespace(n_corpus=10_000_000, k=1000, qb=128, dim=768)
+        bench.cpu_baseline(a, shard, qs[0], res[0])
+        del shard, qs, idx, res
+
+    def cpu_leg():
+        import bench
+        bench.encode_cpu_baseline()
+
+    legs = {"search": search_leg, "cpu": cpu_leg,
+            "encode": lambda: bl.run(dev), "rerank": lambda: bl.run_rerank(dev),
             "query": lambda: bl.run_query_encode(dev), "scores": lambda: bl.run_train_scores(dev),
             "train": lambda: bl.run_train_step(dev)}
     for name in args.legs.split(","):
@@ -41,7 +61,7 @@ def main():
         torch.cuda.synchronize()
         torch.cuda.empty_cache()
         mem(name)
-        if name in ("encode", "query", "train"):
+        if name in ("search", "cpu", "encode", "query", "train"):
             recipe("after_" + name)
             torch.cuda.empty_cache()
 
