@@ -301,6 +301,14 @@ class FlatIPIndex:
         BaseFaissIPRetriever.batch_search, Trainer.evaluate and bench.py time."""
         return list(self.search_batches_iter(batches, k, id_offset, outs))
 
+    def enqueue_batches(self, batches, k: int, id_offset: int = 0, to_host: bool = False) -> list:
+        """Every batch's search enqueued now (per-batch path); collect each with ``finish_batch``."""
+        return [self._enqueue(q, k, id_offset, None, to_host) for q in batches]
+
+    def finish_batch(self, pend):
+        """(scores, ids) of one ``enqueue_batches`` entry, certified (uncertified queries redone)."""
+        return self._finish(pend)
+
     def search_batches_iter(self, batches, k: int, id_offset: int = 0, outs=None, to_host: bool = False):
         """search_batches as a generator: batch j's result is yielded once batch j + 1 (or the next
         group) is on the GPU, so the caller's host work on batch j overlaps the device work on

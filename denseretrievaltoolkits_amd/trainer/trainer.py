@@ -225,6 +225,9 @@ class Trainer:
     # behind an event.  Metrics stay per LOADER batch (get_metrics' NDCG is a batch-level ratio).
     ENCODE_WINDOW = 4096
     SEARCH_BATCH = 128
+    # one rank: enqueue a whole window's searches before the next window's tower pass (A/B switch of
+    # tools/c2_host_prof.py; off: the next tower pass goes behind the window's first searches)
+    EAGER_WINDOW_SEARCH = False
     prefill_answer_tokens = True
     # host (and, mirrored, HBM) bytes of passage tokens prefilled during the corpus encode
     prefill_answer_max_bytes = 1 << 30
@@ -319,7 +322,16 @@ class Trainer:
             n = q_reps.shape[0]
             ids_all = np.empty((n, k), dtype=np.int64)
             done, bi, b0 = 0, 0, 0
-            for row0, ids in self._search_rows(q_reps, k):
+            if self.world == 1 and self.EAGER_WINDOW_SEARCH and n:
+                # A/B: the whole window's searches first, then the next window's tower pass
+                sb = self.SEARCH_BATCH
+                loc = self.index.local
+                pend = loc.enqueue_batches([q_reps[a: a + sb] for a in range(0, n, sb)], k, to_host=True)
+                nxt = encode_next()
+                rows_iter = ((j * sb, loc.finish_batch(p_)[1]) for j, p_ in enumerate(pend))
+            else:
+                rows_iter = self._search_rows(q_reps, k)
+            for row0, ids in rows_iter:
                 if nxt is None:
                     # the next window's tower pass goes on the GPU behind this window's first search
                     # runs, so it runs while the host matches this window's batches
@@ -401,16 +413,27 @@ class Trainer:
                 m_all[key] += metrics[key]
 
         pend = None
-        for batch, indices in self._eval_results(query_loader, k):
+        tw = {"results_wait_s": 0.0, "match_issue_s": 0.0, "match_finish_s": 0.0}
+        res_iter = self._eval_results(query_loader, k)
+        while True:
+            t0w = time.perf_counter()
+            nxt_res = next(res_iter, None)
+            tw["results_wait_s"] += time.perf_counter() - t0w
+            if nxt_res is None:
+                break
+            batch, indices = nxt_res
             th = time.perf_counter()
             if hasattr(matcher, "match_rows_async"):
                 cur = (batch, indices, matcher.match_rows_async(indices, text_of, batch[2]))
             else:
                 cur = (batch, indices, _Ready(matcher.match_rows(indices, text_of, batch[2])))
             eval_num += len(indices)
+            tm = time.perf_counter()
+            tw["match_issue_s"] += tm - th
             if pend is not None:
                 finish(pend)
             pend = cur
+            tw["match_finish_s"] += time.perf_counter() - tm
             t_host += time.perf_counter() - th
         if pend is not None:
             th = time.perf_counter()
@@ -438,7 +461,7 @@ class Trainer:
             dist.barrier()
         self.last_metrics = m_all
         self.last_eval_timing = {"corpus_s": t1 - t0, "queries_s": t2 - t1, "host_match_s": t_host,
-                                 "files_s": time.perf_counter() - t2}
+                                 "files_s": time.perf_counter() - t2, **tw}
         return m_all
 
     # ------------------------------------------------------------------
