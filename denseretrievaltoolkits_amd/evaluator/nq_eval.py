@@ -158,6 +158,8 @@ class RowAnswerMatcher:
         self.tok = np.full((0, self.width), -1, dtype=np.int32)
         self.n_slots = 0
         self.version = 0
+        self.n_filled = 0        # rows of [0, n_rows) that have a slot (fill's fast exit when all do)
+        self.slot_version = 0    # bumped whenever ``slot`` changes (the device mirror re-uploads it)
 
     @property
     def seen(self) -> np.ndarray:
@@ -174,6 +176,7 @@ class RowAnswerMatcher:
             sl = np.full(n_rows, -1, dtype=np.int64)
             sl[: self.n_rows] = self.slot
             self.slot, self.n_rows = sl, int(n_rows)
+            self.slot_version += 1
 
     def rebase(self, offset: int, n_local: int, n_total: int):
         """Move rows [0, n_local) (a shard tokenised by local row) to [offset, offset + n_local) of
@@ -181,6 +184,8 @@ class RowAnswerMatcher:
         sl = np.full(n_total, -1, dtype=np.int64)
         sl[offset: offset + n_local] = self.slot[:n_local]
         self.slot, self.n_rows = sl, int(n_total)
+        self.n_filled = int((sl >= 0).sum())
+        self.slot_version += 1
 
     def _reserve(self, n_slots: int, width: int):
         cap, w = self.tok.shape[0], self.width
@@ -196,6 +201,8 @@ class RowAnswerMatcher:
 
     def fill(self, rows, text_of) -> int:
         """Tokenise every row of ``rows`` not tokenised yet (``text_of(row)`` -> passage text)."""
+        if self.n_filled >= self.n_rows:   # every row tokenised (the corpus prefill): nothing to look up
+            return 0
         r = np.asarray(rows).reshape(-1)
         r = r[r >= 0]
         miss = r[self.slot[r] < 0]          # a gather; np.unique only over the (usually no) misses
@@ -211,6 +218,8 @@ class RowAnswerMatcher:
                     self.tok[s0 + j, : len(toks)] = [v[t] if t in v else v.setdefault(t, len(v)) for t in toks]
             self.slot[miss] = np.arange(s0, s0 + miss.size)
             self.n_slots = s0 + int(miss.size)
+            self.n_filled += int(miss.size)
+            self.slot_version += 1
         return int(miss.size)
 
     def _answer_ids(self, answers_i):
@@ -281,6 +290,8 @@ class DeviceRowMatcher:
         self.tok = None
         self._version = None
         self._slots = 0
+        self.slot_dev = None
+        self._slot_version = None
         self.stream = torch.cuda.Stream(self.device)
 
     def _upload(self):
@@ -295,6 +306,9 @@ class DeviceRowMatcher:
             elif h.n_slots > self._slots:
                 a, b = self._slots, h.n_slots
                 self.tok[a:b] = torch.from_numpy(np.ascontiguousarray(h.tok[a:b])).to(self.device)
+            if h.slot_version != self._slot_version or self.slot_dev is None:
+                self.slot_dev = torch.from_numpy(np.ascontiguousarray(h.slot)).to(self.device)
+                self._slot_version = h.slot_version
         self._slots = h.n_slots
 
     def match_rows(self, rows: np.ndarray, text_of, answers) -> np.ndarray:
@@ -324,20 +338,21 @@ class DeviceRowMatcher:
             for a, ids in enumerate(x):
                 ans[i, a, : len(ids)] = ids
                 alen[i, a] = len(ids)
-        slots = np.where(rows >= 0, h.slot[np.maximum(rows, 0)], -1)
         if h.n_slots == 0:   # no row tokenised: every retrieved row is a pad
             return _PendingMatch(np.zeros((B, k), dtype=np.int8), None)
         lib = _native.load()
         with torch.cuda.stream(self.stream):
             dev = self.device
-            r = torch.from_numpy(np.ascontiguousarray(slots, dtype=np.int64)).pin_memory().to(dev, non_blocking=True)
+            # the retrieved rows go up as they are; the kernel maps row -> token slot on the device
+            r = torch.from_numpy(np.ascontiguousarray(rows, dtype=np.int64)).pin_memory().to(dev, non_blocking=True)
             at = torch.from_numpy(ans).pin_memory().to(dev, non_blocking=True)
             lt = torch.from_numpy(alen.astype(np.int32)).pin_memory().to(dev, non_blocking=True)
             ev = torch.from_numpy(every.astype(np.uint8)).pin_memory().to(dev, non_blocking=True)
             hit = torch.empty((B, k), dtype=torch.int8, device=dev)
             # one launch: wave (i, j) scans retrieved row j of query i for every answer of query i
-            _native.check(lib.drt_answer_match_i32(self.tok.data_ptr(), W, r.data_ptr(), B, k, at.data_ptr(),
-                                                   lt.data_ptr(), A, n_max, ev.data_ptr(), hit.data_ptr(),
+            _native.check(lib.drt_answer_match_i32(self.tok.data_ptr(), W, r.data_ptr(), self.slot_dev.data_ptr(),
+                                                   int(self.slot_dev.numel()), B, k, at.data_ptr(), lt.data_ptr(),
+                                                   A, n_max, ev.data_ptr(), hit.data_ptr(),
                                                    self.stream.cuda_stream), "drt_answer_match_i32")
             out = torch.empty((B, k), dtype=torch.int8, pin_memory=True)
             out.copy_(hit, non_blocking=True)

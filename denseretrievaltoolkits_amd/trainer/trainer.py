@@ -225,9 +225,11 @@ class Trainer:
     # behind an event.  Metrics stay per LOADER batch (get_metrics' NDCG is a batch-level ratio).
     ENCODE_WINDOW = 4096
     SEARCH_BATCH = 128
-    # one rank: enqueue a whole window's searches before the next window's tower pass (A/B switch of
-    # tools/c2_host_prof.py; off: the next tower pass goes behind the window's first searches)
-    EAGER_WINDOW_SEARCH = False
+    # one rank: a whole window's searches are enqueued before the next window's tower pass, so the host
+    # certifies and matches the window while the GPU runs that pass (in-process A/B, tools/c2_ab.py,
+    # profiles/r04ab_c2_window_order_ab.log: query stage 0.150 / 0.152 s vs 0.191 / 0.211 s with the
+    # next tower pass queued behind the window's first searches)
+    EAGER_WINDOW_SEARCH = True
     prefill_answer_tokens = True
     # host (and, mirrored, HBM) bytes of passage tokens prefilled during the corpus encode
     prefill_answer_max_bytes = 1 << 30
@@ -323,7 +325,7 @@ class Trainer:
             ids_all = np.empty((n, k), dtype=np.int64)
             done, bi, b0 = 0, 0, 0
             if self.world == 1 and self.EAGER_WINDOW_SEARCH and n:
-                # A/B: the whole window's searches first, then the next window's tower pass
+                # the whole window's searches first, then the next window's tower pass
                 sb = self.SEARCH_BATCH
                 loc = self.index.local
                 pend = loc.enqueue_batches([q_reps[a: a + sb] for a in range(0, n, sb)], k, to_host=True)

@@ -113,13 +113,14 @@ int drt_refine_sort(const float* cand_s, const int64_t* cand_i, const float* del
                     int64_t nq, int32_t kc, int32_t k, float* out_scores, int64_t* out_ids, void* stream);
 
 /* Answer matching of retrieved passages (has_answers, DRT/evaluator/nq_eval.py:187-218) on token ids
- * resident in HBM: tok [slots][W] int32 (-1 pads; evaluator/nq_eval.py RowAnswerMatcher), slots
- * [B][k] int64 = the token slot of each retrieved row (-1: pad row -> 0), ans [B][A][n_max] int32 +
- * alen [B][A] (the answers' token ids; alen 0 = no answer), every [B] (1: an empty answer, every
- * passage matches).  hit [B][k] int8 = 1 iff some answer occurs as a contiguous token window.  */
-int drt_answer_match_i32(const int32_t* tok, int32_t W, const int64_t* slots, int64_t B, int64_t k,
-                         const int32_t* ans, const int32_t* alen, int32_t A, int32_t n_max, const uint8_t* every,
-                         int8_t* hit, void* stream);
+ * resident in HBM: tok [slots][W] int32 (-1 pads; evaluator/nq_eval.py RowAnswerMatcher), rows [B][k]
+ * int64 = the retrieved index rows (-1: pad -> 0), slot_of [n_rows] int64 = each row's token slot (-1:
+ * not tokenised -> 0; slot_of NULL: rows already hold slots), ans [B][A][n_max] int32 + alen [B][A]
+ * (the answers' token ids; alen 0 = no answer), every [B] (1: an empty answer, every passage matches).
+ * hit [B][k] int8 = 1 iff some answer occurs as a contiguous token window.                      */
+int drt_answer_match_i32(const int32_t* tok, int32_t W, const int64_t* rows, const int64_t* slot_of, int64_t n_rows,
+                         int64_t B, int64_t k, const int32_t* ans, const int32_t* alen, int32_t A, int32_t n_max,
+                         const uint8_t* every, int8_t* hit, void* stream);
 
 /* Merge `nparts` per-shard top-k lists into one global top-k.
  * scores/ids: [nparts, nq, k_in] (each part sorted score desc, id asc, as
