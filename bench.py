@@ -190,6 +190,17 @@ def _tie_check(q, shard, gi, ci):
     return int(qi.size), gap
 
 
+def _quiesce_gc():
+    """Collect, then freeze every object alive so far (setup, earlier legs, the CPU baselines'
+    imports) into the collector's permanent generation: a full collection over that heap inside a
+    timed region is harness cost, not the path's (it was 0.215 s of the recipe leg's three timed
+    steps, 165 vs 119 ms per step, profiles/r04ad_*).  Objects the timed code creates are still
+    collected as usual."""
+    import gc
+    gc.collect()
+    gc.freeze()
+
+
 def cpu_baseline(args, shard, queries, gpu_result):
     """The oracle (numpy fp32 BLAS, like faiss IndexFlatIP's sgemm + top-k) timed on the host
     cores against the SAME 10M-row corpus the GPU searched: the shard streams to host in
@@ -364,6 +375,7 @@ def main():
     fb0 = fallbacks()
     unc0 = index.order_uncertified
 
+    _quiesce_gc()
     lib.drt_profile_enable(_native.PROF_SCAN, 1)
     if world > 1:
         dist.barrier()
@@ -453,9 +465,8 @@ def main():
         }
         if world == 1 and not args.no_cpu_baseline:
             out["cpu_baseline"] = cpu_baseline(args, shard, queries[args.warmup], results[0])
-    # the search leg's 15 GB corpus, index and results leave HBM before the model legs: the training
-    # legs' torch baselines reserve ~140 GB, and with the corpus still cached the recipe leg's
-    # allocations ran into the pool's limit (169 vs 119 ms per step in one process, r04s vs r04v)
+    # the search leg's 15 GB corpus, index and results leave HBM before the model legs (the training
+    # legs' torch baselines reserve ~140 GB)
     del shard, queries, results, index, local_index
     torch.cuda.synchronize()
     torch.cuda.empty_cache()
@@ -477,7 +488,8 @@ def main():
         import bench_legs as bench_encode
         if not args.no_cpu_baseline:
             out["encode"]["cpu_baseline"] = encode_cpu_baseline()
-        def leg(fn, *a, **kw):   # each leg starts from an empty cache (no pool pressure from the last)
+        def leg(fn, *a, **kw):   # each leg starts from an empty cache and a frozen heap
+            _quiesce_gc()
             r = fn(*a, **kw)
             torch.cuda.synchronize()
             torch.cuda.empty_cache()

@@ -240,6 +240,26 @@ def run_train_scores(device, bq=512, d=768, n_passages=(2, 8), steps=20, warmup=
     return res
 
 
+class _GcTimer:
+    """Wall time spent in Python's cyclic collector while registered."""
+
+    def __init__(self):
+        import gc
+        self.total, self.runs, self._t = 0.0, 0, None
+        gc.callbacks.append(self._cb)
+
+    def _cb(self, phase, info):
+        if phase == "start":
+            self._t = time.perf_counter()
+        elif self._t is not None:
+            self.total += time.perf_counter() - self._t
+            self.runs += 1
+
+    def close(self):
+        import gc
+        gc.callbacks.remove(self._cb)
+
+
 def run_train_step(device, bq=512, n=2, q_len=32, p_len=128, steps=3, warmup=1):
     """Config C3 end to end: one in-batch-negative training step of DRModel.forward (query tower on
     512 x 32 tokens, passage tower on 1024 x 128 tokens, score matrix + CE, backward into every
@@ -281,11 +301,19 @@ def run_train_step(device, bq=512, n=2, q_len=32, p_len=128, steps=3, warmup=1):
         for _ in range(warmup):
             step()
         torch.cuda.synchronize()
+        st0 = torch.cuda.memory_stats(device)
+        gc_t = _GcTimer()
         t0 = time.perf_counter()
         for _ in range(steps):
             step()
         torch.cuda.synchronize()
         ms = (time.perf_counter() - t0) / steps * 1e3
+        gc_t.close()
+        if name == "hip":   # host-side stalls inside the timed steps (allocator, collector)
+            st1 = torch.cuda.memory_stats(device)
+            res["hip_timed_host"] = {"gc_s": round(gc_t.total, 4), "gc_runs": gc_t.runs} | {
+                key: st1.get(key, 0) - st0.get(key, 0) for key in ("num_alloc_retries", "num_device_alloc",
+                                                                   "num_device_free")}
         res[name + "_ms"] = round(ms, 2)
         res[name + "_tflops"] = round(fl / (ms * 1e-3) / 1e12, 1)
     res["speedup"] = round(res["torch_fp32_ms"] / res["hip_ms"], 2)
