@@ -292,7 +292,9 @@ class DeviceRowMatcher:
         self._slots = 0
         self.slot_dev = None
         self._slot_version = None
-        self.stream = torch.cuda.Stream(self.device)
+        # high priority: a stream of its own hardware-queue class, so a batch's comparison kernels never
+        # queue behind the query tower pass the host enqueued on the compute stream meanwhile
+        self.stream = torch.cuda.Stream(self.device, priority=-1)
 
     def _upload(self):
         """Mirror the host slots: whole after a reallocation (version change), else only the slots
