@@ -1920,14 +1920,15 @@ __global__ __launch_bounds__(kMergeThreads) void merge_kernel(const float* score
 // caller's exact rescan).  Integer-valued rows and queries whose |partial sums| stay below 2^23
 // are scored exactly in fp32: eps = 0 and the fp32 order IS the exact order.
 //
-// refine_delta_kernel  grid (nq, kc / kRefSlice): exact sum for each candidate this rank owns
+// refine_delta_kernel  grid (nq, kc / slice): exact sum for each candidate this rank owns
 //   (global id in [row_offset, row_offset + n_local)) -> delta = exact - fp32 score (0 where not
 //   owned or past the window: shards add their deltas with one all-reduce SUM); cnt[q] = window
 //   size (-1 when eps = 0).
 // refine_sort_kernel   grid nq: the window by (fp32 score + delta desc, id asc) -> top-k.
 // ---------------------------------------------------------------------------
 constexpr int kRefThreads = 256;
-constexpr int kRefSlice = 64;   // candidates per work-group of refine_delta (16 per wave)
+constexpr int kRefSlice = 64;        // candidates per work-group of refine_delta, one GPU
+constexpr int kRefSliceShard = 256;  // ... on a shard of a sharded index (~1/W of them owned)
 constexpr int kRefSortThreads = 512;
 constexpr int kRefMax = kSelMaxK;
 
@@ -1948,6 +1949,7 @@ struct RefineArgs {
   int32_t* status;      // [nq] (indexed through qmap) or NULL
   const int32_t* qmap;  // output row of query q, or NULL
   bool set_status;      // status[row] = this stage's bits (the exact rescan clears it) instead of |=
+  int32_t slice;        // refine_delta: candidates per work-group (64 or 256; 0 = kRefSlice)
   float* out_s;         // refine_sort: [*, k]
   int64_t* out_i;
 };
@@ -2025,20 +2027,50 @@ __global__ __launch_bounds__(kRefThreads) void refine_prep_kernel(RefineArgs a) 
   }
 }
 
-// exact sums of the window's candidates this shard owns: each wave takes kRefSlice / 4 of them,
-// kRefUnroll at a time with every row load of the group in flight together (one HBM round trip
-// per group instead of one per candidate)
+// exact sums of the window's candidates this shard owns.  A work-group takes a slice of `slice`
+// candidates (64 on one GPU, 256 on a shard of a sharded index), writes delta 0 for the ones another
+// shard owns and compacts the owned ones into LDS; its 4 waves then split the owned list, kRefUnroll
+// rows at a time with every row load of the group in flight together (one HBM round trip per group
+// instead of one per candidate).  Round 4: the waves used to walk the slice itself, so on a W-way
+// sharded index ~(W-1)/W of their row slots were idle -- 461 us per 2048-query group at W = 8
+// for ~1/8 of the gathers (tools/sim_rank.py, profiles/r04af_*).
 constexpr int kRefUnroll = 8;
+constexpr int kRefSliceMax = kRefThreads;
 __global__ __launch_bounds__(kRefThreads) void refine_delta_kernel(RefineArgs a) {
+  __shared__ int own_j[kRefSliceMax];
+  __shared__ int n_own;
   const int64_t q = blockIdx.x;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int C = a.cnt[2 * q];
-  const int j0 = blockIdx.y * kRefSlice + wave * (kRefSlice / 4);
-  if (C <= j0) return;   // also: exact in fp32 (-1) or window too wide (-2)
-  const int j1 = j0 + kRefSlice / 4 < C ? j0 + kRefSlice / 4 : C;
+  const int jb = (int)blockIdx.y * a.slice;
+  if (C <= jb) return;   // also: exact in fp32 (-1) or window too wide (-2)
   const float* cs = a.cs + q * (int64_t)a.kc;
   const int64_t* ci = a.ci + q * (int64_t)a.kc;
   float* dq = a.delta + q * (int64_t)a.kc;
+  if (tid == 0) n_own = 0;
+  __syncthreads();
+  {
+    const int j = jb + tid;
+    bool own = false;
+    if (tid < a.slice && j < C) {
+      const int64_t id = ci[j];
+      const int64_t row = id - a.row_offset;
+      own = id >= 0 && row >= 0 && row < a.n_local;
+      if (!own) dq[j] = 0.0f;   // another shard's row: its delta arrives through the all-reduce
+    }
+    const uint64_t m = __ballot(own);
+    int base = 0;
+    if (lane == 0 && m) base = atomicAdd(&n_own, __builtin_popcountll(m));
+    base = __shfl(base, 0, 64);
+    if (own)
+      own_j[base + (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u))] = j;
+  }
+  __syncthreads();
+  const int n = n_own;
+  const int per = (n + 3) >> 2;
+  const int e0 = wave * per;
+  const int e1 = e0 + per < n ? e0 + per : n;
+  if (e0 >= e1) return;
   // this lane's query elements: 4-element chunks c = lane + 64 t of the row, in fp64
   constexpr int kMaxT = 4;   // d <= 1024
   const int nch = a.d >> 2;
@@ -2051,24 +2083,24 @@ __global__ __launch_bounds__(kRefThreads) void refine_delta_kernel(RefineArgs a)
 #pragma unroll
     for (int u = 0; u < 4; ++u) qv[t][u] = (double)(float)x[u];
   }
-  for (int jb = j0; jb < j1; jb += kRefUnroll) {
-    bool own[kRefUnroll];
+  for (int eb = e0; eb < e1; eb += kRefUnroll) {
+    bool ok[kRefUnroll];
+    int jj[kRefUnroll];
     int64_t row[kRefUnroll];
 #pragma unroll
     for (int u = 0; u < kRefUnroll; ++u) {
-      const int j = jb + u;
-      const int64_t id = j < j1 ? ci[j] : -1;
-      row[u] = id - a.row_offset;
-      own[u] = j < j1 && id >= 0 && row[u] >= 0 && row[u] < a.n_local;   // wave-uniform
+      ok[u] = eb + u < e1;   // wave-uniform
+      jj[u] = ok[u] ? own_j[eb + u] : 0;
+      row[u] = ok[u] ? ci[jj[u]] - a.row_offset : 0;
     }
     bf16x4 x[kRefUnroll][kMaxT];
 #pragma unroll
     for (int u = 0; u < kRefUnroll; ++u) {
-      const __bf16* pr = a.P + (own[u] ? row[u] : 0) * (int64_t)a.d;
+      const __bf16* pr = a.P + row[u] * (int64_t)a.d;
 #pragma unroll
       for (int t = 0; t < kMaxT; ++t) {
         const int c = lane + 64 * t;
-        x[u][t] = (own[u] && c < nch) ? *(const bf16x4*)(pr + 4 * c) : bf16x4{};
+        x[u][t] = (ok[u] && c < nch) ? *(const bf16x4*)(pr + 4 * c) : bf16x4{};
       }
     }
     double acc[kRefUnroll];
@@ -2087,7 +2119,7 @@ __global__ __launch_bounds__(kRefThreads) void refine_delta_kernel(RefineArgs a)
     if (lane == 0) {
 #pragma unroll
       for (int u = 0; u < kRefUnroll; ++u)
-        if (jb + u < j1) dq[jb + u] = own[u] ? (float)(acc[u] - (double)cs[jb + u]) : 0.0f;
+        if (ok[u]) dq[jj[u]] = (float)(acc[u] - (double)cs[jj[u]]);
     }
   }
 }
@@ -2472,7 +2504,8 @@ static int launch_refine(RefineArgs& ra, hipStream_t s) {
   if (ra.nq == 0) return DRT_OK;
   const ProfPair pp = prof_begin(PROF_SELECT, s);
   hipLaunchKernelGGL(refine_prep_kernel, dim3((unsigned)ra.nq), dim3(kRefThreads), 0, s, ra);
-  hipLaunchKernelGGL(refine_delta_kernel, dim3((unsigned)ra.nq, (unsigned)((ra.kc + kRefSlice - 1) / kRefSlice)),
+  if (ra.slice <= 0) ra.slice = kRefSlice;
+  hipLaunchKernelGGL(refine_delta_kernel, dim3((unsigned)ra.nq, (unsigned)((ra.kc + ra.slice - 1) / ra.slice)),
                      dim3(kRefThreads), 0, s, ra);
   hipLaunchKernelGGL(refine_sort_kernel, dim3((unsigned)ra.nq), dim3(kRefSortThreads), 0, s, ra);
   prof_end(pp, s);
@@ -2682,7 +2715,8 @@ int drt_refine_delta_bf16(const void* Q, int64_t nq, int32_t d, const void* P, i
   ra.status = status;
   hipStream_t s = (hipStream_t)stream;
   hipLaunchKernelGGL(refine_prep_kernel, dim3((unsigned)nq), dim3(kRefThreads), 0, s, ra);
-  hipLaunchKernelGGL(refine_delta_kernel, dim3((unsigned)nq, (unsigned)((kc + kRefSlice - 1) / kRefSlice)),
+  ra.slice = kRefSliceShard;   // the sharded protocol's entry: most candidates live on other shards
+  hipLaunchKernelGGL(refine_delta_kernel, dim3((unsigned)nq, (unsigned)((kc + ra.slice - 1) / ra.slice)),
                      dim3(kRefThreads), 0, s, ra);
   return hip_status(hipGetLastError());
 }

@@ -129,12 +129,14 @@ def test_dist_shape_errors(dev):
 
 @pytest.mark.parametrize("nparts,nq,k,fill", [(8, 128, 1000, 0.5), (2, 5, 2048, 1.0), (3, 7, 100, 0.0),
                                               (5, 9, 10, 0.3), (9, 4, 1000, 0.4), (16, 3, 1000, 0.2),
-                                              (8, 2, 1000, 0.05), (1, 6, 64, 0.7), (5, 3, 2048, 0.6)])
+                                              (8, 2, 1000, 0.05), (1, 6, 64, 0.7), (5, 3, 2048, 0.6),
+                                              (8, 3, 2048, 1.0), (6, 4, 1500, 0.95)])
 @pytest.mark.parametrize("count_word", [True, False])
 def test_merge_packed_vs_oracle(dev, nparts, nq, k, fill, count_word):
     """drt_topk_merge_packed against the oracle on random packed lists (unique keys, ragged fills,
     empty parts, overflow flags) for every kernel the shape selects: count merge (2-8 parts,
-    nparts * k <= 8192), tree merge (more parts or keys), plain per-query merge (one part).
+    nparts * k <= 16384, incl. full lists at that bound), tree merge (more parts or keys), plain
+    per-query merge (one part).
     count_word False: entry k carries the flags only (the pre-0.3 contract) -> the count merge
     measures each list itself and must give the same result."""
     import torch
