@@ -3,7 +3,7 @@
 n-row bf16 shard for 128 Gaussian queries, against thresholds that admit a chosen number of hits
 per query (the scores' rank-R value; R = 0 means no hits), in both hit-append flavours (picked by
 the expected-hit estimate the call derives from n_global).  HIP events on torch's stream.
-usage: python tools/scan_probe.py [--n 1000000] [--reps 20] [--ranks 0,1000,2000]"""
+usage: python tools/scan_probe.py [--n 1000000] [--reps 20] [--ranks 0,1000,2000] (-1: the sampled tau)"""
 from __future__ import annotations
 
 import argparse
@@ -34,9 +34,14 @@ def main():
     for R in ranks:
         if R == 0:
             taus[R] = torch.full((128,), float("inf"), device=dev)
-        else:
+        elif R < 0:   # the product's own sampled threshold (what ip_topk's filter pass runs against)
+            taus[R] = kernels.dist_tau(kernels.dist_sample(q, p, args.n, args.k)[None].contiguous(), args.k)
+        elif R <= 2048:
             sc, _, _ = kernels.ip_topk(q, p, R)
             taus[R] = sc[:, R - 1].contiguous()
+        else:   # past the kernel's k bound: a dense fp32 torch reference (rank-R score, near-exact)
+            taus[R] = torch.cat([(q.float() @ p[a: a + 2_000_000].float().T) for a in range(0, p.shape[0], 2_000_000)],
+                                1).topk(R, dim=1).values[:, R - 1].contiguous()
     torch.cuda.synchronize()
     from denseretrievaltoolkits_amd import _native
     lib = _native.load()
@@ -65,6 +70,11 @@ def main():
           f"{prof_read(1):.1f}, select + threshold {prof_read(2):.1f} us per launch", flush=True)
     for R in ranks:
         tau = taus[R]
+        if R < 0:
+            hits = sum(((q.float() @ p[a: a + 2_000_000].float().T) >= tau[:, None]).sum(1)
+                       for a in range(0, p.shape[0], 2_000_000)).float()
+            print(f"sampled tau: hits/query mean {hits.mean().item():.0f} min {hits.min().item():.0f} "
+                  f"max {hits.max().item():.0f}", flush=True)
         for flav, ng in (("dense", args.n), ("sparse", 10 * args.n)):
             for _ in range(2):
                 kernels.dist_filter(q, p, ng, args.k, 0, tau)
