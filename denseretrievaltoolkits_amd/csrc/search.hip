@@ -157,9 +157,9 @@ __device__ __forceinline__ void flush_hits(const ScanArgs& a, int64_t qbase, uin
 }
 
 // ---------------------------------------------------------------------------
-// Production scan: 16-row tiles on v_mfma_f32_16x16x32_bf16, 6-slot LDS ring
-// (prefetch distance 5: up to 5 x 24 KiB in flight per CU while the waves
-// compute, vs 2 x 48 KiB for the 32-row ring above).
+// Production scan: 16-row tiles on v_mfma_f32_16x16x32_bf16, 5-slot LDS ring at d = 768
+// (up to 4 x 24 KiB in flight per CU while the waves compute, vs 2 x 48 KiB for the
+// 32-row ring above).
 //   B operand (queries, VGPR-resident): lane l holds Q[q0 + 16 b + (l&15)]
 //     [32 s + 8 (l>>4) .. +8] for column block b = 0, 1 and k-step s.
 //   A operand (corpus, LDS): lane l reads row (l&15), 16-B chunk 4 s + (l>>4).
@@ -179,7 +179,10 @@ struct Scan16Cfg {
   static constexpr int GLDS_PER_WAVE = (GLDS_PER_TILE + NW - 1) / NW;   // 6 (4 waves) / 3 (8 waves) at d = 768
   static constexpr int HITS_BYTES = kHitCap * 10 + 16 + 2 * kQueriesPerWG * 4;
   static constexpr int NBUF_RAW = (160 * 1024 - HITS_BYTES) / TILE_BYTES;
-  static constexpr int NBUF = NBUF_RAW > 8 ? 8 : NBUF_RAW;
+  // at d = 768 a 5-slot ring (4 tiles = 96 KiB in flight per CU) beat 6 slots in three alternating A/B
+  // pairs on one box: 2.654-2.665 vs 2.687-2.704 ms per 10M launch (round 4, profiles/r04am_*)
+  static constexpr int NBUF_CAP = TILE_BYTES >= 24 * 1024 ? 5 : 8;
+  static constexpr int NBUF = NBUF_RAW > NBUF_CAP ? NBUF_CAP : NBUF_RAW;
   static constexpr int PD = NBUF - 1;
   static constexpr int RING_BYTES = NBUF * TILE_BYTES;
   static constexpr int HIT_KEY_OFF = RING_BYTES;
