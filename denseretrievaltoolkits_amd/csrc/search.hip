@@ -215,6 +215,77 @@ __device__ __forceinline__ void issue_tile16(const ScanArgs& a, uint32_t buf_lds
   }
 }
 
+// Lean LDS-DMA issue for the filter scan (rows contiguous: row0 0, rstride 1).  A lane's chunks sit at
+// fixed byte offsets from the tile's first row, so the tile address is ONE scalar 64-bit base (the
+// saddr form of global_load_lds) and the lane offsets are set once per launch -- no per-tile 64-bit
+// vector address math -- and the wave's loads of a tile share one m0 save / restore; the steady-state
+// ring wait is one constant s_waitcnt.  The last tile of a shard whose row count is not a multiple of
+// 16 takes issue_tile16 (row clamp).  Round 4: the per-tile issue was on the barrier-synchronised
+// critical path -- 2.707-2.718 -> 2.485-2.510 ms per 10M launch (-8 %) in three alternating A/B
+// pairs on one box (profiles/r04at_*; SQ counters before: 51 SALU + ~40 VALU per wave per tile,
+// profiles/r04ar_scan_pmc_hits.json).
+template <int D, int NW>
+struct LeanTile {
+  using C = Scan16Cfg<D, NW>;
+  static constexpr int G = C::GLDS_PER_WAVE;
+  uint32_t voff[G];   // per lane: byte offset of its 16-B chunk from the tile's first row
+  uint32_t loff[G];   // wave-uniform: LDS byte offset of the instruction's 1 KiB within a slot
+  __device__ __forceinline__ void init(const ScanArgs& a, int wave, int lane) {
+    const int rsub = lane >> 3, pos = lane & 7;
+#pragma unroll
+    for (int j = 0; j < G; ++j) {
+      int J = j * NW + wave;
+      if (C::GLDS_PER_TILE % NW != 0) J %= C::GLDS_PER_TILE;
+      const int g = J >> 1;
+      const int row = ((J & 1) << 3) + rsub;
+      const int c = pos ^ ((row >> 1) & 7);
+      voff[j] = (uint32_t)((row * a.ldp + g * 64 + c * 8) * 2);
+      loff[j] = (uint32_t)__builtin_amdgcn_readfirstlane(J * 1024);
+    }
+  }
+  __device__ __forceinline__ void issue(const ScanArgs& a, uint32_t slot_lds, int64_t tile, int64_t ntiles,
+                                        int wave, int lane) {
+    if (tile == ntiles - 1 && (a.nrows & (kT16 - 1)) != 0) {
+      issue_tile16<D, NW, true>(a, slot_lds, tile, wave, lane);
+      return;
+    }
+    const char* base = (const char*)(a.P + tile * kT16 * a.ldp);
+    if constexpr (G == 3) {
+      uint32_t keep;
+      asm volatile(
+          "s_mov_b32 %0, m0\n\t"
+          "s_mov_b32 m0, %2\n\t"
+          "s_nop 0\n\t"
+          "global_load_lds_dwordx4 %3, %1 nt\n\t"
+          "s_mov_b32 m0, %4\n\t"
+          "s_nop 0\n\t"
+          "global_load_lds_dwordx4 %5, %1 nt\n\t"
+          "s_mov_b32 m0, %6\n\t"
+          "s_nop 0\n\t"
+          "global_load_lds_dwordx4 %7, %1 nt\n\t"
+          "s_mov_b32 m0, %0"
+          : "=&s"(keep)
+          : "s"(base), "s"(slot_lds + loff[0]), "v"(voff[0]), "s"(slot_lds + loff[1]), "v"(voff[1]),
+            "s"(slot_lds + loff[2]), "v"(voff[2])
+          : "memory");
+    } else {
+#pragma unroll
+      for (int j = 0; j < G; ++j) {
+        uint32_t keep;
+        asm volatile(
+            "s_mov_b32 %0, m0\n\t"
+            "s_mov_b32 m0, %2\n\t"
+            "s_nop 0\n\t"
+            "global_load_lds_dwordx4 %3, %1 nt\n\t"
+            "s_mov_b32 m0, %0"
+            : "=&s"(keep)
+            : "s"(base), "s"(slot_lds + loff[j]), "v"(voff[j])
+            : "memory");
+      }
+    }
+  }
+};
+
 template <int N>
 __device__ __forceinline__ void wait_tiles_younger(int younger) {
   // this wave has `younger` tiles issued after the one it needs; each is N instructions
@@ -516,9 +587,11 @@ __global__ __launch_bounds__(512, 1) void ip_scan16r_kernel(ScanArgs a) {
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 
   // prologue: tiles 0 .. PD-1 in flight, tile 0 landed and read into registers
+  LeanTile<D, NW> lt;
+  lt.init(a, wave, lane);
 #pragma unroll
   for (int p = 0; p < PD; ++p)
-    if (p < my_tiles) issue_tile16<D, NW, true>(a, ring + p * C::TILE_BYTES, t0 + p * tstep, wave, lane);
+    if (p < my_tiles) lt.issue(a, ring + p * C::TILE_BYTES, t0 + p * tstep, ntiles, wave, lane);
   if (wave >= NW / 2) __builtin_amdgcn_s_setprio(1);
   {
     const int64_t last = my_tiles - 1 < PD - 1 ? my_tiles - 1 : PD - 1;
@@ -608,12 +681,13 @@ __global__ __launch_bounds__(512, 1) void ip_scan16r_kernel(ScanArgs a) {
   // registers flow straight through and the accumulators are never selected at run time
   auto iter = [&](int64_t it, f32x4& acc, int64_t& rb, const f32x4& prev, int64_t rb_prev) {
     const int64_t tile = t0 + it * tstep;
-    if (it + 1 < my_tiles) {
-      const int64_t last = it + PD - 1 < my_tiles - 1 ? it + PD - 1 : my_tiles - 1;
-      wait_tiles_younger<C::GLDS_PER_WAVE>((int)(last - it - 1));
+    if (it + PD <= my_tiles) {   // steady state: tiles it+1 .. it+PD-1 in flight, need it+1
+      wait_vmcnt<C::GLDS_PER_WAVE * (PD - 2)>();
+    } else if (it + 1 < my_tiles) {
+      wait_tiles_younger<C::GLDS_PER_WAVE>((int)(my_tiles - 1 - it - 1));
     }
     lds_barrier();   // tile it+1 landed (every wave's share); slot(it) fully read
-    if (it + PD < my_tiles) issue_tile16<D, NW, true>(a, ring + buf * C::TILE_BYTES, tile + PD * tstep, wave, lane);
+    if (it + PD < my_tiles) lt.issue(a, ring + buf * C::TILE_BYTES, tile + PD * tstep, ntiles, wave, lane);
     const int nslot = buf + 1 == C::NBUF ? 0 : buf + 1;
     mma_roll(acc, nslot);
     if (it > 0) epilogue(prev, rb_prev);
@@ -2456,7 +2530,8 @@ static int launch_scan_d(const ScanArgs& a, int mode, hipStream_t s) {
     // d > 768: the rolled reads hold two tiles' fragments beside the queries' (2 x d / 32 x 4 VGPRs +
     // d / 32 x 4): that spills from d = 832, so wider rows take the same loop with the fragments read
     // per k-step (ip_scan16_kernel: same MFMA order, identical results)
-    if (D > 768) {
+    // (ip_scan16r addresses rows as one contiguous run: row0 0, rstride 1 -- every filter pass)
+    if (D > 768 || a.row0 != 0 || a.rstride != 1) {
       if (dense_hits) hipLaunchKernelGGL((ip_scan16_kernel<D, SCAN_FILTER, 8, true>), grid, dim3(512), 0, s, a);
       else hipLaunchKernelGGL((ip_scan16_kernel<D, SCAN_FILTER, 8, false>), grid, dim3(512), 0, s, a);
     } else {
