@@ -223,7 +223,8 @@ __device__ __forceinline__ void issue_tile16(const ScanArgs& a, uint32_t buf_lds
 // 16 takes issue_tile16 (row clamp).  Round 4: the per-tile issue was on the barrier-synchronised
 // critical path -- 2.707-2.718 -> 2.485-2.510 ms per 10M launch (-8 %) in three alternating A/B
 // pairs on one box (profiles/r04at_*; SQ counters before: 51 SALU + ~40 VALU per wave per tile,
-// profiles/r04ar_scan_pmc_hits.json).
+// profiles/r04ar_scan_pmc_hits.json); then 32-bit tile / row counters and a tile base advanced by a
+// constant stride: 2.44-2.46 -> 2.38-2.40 ms (profiles/r04au_*).
 template <int D, int NW>
 struct LeanTile {
   using C = Scan16Cfg<D, NW>;
@@ -243,13 +244,14 @@ struct LeanTile {
       loff[j] = (uint32_t)__builtin_amdgcn_readfirstlane(J * 1024);
     }
   }
-  __device__ __forceinline__ void issue(const ScanArgs& a, uint32_t slot_lds, int64_t tile, int64_t ntiles,
-                                        int wave, int lane) {
-    if (tile == ntiles - 1 && (a.nrows & (kT16 - 1)) != 0) {
+  // `base` = the tile's first row (the caller advances it by a constant per tile); `partial` = this is
+  // the shard's last tile and it is short
+  __device__ __forceinline__ void issue(const ScanArgs& a, uint32_t slot_lds, const char* base, bool partial,
+                                        int64_t tile, int wave, int lane) {
+    if (partial) {
       issue_tile16<D, NW, true>(a, slot_lds, tile, wave, lane);
       return;
     }
-    const char* base = (const char*)(a.P + tile * kT16 * a.ldp);
     if constexpr (G == 3) {
       uint32_t keep;
       asm volatile(
@@ -557,12 +559,18 @@ __global__ __launch_bounds__(512, 1) void ip_scan16r_kernel(ScanArgs a) {
   uint8_t* hq = (uint8_t*)(smem + C::HIT_Q_OFF) + wave * kWaveSeg;
 
   const int64_t qbase = (int64_t)blockIdx.y * kQueriesPerWG;
-  const int64_t ntiles = (a.nrows + kT16 - 1) / kT16;
-  const int64_t t0 = blockIdx.x;
-  const int64_t tstep = gridDim.x;
-  const int64_t my_tiles = t0 < ntiles ? (ntiles - 1 - t0) / tstep + 1 : 0;
+  // tile and row indices in 32 bits (rows < 2^32: the hit keys carry 32-bit rows)
+  const int ntiles = (int)((a.nrows + kT16 - 1) / kT16);
+  const uint32_t nrows = (uint32_t)a.nrows;
+  const int t0 = blockIdx.x;
+  const int tstep = gridDim.x;
+  const int my_tiles = t0 < ntiles ? (ntiles - 1 - t0) / tstep + 1 : 0;
   if (my_tiles == 0) return;
+  const int partial_tile = (a.nrows & (kT16 - 1)) != 0 ? ntiles - 1 : -1;
   const uint32_t ring = lds_addr_of(smem);
+  // the next tile to issue, as a row pointer advanced by a constant (scalar) stride per tile
+  const int64_t tile_stride = (int64_t)tstep * kT16 * a.ldp * 2;
+  const char* next_base = (const char*)(a.P + (int64_t)t0 * kT16 * a.ldp);
 
   // 16 queries per wave: qbase + 16 * wave + r
   const int64_t qw = qbase + wave * 16;
@@ -590,11 +598,16 @@ __global__ __launch_bounds__(512, 1) void ip_scan16r_kernel(ScanArgs a) {
   LeanTile<D, NW> lt;
   lt.init(a, wave, lane);
 #pragma unroll
-  for (int p = 0; p < PD; ++p)
-    if (p < my_tiles) lt.issue(a, ring + p * C::TILE_BYTES, t0 + p * tstep, ntiles, wave, lane);
+  for (int p = 0; p < PD; ++p) {
+    if (p < my_tiles) {
+      const int tile = t0 + p * tstep;
+      lt.issue(a, ring + p * C::TILE_BYTES, next_base, tile == partial_tile, tile, wave, lane);
+      next_base += tile_stride;
+    }
+  }
   if (wave >= NW / 2) __builtin_amdgcn_s_setprio(1);
   {
-    const int64_t last = my_tiles - 1 < PD - 1 ? my_tiles - 1 : PD - 1;
+    const int last = my_tiles - 1 < PD - 1 ? my_tiles - 1 : PD - 1;
     wait_tiles_younger<C::GLDS_PER_WAVE>((int)last);
   }
   lds_barrier();
@@ -622,7 +635,7 @@ __global__ __launch_bounds__(512, 1) void ip_scan16r_kernel(ScanArgs a) {
     }
   };
   int wcnt = 0;   // entries in this wave's segment (wave-uniform)
-  auto epilogue = [&](const f32x4& acc, int64_t rowbase) {
+  auto epilogue = [&](const f32x4& acc, uint32_t rowbase) {
     const float mx = fmaxf(fmaxf(acc[0], acc[1]), fmaxf(acc[2], acc[3])) - tau;
     if (__ballot(mx >= 0.0f) == 0ull) return;
     // the tile's four row ballots at once (independent compares / popcounts, no branch per row);
@@ -633,7 +646,7 @@ __global__ __launch_bounds__(512, 1) void ip_scan16r_kernel(ScanArgs a) {
     int cv[4];
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
-      hv[j] = acc[j] >= tau && rowbase + j < a.nrows;
+      hv[j] = acc[j] >= tau && rowbase + j < nrows;
       mv[j] = __ballot(hv[j]);
       cv[j] = __builtin_popcountll(mv[j]);
     }
@@ -645,7 +658,7 @@ __global__ __launch_bounds__(512, 1) void ip_scan16r_kernel(ScanArgs a) {
         if (hv[j]) {
           const int pos = base + (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(mv[j] >> 32),
                                                                 __builtin_amdgcn_mbcnt_lo((uint32_t)mv[j], 0u));
-          hk[pos] = ((uint64_t)desc_key(acc[j]) << 32) | (uint64_t)(uint32_t)(rowbase + j);
+          hk[pos] = ((uint64_t)desc_key(acc[j]) << 32) | (uint64_t)(rowbase + j);
           hq[pos] = (uint8_t)r;
         }
         base += cv[j];
@@ -655,7 +668,7 @@ __global__ __launch_bounds__(512, 1) void ip_scan16r_kernel(ScanArgs a) {
     }
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
-      const bool hit = acc[j] >= tau && rowbase + j < a.nrows;
+      const bool hit = acc[j] >= tau && rowbase + j < nrows;
       const uint64_t m = __ballot(hit);
       if (m == 0ull) continue;
       const int c = __builtin_popcountll(m);
@@ -666,7 +679,7 @@ __global__ __launch_bounds__(512, 1) void ip_scan16r_kernel(ScanArgs a) {
       if (hit) {
         const int pos = wcnt + (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32),
                                                               __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
-        hk[pos] = ((uint64_t)desc_key(acc[j]) << 32) | (uint64_t)(uint32_t)(rowbase + j);
+        hk[pos] = ((uint64_t)desc_key(acc[j]) << 32) | (uint64_t)(rowbase + j);
         hq[pos] = (uint8_t)r;
       }
       wcnt += c;
@@ -674,27 +687,31 @@ __global__ __launch_bounds__(512, 1) void ip_scan16r_kernel(ScanArgs a) {
   };
 
   f32x4 accA, accB;
-  int64_t rbA = 0, rbB = 0;
+  uint32_t rbA = 0, rbB = 0;
   int buf = 0;   // slot of tile it (its fragments are in af[])
   // one tile: barrier, ring refill, MFMAs (+ reads of the next tile), deferred epilogue of the
   // previous tile; the loop body runs two of them in sequence (accA / accB) so the fragment
   // registers flow straight through and the accumulators are never selected at run time
-  auto iter = [&](int64_t it, f32x4& acc, int64_t& rb, const f32x4& prev, int64_t rb_prev) {
-    const int64_t tile = t0 + it * tstep;
+  auto iter = [&](int it, f32x4& acc, uint32_t& rb, const f32x4& prev, uint32_t rb_prev) {
+    const int tile = t0 + it * tstep;
     if (it + PD <= my_tiles) {   // steady state: tiles it+1 .. it+PD-1 in flight, need it+1
       wait_vmcnt<C::GLDS_PER_WAVE * (PD - 2)>();
     } else if (it + 1 < my_tiles) {
-      wait_tiles_younger<C::GLDS_PER_WAVE>((int)(my_tiles - 1 - it - 1));
+      wait_tiles_younger<C::GLDS_PER_WAVE>(my_tiles - 1 - it - 1);
     }
     lds_barrier();   // tile it+1 landed (every wave's share); slot(it) fully read
-    if (it + PD < my_tiles) lt.issue(a, ring + buf * C::TILE_BYTES, tile + PD * tstep, ntiles, wave, lane);
+    if (it + PD < my_tiles) {
+      const int ntile = tile + PD * tstep;
+      lt.issue(a, ring + buf * C::TILE_BYTES, next_base, ntile == partial_tile, ntile, wave, lane);
+      next_base += tile_stride;
+    }
     const int nslot = buf + 1 == C::NBUF ? 0 : buf + 1;
     mma_roll(acc, nslot);
     if (it > 0) epilogue(prev, rb_prev);
-    rb = tile * kT16 + 4 * kq;
+    rb = (uint32_t)tile * kT16 + 4 * kq;
     buf = nslot;
   };
-  for (int64_t it = 0; it < my_tiles; it += 2) {
+  for (int it = 0; it < my_tiles; it += 2) {
     iter(it, accA, rbA, accB, rbB);
     if (it + 1 < my_tiles) iter(it + 1, accB, rbB, accA, rbA);
   }
