@@ -2168,42 +2168,10 @@ __global__ __launch_bounds__(kRefThreads) void refine_prep_kernel(RefineArgs a) 
 // sharded index ~(W-1)/W of their row slots were idle -- 461 us per 2048-query group at W = 8
 // for ~1/8 of the gathers (tools/sim_rank.py, profiles/r04af_*).
 constexpr int kRefUnroll = 8;
-constexpr int kRefSliceMax = kRefThreads;
-__global__ __launch_bounds__(kRefThreads) void refine_delta_kernel(RefineArgs a) {
-  __shared__ int own_j[kRefSliceMax];
-  __shared__ int n_own;
-  const int64_t q = blockIdx.x;
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int C = a.cnt[2 * q];
-  const int jb = (int)blockIdx.y * a.slice;
-  if (C <= jb) return;   // also: exact in fp32 (-1) or window too wide (-2)
-  const float* cs = a.cs + q * (int64_t)a.kc;
-  const int64_t* ci = a.ci + q * (int64_t)a.kc;
-  float* dq = a.delta + q * (int64_t)a.kc;
-  if (tid == 0) n_own = 0;
-  __syncthreads();
-  {
-    const int j = jb + tid;
-    bool own = false;
-    if (tid < a.slice && j < C) {
-      const int64_t id = ci[j];
-      const int64_t row = id - a.row_offset;
-      own = id >= 0 && row >= 0 && row < a.n_local;
-      if (!own) dq[j] = 0.0f;   // another shard's row: its delta arrives through the all-reduce
-    }
-    const uint64_t m = __ballot(own);
-    int base = 0;
-    if (lane == 0 && m) base = atomicAdd(&n_own, __builtin_popcountll(m));
-    base = __shfl(base, 0, 64);
-    if (own)
-      own_j[base + (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u))] = j;
-  }
-  __syncthreads();
-  const int n = n_own;
-  const int per = (n + 3) >> 2;
-  const int e0 = wave * per;
-  const int e1 = e0 + per < n ? e0 + per : n;
-  if (e0 >= e1) return;
+// exact sums of the compacted owned candidates e0 .. e1 (own_j / own_row in LDS)
+__device__ __forceinline__ void refine_delta_rows(const RefineArgs& a, int64_t q, const float* cs, const int64_t* ci,
+                                                  float* dq, int lane, int e0, int e1, const int* own_j,
+                                                  const int64_t* own_row) {
   // this lane's query elements: 4-element chunks c = lane + 64 t of the row, in fp64
   constexpr int kMaxT = 4;   // d <= 1024
   const int nch = a.d >> 2;
@@ -2224,7 +2192,7 @@ __global__ __launch_bounds__(kRefThreads) void refine_delta_kernel(RefineArgs a)
     for (int u = 0; u < kRefUnroll; ++u) {
       ok[u] = eb + u < e1;   // wave-uniform
       jj[u] = ok[u] ? own_j[eb + u] : 0;
-      row[u] = ok[u] ? ci[jj[u]] - a.row_offset : 0;
+      row[u] = ok[u] ? own_row[eb + u] : 0;
     }
     bf16x4 x[kRefUnroll][kMaxT];
 #pragma unroll
@@ -2253,6 +2221,113 @@ __global__ __launch_bounds__(kRefThreads) void refine_delta_kernel(RefineArgs a)
 #pragma unroll
       for (int u = 0; u < kRefUnroll; ++u)
         if (ok[u]) dq[jj[u]] = (float)(acc[u] - (double)cs[jj[u]]);
+    }
+  }
+}
+constexpr int kRefSliceMax = kRefThreads;
+__global__ __launch_bounds__(kRefThreads) void refine_delta_kernel(RefineArgs a) {
+  __shared__ int own_j[kRefSliceMax];
+  __shared__ int64_t own_row[kRefSliceMax];   // the owned candidates' local rows (no dependent id load later)
+  __shared__ int n_own;
+  const int64_t q = blockIdx.x;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int C = a.cnt[2 * q];
+  const int jb = (int)blockIdx.y * a.slice;
+  if (C <= jb) return;   // also: exact in fp32 (-1) or window too wide (-2)
+  const float* cs = a.cs + q * (int64_t)a.kc;
+  const int64_t* ci = a.ci + q * (int64_t)a.kc;
+  float* dq = a.delta + q * (int64_t)a.kc;
+  if (tid == 0) n_own = 0;
+  __syncthreads();
+  {
+    const int j = jb + tid;
+    bool own = false;
+    int64_t row = 0;
+    if (tid < a.slice && j < C) {
+      const int64_t id = ci[j];
+      row = id - a.row_offset;
+      own = id >= 0 && row >= 0 && row < a.n_local;
+      if (!own) dq[j] = 0.0f;   // another shard's row: its delta arrives through the all-reduce
+    }
+    const uint64_t m = __ballot(own);
+    int base = 0;
+    if (lane == 0 && m) base = atomicAdd(&n_own, __builtin_popcountll(m));
+    base = __shfl(base, 0, 64);
+    if (own) {
+      const int e = base + (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+      own_j[e] = j;
+      own_row[e] = row;
+    }
+  }
+  __syncthreads();
+  const int n = n_own;
+  const int per = (n + 3) >> 2;
+  const int e0 = wave * per;
+  const int e1 = e0 + per < n ? e0 + per : n;
+  if (e0 < e1) refine_delta_rows(a, q, cs, ci, dq, lane, e0, e1, own_j, own_row);
+}
+
+// One shard (ip_topk / resolve: every candidate is this shard's): each wave takes kRefSlice / 4 window
+// entries directly, no compaction (the compaction kernel above measured 71-82 vs 57 us per 10M batch).
+__global__ __launch_bounds__(kRefThreads) void refine_delta_local_kernel(RefineArgs a) {
+  const int64_t q = blockIdx.x;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int C = a.cnt[2 * q];
+  const int j0 = blockIdx.y * kRefSlice + wave * (kRefSlice / 4);
+  if (C <= j0) return;   // also: exact in fp32 (-1) or window too wide (-2)
+  const int j1 = j0 + kRefSlice / 4 < C ? j0 + kRefSlice / 4 : C;
+  const float* cs = a.cs + q * (int64_t)a.kc;
+  const int64_t* ci = a.ci + q * (int64_t)a.kc;
+  float* dq = a.delta + q * (int64_t)a.kc;
+  // this lane's query elements: 4-element chunks c = lane + 64 t of the row, in fp64
+  constexpr int kMaxT = 4;   // d <= 1024
+  const int nch = a.d >> 2;
+  double qv[kMaxT][4];
+  const __bf16* qr = a.Q + q * (int64_t)a.d;
+#pragma unroll
+  for (int t = 0; t < kMaxT; ++t) {
+    const int c = lane + 64 * t;
+    const bf16x4 x = c < nch ? *(const bf16x4*)(qr + 4 * c) : bf16x4{};
+#pragma unroll
+    for (int u = 0; u < 4; ++u) qv[t][u] = (double)(float)x[u];
+  }
+  for (int jb = j0; jb < j1; jb += kRefUnroll) {
+    bool own[kRefUnroll];
+    int64_t row[kRefUnroll];
+#pragma unroll
+    for (int u = 0; u < kRefUnroll; ++u) {
+      const int j = jb + u;
+      const int64_t id = j < j1 ? ci[j] : -1;
+      row[u] = id - a.row_offset;
+      own[u] = j < j1 && id >= 0 && row[u] >= 0 && row[u] < a.n_local;   // wave-uniform
+    }
+    bf16x4 x[kRefUnroll][kMaxT];
+#pragma unroll
+    for (int u = 0; u < kRefUnroll; ++u) {
+      const __bf16* pr = a.P + (own[u] ? row[u] : 0) * (int64_t)a.d;
+#pragma unroll
+      for (int t = 0; t < kMaxT; ++t) {
+        const int c = lane + 64 * t;
+        x[u][t] = (own[u] && c < nch) ? *(const bf16x4*)(pr + 4 * c) : bf16x4{};
+      }
+    }
+    double acc[kRefUnroll];
+#pragma unroll
+    for (int u = 0; u < kRefUnroll; ++u) {
+      acc[u] = 0.0;
+#pragma unroll
+      for (int t = 0; t < kMaxT; ++t)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) acc[u] = __builtin_fma(qv[t][e], (double)(float)x[u][t][e], acc[u]);
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1)
+#pragma unroll
+      for (int u = 0; u < kRefUnroll; ++u) acc[u] += __shfl_xor(acc[u], o, 64);
+    if (lane == 0) {
+#pragma unroll
+      for (int u = 0; u < kRefUnroll; ++u)
+        if (jb + u < j1) dq[jb + u] = own[u] ? (float)(acc[u] - (double)cs[jb + u]) : 0.0f;
     }
   }
 }
@@ -2533,7 +2608,18 @@ static int launch_scan_d(const ScanArgs& a, int mode, hipStream_t s) {
   if (a.nq == 0 || a.nrows == 0) return DRT_OK;
   const unsigned gy = (unsigned)((a.nq + kQueriesPerWG - 1) / kQueriesPerWG);
   const int64_t ntiles = (a.nrows + kT16 - 1) / kT16;
-  const dim3 grid(scan_grid_x(ntiles), gy);
+  // Several 128-query blocks in one launch (a group of batches): gridDim.x = CUs / blocks, a multiple
+  // of 8, so work-groups (x, y) and (x, y') -- the same tiles for different query blocks -- sit on the
+  // same XCD (work-groups are dealt to XCDs round-robin by linear id) and run at the same time: a tile
+  // comes from HBM once and from that XCD's L2 for the other blocks.  (gridDim.x = CUs ran the blocks
+  // one after another, each streaming the whole shard from HBM.)
+  int gx = scan_grid_x(ntiles);
+  if (gy > 1 && ntiles >= 8) {
+    const int cus = scan_grid_x((int64_t)1 << 40);
+    const int share = std::max(8, (cus / (int)gy) & ~7);
+    gx = (int)std::min<int64_t>(ntiles, share);
+  }
+  const dim3 grid(gx, gy);
   if (mode == SCAN_FILTER) {
     // 8 waves (2 per SIMD), 16 queries each; fragment reads of the next tile rolled into this
     // tile's MFMAs, non-temporal corpus loads, s_setprio 1 for waves 4-7 (r02 A/B, tools/scan_ab.py,
@@ -2638,8 +2724,8 @@ static int launch_refine(RefineArgs& ra, hipStream_t s) {
   if (ra.nq == 0) return DRT_OK;
   const ProfPair pp = prof_begin(PROF_SELECT, s);
   hipLaunchKernelGGL(refine_prep_kernel, dim3((unsigned)ra.nq), dim3(kRefThreads), 0, s, ra);
-  if (ra.slice <= 0) ra.slice = kRefSlice;
-  hipLaunchKernelGGL(refine_delta_kernel, dim3((unsigned)ra.nq, (unsigned)((ra.kc + ra.slice - 1) / ra.slice)),
+  // the one-GPU entries (ip_topk, resolve): every candidate is this shard's
+  hipLaunchKernelGGL(refine_delta_local_kernel, dim3((unsigned)ra.nq, (unsigned)((ra.kc + kRefSlice - 1) / kRefSlice)),
                      dim3(kRefThreads), 0, s, ra);
   hipLaunchKernelGGL(refine_sort_kernel, dim3((unsigned)ra.nq), dim3(kRefSortThreads), 0, s, ra);
   prof_end(pp, s);
