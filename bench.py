@@ -345,7 +345,8 @@ def main():
         srch.GROUP_QUERIES = qb                 # several GPUs: one batch per group
     elif args.group_queries > 0:
         srch.GROUP_QUERIES = args.group_queries
-        srch.GROUP_MIN_ROWS = 0                 # one-GPU: grouped path too
+        srch.GROUP_MIN_ROWS = 0                 # one-GPU: grouped path too, at any shard size
+        srch.GROUP_MAX_ROWS = 1 << 62
     use_global = (world > 1 and args.protocol == "global_tau") or (world == 1 and n_local >= srch.GROUP_MIN_ROWS)
     # the product path: the same index objects and certified, pipelined batch search that
     # BaseFaissIPRetriever.batch_search / Trainer.evaluate use (search.py); every query

@@ -109,12 +109,16 @@ def _pipeline(batches, enqueue, finish):
 # all-gather and the merge -- are paid once per GROUP of query batches; every batch still streams
 # the whole shard once in its own filter scan.  Queries per group (16 batches of 128):
 GROUP_QUERIES = 2048
-# one-GPU indexes take the grouped path from this many rows up.  Off by default: on one GPU the
-# group's sample launch (2048 queries over ~0.7 % of the rows, every score written out) costs
-# what the per-batch sample launches cost, and the back-to-back filter scans measured 2-3 %
-# slower (tools/search_ab.py, bench.py --group-queries 0 vs default on one box:
-# profiles/r02j_bench_*.json); across GPUs the group also saves two collectives per batch.
-GROUP_MIN_ROWS = 1 << 62
+# one-GPU indexes take the grouped path from this many rows up (round 2/3 it was off: the group's
+# blocks then ran one after another and the back-to-back filter scans measured 2-3 % slower,
+# profiles/r02j_bench_*.json; across GPUs the group also saves two collectives per batch)
+GROUP_MIN_ROWS = 500_000
+# ... and up to this many (round 4): a group's filter launch runs its 16 query blocks side by side on
+# each XCD (csrc/search.hip launch_scan_d) and a tile is fetched once for all of them while they stay
+# within the XCD's L2 of each other -- 1M rows: 0.30-0.33 vs 0.42 ms per 128-query batch (same ids,
+# profiles/r04be_ab1m.log); over a 10M shard they drift apart and the per-batch path stays
+# (profiles/r04bc_trace_grouped_1gpu.txt).  Several GPUs: ShardedFlatIP groups at any size.
+GROUP_MAX_ROWS = 2_500_000
 
 
 def _groups(batches, cap=None):
@@ -181,6 +185,22 @@ def _gtau_finish_group(pend, redo):
             res.append((s[o:o + nb], i[o:o + nb]))
         o += nb
     return res, nredo, _order_uncertified(h)
+
+
+class _GroupPend:
+    """One enqueued group of ``FlatIPIndex.enqueue_batches`` (its result, once finished)."""
+    __slots__ = ("pend", "k", "id_offset", "res")
+
+    def __init__(self, pend, k, id_offset):
+        self.pend, self.k, self.id_offset, self.res = pend, k, id_offset, None
+
+
+class _GroupMember:
+    """Batch j of an enqueued group."""
+    __slots__ = ("group", "j")
+
+    def __init__(self, group, j):
+        self.group, self.j = group, j
 
 
 class FlatIPIndex:
@@ -301,12 +321,32 @@ class FlatIPIndex:
         BaseFaissIPRetriever.batch_search, Trainer.evaluate and bench.py time."""
         return list(self.search_batches_iter(batches, k, id_offset, outs))
 
+    def _use_groups(self) -> bool:
+        return GROUP_MIN_ROWS <= self.ntotal <= GROUP_MAX_ROWS and self.ntotal < 0xFFFFFFFF
+
     def enqueue_batches(self, batches, k: int, id_offset: int = 0, to_host: bool = False) -> list:
-        """Every batch's search enqueued now (per-batch path); collect each with ``finish_batch``."""
-        return [self._enqueue(q, k, id_offset, None, to_host) for q in batches]
+        """Every batch's search enqueued now (in groups where ``search_batches`` would group them);
+        collect each with ``finish_batch``."""
+        if not self._use_groups():
+            return [self._enqueue(q, k, id_offset, None, to_host) for q in batches]
+        out = []
+        stats = self._stats_arg()
+        for g in _groups(list(batches)):
+            gp = _GroupPend(_gtau_enqueue_group(self, [self._queries(q) for q in g], k, self.ntotal, id_offset,
+                                                lambda t: t.unsqueeze(0), to_host, stats=stats), k, id_offset)
+            out += [_GroupMember(gp, j) for j in range(len(g))]
+        return out
 
     def finish_batch(self, pend):
         """(scores, ids) of one ``enqueue_batches`` entry, certified (uncertified queries redone)."""
+        if isinstance(pend, _GroupMember):
+            gp = pend.group
+            if gp.res is None:   # the group's certificates are checked once, by its first member
+                res, nredo, nunc = _gtau_finish_group(gp.pend, lambda q: self.search_device(q, gp.k, gp.id_offset))
+                self.group_fallbacks += nredo
+                self.order_uncertified += nunc
+                gp.res = res
+            return gp.res[pend.j]
         return self._finish(pend)
 
     def search_batches_iter(self, batches, k: int, id_offset: int = 0, outs=None, to_host: bool = False):
@@ -315,7 +355,7 @@ class FlatIPIndex:
         batch j + 1.  ``to_host``: yield numpy (scores, ids) from pinned copies staged behind each
         batch (no stream-draining .cpu() per batch)."""
         batches = list(batches)
-        if outs is None and self.ntotal >= GROUP_MIN_ROWS and self.ntotal < 0xFFFFFFFF:
+        if outs is None and self._use_groups():
             yield from self._search_groups(batches, k, id_offset, to_host)
             return
         yield from _pipeline(batches, lambda j, q: self._enqueue(q, k, id_offset, outs[j] if outs else None,

@@ -84,6 +84,30 @@ def test_filter_scan_flavours_bit_exact(dev, nq, n, d, k):
     np.testing.assert_array_equal(gs, es)
 
 
+@pytest.mark.gpu
+def test_flat_index_enqueue_batches_grouped(dev, monkeypatch):
+    """enqueue_batches / finish_batch (Trainer.evaluate's eager window path) on a shard inside the
+    grouped range: batches enqueued in groups, collected per batch in any order, host-staged ids equal
+    to the oracle's."""
+    import torch
+    from denseretrievaltoolkits_amd import search as srch
+    monkeypatch.setattr(srch, "GROUP_MIN_ROWS", 0)
+    monkeypatch.setattr(srch, "GROUP_QUERIES", 64)
+    rng = np.random.default_rng(78)
+    q, p, k = int_bf16(rng, (150, 768), -4, 4), int_bf16(rng, (120001, 768), -4, 4), 1000
+    es, ei = orc.ip_topk(q, p, k)
+    idx = srch.FlatIPIndex.from_rows(to_dev_bf16(p, dev))
+    qd = to_dev_bf16(q, dev)
+    bounds = [(0, 40), (40, 64), (64, 100), (100, 150)]   # ragged, across groups of 64 queries
+    pend = idx.enqueue_batches([qd[a:b] for a, b in bounds], k, to_host=True)
+    assert all(isinstance(x, srch._GroupMember) for x in pend)
+    for j in (2, 0, 3, 1):   # any order: a group is finished once, by whichever member comes first
+        s, i = idx.finish_batch(pend[j])
+        a, b = bounds[j]
+        np.testing.assert_array_equal(np.asarray(i), ei[a:b])
+        np.testing.assert_array_equal(np.asarray(s), es[a:b])
+
+
 @pytest.mark.parametrize("case", ["int", "gauss", "ties"])
 def test_flat_index_search_batches_grouped(dev, case, monkeypatch):
     """FlatIPIndex.search_batches in groups (one sample launch + one merge per group, one filter
