@@ -300,7 +300,12 @@ def pmc_traffic(args, world):
     configuration; None when no such measurement exists."""
     import glob
     want = {"n_corpus": args.n_corpus, "world": world, "qb": args.qb, "k": args.k, "dim": args.dim}
-    for f in sorted(glob.glob(os.path.join(REPO, "profiles", "*_pmc_traffic.json")), reverse=True):
+    import re
+
+    def order(f):   # newest measurement first: round, then tag (a..z, aa..az, ba.. : by length, then letters)
+        m = re.match(r"r(\d+)([a-z]*)_", os.path.basename(f))
+        return (int(m.group(1)), len(m.group(2)), m.group(2)) if m else (-1, 0, "")
+    for f in sorted(glob.glob(os.path.join(REPO, "profiles", "*_pmc_traffic.json")), key=order, reverse=True):
         try:
             with open(f) as fh:
                 rec = json.load(fh)
