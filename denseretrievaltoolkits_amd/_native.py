@@ -17,6 +17,7 @@ from .build_native import LIB_PATH
 
 DRT_OK = 0
 DRT_EINVAL = -1
+ROW_STATS_LEN = 34   # DRT_ROW_STATS_LEN (include/drt.h): floats of drt_row_stats_bf16's statistics
 
 _lock = threading.Lock()
 _lib = None
@@ -57,6 +58,9 @@ _SIGNATURES = [
                                      c_vp, c_vp]),
     ("drt_ip_topk_resolve_exact", c_i32, [c_vp, c_i64, c_vp, c_i64, c_i32, c_i32, c_i64, c_vp, c_vp, c_vp, c_vp,
                                           c_vp, c_sz, c_vp, c_vp]),
+    ("drt_ip_topk_resolve_wide_workspace", c_sz, [c_i64, c_i32]),
+    ("drt_ip_topk_resolve_wide", c_i32, [c_vp, c_i64, c_vp, c_i64, c_i32, c_i32, c_i64, c_vp, c_vp, c_vp, c_vp,
+                                         c_vp, c_sz, c_vp, c_vp]),
     ("drt_refine_delta_bf16", c_i32, [c_vp, c_i64, c_i32, c_vp, c_i64, c_i64, c_vp, c_vp, c_i32, c_i32, c_vp, c_vp,
                                       c_vp, c_vp, c_vp, c_vp]),
     ("drt_refine_sort", c_i32, [c_vp, c_vp, c_vp, c_vp, c_i64, c_i32, c_i32, c_vp, c_vp, c_vp]),

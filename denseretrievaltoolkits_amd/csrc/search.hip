@@ -2042,16 +2042,32 @@ __global__ __launch_bounds__(kMergeThreads) void merge_kernel(const float* score
 // in yet another order); this stage makes the result canonical: the order of the EXACT scores
 // (fp64 sums of the bf16 products), ties by ascending id -- what an fp64 CPU evaluator returns.
 //
-// Error bound (any fp32 summation order, each addition rounded to nearest): |fl(s) - s| <=
-// gamma_d sum_i |q_i p_i| <= d u ||q||_2 ||p||_2 (u = 2^-24); eps = 2.5 d u ||q|| max_row ||p||
-// leaves a factor 2.5 of slack (faithful rather than nearest rounding inside the MFMA, the fp32
-// norms' own rounding).  With s_k the k-th candidate's fp32 score, every row of the exact top-k
-// has fp32 score >= B = s_k - 2 eps, so the candidates are exactly the entries >= B of a list
-// that (a) holds every hit >= B -- its last entry is < B, or the hits ended -- and (b) saw every
-// row >= B -- the filter threshold tau <= B.  (a) fails: status bit 1 (the window is wider than
-// the list: more than kc - k near-ties; the fp32 order is kept).  (b) fails: status bit 0 (the
-// caller's exact rescan).  Integer-valued rows and queries whose |partial sums| stay below 2^23
-// are scored exactly in fp32: eps = 0 and the fp32 order IS the exact order.
+// Error bound of the scan's fp32 score (round 5, measured: tools/mfma_numerics.py,
+// profiles/r05b_mfma.json).  Every kernel that produces candidate scores (ip_scan16r_kernel,
+// ip_scan16_kernel) accumulates one (query, row) score as a chain of T = d / 32 dependent
+// v_mfma_f32_16x16x32_bf16 steps, step t adding the 32 exact bf16 products of elements
+// [32t, 32t + 32) to the accumulator S_t.  One step is NOT a sequence of fp32 additions: the 33 terms
+// are aligned to the largest one with 3 guard bits below fp32's last bit and the bits below that are
+// truncated (32 products of 2^-28 next to a 1 vanish, 2^-26 survive; C = 2^24 plus 32 ones gives
+// 2^24 + 32), then the sum is rounded once.  Worst measured error of one step: 7.9 u (|C| + sum |p|)
+// (one large product, 31 just under the cut); the model gives < 8 u max|term| + 2 u |result|, so
+//     |err step t| <= 10 u (|S_t| + sum_{i in step t} |q_i p_i|),      u = 2^-24.
+// By Cauchy-Schwarz on the prefixes, |S_t| <= ||q_[0,32t)|| * max_rows ||p_[0,32t)||, and the products
+// sum to at most ||q|| max ||p||, so over the chain
+//     eps = 10 u (1 + 1e-3) (sum_{t=1}^{T-1} Qp_t Pp_t + ||q|| Pp_T),
+// Qp_t = ||q_[0,32t)|| (per query), Pp_t = max over rows of ||p_[0,32t)|| (row statistics, one value
+// per k-step).  Uniformly spread energy gives ~T/2 + 1 = 13 (x 10 u ||q|| max ||p||) at d = 768:
+// 15x tighter than the round-4 bound 2.5 d u ||q|| max ||p|| (an fp32 summation in any order) -- the
+// C2 leg's untrained-tower embeddings, whose 1000th score has ~100 rows within the old 2 eps, now
+// certify (tools/c2_window_probe.py).  Chains of 24 steps measured at most 1.5 u sum_t |S_t|.
+// With s_k the k-th candidate's fp32 score, every row of the exact top-k has fp32 score >= B =
+// s_k - 2 eps (the k-th exact score is >= s_k - eps), so the candidates are exactly the entries >= B
+// of a list that (a) holds every hit >= B -- its last entry is < B, or the hits ended -- and (b) saw
+// every row >= B -- the filter threshold tau <= B.  Either failing sets status bit 1; the product then
+// runs the wide resolve (drt_ip_topk_resolve_wide): a filter pass at threshold B, the exact sums of
+// every row it collects (up to kWideCap per query) and an exact-key selection.  Integer-valued rows
+// and queries whose |partial sums| stay below 2^23 are scored exactly in fp32: eps = 0 and the fp32
+// order IS the exact order.
 //
 // refine_delta_kernel  grid (nq, kc / slice): exact sum for each candidate this rank owns
 //   (global id in [row_offset, row_offset + n_local)) -> delta = exact - fp32 score (0 where not
@@ -2106,32 +2122,59 @@ __device__ __forceinline__ T ref_block_sum(T v, T* scr) {
   return r;
 }
 
-// eps of query q (0: exact in fp32).  Every work-group of q computes the same value.
-__device__ __forceinline__ float refine_eps(const RefineArgs& a, int64_t q, float* fscr, int* iscr) {
+// Row statistics (drt_row_stats_bf16): [0] max_rows ||p||^2, [1] 1.0f while every element is an
+// integer, [2 + t] max_rows ||p_[0, 32 (t + 1))||^2 for the k-steps t < ceil(d / 32) (the prefix
+// norms of the error bound above).
+constexpr int kStatBlocks = 32;   // d <= 1024
+constexpr int kStatsLen = 2 + kStatBlocks;
+
+// eps of query q (0: exact in fp32; the bound above).  Every work-group of q computes the same value.
+// dscr: >= kStatBlocks + 1 doubles of LDS.
+__device__ __forceinline__ float refine_eps(const RefineArgs& a, int64_t q, float* fscr, int* iscr, double* dscr) {
   const __bf16* qr = a.Q + q * (int64_t)a.d;
-  float ss = 0.0f;
+  const int nb = (a.d + 31) >> 5;
   int nonint = 0;
   for (int i = threadIdx.x; i < a.d; i += blockDim.x) {
     const float v = (float)qr[i];
-    ss += v * v;
     nonint |= (v != __builtin_rintf(v)) ? 1 : 0;
   }
-  ss = ref_block_sum(ss, fscr);
-  nonint = ref_block_sum(nonint, iscr);
-  const float qn = __builtin_sqrtf(ss) * 1.0001f;
-  const float pmax = __builtin_sqrtf(a.stats[0]) * 1.0001f;
-  const bool pint = a.stats[1] != 0.0f;
-  if (pint && nonint == 0 && qn * pmax < 8388608.0f) return 0.0f;
-  return 2.5f * (float)a.d * 5.9604645e-8f * qn * pmax + 1e-30f;
+  if ((int)threadIdx.x < nb) {   // this k-step's squared query norm, exactly enough in fp64
+    double ss = 0.0;
+    const int e1 = min(a.d, 32 * (int)threadIdx.x + 32);
+    for (int i = 32 * threadIdx.x; i < e1; ++i) {
+      const double v = (double)(float)qr[i];
+      ss += v * v;
+    }
+    dscr[threadIdx.x] = ss;
+  }
+  nonint = ref_block_sum(nonint, iscr);   // (its barriers also publish dscr)
+  if (threadIdx.x == 0) {
+    double qp2 = 0.0, acc = 0.0;
+    for (int t = 0; t < nb; ++t) {
+      if (t > 0) acc += __builtin_sqrt(qp2 * (double)a.stats[2 + t - 1]);
+      qp2 += dscr[t];
+    }
+    const double pmax2 = (double)a.stats[0];
+    acc += __builtin_sqrt(qp2 * pmax2);
+    const bool pint = a.stats[1] != 0.0f;
+    const double qn = __builtin_sqrt(qp2) * 1.0001, pmax = __builtin_sqrt(pmax2) * 1.0001;
+    float e;
+    if (pint && nonint == 0 && qn * pmax < 8388608.0) e = 0.0f;
+    else e = (float)(10.0 * 5.9604644775390625e-8 * 1.001 * acc) + 1e-30f;
+    dscr[kStatBlocks] = (double)e;
+  }
+  __syncthreads();
+  return (float)dscr[kStatBlocks];
 }
 
 // per query: eps, the window C (entries >= B = s_k - 2 eps) and the certificate bits -> cnt[q]
 __global__ __launch_bounds__(kRefThreads) void refine_prep_kernel(RefineArgs a) {
   __shared__ float fscr[kRefThreads / 64];
   __shared__ int iscr[kRefThreads / 64];
+  __shared__ double dscr[kStatBlocks + 1];
   const int64_t q = blockIdx.x;
   const int tid = threadIdx.x;
-  const float eps = refine_eps(a, q, fscr, iscr);
+  const float eps = refine_eps(a, q, fscr, iscr, dscr);
   const float* cs = a.cs + q * (int64_t)a.kc;
   const int64_t* ci = a.ci + q * (int64_t)a.kc;
   int nval = 0;
@@ -2144,9 +2187,8 @@ __global__ __launch_bounds__(kRefThreads) void refine_prep_kernel(RefineArgs a) 
   const bool wide = eps != 0.0f && C == a.kc && nval == a.kc;               // window wider than the list
   // the window reaches below the filter threshold: rows in [B, tau) were never collected, so the
   // exact order of the window cannot be certified from the list.  The fp32 top-k itself is exact
-  // (every row >= tau was collected; the select certified k <= hits): keep it in the fp32 order
-  // (faiss's semantics) rather than rescanning the shard densely -- degenerate embeddings (e.g. an
-  // untrained tower, every score within the fp32 error of the k-th) hit this for every query.
+  // (every row >= tau was collected; the select certified k <= hits): it stays in place in the fp32
+  // order with status bit 1, and the caller's wide resolve (a filter pass at B) replaces it.
   const bool below = eps != 0.0f && a.tau && nval >= a.k && a.tau[q] > B;
   if (tid == 0) {
     a.cnt[2 * q] = eps == 0.0f ? -1 : ((wide || below) ? -2 : C);
@@ -2402,55 +2444,286 @@ __global__ __launch_bounds__(kRefSortThreads) void refine_sort_kernel(RefineArgs
   }
 }
 
-// Row statistics for the refine bound: stats[0] = max over rows of the fp32 sum of squares
-// (as a non-negative float, combined by an integer max of its bits), stats[1] = 1.0f while every
-// element seen is an integer (combined by AND of the bits of 1.0f / 0.0f).
+// ---------------------------------------------------------------------------
+// Wide resolve (status bit 1): the canonical order of a query whose near-tie window did not fit the
+// candidate list, or reached below the filter threshold -- degenerate embeddings whose scores crowd
+// within the fp32 error of the k-th one.  Per query of a chunk (host: drt_ip_topk_resolve_wide):
+//   wide_prep_kernel    B = s_k - 2 eps from the query's fp32 top-k (its output row), counters zeroed;
+//   filter scan         every row with fp32 score >= B (the same scan kernel: the same fp32 scores),
+//                       up to kWideCap keys (desc fp32 key << 32 | row);
+//   wide_exact_kernel   the exact sum (fp64) of each collected row -> 64-bit exact order key;
+//   wide_select_kernel  the k smallest (exact key, row) pairs: an 8-bit MSD radix select on the exact
+//                       key for rank k, a second one on the rows tied at that key, then each selected
+//                       entry's rank by counting -- written in (exact score desc, id asc) order.
+// The exact top-k lies inside {fp32 >= B} (see the bound above), so the result is the fp64 evaluator's
+// for every query whose collected set fits kWideCap; a larger set keeps bit 1 (fp32 order).
+// ---------------------------------------------------------------------------
+constexpr int64_t kWideCap = 65536;
+constexpr int kWideThreads = 1024;
+constexpr int kWideSlice = 256;   // collected rows per work-group of wide_exact_kernel
+
+struct WideArgs {
+  RefineArgs ra;          // Q (the chunk's queries), d, stats: refine_eps
+  const int32_t* qmap;    // chunk query -> output row
+  int32_t nb;             // queries in the chunk
+  int32_t k;
+  float* tau;             // [kQueriesPerWG]
+  uint32_t* counts;       // [kQueriesPerWG * kCntStride]
+  const uint64_t* keys;   // [kQueriesPerWG][cap] filter hits
+  uint64_t* ekeys;        // [kQueriesPerWG][cap] exact order keys
+  int64_t cap;
+  int64_t id_offset;
+  float* out_s;           // [*, k] (rows through qmap)
+  int64_t* out_i;
+  int32_t* status;
+};
+
+__global__ __launch_bounds__(kRefThreads) void wide_prep_kernel(WideArgs w) {
+  __shared__ float fscr[kRefThreads / 64];
+  __shared__ int iscr[kRefThreads / 64];
+  __shared__ double dscr[kStatBlocks + 1];
+  const int j = blockIdx.x;
+  if (j >= w.nb) {   // padding queries of the 128-query scan block: inactive
+    if (threadIdx.x == 0) {
+      w.tau[j] = __builtin_nanf("");
+      w.counts[j * kCntStride] = 0u;
+    }
+    return;
+  }
+  const float eps = refine_eps(w.ra, j, fscr, iscr, dscr);
+  if (threadIdx.x == 0) {
+    const int64_t orow = w.qmap[j];
+    w.tau[j] = w.out_s[orow * w.k + w.k - 1] - 2.0f * eps;
+    w.counts[j * kCntStride] = 0u;
+  }
+}
+
+__global__ __launch_bounds__(kRefThreads) void wide_exact_kernel(WideArgs w) {
+  const int j = blockIdx.x;
+  const uint32_t c = w.counts[j * kCntStride];
+  const int64_t h0 = (int64_t)blockIdx.y * kWideSlice;
+  if (c > (uint64_t)w.cap || h0 >= (int64_t)c) return;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int d = w.ra.d;
+  constexpr int kMaxT = 4;   // d <= 1024
+  const int nch = d >> 2;
+  double qv[kMaxT][4];
+  const __bf16* qr = w.ra.Q + (int64_t)j * d;
+#pragma unroll
+  for (int t = 0; t < kMaxT; ++t) {
+    const int cc = lane + 64 * t;
+    const bf16x4 x = cc < nch ? *(const bf16x4*)(qr + 4 * cc) : bf16x4{};
+#pragma unroll
+    for (int u = 0; u < 4; ++u) qv[t][u] = (double)(float)x[u];
+  }
+  const uint64_t* kj = w.keys + (int64_t)j * w.cap;
+  uint64_t* ej = w.ekeys + (int64_t)j * w.cap;
+  const int64_t h1 = std::min<int64_t>((int64_t)c, h0 + kWideSlice);
+  for (int64_t hb = h0 + wave * kRefUnroll; hb < h1; hb += 4 * kRefUnroll) {
+    bool ok[kRefUnroll];
+    int64_t row[kRefUnroll];
+#pragma unroll
+    for (int u = 0; u < kRefUnroll; ++u) {
+      ok[u] = hb + u < h1;   // wave-uniform
+      row[u] = ok[u] ? (int64_t)(uint32_t)kj[hb + u] : 0;
+    }
+    bf16x4 x[kRefUnroll][kMaxT];
+#pragma unroll
+    for (int u = 0; u < kRefUnroll; ++u) {
+      const __bf16* pr = w.ra.P + row[u] * (int64_t)d;
+#pragma unroll
+      for (int t = 0; t < kMaxT; ++t) {
+        const int cc = lane + 64 * t;
+        x[u][t] = (ok[u] && cc < nch) ? *(const bf16x4*)(pr + 4 * cc) : bf16x4{};
+      }
+    }
+    double acc[kRefUnroll];
+#pragma unroll
+    for (int u = 0; u < kRefUnroll; ++u) {
+      acc[u] = 0.0;
+#pragma unroll
+      for (int t = 0; t < kMaxT; ++t)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) acc[u] = __builtin_fma(qv[t][e], (double)(float)x[u][t][e], acc[u]);
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1)
+#pragma unroll
+      for (int u = 0; u < kRefUnroll; ++u) acc[u] += __shfl_xor(acc[u], o, 64);
+    if (lane == 0) {
+#pragma unroll
+      for (int u = 0; u < kRefUnroll; ++u)
+        if (ok[u]) ej[hb + u] = desc_key64(acc[u]);
+    }
+  }
+}
+
+// 8-bit MSD radix select over the entries of `src` that match (prefix, mask) on `key`: the value whose
+// ascending rank is `want` (1-based); `want` becomes that value's rank among the entries equal to it.
+template <typename KeyFn>
+__device__ __forceinline__ uint64_t wide_radix_select(int64_t n, int bits, KeyFn key_of, uint32_t* hist, uint64_t* sh,
+                                                      int64_t& want) {
+  uint64_t prefix = 0, mask = 0;
+  for (int shift = bits - 8; shift >= 0; shift -= 8) {
+    for (int b = threadIdx.x; b < 256; b += blockDim.x) hist[b] = 0u;
+    __syncthreads();
+    for (int64_t h = threadIdx.x; h < n; h += blockDim.x) {
+      bool take;
+      const uint64_t v = key_of(h, take);
+      if (take && (v & mask) == prefix) atomicAdd(&hist[(v >> shift) & 255u], 1u);
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      int64_t cum = 0;
+      int dg = 255;
+      for (int b = 0; b < 256; ++b) {
+        if (cum + (int64_t)hist[b] >= want) {
+          dg = b;
+          break;
+        }
+        cum += hist[b];
+      }
+      sh[0] = prefix | ((uint64_t)dg << shift);
+      sh[1] = (uint64_t)(want - cum);
+    }
+    __syncthreads();
+    prefix = sh[0];
+    want = (int64_t)sh[1];
+    mask |= (uint64_t)0xFF << shift;
+    __syncthreads();
+  }
+  return prefix;
+}
+
+__global__ __launch_bounds__(kWideThreads) void wide_select_kernel(WideArgs w) {
+  __shared__ uint32_t hist[256];
+  __shared__ uint64_t sh[2];
+  __shared__ uint64_t sek[kSelMaxK];
+  __shared__ uint32_t srow[kSelMaxK];
+  __shared__ int ns;
+  const int j = blockIdx.x;
+  if (j >= w.nb) return;
+  const uint32_t c = w.counts[j * kCntStride];
+  if (c > (uint64_t)w.cap) return;   // more rows within 2 eps of the k-th than the cap: bit 1 stays
+  const int64_t nh = c;
+  const uint64_t* kj = w.keys + (int64_t)j * w.cap;
+  const uint64_t* ej = w.ekeys + (int64_t)j * w.cap;
+  const int64_t keff = std::min<int64_t>(w.k, nh);
+  const int64_t orow = w.qmap[j];
+  float* os = w.out_s + orow * w.k;
+  int64_t* oi = w.out_i + orow * w.k;
+  uint64_t kstar = ~0ull;
+  uint64_t rstar = ~0ull;
+  if (keff > 0) {
+    int64_t want = keff;
+    kstar = wide_radix_select(nh, 64, [&](int64_t h, bool& take) { take = true; return ej[h]; }, hist, sh, want);
+    // rows tied at the k-th exact key: the `want` smallest
+    const uint64_t ks = kstar;
+    rstar = wide_radix_select(nh, 32, [&](int64_t h, bool& take) {
+      take = ej[h] == ks;
+      return (uint64_t)(uint32_t)kj[h];
+    }, hist, sh, want);
+  }
+  if (threadIdx.x == 0) ns = 0;
+  __syncthreads();
+  for (int64_t h = threadIdx.x; h < nh && keff > 0; h += kWideThreads) {
+    const uint64_t ek = ej[h];
+    const uint64_t row = (uint32_t)kj[h];
+    if (ek < kstar || (ek == kstar && row <= rstar)) {
+      const int pos = atomicAdd(&ns, 1);
+      if (pos < kSelMaxK) {
+        sek[pos] = ek;
+        srow[pos] = (uint32_t)row;
+      }
+    }
+  }
+  __syncthreads();
+  const int m = ns < kSelMaxK ? ns : kSelMaxK;
+  for (int i = threadIdx.x; i < m; i += kWideThreads) {
+    const uint64_t ki = sek[i];
+    const uint32_t ri = srow[i];
+    int rank = 0;
+    for (int t = 0; t < m; ++t) rank += (sek[t] < ki || (sek[t] == ki && srow[t] < ri)) ? 1 : 0;
+    if (rank < w.k) {
+      const uint64_t ord = ~ki;
+      const uint64_t u = (ord >> 63) ? (ord & 0x7FFFFFFFFFFFFFFFull) : ~ord;
+      os[rank] = (float)__builtin_bit_cast(double, u);
+      oi[rank] = (int64_t)ri + w.id_offset;
+    }
+  }
+  for (int i = m + threadIdx.x; i < w.k; i += kWideThreads) {
+    os[i] = kPadScore;
+    oi[i] = -1;
+  }
+  if (threadIdx.x == 0 && m == keff) w.status[orow] &= ~2;
+}
+
+// Row statistics for the refine bound (layout above kStatsLen).  One wave per row: lane L holds the
+// 4-element chunks c = L + 64 i, whose squares a wave-wide inclusive scan turns into running prefix
+// sums; the lane whose chunk ends k-step t (c = 8 t + 7, or the last chunk) keeps the max over its rows
+// of the prefix through step t.  Non-negative floats are combined across work-groups by an integer max
+// of their bits; the integer flag by AND of the bits of 1.0f / 0.0f.
 __global__ __launch_bounds__(256) void row_stats_kernel(const __bf16* P, int64_t n, int32_t d, uint32_t* stats) {
-  __shared__ float fm[4];
+  constexpr int kIt = 4;   // chunks per lane: d <= 1024
+  __shared__ float fm[4][kStatBlocks];
   __shared__ int fi[4];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int64_t gw = (int64_t)blockIdx.x * 4 + wave, nw = (int64_t)gridDim.x * 4;
   const int nch = d >> 2;
-  float mx = 0.0f;
+  float pm[kIt];
+#pragma unroll
+  for (int i = 0; i < kIt; ++i) pm[i] = 0.0f;
   int nonint = 0;
   for (int64_t r = gw; r < n; r += nw) {
     const __bf16* pr = P + r * (int64_t)d;
-    float ss = 0.0f;
-    for (int c = lane; c < nch; c += 64) {
-      const bf16x4 x = *(const bf16x4*)(pr + 4 * c);
+    float carry = 0.0f;
 #pragma unroll
-      for (int u = 0; u < 4; ++u) {
-        const float v = (float)x[u];
-        ss += v * v;
-        nonint |= (v != __builtin_rintf(v)) ? 1 : 0;
+    for (int it = 0; it < kIt; ++it) {
+      if (64 * it >= nch) break;   // wave-uniform
+      const int c = lane + 64 * it;
+      float ss = 0.0f;
+      if (c < nch) {
+        const bf16x4 x = *(const bf16x4*)(pr + 4 * c);
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          const float v = (float)x[u];
+          ss += v * v;
+          nonint |= (v != __builtin_rintf(v)) ? 1 : 0;
+        }
       }
-    }
 #pragma unroll
-    for (int o = 32; o > 0; o >>= 1) ss += __shfl_xor(ss, o, 64);
-    mx = fmaxf(mx, ss);
+      for (int o = 1; o < 64; o <<= 1) {
+        const float t = __shfl_up(ss, o, 64);
+        if (lane >= o) ss += t;
+      }
+      const float v = carry + ss;
+      pm[it] = fmaxf(pm[it], v);
+      carry = __shfl(v, 63, 64);
+    }
   }
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) nonint |= __shfl_xor(nonint, o, 64);
-  if (lane == 0) {
-    fm[wave] = mx;
-    fi[wave] = nonint;
+  const int nb = (d + 31) >> 5;
+  for (int b = lane; b < kStatBlocks; b += 64) fm[wave][b] = 0.0f;
+  if (lane == 0) fi[wave] = nonint;
+  __syncthreads();
+#pragma unroll
+  for (int it = 0; it < kIt; ++it) {
+    const int c = lane + 64 * it;
+    if (c < nch && ((c & 7) == 7 || c == nch - 1)) fm[wave][c >> 3] = pm[it];
   }
   __syncthreads();
-  if (threadIdx.x == 0) {
-    float m = 0.0f;
-    int ni = 0;
-    for (int w = 0; w < 4; ++w) {
-      m = fmaxf(m, fm[w]);
-      ni |= fi[w];
-    }
-    atomicMax(stats, __builtin_bit_cast(uint32_t, m));
-    if (ni) atomicAnd(stats + 1, 0u);
+  if ((int)threadIdx.x < nb) {
+    const int b = threadIdx.x;
+    const float m = fmaxf(fmaxf(fm[0][b], fm[1][b]), fmaxf(fm[2][b], fm[3][b]));
+    atomicMax(stats + 2 + b, __builtin_bit_cast(uint32_t, m));
+    if (b == nb - 1) atomicMax(stats, __builtin_bit_cast(uint32_t, m));
   }
+  if (threadIdx.x == 0 && (fi[0] | fi[1] | fi[2] | fi[3])) atomicAnd(stats + 1, 0u);
 }
 
 __global__ void row_stats_init_kernel(uint32_t* stats) {
-  stats[0] = 0u;
-  stats[1] = __builtin_bit_cast(uint32_t, 1.0f);
+  if (threadIdx.x < kStatsLen) stats[threadIdx.x] = threadIdx.x == 1 ? __builtin_bit_cast(uint32_t, 1.0f) : 0u;
 }
 
 // ---------------------------------------------------------------------------
@@ -2472,8 +2745,9 @@ struct TopkPlan {
 static size_t align_up(size_t x, size_t a) { return (x + a - 1) / a * a; }
 
 // Candidates the canonical-order stage selects per query: k plus a window for the entries within
-// 2 eps of the k-th score (a few dozen on real-valued data; up to 2048 in all).
-static int64_t refine_width(int64_t k) { return std::min<int64_t>(kSelMaxK, k + std::max<int64_t>(256, k / 4)); }
+// 2 eps of the k-th score (a few on Gaussian data, ~120 on the C2 leg's untrained-tower embeddings at
+// k = 1000; up to 2048 in all).  A wider window goes to the wide resolve.
+static int64_t refine_width(int64_t k) { return std::min<int64_t>(kSelMaxK, k + std::max<int64_t>(512, k / 2)); }
 
 static size_t plan_refine_tail(TopkPlan& p, size_t o) {
   p.kc = refine_width(p.k);
@@ -2896,7 +3170,8 @@ int drt_ip_topk_exact_bf16(const void* Q, int64_t nq, const void* P, int64_t n, 
 int drt_row_stats_bf16(const void* P, int64_t n, int32_t d, float* stats, int32_t accumulate, void* stream) {
   DRT_REQUIRE(n >= 0 && d > 0 && d % 4 == 0 && stats != nullptr);
   hipStream_t s = (hipStream_t)stream;
-  if (!accumulate) hipLaunchKernelGGL(row_stats_init_kernel, dim3(1), dim3(1), 0, s, (uint32_t*)stats);
+  DRT_REQUIRE(d <= 32 * kStatBlocks);
+  if (!accumulate) hipLaunchKernelGGL(row_stats_init_kernel, dim3(1), dim3(64), 0, s, (uint32_t*)stats);
   if (n > 0) {
     DRT_REQUIRE(P != nullptr);
     const int64_t blocks = std::min<int64_t>((n + 3) / 4, 4096);
@@ -3099,6 +3374,94 @@ static int resolve_impl(const void* Q, int64_t nq, const void* P, int64_t n, int
 }  // namespace drt
 
 extern "C" {
+
+static size_t wide_ws_bytes(int32_t d) {
+  const int64_t B = kQueriesPerWG;
+  return (size_t)(align_up(B * (int64_t)d * 2, 256) + align_up(B * 4, 256) + align_up(B * 4, 256) +
+                  align_up(B * kCntStride * 4, 256) + 2 * align_up(B * kWideCap * 8, 256));
+}
+
+size_t drt_ip_topk_resolve_wide_workspace(int64_t n, int32_t d) {
+  if (n < 0 || d <= 0 || d % 64 || d > 1024) return 0;
+  return wide_ws_bytes(d);
+}
+
+int drt_ip_topk_resolve_wide(const void* Q, int64_t nq, const void* P, int64_t n, int32_t d, int32_t k,
+                             int64_t id_offset, const float* stats, float* out_scores, int64_t* out_ids,
+                             int32_t* status, void* ws, size_t ws_bytes, int64_t* n_resolved, void* stream) {
+  DRT_REQUIRE(valid_dims(nq, n, d, k));
+  if (n_resolved) *n_resolved = 0;
+  if (nq == 0 || n == 0) return DRT_OK;
+  DRT_REQUIRE(Q && P && stats && out_scores && out_ids && status && ws && ws_bytes >= wide_ws_bytes(d));
+  hipStream_t s = (hipStream_t)stream;
+  std::vector<int32_t> st(nq);
+  DRT_CHECK_HIP(hipMemcpyAsync(st.data(), status, nq * 4, hipMemcpyDeviceToHost, s));
+  DRT_CHECK_HIP(hipStreamSynchronize(s));
+  std::vector<int32_t> wide;   // order not certified and the fp32 top-k itself certified
+  for (int64_t i = 0; i < nq; ++i)
+    if ((st[i] & 3) == 2) wide.push_back((int32_t)i);
+  if (wide.empty()) return DRT_OK;
+  const int64_t B = kQueriesPerWG;
+  char* wp = (char*)ws;
+  char* qbuf = wp;
+  int32_t* qmap = (int32_t*)(qbuf + align_up(B * (int64_t)d * 2, 256));
+  float* tau = (float*)((char*)qmap + align_up(B * 4, 256));
+  uint32_t* counts = (uint32_t*)((char*)tau + align_up(B * 4, 256));
+  uint64_t* keys = (uint64_t*)((char*)counts + align_up(B * kCntStride * 4, 256));
+  uint64_t* ekeys = (uint64_t*)((char*)keys + align_up(B * kWideCap * 8, 256));
+  for (size_t b0 = 0; b0 < wide.size(); b0 += B) {
+    const int nb = (int)std::min<int64_t>(B, (int64_t)wide.size() - (int64_t)b0);
+    for (int i = 0; i < nb; ++i)
+      DRT_CHECK_HIP(hipMemcpyAsync(qbuf + (int64_t)i * d * 2, (const char*)Q + (int64_t)wide[b0 + i] * d * 2, d * 2,
+                                   hipMemcpyDeviceToDevice, s));
+    DRT_CHECK_HIP(hipMemcpyAsync(qmap, wide.data() + b0, nb * 4, hipMemcpyHostToDevice, s));
+    WideArgs w{};
+    w.ra.Q = (const __bf16*)qbuf;
+    w.ra.d = d;
+    w.ra.P = (const __bf16*)P;
+    w.ra.stats = stats;
+    w.qmap = qmap;
+    w.nb = nb;
+    w.k = k;
+    w.tau = tau;
+    w.counts = counts;
+    w.keys = keys;
+    w.ekeys = ekeys;
+    w.cap = kWideCap;
+    w.id_offset = id_offset;
+    w.out_s = out_scores;
+    w.out_i = out_ids;
+    w.status = status;
+    hipLaunchKernelGGL(wide_prep_kernel, dim3((unsigned)B), dim3(kRefThreads), 0, s, w);
+    DRT_CHECK_HIP(hipGetLastError());
+    ScanArgs a{};
+    a.Q = (const __bf16*)qbuf;
+    a.nq = nb;
+    a.ldq = d;
+    a.P = (const __bf16*)P;
+    a.ldp = d;
+    a.row0 = 0;
+    a.nrows = n;
+    a.rstride = 1;
+    a.tau = tau;
+    a.counts = counts;
+    a.out = keys;
+    a.cap = kWideCap;
+    const int rc = launch_scan(a, d, SCAN_FILTER, s, PROF_SCAN);
+    if (rc) return rc;
+    hipLaunchKernelGGL(wide_exact_kernel, dim3((unsigned)nb, (unsigned)(kWideCap / kWideSlice)), dim3(kRefThreads), 0,
+                       s, w);
+    hipLaunchKernelGGL(wide_select_kernel, dim3((unsigned)nb), dim3(kWideThreads), 0, s, w);
+    DRT_CHECK_HIP(hipGetLastError());
+  }
+  std::vector<int32_t> st2(nq);
+  DRT_CHECK_HIP(hipMemcpyAsync(st2.data(), status, nq * 4, hipMemcpyDeviceToHost, s));
+  DRT_CHECK_HIP(hipStreamSynchronize(s));
+  int64_t nres = 0;
+  for (int32_t i : wide) nres += (st2[i] & 2) == 0 ? 1 : 0;
+  if (n_resolved) *n_resolved = nres;
+  return DRT_OK;
+}
 
 int drt_ip_topk_resolve(const void* Q, int64_t nq, const void* P, int64_t n, int32_t d, int32_t k,
                         int64_t id_offset, float* out_scores, int64_t* out_ids, int32_t* status,

@@ -72,12 +72,13 @@ static void check_topk_outputs(const Tensor& q, int64_t nq, int64_t k, const Ten
                     "status: expected a contiguous int32 [", nq, "] tensor, got ", status.sizes());
 }
 
-// row statistics of the canonical-order stage: a [2] float tensor on p's device (drt_row_stats_bf16)
+// row statistics of the canonical-order stage: a [DRT_ROW_STATS_LEN] float tensor on p's device
+// (drt_row_stats_bf16)
 static const float* stats_ptr(const c10::optional<Tensor>& stats, const Tensor& q) {
   if (!stats.has_value()) return nullptr;
-  TORCH_CHECK_VALUE(stats->device() == q.device() && stats->scalar_type() == at::kFloat && stats->numel() == 2 &&
-                        stats->is_contiguous(),
-                    "stats: expected a contiguous float [2] tensor on ", q.device());
+  TORCH_CHECK_VALUE(stats->device() == q.device() && stats->scalar_type() == at::kFloat &&
+                        stats->numel() == DRT_ROW_STATS_LEN && stats->is_contiguous(),
+                    "stats: expected a contiguous float [", DRT_ROW_STATS_LEN, "] tensor on ", q.device());
   return stats->data_ptr<float>();
 }
 
@@ -152,6 +153,33 @@ int64_t ip_topk_resolve(const Tensor& q_, const Tensor& p_, int64_t k, int64_t i
   return nres;
 }
 
+// canonical order of the queries whose status is exactly 2 (drt_ip_topk_resolve_wide): a filter pass at
+// the lowered threshold, exact sums of what it collects, exact-key top-k in place; returns the number of
+// queries whose bit 1 it cleared (synchronises, like the C entry)
+int64_t ip_topk_resolve_wide(const Tensor& q_, const Tensor& p_, int64_t k, int64_t id_offset, Tensor& scores,
+                             Tensor& ids, Tensor& status, const Tensor& stats) {
+  need(q_, "q", at::kBFloat16, 2);
+  need(p_, "p", at::kBFloat16, 2);
+  const c10::DeviceGuard g(q_.device());
+  const Tensor q = q_.contiguous(), p = p_.contiguous();
+  TORCH_CHECK_VALUE(q.size(1) == p.size(1), "q and p differ in dimension: ", q.sizes(), " vs ", p.sizes());
+  TORCH_CHECK_VALUE(p.device() == q.device(), "q and p must be on the same device");
+  const int64_t nq = q.size(0), n = p.size(0), d = q.size(1);
+  TORCH_CHECK_VALUE(k >= 1 && k <= 2048, "unsupported k=", k);
+  check_topk_outputs(q, nq, k, scores, ids, status);
+  const float* sp = stats_ptr(stats, q);
+  if (nq == 0 || n == 0) return 0;
+  const size_t wsb = drt_ip_topk_resolve_wide_workspace(n, (int32_t)d);
+  TORCH_CHECK_VALUE(wsb > 0, "unsupported resolve_wide shape n=", n, " d=", d);
+  Tensor ws = workspace(q, wsb);
+  int64_t nres = 0;
+  check_rc(drt_ip_topk_resolve_wide(q.data_ptr(), nq, p.data_ptr(), n, (int32_t)d, (int32_t)k, id_offset, sp,
+                                    scores.data_ptr<float>(), ids.data_ptr<int64_t>(), status.data_ptr<int32_t>(),
+                                    ws.data_ptr(), wsb, &nres, stream_of(q)),
+           "drt_ip_topk_resolve_wide");
+  return nres;
+}
+
 // row statistics of p (+ those of earlier rows in `prev`, appended rows)
 Tensor row_stats(const Tensor& p_, const c10::optional<Tensor>& prev) {
   need(p_, "p", at::kBFloat16, 2);
@@ -162,7 +190,7 @@ Tensor row_stats(const Tensor& p_, const c10::optional<Tensor>& prev) {
     stats_ptr(prev, p);
     st = prev->clone();
   } else {
-    st = at::empty({2}, p.options().dtype(at::kFloat));
+    st = at::empty({DRT_ROW_STATS_LEN}, p.options().dtype(at::kFloat));
   }
   check_rc(drt_row_stats_bf16(p.size(0) ? p.data_ptr() : nullptr, p.size(0), (int32_t)p.size(1),
                               st.data_ptr<float>(), prev.has_value() ? 1 : 0, stream_of(p)),
@@ -526,6 +554,8 @@ TORCH_LIBRARY(drt, m) {
         "Tensor(b!) ids, Tensor(c!) status) -> ()");
   m.def("ip_topk_resolve(Tensor q, Tensor p, int k, int id_offset, Tensor(a!) scores, Tensor(b!) ids, "
         "Tensor(c!) status, Tensor? stats=None) -> int");
+  m.def("ip_topk_resolve_wide(Tensor q, Tensor p, int k, int id_offset, Tensor(a!) scores, Tensor(b!) ids, "
+        "Tensor(c!) status, Tensor stats) -> int");
   m.def("row_stats(Tensor p, Tensor? prev=None) -> Tensor");
   m.def("refine_delta(Tensor q, Tensor p, int row_offset, Tensor cand_scores, Tensor cand_ids, int k, Tensor stats, "
         "Tensor? tau, Tensor(a!) status) -> (Tensor, Tensor)");
@@ -555,6 +585,7 @@ TORCH_LIBRARY_IMPL(drt, CUDA, m) {   // the GPU dispatch key of torch-ROCm
   m.impl("ip_topk", &ip_topk);
   m.impl("ip_topk.out", &ip_topk_out);
   m.impl("ip_topk_resolve", &ip_topk_resolve);
+  m.impl("ip_topk_resolve_wide", &ip_topk_resolve_wide);
   m.impl("row_stats", &row_stats);
   m.impl("refine_delta", &refine_delta);
   m.impl("refine_sort", &refine_sort);

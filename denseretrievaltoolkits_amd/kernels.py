@@ -75,9 +75,23 @@ def resolve_failed(q, p, k, id_offset, scores, ids, status, n_failed: Optional[i
     return int(ops.load().ip_topk_resolve(q, p, k, id_offset, scores, ids, status, stats))
 
 
+def resolve_wide(q, p, k, id_offset, scores, ids, status, stats: torch.Tensor, n_wide: Optional[int] = None) -> int:
+    """Canonical order of every query whose status is exactly 2 (its near-tie window did not fit the
+    candidate list): a filter pass at the lowered threshold s_k - 2 eps collects every row that can
+    belong to the exact top-k (up to 65536 per query), their exact sums are ranked and the top-k is
+    written in place; status bit 1 is cleared where that worked.  Synchronous.  Returns the number of
+    queries resolved.  ``n_wide``: the caller's count of such queries (0 returns at once)."""
+    if n_wide == 0 or q.shape[0] == 0:
+        return 0
+    _require_device(q, p, stats)
+    return int(ops.load().ip_topk_resolve_wide(q, p, k, id_offset, scores, ids, status, stats))
+
+
 def row_stats(p: torch.Tensor, prev: Optional[torch.Tensor] = None) -> torch.Tensor:
-    """[2] fp32 device tensor: (max squared row norm, 1.0 if every element is an integer) of the
-    bf16 rows p [n, d], combined with ``prev`` (the stats of earlier rows) when given."""
+    """[ROW_STATS_LEN] fp32 device tensor: (max squared row norm, 1.0 if every element is an integer,
+    then per 32-element k-step t the max squared norm of the row prefixes [0, 32 (t + 1))) of the bf16
+    rows p [n, d] -- the error bound of the scan's MFMA chain (csrc/search.hip) -- combined with
+    ``prev`` (the stats of earlier rows) when given."""
     _require_device(p)
     return ops.load().row_stats(p, prev)
 

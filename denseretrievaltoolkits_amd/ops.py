@@ -23,6 +23,7 @@ import threading
 import torch
 
 from . import _native
+from ._native import ROW_STATS_LEN
 from .build_native import OPS_LIB_PATH
 
 _lock = threading.Lock()
@@ -65,9 +66,13 @@ def _register_python_parts():
         # the count of rescanned queries is data-dependent (it reads the status back)
         return torch.library.get_ctx().new_dynamic_size()
 
+    @lib.register_fake("drt::ip_topk_resolve_wide")
+    def _(q, p, k, id_offset, scores, ids, status, stats):
+        return torch.library.get_ctx().new_dynamic_size()
+
     @lib.register_fake("drt::row_stats")
     def _(p, prev=None):
-        return p.new_empty((2,), dtype=torch.float32)
+        return p.new_empty((ROW_STATS_LEN,), dtype=torch.float32)
 
     @lib.register_fake("drt::refine_delta")
     def _(q, p, row_offset, cand_scores, cand_ids, k, stats, tau, status):

@@ -22,7 +22,7 @@ from typing import Optional, Tuple
 import numpy as np
 import torch
 
-from . import comm, kernels, shards
+from . import _native, comm, kernels, shards
 
 
 def _as_device_bf16(x, device) -> torch.Tensor:
@@ -135,7 +135,7 @@ def _groups(batches, cap=None):
 
 
 def _gtau_enqueue_group(local, qs, k: int, n_global: int, offset: int, gather, to_host: bool = False,
-                        stats=None, all_reduce_sum=None):
+                        stats=None, all_reduce_sum=None, id_shift: int = 0):
     """One group of query batches through the global-threshold protocol (see ShardedFlatIP):
     ONE sample launch for all of the group's queries, one exchange of the sample lists, one
     threshold launch, one filter scan (+ select) per batch writing its packed top-k into a group buffer,
@@ -143,7 +143,9 @@ def _gtau_enqueue_group(local, qs, k: int, n_global: int, offset: int, gather, t
     [world, *t.shape] (identity stack on one GPU).  ``to_host``: the merged group's results are
     also staged to pinned host memory behind the merge.  ``stats`` (the GLOBAL row statistics):
     the shards keep kc = refine_width(k) candidates each, the merge keeps kc, and the canonical
-    stage (kernels.refine, deltas summed across shards by ``all_reduce_sum``) orders the top-k."""
+    stage (kernels.refine, deltas summed across shards by ``all_reduce_sum``) orders the top-k.
+    ``id_shift`` is added to every returned id (a one-GPU index searched with an id offset: the
+    protocol itself runs on the index's own row numbers, packed in 32 bits)."""
     sizes = [q.shape[0] for q in qs]
     qg = qs[0] if len(qs) == 1 else torch.cat(qs)
     best = local.dist_sample(qg, n_global, k)                       # [Qg, r]
@@ -157,34 +159,47 @@ def _gtau_enqueue_group(local, qs, k: int, n_global: int, offset: int, gather, t
     s, i, st = kernels.merge_packed(gather(packed), kc, n_global, k_cert=k)
     if stats is not None:
         s, i = kernels.refine(qg, local.rows, offset, s, i, k, stats, tau, st, all_reduce_sum)
+    if id_shift:
+        i = torch.where(i >= 0, i + id_shift, i)
     h, ev = _stage_status(st)
     host = _HostResult(s, i) if to_host else None
-    return qs, sizes, s, i, h, ev, host
+    return qs, sizes, s, i, st, h, ev, host
 
 
-def _gtau_finish_group(pend, redo):
+def _gtau_finish_group(pend, redo, wide=None):
     """Per-batch results of a group; a batch with an uncertified query is redone by ``redo(q)``
     (the exact path).  Every rank merged the same gathered lists, so all ranks redo the same
-    batches (their collectives stay matched).  With staged host copies the results are numpy."""
-    qs, sizes, s, i, h, ev, host = pend
+    batches (their collectives stay matched).  ``wide(q, s, i, st)`` (one GPU): the wide resolve of
+    a batch's queries whose canonical order the candidate list could not certify (status 2), in
+    place; returns how many it resolved.  With staged host copies the results are numpy.
+    Returns (results, batches redone, queries left in the fp32 order)."""
+    qs, sizes, s, i, st, h, ev, host = pend
     if ev is not None:
         ev.synchronize()
     bad = (h & 1) != 0
-    res, o, nredo = [], 0, 0
+    wid = (h & 3) == 2
+    res, o, nredo, nunc = [], 0, 0, 0
     hs = hi = None
     for q, nb in zip(qs, sizes):
-        if bool(bad[o:o + nb].any()):
+        nw = int(wid[o:o + nb].sum()) if not bool(bad[o:o + nb].any()) else 0
+        if nw and wide is not None:
+            nunc += nw - wide(q, s[o:o + nb], i[o:o + nb], st[o:o + nb])
+            res.append((s[o:o + nb].cpu().numpy(), i[o:o + nb].cpu().numpy()) if host is not None
+                       else (s[o:o + nb], i[o:o + nb]))
+        elif bool(bad[o:o + nb].any()):
             rs, ri = redo(q)
             res.append((rs.cpu().numpy(), ri.cpu().numpy()) if host is not None else (rs, ri))
             nredo += 1
         elif host is not None:
+            nunc += nw
             if hs is None:
                 hs, hi = host.get(s, i, False)
             res.append((hs[o:o + nb], hi[o:o + nb]))
         else:
+            nunc += nw
             res.append((s[o:o + nb], i[o:o + nb]))
         o += nb
-    return res, nredo, _order_uncertified(h)
+    return res, nredo, nunc
 
 
 class _GroupPend:
@@ -231,6 +246,8 @@ class FlatIPIndex:
 
     def reset(self):
         self.ntotal = 0
+        self._stats = None   # refilled rows must be rescanned (a stale max-norm / integer flag would
+        self._stats_n = 0    # make the canonical stage's error bound wrong)
 
     def reserve(self, n: int):
         if n > self._buf.shape[0]:
@@ -294,12 +311,25 @@ class FlatIPIndex:
     def _finish(self, pend):
         qd, s, i, st, h, ev, off, k, host, stats = pend
         nbad = _status_failed(h, ev)
-        self.order_uncertified += _order_uncertified(h)
         if nbad:
             self.resolved += kernels.resolve_failed(qd, self.rows, k, off, s, i, st, n_failed=nbad, stats=stats)
+            h = st.cpu()   # the rescan set each redone query's status anew
+        nwide = int(((h & 3) == 2).sum().item()) if stats is not None else 0
+        nres = self._wide(qd, k, off, s, i, st, stats, nwide)
+        self.order_uncertified += _order_uncertified(h) - nres
         if host is not None:
-            return host.get(s, i, nbad > 0)
+            return host.get(s, i, nbad > 0 or nres > 0)
         return s, i
+
+    wide_resolved = 0   # queries put in the canonical order by the wide resolve (massive near-ties)
+
+    def _wide(self, qd, k, off, s, i, st, stats, nwide=None) -> int:
+        """Wide resolve (kernels.resolve_wide) of the queries with status 2; returns how many it resolved."""
+        if stats is None or nwide == 0:
+            return 0
+        n = kernels.resolve_wide(qd, self.rows, k, off, s, i, st, stats, n_wide=nwide)
+        self.wide_resolved += n
+        return n
 
     def search_unresolved(self, q, k: int, id_offset: int = 0):
         """(scores, ids, status) with status still on device (the per-shard protocol gathers it);
@@ -322,6 +352,7 @@ class FlatIPIndex:
         return list(self.search_batches_iter(batches, k, id_offset, outs))
 
     def _use_groups(self) -> bool:
+        # the grouped path packs row numbers into 32 bits (an id offset is added afterwards)
         return GROUP_MIN_ROWS <= self.ntotal <= GROUP_MAX_ROWS and self.ntotal < 0xFFFFFFFF
 
     def enqueue_batches(self, batches, k: int, id_offset: int = 0, to_host: bool = False) -> list:
@@ -332,8 +363,9 @@ class FlatIPIndex:
         out = []
         stats = self._stats_arg()
         for g in _groups(list(batches)):
-            gp = _GroupPend(_gtau_enqueue_group(self, [self._queries(q) for q in g], k, self.ntotal, id_offset,
-                                                lambda t: t.unsqueeze(0), to_host, stats=stats), k, id_offset)
+            gp = _GroupPend(_gtau_enqueue_group(self, [self._queries(q) for q in g], k, self.ntotal, 0,
+                                                lambda t: t.unsqueeze(0), to_host, stats=stats, id_shift=id_offset),
+                            k, id_offset)
             out += [_GroupMember(gp, j) for j in range(len(g))]
         return out
 
@@ -342,7 +374,10 @@ class FlatIPIndex:
         if isinstance(pend, _GroupMember):
             gp = pend.group
             if gp.res is None:   # the group's certificates are checked once, by its first member
-                res, nredo, nunc = _gtau_finish_group(gp.pend, lambda q: self.search_device(q, gp.k, gp.id_offset))
+                stats = self._stats_arg()
+                res, nredo, nunc = _gtau_finish_group(
+                    gp.pend, lambda q: self.search_device(q, gp.k, gp.id_offset),
+                    lambda q, s, i, st: self._wide(q, gp.k, gp.id_offset, s, i, st, stats))
                 self.group_fallbacks += nredo
                 self.order_uncertified += nunc
                 gp.res = res
@@ -365,15 +400,16 @@ class FlatIPIndex:
         groups = [[self._queries(q) for q in g] for g in _groups(batches)]
 
         def fin(pend):
-            res, nredo, nunc = _gtau_finish_group(pend, lambda q: self.search_device(q, k, id_offset))
+            res, nredo, nunc = _gtau_finish_group(pend, lambda q: self.search_device(q, k, id_offset),
+                                                  lambda q, s, i, st: self._wide(q, k, id_offset, s, i, st, stats))
             self.group_fallbacks += nredo
             self.order_uncertified += nunc
             return res
 
         stats = self._stats_arg()
-        for res in _pipeline(groups, lambda j, g: _gtau_enqueue_group(self, g, k, self.ntotal, id_offset,
+        for res in _pipeline(groups, lambda j, g: _gtau_enqueue_group(self, g, k, self.ntotal, 0,
                                                                       lambda t: t.unsqueeze(0), to_host,
-                                                                      stats=stats), fin):
+                                                                      stats=stats, id_shift=id_offset), fin):
             yield from res
 
     def search(self, q, k: int) -> Tuple[np.ndarray, np.ndarray]:
@@ -476,8 +512,11 @@ class ShardedFlatIP:
         self.ntotal = sum(counts)
         self.stats = None
         if isinstance(self.local, FlatIPIndex) and self.local.exact_order:
-            st = self.local.row_stats() if self.local.ntotal > 0 else \
-                torch.tensor([0.0, 1.0], dtype=torch.float32, device=self.local.device)
+            if self.local.ntotal > 0:
+                st = self.local.row_stats()
+            else:   # an empty shard: the neutral element of the combination below
+                st = torch.zeros(_native.ROW_STATS_LEN, dtype=torch.float32, device=self.local.device)
+                st[1] = 1.0
             if self._multi():
                 # max of the squared norms, AND of the integer flags (as a max of their negations)
                 st = st.clone()
@@ -545,7 +584,7 @@ class ShardedFlatIP:
             if isinstance(self.local, FlatIPIndex):
                 # the HIP shard: one batch as a group of one (canonical order included)
                 qd = self.local._queries(q)
-                _, _, s, i, h, ev, _ = _gtau_enqueue_group(
+                _, _, s, i, _, h, ev, _ = _gtau_enqueue_group(
                     self.local, [qd], k, self.ntotal, self.offset, self._all_gather, stats=self.stats,
                     all_reduce_sum=lambda t: comm.all_reduce_sum_(t, self.group))
                 return ("gtau", qd, k, s, i, h, ev)

@@ -104,7 +104,13 @@ class Trainer:
             # the LR schedulers are off the hot path (scalar lr arithmetic): the user's own
             # DRT.trainer.scheduler classes wrap the optimizer, as the reference does (trainer.py:85-112)
             import importlib
-            us = importlib.import_module("DRT.trainer.scheduler")
+            try:
+                us = importlib.import_module("DRT.trainer.scheduler")
+            except ImportError as e:
+                raise ImportError(
+                    f"scheduler={sname!r} uses the reference's own LR schedulers (DRT.trainer.scheduler), which "
+                    "are not part of this package: put the DRT checkout on PYTHONPATH (INTEGRATION.md) or pass "
+                    "scheduler=None") from e
             sched = {"inverse": us.InverseSquareRootScheduler, "cosine": us.CosineScheduler,
                      "linear": us.LinearScheduler, "constant": us.ConstantScheduler}
             skw = dict(getattr(a, "scheduler_kwargs", {}) or {})

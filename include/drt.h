@@ -41,6 +41,7 @@ extern "C" {
 
 #define DRT_OK 0
 #define DRT_EINVAL (-1)
+#define DRT_ROW_STATS_LEN 34   /* floats of drt_row_stats_bf16's statistics (2 + 32 k-steps) */
 
 /* Library version / self-description (host only, no GPU needed). */
 const char* drt_version(void);
@@ -81,15 +82,23 @@ int drt_ip_topk_resolve(const void* Q, int64_t nq, const void* P, int64_t n, int
  * order.  These entry points put a result in the order of the EXACT products (fp64 sums of the
  * bf16 products, ties by ascending id), as an fp64 CPU evaluator (faiss's semantics without its
  * rounding) ranks them, with scores = the exact sums rounded to fp32.
- * drt_row_stats_bf16: stats[2] (device floats) = (max squared L2 norm over the rows, 1.0f while
- *   every element is an integer); accumulate = 0 (re)initialises, 1 combines with the stats
- *   already there (appended rows).  Across shards combine by max / min.  Reads every row once.
+ * drt_row_stats_bf16: stats[DRT_ROW_STATS_LEN] (device floats) = (max squared L2 norm over the rows,
+ *   1.0f while every element is an integer, then for each 32-element k-step t < ceil(d / 32) the max
+ *   over the rows of the squared norm of the prefix [0, 32 (t + 1))) -- the error bound of the scan's
+ *   MFMA chain (csrc/search.hip, "Error bound"); accumulate = 0 (re)initialises, 1 combines with the
+ *   stats already there (appended rows).  Across shards combine by max (the flag by min).  Reads
+ *   every row once.  d <= 1024.
  * drt_ip_topk_exact_bf16: drt_ip_topk_bf16 in the canonical order (same workspace).  status bit 0
  *   as drt_ip_topk_bf16 (call drt_ip_topk_resolve_exact); bit 1 = the exact order could not be
- *   certified and the query keeps the (exact) fp32 top-k in the fp32 order: more than
- *   drt_refine_width(k) - k rows within the fp32 error of the k-th score, or that window reaching
- *   below the filter threshold (massive near-ties, e.g. an untrained tower's embeddings).
+ *   certified from the candidate list and the query holds the (exact) fp32 top-k in the fp32 order:
+ *   more than drt_refine_width(k) - k rows within the fp32 error of the k-th score, or that window
+ *   reaching below the filter threshold (massive near-ties) -- call drt_ip_topk_resolve_wide.
  * drt_ip_topk_resolve_exact: drt_ip_topk_resolve in the canonical order (status bit 0 only).
+ * drt_ip_topk_resolve_wide: SYNCHRONOUS, for the queries whose status is exactly 2: a filter pass at
+ *   the lowered threshold s_k - 2 eps collects every row that may belong to the exact top-k (up to
+ *   65536 per query), their exact sums are computed and the top-k by (exact score desc, id asc) is
+ *   written in place; bit 1 is cleared for every such query whose collected set fit.  Workspace:
+ *   drt_ip_topk_resolve_wide_workspace(n, d) bytes (~134 MB, chunks of 128 queries).
  * drt_refine_delta_bf16 / drt_refine_sort: the stage alone, on a candidate list cand [nq][kc]
  *   (scores desc, global ids, kc = drt_refine_width(k), e.g. a merged sharded result): delta =
  *   exact - fp32 score for the candidates whose rows this shard holds (row_offset = global id of
@@ -105,6 +114,11 @@ int drt_ip_topk_resolve_exact(const void* Q, int64_t nq, const void* P, int64_t 
                               int64_t id_offset, const float* stats, float* out_scores, int64_t* out_ids,
                               int32_t* status, void* workspace, size_t workspace_bytes, int64_t* n_resolved,
                               void* stream);
+size_t drt_ip_topk_resolve_wide_workspace(int64_t n, int32_t d);
+int drt_ip_topk_resolve_wide(const void* Q, int64_t nq, const void* P, int64_t n, int32_t d, int32_t k,
+                             int64_t id_offset, const float* stats, float* out_scores, int64_t* out_ids,
+                             int32_t* status, void* workspace, size_t workspace_bytes, int64_t* n_resolved,
+                             void* stream);
 int drt_refine_delta_bf16(const void* Q, int64_t nq, int32_t d, const void* P, int64_t n_local,
                           int64_t row_offset, const float* cand_s, const int64_t* cand_i, int32_t kc,
                           int32_t k, const float* stats, const float* tau, float* delta, int32_t* cnt,

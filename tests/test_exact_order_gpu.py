@@ -34,20 +34,97 @@ def _assert_scores(gs, es):
     assert (gs == es).mean() > 0.999
 
 
+def _np_stats(p):
+    """oracle restatement of drt_row_stats_bf16: (max ||p||^2, integer flag, max prefix ||p_[0,32(t+1))||^2)."""
+    p64 = p.astype(np.float64)
+    nb = (p.shape[1] + 31) // 32
+    pref = np.stack([(p64[:, : 32 * (t + 1)] ** 2).sum(1).max() for t in range(nb)])
+    return (p64 ** 2).sum(1).max(), float((p == np.rint(p)).all()), pref
+
+
+def _np_eps(q, p):
+    """The scan's certified fp32 error bound per query (csrc/search.hip "Error bound", refine_eps):
+    10 u (1 + 1e-3) (sum_{t=1}^{T-1} ||q_[0,32t)|| max ||p_[0,32t)|| + ||q|| max ||p||)."""
+    _, _, pref = _np_stats(p)
+    q64 = q.astype(np.float64)
+    nb = len(pref)
+    acc = np.sqrt((q64 ** 2).sum(1) * pref[-1])
+    for t in range(1, nb):
+        acc += np.sqrt((q64[:, : 32 * t] ** 2).sum(1) * pref[t - 1])
+    return 10.0 * 2.0 ** -24 * 1.001 * acc
+
+
 def test_row_stats_vs_numpy(dev):
     import torch
-    from denseretrievaltoolkits_amd import kernels
+    from denseretrievaltoolkits_amd import _native, kernels
     rng = np.random.default_rng(1)
     p = gauss_bf16(rng, (10007, 320))
+    p[17, :40] *= 3.0   # a row whose PREFIX norm is the largest, not its total
+    p = orc.bf16_round(p)
     st = kernels.row_stats(to_dev_bf16(p, dev)).cpu().numpy()
-    sq = (p.astype(np.float64) ** 2).sum(1).max()
+    assert st.shape == (_native.ROW_STATS_LEN,)
+    sq, flag, pref = _np_stats(p)
     assert abs(st[0] - sq) <= 1e-4 * sq and st[1] == 0.0
+    np.testing.assert_allclose(st[2: 2 + len(pref)], pref, rtol=1e-4)
+    assert (st[2 + len(pref):] == 0).all()
     pi = int_bf16(rng, (5000, 320), -4, 4)
     st2 = kernels.row_stats(to_dev_bf16(pi, dev)).cpu().numpy()
     assert st2[1] == 1.0 and abs(st2[0] - (pi.astype(np.float64) ** 2).sum(1).max()) <= 1e-3
     # appended rows combine with the earlier statistics
     both = kernels.row_stats(to_dev_bf16(p[:100], dev), prev=torch.from_numpy(st2).to(dev)).cpu().numpy()
     assert both[1] == 0.0 and both[0] == max(st2[0], np.float32(both[0]))
+    np.testing.assert_allclose(both[2:12], np.maximum(st2[2:12], _np_stats(p[:100])[2]), rtol=1e-4)
+
+
+def _bound_cases(rng):
+    """(name, q, p): data that pushes the scan's fp32 error toward the bound."""
+    d = 768
+    yield "gauss", gauss_bf16(rng, (64, d)), gauss_bf16(rng, (30000, d))
+    # the C2 tower's regime: a large common component, every product positive
+    yield "common", orc.bf16_round(1.0 + 0.01 * rng.standard_normal((64, d))), \
+        orc.bf16_round(1.0 + 0.01 * rng.standard_normal((30000, d)))
+    # every k-step drops 31-32 products just under the MFMA's alignment cut (2^-26 below the
+    # accumulator): the truncation worst case, with Cauchy-Schwarz tight (q ~ p)
+    eps_v = orc.bf16_round(np.float32(2.0 ** -13 * 0.99))
+    big = orc.bf16_round(1.0 + rng.integers(0, 64, size=(30000, 1)) / 128.0)
+    p = np.full((30000, d), eps_v, np.float32)
+    p[:, :1] = big
+    q = np.full((16, d), eps_v, np.float32)
+    q[:, 0] = 1.0
+    yield "truncation", q, orc.bf16_round(p)
+    # exponents spread over 16 binades, mixed signs
+    yield "spread", orc.bf16_round(rng.standard_normal((64, d)) * np.exp2(rng.integers(-8, 9, size=(64, d)))), \
+        orc.bf16_round(rng.standard_normal((30000, d)) * np.exp2(rng.integers(-8, 9, size=(30000, d))))
+
+
+def test_scan_fp32_error_within_certified_bound(dev):
+    """The canonical stage is only as good as its bound: the filter scan's fp32 score of every returned
+    row lies within eps (refine_eps) of its exact (fp64) inner product, on data built to approach the
+    bound (truncated alignment inside each MFMA step, C-S-tight partial sums)."""
+    from denseretrievaltoolkits_amd import kernels
+    rng = np.random.default_rng(2024)
+    worst = {}
+    for name, q, p in _bound_cases(rng):
+        qt, pt = to_dev_bf16(q, dev), to_dev_bf16(p, dev)
+        s, i, st = kernels.ip_topk(qt, pt, 256)
+        s, i = s.cpu().numpy().astype(np.float64), i.cpu().numpy()
+        exact = np.einsum("qd,qkd->qk", q.astype(np.float64), p.astype(np.float64)[i])
+        ratio = np.abs(s - exact) / _np_eps(q, p)[:, None]
+        worst[name] = float(ratio.max())
+        assert (ratio <= 1.0).all(), (name, worst)
+    assert worst["truncation"] > 0.3, worst   # the case really exercises the truncation term
+
+
+def test_exact_order_truncation_case_bit_exact(dev):
+    """The truncation-worst-case data through the product index: canonical ids equal the fp64 oracle."""
+    from denseretrievaltoolkits_amd import search as srch
+    rng = np.random.default_rng(7)
+    name, q, p = [c for c in _bound_cases(rng) if c[0] == "truncation"][0]
+    idx = srch.FlatIPIndex.from_rows(to_dev_bf16(p, dev))
+    s, i = idx.search(q, 500)
+    es, ei = orc.ip_topk(q, p, 500)
+    np.testing.assert_array_equal(i, ei)
+    assert idx.order_uncertified == 0
 
 
 @pytest.mark.parametrize("nq,n,d,k", [
@@ -122,20 +199,44 @@ def test_exact_order_resolve_path(dev):
     assert (st.cpu().numpy() == 0).all()
 
 
-def test_exact_order_window_wider_than_list_keeps_fp32_order(dev):
-    """Massive exact ties on non-integer values (every row identical, values k + 0.5): the
-    near-tie window holds every row, more than the kc candidates -> status bit 1, the fp32 order
-    (here: ascending id, all scores equal) is kept, and nothing is rescanned (bit 0 clear)."""
+def test_exact_order_window_wider_than_list_resolved_wide(dev):
+    """Massive exact ties on non-integer values (every row identical, values k + 0.5): the near-tie
+    window holds every row, more than the kc candidates -> status 2 (not a rescan: bit 0 clear); the
+    wide resolve collects the window, ranks it by exact score and id and clears the bit."""
+    import torch
+    from denseretrievaltoolkits_amd import kernels
     rng = np.random.default_rng(8)
     n, d, k = 12000, 128, 500          # n <= cap: the dense path (every row scored)
     row = orc.bf16_round(int_bf16(rng, (1, d), -3, 3) + 0.5)
     p = np.repeat(row, n, axis=0)
     q = orc.bf16_round(int_bf16(rng, (4, d), -3, 3) + 0.25)
-    gs, gi, st = _exact(dev, q, p, k, resolve=False)
-    assert ((st & 2) != 0).all() and ((st & 1) == 0).all(), st
+    qt, pt = to_dev_bf16(q, dev), to_dev_bf16(p, dev)
+    stats = kernels.row_stats(pt)
+    s, i, st = kernels.ip_topk(qt, pt, k, resolve=False, stats=stats)
+    torch.cuda.synchronize()
+    assert (st.cpu().numpy() == 2).all(), st
+    assert kernels.resolve_wide(qt, pt, k, 0, s, i, st, stats) == 4
     es, ei = orc.ip_topk(q, p, k)
-    np.testing.assert_array_equal(gi, ei)
-    np.testing.assert_array_equal(gs, es)
+    np.testing.assert_array_equal(i.cpu().numpy(), ei)
+    np.testing.assert_array_equal(s.cpu().numpy(), es)
+    assert (st.cpu().numpy() == 0).all()
+
+
+def test_exact_order_window_beyond_wide_cap_keeps_fp32_order(dev):
+    """More tied rows than the wide resolve can rank (65536 per query): status bit 1 stays and the
+    certified fp32 top-k is kept in the fp32 order (here ascending id, all scores equal), counted by
+    the index."""
+    from denseretrievaltoolkits_amd import search as srch
+    rng = np.random.default_rng(9)
+    n, d, k = 70000, 64, 10
+    row = orc.bf16_round(int_bf16(rng, (1, d), -3, 3) + 0.5)
+    p = np.repeat(row, n, axis=0)
+    q = orc.bf16_round(int_bf16(rng, (2, d), -3, 3) + 0.25)
+    idx = srch.FlatIPIndex.from_rows(to_dev_bf16(p, dev))
+    s, i = idx.search(q, k)
+    es, ei = orc.ip_topk(q, p, k)
+    np.testing.assert_array_equal(i, ei)
+    assert idx.order_uncertified == 2 and idx.wide_resolved == 0
 
 
 def test_flat_index_exact_order_default_and_counter(dev):
@@ -163,14 +264,16 @@ def test_flat_index_exact_order_default_and_counter(dev):
     assert idx.order_uncertified == 0 and idx.group_fallbacks == 0
 
 
-def test_exact_order_degenerate_near_ties_keep_fp32_result_without_rescan(dev):
-    """Sampled path, every score within the fp32 error bound of every other (a common large
-    component + 1e-4-scale rest: the untrained-tower case of the C2 leg): the near-tie window
-    reaches below the filter threshold, so the canonical order cannot be certified from the list.
-    Status bit 1 is set, bit 0 is NOT (no dense rescan), and the result is exactly the fp32 path's
-    (ip_topk without row statistics): the certified fp32 top-k in the fp32 order."""
+@pytest.mark.parametrize("grouped", [False, True])
+def test_exact_order_degenerate_near_ties_bit_exact(dev, grouped):
+    """Sampled path, every score within the fp32 resolution of the others (a common large component +
+    1e-4-scale rest: ~76 rows per fp32 ulp of the scores, the untrained-tower regime): the near-tie
+    window is far wider than the candidate list, so the product index runs the wide resolve (a filter
+    pass at s_k - 2 eps, exact sums, exact-key selection) and the ids equal the fp64 oracle's -- per
+    batch and through the grouped path."""
     import torch
     from denseretrievaltoolkits_amd import kernels
+    from denseretrievaltoolkits_amd import search as srch
     rng = np.random.default_rng(21)
     n, d, k, nq = 60000, 128, 1000, 4
     p = orc.bf16_round(1e-4 * rng.standard_normal((n, d)))
@@ -178,11 +281,18 @@ def test_exact_order_degenerate_near_ties_keep_fp32_result_without_rescan(dev):
     q = orc.bf16_round(rng.standard_normal((nq, d)))
     q[:, 0] = 8.0
     qt, pt = to_dev_bf16(q, dev), to_dev_bf16(p, dev)
-    stats = kernels.row_stats(pt)
-    s, i, st = kernels.ip_topk(qt, pt, k, resolve=False, stats=stats)
-    s32, i32, st32 = kernels.ip_topk(qt, pt, k, resolve=False)
+    _, _, st = kernels.ip_topk(qt, pt, k, resolve=False, stats=kernels.row_stats(pt))
     torch.cuda.synchronize()
-    st = st.cpu().numpy()
-    assert ((st & 2) != 0).all() and ((st & 1) == 0).all(), st
-    assert (st32.cpu().numpy() == 0).all()
-    assert torch.equal(i, i32) and torch.equal(s, s32)
+    assert (st.cpu().numpy() == 2).all(), st          # uncertifiable from the candidate list
+    idx = srch.FlatIPIndex.from_rows(pt)
+    saved = srch.GROUP_MIN_ROWS
+    srch.GROUP_MIN_ROWS = 0 if grouped else 1 << 62
+    try:
+        res = idx.search_batches([qt[:2], qt[2:]], k, id_offset=5)
+        torch.cuda.synchronize()
+    finally:
+        srch.GROUP_MIN_ROWS = saved
+    es, ei = orc.ip_topk(q, p, k, id_offset=5)
+    np.testing.assert_array_equal(torch.cat([r[1] for r in res]).cpu().numpy(), ei)
+    _assert_scores(torch.cat([r[0] for r in res]).cpu().numpy(), es)
+    assert idx.order_uncertified == 0 and idx.wide_resolved == nq

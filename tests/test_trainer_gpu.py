@@ -82,10 +82,12 @@ def test_evaluate_end_to_end_matches_oracle(dev, tmp_path, layers, n_docs, n_q, 
     # independent restatement from the written shard file + a fresh query encode
     rows = shards.load_rows(shards.list_shards(str(tmp_path / "emb"), 0), 0, n_docs, "cpu").float().numpy()
     assert rows.shape == (n_docs, 768)
+    # the query reps exactly as evaluate made them (one tower pass per query window)
     with torch.no_grad():
-        qr = torch.cat([model(query={kk: v.to(dev) for kk, v in b[1].items()}).q_reps for b in ql]).float().cpu()
+        qr = torch.cat([tr._encode_window(w) for w in tr._query_windows(ql)]).float().cpu()
     q = qr.to(torch.bfloat16).float().numpy()
-    es, ei = orc.ip_topk(q, rows, k)
+    es, ei = orc.ip_topk(q, rows, k)   # fp64: the canonical order (ties by ascending id)
+    assert tr.index.local.order_uncertified == 0
     got = {}
     with open(tmp_path / "ret" / "0.0.json", encoding="utf-8") as f:
         for line in f:
@@ -97,11 +99,9 @@ def test_evaluate_end_to_end_matches_oracle(dev, tmp_path, layers, n_docs, n_q, 
     for qi in range(n_q):
         g = got[qi]
         assert len(g) == k
-        # ids identical except where the oracle's scores tie within the 1e-3 score tolerance
+        # north_star: bit-exact retrieved doc ids and ranks against the fp64 evaluator
+        np.testing.assert_array_equal(np.asarray(g), ei[qi])
         for j in range(k):
-            if g[j] != ei[qi, j]:
-                s_true = float(q[qi] @ rows[g[j]])
-                assert abs(s_true - es[qi, j]) <= 1e-3, (qi, j, g[j], ei[qi, j])
             pos[qi, j] = has_answers(corpus[g[j]]["original"], answers[qi])
     ref = get_metrics(pos, topk)
     for key, v in ref.items():
