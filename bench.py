@@ -316,6 +316,101 @@ def pmc_traffic(args, world):
     return None, None
 
 
+def launch_queries(steps, qb, grouped, group_queries):
+    """Queries of every filter-scan launch in the timed region: one launch per batch on the per-batch
+    path, one per group of batches (search._groups: at most group_queries queries) on the grouped one."""
+    if not grouped:
+        return [qb] * steps
+    sizes, cur = [], 0
+    for _ in range(steps):
+        if cur and cur + qb > group_queries:
+            sizes.append(cur)
+            cur = 0
+        cur += qb
+    if cur:
+        sizes.append(cur)
+    return sizes
+
+
+def scan_roofline(n_corpus, world, d, k, kc, sizes, grouped, launch_ms_total):
+    """Roofline of the filter-scan launches of the timed region from their own shapes:
+    per launch over a shard of N_s rows with Q queries, bytes = N_s d 2 + Q d 2 + the result lists
+    (Q k 12 per batch; the grouped launch writes packed [Q, kc + 1] u64 lists), flops = 2 Q N_s d;
+    t_roof = max(bytes / 8 TB/s, flops / 2.5 PF/s) summed over the launches; frac = t_roof / measured;
+    achieved = the bound's quantity / measured.  A grouped launch (Q = 2048) is MFMA-side, a
+    128-query pass HBM-bound."""
+    per = -(-n_corpus // world)
+    byts = sum(per * d * 2 + q * d * 2 + (q * (kc + 1) * 8 if grouped else q * k * 12) for q in sizes)
+    flops = sum(2 * q * per * d for q in sizes)
+    t_hbm = byts / (HBM_PEAK_GBS * 1e9)
+    t_mfma = flops / (BF16_PEAK_TFLOPS * 1e12)
+    t = launch_ms_total * 1e-3
+    hbm = t_hbm >= t_mfma
+    rec = {
+        "bound": "hbm" if hbm else "mfma",
+        "achieved": round(byts / t / 1e9 if hbm else flops / t / 1e12, 1),
+        "peak": HBM_PEAK_GBS if hbm else BF16_PEAK_TFLOPS,
+        "unit": "GB/s" if hbm else "TFLOP/s",
+        "frac": round(max(t_hbm, t_mfma) / t, 4),
+        "launches": len(sizes),
+        "queries_per_launch": sorted(set(sizes)),
+        "avg_launch_ms": round(launch_ms_total / max(1, len(sizes)), 4),
+        "alg_bytes_per_launch": int(byts // max(1, len(sizes))),
+        "alg_flops_per_launch": int(flops // max(1, len(sizes))),
+    }
+    return rec
+
+
+def search_record(args, world, grouped, group_queries, kc, elapsed_s, launch_ms_total, launches, traffic):
+    """The headline JSON record of the search leg (rank 0)."""
+    d, k, qb = args.dim, args.k, args.qb
+    sizes = launch_queries(args.steps, qb, grouped, group_queries)
+    rf = scan_roofline(args.n_corpus, world, d, k, kc, sizes, grouped, launch_ms_total)
+    rf = {"kernel": "ip_scan16r_kernel<%d> (csrc/search.hip)" % d, **rf}
+    if launches != len(sizes):
+        rf["launches_counted"] = launches   # the profiler's count (differs only if a batch was redone)
+    # PMC traffic: recorded for the per-batch configuration (tools/pmc_traffic.py)
+    tb, tsrc = traffic if not grouped else (None, None)
+    rf["traffic"] = tb
+    rf["traffic_source"] = tsrc
+    if world == 1:
+        path = ("FlatIPIndex.search_batches (certified, pipelined; " +
+                (f"grouped: one sample launch, one filter launch over all {group_queries} queries of a group "
+                 "(16 query blocks sharing each corpus tile through L2) and one merge per group)" if grouped else
+                 "per batch: sample scan + k-th selection, one filter launch, select, canonical-order stage)"))
+    else:
+        path = (f"ShardedFlatIP.search_batches ({args.protocol}, certified, pipelined; " +
+                (f"grouped: one sample launch, sample-list all-gather, one filter launch over all "
+                 f"{group_queries} queries of a group, packed all-gather and merge per group)" if grouped else
+                 "per batch: per-shard exact top-k, all-gather, merge)"))
+    qps = args.steps * qb / elapsed_s
+    return {
+        "metric": "queries/sec@top-1000, 10Mx768 corpus (BASELINE: passages encoded/sec + queries/sec@top-1000, "
+                  "10Mx768 corpus, 1/2/4/8 GPU)",
+        "value": round(qps, 2),
+        "unit": "queries/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(elapsed_s / args.steps * 1e3, 4),
+        "higher_is_better": True,
+        "scaling": "strong",
+        "vs_baseline": None,
+        "dtype": "bf16",
+        "data": "synthetic: N(0,1) corpus and queries rounded to bf16, generated in HBM (seeded)",
+        "config": {
+            "workload": f"exact IP top-{k}, {args.n_corpus} x {d} bf16 corpus row-sharded over {world} GPU(s), "
+                        f"loader batch {qb} queries" + (f", searched in groups of {group_queries}" if grouped else
+                                                        ", searched per batch"),
+            "n_corpus": args.n_corpus, "dim": d, "query_batch": qb, "k": k,
+            "queries_per_filter_launch": group_queries if grouped else qb,
+            "parallelism": f"row-shard x{world}",
+            "path": path,
+        },
+        "roofline": rf,
+    }
+
+
 def encode_leg(args, device):
     import bench_legs
     return bench_legs.run(device)
@@ -352,7 +447,6 @@ def main():
         srch.GROUP_QUERIES = args.group_queries
         srch.GROUP_MIN_ROWS = 0                 # one-GPU: grouped path too, at any shard size
         srch.GROUP_MAX_ROWS = 1 << 62
-    use_global = (world > 1 and args.protocol == "global_tau") or (world == 1 and n_local >= srch.GROUP_MIN_ROWS)
     # the product path: the same index objects and certified, pipelined batch search that
     # BaseFaissIPRetriever.batch_search / Trainer.evaluate use (search.py); every query
     # certified exact inside the timed region (an uncertified one is rescanned there)
@@ -374,101 +468,69 @@ def main():
     run(0, args.warmup)
     torch.cuda.synchronize()
     local_index = index if world == 1 else index.local
-    res0 = local_index.resolved
 
     def fallbacks():
         return index.group_fallbacks if world == 1 else index.fallbacks
-    fb0 = fallbacks()
-    unc0 = index.order_uncertified
 
-    _quiesce_gc()
-    lib.drt_profile_enable(_native.PROF_SCAN, 1)
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    results = run(args.warmup, nsteps)
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    t1 = time.perf_counter()
-    lib.drt_profile_enable(_native.PROF_SCAN, 0)
-    n_resolved = local_index.resolved - res0
-    n_fallback = fallbacks() - fb0
-    n_unc = index.order_uncertified - unc0
-    tot_ms = _native.ctypes.c_double(0.0)
-    cnt = _native.c_i64(0)
-    _native.check(lib.drt_profile_read(_native.PROF_SCAN, _native.ctypes.byref(tot_ms), _native.ctypes.byref(cnt)),
-                  "drt_profile_read")
+    def timed(first, last):
+        """Batches [first, last) between barriers + syncs: (results, max-over-ranks elapsed s, filter-launch
+        ms summed over the launches (slowest rank's average x count), launches, counter deltas)."""
+        res0, fb0, unc0 = local_index.resolved, fallbacks(), index.order_uncertified
+        _quiesce_gc()
+        lib.drt_profile_enable(_native.PROF_SCAN, 1)
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        res = run(first, last)
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        t1 = time.perf_counter()
+        lib.drt_profile_enable(_native.PROF_SCAN, 0)
+        tot_ms = _native.ctypes.c_double(0.0)
+        cnt = _native.c_i64(0)
+        _native.check(lib.drt_profile_read(_native.PROF_SCAN, _native.ctypes.byref(tot_ms),
+                                           _native.ctypes.byref(cnt)), "drt_profile_read")
+        elapsed = torch.tensor([t1 - t0], dtype=torch.float64, device=dev)
+        scan_ms = torch.tensor([tot_ms.value / max(1, cnt.value)], dtype=torch.float64, device=dev)
+        if world > 1:
+            if gloo:
+                elapsed, scan_ms = elapsed.cpu(), scan_ms.cpu()
+            dist.all_reduce(elapsed, op=dist.ReduceOp.MAX)
+            dist.all_reduce(scan_ms, op=dist.ReduceOp.MAX)
+        counters = (local_index.resolved - res0, fallbacks() - fb0, index.order_uncertified - unc0)
+        return res, float(elapsed.item()), float(scan_ms.item()) * int(cnt.value), int(cnt.value), counters
 
-    elapsed = torch.tensor([t1 - t0], dtype=torch.float64, device=dev)
-    scan_ms = torch.tensor([tot_ms.value / max(1, cnt.value)], dtype=torch.float64, device=dev)
-    if world > 1:
-        if gloo:
-            elapsed, scan_ms = elapsed.cpu(), scan_ms.cpu()
-        dist.all_reduce(elapsed, op=dist.ReduceOp.MAX)
-        dist.all_reduce(scan_ms, op=dist.ReduceOp.MAX)
-    el = float(elapsed.item())
-    scan_ms_v = float(scan_ms.item())
+    results, el, scan_ms_total, launches, (n_resolved, n_fallback, n_unc) = timed(args.warmup, nsteps)
+    grouped = index._use_groups()
+    sub = None
+    if world > 1 and grouped:
+        # SURVEY §8(d)'s HBM-bound configuration beside the product default: the same protocol with one
+        # 128-query batch per group (one filter launch per batch)
+        gq_saved = srch.GROUP_QUERIES
+        srch.GROUP_QUERIES = qb
+        run(0, 1)
+        _, el1, ms1, n1, _ = timed(args.warmup, nsteps)
+        srch.GROUP_QUERIES = gq_saved
+        if rank == 0:
+            sub = search_record(args, world, True, qb, kernels.refine_width(k), el1, ms1, n1, (None, None))
+            sub = {"value": sub["value"], "ms_per_step": sub["ms_per_step"],
+                   "config": "one 128-query batch per group (per-batch global-threshold protocol)",
+                   "roofline": sub["roofline"]}
 
     out = None
     if rank == 0:
-        qps = args.steps * qb / el
-        # algorithmic bytes of ONE filter-scan launch on the largest shard:
-        # corpus shard (per-row d*2 B) + query block + result lists
-        per = -(-args.n_corpus // world)
-        alg_bytes = per * d * 2 + qb * d * 2 + (qb * (k + 1) * 8 if use_global else qb * k * 12)
-        achieved = alg_bytes / (scan_ms_v * 1e-3) / 1e9
-        traffic, traffic_src = pmc_traffic(args, world)
-        out = {
-            "metric": "queries/sec@top-1000, 10Mx768 corpus (BASELINE: passages encoded/sec + queries/sec@top-1000, 10Mx768 corpus, 1/2/4/8 GPU)",
-            "value": round(qps, 2),
-            "unit": "queries/s",
-            "n_gpus": world,
-            "steps": args.steps,
-            "warmup": args.warmup,
-            "ms_per_step": round(el / args.steps * 1e3, 4),
-            "higher_is_better": True,
-            "scaling": "strong",
-            "vs_baseline": None,
-            "dtype": "bf16",
-            "data": "synthetic: N(0,1) corpus and queries rounded to bf16, generated in HBM (seeded)",
-            "config": {
-                "workload": f"exact IP top-{k}, {args.n_corpus} x {d} bf16 corpus row-sharded over {world} GPU(s), "
-                            f"query batch {qb}" + (", global-threshold protocol (RCCL all-gather of sample lists "
-                                                   "and packed per-shard top-k, device merge)" if use_global else
-                                                   (", RCCL all-gather of per-shard top-k + device merge"
-                                                    if world > 1 else "")),
-                "n_corpus": args.n_corpus, "dim": d, "query_batch": qb, "k": k,
-                "parallelism": f"row-shard x{world}",
-                "path": ("FlatIPIndex.search_batches (certified, pipelined" +
-                         (f"; sample phase and merge per group of {srch.GROUP_QUERIES} queries, one filter scan "
-                          "per batch)" if use_global else ")")) if world == 1 else
-                        (f"ShardedFlatIP.search_batches ({args.protocol}, certified, pipelined" +
-                         (f"; sample phase, exchanges and merge per group of {srch.GROUP_QUERIES} queries, one "
-                          "filter scan per batch)" if use_global else ")")),
-            },
-            "roofline": {
-                "kernel": "ip_scan16r_kernel<768> (csrc/search.hip)",
-                "bound": "hbm",
-                "achieved": round(achieved, 1),
-                "peak": HBM_PEAK_GBS,
-                "unit": "GB/s",
-                "frac": round(achieved / HBM_PEAK_GBS, 4),
-                "traffic": traffic,
-                "traffic_source": traffic_src,
-                "avg_launch_ms": round(scan_ms_v, 4),
-                "launches": int(cnt.value),
-                "alg_bytes_per_launch": alg_bytes,
-            },
-            "order": ("canonical: exact-score re-rank of each query's near-tie window (fp64 sums of the bf16 "
-                      "products, ties by id), the product default" if args.order == "exact" else
-                      "fp32 scan order (A/B leg)"),
-            "order_uncertified_queries": int(n_unc),
-            "uncertified_queries_resolved": int(n_resolved),
-            "global_tau_fallback_batches": int(n_fallback),
-            "query_group": srch.GROUP_QUERIES if use_global else qb,
-        }
+        out = search_record(args, world, grouped, srch.GROUP_QUERIES, kernels.refine_width(k), el,
+                            scan_ms_total, launches, pmc_traffic(args, world))
+        if sub is not None:
+            out["per_batch_qb%d" % qb] = sub
+        out["order"] = ("canonical: exact-score re-rank of each query's near-tie window (fp64 sums of the bf16 "
+                        "products, ties by id), the product default" if args.order == "exact" else
+                        "fp32 scan order (A/B leg)")
+        out["order_uncertified_queries"] = int(n_unc)
+        out["uncertified_queries_resolved"] = int(n_resolved)
+        out["global_tau_fallback_batches"] = int(n_fallback)
         if world == 1 and not args.no_cpu_baseline:
             out["cpu_baseline"] = cpu_baseline(args, shard, queries[args.warmup], results[0])
     # the search leg's 15 GB corpus, index and results leave HBM before the model legs (the training

@@ -3447,7 +3447,7 @@ int drt_ip_topk_resolve_wide(const void* Q, int64_t nq, const void* P, int64_t n
     a.counts = counts;
     a.out = keys;
     a.cap = kWideCap;
-    const int rc = launch_scan(a, d, SCAN_FILTER, s, PROF_SCAN);
+    const int rc = launch_scan(a, d, SCAN_FILTER, s, -1);   // (not a headline filter launch)
     if (rc) return rc;
     hipLaunchKernelGGL(wide_exact_kernel, dim3((unsigned)nb, (unsigned)(kWideCap / kWideSlice)), dim3(kRefThreads), 0,
                        s, w);

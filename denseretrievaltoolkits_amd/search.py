@@ -542,8 +542,7 @@ class ShardedFlatIP:
         checks group g's certificates.  Otherwise batch j + 1 is enqueued (scan, exchange, merge)
         before the host checks batch j's certificate."""
         batches = list(batches)
-        if self._multi() and self.protocol == "global_tau" and self.ntotal < 0xFFFFFFFF \
-                and isinstance(self.local, FlatIPIndex):
+        if self._use_groups():
             groups = [[self.local._queries(q) for q in g] for g in _groups(batches)]
 
             def redo(q):
@@ -566,6 +565,11 @@ class ShardedFlatIP:
             if to_host and isinstance(r[0], torch.Tensor):
                 r = (r[0].cpu().numpy(), r[1].cpu().numpy())
             yield r
+
+    def _use_groups(self) -> bool:
+        """search_batches runs the grouped global-threshold protocol (one filter launch per group)."""
+        return (self._multi() and self.protocol == "global_tau" and self.ntotal < 0xFFFFFFFF
+                and isinstance(self.local, FlatIPIndex))
 
     def _all_gather(self, t: torch.Tensor) -> torch.Tensor:
         """[world, *t.shape] all-gather (RCCL on device; host-staged under gloo, comm.py)."""

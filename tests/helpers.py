@@ -61,16 +61,22 @@ def corpus_topk_golden():
     return q, p, int(z["k"]), int(z["parts"]), z["ids"].astype(np.int64), z["scores"]
 
 
-def oracle_topk_streamed(q, p_dev, k, chunk=1 << 20, id_offset=0):
+def oracle_topk_streamed(q, p_dev, k, chunk=1 << 20, id_offset=0, exact=False):
     """oracle.ip_topk of host queries q [nq, d] over a DEVICE corpus p_dev [n, d] (bf16), streamed to
-    the host chunk by chunk (fp32 BLAS: exact for the integer-valued fixtures) and merged with the
-    oracle's partition merge -- the full-size reference answer without a full host copy."""
+    the host chunk by chunk (fp32 BLAS: exact for the integer-valued fixtures; ``exact``: fp64, the
+    canonical order of real-valued data) and merged with the oracle's partition merge -- the
+    full-size reference answer without a full host copy."""
     from oracle.search_oracle import ip_topk, merge_topk
     es = ei = None
     n = p_dev.shape[0]
     for a in range(0, n, chunk):
-        pc = p_dev[a: a + chunk].float().cpu().numpy()
-        cs, ci = ip_topk(q, pc, k, id_offset=id_offset + a, dtype=np.float32)
+        if exact:
+            pc = p_dev[a: a + chunk].double().cpu().numpy()
+            cs, ci = ip_topk(q.astype(np.float64), pc, k, id_offset=id_offset + a, dtype=np.float64,
+                             out_dtype=np.float64)
+        else:
+            pc = p_dev[a: a + chunk].float().cpu().numpy()
+            cs, ci = ip_topk(q, pc, k, id_offset=id_offset + a, dtype=np.float32)
         es, ei = (cs, ci) if es is None else merge_topk(np.stack([es, cs]), np.stack([ei, ci]), k)
     return es, ei
 

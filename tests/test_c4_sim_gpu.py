@@ -1,0 +1,118 @@
+"""GPU: BASELINE config C4 -- a 10M x 768 bf16 corpus row-sharded over 8 GPUs -- at its own size on ONE
+GPU, through the product's per-rank code (search._gtau_enqueue_group / _gtau_finish_group, the path
+ShardedFlatIP.search_batches runs on every rank).
+
+Every shard of the 8-way contiguous split (bench.gen_shard's split) lives on this GPU.  For each
+simulated rank R the collectives are replaced by what RCCL would hand that rank: the `gather` hook
+splices R's own sample / packed lists into buffers holding the other ranks' (computed beforehand by
+the same kernels on their shards), and the canonical stage's delta all-reduce is the SUM of every
+shard's refine_delta over the same merged candidate list.  Every rank must produce the same result,
+and that result must equal the oracle over the whole corpus: bit for bit on the integer corpus (heavy
+ties at the k-th score), id for id against the fp64 order on a Gaussian corpus.  Grouped (one filter
+launch per group of batches, the product default across GPUs) and one batch per group.
+Reference: DRT/trainer/trainer.py:220-262 (shard exchange), DRT/model/utils.py:215-229 (partition
+merge), DRT/evaluator/index.py:31-33."""
+import numpy as np
+import pytest
+
+from helpers import device_int_corpus, gauss_bf16, int_bf16, oracle_topk_streamed, to_dev_bf16
+
+pytestmark = pytest.mark.gpu
+
+W, N, D, K, QB = 8, 10_000_000, 768, 1000, 128
+
+
+def _simulate(dev, pt, batches, k, group_queries, monkeypatch):
+    """Per simulated rank: [(scores, ids)] of every batch, through the product's group functions."""
+    import torch
+    from denseretrievaltoolkits_amd import kernels, ops
+    from denseretrievaltoolkits_amd import search as srch
+    per = -(-N // W)
+    offs = [min(N, r * per) for r in range(W)]
+    locs = [srch.FlatIPIndex.from_rows(pt[o: min(N, o + per)]) for o in offs]
+    st = torch.stack([loc.row_stats() for loc in locs])
+    stats = st.max(0).values.clone()
+    stats[1] = st[:, 1].min()                  # ShardedFlatIP.sync_offsets' combination
+    groups = list(srch._groups(batches, cap=group_queries))
+    kc = kernels.refine_width(k)
+    exch = []                                  # the other ranks' exchanged data, per group
+    for grp in groups:
+        qg = torch.cat(grp)
+        lists = torch.stack([loc.dist_sample(qg, N, k) for loc in locs]).contiguous()
+        tau = kernels.dist_tau(lists, k)
+        parts = torch.empty((W, qg.shape[0], kc + 1), dtype=torch.int64, device=dev)
+        for r in range(W):
+            kernels.dist_filter_into(qg, locs[r].rows, N, kc, offs[r], tau, parts[r])
+        exch.append((lists, parts))
+    drt = ops.load()
+    cur = {}
+
+    def refine_all_shards(q, p, row_offset, cand_s, cand_i, k_, stats_, tau, status, all_reduce_sum=None):
+        # rank R's own deltas (status bits set there), plus every other shard's: the SUM all-reduce
+        delta, cnt = drt.refine_delta(q, p, row_offset, cand_s, cand_i, k_, stats_, tau, status)
+        for r in range(W):
+            if r != cur["R"]:
+                dr, _ = drt.refine_delta(q, locs[r].rows, offs[r], cand_s, cand_i, k_, stats_, tau, status.clone())
+                delta += dr
+        return drt.refine_sort(cand_s, cand_i, delta, cnt, k_)
+
+    monkeypatch.setattr(kernels, "refine", refine_all_shards)
+    out = []
+    for R in range(W):
+        cur["R"] = R
+        res = []
+        for (lists, parts), grp in zip(exch, groups):
+            calls = [0]
+
+            def gather(t, lists=lists, parts=parts, calls=calls):
+                buf = (lists if calls[0] == 0 else parts).clone()
+                calls[0] += 1
+                buf[R].copy_(t)
+                return buf
+            pend = srch._gtau_enqueue_group(locs[R], grp, k, N, offs[R], gather, stats=stats,
+                                            all_reduce_sum=lambda t: t)
+
+            def redo(q):
+                raise AssertionError("a group the global-threshold protocol could not certify")
+            r_, nredo, nunc = srch._gtau_finish_group(pend, redo)
+            assert nredo == 0 and nunc == 0
+            res += r_
+        torch.cuda.synchronize()
+        out.append((torch.cat([a for a, _ in res]).cpu().numpy(), torch.cat([b for _, b in res]).cpu().numpy()))
+    return out
+
+
+def test_c4_integer_corpus_full_size_bit_exact(dev, monkeypatch):
+    import torch
+    rng = np.random.default_rng(444)
+    q = int_bf16(rng, (2 * QB, D), -4, 4)
+    pt = device_int_corpus(N, D, -4, 4, 4321, dev)
+    qd = to_dev_bf16(q, dev)
+    es, ei = oracle_topk_streamed(q, pt, K)
+    for group_queries in (2 * QB, QB):   # one group of both batches; one batch per group
+        ranks = _simulate(dev, pt, [qd[:QB], qd[QB:]], K, group_queries, monkeypatch)
+        for R, (gs, gi) in enumerate(ranks):
+            np.testing.assert_array_equal(gi, ei, err_msg=f"rank {R}, group {group_queries}")
+            np.testing.assert_array_equal(gs, es, err_msg=f"rank {R}, group {group_queries}")
+    assert (es[:, 1:] == es[:, :-1]).mean() > 0.5   # the k-th boundary really is tied
+    del pt
+    torch.cuda.empty_cache()
+
+
+def test_c4_gaussian_batch_matches_fp64_order(dev, monkeypatch):
+    """Real-valued data: the canonical stage (deltas summed over the 8 shards) ranks the merged
+    candidates by their exact scores -- id for id the fp64 evaluator's order over the whole corpus."""
+    import torch
+    import bench
+    pt = torch.cat([bench.gen_shard(N, W, r, D, dev)[0] for r in range(W)])
+    rng = np.random.default_rng(445)
+    q = gauss_bf16(rng, (QB, D))
+    qd = to_dev_bf16(q, dev)
+    ranks = _simulate(dev, pt, [qd], K, 2048, monkeypatch)
+    es, ei = oracle_topk_streamed(q, pt, K, exact=True)
+    for R, (gs, gi) in enumerate(ranks):
+        np.testing.assert_array_equal(gi, ei, err_msg=f"rank {R}")
+        ulp = np.spacing(np.abs(es).astype(np.float32))
+        assert (np.abs(gs.astype(np.float64) - es) <= ulp).all()
+    del pt
+    torch.cuda.empty_cache()

@@ -44,7 +44,8 @@ def main():
     locs = [FlatIPIndex.from_rows(sh) for sh, _, _ in shards]
     offs = [lo for _, lo, _ in shards]
     st = torch.stack([l.row_stats() for l in locs])
-    stats = torch.stack([st[:, 0].max(), st[:, 1].min()]).contiguous()
+    stats = st.max(0).values.clone()
+    stats[1] = st[:, 1].min()   # (ShardedFlatIP.sync_offsets)
     g = torch.Generator(device=dev)
     g.manual_seed(5678)
     queries = [torch.randn((qb, a.dim), generator=g, device=dev).to(torch.bfloat16) for _ in range(a.batches)]
