@@ -43,8 +43,10 @@ BF16_PEAK_TFLOPS = 2500.0  # dense bf16 MFMA spec
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=20)
-    ap.add_argument("--warmup", type=int, default=3)
+    # 32 steps = two full groups of 16 batches on the grouped path (search.GROUP_QUERIES); the warm-up
+    # runs one full group too (first-use allocations of the group-sized buffers)
+    ap.add_argument("--steps", type=int, default=32)
+    ap.add_argument("--warmup", type=int, default=16)
     ap.add_argument("--n-corpus", type=int, default=10_000_000)
     ap.add_argument("--dim", type=int, default=768)
     ap.add_argument("--qb", type=int, default=128)
@@ -294,12 +296,15 @@ def encode_cpu_baseline(batch=32, L=128, min_seconds=10.0):
             "kind": "port", "sample": f"{steps} batches of {batch} x {L} tokens, fp32, {el:.1f} s", **thr}
 
 
-def pmc_traffic(args, world):
+def pmc_traffic(args, world, shape=None):
     """HBM bytes per launch of the dominant kernel from a committed rocprofv3 PMC pass
     (tools/pmc_traffic.py -> profiles/*_pmc_traffic.json) measured on this exact
-    configuration; None when no such measurement exists."""
+    configuration (``shape`` = (queries, rows) of a grouped launch); None when no such measurement
+    exists."""
     import glob
     want = {"n_corpus": args.n_corpus, "world": world, "qb": args.qb, "k": args.k, "dim": args.dim}
+    if shape is not None:
+        want.update(launch_queries=int(shape[0]), launch_rows=int(shape[1]))
     import re
 
     def order(f):   # newest measurement first: round, then tag (a..z, aa..az, ba.. : by length, then letters)
@@ -316,11 +321,12 @@ def pmc_traffic(args, world):
     return None, None
 
 
-def launch_queries(steps, qb, grouped, group_queries):
-    """Queries of every filter-scan launch in the timed region: one launch per batch on the per-batch
-    path, one per group of batches (search._groups: at most group_queries queries) on the grouped one."""
+def launch_shapes(steps, qb, grouped, group_queries, rows, chunks=None):
+    """(queries, rows) of every filter-scan launch in the timed region: one launch per batch over the
+    shard on the per-batch path; on the grouped one, per group of batches (search._groups: at most
+    group_queries queries) one launch over the shard, or one per row chunk (one GPU, search.group_chunks)."""
     if not grouped:
-        return [qb] * steps
+        return [(qb, rows)] * steps
     sizes, cur = [], 0
     for _ in range(steps):
         if cur and cur + qb > group_queries:
@@ -329,54 +335,58 @@ def launch_queries(steps, qb, grouped, group_queries):
         cur += qb
     if cur:
         sizes.append(cur)
-    return sizes
+    parts = [b - a for a, b in chunks] if chunks else [rows]
+    return [(q, r) for q in sizes for r in parts]
 
 
-def scan_roofline(n_corpus, world, d, k, kc, sizes, grouped, launch_ms_total):
+def scan_roofline(d, k, kc, shapes, grouped, launch_ms_total):
     """Roofline of the filter-scan launches of the timed region from their own shapes:
-    per launch over a shard of N_s rows with Q queries, bytes = N_s d 2 + Q d 2 + the result lists
-    (Q k 12 per batch; the grouped launch writes packed [Q, kc + 1] u64 lists), flops = 2 Q N_s d;
-    t_roof = max(bytes / 8 TB/s, flops / 2.5 PF/s) summed over the launches; frac = t_roof / measured;
+    per launch over N_s rows with Q queries, bytes = N_s d 2 + Q d 2 + the result lists (Q k 12 per
+    batch; the grouped launch writes packed [Q, kc + 1] u64 lists), flops = 2 Q N_s d; t_roof =
+    max(bytes / 8 TB/s, flops / 2.5 PF/s) summed over the launches; frac = t_roof / measured;
     achieved = the bound's quantity / measured.  A grouped launch (Q = 2048) is MFMA-side, a
     128-query pass HBM-bound."""
-    per = -(-n_corpus // world)
-    byts = sum(per * d * 2 + q * d * 2 + (q * (kc + 1) * 8 if grouped else q * k * 12) for q in sizes)
-    flops = sum(2 * q * per * d for q in sizes)
+    byts = sum(r * d * 2 + q * d * 2 + (q * (kc + 1) * 8 if grouped else q * k * 12) for q, r in shapes)
+    flops = sum(2 * q * r * d for q, r in shapes)
     t_hbm = byts / (HBM_PEAK_GBS * 1e9)
     t_mfma = flops / (BF16_PEAK_TFLOPS * 1e12)
     t = launch_ms_total * 1e-3
     hbm = t_hbm >= t_mfma
-    rec = {
+    n = max(1, len(shapes))
+    return {
         "bound": "hbm" if hbm else "mfma",
         "achieved": round(byts / t / 1e9 if hbm else flops / t / 1e12, 1),
         "peak": HBM_PEAK_GBS if hbm else BF16_PEAK_TFLOPS,
         "unit": "GB/s" if hbm else "TFLOP/s",
         "frac": round(max(t_hbm, t_mfma) / t, 4),
-        "launches": len(sizes),
-        "queries_per_launch": sorted(set(sizes)),
-        "avg_launch_ms": round(launch_ms_total / max(1, len(sizes)), 4),
-        "alg_bytes_per_launch": int(byts // max(1, len(sizes))),
-        "alg_flops_per_launch": int(flops // max(1, len(sizes))),
+        "launches": len(shapes),
+        "launch_shapes": sorted(set(shapes)),
+        "avg_launch_ms": round(launch_ms_total / n, 4),
+        "alg_bytes_per_launch": int(byts // n),
+        "alg_flops_per_launch": int(flops // n),
     }
-    return rec
 
 
-def search_record(args, world, grouped, group_queries, kc, elapsed_s, launch_ms_total, launches, traffic):
-    """The headline JSON record of the search leg (rank 0)."""
+def search_record(args, world, grouped, group_queries, kc, elapsed_s, launch_ms_total, launches, traffic,
+                  chunks=None):
+    """The headline JSON record of the search leg (rank 0).  ``chunks``: the row ranges of a one-GPU
+    group filter (search.group_chunks)."""
     d, k, qb = args.dim, args.k, args.qb
-    sizes = launch_queries(args.steps, qb, grouped, group_queries)
-    rf = scan_roofline(args.n_corpus, world, d, k, kc, sizes, grouped, launch_ms_total)
+    per = -(-args.n_corpus // world)
+    shapes = launch_shapes(args.steps, qb, grouped, group_queries, per, chunks if world == 1 else None)
+    rf = scan_roofline(d, k, kc, shapes, grouped, launch_ms_total)
     rf = {"kernel": "ip_scan16r_kernel<%d> (csrc/search.hip)" % d, **rf}
-    if launches != len(sizes):
+    if launches != len(shapes):
         rf["launches_counted"] = launches   # the profiler's count (differs only if a batch was redone)
-    # PMC traffic: recorded for the per-batch configuration (tools/pmc_traffic.py)
-    tb, tsrc = traffic if not grouped else (None, None)
+    # PMC traffic (tools/pmc_traffic.py) of this configuration's dominant launch shape
+    tb, tsrc = traffic
     rf["traffic"] = tb
     rf["traffic_source"] = tsrc
     if world == 1:
         path = ("FlatIPIndex.search_batches (certified, pipelined; " +
-                (f"grouped: one sample launch, one filter launch over all {group_queries} queries of a group "
-                 "(16 query blocks sharing each corpus tile through L2) and one merge per group)" if grouped else
+                (f"grouped: one sample launch, the filter over all {group_queries} queries of a group (16 query "
+                 f"blocks sharing each corpus tile through L2) as {len(chunks or [0])} launch(es) over row chunks "
+                 "of <= search.GROUP_CHUNK_ROWS rows, one merge of the chunks' lists per group)" if grouped else
                  "per batch: sample scan + k-th selection, one filter launch, select, canonical-order stage)"))
     else:
         path = (f"ShardedFlatIP.search_batches ({args.protocol}, certified, pipelined; " +
@@ -446,7 +456,6 @@ def main():
     elif args.group_queries > 0:
         srch.GROUP_QUERIES = args.group_queries
         srch.GROUP_MIN_ROWS = 0                 # one-GPU: grouped path too, at any shard size
-        srch.GROUP_MAX_ROWS = 1 << 62
     # the product path: the same index objects and certified, pipelined batch search that
     # BaseFaissIPRetriever.batch_search / Trainer.evaluate use (search.py); every query
     # certified exact inside the timed region (an uncertified one is rescanned there)
@@ -521,8 +530,10 @@ def main():
 
     out = None
     if rank == 0:
+        chunks = srch.group_chunks(n_local)
+        shape = (srch.GROUP_QUERIES, max(b - a for a, b in chunks) if world == 1 else n_local) if grouped else None
         out = search_record(args, world, grouped, srch.GROUP_QUERIES, kernels.refine_width(k), el,
-                            scan_ms_total, launches, pmc_traffic(args, world))
+                            scan_ms_total, launches, pmc_traffic(args, world, shape), chunks=chunks)
         if sub is not None:
             out["per_batch_qb%d" % qb] = sub
         out["order"] = ("canonical: exact-score re-rank of each query's near-tie window (fp64 sums of the bf16 "

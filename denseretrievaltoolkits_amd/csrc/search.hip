@@ -245,46 +245,60 @@ struct LeanTile {
     }
   }
   // `base` = the tile's first row (the caller advances it by a constant per tile); `partial` = this is
-  // the shard's last tile and it is short
+  // the shard's last tile and it is short.  NT: non-temporal loads (a tile is read by one work-group:
+  // a single-block launch); a grouped launch's blocks share each tile through L2 and load it plainly.
+  template <bool NT>
   __device__ __forceinline__ void issue(const ScanArgs& a, uint32_t slot_lds, const char* base, bool partial,
                                         int64_t tile, int wave, int lane) {
     if (partial) {
-      issue_tile16<D, NW, true>(a, slot_lds, tile, wave, lane);
+      issue_tile16<D, NW, NT>(a, slot_lds, tile, wave, lane);
       return;
     }
+#define DRT_LEAN3(POL)                                                                                   \
+  {                                                                                                     \
+    uint32_t keep;                                                                                      \
+    asm volatile(                                                                                       \
+        "s_mov_b32 %0, m0\n\t"                                                                          \
+        "s_mov_b32 m0, %2\n\t"                                                                          \
+        "s_nop 0\n\t"                                                                                   \
+        "global_load_lds_dwordx4 %3, %1" POL "\n\t"                                                     \
+        "s_mov_b32 m0, %4\n\t"                                                                          \
+        "s_nop 0\n\t"                                                                                   \
+        "global_load_lds_dwordx4 %5, %1" POL "\n\t"                                                     \
+        "s_mov_b32 m0, %6\n\t"                                                                          \
+        "s_nop 0\n\t"                                                                                   \
+        "global_load_lds_dwordx4 %7, %1" POL "\n\t"                                                     \
+        "s_mov_b32 m0, %0"                                                                              \
+        : "=&s"(keep)                                                                                   \
+        : "s"(base), "s"(slot_lds + loff[0]), "v"(voff[0]), "s"(slot_lds + loff[1]), "v"(voff[1]),      \
+          "s"(slot_lds + loff[2]), "v"(voff[2])                                                         \
+        : "memory");                                                                                    \
+  }
+#define DRT_LEAN1(POL, J)                                                                                \
+  {                                                                                                     \
+    uint32_t keep;                                                                                      \
+    asm volatile(                                                                                       \
+        "s_mov_b32 %0, m0\n\t"                                                                          \
+        "s_mov_b32 m0, %2\n\t"                                                                          \
+        "s_nop 0\n\t"                                                                                   \
+        "global_load_lds_dwordx4 %3, %1" POL "\n\t"                                                     \
+        "s_mov_b32 m0, %0"                                                                              \
+        : "=&s"(keep)                                                                                   \
+        : "s"(base), "s"(slot_lds + loff[J]), "v"(voff[J])                                              \
+        : "memory");                                                                                    \
+  }
     if constexpr (G == 3) {
-      uint32_t keep;
-      asm volatile(
-          "s_mov_b32 %0, m0\n\t"
-          "s_mov_b32 m0, %2\n\t"
-          "s_nop 0\n\t"
-          "global_load_lds_dwordx4 %3, %1 nt\n\t"
-          "s_mov_b32 m0, %4\n\t"
-          "s_nop 0\n\t"
-          "global_load_lds_dwordx4 %5, %1 nt\n\t"
-          "s_mov_b32 m0, %6\n\t"
-          "s_nop 0\n\t"
-          "global_load_lds_dwordx4 %7, %1 nt\n\t"
-          "s_mov_b32 m0, %0"
-          : "=&s"(keep)
-          : "s"(base), "s"(slot_lds + loff[0]), "v"(voff[0]), "s"(slot_lds + loff[1]), "v"(voff[1]),
-            "s"(slot_lds + loff[2]), "v"(voff[2])
-          : "memory");
+      if constexpr (NT) DRT_LEAN3(" nt")
+      else DRT_LEAN3("")
     } else {
 #pragma unroll
       for (int j = 0; j < G; ++j) {
-        uint32_t keep;
-        asm volatile(
-            "s_mov_b32 %0, m0\n\t"
-            "s_mov_b32 m0, %2\n\t"
-            "s_nop 0\n\t"
-            "global_load_lds_dwordx4 %3, %1 nt\n\t"
-            "s_mov_b32 m0, %0"
-            : "=&s"(keep)
-            : "s"(base), "s"(slot_lds + loff[j]), "v"(voff[j])
-            : "memory");
+        if constexpr (NT) DRT_LEAN1(" nt", j)
+        else DRT_LEAN1("", j)
       }
     }
+#undef DRT_LEAN3
+#undef DRT_LEAN1
   }
 };
 
@@ -542,7 +556,7 @@ __device__ __forceinline__ void wave_flush_hits(const ScanArgs& a, int64_t qw, c
   }
 }
 
-template <int D>
+template <int D, bool NT = true>
 __global__ __launch_bounds__(512, 1) void ip_scan16r_kernel(ScanArgs a) {
   constexpr int NW = 8;
   using C = Scan16Cfg<D, NW>;
@@ -601,7 +615,7 @@ __global__ __launch_bounds__(512, 1) void ip_scan16r_kernel(ScanArgs a) {
   for (int p = 0; p < PD; ++p) {
     if (p < my_tiles) {
       const int tile = t0 + p * tstep;
-      lt.issue(a, ring + p * C::TILE_BYTES, next_base, tile == partial_tile, tile, wave, lane);
+      lt.template issue<NT>(a, ring + p * C::TILE_BYTES, next_base, tile == partial_tile, tile, wave, lane);
       next_base += tile_stride;
     }
   }
@@ -702,7 +716,7 @@ __global__ __launch_bounds__(512, 1) void ip_scan16r_kernel(ScanArgs a) {
     lds_barrier();   // tile it+1 landed (every wave's share); slot(it) fully read
     if (it + PD < my_tiles) {
       const int ntile = tile + PD * tstep;
-      lt.issue(a, ring + buf * C::TILE_BYTES, next_base, ntile == partial_tile, ntile, wave, lane);
+      lt.template issue<NT>(a, ring + buf * C::TILE_BYTES, next_base, ntile == partial_tile, ntile, wave, lane);
       next_base += tile_stride;
     }
     const int nslot = buf + 1 == C::NBUF ? 0 : buf + 1;
@@ -2745,9 +2759,9 @@ struct TopkPlan {
 static size_t align_up(size_t x, size_t a) { return (x + a - 1) / a * a; }
 
 // Candidates the canonical-order stage selects per query: k plus a window for the entries within
-// 2 eps of the k-th score (a few on Gaussian data, ~120 on the C2 leg's untrained-tower embeddings at
-// k = 1000; up to 2048 in all).  A wider window goes to the wide resolve.
-static int64_t refine_width(int64_t k) { return std::min<int64_t>(kSelMaxK, k + std::max<int64_t>(512, k / 2)); }
+// 2 eps of the k-th score (a few on Gaussian data, <= 120 on the C2 leg's untrained-tower embeddings
+// at k = 1000, tools/c2_window_probe.py; up to 2048 in all).  A wider window goes to the wide resolve.
+static int64_t refine_width(int64_t k) { return std::min<int64_t>(kSelMaxK, k + std::max<int64_t>(256, k / 4)); }
 
 static size_t plan_refine_tail(TopkPlan& p, size_t o) {
   p.kc = refine_width(p.k);
@@ -2912,7 +2926,9 @@ static int launch_scan_d(const ScanArgs& a, int mode, hipStream_t s) {
       if (dense_hits) hipLaunchKernelGGL((ip_scan16_kernel<D, SCAN_FILTER, 8, true>), grid, dim3(512), 0, s, a);
       else hipLaunchKernelGGL((ip_scan16_kernel<D, SCAN_FILTER, 8, false>), grid, dim3(512), 0, s, a);
     } else {
-      hipLaunchKernelGGL((ip_scan16r_kernel<D>), grid, dim3(512), 0, s, a);
+      // non-temporal corpus loads for a single block; a group's blocks share each tile through L2
+      if (gy > 1) hipLaunchKernelGGL((ip_scan16r_kernel<D, false>), grid, dim3(512), 0, s, a);
+      else hipLaunchKernelGGL((ip_scan16r_kernel<D, true>), grid, dim3(512), 0, s, a);
     }
   } else {
     hipLaunchKernelGGL((ip_scan16_kernel<D, SCAN_DENSE>), grid, dim3(512), 0, s, a);

@@ -159,7 +159,9 @@ class RowAnswerMatcher:
         self.n_slots = 0
         self.version = 0
         self.n_filled = 0        # rows of [0, n_rows) that have a slot (fill's fast exit when all do)
-        self.slot_version = 0    # bumped whenever ``slot`` changes (the device mirror re-uploads it)
+        self.slot_version = 0    # bumped whenever ``slot`` changes
+        self.slot_epoch = 0      # bumped when ``slot`` is reallocated or rebased (a mirror re-uploads it whole)
+        self.slot_log = []       # (rows, slots) assigned by each fill since: a mirror applies only these
 
     @property
     def seen(self) -> np.ndarray:
@@ -177,6 +179,8 @@ class RowAnswerMatcher:
             sl[: self.n_rows] = self.slot
             self.slot, self.n_rows = sl, int(n_rows)
             self.slot_version += 1
+            self.slot_epoch += 1
+            self.slot_log = []
 
     def rebase(self, offset: int, n_local: int, n_total: int):
         """Move rows [0, n_local) (a shard tokenised by local row) to [offset, offset + n_local) of
@@ -186,6 +190,8 @@ class RowAnswerMatcher:
         self.slot, self.n_rows = sl, int(n_total)
         self.n_filled = int((sl >= 0).sum())
         self.slot_version += 1
+        self.slot_epoch += 1
+        self.slot_log = []
 
     def _reserve(self, n_slots: int, width: int):
         cap, w = self.tok.shape[0], self.width
@@ -220,6 +226,7 @@ class RowAnswerMatcher:
             self.n_slots = s0 + int(miss.size)
             self.n_filled += int(miss.size)
             self.slot_version += 1
+            self.slot_log.append((miss, s0))
         return int(miss.size)
 
     def _answer_ids(self, answers_i):
@@ -291,14 +298,16 @@ class DeviceRowMatcher:
         self._version = None
         self._slots = 0
         self.slot_dev = None
-        self._slot_version = None
+        self._slot_epoch = None
+        self._log_i = 0
         # high priority: a stream of its own hardware-queue class, so a batch's comparison kernels never
         # queue behind the query tower pass the host enqueued on the compute stream meanwhile
         self.stream = torch.cuda.Stream(self.device, priority=-1)
 
     def _upload(self):
-        """Mirror the host slots: whole after a reallocation (version change), else only the slots
-        tokenised since the last upload."""
+        """Mirror the host token matrix and row -> slot table: whole after a reallocation (version /
+        epoch change), else only what the fills since the last upload added (new token slots; the
+        newly assigned rows' slots scattered into the device table, not an O(rows) re-upload)."""
         import torch
         h = self.h
         with torch.cuda.stream(self.stream):
@@ -308,9 +317,18 @@ class DeviceRowMatcher:
             elif h.n_slots > self._slots:
                 a, b = self._slots, h.n_slots
                 self.tok[a:b] = torch.from_numpy(np.ascontiguousarray(h.tok[a:b])).to(self.device)
-            if h.slot_version != self._slot_version or self.slot_dev is None:
+            if h.slot_epoch != self._slot_epoch or self.slot_dev is None:
                 self.slot_dev = torch.from_numpy(np.ascontiguousarray(h.slot)).to(self.device)
-                self._slot_version = h.slot_version
+                self._slot_epoch = h.slot_epoch
+                self._log_i = len(h.slot_log)
+            elif self._log_i < len(h.slot_log):
+                new = h.slot_log[self._log_i:]
+                rows = np.concatenate([r for r, _ in new])
+                slots = np.concatenate([np.arange(s0, s0 + r.size, dtype=np.int64) for r, s0 in new])
+                rd = torch.from_numpy(rows.astype(np.int64)).pin_memory().to(self.device, non_blocking=True)
+                sd = torch.from_numpy(slots).pin_memory().to(self.device, non_blocking=True)
+                self.slot_dev.index_copy_(0, rd, sd)
+                self._log_i = len(h.slot_log)
         self._slots = h.n_slots
 
     def match_rows(self, rows: np.ndarray, text_of, answers) -> np.ndarray:

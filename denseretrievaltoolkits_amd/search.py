@@ -113,12 +113,24 @@ GROUP_QUERIES = 2048
 # blocks then ran one after another and the back-to-back filter scans measured 2-3 % slower,
 # profiles/r02j_bench_*.json; across GPUs the group also saves two collectives per batch)
 GROUP_MIN_ROWS = 500_000
-# ... and up to this many (round 4): a group's filter launch runs its 16 query blocks side by side on
-# each XCD (csrc/search.hip launch_scan_d) and a tile is fetched once for all of them while they stay
-# within the XCD's L2 of each other -- 1M rows: 0.30-0.33 vs 0.42 ms per 128-query batch (same ids,
-# profiles/r04be_ab1m.log); over a 10M shard they drift apart and the per-batch path stays
-# (profiles/r04bc_trace_grouped_1gpu.txt).  Several GPUs: ShardedFlatIP groups at any size.
-GROUP_MAX_ROWS = 2_500_000
+# A group's filter launch runs its 16 query blocks side by side on each XCD (csrc/search.hip
+# launch_scan_d) and a corpus tile is fetched from HBM once for all of them while they stay within the
+# XCD's 4 MB L2 of each other.  Over a long shard they drift apart (10M rows: 2.13-2.33 ms per batch, no
+# better than 16 per-batch launches), so a one-GPU index runs the group's filter as one launch per row
+# chunk of at most this many rows, each chunk's packed lists a part of the merge like the shards of a
+# sharded index (round 5: 10M rows 1.90 vs 2.13 ms per batch, tools/group_chunk_probe.py,
+# profiles/r05g/; 1.25M rows is also the W = 8 shard).
+GROUP_CHUNK_ROWS = 1_250_000
+
+
+def group_chunks(nrows: int, chunk_rows: int = None):
+    """Row ranges [(a, b)] of a one-GPU group filter: balanced chunks of <= chunk_rows rows."""
+    chunk_rows = GROUP_CHUNK_ROWS if chunk_rows is None else chunk_rows
+    if chunk_rows <= 0 or nrows <= chunk_rows:
+        return [(0, nrows)]
+    nch = -(-nrows // chunk_rows)
+    per = -(-nrows // nch)
+    return [(a, min(nrows, a + per)) for a in range(0, nrows, per)]
 
 
 def _groups(batches, cap=None):
@@ -135,7 +147,7 @@ def _groups(batches, cap=None):
 
 
 def _gtau_enqueue_group(local, qs, k: int, n_global: int, offset: int, gather, to_host: bool = False,
-                        stats=None, all_reduce_sum=None, id_shift: int = 0):
+                        stats=None, all_reduce_sum=None, id_shift: int = 0, chunks=None):
     """One group of query batches through the global-threshold protocol (see ShardedFlatIP):
     ONE sample launch for all of the group's queries, one exchange of the sample lists, one
     threshold launch, one filter scan (+ select) per batch writing its packed top-k into a group buffer,
@@ -145,18 +157,28 @@ def _gtau_enqueue_group(local, qs, k: int, n_global: int, offset: int, gather, t
     the shards keep kc = refine_width(k) candidates each, the merge keeps kc, and the canonical
     stage (kernels.refine, deltas summed across shards by ``all_reduce_sum``) orders the top-k.
     ``id_shift`` is added to every returned id (a one-GPU index searched with an id offset: the
-    protocol itself runs on the index's own row numbers, packed in 32 bits)."""
+    protocol itself runs on the index's own row numbers, packed in 32 bits).  ``chunks`` (one GPU:
+    ``gather`` is the identity stack): the filter runs as one launch per row range (group_chunks),
+    whose packed lists are merged as parts."""
     sizes = [q.shape[0] for q in qs]
     qg = qs[0] if len(qs) == 1 else torch.cat(qs)
     best = local.dist_sample(qg, n_global, k)                       # [Qg, r]
     lists = gather(best).contiguous()                               # [world, Qg, r]
     tau = kernels.dist_tau(lists, k)                                # [Qg]: one launch for the group
     kc = kernels.refine_width(k) if stats is not None else k
-    packed = torch.empty((qg.shape[0], kc + 1), dtype=torch.int64, device=qg.device)
-    # ONE filter launch for the whole group (grid: corpus tiles x 128-query blocks; every block still
-    # streams the shard once) and one select over all of its queries
-    kernels.dist_filter_into(qg, local.rows, n_global, kc, offset, tau, packed)
-    s, i, st = kernels.merge_packed(gather(packed), kc, n_global, k_cert=k)
+    if chunks is not None and len(chunks) > 1:
+        # one GPU, long shard: one filter launch per row chunk (the group's query blocks stay in step
+        # over a chunk, so its tiles are read from HBM once), the chunks' lists merged as parts
+        parts = torch.empty((len(chunks), qg.shape[0], kc + 1), dtype=torch.int64, device=qg.device)
+        for c, (a, b) in enumerate(chunks):
+            kernels.dist_filter_into(qg, local.rows[a:b], n_global, kc, offset + a, tau, parts[c])
+        s, i, st = kernels.merge_packed(parts, kc, n_global, k_cert=k)
+    else:
+        packed = torch.empty((qg.shape[0], kc + 1), dtype=torch.int64, device=qg.device)
+        # ONE filter launch for the whole group (grid: corpus tiles x 128-query blocks, the blocks of
+        # a tile co-located per XCD) and one select over all of its queries
+        kernels.dist_filter_into(qg, local.rows, n_global, kc, offset, tau, packed)
+        s, i, st = kernels.merge_packed(gather(packed), kc, n_global, k_cert=k)
     if stats is not None:
         s, i = kernels.refine(qg, local.rows, offset, s, i, k, stats, tau, st, all_reduce_sum)
     if id_shift:
@@ -353,7 +375,7 @@ class FlatIPIndex:
 
     def _use_groups(self) -> bool:
         # the grouped path packs row numbers into 32 bits (an id offset is added afterwards)
-        return GROUP_MIN_ROWS <= self.ntotal <= GROUP_MAX_ROWS and self.ntotal < 0xFFFFFFFF
+        return GROUP_MIN_ROWS <= self.ntotal < 0xFFFFFFFF
 
     def enqueue_batches(self, batches, k: int, id_offset: int = 0, to_host: bool = False) -> list:
         """Every batch's search enqueued now (in groups where ``search_batches`` would group them);
@@ -364,7 +386,8 @@ class FlatIPIndex:
         stats = self._stats_arg()
         for g in _groups(list(batches)):
             gp = _GroupPend(_gtau_enqueue_group(self, [self._queries(q) for q in g], k, self.ntotal, 0,
-                                                lambda t: t.unsqueeze(0), to_host, stats=stats, id_shift=id_offset),
+                                                lambda t: t.unsqueeze(0), to_host, stats=stats, id_shift=id_offset,
+                                                chunks=group_chunks(self.ntotal)),
                             k, id_offset)
             out += [_GroupMember(gp, j) for j in range(len(g))]
         return out
@@ -407,9 +430,11 @@ class FlatIPIndex:
             return res
 
         stats = self._stats_arg()
+        chunks = group_chunks(self.ntotal)
         for res in _pipeline(groups, lambda j, g: _gtau_enqueue_group(self, g, k, self.ntotal, 0,
                                                                       lambda t: t.unsqueeze(0), to_host,
-                                                                      stats=stats, id_shift=id_offset), fin):
+                                                                      stats=stats, id_shift=id_offset,
+                                                                      chunks=chunks), fin):
             yield from res
 
     def search(self, q, k: int) -> Tuple[np.ndarray, np.ndarray]:

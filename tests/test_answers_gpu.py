@@ -26,6 +26,9 @@ def test_device_matcher_equals_host_random(dev, max_words):
     ref_m = RowAnswerMatcher(0)
     ref_m.ensure_rows(500)
     for it in range(40):
+        if it == 20:   # the row table grows mid-way: the mirror re-uploads it once, then scatters again
+            host.ensure_rows(900)
+            ref_m.ensure_rows(900)
         B, k = int(rng.integers(1, 9)), int(rng.integers(1, 60))
         rows = rng.integers(-1, 500, size=(B, k))
         ans = [[" ".join(rng.choice(vocab + ["zzz"], size=int(rng.integers(0, 5))))
@@ -36,6 +39,8 @@ def test_device_matcher_equals_host_random(dev, max_words):
         if it % 10 == 0:
             ref = [[int(has_answers(docs[r], ans[i])) if r >= 0 else 0 for r in rows[i]] for i in range(B)]
             assert got.tolist() == ref
+    # the device row -> slot table was kept in step by scatters of each fill's new rows
+    assert np.array_equal(dm.slot_dev.cpu().numpy(), host.slot)
 
 
 def test_device_matcher_reference_golden(dev):

@@ -15,20 +15,31 @@ def _args(n, steps=20):
     return SimpleNamespace(n_corpus=n, dim=768, k=1000, qb=128, steps=steps, warmup=3, protocol="global_tau")
 
 
-def _rec(n, world, grouped, launch_ms, steps=20, group=2048):
+KC = 1256
+
+
+def _rec(n, world, grouped, launch_ms, steps=20, group=2048, chunks=None):
     import bench
     a = _args(n, steps)
-    sizes = bench.launch_queries(steps, 128, grouped, group)
-    return bench.search_record(a, world, grouped, group, 1512, steps * 2.7e-3, launch_ms * len(sizes), len(sizes),
-                               (15_385_000_000, "r04aw_pmc_traffic.json"))
+    per = -(-n // world)
+    shapes = bench.launch_shapes(steps, 128, grouped, group, per, chunks if world == 1 else None)
+    traffic = (None, None) if grouped else (15_385_000_000, "r04aw_pmc_traffic.json")
+    return bench.search_record(a, world, grouped, group, KC, steps * 2.7e-3, launch_ms * len(shapes), len(shapes),
+                               traffic, chunks=chunks)
 
 
-def test_launch_queries_groups_batches_like_search():
+def test_launch_shapes_group_batches_and_chunks_like_search():
     import bench
-    assert bench.launch_queries(20, 128, False, 2048) == [128] * 20
-    assert bench.launch_queries(20, 128, True, 2048) == [2048, 512]
-    assert bench.launch_queries(16, 128, True, 2048) == [2048]
-    assert bench.launch_queries(3, 128, True, 128) == [128] * 3
+    from denseretrievaltoolkits_amd import search as srch
+    assert bench.launch_shapes(20, 128, False, 2048, 10_000_000) == [(128, 10_000_000)] * 20
+    assert bench.launch_shapes(20, 128, True, 2048, 1_000_000) == [(2048, 1_000_000), (512, 1_000_000)]
+    assert bench.launch_shapes(16, 128, True, 2048, 5) == [(2048, 5)]
+    assert bench.launch_shapes(3, 128, True, 128, 7) == [(128, 7)] * 3
+    ch = srch.group_chunks(10_000_000)
+    assert len(ch) == 8 and ch[0] == (0, 1_250_000) and ch[-1][1] == 10_000_000
+    assert bench.launch_shapes(16, 128, True, 2048, 10_000_000, ch) == [(2048, 1_250_000)] * 8
+    assert srch.group_chunks(1_000_000) == [(0, 1_000_000)]
+    assert [b - a for a, b in srch.group_chunks(2_600_000)] == [866_667, 866_667, 866_666]
 
 
 def test_world1_10m_per_batch_is_hbm_bound_with_survey_bytes():
@@ -36,6 +47,7 @@ def test_world1_10m_per_batch_is_hbm_bound_with_survey_bytes():
     rf = r["roofline"]
     assert rf["bound"] == "hbm" and rf["unit"] == "GB/s"
     assert rf["alg_bytes_per_launch"] == 10_000_000 * 768 * 2 + 128 * 768 * 2 + 128 * 1000 * 12
+    assert rf["launch_shapes"] == [(128, 10_000_000)]
     assert 0.78 <= rf["frac"] <= 0.80 and rf["frac"] <= 1.0
     assert rf["traffic"] == 15_385_000_000
     assert "per batch" in r["config"]["workload"] and "per batch" in r["config"]["path"]
@@ -51,6 +63,16 @@ def test_world1_1m_grouped_is_mfma_side():
     assert "groups of 2048" in r["config"]["workload"] and r["config"]["queries_per_filter_launch"] == 2048
 
 
+def test_world1_10m_grouped_chunks_are_priced_per_chunk_launch():
+    from denseretrievaltoolkits_amd import search as srch
+    ch = srch.group_chunks(10_000_000)
+    r = _rec(10_000_000, 1, True, 3.8, steps=16, chunks=ch)
+    rf = r["roofline"]
+    assert rf["launches"] == 8 and rf["launch_shapes"] == [(2048, 1_250_000)]
+    assert rf["bound"] == "mfma" and abs(rf["frac"] - 2 * 2048 * 1_250_000 * 768 / 2.5e15 / 3.8e-3) < 1e-3
+    assert "8 launch(es) over row chunks" in r["config"]["path"]
+
+
 @pytest.mark.parametrize("grouped,launch_ms,bound", [(True, 3.9, "mfma"), (False, 0.30, "hbm")])
 def test_world8_prices_the_launch_it_ran(grouped, launch_ms, bound):
     r = _rec(10_000_000, 8, grouped, launch_ms * (1 if not grouped else 1), steps=16, group=2048 if grouped else 128)
@@ -61,5 +83,5 @@ def test_world8_prices_the_launch_it_ran(grouped, launch_ms, bound):
         assert abs(rf["frac"] - 2 * 2048 * per * 768 / 2.5e15 / 3.9e-3) < 1e-3
         assert "ShardedFlatIP" in r["config"]["path"] and "groups of 2048" in r["config"]["workload"]
     else:
-        t_hbm = (per * 768 * 2 + 128 * 768 * 2 + 128 * 1513 * 8) / 8e12
+        t_hbm = (per * 768 * 2 + 128 * 768 * 2 + 128 * (KC + 1) * 8) / 8e12
         assert abs(rf["frac"] - t_hbm / 0.30e-3) < 1e-3

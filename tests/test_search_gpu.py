@@ -85,14 +85,16 @@ def test_filter_scan_flavours_bit_exact(dev, nq, n, d, k):
 
 
 @pytest.mark.gpu
-def test_flat_index_enqueue_batches_grouped(dev, monkeypatch):
+@pytest.mark.parametrize("chunk", [0, 50_000])
+def test_flat_index_enqueue_batches_grouped(dev, monkeypatch, chunk):
     """enqueue_batches / finish_batch (Trainer.evaluate's eager window path) on a shard inside the
     grouped range: batches enqueued in groups, collected per batch in any order, host-staged ids equal
-    to the oracle's."""
+    to the oracle's -- with the group filter as one launch and as one launch per row chunk."""
     import torch
     from denseretrievaltoolkits_amd import search as srch
     monkeypatch.setattr(srch, "GROUP_MIN_ROWS", 0)
     monkeypatch.setattr(srch, "GROUP_QUERIES", 64)
+    monkeypatch.setattr(srch, "GROUP_CHUNK_ROWS", chunk)
     rng = np.random.default_rng(78)
     q, p, k = int_bf16(rng, (150, 768), -4, 4), int_bf16(rng, (120001, 768), -4, 4), 1000
     es, ei = orc.ip_topk(q, p, k)
@@ -108,15 +110,18 @@ def test_flat_index_enqueue_batches_grouped(dev, monkeypatch):
         np.testing.assert_array_equal(np.asarray(s), es[a:b])
 
 
-@pytest.mark.parametrize("case", ["int", "gauss", "ties"])
-def test_flat_index_search_batches_grouped(dev, case, monkeypatch):
-    """FlatIPIndex.search_batches in groups (one sample launch + one merge per group, one filter
-    scan per batch): ragged batches over several groups vs the oracle; the all-ties corpus makes
-    every batch uncertified, so each is redone by the exact per-batch path."""
+@pytest.mark.parametrize("case,chunk", [("int", 0), ("gauss", 0), ("ties", 0), ("int", 37_000), ("gauss", 45_000),
+                                        ("ties", 20_000)])
+def test_flat_index_search_batches_grouped(dev, case, chunk, monkeypatch):
+    """FlatIPIndex.search_batches in groups (one sample launch + one merge per group, the group's
+    filter as one launch or, on a long shard, one launch per row chunk whose lists are merged as
+    parts): ragged batches over several groups vs the oracle; the all-ties corpus makes every batch
+    uncertified, so each is redone by the exact per-batch path."""
     import torch
     from denseretrievaltoolkits_amd import search as srch
     monkeypatch.setattr(srch, "GROUP_MIN_ROWS", 0)
     monkeypatch.setattr(srch, "GROUP_QUERIES", 64)
+    monkeypatch.setattr(srch, "GROUP_CHUNK_ROWS", chunk)
     rng = np.random.default_rng(77)
     if case == "int":
         q, p, k = int_bf16(rng, (150, 768), -4, 4), int_bf16(rng, (120001, 768), -4, 4), 1000

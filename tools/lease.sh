@@ -12,7 +12,8 @@
 #   prof_bench   rocprofv3 --kernel-trace --stats of the search-only bench
 #   prof_c2      rocprofv3 kernel trace of search_batches over 1M rows (C2 shard size) + trace tail
 #   prof_sim8    rocprofv3 kernel trace of the simulated W = 8 per-rank step + trace tail
-#   pmc_scan     HBM traffic of the filter scan (FETCH_SIZE / WRITE_SIZE passes)
+#   pmc_scan     HBM traffic of the filter scan (FETCH_SIZE / WRITE_SIZE passes); PMC_BENCH_ARGS (bench.py
+#                steps / path), PMC_SHAPE_ARGS (pmc_traffic.py --launch-queries Q --launch-rows R: a grouped launch)
 #   cmd          run "$CMD" (a python tool invocation) under a 600 s limit
 set -u
 R=$(cd "$(dirname "$0")/.." && pwd)
@@ -56,17 +57,19 @@ for s in "$@"; do
              --no-encode ${BENCH_ARGS:-} || exit $? ;;
     bench_gloo2) DRT_BENCH_BACKEND=gloo step bench_gloo2 600 python3 -u bench.py --gpus 2 --n-corpus 2000000 \
              --steps 8 --warmup 2 --no-cpu-baseline ${BENCH_ARGS:-} || exit $? ;;
-    prof_bench) prof prof_bench 600 $R/bench.py --steps 20 --warmup 3 --no-cpu-baseline --no-evaluate --no-encode || exit $? ;;
+    prof_bench) prof prof_bench 600 $R/bench.py --steps ${STEPS:-20} --warmup 3 --no-cpu-baseline --no-evaluate --no-encode \
+                  ${BENCH_ARGS:-} || exit $? ;;
     prof_c2) LAST=${LAST:-800} prof prof_c2 600 $R/tools/search_ab.py --n 1000000 --steps 78 --rounds 2 \
              --groups ${GROUPS_AB:-0,2048} || exit $? ;;
     prof_sim8) prof prof_sim8 600 $R/tools/sim_dist.py --world 8 --steps 20 || exit $? ;;
     pmc_scan) for C in FETCH_SIZE WRITE_SIZE; do
                 ( cd /tmp && timeout -s KILL 300 rocprofv3 --pmc $C --output-format csv -d $OUT/${TAG}_pmc_$C -o run \
-                    -- python3 $R/bench.py --steps 3 --warmup 1 --no-cpu-baseline --no-encode > $OUT/${TAG}_pmc_$C.log 2>&1 )
+                    -- python3 $R/bench.py ${PMC_BENCH_ARGS:---steps 3 --warmup 1} --no-cpu-baseline --no-encode \
+                    > $OUT/${TAG}_pmc_$C.log 2>&1 )
                 rc=$?; echo "=== $TAG pmc $C rc=$rc" | tee -a $OUT/session.log; [ $rc -ne 0 ] && exit $rc
               done
               python3 $R/tools/pmc_traffic.py $OUT/${TAG}_pmc_FETCH_SIZE $OUT/${TAG}_pmc_WRITE_SIZE \
-                $OUT/${TAG}_pmc_traffic.json --n-corpus ${NCORPUS:-10000000} || exit $? ;;
+                $OUT/${TAG}_pmc_traffic.json --n-corpus ${NCORPUS:-10000000} ${PMC_SHAPE_ARGS:-} || exit $? ;;
     cmd) step cmd 600 ${CMD} || exit $? ;;
     *) echo "unknown step $s"; exit 2 ;;
   esac

@@ -33,6 +33,8 @@ def main():
     ap.add_argument("--qb", type=int, default=128)
     ap.add_argument("--k", type=int, default=1000)
     ap.add_argument("--dim", type=int, default=768)
+    ap.add_argument("--launch-queries", type=int, default=0, help="a grouped launch: queries per filter launch")
+    ap.add_argument("--launch-rows", type=int, default=0, help="a grouped launch: rows per filter launch")
     a = ap.parse_args()
     fetch = per_kernel(a.fetch_dir, "FETCH_SIZE")
     write = per_kernel(a.write_dir, "WRITE_SIZE")
@@ -45,7 +47,10 @@ def main():
                          "hbm_bytes_per_launch": 2 * fkb * 1024 + wkb * 1024}
     # the dominant kernel = the one moving the most HBM bytes per launch (the filter scan)
     scan = max(kernels, key=lambda k: kernels[k]["hbm_bytes_per_launch"])
-    out = {"config": {"n_corpus": a.n_corpus, "world": a.world, "qb": a.qb, "k": a.k, "dim": a.dim},
+    cfg = {"n_corpus": a.n_corpus, "world": a.world, "qb": a.qb, "k": a.k, "dim": a.dim}
+    if a.launch_queries:
+        cfg.update(launch_queries=a.launch_queries, launch_rows=a.launch_rows)
+    out = {"config": cfg,
            "dominant_kernel": scan, "traffic_bytes_per_launch": kernels[scan]["hbm_bytes_per_launch"],
            "correction": "HBM bytes = 2 x FETCH_SIZE (gfx950 wide-read tally) + WRITE_SIZE, KB = 1024 B",
            "kernels": kernels}

@@ -41,7 +41,6 @@ def main():
                 srch.GROUP_MIN_ROWS = 1 << 62
             else:
                 srch.GROUP_MIN_ROWS = 0
-                srch.GROUP_MAX_ROWS = 1 << 62
                 srch.GROUP_QUERIES = v
             idx.search_batches(batches[:2], 1000)
             torch.cuda.synchronize()
