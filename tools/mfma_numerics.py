@@ -33,7 +33,7 @@ def from_bf16(u):
     return (u.astype(np.uint32) << 16).view(np.float32)
 
 
-def run(lib, A, B, C):
+def run(lib, A, B, C, fn="mfma_chain"):
     T, S = A.shape[0], A.shape[1]
     dev = torch.device("cuda", 0)
     a = torch.from_numpy(A.view(np.int16).copy()).to(dev)
@@ -41,7 +41,7 @@ def run(lib, A, B, C):
     c = torch.from_numpy(C.astype(np.float32)).to(dev)
     d = torch.empty_like(c)
     s = torch.cuda.current_stream().cuda_stream
-    rc = lib.mfma_chain(ctypes.c_void_p(a.data_ptr()), ctypes.c_void_p(b.data_ptr()), ctypes.c_void_p(c.data_ptr()),
+    rc = getattr(lib, fn)(ctypes.c_void_p(a.data_ptr()), ctypes.c_void_p(b.data_ptr()), ctypes.c_void_p(c.data_ptr()),
                         ctypes.c_void_p(d.data_ptr()), T, S, ctypes.c_void_p(s))
     assert rc == 0, rc
     torch.cuda.synchronize()
@@ -189,6 +189,28 @@ def main():
         x[..., 0] = 64.0 * np.sign(rng.standard_normal(sh[:-1]))
         return x
     out["chain24_cancel"] = chain(lib, rng, 512, 24, adv)
+    # v_mfma_f32_32x32x16_bf16 (the grouped filter scan): 16 products per step
+    def one_step32(gen_ab, gen_c, T=512):
+        A = bf16(gen_ab((T, 1, 32, 16)))
+        B = bf16(gen_ab((T, 1, 32, 16)))
+        C = gen_c((T, 32, 32)).astype(np.float32)
+        D = run(lib, A, B, C, "mfma32_chain")
+        P = products(A, B)[:, 0]
+        ex = C.astype(np.float64) + P.sum(-1)
+        err = np.abs(D.astype(np.float64) - ex)
+        u = 2.0 ** -24
+        return {"exact_rn_match": float((D == ex.astype(np.float32)).mean()),
+                "err_over_u_c_plus_abs": float((err / (u * (np.abs(C) + np.abs(P).sum(-1)) + 1e-300)).max())}
+    out["mm32_gauss_c0"] = one_step32(g, lambda sh: np.zeros(sh))
+    out["mm32_spread_c"] = one_step32(w, lambda sh: 30.0 * rng.standard_normal(sh))
+    out["mm32_pos_one_big"] = one_step32(ps2, lambda sh: np.zeros(sh))
+    out["mm32_dominant_c"] = one_step32(dom, lambda sh: 100.0 * rng.standard_normal(sh))
+    def ones_in_c(j):
+        A = np.full((1, 1, 32, 16), bf16(np.float32(2.0 ** -j))[()], np.uint16)
+        Bm = np.full((1, 1, 32, 16), 0x3F80, np.uint16)
+        D = run(lib, A, Bm, np.ones((1, 32, 32), np.float32), "mfma32_chain")
+        return float((D[0, 0, 0].astype(np.float64) - 1.0) / 2.0 ** -24)
+    out["mm32_align_c_units_2m24"] = {j: ones_in_c(j) for j in (22, 24, 26, 27, 28)}
     print(json.dumps(out, indent=1))
 
 
