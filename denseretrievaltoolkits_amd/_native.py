@@ -54,6 +54,7 @@ _SIGNATURES = [
     ("drt_refine_width", c_i32, [c_i32]),
     ("drt_ip_topk_exact_bf16", c_i32, [c_vp, c_i64, c_vp, c_i64, c_i32, c_i32, c_i64, c_vp, c_vp, c_vp, c_vp, c_vp,
                                        c_sz, c_vp]),
+    ("drt_hit_metrics_i8", c_i32, [c_vp, c_i64, c_i64, c_vp, c_i32, c_vp, c_vp]),
     ("drt_answer_match_i32", c_i32, [c_vp, c_i32, c_vp, c_vp, c_i64, c_i64, c_i64, c_vp, c_vp, c_i32, c_i32, c_vp,
                                      c_vp, c_vp]),
     ("drt_ip_topk_resolve_exact", c_i32, [c_vp, c_i64, c_vp, c_i64, c_i32, c_i32, c_i64, c_vp, c_vp, c_vp, c_vp,

@@ -158,7 +158,8 @@ class RowAnswerMatcher:
         self.tok = np.full((0, self.width), -1, dtype=np.int32)
         self.n_slots = 0
         self.version = 0
-        self.n_filled = 0        # rows of [0, n_rows) that have a slot (fill's fast exit when all do)
+        self.n_filled = 0        # rows of [0, n_valid) that have a slot (fill's fast exit when all do)
+        self.n_valid = self.n_rows   # rows the index really has (n_rows grows geometrically past it)
         self.slot_version = 0    # bumped whenever ``slot`` changes
         self.slot_epoch = 0      # bumped when ``slot`` is reallocated or rebased (a mirror re-uploads it whole)
         self.slot_log = []       # (rows, slots) assigned by each fill since: a mirror applies only these
@@ -173,6 +174,7 @@ class RowAnswerMatcher:
 
     def ensure_rows(self, n_rows: int):
         """Rows [0, n_rows) addressable (geometric growth: called once per corpus batch)."""
+        self.n_valid = max(self.n_valid, int(n_rows))
         if n_rows > self.n_rows:
             n_rows = max(int(n_rows), self.n_rows + self.n_rows // 2)
             sl = np.full(n_rows, -1, dtype=np.int64)
@@ -188,6 +190,7 @@ class RowAnswerMatcher:
         sl = np.full(n_total, -1, dtype=np.int64)
         sl[offset: offset + n_local] = self.slot[:n_local]
         self.slot, self.n_rows = sl, int(n_total)
+        self.n_valid = int(n_total)
         self.n_filled = int((sl >= 0).sum())
         self.slot_version += 1
         self.slot_epoch += 1
@@ -207,7 +210,7 @@ class RowAnswerMatcher:
 
     def fill(self, rows, text_of) -> int:
         """Tokenise every row of ``rows`` not tokenised yet (``text_of(row)`` -> passage text)."""
-        if self.n_filled >= self.n_rows:   # every row tokenised (the corpus prefill): nothing to look up
+        if self.n_filled >= self.n_valid:   # every row tokenised (the corpus prefill): nothing to look up
             return 0
         r = np.asarray(rows).reshape(-1)
         r = r[r >= 0]
@@ -342,8 +345,42 @@ class DeviceRowMatcher:
         B, k = rows.shape
         if B == 0 or k == 0:
             return _PendingMatch(np.zeros((B, k), dtype=np.int8), None)
+        hit = self._enqueue_hits(rows, text_of, answers)
+        if hit is None:   # no row tokenised: every retrieved row is a pad
+            return _PendingMatch(np.zeros((B, k), dtype=np.int8), None)
+        with torch.cuda.stream(self.stream):
+            out = torch.empty((B, k), dtype=torch.int8, pin_memory=True)
+            out.copy_(hit, non_blocking=True)
+            done = torch.cuda.Event()
+            done.record(self.stream)
+        return _PendingMatch(out, done)
+
+    def match_metrics(self, rows, text_of, answers, topk_dev, acc) -> None:
+        """The batch's answer matches AND its get_metrics (DRT/evaluator/metrics.py:4-59) added to the
+        device sums ``acc`` [3 T] fp64 (recall, mrr, ndcg per cut-off of ``topk_dev`` [T] int32) on the
+        matcher's stream -- nothing is read back per batch (drt_hit_metrics_i8).  ``rows``: the
+        retrieved index rows [B, k], host int64 or a device tensor (Trainer.evaluate hands over the
+        search's device ids; the host copy is taken only if some row still needs tokenising)."""
+        import torch
+        B, k = rows.shape
+        if B == 0:
+            return
+        hit = self._enqueue_hits(rows, text_of, answers)
+        with torch.cuda.stream(self.stream):
+            if hit is None:
+                hit = torch.zeros((B, k), dtype=torch.int8, device=self.device)
+            _native.check(_native.load().drt_hit_metrics_i8(hit.data_ptr(), B, k, topk_dev.data_ptr(),
+                                                             int(topk_dev.numel()), acc.data_ptr(),
+                                                             self.stream.cuda_stream), "drt_hit_metrics_i8")
+
+    def _enqueue_hits(self, rows, text_of, answers):
+        """hit [B, k] int8 on the device (the matcher's stream), or None when no row has tokens."""
+        import torch
+        B, k = rows.shape
         h = self.h
-        h.fill(rows, text_of)
+        on_dev = isinstance(rows, torch.Tensor)
+        if h.n_filled < h.n_valid:   # rows without tokens yet: the host tokenises them first
+            h.fill(rows.cpu().numpy() if on_dev else rows, text_of)
         self._upload()
         W = h.width
         lists, every = [], np.zeros(B, dtype=bool)
@@ -353,32 +390,35 @@ class DeviceRowMatcher:
         A = max(1, max(len(x) for x in lists))
         n_max = max([1] + [len(a) for x in lists for a in x])
         ans = np.full((B, A, n_max), -3, dtype=np.int32)
-        alen = np.zeros((B, A), dtype=np.int64)
+        alen = np.zeros((B, A), dtype=np.int32)
         for i, x in enumerate(lists):
             for a, ids in enumerate(x):
                 ans[i, a, : len(ids)] = ids
                 alen[i, a] = len(ids)
-        if h.n_slots == 0:   # no row tokenised: every retrieved row is a pad
-            return _PendingMatch(np.zeros((B, k), dtype=np.int8), None)
+        if h.n_slots == 0:
+            return None
         lib = _native.load()
+        dev = self.device
+        if on_dev:   # the search's ids: produced on the index's stream, read on the matcher's
+            self.stream.wait_stream(torch.cuda.current_stream(dev))
         with torch.cuda.stream(self.stream):
-            dev = self.device
-            # the retrieved rows go up as they are; the kernel maps row -> token slot on the device
-            r = torch.from_numpy(np.ascontiguousarray(rows, dtype=np.int64)).pin_memory().to(dev, non_blocking=True)
-            at = torch.from_numpy(ans).pin_memory().to(dev, non_blocking=True)
-            lt = torch.from_numpy(alen.astype(np.int32)).pin_memory().to(dev, non_blocking=True)
-            ev = torch.from_numpy(every.astype(np.uint8)).pin_memory().to(dev, non_blocking=True)
+            if on_dev:
+                r = rows.contiguous()
+                r.record_stream(self.stream)
+            else:   # the retrieved rows go up as they are; the kernel maps row -> token slot on the device
+                r = torch.from_numpy(np.ascontiguousarray(rows, dtype=np.int64)).pin_memory().to(dev, non_blocking=True)
+            # answers and flags in one pinned upload
+            meta = np.concatenate([ans.reshape(-1), alen.reshape(-1), every.astype(np.int32)])
+            mt = torch.from_numpy(meta).pin_memory().to(dev, non_blocking=True)
+            at, lt = mt[: ans.size], mt[ans.size: ans.size + alen.size]
+            ev = mt[ans.size + alen.size:].to(torch.uint8)
             hit = torch.empty((B, k), dtype=torch.int8, device=dev)
             # one launch: wave (i, j) scans retrieved row j of query i for every answer of query i
             _native.check(lib.drt_answer_match_i32(self.tok.data_ptr(), W, r.data_ptr(), self.slot_dev.data_ptr(),
                                                    int(self.slot_dev.numel()), B, k, at.data_ptr(), lt.data_ptr(),
                                                    A, n_max, ev.data_ptr(), hit.data_ptr(),
                                                    self.stream.cuda_stream), "drt_answer_match_i32")
-            out = torch.empty((B, k), dtype=torch.int8, pin_memory=True)
-            out.copy_(hit, non_blocking=True)
-            done = torch.cuda.Event()
-            done.record(self.stream)
-        return _PendingMatch(out, done)
+        return hit
 
 
 class _PendingMatch:

@@ -272,7 +272,7 @@ class Trainer:
             data = {kk: (torch.cat([d[kk] for d in datas]) if datas[0][kk] is not None else None) for kk in datas[0]}
         return self._encode(query=data).q_reps
 
-    def _search_rows(self, q_reps: torch.Tensor, k: int):
+    def _search_rows(self, q_reps: torch.Tensor, k: int, to_host: bool = True):
         """Yields (row0, ids [n, k] host) for consecutive row ranges of this rank's query reps.
 
         W = 1: the window's rows in SEARCH_BATCH batches.  W > 1: the corpus is row-sharded, so the
@@ -283,7 +283,7 @@ class Trainer:
         sb = self.SEARCH_BATCH
         if self.world == 1:
             batches = [q_reps[a: a + sb] for a in range(0, q_reps.shape[0], sb)]
-            for j, (_, ids) in enumerate(self.index.local.search_batches_iter(batches, k, to_host=True)):
+            for j, (_, ids) in enumerate(self.index.local.search_batches_iter(batches, k, to_host=to_host)):
                 yield j * sb, ids
             return
         # every rank hands the collective the same dtype (a rank with no queries left sends an
@@ -292,7 +292,7 @@ class Trainer:
         lo = sum(sizes[: self.rank])
         hi = lo + sizes[self.rank]
         batches = [allq[a: a + sb] for a in range(0, allq.shape[0], sb)]
-        for j, (_, ids) in enumerate(self.index.search_batches_iter(batches, k, to_host=True)):
+        for j, (_, ids) in enumerate(self.index.search_batches_iter(batches, k, to_host=to_host)):
             a, b = max(lo, j * sb), min(hi, (j + 1) * sb)
             if a < b:
                 yield a - lo, ids[a - j * sb: b - j * sb]
@@ -304,8 +304,9 @@ class Trainer:
             out[row0: row0 + ids.shape[0]] = ids
         return out
 
-    def _eval_results(self, query_loader, k: int):
-        """Yields (loader batch, ids [B, k] host) in loader order (all ranks call it together)."""
+    def _eval_results(self, query_loader, k: int, to_host: bool = True):
+        """Yields (loader batch, ids [B, k]) in loader order (all ranks call it together); the ids are
+        host arrays, or device tensors with ``to_host`` False (the device answer matcher's input)."""
         windows = self._query_windows(query_loader)
         d = self.index.d
 
@@ -328,17 +329,18 @@ class Trainer:
                 q_reps = torch.empty((0, d), dtype=torch.float32, device=self.device)
                 win = []
             n = q_reps.shape[0]
-            ids_all = np.empty((n, k), dtype=np.int64)
+            ids_all = np.empty((n, k), dtype=np.int64) if to_host else \
+                torch.empty((n, k), dtype=torch.int64, device=self.device)
             done, bi, b0 = 0, 0, 0
             if self.world == 1 and self.EAGER_WINDOW_SEARCH and n:
                 # the whole window's searches first, then the next window's tower pass
                 sb = self.SEARCH_BATCH
                 loc = self.index.local
-                pend = loc.enqueue_batches([q_reps[a: a + sb] for a in range(0, n, sb)], k, to_host=True)
+                pend = loc.enqueue_batches([q_reps[a: a + sb] for a in range(0, n, sb)], k, to_host=to_host)
                 nxt = encode_next()
                 rows_iter = ((j * sb, loc.finish_batch(p_)[1]) for j, p_ in enumerate(pend))
             else:
-                rows_iter = self._search_rows(q_reps, k)
+                rows_iter = self._search_rows(q_reps, k, to_host)
             for row0, ids in rows_iter:
                 if nxt is None:
                     # the next window's tower pass goes on the GPU behind this window's first search
@@ -404,6 +406,14 @@ class Trainer:
         def text_of(row):
             return self._doc_text(self.idx[row])
 
+        # device metrics: the matches and get_metrics of every loader batch stay on the GPU (summed there,
+        # read back once after the last batch) and the search's ids never leave the device -- unless the
+        # retrieve/ output file needs the documents on the host
+        dev_metrics = isinstance(matcher, DeviceRowMatcher) and not rdir
+        if dev_metrics:
+            macc = torch.zeros(3 * len(topk), dtype=torch.float64, device=self.device)
+            topk_dev = torch.tensor(topk, dtype=torch.int32, device=self.device)
+
         def finish(pend):
             # batch j's matches are read (and its metrics taken) after batch j + 1's are enqueued
             batch, indices, match = pend
@@ -422,7 +432,7 @@ class Trainer:
 
         pend = None
         tw = {"results_wait_s": 0.0, "match_issue_s": 0.0, "match_finish_s": 0.0}
-        res_iter = self._eval_results(query_loader, k)
+        res_iter = self._eval_results(query_loader, k, to_host=not dev_metrics)
         while True:
             t0w = time.perf_counter()
             nxt_res = next(res_iter, None)
@@ -431,6 +441,12 @@ class Trainer:
                 break
             batch, indices = nxt_res
             th = time.perf_counter()
+            if dev_metrics:
+                matcher.match_metrics(indices, text_of, batch[2], topk_dev, macc)
+                eval_num += len(indices)
+                t_host += time.perf_counter() - th
+                tw["match_issue_s"] += time.perf_counter() - th
+                continue
             if hasattr(matcher, "match_rows_async"):
                 cur = (batch, indices, matcher.match_rows_async(indices, text_of, batch[2]))
             else:
@@ -447,6 +463,14 @@ class Trainer:
             th = time.perf_counter()
             finish(pend)
             t_host += time.perf_counter() - th
+        if dev_metrics:
+            torch.cuda.current_stream(self.device).wait_stream(matcher.stream)
+            acc = macc.cpu().numpy()
+            T = len(topk)
+            for t, kk in enumerate(topk):
+                m_all[f"Recall@{kk}"] += float(acc[t])
+                m_all[f"MRR@{kk}"] += float(acc[T + t])
+                m_all[f"NDCG@{kk}"] += float(acc[2 * T + t])
         t2 = time.perf_counter()
         if rdir:
             os.makedirs(rdir, exist_ok=True)

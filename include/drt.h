@@ -136,6 +136,13 @@ int drt_answer_match_i32(const int32_t* tok, int32_t W, const int64_t* rows, con
                          int64_t B, int64_t k, const int32_t* ans, const int32_t* alen, int32_t A, int32_t n_max,
                          const uint8_t* every, int8_t* hit, void* stream);
 
+/* get_metrics (DRT/evaluator/metrics.py:4-59) of one loader batch's hit matrix hit [B][k] (int8, from
+ * drt_answer_match_i32), ADDED to the evaluation's running sums acc [3 T] (fp64, device): acc[t] +=
+ * recall@topk[t] (rows whose first hit is < topk[t]), acc[T + t] += mrr@topk[t], acc[2 T + t] += the
+ * batch's ndcg@topk[t] ratio.  topk [T] int32 on the device; B <= 4096, k <= 2048, T <= 16.          */
+int drt_hit_metrics_i8(const int8_t* hit, int64_t B, int64_t k, const int32_t* topk, int32_t T, double* acc,
+                       void* stream);
+
 /* Merge `nparts` per-shard top-k lists into one global top-k.
  * scores/ids: [nparts, nq, k_in] (each part sorted score desc, id asc, as
  * drt_ip_topk_bf16 writes them); out: [nq, k_out], k_out <= k_in*nparts,

@@ -52,3 +52,32 @@ def test_device_matcher_reference_golden(dev):
         rows = np.array([c["docs"] + [-1, -1]], dtype=np.int64)
         got = dm.match_rows(rows, lambda r: g["docs"][r], [c["answers"]])
         assert got[0].tolist() == c["has"] + [0, 0], c
+
+
+@pytest.mark.parametrize("B,k,topk", [(128, 1000, [1, 5, 20, 100, 1000]), (7, 50, [1, 3, 100]), (1, 1, [1, 2]),
+                                      (300, 64, [64, 10])])
+def test_device_metrics_equal_get_metrics(dev, B, k, topk):
+    """drt_hit_metrics_i8 adds each batch's get_metrics (DRT/evaluator/metrics.py:4-59 restated in
+    evaluator/metrics.py, pinned by tests/golden/metrics.json) to device sums: rows without hits, cut-offs
+    beyond k, several batches accumulated."""
+    import torch
+    from denseretrievaltoolkits_amd import _native
+    from denseretrievaltoolkits_amd.evaluator.metrics import get_metrics
+    rng = np.random.default_rng(B + k)
+    acc = torch.zeros(3 * len(topk), dtype=torch.float64, device=dev)
+    tk = torch.tensor(topk, dtype=torch.int32, device=dev)
+    ref = {}
+    for it in range(3):
+        hit = (rng.random((B, k)) < [0.0, 0.002, 0.05][it]).astype(np.int8)
+        hit[0] = 0
+        ht = torch.from_numpy(hit).to(dev)
+        _native.check(_native.load().drt_hit_metrics_i8(ht.data_ptr(), B, k, tk.data_ptr(), len(topk), acc.data_ptr(),
+                                                        _native.stream_ptr(dev)), "drt_hit_metrics_i8")
+        for key, v in get_metrics(hit, topk).items():
+            ref[key] = ref.get(key, 0.0) + v
+    got = acc.cpu().numpy()
+    T = len(topk)
+    for t, kk in enumerate(topk):
+        assert got[t] == ref[f"Recall@{kk}"]
+        assert abs(got[T + t] - ref[f"MRR@{kk}"]) <= 1e-12 * max(1.0, abs(ref[f"MRR@{kk}"]))
+        assert abs(got[2 * T + t] - ref[f"NDCG@{kk}"]) <= 1e-12 * max(1.0, abs(ref[f"NDCG@{kk}"]))
