@@ -22,7 +22,11 @@ def main():
     ap.add_argument("--legs", default="encode,rerank,query,scores,train,recipe,evaluate")
     ap.add_argument("--trace-linear", action="store_true")
     ap.add_argument("--c2-passages", type=int, default=200_000)
+    ap.add_argument("--maps", default="", help="write /proc/self/maps here before each leg (to symbolise a "
+                                               "crash's raw frame addresses offline: tools/symbolize_crash.py)")
     args = ap.parse_args()
+    import faulthandler
+    faulthandler.enable()
     import torch
     import bench_legs as bl
     from denseretrievaltoolkits_amd.model import encoder as enc_mod
@@ -49,7 +53,11 @@ def main():
         "recipe": lambda: bl.run_train_step(dev, bq=128, n=8, p_len=156, steps=1, warmup=1),
         "evaluate": lambda: bl.run_evaluate_c2(dev, n_passages=args.c2_passages),
     }
+    torch.zeros(1, device=dev)   # the runtime (and a profiler's hooks) loaded before the first map dump
     for name in args.legs.split(","):
+        if args.maps:
+            with open("/proc/self/maps") as src, open(args.maps, "w") as dst:
+                dst.write(src.read())
         print(f"LEG {name} start (linear calls so far {ncall[0]})", file=sys.stderr, flush=True)
         t0 = time.perf_counter()
         legs[name]()
