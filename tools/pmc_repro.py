@@ -1,7 +1,9 @@
 #!/usr/bin/env python3
 """Smallest steps towards the rocprofv3 --pmc abort seen in the evaluate leg (SIGSEGV in a memcpy
 under THCPEvent_wait / hipLaunchKernel, no DRT frame below it): each step prints before it runs, so
-the last line names the HIP operation the profiler fails on.  Torch ops only (no DRT kernels)."""
+the last line names the HIP operation the profiler fails on.  Torch ops only (no DRT kernels).
+usage: python tools/pmc_repro.py [N [nocopy]]   (N > 0: step 9, N tiny kernels on a side stream; nocopy:
+without the pinned H2D copies)"""
 import sys
 
 import torch
@@ -68,6 +70,24 @@ def main():
         e4.wait(torch.cuda.current_stream(dev))
         _ = dv * 2.0
     torch.cuda.synchronize()
+    n = int(sys.argv[1]) if len(sys.argv) > 1 else 0
+    copies = "nocopy" not in sys.argv[2:]
+    if n:
+        # the evaluate leg dies after ~9k encoder linears (tens of thousands of dispatches): the same
+        # number of tiny kernels on one side stream, a pinned H2D copy every 64 of them
+        say(f"9 {n} kernels on a side stream with periodic pinned H2D copies")
+        s3 = torch.cuda.Stream(dev)
+        hb = torch.randint(0, 30000, (256, 128), dtype=torch.int64).pin_memory()
+        with torch.cuda.stream(s3):
+            acc = torch.zeros(256, 128, dtype=torch.int64, device=dev)
+            for j in range(n):
+                if j % 64 == 0 and copies:
+                    acc += hb.to(dev, non_blocking=True)
+                else:
+                    acc.add_(1)
+                if j % 5000 == 0:
+                    say(f"  kernel {j}")
+        torch.cuda.synchronize()
     say("done")
 
 
