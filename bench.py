@@ -324,7 +324,8 @@ def pmc_traffic(args, world, shape=None):
 def launch_shapes(steps, qb, grouped, group_queries, rows, chunks=None):
     """(queries, rows) of every filter-scan launch in the timed region: one launch per batch over the
     shard on the per-batch path; on the grouped one, per group of batches (search._groups: at most
-    group_queries queries) one launch over the shard, or one per row chunk (one GPU, search.group_chunks)."""
+    group_queries queries) one launch over the shard, or one per row chunk (search.group_chunks; a
+    sharded index splits every shard into the same count, ShardedFlatIP.group_chunks)."""
     if not grouped:
         return [(qb, rows)] * steps
     sizes, cur = [], 0
@@ -369,11 +370,12 @@ def scan_roofline(d, k, kc, shapes, grouped, launch_ms_total):
 
 def search_record(args, world, grouped, group_queries, kc, elapsed_s, launch_ms_total, launches, traffic,
                   chunks=None):
-    """The headline JSON record of the search leg (rank 0).  ``chunks``: the row ranges of a one-GPU
-    group filter (search.group_chunks)."""
+    """The headline JSON record of the search leg (rank 0).  ``chunks``: the row ranges of rank 0's
+    group filter launches (search.group_chunks / ShardedFlatIP.group_chunks; rank 0 holds the largest
+    shard)."""
     d, k, qb = args.dim, args.k, args.qb
     per = -(-args.n_corpus // world)
-    shapes = launch_shapes(args.steps, qb, grouped, group_queries, per, chunks if world == 1 else None)
+    shapes = launch_shapes(args.steps, qb, grouped, group_queries, per, chunks)
     rf = scan_roofline(d, k, kc, shapes, grouped, launch_ms_total)
     rf = {"kernel": "ip_scan16r_kernel<%d> (csrc/search.hip)" % d, **rf}
     if launches != len(shapes):
@@ -390,8 +392,9 @@ def search_record(args, world, grouped, group_queries, kc, elapsed_s, launch_ms_
                  "per batch: sample scan + k-th selection, one filter launch, select, canonical-order stage)"))
     else:
         path = (f"ShardedFlatIP.search_batches ({args.protocol}, certified, pipelined; " +
-                (f"grouped: one sample launch, sample-list all-gather, one filter launch over all "
-                 f"{group_queries} queries of a group, packed all-gather and merge per group)" if grouped else
+                (f"grouped: one sample launch, sample-list all-gather, the filter over all {group_queries} "
+                 f"queries of a group as {len(chunks or [0])} launch(es) over row chunks of the shard, packed "
+                 "all-gather of every chunk's lists and one merge per group)" if grouped else
                  "per batch: per-shard exact top-k, all-gather, merge)"))
     qps = args.steps * qb / elapsed_s
     return {
@@ -523,15 +526,16 @@ def main():
         _, el1, ms1, n1, _ = timed(args.warmup, nsteps)
         srch.GROUP_QUERIES = gq_saved
         if rank == 0:
-            sub = search_record(args, world, True, qb, kernels.refine_width(k), el1, ms1, n1, (None, None))
+            sub = search_record(args, world, True, qb, kernels.refine_width(k), el1, ms1, n1, (None, None),
+                                chunks=index.group_chunks())
             sub = {"value": sub["value"], "ms_per_step": sub["ms_per_step"],
                    "config": "one 128-query batch per group (per-batch global-threshold protocol)",
                    "roofline": sub["roofline"]}
 
     out = None
     if rank == 0:
-        chunks = srch.group_chunks(n_local)
-        shape = (srch.GROUP_QUERIES, max(b - a for a, b in chunks) if world == 1 else n_local) if grouped else None
+        chunks = srch.group_chunks(n_local) if world == 1 else index.group_chunks()
+        shape = (srch.GROUP_QUERIES, max(b - a for a, b in chunks)) if grouped else None
         out = search_record(args, world, grouped, srch.GROUP_QUERIES, kernels.refine_width(k), el,
                             scan_ms_total, launches, pmc_traffic(args, world, shape), chunks=chunks)
         if sub is not None:

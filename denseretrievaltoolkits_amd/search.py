@@ -123,14 +123,19 @@ GROUP_MIN_ROWS = 500_000
 GROUP_CHUNK_ROWS = 1_250_000
 
 
-def group_chunks(nrows: int, chunk_rows: int = None):
-    """Row ranges [(a, b)] of a one-GPU group filter: balanced chunks of <= chunk_rows rows."""
+def group_chunks(nrows: int, chunk_rows: int = None, nch: int = None):
+    """Row ranges [(a, b)] of a group filter: balanced chunks of <= chunk_rows rows, or exactly ``nch``
+    chunks (a sharded index: every rank splits its shard into the same count, so the ranks' part buffers
+    have one shape; a chunk may be empty)."""
     chunk_rows = GROUP_CHUNK_ROWS if chunk_rows is None else chunk_rows
-    if chunk_rows <= 0 or nrows <= chunk_rows:
+    if nch is None:
+        if chunk_rows <= 0 or nrows <= chunk_rows:
+            return [(0, nrows)]
+        nch = -(-nrows // chunk_rows)
+    if nch <= 1:
         return [(0, nrows)]
-    nch = -(-nrows // chunk_rows)
     per = -(-nrows // nch)
-    return [(a, min(nrows, a + per)) for a in range(0, nrows, per)]
+    return [(min(nrows, c * per), min(nrows, (c + 1) * per)) for c in range(nch)]
 
 
 def _groups(batches, cap=None):
@@ -167,12 +172,13 @@ def _gtau_enqueue_group(local, qs, k: int, n_global: int, offset: int, gather, t
     tau = kernels.dist_tau(lists, k)                                # [Qg]: one launch for the group
     kc = kernels.refine_width(k) if stats is not None else k
     if chunks is not None and len(chunks) > 1:
-        # one GPU, long shard: one filter launch per row chunk (the group's query blocks stay in step
-        # over a chunk, so its tiles are read from HBM once), the chunks' lists merged as parts
+        # long shard: one filter launch per row chunk (the group's query blocks stay in step over a
+        # chunk, so its tiles are read from HBM once), every chunk's lists a part of the merge
         parts = torch.empty((len(chunks), qg.shape[0], kc + 1), dtype=torch.int64, device=qg.device)
         for c, (a, b) in enumerate(chunks):
             kernels.dist_filter_into(qg, local.rows[a:b], n_global, kc, offset + a, tau, parts[c])
-        s, i, st = kernels.merge_packed(parts, kc, n_global, k_cert=k)
+        allp = gather(parts)
+        s, i, st = kernels.merge_packed(allp.reshape(-1, qg.shape[0], kc + 1), kc, n_global, k_cert=k)
     else:
         packed = torch.empty((qg.shape[0], kc + 1), dtype=torch.int64, device=qg.device)
         # ONE filter launch for the whole group (grid: corpus tiles x 128-query blocks, the blocks of
@@ -581,15 +587,23 @@ class ShardedFlatIP:
                 self.order_uncertified += nunc
                 return res
 
+            chunks = self.group_chunks()
             for res in _pipeline(groups, lambda j, g: _gtau_enqueue_group(
                     self.local, g, k, self.ntotal, self.offset, self._all_gather, to_host, stats=self.stats,
-                    all_reduce_sum=lambda t: comm.all_reduce_sum_(t, self.group)), fin):
+                    all_reduce_sum=lambda t: comm.all_reduce_sum_(t, self.group), chunks=chunks), fin):
                 yield from res
             return
         for r in _pipeline(batches, lambda j, q: self._enqueue(q, k, to_host), self._finish):
             if to_host and isinstance(r[0], torch.Tensor):
                 r = (r[0].cpu().numpy(), r[1].cpu().numpy())
             yield r
+
+    def group_chunks(self):
+        """This shard's row chunks of a group filter: as many as the largest shard needs (every rank the
+        same count: the gathered part buffers have one shape; W = 8 over 10M rows: one)."""
+        per = -(-self.ntotal // max(1, self.world))
+        nch = len(group_chunks(per)) if GROUP_CHUNK_ROWS > 0 else 1
+        return group_chunks(self.local.ntotal, nch=nch)
 
     def _use_groups(self) -> bool:
         """search_batches runs the grouped global-threshold protocol (one filter launch per group)."""

@@ -22,7 +22,7 @@ def _rec(n, world, grouped, launch_ms, steps=20, group=2048, chunks=None):
     import bench
     a = _args(n, steps)
     per = -(-n // world)
-    shapes = bench.launch_shapes(steps, 128, grouped, group, per, chunks if world == 1 else None)
+    shapes = bench.launch_shapes(steps, 128, grouped, group, per, chunks)
     traffic = (None, None) if grouped else (15_385_000_000, "r04aw_pmc_traffic.json")
     return bench.search_record(a, world, grouped, group, KC, steps * 2.7e-3, launch_ms * len(shapes), len(shapes),
                                traffic, chunks=chunks)
@@ -85,3 +85,20 @@ def test_world8_prices_the_launch_it_ran(grouped, launch_ms, bound):
     else:
         t_hbm = (per * 768 * 2 + 128 * 768 * 2 + 128 * (KC + 1) * 8) / 8e12
         assert abs(rf["frac"] - t_hbm / 0.30e-3) < 1e-3
+
+
+def test_world2_grouped_prices_the_shard_chunks():
+    """World 2 over 10M rows: each 5M-row shard is filtered in 4 chunk launches (the count of the
+    largest shard, the same on every rank)."""
+    from types import SimpleNamespace as NS
+    from denseretrievaltoolkits_amd import search as srch
+    fake = NS(ntotal=10_000_000, world=2, local=NS(ntotal=5_000_000))
+    ch = srch.ShardedFlatIP.group_chunks(fake)
+    assert ch == [(0, 1_250_000), (1_250_000, 2_500_000), (2_500_000, 3_750_000), (3_750_000, 5_000_000)]
+    # a short last shard keeps the count (empty chunks allowed)
+    short = srch.ShardedFlatIP.group_chunks(NS(ntotal=10_000_000, world=3, local=NS(ntotal=2)))
+    assert len(short) == 3 and short[-1] == (2, 2)
+    r = _rec(10_000_000, 2, True, 3.8, steps=16, chunks=ch)
+    rf = r["roofline"]
+    assert rf["launches"] == 4 and rf["launch_shapes"] == [(2048, 1_250_000)]
+    assert "4 launch(es) over row chunks of the shard" in r["config"]["path"]

@@ -141,19 +141,24 @@ def _w_sharded(rank, world, dev, case):
             np.testing.assert_array_equal(s, gscores)
         out[proto] = idx.fallbacks
         # batched search: ragged batches of 5 in groups of <= 16 queries (3 groups of up to 3 batches)
+        # and with the shards' filter split into row chunks (every rank the same chunk count, the
+        # gathered parts [world, chunks, ...] merged as one list set)
         from denseretrievaltoolkits_amd import search as srch
-        saved = srch.GROUP_QUERIES
-        srch.GROUP_QUERIES = 16
-        try:
-            fb0 = idx.fallbacks
-            qd = to_dev_bf16(q, dev)
-            res = idx.search_batches([qd[a: a + 5] for a in range(0, q.shape[0], 5)], k)
-            torch.cuda.synchronize()
-        finally:
-            srch.GROUP_QUERIES = saved
-        np.testing.assert_array_equal(torch.cat([r[1] for r in res]).cpu().numpy(), ei)
-        if case != "gauss":
-            np.testing.assert_array_equal(torch.cat([r[0] for r in res]).cpu().numpy(), es)
+        saved = srch.GROUP_QUERIES, srch.GROUP_CHUNK_ROWS
+        fb0 = idx.fallbacks
+        for chunk_rows in ((saved[1], 20000) if case in ("int", "gauss") else (saved[1],)):
+            srch.GROUP_QUERIES, srch.GROUP_CHUNK_ROWS = 16, chunk_rows
+            try:
+                if chunk_rows == 20000:
+                    assert len(idx.group_chunks()) == -(-(-(-p.shape[0] // world)) // 20000)
+                qd = to_dev_bf16(q, dev)
+                res = idx.search_batches([qd[a: a + 5] for a in range(0, q.shape[0], 5)], k)
+                torch.cuda.synchronize()
+            finally:
+                srch.GROUP_QUERIES, srch.GROUP_CHUNK_ROWS = saved
+            np.testing.assert_array_equal(torch.cat([r[1] for r in res]).cpu().numpy(), ei)
+            if case != "gauss":
+                np.testing.assert_array_equal(torch.cat([r[0] for r in res]).cpu().numpy(), es)
         out[proto + "_batched"] = idx.fallbacks - fb0
     return out
 
