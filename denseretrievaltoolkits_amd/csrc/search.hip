@@ -21,6 +21,7 @@
 //                    that query densely (exact by construction).
 #include <algorithm>
 #include <cmath>
+#include <cstdlib>
 #include <vector>
 
 #include "drt_common.h"
@@ -731,6 +732,212 @@ __global__ __launch_bounds__(512, 1) void ip_scan16r_kernel(ScanArgs a) {
   }
   if (my_tiles & 1) epilogue(accA, rbA);
   else epilogue(accB, rbB);
+  if (wcnt) wave_flush_hits(a, qw, hk, hq, wcnt, lane);
+}
+
+// ---------------------------------------------------------------------------
+// Grouped filter scan (a launch of more than 128 queries): the same 16-row tiles, ring and MFMA
+// step order as ip_scan16r_kernel, but 32 queries per wave (two 16-query B sets held in registers,
+// 256 queries per work-group), so one LDS fragment read of the tile's rows feeds TWO MFMAs.
+// Round 5 ablations of ip_scan16r on the grouped launch (profiles/r05y): its 16x16x32 MFMA per
+// 1 KiB fragment read puts the LDS array (256 B/clk/CU, plus the ring's DMA writes) level with the
+// MFMA pipe, the launch ran at 53 % MFMA / 53 % LDS busy, and the corpus DMA alone added 30 % to the
+// MFMA-only time.  Here the LDS reads per MFMA and the L2 -> LDS bytes per query are halved (a group's
+// tile is loaded by half as many work-groups).  Registers: the 32 queries' fragments (2 x d/32 x 4
+// VGPRs) leave room for a short fragment roll only: fragment s + RD of the same tile (or, near the
+// end of a tile, of the next one) is read into the register fragment s just left, so a slot is read
+// during its own tile and is refilled one tile later (issue distance NB - 1).  A tile's epilogue runs
+// after the next tile's MFMAs are issued (two accumulator sets alternate), as in ip_scan16r.
+// Every score is the same 24-step 16x16x32 chain as ip_scan16r's: identical values and hits.
+// ---------------------------------------------------------------------------
+template <int D>
+struct Scan32Cfg {
+  static constexpr int KS = D / 32;
+#ifdef DRT_SCAN32_RD
+  static constexpr int RD = KS % DRT_SCAN32_RD == 0 ? DRT_SCAN32_RD : 1;
+#else
+  static constexpr int RD = KS % 2 == 0 ? 2 : 1;   // fragment roll depth (round 5: 2, 3, 4, 6 within noise)
+#endif
+  static constexpr int TILE_BYTES = kT16 * D * 2;
+  static constexpr int HIT_BYTES = kHitCap * 9;
+  static constexpr int NB_RAW = (160 * 1024 - HIT_BYTES) / TILE_BYTES;
+  static constexpr int NB = NB_RAW > 6 ? 6 : NB_RAW;
+  static constexpr int RING_BYTES = NB * TILE_BYTES;
+  static constexpr int LDS_BYTES = RING_BYTES + HIT_BYTES;
+  static_assert(NB >= 3, "ring too small");
+  static_assert(LDS_BYTES <= 160 * 1024, "LDS budget");
+};
+constexpr int kQueriesPerWG32 = 256;
+
+template <int D>
+__global__ __launch_bounds__(512, 1) void ip_scan32r_kernel(ScanArgs a) {
+  constexpr int NW = 8;
+  using C = Scan16Cfg<D, NW>;   // tile image, DMA split, per-wave issue count
+  using C32 = Scan32Cfg<D>;
+  constexpr int NB = C32::NB;
+  constexpr int PD = NB - 1;    // tiles issued ahead (the slot of tile it-1 is refilled at tile it+1)
+  constexpr int KS = C32::KS;
+  constexpr int RD = C32::RD;
+  constexpr int kSeg = kHitCap / NW;
+  __shared__ __attribute__((aligned(16))) char smem[C32::LDS_BYTES];
+
+  const int tid = threadIdx.x;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int lane = tid & 63;
+  const int r = lane & 15;
+  const int kq = lane >> 4;
+  uint64_t* hk = (uint64_t*)(smem + C32::RING_BYTES) + wave * kSeg;
+  uint8_t* hq = (uint8_t*)(smem + C32::RING_BYTES + kHitCap * 8) + wave * kSeg;
+
+  const int64_t qbase = (int64_t)blockIdx.y * kQueriesPerWG32;
+  const int ntiles = (int)((a.nrows + kT16 - 1) / kT16);
+  const uint32_t nrows = (uint32_t)a.nrows;
+  const int t0 = blockIdx.x;
+  const int tstep = gridDim.x;
+  const int my_tiles = t0 < ntiles ? (ntiles - 1 - t0) / tstep + 1 : 0;
+  if (my_tiles == 0) return;
+  const int partial_tile = (a.nrows & (kT16 - 1)) != 0 ? ntiles - 1 : -1;
+  const uint32_t ring = lds_addr_of(smem);
+  const int64_t tile_stride = (int64_t)tstep * kT16 * a.ldp * 2;
+  const char* next_base = (const char*)(a.P + (int64_t)t0 * kT16 * a.ldp);
+
+  // 32 queries per wave: qw + 16 b + r, b = 0, 1
+  const int64_t qw = qbase + wave * 32;
+  bf16x8 qf0[KS], qf1[KS];
+  float tau0, tau1;
+  {
+    const int64_t g0 = qw + r, g1 = qw + 16 + r;
+    const bool ok0 = g0 < a.nq, ok1 = g1 < a.nq;
+    const int64_t s0 = ok0 ? g0 : 0, s1 = ok1 ? g1 : 0;
+#pragma unroll
+    for (int s = 0; s < KS; ++s) {
+      qf0[s] = *(const bf16x8*)(a.Q + s0 * a.ldq + s * 32 + kq * 8);
+      qf1[s] = *(const bf16x8*)(a.Q + s1 * a.ldq + s * 32 + kq * 8);
+    }
+    const float v0 = a.tau[s0], v1 = a.tau[s1];
+    tau0 = ok0 ? v0 : __builtin_nanf("");
+    tau1 = ok1 ? v1 : __builtin_nanf("");
+    if (!ok0) {
+#pragma unroll
+      for (int s = 0; s < KS; ++s) qf0[s] = (bf16x8){};
+    }
+    if (!ok1) {
+#pragma unroll
+      for (int s = 0; s < KS; ++s) qf1[s] = (bf16x8){};
+    }
+  }
+#pragma unroll
+  for (int s = 0; s < KS; ++s) asm volatile("" ::"v"(qf0[s]), "v"(qf1[s]));
+  asm volatile("" ::"v"(tau0), "v"(tau1));
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+
+  LeanTile<D, NW> lt;
+  lt.init(a, wave, lane);
+#pragma unroll
+  for (int p = 0; p < PD; ++p) {
+    if (p < my_tiles) {
+      const int tile = t0 + p * tstep;
+      lt.template issue<false>(a, ring + p * C::TILE_BYTES, next_base, tile == partial_tile, tile, wave, lane);
+      next_base += tile_stride;
+    }
+  }
+  if (wave >= NW / 2) __builtin_amdgcn_s_setprio(1);
+  {
+    const int last = my_tiles - 1 < PD - 1 ? my_tiles - 1 : PD - 1;
+    wait_tiles_younger<C::GLDS_PER_WAVE>((int)last);
+  }
+  lds_barrier();
+
+  const int sw = (r >> 1) & 7;
+  int aoff[2];
+#pragma unroll
+  for (int m = 0; m < 2; ++m) aoff[m] = r * 128 + (((4 * m + kq) ^ sw) << 4);
+  auto frag = [&](int slot, int s) -> bf16x8 {
+    return *(const bf16x8*)(smem + slot * C::TILE_BYTES + (s >> 1) * (kT16 * 128) + aoff[s & 1]);
+  };
+  bf16x8 af[RD];
+#pragma unroll
+  for (int s = 0; s < RD; ++s) af[s] = frag(0, s);
+
+  int wcnt = 0;
+  auto append = [&](const f32x4& acc, float tau, int ql, uint32_t rowbase) {
+    const float mx = fmaxf(fmaxf(acc[0], acc[1]), fmaxf(acc[2], acc[3])) - tau;
+    if (__ballot(mx >= 0.0f) == 0ull) return;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const bool hit = acc[j] >= tau && rowbase + j < nrows;
+      const uint64_t m = __ballot(hit);
+      if (m == 0ull) continue;
+      const int c = __builtin_popcountll(m);
+      if (wcnt + c > kSeg) {
+        wave_flush_hits(a, qw, hk, hq, wcnt, lane);
+        wcnt = 0;
+      }
+      if (hit) {
+        const int pos = wcnt + (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32),
+                                                              __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+        hk[pos] = ((uint64_t)desc_key(acc[j]) << 32) | (uint64_t)(rowbase + j);
+        hq[pos] = (uint8_t)ql;
+      }
+      wcnt += c;
+    }
+  };
+
+  int buf = 0;   // slot of tile it
+  // one tile: wait + barrier, ring refill, MFMAs (+ the rolled reads), then the epilogue of the
+  // PREVIOUS tile (its accumulators are complete by then: no wait on this tile's MFMA latency); the
+  // loop body runs two tiles so the accumulator sets alternate without run-time selection
+  auto iter = [&](int it, f32x4& acc0, f32x4& acc1, uint32_t& rb, const f32x4& prev0, const f32x4& prev1,
+                  uint32_t rb_prev) {
+    const int tile = t0 + it * tstep;
+    // issued so far: tiles .. it + PD - 1; tile it+1 must have landed (its first RD fragments are
+    // read near the end of this tile's MFMAs)
+    if (it + PD <= my_tiles) {
+      wait_vmcnt<C::GLDS_PER_WAVE * (PD - 2)>();
+    } else if (it + 1 < my_tiles) {
+      wait_tiles_younger<C::GLDS_PER_WAVE>(my_tiles - 1 - it - 1);
+    }
+    // every wave's share of tile it+1 landed, and every wave issued tile it-1's MFMAs (so its reads of
+    // slot(it-1) completed: each MFMA waited for its own fragment) -- that slot is refilled below
+    lds_barrier();
+    if (it + PD < my_tiles) {
+      const int ntile = tile + PD * tstep;
+      const int pslot = buf == 0 ? NB - 1 : buf - 1;   // slot of tile it-1 (it = 0: the unused slot)
+      lt.template issue<false>(a, ring + pslot * C::TILE_BYTES, next_base, ntile == partial_tile, ntile, wave,
+                               lane);
+      next_base += tile_stride;
+    }
+    const int nslot = buf + 1 == NB ? 0 : buf + 1;
+    acc0 = (f32x4){0.f, 0.f, 0.f, 0.f};
+    acc1 = (f32x4){0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int s = 0; s < KS; ++s) {
+      acc0 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[s % RD], qf0[s], acc0, 0, 0, 0);
+      acc1 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[s % RD], qf1[s], acc1, 0, 0, 0);
+      // fragment s + RD: of this tile, or (the last RD steps) the first ones of tile it+1
+      af[s % RD] = s + RD < KS ? frag(buf, s + RD) : frag(nslot, s + RD - KS);
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    if (it > 0) {
+      append(prev0, tau0, r, rb_prev);
+      append(prev1, tau1, 16 + r, rb_prev);
+    }
+    rb = (uint32_t)tile * kT16 + 4 * kq;
+    buf = nslot;
+  };
+  f32x4 a0, a1, b0, b1;
+  uint32_t rbA = 0, rbB = 0;
+  for (int it = 0; it < my_tiles; it += 2) {
+    iter(it, a0, a1, rbA, b0, b1, rbB);
+    if (it + 1 < my_tiles) iter(it + 1, b0, b1, rbB, a0, a1, rbA);
+  }
+  if (my_tiles & 1) {
+    append(a0, tau0, r, rbA);
+    append(a1, tau1, 16 + r, rbA);
+  } else {
+    append(b0, tau0, r, rbB);
+    append(b1, tau1, 16 + r, rbB);
+  }
   if (wcnt) wave_flush_hits(a, qw, hk, hq, wcnt, lane);
 }
 
@@ -2891,6 +3098,15 @@ static int scan_grid_x(int64_t ntiles) {
   return (int)std::max<int64_t>(g, 1);
 }
 
+// DRT_SCAN32=0 keeps grouped launches on ip_scan16r_kernel (A/B switch; results are identical)
+static bool scan32_enabled() {
+  static const bool on = [] {
+    const char* e = getenv("DRT_SCAN32");
+    return !(e && e[0] == '0');
+  }();
+  return on;
+}
+
 template <int D>
 static int launch_scan_d(const ScanArgs& a, int mode, hipStream_t s) {
   if (a.nq == 0 || a.nrows == 0) return DRT_OK;
@@ -2926,9 +3142,22 @@ static int launch_scan_d(const ScanArgs& a, int mode, hipStream_t s) {
       if (dense_hits) hipLaunchKernelGGL((ip_scan16_kernel<D, SCAN_FILTER, 8, true>), grid, dim3(512), 0, s, a);
       else hipLaunchKernelGGL((ip_scan16_kernel<D, SCAN_FILTER, 8, false>), grid, dim3(512), 0, s, a);
     } else {
-      // non-temporal corpus loads for a single block; a group's blocks share each tile through L2
-      if (gy > 1) hipLaunchKernelGGL((ip_scan16r_kernel<D, false>), grid, dim3(512), 0, s, a);
-      else hipLaunchKernelGGL((ip_scan16r_kernel<D, true>), grid, dim3(512), 0, s, a);
+      // non-temporal corpus loads for a single block; a group's blocks share each tile through L2, and a
+      // group of more than 128 queries takes the 32-queries-per-wave kernel (256 per work-group)
+      if (D <= 768 && gy > 1 && scan32_enabled()) {   // (wider rows: the 32 queries' fragments spill)
+        const unsigned gy32 = (unsigned)((a.nq + kQueriesPerWG32 - 1) / kQueriesPerWG32);
+        int gx32 = scan_grid_x(ntiles);
+        if (gy32 > 1 && ntiles >= 8) {
+          const int cus = scan_grid_x((int64_t)1 << 40);
+          const int share = std::max(8, (cus / (int)gy32) & ~7);
+          gx32 = (int)std::min<int64_t>(ntiles, share);
+        }
+        hipLaunchKernelGGL((ip_scan32r_kernel<D <= 768 ? D : 768>), dim3(gx32, gy32), dim3(512), 0, s, a);
+      } else if (gy > 1) {
+        hipLaunchKernelGGL((ip_scan16r_kernel<D, false>), grid, dim3(512), 0, s, a);
+      } else {
+        hipLaunchKernelGGL((ip_scan16r_kernel<D, true>), grid, dim3(512), 0, s, a);
+      }
     }
   } else {
     hipLaunchKernelGGL((ip_scan16_kernel<D, SCAN_DENSE>), grid, dim3(512), 0, s, a);
