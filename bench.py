@@ -377,7 +377,9 @@ def search_record(args, world, grouped, group_queries, kc, elapsed_s, launch_ms_
     per = -(-args.n_corpus // world)
     shapes = launch_shapes(args.steps, qb, grouped, group_queries, per, chunks)
     rf = scan_roofline(d, k, kc, shapes, grouped, launch_ms_total)
-    rf = {"kernel": "ip_scan16r_kernel<%d> (csrc/search.hip)" % d, **rf}
+    # launches of more than 128 queries run the 32-queries-per-wave kernel (search.hip, launch_scan_d)
+    kname = "ip_scan32r_kernel" if grouped and group_queries > 128 and d <= 768 else "ip_scan16r_kernel"
+    rf = {"kernel": "%s<%d> (csrc/search.hip)" % (kname, d), **rf}
     if launches != len(shapes):
         rf["launches_counted"] = launches   # the profiler's count (differs only if a batch was redone)
     # PMC traffic (tools/pmc_traffic.py) of this configuration's dominant launch shape

@@ -21,7 +21,6 @@
 //                    that query densely (exact by construction).
 #include <algorithm>
 #include <cmath>
-#include <cstdlib>
 #include <vector>
 
 #include "drt_common.h"
@@ -883,6 +882,12 @@ __global__ __launch_bounds__(512, 1) void ip_scan32r_kernel(ScanArgs a) {
     }
   };
 
+  // (one ballot over both query sets' tiles measured slower: 2.95-2.97 vs 2.91 ms, profiles/r05y)
+  auto epilogue = [&](const f32x4& p0, const f32x4& p1, uint32_t rowbase) {
+    append(p0, tau0, r, rowbase);
+    append(p1, tau1, 16 + r, rowbase);
+  };
+
   int buf = 0;   // slot of tile it
   // one tile: wait + barrier, ring refill, MFMAs (+ the rolled reads), then the epilogue of the
   // PREVIOUS tile (its accumulators are complete by then: no wait on this tile's MFMA latency); the
@@ -900,13 +905,12 @@ __global__ __launch_bounds__(512, 1) void ip_scan32r_kernel(ScanArgs a) {
     // every wave's share of tile it+1 landed, and every wave issued tile it-1's MFMAs (so its reads of
     // slot(it-1) completed: each MFMA waited for its own fragment) -- that slot is refilled below
     lds_barrier();
-    if (it + PD < my_tiles) {
-      const int ntile = tile + PD * tstep;
-      const int pslot = buf == 0 ? NB - 1 : buf - 1;   // slot of tile it-1 (it = 0: the unused slot)
-      lt.template issue<false>(a, ring + pslot * C::TILE_BYTES, next_base, ntile == partial_tile, ntile, wave,
-                               lane);
-      next_base += tile_stride;
-    }
+    // the refill of slot(it-1) is issued a quarter into this tile's MFMAs (its SALU / address work then
+    // overlaps queued matrix work instead of delaying every wave's first MFMA after the barrier: round 5,
+    // 2.89-2.91 vs 2.95-2.97 ms per grouped launch in three alternating rounds, profiles/r05y)
+    const bool do_dma = it + PD < my_tiles;
+    const int ntile = tile + PD * tstep;
+    const int pslot = buf == 0 ? NB - 1 : buf - 1;   // slot of tile it-1 (it = 0: the unused slot)
     const int nslot = buf + 1 == NB ? 0 : buf + 1;
     acc0 = (f32x4){0.f, 0.f, 0.f, 0.f};
     acc1 = (f32x4){0.f, 0.f, 0.f, 0.f};
@@ -917,11 +921,14 @@ __global__ __launch_bounds__(512, 1) void ip_scan32r_kernel(ScanArgs a) {
       // fragment s + RD: of this tile, or (the last RD steps) the first ones of tile it+1
       af[s % RD] = s + RD < KS ? frag(buf, s + RD) : frag(nslot, s + RD - KS);
       __builtin_amdgcn_sched_barrier(0);
+      if (s == KS / 4 && do_dma) {
+        lt.template issue<false>(a, ring + pslot * C::TILE_BYTES, next_base, ntile == partial_tile, ntile, wave,
+                                 lane);
+        next_base += tile_stride;
+      }
+      __builtin_amdgcn_sched_barrier(0);
     }
-    if (it > 0) {
-      append(prev0, tau0, r, rb_prev);
-      append(prev1, tau1, 16 + r, rb_prev);
-    }
+    if (it > 0) epilogue(prev0, prev1, rb_prev);
     rb = (uint32_t)tile * kT16 + 4 * kq;
     buf = nslot;
   };
@@ -931,13 +938,8 @@ __global__ __launch_bounds__(512, 1) void ip_scan32r_kernel(ScanArgs a) {
     iter(it, a0, a1, rbA, b0, b1, rbB);
     if (it + 1 < my_tiles) iter(it + 1, b0, b1, rbB, a0, a1, rbA);
   }
-  if (my_tiles & 1) {
-    append(a0, tau0, r, rbA);
-    append(a1, tau1, 16 + r, rbA);
-  } else {
-    append(b0, tau0, r, rbB);
-    append(b1, tau1, 16 + r, rbB);
-  }
+  if (my_tiles & 1) epilogue(a0, a1, rbA);
+  else epilogue(b0, b1, rbB);
   if (wcnt) wave_flush_hits(a, qw, hk, hq, wcnt, lane);
 }
 
@@ -3098,14 +3100,13 @@ static int scan_grid_x(int64_t ntiles) {
   return (int)std::max<int64_t>(g, 1);
 }
 
-// DRT_SCAN32=0 keeps grouped launches on ip_scan16r_kernel (A/B switch; results are identical)
-static bool scan32_enabled() {
-  static const bool on = [] {
-    const char* e = getenv("DRT_SCAN32");
-    return !(e && e[0] == '0');
-  }();
-  return on;
-}
+// Built with -DDRT_SCAN32_OFF (an A/B variant library, tools/build_variant.sh), grouped launches keep
+// ip_scan16r_kernel; results are identical either way.
+#ifdef DRT_SCAN32_OFF
+constexpr bool kScan32 = false;
+#else
+constexpr bool kScan32 = true;
+#endif
 
 template <int D>
 static int launch_scan_d(const ScanArgs& a, int mode, hipStream_t s) {
@@ -3144,7 +3145,7 @@ static int launch_scan_d(const ScanArgs& a, int mode, hipStream_t s) {
     } else {
       // non-temporal corpus loads for a single block; a group's blocks share each tile through L2, and a
       // group of more than 128 queries takes the 32-queries-per-wave kernel (256 per work-group)
-      if (D <= 768 && gy > 1 && scan32_enabled()) {   // (wider rows: the 32 queries' fragments spill)
+      if (kScan32 && D <= 768 && gy > 1) {   // (wider rows: the 32 queries' fragments spill)
         const unsigned gy32 = (unsigned)((a.nq + kQueriesPerWG32 - 1) / kQueriesPerWG32);
         int gx32 = scan_grid_x(ntiles);
         if (gy32 > 1 && ntiles >= 8) {

@@ -51,6 +51,12 @@ def _gpu_protocol(dev, q, p, k, world, check_intermediates=True):
     (4, 5, 12000, 64, 10),         # n_global <= cap: tau = -inf, everything filtered
     (5, 4, 3, 128, 10),            # fewer rows than k, empty shards
     (2, 7, 60000, 1024, 2048),     # k at its maximum
+    # more than 128 queries in one launch: the 32-queries-per-wave filter kernel (ip_scan32r), full
+    # and partial 256-query blocks, ragged shards (partial 16-row tiles), several d
+    (2, 300, 30000, 768, 1000),
+    (3, 129, 20011, 320, 100),
+    (1, 257, 5003, 64, 10),
+    (2, 520, 40000, 576, 200),
 ])
 def test_dist_protocol_integer_bit_exact(dev, world, nq, n, d, k):
     rng = np.random.default_rng(world * 7 + n + d + k)

@@ -47,7 +47,7 @@ def main():
                          "hbm_bytes_per_launch": 2 * fkb * 1024 + wkb * 1024}
     # the dominant kernel = the filter scan (the bench's roofline kernel; not row_stats, which reads the
     # corpus once per index and moves as many bytes in its single launch), else the largest mover
-    scans = [k for k in kernels if "ip_scan16r_kernel" in k]
+    scans = [k for k in kernels if "ip_scan16r_kernel" in k or "ip_scan32r_kernel" in k]
     scan = max(scans or kernels, key=lambda k: kernels[k]["hbm_bytes_per_launch"])
     cfg = {"n_corpus": a.n_corpus, "world": a.world, "qb": a.qb, "k": a.k, "dim": a.dim}
     if a.launch_queries:
