@@ -479,6 +479,11 @@ def main():
         def run(first, last):
             return index.search_batches([queries[j] for j in range(first, last)], k)
 
+    # the collector is quiesced BEFORE the warm-up, so the timed steps follow the warm-up's last launch
+    # with no host pause: a 49 ms collection between them left the GPU idle long enough that the first
+    # timed launches ran 10-20 % slow (clocks ramping back: 3.45, 3.53, 3.24 ms vs 2.85-2.98 back to back,
+    # profiles/r05ap/kernel_stats)
+    _quiesce_gc()
     run(0, args.warmup)
     torch.cuda.synchronize()
     local_index = index if world == 1 else index.local
@@ -490,7 +495,6 @@ def main():
         """Batches [first, last) between barriers + syncs: (results, max-over-ranks elapsed s, filter-launch
         ms summed over the launches (slowest rank's average x count), launches, counter deltas)."""
         res0, fb0, unc0 = local_index.resolved, fallbacks(), index.order_uncertified
-        _quiesce_gc()
         lib.drt_profile_enable(_native.PROF_SCAN, 1)
         if world > 1:
             dist.barrier()
@@ -524,6 +528,7 @@ def main():
         # 128-query batch per group (one filter launch per batch)
         gq_saved = srch.GROUP_QUERIES
         srch.GROUP_QUERIES = qb
+        _quiesce_gc()
         run(0, 1)
         _, el1, ms1, n1, _ = timed(args.warmup, nsteps)
         srch.GROUP_QUERIES = gq_saved
