@@ -44,6 +44,8 @@ _SIGNATURES = [
     ("drt_ip_topk_dist_tau", c_i32, [c_vp, c_i64, c_i32, c_i32, c_vp, c_vp]),
     ("drt_ip_topk_dist_filter", c_i32, [c_vp, c_i64, c_vp, c_i64, c_i64, c_i32, c_i32, c_i64, c_vp, c_vp, c_vp,
                                         c_sz, c_vp]),
+    ("drt_ip_topk_dist_filter_chunks", c_i32, [c_vp, c_i64, c_vp, c_i64, c_i64, c_i32, c_i32, c_i64, c_vp, c_vp,
+                                               c_vp, c_i32, c_vp, c_sz, c_vp]),
     ("drt_ip_topk_dist_filter_lists", c_i32, [c_vp, c_i64, c_vp, c_i64, c_i64, c_i32, c_i32, c_i64, c_vp, c_i32,
                                               c_vp, c_vp, c_vp, c_sz, c_vp]),
     ("drt_ip_topk_dist_filter_lists_at", c_i32, [c_vp, c_i64, c_vp, c_i64, c_i64, c_i32, c_i32, c_i64, c_vp,

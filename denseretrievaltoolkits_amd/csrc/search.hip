@@ -52,6 +52,7 @@ struct ScanArgs {
   void* out;          // FILTER: u64 [nq][cap] keys; DENSE: u32 [nq][cap] desc keys
   int64_t cap;
   int64_t exp_hits;   // FILTER: expected hits per query (0: cap / 4); picks the append flavour
+  uint32_t row_base;  // FILTER (lean kernels): added to the row of every hit key (a chunk of a longer shard)
 };
 
 // LDS-DMA of 16 B per lane.  Issued through inline asm on purpose: with the
@@ -672,7 +673,7 @@ __global__ __launch_bounds__(512, 1) void ip_scan16r_kernel(ScanArgs a) {
         if (hv[j]) {
           const int pos = base + (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(mv[j] >> 32),
                                                                 __builtin_amdgcn_mbcnt_lo((uint32_t)mv[j], 0u));
-          hk[pos] = ((uint64_t)desc_key(acc[j]) << 32) | (uint64_t)(rowbase + j);
+          hk[pos] = ((uint64_t)desc_key(acc[j]) << 32) | (uint64_t)(a.row_base + rowbase + j);
           hq[pos] = (uint8_t)r;
         }
         base += cv[j];
@@ -693,7 +694,7 @@ __global__ __launch_bounds__(512, 1) void ip_scan16r_kernel(ScanArgs a) {
       if (hit) {
         const int pos = wcnt + (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32),
                                                               __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
-        hk[pos] = ((uint64_t)desc_key(acc[j]) << 32) | (uint64_t)(rowbase + j);
+        hk[pos] = ((uint64_t)desc_key(acc[j]) << 32) | (uint64_t)(a.row_base + rowbase + j);
         hq[pos] = (uint8_t)r;
       }
       wcnt += c;
@@ -875,7 +876,7 @@ __global__ __launch_bounds__(512, 1) void ip_scan32r_kernel(ScanArgs a) {
       if (hit) {
         const int pos = wcnt + (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32),
                                                               __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
-        hk[pos] = ((uint64_t)desc_key(acc[j]) << 32) | (uint64_t)(rowbase + j);
+        hk[pos] = ((uint64_t)desc_key(acc[j]) << 32) | (uint64_t)(a.row_base + rowbase + j);
         hq[pos] = (uint8_t)ql;
       }
       wcnt += c;
@@ -3846,6 +3847,71 @@ int drt_ip_topk_dist_filter(const void* Q, int64_t nq, const void* P, int64_t n_
   a.exp_hits = p.sample ? std::max<int64_t>(1, target * n_local / std::max<int64_t>(1, n_global)) : n_local;
   int rc = launch_scan(a, d, SCAN_FILTER, s, PROF_SCAN);
   if (rc) return rc;
+  sa.counts = cnt;
+  sa.cap = p.cap;
+  sa.n_total = n_local;
+  return launch_select(sa, SEL_KEYS64, SEL_TOPK, s);
+}
+
+// dist_filter over a shard in row chunks with ONE hit list and ONE select: chunk c = rows
+// [starts[c], starts[c + 1]) (host array, starts[0] = 0, starts[nchunks] = n_local) is one scan launch
+// (a grouped launch's query blocks stay in step over a chunk, so each tile comes from HBM once), every
+// chunk appends to the same per-query key lists (keys carry shard rows: row_base = the chunk's start),
+// and the select runs once over the shard's hits -- the packed lists equal drt_ip_topk_dist_filter's
+// over the whole shard.  (Round 5: replaces one select per chunk plus a merge of the chunks' lists.)
+// Chunks of a shard whose rows need the strided / wide-row kernels (d > 768) are not supported.
+int drt_ip_topk_dist_filter_chunks(const void* Q, int64_t nq, const void* P, int64_t n_local, int64_t n_global,
+                                   int32_t d, int32_t k, int64_t id_offset, const float* tau, uint64_t* packed,
+                                   const int64_t* starts, int32_t nchunks, void* ws, size_t ws_bytes, void* stream) {
+  DRT_REQUIRE(valid_dist_dims(nq, n_local, n_global, d, k));
+  DRT_REQUIRE(id_offset >= 0 && id_offset + n_local <= n_global);
+  DRT_REQUIRE(d <= 768 && n_local < ((int64_t)1 << 32));
+  DRT_REQUIRE(starts != nullptr && nchunks >= 1 && starts[0] == 0 && starts[nchunks] == n_local);
+  for (int c = 0; c < nchunks; ++c) DRT_REQUIRE(starts[c] <= starts[c + 1]);
+  if (nq == 0) return DRT_OK;
+  DRT_REQUIRE(Q && tau && packed && ws);
+  const TopkPlan p = make_dist_plan(nq, n_local, n_global, k);
+  DRT_REQUIRE(ws_bytes >= p.total);
+  hipStream_t s = (hipStream_t)stream;
+  char* w = (char*)ws;
+  uint32_t* cnt = (uint32_t*)(w + p.off_cnt);
+  SelectArgs sa{};
+  sa.in = w + p.off_keys;
+  sa.in_stride = p.cap;
+  sa.k = k;
+  sa.nq = nq;
+  sa.id_offset = id_offset;
+  sa.out_packed = packed;
+  sa.global_tau = true;
+  if (n_local == 0) {
+    sa.n_in = 0;
+    sa.n_total = 0;
+    return launch_select(sa, SEL_DENSE32, SEL_TOPK, s);
+  }
+  DRT_REQUIRE(P != nullptr);
+  DRT_CHECK_HIP(hipMemsetAsync(cnt, 0, p.nq_pad * 4 * kCntStride, s));
+  const int64_t target = std::max<int64_t>(4096, 4 * (int64_t)k);
+  for (int c = 0; c < nchunks; ++c) {
+    const int64_t r0 = starts[c], rows = starts[c + 1] - starts[c];
+    if (rows == 0) continue;
+    ScanArgs a{};
+    a.Q = (const __bf16*)Q;
+    a.nq = nq;
+    a.ldq = d;
+    a.P = (const __bf16*)P + r0 * d;
+    a.ldp = d;
+    a.row0 = 0;
+    a.nrows = rows;
+    a.rstride = 1;
+    a.tau = tau;
+    a.counts = cnt;
+    a.out = w + p.off_keys;
+    a.cap = p.cap;
+    a.exp_hits = p.sample ? std::max<int64_t>(1, target * rows / std::max<int64_t>(1, n_global)) : rows;
+    a.row_base = (uint32_t)r0;
+    const int rc = launch_scan(a, d, SCAN_FILTER, s, PROF_SCAN);
+    if (rc) return rc;
+  }
   sa.counts = cnt;
   sa.cap = p.cap;
   sa.n_total = n_local;

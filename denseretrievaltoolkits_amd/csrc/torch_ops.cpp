@@ -14,6 +14,8 @@
 //                                                                          l2_normalize
 // Fake (meta) kernels and the autograd formula of score_ce_fwd are registered from Python
 // (denseretrievaltoolkits_amd/ops.py).
+#include <vector>
+
 #include <torch/library.h>
 #include <ATen/ATen.h>
 #include <c10/core/DeviceGuard.h>
@@ -356,6 +358,33 @@ void dist_filter_into(const Tensor& q_, const Tensor& p_, int64_t n_global, int6
            "drt_ip_topk_dist_filter");
 }
 
+// dist_filter over the shard in row chunks (chunk c = rows [starts[c], starts[c + 1])): one scan launch per
+// chunk, one hit list and one select -- the same packed lists as dist_filter_into over the whole shard.
+void dist_filter_chunks_into(const Tensor& q_, const Tensor& p_, int64_t n_global, int64_t k, int64_t id_offset,
+                             const Tensor& tau_, at::IntArrayRef starts, Tensor& packed) {
+  need(q_, "q", at::kBFloat16, 2);
+  need(p_, "p", at::kBFloat16, 2);
+  need(tau_, "tau", at::kFloat, 1);
+  need(packed, "packed", at::kLong, 2);
+  const c10::DeviceGuard g(q_.device());
+  const Tensor q = q_.contiguous(), p = p_.contiguous(), tau = tau_.contiguous();
+  TORCH_CHECK_VALUE(tau.size(0) == q.size(0), "tau must hold one threshold per query");
+  TORCH_CHECK_VALUE(packed.is_contiguous() && packed.size(0) == q.size(0) && packed.size(1) == k + 1,
+                    "packed must be a contiguous [nq, k + 1] tensor");
+  TORCH_CHECK_VALUE(starts.size() >= 2 && starts.front() == 0 && starts.back() == p.size(0),
+                    "starts must run from 0 to the shard's row count");
+  for (size_t c = 1; c < starts.size(); ++c) TORCH_CHECK_VALUE(starts[c - 1] <= starts[c], "starts must not decrease");
+  TORCH_CHECK_VALUE(q.size(1) <= 768, "chunked filtering takes d <= 768");
+  size_t wsb = 0;
+  Tensor ws = dist_ws(q, p.size(0), n_global, k, &wsb);
+  const std::vector<int64_t> st(starts.begin(), starts.end());
+  check_rc(drt_ip_topk_dist_filter_chunks(q.data_ptr(), q.size(0), p.size(0) ? p.data_ptr() : nullptr, p.size(0),
+                                          n_global, (int32_t)q.size(1), (int32_t)k, id_offset,
+                                          tau.data_ptr<float>(), (uint64_t*)packed.data_ptr<int64_t>(), st.data(),
+                                          (int32_t)st.size() - 1, ws.data_ptr(), wsb, stream_of(q)),
+           "drt_ip_topk_dist_filter_chunks");
+}
+
 // dist_filter_lists for query rows [q0, q0 + nq) of lists [nlists, NQ, r] gathered for a group of
 // batches, writing the packed lists into `packed` ([nq, k + 1], e.g. a row slice of a group buffer).
 void dist_filter_lists_into(const Tensor& q_, const Tensor& p_, int64_t n_global, int64_t k, int64_t id_offset,
@@ -568,6 +597,8 @@ TORCH_LIBRARY(drt, m) {
   m.def("dist_filter_lists_into(Tensor q, Tensor p, int n_global, int k, int id_offset, Tensor lists, int q0, "
         "Tensor(a!) packed) -> ()");
   m.def("dist_filter_into(Tensor q, Tensor p, int n_global, int k, int id_offset, Tensor tau, Tensor(a!) packed) -> ()");
+  m.def("dist_filter_chunks_into(Tensor q, Tensor p, int n_global, int k, int id_offset, Tensor tau, int[] starts, "
+        "Tensor(a!) packed) -> ()");
   m.def("merge_packed(Tensor parts, int k, int n_global, int k_cert=-1) -> (Tensor, Tensor, Tensor)");
   m.def("score_ce_fwd(Tensor q, Tensor p, int target_stride, float scale) -> (Tensor, Tensor, Tensor)");
   m.def("score_ce_bwd(Tensor grad, Tensor q, Tensor p, Tensor scores, Tensor lse, int target_stride, "
@@ -584,6 +615,7 @@ TORCH_LIBRARY(drt, m) {
 TORCH_LIBRARY_IMPL(drt, CUDA, m) {   // the GPU dispatch key of torch-ROCm
   m.impl("ip_topk", &ip_topk);
   m.impl("ip_topk.out", &ip_topk_out);
+  m.impl("dist_filter_chunks_into", &dist_filter_chunks_into);
   m.impl("ip_topk_resolve", &ip_topk_resolve);
   m.impl("ip_topk_resolve_wide", &ip_topk_resolve_wide);
   m.impl("row_stats", &row_stats);

@@ -173,6 +173,14 @@ def dist_filter_into(q: torch.Tensor, p: torch.Tensor, n_global: int, k: int, id
     ops.load().dist_filter_into(q, p, n_global, k, id_offset, tau, packed)
 
 
+def dist_filter_chunks_into(q: torch.Tensor, p: torch.Tensor, n_global: int, k: int, id_offset: int,
+                            tau: torch.Tensor, starts, packed: torch.Tensor) -> None:
+    """dist_filter_into over ``p`` in row chunks [starts[c], starts[c + 1]) (one scan launch each), one hit
+    list and one select: the packed lists equal dist_filter_into's over all of ``p`` (d <= 768)."""
+    _require_device(q, p, tau, packed)
+    ops.load().dist_filter_chunks_into(q, p, n_global, k, id_offset, tau, [int(x) for x in starts], packed)
+
+
 def dist_filter_lists_into(q: torch.Tensor, p: torch.Tensor, n_global: int, k: int, id_offset: int,
                            lists: torch.Tensor, q0: int, packed: torch.Tensor) -> None:
     """dist_filter_lists for the query rows [q0, q0 + nq) of lists [nlists, NQ, r] gathered for a

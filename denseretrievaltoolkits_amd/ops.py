@@ -10,7 +10,8 @@ formula of the fused score + cross-entropy op.
     torch.ops.drt.ip_topk_resolve(q, p, k, off, s, i, st, stats) -> n_resolved  (in place, synchronous)
     torch.ops.drt.row_stats / refine_delta / refine_sort  (canonical exact-score order, include/drt.h)
     torch.ops.drt.topk_merge(scores, ids, k_out)        -> (scores, ids)           utils.py:215-229
-    torch.ops.drt.dist_sample / dist_tau / dist_filter / dist_filter_lists / merge_packed  (sharded, §8e)
+    torch.ops.drt.dist_sample / dist_tau / dist_filter / dist_filter_chunks_into / dist_filter_lists / merge_packed
+                                                                                            (sharded, §8e)
     torch.ops.drt.score_ce_fwd(q, p, stride, scale)     -> (loss, scores, lse)     biencoder.py:107-119
     torch.ops.drt.score_ce_bwd(g, q, p, scores, lse, stride, scale) -> (dq, dp)
     torch.ops.drt.embed_ln / linear / attention / layernorm / pool / l2_normalize  (BertModel pieces)
@@ -108,6 +109,10 @@ def _register_python_parts():
 
     @lib.register_fake("drt::dist_filter_into")
     def _(q, p, n_global, k, id_offset, tau, packed):
+        return None
+
+    @lib.register_fake("drt::dist_filter_chunks_into")
+    def _(q, p, n_global, k, id_offset, tau, starts, packed):
         return None
 
     @lib.register_fake("drt::dist_filter_lists_into")

@@ -162,18 +162,25 @@ def _gtau_enqueue_group(local, qs, k: int, n_global: int, offset: int, gather, t
     the shards keep kc = refine_width(k) candidates each, the merge keeps kc, and the canonical
     stage (kernels.refine, deltas summed across shards by ``all_reduce_sum``) orders the top-k.
     ``id_shift`` is added to every returned id (a one-GPU index searched with an id offset: the
-    protocol itself runs on the index's own row numbers, packed in 32 bits).  ``chunks`` (one GPU:
-    ``gather`` is the identity stack): the filter runs as one launch per row range (group_chunks),
-    whose packed lists are merged as parts."""
+    protocol itself runs on the index's own row numbers, packed in 32 bits).  ``chunks``: the filter runs as
+    one launch per row range of this shard (group_chunks) and the chunks' hits are selected once
+    (kernels.dist_filter_chunks_into; d > 768: each chunk's packed lists are a part of the merge, gathered
+    [world, chunks, ...] -- the same chunk count on every rank)."""
     sizes = [q.shape[0] for q in qs]
     qg = qs[0] if len(qs) == 1 else torch.cat(qs)
     best = local.dist_sample(qg, n_global, k)                       # [Qg, r]
     lists = gather(best).contiguous()                               # [world, Qg, r]
     tau = kernels.dist_tau(lists, k)                                # [Qg]: one launch for the group
     kc = kernels.refine_width(k) if stats is not None else k
-    if chunks is not None and len(chunks) > 1:
+    if chunks is not None and len(chunks) > 1 and qg.shape[1] <= 768:
         # long shard: one filter launch per row chunk (the group's query blocks stay in step over a
-        # chunk, so its tiles are read from HBM once), every chunk's lists a part of the merge
+        # chunk, so its tiles are read from HBM once), all chunks' hits in one list, one select
+        packed = torch.empty((qg.shape[0], kc + 1), dtype=torch.int64, device=qg.device)
+        starts = [a for a, _ in chunks] + [chunks[-1][1]]
+        kernels.dist_filter_chunks_into(qg, local.rows, n_global, kc, offset, tau, starts, packed)
+        s, i, st = kernels.merge_packed(gather(packed), kc, n_global, k_cert=k)
+    elif chunks is not None and len(chunks) > 1:
+        # (wider rows) one filter launch + select per chunk, every chunk's lists a part of the merge
         parts = torch.empty((len(chunks), qg.shape[0], kc + 1), dtype=torch.int64, device=qg.device)
         for c, (a, b) in enumerate(chunks):
             kernels.dist_filter_into(qg, local.rows[a:b], n_global, kc, offset + a, tau, parts[c])

@@ -181,6 +181,15 @@ int drt_ip_topk_dist_filter(const void* Q, int64_t nq, const void* P, int64_t n_
                             int64_t n_global, int32_t d, int32_t k, int64_t id_offset,
                             const float* tau, uint64_t* packed, void* ws, size_t ws_bytes,
                             void* stream);
+/* 4 over a shard in row chunks (d <= 768, n_local < 2^32): chunk c = rows [starts[c], starts[c + 1])
+ * (host array of nchunks + 1 entries, starts[0] = 0, starts[nchunks] = n_local) is one filter scan
+ * launch, all chunks append to one hit list and one select emits this shard's packed top-k -- the
+ * same lists as drt_ip_topk_dist_filter over the whole shard (workspace: drt_ip_topk_dist_workspace
+ * for n_local).  A group of query batches keeps its query blocks in step over each chunk. */
+int drt_ip_topk_dist_filter_chunks(const void* Q, int64_t nq, const void* P, int64_t n_local,
+                                   int64_t n_global, int32_t d, int32_t k, int64_t id_offset,
+                                   const float* tau, uint64_t* packed, const int64_t* starts,
+                                   int32_t nchunks, void* ws, size_t ws_bytes, void* stream);
 /* 3+4 fused: tau from the gathered lists [nlists][nq][r] (written to tau_out when it is not
  * NULL) and this shard's packed top-k, with the hit counters zeroed by the threshold kernel
  * (3 launches).  Same results as drt_ip_topk_dist_tau followed by drt_ip_topk_dist_filter. */

@@ -165,3 +165,36 @@ def test_merge_packed_vs_oracle(dev, nparts, nq, k, fill, count_word):
     np.testing.assert_array_equal(i.cpu().numpy(), ei)
     np.testing.assert_array_equal(s.cpu().numpy(), es)
     np.testing.assert_array_equal(st.cpu().numpy(), est)
+
+
+@pytest.mark.parametrize("nq,n,d,k,starts", [
+    (300, 50011, 768, 1000, [0, 12000, 12000, 30001, 50011]),   # 32-query kernel, an empty chunk, ragged
+    (128, 40000, 768, 100, [0, 16, 20000, 40000]),               # 16-query kernel, a one-tile chunk
+    (513, 30000, 128, 200, [0, 7, 29993, 30000]),                # partial tiles at both chunk edges
+    (64, 5000, 768, 10, [0, 5000]),                              # one chunk
+])
+def test_dist_filter_chunks_equals_whole_shard(dev, nq, n, d, k, starts):
+    """kernels.dist_filter_chunks_into (one scan launch per chunk, one hit list, one select -- the grouped
+    search's chunked filter) returns the packed lists of dist_filter_into over the whole shard, bit for
+    bit, on integer data (exact scores) and on Gaussian data (same fp32 chains)."""
+    import torch
+    from denseretrievaltoolkits_amd import kernels
+    rng = np.random.default_rng(nq + n + d)
+    for data in ("int", "gauss"):
+        if data == "int":
+            q = int_bf16(rng, (nq, d), -4, 4)
+            p = int_bf16(rng, (n, d), -4, 4)
+        else:
+            q = gauss_bf16(rng, (nq, d))
+            p = gauss_bf16(rng, (n, d))
+        qt, pt = to_dev_bf16(q, dev), to_dev_bf16(p, dev)
+        n_global = 8 * n   # a shard of a larger corpus: sampled threshold, id offset
+        off = 3 * n
+        lists = kernels.dist_sample(qt, pt, n_global, k).unsqueeze(0)
+        tau = kernels.dist_tau(lists, k)
+        whole = torch.empty((nq, k + 1), dtype=torch.int64, device=dev)
+        kernels.dist_filter_into(qt, pt, n_global, k, off, tau, whole)
+        chunked = torch.full((nq, k + 1), -7, dtype=torch.int64, device=dev)
+        kernels.dist_filter_chunks_into(qt, pt, n_global, k, off, tau, starts, chunked)
+        torch.cuda.synchronize()
+        assert torch.equal(chunked, whole), data
