@@ -66,6 +66,8 @@ _SIGNATURES = [
                                          c_vp, c_sz, c_vp, c_vp]),
     ("drt_refine_delta_bf16", c_i32, [c_vp, c_i64, c_i32, c_vp, c_i64, c_i64, c_vp, c_vp, c_i32, c_i32, c_vp, c_vp,
                                       c_vp, c_vp, c_vp, c_vp]),
+    ("drt_refine_delta_local_bf16", c_i32, [c_vp, c_i64, c_i32, c_vp, c_i64, c_i64, c_vp, c_vp, c_i32, c_i32, c_vp,
+                                            c_vp, c_vp, c_vp, c_vp, c_vp]),
     ("drt_refine_sort", c_i32, [c_vp, c_vp, c_vp, c_vp, c_i64, c_i32, c_i32, c_vp, c_vp, c_vp]),
     ("drt_gemm_nt_bf16_f32", c_i32, [c_vp, c_vp, c_vp, c_i64, c_i64, c_i32, c_i64, c_vp]),
     ("drt_embed_ln", c_i32, [c_vp, c_vp, c_i64, c_i64, c_vp, c_vp, c_vp, c_vp, c_vp, c_f32, c_i32, c_vp, c_vp]),

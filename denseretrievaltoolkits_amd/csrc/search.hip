@@ -3433,9 +3433,10 @@ int32_t drt_refine_width(int32_t k) {
   return (int32_t)refine_width(k);
 }
 
-int drt_refine_delta_bf16(const void* Q, int64_t nq, int32_t d, const void* P, int64_t n_local, int64_t row_offset,
-                          const float* cand_s, const int64_t* cand_i, int32_t kc, int32_t k, const float* stats,
-                          const float* tau, float* delta, int32_t* cnt, int32_t* status, void* stream) {
+static int refine_delta_impl(const void* Q, int64_t nq, int32_t d, const void* P, int64_t n_local, int64_t row_offset,
+                             const float* cand_s, const int64_t* cand_i, int32_t kc, int32_t k, const float* stats,
+                             const float* tau, float* delta, int32_t* cnt, int32_t* status, void* stream,
+                             bool local) {
   DRT_REQUIRE(nq >= 0 && d > 0 && d % 64 == 0 && d <= 1024 && k >= 1 && kc >= k && kc <= kSelMaxK && n_local >= 0);
   if (nq == 0) return DRT_OK;
   DRT_REQUIRE(Q && cand_s && cand_i && stats && delta && cnt && (P || n_local == 0));
@@ -3457,10 +3458,30 @@ int drt_refine_delta_bf16(const void* Q, int64_t nq, int32_t d, const void* P, i
   ra.status = status;
   hipStream_t s = (hipStream_t)stream;
   hipLaunchKernelGGL(refine_prep_kernel, dim3((unsigned)nq), dim3(kRefThreads), 0, s, ra);
-  ra.slice = kRefSliceShard;   // the sharded protocol's entry: most candidates live on other shards
-  hipLaunchKernelGGL(refine_delta_kernel, dim3((unsigned)nq, (unsigned)((kc + ra.slice - 1) / ra.slice)),
-                     dim3(kRefThreads), 0, s, ra);
+  if (local) {   // one shard holds every candidate: waves walk the window directly (no compaction)
+    hipLaunchKernelGGL(refine_delta_local_kernel, dim3((unsigned)nq, (unsigned)((kc + kRefSlice - 1) / kRefSlice)),
+                       dim3(kRefThreads), 0, s, ra);
+  } else {
+    ra.slice = kRefSliceShard;   // the sharded protocol's entry: most candidates live on other shards
+    hipLaunchKernelGGL(refine_delta_kernel, dim3((unsigned)nq, (unsigned)((kc + ra.slice - 1) / ra.slice)),
+                       dim3(kRefThreads), 0, s, ra);
+  }
   return hip_status(hipGetLastError());
+}
+
+int drt_refine_delta_bf16(const void* Q, int64_t nq, int32_t d, const void* P, int64_t n_local, int64_t row_offset,
+                          const float* cand_s, const int64_t* cand_i, int32_t kc, int32_t k, const float* stats,
+                          const float* tau, float* delta, int32_t* cnt, int32_t* status, void* stream) {
+  return refine_delta_impl(Q, nq, d, P, n_local, row_offset, cand_s, cand_i, kc, k, stats, tau, delta, cnt, status,
+                           stream, false);
+}
+
+int drt_refine_delta_local_bf16(const void* Q, int64_t nq, int32_t d, const void* P, int64_t n_local,
+                                int64_t row_offset, const float* cand_s, const int64_t* cand_i, int32_t kc, int32_t k,
+                                const float* stats, const float* tau, float* delta, int32_t* cnt, int32_t* status,
+                                void* stream) {
+  return refine_delta_impl(Q, nq, d, P, n_local, row_offset, cand_s, cand_i, kc, k, stats, tau, delta, cnt, status,
+                           stream, true);
 }
 
 int drt_refine_sort(const float* cand_s, const int64_t* cand_i, const float* delta, const int32_t* cnt, int64_t nq,

@@ -203,7 +203,7 @@ Tensor row_stats(const Tensor& p_, const c10::optional<Tensor>& prev) {
 // canonical-order stage on a candidate list [nq, kc] (drt_refine_delta_bf16); status updated in place
 std::tuple<Tensor, Tensor> refine_delta(const Tensor& q_, const Tensor& p_, int64_t row_offset, const Tensor& cs_,
                                         const Tensor& ci_, int64_t k, const Tensor& stats,
-                                        const c10::optional<Tensor>& tau_, Tensor& status) {
+                                        const c10::optional<Tensor>& tau_, Tensor& status, bool local) {
   need(q_, "q", at::kBFloat16, 2);
   need(p_, "p", at::kBFloat16, 2);
   need(cs_, "cand_scores", at::kFloat, 2);
@@ -222,11 +222,12 @@ std::tuple<Tensor, Tensor> refine_delta(const Tensor& q_, const Tensor& p_, int6
   }
   Tensor delta = at::empty({nq, kc}, cs.options());
   Tensor cnt = at::empty({nq, 2}, cs.options().dtype(at::kInt));
-  check_rc(drt_refine_delta_bf16(q.data_ptr(), nq, (int32_t)q.size(1), p.size(0) ? p.data_ptr() : nullptr, p.size(0),
-                                 row_offset, cs.data_ptr<float>(), ci.data_ptr<int64_t>(), (int32_t)kc, (int32_t)k,
-                                 stats_ptr(stats, q), tau.defined() ? tau.data_ptr<float>() : nullptr,
-                                 delta.data_ptr<float>(), cnt.data_ptr<int32_t>(), status.data_ptr<int32_t>(),
-                                 stream_of(q)),
+  // local: every candidate is a row of p (one GPU) -- drt_refine_delta_local_bf16, identical deltas
+  check_rc((local ? drt_refine_delta_local_bf16 : drt_refine_delta_bf16)(
+               q.data_ptr(), nq, (int32_t)q.size(1), p.size(0) ? p.data_ptr() : nullptr, p.size(0), row_offset,
+               cs.data_ptr<float>(), ci.data_ptr<int64_t>(), (int32_t)kc, (int32_t)k, stats_ptr(stats, q),
+               tau.defined() ? tau.data_ptr<float>() : nullptr, delta.data_ptr<float>(), cnt.data_ptr<int32_t>(),
+               status.data_ptr<int32_t>(), stream_of(q)),
            "drt_refine_delta_bf16");
   return {delta, cnt};
 }
@@ -587,7 +588,7 @@ TORCH_LIBRARY(drt, m) {
         "Tensor(c!) status, Tensor stats) -> int");
   m.def("row_stats(Tensor p, Tensor? prev=None) -> Tensor");
   m.def("refine_delta(Tensor q, Tensor p, int row_offset, Tensor cand_scores, Tensor cand_ids, int k, Tensor stats, "
-        "Tensor? tau, Tensor(a!) status) -> (Tensor, Tensor)");
+        "Tensor? tau, Tensor(a!) status, bool local=False) -> (Tensor, Tensor)");
   m.def("refine_sort(Tensor cand_scores, Tensor cand_ids, Tensor delta, Tensor cnt, int k) -> (Tensor, Tensor)");
   m.def("topk_merge(Tensor scores, Tensor ids, int k_out) -> (Tensor, Tensor)");
   m.def("dist_sample(Tensor q, Tensor p, int n_global, int k) -> Tensor");

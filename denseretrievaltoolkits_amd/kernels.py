@@ -114,7 +114,8 @@ def refine(q: torch.Tensor, p: torch.Tensor, row_offset: int, cand_s: torch.Tens
     the fp32 top-k in the fp32 order."""
     _require_device(q, p, cand_s, cand_i, stats, status)
     drt = ops.load()
-    delta, cnt = drt.refine_delta(q, p, row_offset, cand_s, cand_i, k, stats, tau, status)
+    # one GPU (no all-reduce): every candidate is a row of p -- the local delta kernel
+    delta, cnt = drt.refine_delta(q, p, row_offset, cand_s, cand_i, k, stats, tau, status, all_reduce_sum is None)
     if all_reduce_sum is not None:
         all_reduce_sum(delta)
     return drt.refine_sort(cand_s, cand_i, delta, cnt, k)

@@ -76,7 +76,7 @@ def _register_python_parts():
         return p.new_empty((ROW_STATS_LEN,), dtype=torch.float32)
 
     @lib.register_fake("drt::refine_delta")
-    def _(q, p, row_offset, cand_scores, cand_ids, k, stats, tau, status):
+    def _(q, p, row_offset, cand_scores, cand_ids, k, stats, tau, status, local=False):
         return cand_scores.new_empty(cand_scores.shape), cand_scores.new_empty((cand_scores.shape[0], 2),
                                                                                  dtype=torch.int32)
 

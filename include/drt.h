@@ -123,6 +123,12 @@ int drt_refine_delta_bf16(const void* Q, int64_t nq, int32_t d, const void* P, i
                           int64_t row_offset, const float* cand_s, const int64_t* cand_i, int32_t kc,
                           int32_t k, const float* stats, const float* tau, float* delta, int32_t* cnt,
                           int32_t* status, void* stream);
+/* The same for an index whose single shard holds every candidate (one GPU): identical deltas, the
+ * exact sums computed by waves walking the window directly instead of compacting owned rows. */
+int drt_refine_delta_local_bf16(const void* Q, int64_t nq, int32_t d, const void* P, int64_t n_local,
+                                int64_t row_offset, const float* cand_s, const int64_t* cand_i, int32_t kc,
+                                int32_t k, const float* stats, const float* tau, float* delta, int32_t* cnt,
+                                int32_t* status, void* stream);
 int drt_refine_sort(const float* cand_s, const int64_t* cand_i, const float* delta, const int32_t* cnt,
                     int64_t nq, int32_t kc, int32_t k, float* out_scores, int64_t* out_ids, void* stream);
 

@@ -296,3 +296,37 @@ def test_exact_order_degenerate_near_ties_bit_exact(dev, grouped):
     np.testing.assert_array_equal(torch.cat([r[1] for r in res]).cpu().numpy(), ei)
     _assert_scores(torch.cat([r[0] for r in res]).cpu().numpy(), es)
     assert idx.order_uncertified == 0 and idx.wide_resolved == nq
+
+
+@pytest.mark.parametrize("row_offset", [0, 5000])
+def test_refine_delta_local_equals_sharded(dev, row_offset):
+    """drt_refine_delta_local_bf16 (one shard holds every candidate: the one-GPU grouped search) writes
+    the same deltas, window sizes and status as the sharded entry, on Gaussian rows with a candidate list
+    of width refine_width(k); candidates outside [row_offset, row_offset + n) get delta 0 in both."""
+    import torch
+    from denseretrievaltoolkits_amd import kernels, ops
+    rng = np.random.default_rng(71 + row_offset)
+    nq, n, d, k = 96, 20000, 768, 200
+    q = to_dev_bf16(gauss_bf16(rng, (nq, d)), dev)
+    p = to_dev_bf16(gauss_bf16(rng, (n, d)), dev)
+    kc = kernels.refine_width(k)
+    cs, ci = (q.float() @ p.float().T).topk(kc, dim=1)
+    ci = ci + row_offset
+    if row_offset:   # a few candidates another shard would own
+        ci[:, -3:] = row_offset + n + 7
+    stats = kernels.row_stats(p)
+    drt = ops.load()
+    outs = []
+    for local in (False, True):
+        st = torch.zeros(nq, dtype=torch.int32, device=dev)
+        delta, cnt = drt.refine_delta(q, p, row_offset, cs.contiguous(), ci.contiguous(), k, stats, None, st, local)
+        torch.cuda.synchronize()
+        outs.append((delta.cpu(), cnt.cpu(), st.cpu()))
+    (d0, c0, s0), (d1, c1, s1) = outs
+    assert torch.equal(c0, c1) and torch.equal(s0, s1)
+    win = c0[:, 0]
+    for qi in range(nq):   # deltas are defined inside each query's window
+        w = int(win[qi])
+        if w > 0:
+            assert torch.equal(d0[qi, :w], d1[qi, :w]), qi
+    assert (win > 0).any()
