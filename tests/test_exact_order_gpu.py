@@ -330,3 +330,32 @@ def test_refine_delta_local_equals_sharded(dev, row_offset):
         if w > 0:
             assert torch.equal(d0[qi, :w], d1[qi, :w]), qi
     assert (win > 0).any()
+
+
+def test_reset_drops_row_statistics(dev):
+    """(round-4 advisor) reset() must drop the row statistics: an index searched over integer rows (exact
+    fp32 scores: the integer flag lets the canonical stage skip the near-tie window), reset and refilled
+    with at least as many Gaussian rows of larger norm, must rescan them -- ids equal the fp64 oracle."""
+    import torch
+    from helpers import oracle_topk_streamed
+    from denseretrievaltoolkits_amd.search import FlatIPIndex
+    rng = np.random.default_rng(97)
+    nq, n, d, k = 32, 30000, 768, 100
+    idx = FlatIPIndex(d, device=dev)
+    idx.add(to_dev_bf16(int_bf16(rng, (n, d), -1, 1), dev))
+    qi = int_bf16(rng, (nq, d), -1, 1)
+    s0, _ = idx.search_device(to_dev_bf16(qi, dev), k)
+    torch.cuda.synchronize()
+    st0 = idx.row_stats().cpu().numpy()
+    assert st0[1] == 1.0   # integer rows
+    idx.reset()
+    p = gauss_bf16(rng, (n + 5000, d)) * 3.0
+    pd = to_dev_bf16(p, dev)
+    idx.add(pd)
+    st1 = idx.row_stats().cpu().numpy()
+    assert st1[1] == 0.0 and st1[0] > st0[0]
+    q = gauss_bf16(rng, (nq, d))
+    s, i = idx.search_device(to_dev_bf16(q, dev), k)
+    torch.cuda.synchronize()
+    es, ei = oracle_topk_streamed(q, pd, k, exact=True)
+    np.testing.assert_array_equal(i.cpu().numpy(), ei)
