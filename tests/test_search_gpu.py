@@ -111,7 +111,7 @@ def test_flat_index_enqueue_batches_grouped(dev, monkeypatch, chunk):
 
 
 @pytest.mark.parametrize("case,chunk", [("int", 0), ("gauss", 0), ("ties", 0), ("int", 37_000), ("gauss", 45_000),
-                                        ("ties", 20_000)])
+                                        ("ties", 20_000), ("int1024", 30_000)])
 def test_flat_index_search_batches_grouped(dev, case, chunk, monkeypatch):
     """FlatIPIndex.search_batches in groups (one sample launch + one merge per group, the group's
     filter as one launch or, on a long shard, one launch per row chunk whose lists are merged as
@@ -127,6 +127,8 @@ def test_flat_index_search_batches_grouped(dev, case, chunk, monkeypatch):
         q, p, k = int_bf16(rng, (150, 768), -4, 4), int_bf16(rng, (120001, 768), -4, 4), 1000
     elif case == "gauss":
         q, p, k = gauss_bf16(rng, (100, 768)), gauss_bf16(rng, (200000, 768)), 1000
+    elif case == "int1024":   # rows wider than 768: each chunk its own filter + select, merged as parts
+        q, p, k = int_bf16(rng, (70, 1024), -4, 4), int_bf16(rng, (90001, 1024), -4, 4), 500
     else:
         q, p, k = int_bf16(rng, (10, 256), -3, 3), np.repeat(int_bf16(rng, (1, 256), -3, 3), 50000, axis=0), 100
     idx = srch.FlatIPIndex.from_rows(to_dev_bf16(p, dev))
@@ -146,7 +148,7 @@ def test_flat_index_search_batches_grouped(dev, case, chunk, monkeypatch):
     else:
         np.testing.assert_array_equal(gi, ei)
         np.testing.assert_array_equal(gs, es)
-        assert idx.group_fallbacks == (0 if case == "int" else 3)
+        assert idx.group_fallbacks == (0 if case in ("int", "int1024") else 3)
 
 
 def test_ip_topk_gaussian_tolerance(dev):
