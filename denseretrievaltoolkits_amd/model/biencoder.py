@@ -53,12 +53,11 @@ _FALLBACK_LOGGED = set()
 
 
 def _log_fallback(why: str):
-    """Once per reason: a differentiable encode that cannot take the HIP training tower runs the HF
-    module under torch autograd (the reference's own arithmetic) -- say so instead of silently."""
+    """Once per reason: an encode that cannot take the HIP towers runs the HF module under torch
+    (the reference's own arithmetic) -- say so instead of silently."""
     if why not in _FALLBACK_LOGGED:
         _FALLBACK_LOGGED.add(why)
-        logger.warning("DRModel.encode with autograd: HF module under torch autograd, not the HIP training "
-                       "tower (%s)", why)
+        logger.warning("DRModel.encode: HF module under torch, not the HIP tower (%s)", why)
 
 
 def _torch_mean_pooling(h, mask):
@@ -168,9 +167,9 @@ class DRModel(nn.Module):
             raise NotImplementedError("T5 towers are outside the MI355X hot path (BERT-family encoders only)")
         if self.pooling not in ("first", "mean", "max"):
             raise ValueError("Unknown pooling type: {}".format(self.pooling))
-        if self._use_hip(model):
-            if self.feature != "last_hidden_state":
-                raise NotImplementedError(f"feature {self.feature!r}: only last_hidden_state is on the HIP path")
+        # a feature other than last_hidden_state (arguments.py:34-37) is off the HIP path in both modes:
+        # it takes the HF module below, with the reason logged, whether or not autograd is on
+        if self._use_hip(model) and self.feature == "last_hidden_state":
             enc = self._hip_encoder(model)
             hidden = enc(items["input_ids"], items.get("attention_mask"), items.get("token_type_ids"))
             reps, rb = enc.pool(hidden, items.get("attention_mask"), self.pooling, want_bf16=head is not None)
@@ -183,10 +182,10 @@ class DRModel(nn.Module):
         # (saved bf16 activations + backward on HIP kernels, HF dropout semantics in train mode,
         # model/train_tower.py); anything else keeps the HF module under autograd.
         why = None
-        if not self.hip_train:
-            why = "hip_train = False"
-        elif self.feature != "last_hidden_state":
+        if self.feature != "last_hidden_state":
             why = f"feature {self.feature!r}"
+        elif not self.hip_train:
+            why = "hip_train = False"
         elif not next(model.parameters()).is_cuda:
             why = "tower on the CPU"
         elif items["input_ids"].shape[1] > MAX_TRAIN_SEQ:
