@@ -2700,7 +2700,18 @@ struct WideArgs {
   float* out_s;           // [*, k] (rows through qmap)
   int64_t* out_i;
   int32_t* status;
+  // large-k path (drt_ip_topk_large): qmap == nullptr maps chunk query j to output row q0 + j; tau_in
+  // is a per-output-row lower bound of the k-th fp32 score; sel_* hold each query's selected entries
+  int64_t q0;
+  const float* tau_in;
+  uint64_t* sel_k;
+  uint32_t* sel_r;
+  uint32_t* sel_n;
 };
+
+__device__ __forceinline__ int64_t wide_out_row(const WideArgs& w, int j) {
+  return w.qmap ? (int64_t)w.qmap[j] : w.q0 + j;
+}
 
 __global__ __launch_bounds__(kRefThreads) void wide_prep_kernel(WideArgs w) {
   __shared__ float fscr[kRefThreads / 64];
@@ -2716,9 +2727,11 @@ __global__ __launch_bounds__(kRefThreads) void wide_prep_kernel(WideArgs w) {
   }
   const float eps = refine_eps(w.ra, j, fscr, iscr, dscr);
   if (threadIdx.x == 0) {
-    const int64_t orow = w.qmap[j];
-    w.tau[j] = w.out_s[orow * w.k + w.k - 1] - 2.0f * eps;
+    const int64_t orow = wide_out_row(w, j);
+    const float sk = w.tau_in ? w.tau_in[orow] : w.out_s[orow * w.k + w.k - 1];
+    w.tau[j] = sk - 2.0f * eps;
     w.counts[j * kCntStride] = 0u;
+    if (w.tau_in) w.status[orow] = 2;   // large path: cleared once the query's set is ranked
   }
 }
 
@@ -2880,6 +2893,106 @@ __global__ __launch_bounds__(kWideThreads) void wide_select_kernel(WideArgs w) {
     oi[i] = -1;
   }
   if (threadIdx.x == 0 && m == keff) w.status[orow] &= ~2;
+}
+
+// ---------------------------------------------------------------------------
+// Large k (2048 < k <= kLargeMaxK; faiss IndexFlatIP answers any k, the reference's retrieve_num is a
+// free flag: arguments.py:195, trainer.py:296-297).  The wide resolve's machinery with a threshold
+// from outside: the caller passes tau_q <= the query's k-th fp32 score (the host takes the minimum of
+// the m-th scores of C disjoint row ranges, C * m >= k), the filter collects every row with fp32
+// score >= tau_q - 2 eps (it holds the exact top-k, see the bound above), wide_exact_kernel computes
+// their exact sums, large_select_kernel finds the k-th (exact key, row) by the two radix selects and
+// compacts the k selected entries, large_rank_kernel ranks each by counting over LDS tiles of the
+// selected set.  Output: the canonical order (exact score desc, id asc), scores = exact sums rounded to
+// fp32, rows past n padded like ip_topk; status 0, or 2 when the collected set overflowed kWideCap.
+// ---------------------------------------------------------------------------
+constexpr int32_t kLargeMaxK = 32768;
+constexpr int kLargeThreads = 1024;
+constexpr int kLargeTile = 2048;   // selected entries per LDS tile of the rank count
+
+__global__ __launch_bounds__(kWideThreads) void large_select_kernel(WideArgs w) {
+  __shared__ uint32_t hist[256];
+  __shared__ uint64_t sh[2];
+  __shared__ uint32_t ns;
+  const int j = blockIdx.x;
+  if (j >= w.nb) return;
+  const uint32_t c = w.counts[j * kCntStride];
+  if (c > (uint64_t)w.cap) {
+    if (threadIdx.x == 0) w.sel_n[j] = 0xFFFFFFFFu;
+    return;
+  }
+  const int64_t nh = c;
+  const uint64_t* kj = w.keys + (int64_t)j * w.cap;
+  const uint64_t* ej = w.ekeys + (int64_t)j * w.cap;
+  const int64_t keff = std::min<int64_t>(w.k, nh);
+  uint64_t kstar = 0, rstar = 0;
+  if (keff > 0) {
+    int64_t want = keff;
+    kstar = wide_radix_select(nh, 64, [&](int64_t h, bool& take) { take = true; return ej[h]; }, hist, sh, want);
+    const uint64_t ks = kstar;
+    rstar = wide_radix_select(nh, 32, [&](int64_t h, bool& take) {
+      take = ej[h] == ks;
+      return (uint64_t)(uint32_t)kj[h];
+    }, hist, sh, want);
+  }
+  if (threadIdx.x == 0) ns = 0u;
+  __syncthreads();
+  uint64_t* sk = w.sel_k + (int64_t)j * w.k;
+  uint32_t* sr = w.sel_r + (int64_t)j * w.k;
+  for (int64_t h = threadIdx.x; h < nh && keff > 0; h += kWideThreads) {
+    const uint64_t ek = ej[h];
+    const uint64_t row = (uint32_t)kj[h];
+    if (ek < kstar || (ek == kstar && row <= rstar)) {
+      const uint32_t pos = atomicAdd(&ns, 1u);
+      if (pos < (uint32_t)keff) {
+        sk[pos] = ek;
+        sr[pos] = (uint32_t)row;
+      }
+    }
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) w.sel_n[j] = ns == (uint32_t)keff ? ns : 0xFFFFFFFFu;
+}
+
+// grid (queries, ceil(k / kLargeThreads)): entry i of the selected set goes to rank = #entries before it
+__global__ __launch_bounds__(kLargeThreads) void large_rank_kernel(WideArgs w) {
+  __shared__ uint64_t tk[kLargeTile];
+  __shared__ uint32_t tr[kLargeTile];
+  const int j = blockIdx.x;
+  if (j >= w.nb) return;
+  const uint32_t m = w.sel_n[j];
+  if (m == 0xFFFFFFFFu) return;   // overflow: status stays 2
+  const int64_t orow = wide_out_row(w, j);
+  const uint64_t* sk = w.sel_k + (int64_t)j * w.k;
+  const uint32_t* sr = w.sel_r + (int64_t)j * w.k;
+  const int64_t i = (int64_t)blockIdx.y * kLargeThreads + threadIdx.x;
+  const bool have = i < (int64_t)m;
+  const uint64_t ki = have ? sk[i] : 0;
+  const uint32_t ri = have ? sr[i] : 0u;
+  int64_t rank = 0;
+  for (int64_t t0 = 0; t0 < (int64_t)m; t0 += kLargeTile) {
+    const int cnt = (int)std::min<int64_t>(kLargeTile, (int64_t)m - t0);
+    for (int t = threadIdx.x; t < cnt; t += kLargeThreads) {
+      tk[t] = sk[t0 + t];
+      tr[t] = sr[t0 + t];
+    }
+    __syncthreads();
+    if (have)
+      for (int t = 0; t < cnt; ++t) rank += (tk[t] < ki || (tk[t] == ki && tr[t] < ri)) ? 1 : 0;
+    __syncthreads();
+  }
+  float* os = w.out_s + orow * w.k;
+  int64_t* oi = w.out_i + orow * w.k;
+  if (have) {
+    const uint64_t ord = ~ki;
+    const uint64_t u = (ord >> 63) ? (ord & 0x7FFFFFFFFFFFFFFFull) : ~ord;
+    os[rank] = (float)__builtin_bit_cast(double, u);
+    oi[rank] = (int64_t)ri + w.id_offset;
+  } else if (i < w.k) {
+    os[i] = kPadScore;
+    oi[i] = -1;
+  }
+  if (blockIdx.y == 0 && threadIdx.x == 0) w.status[orow] = 0;
 }
 
 // Row statistics for the refine bound (layout above kStatsLen).  One wave per row: lane L holds the
@@ -3728,6 +3841,87 @@ int drt_ip_topk_resolve_wide(const void* Q, int64_t nq, const void* P, int64_t n
   int64_t nres = 0;
   for (int32_t i : wide) nres += (st2[i] & 2) == 0 ? 1 : 0;
   if (n_resolved) *n_resolved = nres;
+  return DRT_OK;
+}
+
+static size_t large_ws_bytes(int32_t d, int32_t k) {
+  const int64_t B = kQueriesPerWG;
+  return wide_ws_bytes(d) + (size_t)(align_up(B * (int64_t)k * 8, 256) + align_up(B * (int64_t)k * 4, 256) +
+                                     align_up(B * 4, 256));
+}
+
+size_t drt_ip_topk_large_workspace(int32_t d, int32_t k) {
+  if (d <= 0 || d % 64 || d > 1024 || k < 1 || k > kLargeMaxK) return 0;
+  return large_ws_bytes(d, k);
+}
+
+int drt_ip_topk_large(const void* Q, int64_t nq, const void* P, int64_t n, int32_t d, int32_t k, int64_t id_offset,
+                      const float* stats, const float* tau, float* out_scores, int64_t* out_ids, int32_t* status,
+                      void* ws, size_t ws_bytes, void* stream) {
+  DRT_REQUIRE(nq >= 0 && n >= 0 && n < (int64_t)0xFFFFFFFFll && drt_ip_topk_large_workspace(d, k) > 0);
+  if (nq == 0) return DRT_OK;
+  DRT_REQUIRE(Q && (P || n == 0) && stats && tau && out_scores && out_ids && status && ws &&
+              ws_bytes >= large_ws_bytes(d, k));
+  hipStream_t s = (hipStream_t)stream;
+  const int64_t B = kQueriesPerWG;
+  char* wp = (char*)ws + align_up(B * (int64_t)d * 2, 256) + align_up(B * 4, 256);   // (qbuf, qmap unused)
+  float* tauc = (float*)wp;
+  uint32_t* counts = (uint32_t*)((char*)tauc + align_up(B * 4, 256));
+  uint64_t* keys = (uint64_t*)((char*)counts + align_up(B * kCntStride * 4, 256));
+  uint64_t* ekeys = (uint64_t*)((char*)keys + align_up(B * kWideCap * 8, 256));
+  uint64_t* sel_k = (uint64_t*)((char*)ekeys + align_up(B * kWideCap * 8, 256));
+  uint32_t* sel_r = (uint32_t*)((char*)sel_k + align_up(B * (int64_t)k * 8, 256));
+  uint32_t* sel_n = (uint32_t*)((char*)sel_r + align_up(B * (int64_t)k * 4, 256));
+  for (int64_t b0 = 0; b0 < nq; b0 += B) {
+    const int nb = (int)std::min<int64_t>(B, nq - b0);
+    WideArgs w{};
+    w.ra.Q = (const __bf16*)Q + b0 * d;
+    w.ra.d = d;
+    w.ra.P = (const __bf16*)P;
+    w.ra.stats = stats;
+    w.qmap = nullptr;
+    w.q0 = b0;
+    w.tau_in = tau;
+    w.nb = nb;
+    w.k = k;
+    w.tau = tauc;
+    w.counts = counts;
+    w.keys = keys;
+    w.ekeys = ekeys;
+    w.cap = kWideCap;
+    w.id_offset = id_offset;
+    w.out_s = out_scores;
+    w.out_i = out_ids;
+    w.status = status;
+    w.sel_k = sel_k;
+    w.sel_r = sel_r;
+    w.sel_n = sel_n;
+    hipLaunchKernelGGL(wide_prep_kernel, dim3((unsigned)B), dim3(kRefThreads), 0, s, w);
+    DRT_CHECK_HIP(hipGetLastError());
+    if (n > 0) {
+      ScanArgs a{};
+      a.Q = w.ra.Q;
+      a.nq = nb;
+      a.ldq = d;
+      a.P = (const __bf16*)P;
+      a.ldp = d;
+      a.row0 = 0;
+      a.nrows = n;
+      a.rstride = 1;
+      a.tau = tauc;
+      a.counts = counts;
+      a.out = keys;
+      a.cap = kWideCap;
+      const int rc = launch_scan(a, d, SCAN_FILTER, s, -1);
+      if (rc) return rc;
+      hipLaunchKernelGGL(wide_exact_kernel, dim3((unsigned)nb, (unsigned)(kWideCap / kWideSlice)), dim3(kRefThreads),
+                         0, s, w);
+    }
+    hipLaunchKernelGGL(large_select_kernel, dim3((unsigned)nb), dim3(kWideThreads), 0, s, w);
+    hipLaunchKernelGGL(large_rank_kernel, dim3((unsigned)nb, (unsigned)((k + kLargeThreads - 1) / kLargeThreads)),
+                       dim3(kLargeThreads), 0, s, w);
+    DRT_CHECK_HIP(hipGetLastError());
+  }
   return DRT_OK;
 }
 

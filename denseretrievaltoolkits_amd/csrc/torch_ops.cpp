@@ -182,6 +182,34 @@ int64_t ip_topk_resolve_wide(const Tensor& q_, const Tensor& p_, int64_t k, int6
   return nres;
 }
 
+// top-k for 2048 < k <= 32768 in the canonical order (drt_ip_topk_large): tau [nq] = a lower bound of each
+// query's k-th fp32 score; asynchronous, status 2 marks a query whose collected set overflowed
+std::tuple<Tensor, Tensor, Tensor> ip_topk_large(const Tensor& q_, const Tensor& p_, int64_t k, int64_t id_offset,
+                                                 const Tensor& stats, const Tensor& tau) {
+  need(q_, "q", at::kBFloat16, 2);
+  need(p_, "p", at::kBFloat16, 2);
+  need(tau, "tau", at::kFloat, 1);
+  const c10::DeviceGuard g(q_.device());
+  const Tensor q = q_.contiguous(), p = p_.contiguous();
+  TORCH_CHECK_VALUE(q.size(1) == p.size(1), "q and p differ in dimension: ", q.sizes(), " vs ", p.sizes());
+  TORCH_CHECK_VALUE(p.device() == q.device() && tau.device() == q.device(), "q, p and tau must share a device");
+  const int64_t nq = q.size(0), n = p.size(0), d = q.size(1);
+  TORCH_CHECK_VALUE(tau.size(0) == nq && tau.is_contiguous(), "tau must be a contiguous [nq] tensor");
+  const size_t wsb = drt_ip_topk_large_workspace((int32_t)d, (int32_t)k);
+  TORCH_CHECK_VALUE(wsb > 0, "unsupported ip_topk_large shape d=", d, " k=", k, " (d % 64 == 0, d <= 1024, k <= 32768)");
+  const float* sp = stats_ptr(stats, q);
+  Tensor scores = at::empty({nq, k}, q.options().dtype(at::kFloat));
+  Tensor ids = at::empty({nq, k}, q.options().dtype(at::kLong));
+  Tensor status = at::empty({nq}, q.options().dtype(at::kInt));
+  if (nq == 0) return {scores, ids, status};
+  Tensor ws = workspace(q, wsb);
+  check_rc(drt_ip_topk_large(q.data_ptr(), nq, n ? p.data_ptr() : nullptr, n, (int32_t)d, (int32_t)k, id_offset, sp,
+                             tau.data_ptr<float>(), scores.data_ptr<float>(), ids.data_ptr<int64_t>(),
+                             status.data_ptr<int32_t>(), ws.data_ptr(), wsb, stream_of(q)),
+           "drt_ip_topk_large");
+  return {scores, ids, status};
+}
+
 // row statistics of p (+ those of earlier rows in `prev`, appended rows)
 Tensor row_stats(const Tensor& p_, const c10::optional<Tensor>& prev) {
   need(p_, "p", at::kBFloat16, 2);
@@ -586,6 +614,7 @@ TORCH_LIBRARY(drt, m) {
         "Tensor(c!) status, Tensor? stats=None) -> int");
   m.def("ip_topk_resolve_wide(Tensor q, Tensor p, int k, int id_offset, Tensor(a!) scores, Tensor(b!) ids, "
         "Tensor(c!) status, Tensor stats) -> int");
+  m.def("ip_topk_large(Tensor q, Tensor p, int k, int id_offset, Tensor stats, Tensor tau) -> (Tensor, Tensor, Tensor)");
   m.def("row_stats(Tensor p, Tensor? prev=None) -> Tensor");
   m.def("refine_delta(Tensor q, Tensor p, int row_offset, Tensor cand_scores, Tensor cand_ids, int k, Tensor stats, "
         "Tensor? tau, Tensor(a!) status, bool local=False) -> (Tensor, Tensor)");
@@ -619,6 +648,7 @@ TORCH_LIBRARY_IMPL(drt, CUDA, m) {   // the GPU dispatch key of torch-ROCm
   m.impl("dist_filter_chunks_into", &dist_filter_chunks_into);
   m.impl("ip_topk_resolve", &ip_topk_resolve);
   m.impl("ip_topk_resolve_wide", &ip_topk_resolve_wide);
+  m.impl("ip_topk_large", &ip_topk_large);
   m.impl("row_stats", &row_stats);
   m.impl("refine_delta", &refine_delta);
   m.impl("refine_sort", &refine_sort);

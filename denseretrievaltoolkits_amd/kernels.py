@@ -37,6 +37,8 @@ def ip_topk(q: torch.Tensor, p: torch.Tensor, k: int, id_offset: int = 0, resolv
     status bit 0: not certified -- with ``resolve`` such queries are recomputed exactly before
     returning (this synchronises the stream), without it the caller must; bit 1: the exact order
     could not be certified (massive near-ties; that query keeps the fp32 order).
+    k > 2048 (up to 32768) takes the large-k path (_ip_topk_large): always the canonical order,
+    synchronous, status 0.
     """
     drt = ops.load()
     _require_device(q, p)
@@ -45,6 +47,8 @@ def ip_topk(q: torch.Tensor, p: torch.Tensor, k: int, id_offset: int = 0, resolv
     if q.dim() != 2 or p.dim() != 2 or q.shape[1] != p.shape[1]:
         raise ValueError(f"shape mismatch: q {tuple(q.shape)} vs p {tuple(p.shape)}")
     nq, d = q.shape
+    if k > MAX_K and nq > 0:
+        return _ip_topk_large(q, p, k, id_offset, out, status, stats)
     if _native.load().drt_ip_topk_workspace(nq, p.shape[0], d, k) == 0 and nq > 0:
         raise ValueError(f"unsupported ip_topk shape nq={nq} n={p.shape[0]} d={d} k={k} "
                          "(d % 64 == 0, d <= 1024, 1 <= k <= 2048)")
@@ -60,6 +64,48 @@ def ip_topk(q: torch.Tensor, p: torch.Tensor, k: int, id_offset: int = 0, resolv
     if resolve:
         resolve_failed(q, p, k, id_offset, scores, ids, status, stats=stats)
     return scores, ids, status
+
+
+MAX_K = 2048          # the candidate-list kernels' k (csrc/search.hip kSelMaxK)
+MAX_K_LARGE = 32768   # the large-k path (drt_ip_topk_large)
+_WIDE_CAP = 65536     # rows one query of the large-k path may collect
+
+
+def _ip_topk_large(q, p, k, id_offset, out, status, stats):
+    """k > MAX_K (faiss IndexFlatIP answers any k; DRT/arguments.py:195 retrieve_num is a free flag):
+    a threshold no larger than each query's k-th fp32 score -- the minimum of the m-th scores of C
+    disjoint row ranges, C = ceil(k / MAX_K), m = ceil(k / C), so at least C * m >= k rows reach it (every
+    row when n <= 65536) -- then drt_ip_topk_large collects the rows within 2 eps of it and ranks them by
+    their exact sums.  Always the canonical order (what ip_topk gives with ``stats``).  Synchronous (the
+    range searches certify their thresholds); a query whose collected set overflows raises."""
+    if k > MAX_K_LARGE:
+        raise ValueError(f"unsupported ip_topk k={k} (1 <= k <= {MAX_K_LARGE})")
+    drt = ops.load()
+    nq, n = q.shape[0], p.shape[0]
+    if stats is None:
+        stats = row_stats(p)
+    if n <= _WIDE_CAP:
+        tau = torch.full((nq,), float("-inf"), dtype=torch.float32, device=q.device)
+    else:
+        c = -(-k // MAX_K)
+        m = -(-k // c)
+        tau = None
+        for j in range(c):
+            s, _, _ = ip_topk(q, p[n * j // c: n * (j + 1) // c], m)   # certified fp32 scan scores
+            tau = s[:, m - 1].clone() if tau is None else torch.minimum(tau, s[:, m - 1])
+    scores, ids, st = drt.ip_topk_large(q, p, k, id_offset, stats, tau.contiguous())
+    nbad = int((st != 0).sum().item())
+    if nbad:
+        raise RuntimeError(f"ip_topk k={k}: {nbad} queries collected more than {_WIDE_CAP} rows within the "
+                           "fp32 error of their threshold (massive near-ties); no exact order was produced")
+    if out is not None:
+        out[0].copy_(scores)
+        out[1].copy_(ids)
+        scores, ids = out
+    if status is not None:
+        status.copy_(st)
+        st = status
+    return scores, ids, st
 
 
 def resolve_failed(q, p, k, id_offset, scores, ids, status, n_failed: Optional[int] = None,

@@ -71,6 +71,12 @@ def _register_python_parts():
     def _(q, p, k, id_offset, scores, ids, status, stats):
         return torch.library.get_ctx().new_dynamic_size()
 
+    @lib.register_fake("drt::ip_topk_large")
+    def _(q, p, k, id_offset, stats, tau):
+        nq = q.shape[0]
+        return (q.new_empty((nq, k), dtype=torch.float32), q.new_empty((nq, k), dtype=torch.int64),
+                q.new_empty((nq,), dtype=torch.int32))
+
     @lib.register_fake("drt::row_stats")
     def _(p, prev=None):
         return p.new_empty((ROW_STATS_LEN,), dtype=torch.float32)

@@ -386,14 +386,15 @@ class FlatIPIndex:
         BaseFaissIPRetriever.batch_search, Trainer.evaluate and bench.py time."""
         return list(self.search_batches_iter(batches, k, id_offset, outs))
 
-    def _use_groups(self) -> bool:
-        # the grouped path packs row numbers into 32 bits (an id offset is added afterwards)
-        return GROUP_MIN_ROWS <= self.ntotal < 0xFFFFFFFF
+    def _use_groups(self, k: int = 0) -> bool:
+        # the grouped path packs row numbers into 32 bits (an id offset is added afterwards); k beyond
+        # the candidate-list kernels' takes the per-batch large-k path (kernels.ip_topk)
+        return k <= kernels.MAX_K and GROUP_MIN_ROWS <= self.ntotal < 0xFFFFFFFF
 
     def enqueue_batches(self, batches, k: int, id_offset: int = 0, to_host: bool = False) -> list:
         """Every batch's search enqueued now (in groups where ``search_batches`` would group them);
         collect each with ``finish_batch``."""
-        if not self._use_groups():
+        if not self._use_groups(k):
             return [self._enqueue(q, k, id_offset, None, to_host) for q in batches]
         out = []
         stats = self._stats_arg()
@@ -426,7 +427,7 @@ class FlatIPIndex:
         batch j + 1.  ``to_host``: yield numpy (scores, ids) from pinned copies staged behind each
         batch (no stream-draining .cpu() per batch)."""
         batches = list(batches)
-        if outs is None and self._use_groups():
+        if outs is None and self._use_groups(k):
             yield from self._search_groups(batches, k, id_offset, to_host)
             return
         yield from _pipeline(batches, lambda j, q: self._enqueue(q, k, id_offset, outs[j] if outs else None,
@@ -580,6 +581,7 @@ class ShardedFlatIP:
         checks group g's certificates.  Otherwise batch j + 1 is enqueued (scan, exchange, merge)
         before the host checks batch j's certificate."""
         batches = list(batches)
+        self._check_k(k)
         if self._use_groups():
             groups = [[self.local._queries(q) for q in g] for g in _groups(batches)]
 
@@ -625,7 +627,14 @@ class ShardedFlatIP:
         """Exchange through collectives: world > 1 (or the test-only world-1 forcing, comm.py)."""
         return self.world > 1 or comm.collective(self.group)
 
+    def _check_k(self, k: int):
+        if k > kernels.MAX_K and self._multi():
+            # per-shard exact lists would merge by exact keys the exchange does not carry
+            raise ValueError(f"ShardedFlatIP over {self.world} ranks: k={k} > {kernels.MAX_K} is supported on "
+                             "one shard only (FlatIPIndex / kernels.ip_topk, up to 32768)")
+
     def _enqueue(self, q, k: int, to_host: bool = False):
+        self._check_k(k)
         if not self._multi():
             if hasattr(self.local, "_enqueue"):
                 return ("local", self.local._enqueue(q, k, self.offset, to_host=to_host))

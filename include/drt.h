@@ -119,6 +119,19 @@ int drt_ip_topk_resolve_wide(const void* Q, int64_t nq, const void* P, int64_t n
                              int64_t id_offset, const float* stats, float* out_scores, int64_t* out_ids,
                              int32_t* status, void* workspace, size_t workspace_bytes, int64_t* n_resolved,
                              void* stream);
+/* drt_ip_topk_large: top-k for 2048 < k <= 32768 (faiss IndexFlatIP answers any k; the reference's
+ *   retrieve_num is a free flag, DRT/arguments.py:195 used at DRT/trainer/trainer.py:296-297, searched
+ *   through DRT/evaluator/index.py:31-33), always in the canonical order (exact score desc, id asc;
+ *   scores = exact sums rounded to fp32; rows past n padded with -1 like drt_ip_topk_bf16).  tau [nq]
+ *   = a lower bound of each query's k-th fp32 scan score, e.g. the minimum over C disjoint row ranges
+ *   of their m-th score with C * m >= k (-inf: every row).  Every row with fp32 score >= tau - 2 eps
+ *   is collected (up to 65536 per query) and ranked by its exact sum.  Asynchronous; status 0, or 2
+ *   where the collected set overflowed (that query's output is then undefined).  Workspace:
+ *   drt_ip_topk_large_workspace(d, k) bytes (0 = unsupported d / k).                            */
+size_t drt_ip_topk_large_workspace(int32_t d, int32_t k);
+int drt_ip_topk_large(const void* Q, int64_t nq, const void* P, int64_t n, int32_t d, int32_t k, int64_t id_offset,
+                      const float* stats, const float* tau, float* out_scores, int64_t* out_ids, int32_t* status,
+                      void* workspace, size_t workspace_bytes, void* stream);
 int drt_refine_delta_bf16(const void* Q, int64_t nq, int32_t d, const void* P, int64_t n_local,
                           int64_t row_offset, const float* cand_s, const int64_t* cand_i, int32_t kc,
                           int32_t k, const float* stats, const float* tau, float* delta, int32_t* cnt,

@@ -1,0 +1,112 @@
+"""GPU: top-k beyond the candidate-list kernels' 2048 (kernels.ip_topk -> drt_ip_topk_large).
+
+faiss IndexFlatIP answers any k and the reference's ``retrieve_num`` is a free flag
+(DRT/arguments.py:195, searched at DRT/trainer/trainer.py:296-297 through
+DRT/evaluator/index.py:31-33).  The large-k path always returns the canonical order: ids equal
+to the fp64 oracle's (oracle/search_oracle.ip_topk, ties by ascending id) and scores = the exact
+sums rounded to fp32 -- on Gaussian data (the threshold from C disjoint row ranges), on
+tie-heavy integer data, with fewer rows than k (padded with -1 like faiss) and through
+FlatIPIndex's batch paths (which would otherwise group the search).
+"""
+import numpy as np
+import pytest
+
+from helpers import gauss_bf16, int_bf16, to_dev_bf16
+from oracle import search_oracle as orc
+
+pytestmark = pytest.mark.gpu
+
+
+def _large(dev, q, p, k, id_offset=0, with_stats=False):
+    import torch
+    from denseretrievaltoolkits_amd import kernels
+    qt, pt = to_dev_bf16(q, dev), to_dev_bf16(p, dev)
+    stats = kernels.row_stats(pt) if with_stats else None
+    s, i, st = kernels.ip_topk(qt, pt, k, id_offset=id_offset, stats=stats)
+    torch.cuda.synchronize()
+    return s.cpu().numpy(), i.cpu().numpy(), st.cpu().numpy()
+
+
+def _assert_scores(gs, es):
+    """fp32 roundings of the same exact sum computed in two fp64 orders: equal up to one fp32 ulp."""
+    ulp = np.spacing(np.abs(es).astype(np.float32))
+    assert (np.abs(gs.astype(np.float64) - es.astype(np.float64)) <= ulp).all()
+    assert (gs == es).mean() > 0.999
+
+
+@pytest.mark.parametrize("nq,n,d,k,stats", [
+    (20, 200000, 768, 5000, False),    # threshold from 3 row ranges (m = 1667), BERT-base width
+    (130, 90000, 256, 2049, True),     # k just past the list kernels, 2 query chunks of 128
+    (3, 30000, 128, 4096, False),      # n <= 65536: every row collected
+    (4, 150000, 64, 32768, False),     # k at its maximum (16 row ranges of 2048)
+])
+def test_large_k_gaussian_bit_exact(dev, nq, n, d, k, stats):
+    rng = np.random.default_rng(nq + n + d + k)
+    q = gauss_bf16(rng, (nq, d))
+    p = gauss_bf16(rng, (n, d))
+    gs, gi, st = _large(dev, q, p, k, id_offset=11, with_stats=stats)
+    es, ei = orc.ip_topk(q, p, k, id_offset=11)
+    assert (st == 0).all()
+    np.testing.assert_array_equal(gi, ei)
+    _assert_scores(gs, es)
+
+
+def test_large_k_integer_ties_by_id(dev):
+    """Small integers: massive exact ties, resolved by ascending id (scores exact in fp32)."""
+    rng = np.random.default_rng(5)
+    q = int_bf16(rng, (6, 64), -2, 2)
+    p = int_bf16(rng, (60000, 64), -2, 2)
+    gs, gi, st = _large(dev, q, p, 3000)
+    es, ei = orc.ip_topk(q, p, 3000)
+    np.testing.assert_array_equal(gi, ei)
+    np.testing.assert_array_equal(gs, es)
+
+
+def test_large_k_fewer_rows_than_k_pads(dev):
+    rng = np.random.default_rng(7)
+    q = int_bf16(rng, (3, 64))
+    p = int_bf16(rng, (2500, 64))
+    gs, gi, st = _large(dev, q, p, 4000, id_offset=100)
+    es, ei = orc.ip_topk(q, p, 4000, id_offset=100)
+    np.testing.assert_array_equal(gi, ei)
+    np.testing.assert_array_equal(gs, es)
+    assert (gi[:, 2500:] == -1).all() and (gs[:, 2500:] == orc.PAD_SCORE).all()
+
+
+def test_large_k_limits(dev):
+    import torch
+    from denseretrievaltoolkits_amd import kernels
+    q = torch.zeros((2, 64), dtype=torch.bfloat16, device=dev)
+    p = torch.zeros((10, 64), dtype=torch.bfloat16, device=dev)
+    with pytest.raises(ValueError):
+        kernels.ip_topk(q, p, 32769)
+    # 70,000 identical rows: every one within the error of the threshold -> more than the 65,536 a
+    # query may collect -> an error, never a silently wrong order
+    p = torch.ones((70000, 64), dtype=torch.bfloat16, device=dev)
+    q = torch.ones((1, 64), dtype=torch.bfloat16, device=dev)
+    with pytest.raises(RuntimeError, match="65536"):
+        kernels.ip_topk(q, p, 3000)
+
+
+def test_flat_index_large_k_batches(dev):
+    """FlatIPIndex at a grouped-path size: k > 2048 takes the per-batch large-k path in search,
+    search_batches and enqueue_batches, equal to the fp64 oracle."""
+    import torch
+    from denseretrievaltoolkits_amd import search as srch
+    rng = np.random.default_rng(31)
+    q = gauss_bf16(rng, (24, 128))
+    p = gauss_bf16(rng, (520000, 128))
+    k = 2500
+    es, ei = orc.ip_topk(q, p, k)
+    idx = srch.FlatIPIndex.from_rows(to_dev_bf16(p, dev))
+    assert idx._use_groups(1000) and not idx._use_groups(k)
+    qd = to_dev_bf16(q, dev)
+    res = idx.search_batches([qd[a: a + 8] for a in range(0, 24, 8)], k)
+    np.testing.assert_array_equal(torch.cat([r[1] for r in res]).cpu().numpy(), ei)
+    _assert_scores(torch.cat([r[0] for r in res]).cpu().numpy(), es)
+    pend = idx.enqueue_batches([qd[:8]], k)
+    s, i = idx.finish_batch(pend[0])
+    np.testing.assert_array_equal(i.cpu().numpy(), ei[:8])
+    s, i = idx.search(q[8:16], k)
+    np.testing.assert_array_equal(i, ei[8:16])
+    assert idx.order_uncertified == 0
