@@ -71,6 +71,17 @@ MAX_K_LARGE = 32768   # the large-k path (drt_ip_topk_large)
 _WIDE_CAP = 65536     # rows one query of the large-k path may collect
 
 
+def large_k_ranges(n: int, k: int):
+    """The large-k threshold plan: None (every row is collected: n <= 65536) or (m, [(a, b), ...]) --
+    C = ceil(k / MAX_K) disjoint row ranges covering [0, n) whose m-th scores, m = ceil(k / C) <= MAX_K,
+    bound the k-th score from below (C * m >= k rows reach their minimum; every range holds >= m rows)."""
+    if n <= _WIDE_CAP:
+        return None
+    c = -(-k // MAX_K)
+    m = -(-k // c)
+    return m, [(n * j // c, n * (j + 1) // c) for j in range(c)]
+
+
 def _ip_topk_large(q, p, k, id_offset, out, status, stats):
     """k > MAX_K (faiss IndexFlatIP answers any k; DRT/arguments.py:195 retrieve_num is a free flag):
     a threshold no larger than each query's k-th fp32 score -- the minimum of the m-th scores of C
@@ -84,14 +95,13 @@ def _ip_topk_large(q, p, k, id_offset, out, status, stats):
     nq, n = q.shape[0], p.shape[0]
     if stats is None:
         stats = row_stats(p)
-    if n <= _WIDE_CAP:
+    ranges = large_k_ranges(n, k)
+    if ranges is None:
         tau = torch.full((nq,), float("-inf"), dtype=torch.float32, device=q.device)
     else:
-        c = -(-k // MAX_K)
-        m = -(-k // c)
-        tau = None
-        for j in range(c):
-            s, _, _ = ip_topk(q, p[n * j // c: n * (j + 1) // c], m)   # certified fp32 scan scores
+        m, tau = ranges[0], None
+        for a, b in ranges[1]:
+            s, _, _ = ip_topk(q, p[a:b], m)   # certified fp32 scan scores
             tau = s[:, m - 1].clone() if tau is None else torch.minimum(tau, s[:, m - 1])
     scores, ids, st = drt.ip_topk_large(q, p, k, id_offset, stats, tau.contiguous())
     nbad = int((st != 0).sum().item())
