@@ -51,7 +51,7 @@ def ip_topk(q: torch.Tensor, p: torch.Tensor, k: int, id_offset: int = 0, resolv
         return _ip_topk_large(q, p, k, id_offset, out, status, stats)
     if _native.load().drt_ip_topk_workspace(nq, p.shape[0], d, k) == 0 and nq > 0:
         raise ValueError(f"unsupported ip_topk shape nq={nq} n={p.shape[0]} d={d} k={k} "
-                         "(d % 64 == 0, d <= 1024, 1 <= k <= 2048)")
+                         "(d % 64 == 0, d <= 1024, k >= 1; k > 2048 takes the large-k path, up to 32768)")
     if out is None and status is None:
         scores, ids, status = drt.ip_topk(q, p, k, id_offset, stats)
     else:
