@@ -338,6 +338,8 @@ class FlatIPIndex:
     def _enqueue(self, q, k: int, id_offset: int = 0, out=None, to_host: bool = False):
         qd = self._queries(q)
         stats = self._stats_arg()
+        if stats is None and k > kernels.MAX_K:   # the large-k path always ranks exactly: reuse the index's stats
+            stats = self.row_stats()
         s, i, st = kernels.ip_topk(qd, self.rows, k, id_offset=id_offset, resolve=False, out=out, stats=stats)
         h, ev = _stage_status(st)
         host = _HostResult(s, i) if to_host else None

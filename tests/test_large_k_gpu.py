@@ -71,6 +71,8 @@ def test_large_k_fewer_rows_than_k_pads(dev):
     np.testing.assert_array_equal(gi, ei)
     np.testing.assert_array_equal(gs, es)
     assert (gi[:, 2500:] == -1).all() and (gs[:, 2500:] == orc.PAD_SCORE).all()
+    gs, gi, st = _large(dev, q, np.zeros((0, 64), np.float32), 4000)   # an empty shard
+    assert (gi == -1).all() and (gs == orc.PAD_SCORE).all() and (st == 0).all()
 
 
 def test_large_k_limits(dev):
@@ -110,3 +112,11 @@ def test_flat_index_large_k_batches(dev):
     s, i = idx.search(q[8:16], k)
     np.testing.assert_array_equal(i, ei[8:16])
     assert idx.order_uncertified == 0
+    # caller-owned output buffers (search_batches' per-batch path), and an index without the exact order
+    outs = [(torch.empty((8, k), dtype=torch.float32, device=dev), torch.empty((8, k), dtype=torch.int64, device=dev))]
+    res = idx.search_batches([qd[16:24]], k, outs=outs)
+    assert res[0][1].data_ptr() == outs[0][1].data_ptr()
+    np.testing.assert_array_equal(outs[0][1].cpu().numpy(), ei[16:24])
+    idx.exact_order = False
+    s, i = idx.search_device(qd[:8], k)
+    np.testing.assert_array_equal(i.cpu().numpy(), ei[:8])
