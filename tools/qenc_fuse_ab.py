@@ -1,5 +1,6 @@
-"""Query tower (32 tokens, eager) with and without the fused dense + residual + LayerNorm call
-(HipBertEncoder.fuse_ln), interleaved rounds, ms per batch."""
+"""Query tower (32 tokens, eager) with and without one of HipBertEncoder's boolean fusion switches
+(default fuse_ln: dense + residual + LayerNorm in one call; round 5 also A/B'd a fuse_attn patch, see
+DESIGN §1), interleaved rounds, ms per batch.  usage: python tools/qenc_fuse_ab.py [attribute]"""
 import json
 import os
 import sys
@@ -10,7 +11,7 @@ import torch
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
 
-def main(rounds=3, steps=30):
+def main(flag="fuse_ln", rounds=3, steps=30):
     from transformers import BertConfig, BertModel
     from denseretrievaltoolkits_amd.model.encoder import HipBertEncoder
     dev = torch.device("cuda", 0)
@@ -23,7 +24,7 @@ def main(rounds=3, steps=30):
             mask = torch.ones((B, 32), dtype=torch.int64, device=dev)
             outs = {}
             for fuse in (False, True):
-                enc.fuse_ln = fuse
+                setattr(enc, flag, fuse)
                 outs[fuse] = enc(ids, mask).clone()
                 torch.cuda.synchronize()
                 t0 = time.perf_counter()
@@ -33,8 +34,9 @@ def main(rounds=3, steps=30):
                 res.setdefault(f"b{B}_{'fused' if fuse else 'unfused'}", []).append(
                     round((time.perf_counter() - t0) / steps * 1e3, 4))
             res[f"b{B}_identical"] = bool(torch.equal(outs[False], outs[True]))
-    print(json.dumps({k: (sorted(v)[len(v) // 2] if isinstance(v, list) else v) for k, v in res.items()}))
+    print(json.dumps({"flag": flag, **{k: (sorted(v)[len(v) // 2] if isinstance(v, list) else v)
+                                       for k, v in res.items()}}))
 
 
 if __name__ == "__main__":
-    main()
+    main(*sys.argv[1:2])
