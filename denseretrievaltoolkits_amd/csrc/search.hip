@@ -2707,6 +2707,8 @@ struct WideArgs {
   uint64_t* sel_k;
   uint32_t* sel_r;
   uint32_t* sel_n;
+  uint64_t* bin_k;        // [*, k] the selected entries regrouped by bin (large_rank_kernel)
+  uint32_t* bin_r;
 };
 
 __device__ __forceinline__ int64_t wide_out_row(const WideArgs& w, int j) {
@@ -2902,13 +2904,12 @@ __global__ __launch_bounds__(kWideThreads) void wide_select_kernel(WideArgs w) {
 // the m-th scores of C disjoint row ranges, C * m >= k), the filter collects every row with fp32
 // score >= tau_q - 2 eps (it holds the exact top-k, see the bound above), wide_exact_kernel computes
 // their exact sums, large_select_kernel finds the k-th (exact key, row) by the two radix selects and
-// compacts the k selected entries, large_rank_kernel ranks each by counting over LDS tiles of the
-// selected set.  Output: the canonical order (exact score desc, id asc), scores = exact sums rounded to
+// compacts the k selected entries, large_rank_kernel ranks each by counting within bins of the exact
+// key (below).  Output: the canonical order (exact score desc, id asc), scores = exact sums rounded to
 // fp32, rows past n padded like ip_topk; status 0, or 2 when the collected set overflowed kWideCap.
 // ---------------------------------------------------------------------------
 constexpr int32_t kLargeMaxK = 32768;
 constexpr int kLargeThreads = 1024;
-constexpr int kLargeTile = 2048;   // selected entries per LDS tile of the rank count
 
 __global__ __launch_bounds__(kWideThreads) void large_select_kernel(WideArgs w) {
   __shared__ uint32_t hist[256];
@@ -2954,45 +2955,116 @@ __global__ __launch_bounds__(kWideThreads) void large_select_kernel(WideArgs w) 
   if (threadIdx.x == 0) w.sel_n[j] = ns == (uint32_t)keff ? ns : 0xFFFFFFFFu;
 }
 
-// grid (queries, ceil(k / kLargeThreads)): entry i of the selected set goes to rank = #entries before it
+// One work-group per query: rank = the number of selected entries before an entry in (exact key, row)
+// order, counted within bins -- a histogram of the exact keys over kLargeBins equal ranges between the
+// set's min and max key (a monotone map: an entry's bin never exceeds a larger entry's), the bins'
+// exclusive prefix, the entries regrouped by bin, then each entry compared only with its own bin's.
+// Ties share a bin, so a set of many equal keys degrades towards the all-pairs count.
+constexpr int kLargeBins = 4096;
+
+__device__ __forceinline__ int large_bin(uint64_t key, uint64_t kmin, double scale) {
+  const int b = (int)((double)(key - kmin) * scale);
+  return b < kLargeBins - 1 ? b : kLargeBins - 1;
+}
+
 __global__ __launch_bounds__(kLargeThreads) void large_rank_kernel(WideArgs w) {
-  __shared__ uint64_t tk[kLargeTile];
-  __shared__ uint32_t tr[kLargeTile];
+  __shared__ uint32_t start[kLargeBins];
+  __shared__ uint32_t cursor[kLargeBins];
+  __shared__ uint64_t red[2][kLargeThreads / 64];
+  __shared__ uint32_t wsum[kLargeThreads / 64];
   const int j = blockIdx.x;
   if (j >= w.nb) return;
   const uint32_t m = w.sel_n[j];
   if (m == 0xFFFFFFFFu) return;   // overflow: status stays 2
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int64_t orow = wide_out_row(w, j);
   const uint64_t* sk = w.sel_k + (int64_t)j * w.k;
   const uint32_t* sr = w.sel_r + (int64_t)j * w.k;
-  const int64_t i = (int64_t)blockIdx.y * kLargeThreads + threadIdx.x;
-  const bool have = i < (int64_t)m;
-  const uint64_t ki = have ? sk[i] : 0;
-  const uint32_t ri = have ? sr[i] : 0u;
-  int64_t rank = 0;
-  for (int64_t t0 = 0; t0 < (int64_t)m; t0 += kLargeTile) {
-    const int cnt = (int)std::min<int64_t>(kLargeTile, (int64_t)m - t0);
-    for (int t = threadIdx.x; t < cnt; t += kLargeThreads) {
-      tk[t] = sk[t0 + t];
-      tr[t] = sr[t0 + t];
-    }
-    __syncthreads();
-    if (have)
-      for (int t = 0; t < cnt; ++t) rank += (tk[t] < ki || (tk[t] == ki && tr[t] < ri)) ? 1 : 0;
-    __syncthreads();
+  uint64_t* bk = w.bin_k + (int64_t)j * w.k;
+  uint32_t* br = w.bin_r + (int64_t)j * w.k;
+  // key range of the set
+  uint64_t lo = ~0ull, hi = 0ull;
+  for (uint32_t i = tid; i < m; i += kLargeThreads) {
+    const uint64_t v = sk[i];
+    lo = v < lo ? v : lo;
+    hi = v > hi ? v : hi;
   }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    const uint64_t a = __shfl_xor(lo, o, 64), b = __shfl_xor(hi, o, 64);
+    lo = a < lo ? a : lo;
+    hi = b > hi ? b : hi;
+  }
+  if (lane == 0) {
+    red[0][wave] = lo;
+    red[1][wave] = hi;
+  }
+  for (int b = tid; b < kLargeBins; b += kLargeThreads) start[b] = 0u;
+  __syncthreads();
+  lo = red[0][0];
+  hi = red[1][0];
+  for (int q = 1; q < kLargeThreads / 64; ++q) {
+    lo = red[0][q] < lo ? red[0][q] : lo;
+    hi = red[1][q] > hi ? red[1][q] : hi;
+  }
+  const double scale = m ? (double)kLargeBins / ((double)(hi - lo) + 1.0) : 0.0;
+  // histogram, exclusive prefix (4 bins per thread, wave scan, wave totals)
+  for (uint32_t i = tid; i < m; i += kLargeThreads) atomicAdd(&start[large_bin(sk[i], lo, scale)], 1u);
+  __syncthreads();
+  constexpr int kPer = kLargeBins / kLargeThreads;
+  uint32_t c[kPer], tot = 0;
+#pragma unroll
+  for (int u = 0; u < kPer; ++u) {
+    c[u] = start[tid * kPer + u];
+    tot += c[u];
+  }
+  uint32_t inc = tot;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const uint32_t t = __shfl_up(inc, o, 64);
+    if (lane >= o) inc += t;
+  }
+  if (lane == 63) wsum[wave] = inc;
+  __syncthreads();
+  uint32_t base = inc - tot;
+  for (int q = 0; q < wave; ++q) base += wsum[q];
+#pragma unroll
+  for (int u = 0; u < kPer; ++u) {
+    start[tid * kPer + u] = base;
+    cursor[tid * kPer + u] = base;
+    base += c[u];
+  }
+  __syncthreads();
+  // regroup by bin (positions within a bin are arbitrary: the counts below do not depend on them)
+  for (uint32_t i = tid; i < m; i += kLargeThreads) {
+    const uint64_t v = sk[i];
+    const uint32_t pos = atomicAdd(&cursor[large_bin(v, lo, scale)], 1u);
+    bk[pos] = v;
+    br[pos] = sr[i];
+  }
+  __syncthreads();
   float* os = w.out_s + orow * w.k;
   int64_t* oi = w.out_i + orow * w.k;
-  if (have) {
+  for (uint32_t i = tid; i < m; i += kLargeThreads) {
+    const uint64_t ki = sk[i];
+    const uint32_t ri = sr[i];
+    const int b = large_bin(ki, lo, scale);
+    const uint32_t b0 = start[b], b1 = cursor[b];   // cursor = end of the bin after the regroup
+    uint32_t rank = b0;
+    for (uint32_t t = b0; t < b1; ++t) {
+      const uint64_t kt = bk[t];
+      rank += (kt < ki || (kt == ki && br[t] < ri)) ? 1u : 0u;
+    }
     const uint64_t ord = ~ki;
     const uint64_t u = (ord >> 63) ? (ord & 0x7FFFFFFFFFFFFFFFull) : ~ord;
     os[rank] = (float)__builtin_bit_cast(double, u);
     oi[rank] = (int64_t)ri + w.id_offset;
-  } else if (i < w.k) {
+  }
+  for (int64_t i = (int64_t)m + tid; i < w.k; i += kLargeThreads) {
     os[i] = kPadScore;
     oi[i] = -1;
   }
-  if (blockIdx.y == 0 && threadIdx.x == 0) w.status[orow] = 0;
+  if (tid == 0) w.status[orow] = 0;
 }
 
 // Row statistics for the refine bound (layout above kStatsLen).  One wave per row: lane L holds the
@@ -3846,7 +3918,7 @@ int drt_ip_topk_resolve_wide(const void* Q, int64_t nq, const void* P, int64_t n
 
 static size_t large_ws_bytes(int32_t d, int32_t k) {
   const int64_t B = kQueriesPerWG;
-  return wide_ws_bytes(d) + (size_t)(align_up(B * (int64_t)k * 8, 256) + align_up(B * (int64_t)k * 4, 256) +
+  return wide_ws_bytes(d) + (size_t)(2 * align_up(B * (int64_t)k * 8, 256) + 2 * align_up(B * (int64_t)k * 4, 256) +
                                      align_up(B * 4, 256));
 }
 
@@ -3872,6 +3944,8 @@ int drt_ip_topk_large(const void* Q, int64_t nq, const void* P, int64_t n, int32
   uint64_t* sel_k = (uint64_t*)((char*)ekeys + align_up(B * kWideCap * 8, 256));
   uint32_t* sel_r = (uint32_t*)((char*)sel_k + align_up(B * (int64_t)k * 8, 256));
   uint32_t* sel_n = (uint32_t*)((char*)sel_r + align_up(B * (int64_t)k * 4, 256));
+  uint64_t* bin_k = (uint64_t*)((char*)sel_n + align_up(B * 4, 256));
+  uint32_t* bin_r = (uint32_t*)((char*)bin_k + align_up(B * (int64_t)k * 8, 256));
   for (int64_t b0 = 0; b0 < nq; b0 += B) {
     const int nb = (int)std::min<int64_t>(B, nq - b0);
     WideArgs w{};
@@ -3896,6 +3970,8 @@ int drt_ip_topk_large(const void* Q, int64_t nq, const void* P, int64_t n, int32
     w.sel_k = sel_k;
     w.sel_r = sel_r;
     w.sel_n = sel_n;
+    w.bin_k = bin_k;
+    w.bin_r = bin_r;
     hipLaunchKernelGGL(wide_prep_kernel, dim3((unsigned)B), dim3(kRefThreads), 0, s, w);
     DRT_CHECK_HIP(hipGetLastError());
     if (n > 0) {
@@ -3918,8 +3994,7 @@ int drt_ip_topk_large(const void* Q, int64_t nq, const void* P, int64_t n, int32
                          0, s, w);
     }
     hipLaunchKernelGGL(large_select_kernel, dim3((unsigned)nb), dim3(kWideThreads), 0, s, w);
-    hipLaunchKernelGGL(large_rank_kernel, dim3((unsigned)nb, (unsigned)((k + kLargeThreads - 1) / kLargeThreads)),
-                       dim3(kLargeThreads), 0, s, w);
+    hipLaunchKernelGGL(large_rank_kernel, dim3((unsigned)nb), dim3(kLargeThreads), 0, s, w);
     DRT_CHECK_HIP(hipGetLastError());
   }
   return DRT_OK;
