@@ -141,19 +141,32 @@ def init_dist(n_gpus):
     return rank, world, local
 
 
+CORPUS_BLOCK_ROWS = 1 << 20
+
+
+def corpus_block_seed(b):
+    """Seed of global row block b (rows [b * CORPUS_BLOCK_ROWS, (b + 1) * CORPUS_BLOCK_ROWS))."""
+    return (1234 << 32) + b
+
+
 def gen_shard(n_total, world, rank, d, device):
-    """Seeded N(0,1) bf16 corpus rows of this rank's contiguous shard (generated in HBM)."""
+    """Seeded N(0,1) bf16 corpus rows of this rank's contiguous shard (generated in HBM).  Rows are
+    generated by GLOBAL row block ("seed 1234 by row-block counter"), so the union of the
+    W shards is the same 10M-row corpus for every W and the 1/2/4/8-GPU lines search the same rows."""
     import torch
     per = -(-n_total // world)
     lo = min(n_total, rank * per)
     hi = min(n_total, lo + per)
     g = torch.Generator(device=device)
-    g.manual_seed(1234 + rank)
     shard = torch.empty((hi - lo, d), dtype=torch.bfloat16, device=device)
-    step = 1 << 20
-    for a in range(0, hi - lo, step):
-        b = min(hi - lo, a + step)
-        shard[a:b] = torch.randn((b - a, d), generator=g, device=device, dtype=torch.float32).to(torch.bfloat16)
+    B = CORPUS_BLOCK_ROWS
+    for b in range(lo // B, -(-hi // B)):
+        a0, b0 = b * B, min(n_total, (b + 1) * B)
+        g.manual_seed(corpus_block_seed(b))
+        blk = torch.randn((b0 - a0, d), generator=g, device=device, dtype=torch.float32).to(torch.bfloat16)
+        x0, x1 = max(lo, a0), min(hi, b0)
+        shard[x0 - lo: x1 - lo] = blk[x0 - a0: x1 - a0]
+        del blk
     return shard, lo, hi
 
 
@@ -368,8 +381,24 @@ def scan_roofline(d, k, kc, shapes, grouped, launch_ms_total):
     }
 
 
+def per_shape(d, k, kc, shapes, grouped, each_ms):
+    """Average launch time and roofline fraction of every launch shape of the timed region (its
+    launches matched to the shapes in issue order; None when the counts differ, e.g. a redone batch)."""
+    if each_ms is None or len(each_ms) != len(shapes):
+        return None
+    acc = {}
+    for sh, ms in zip(shapes, each_ms):
+        acc.setdefault(tuple(sh), []).append(ms)
+    out = []
+    for (q, r), v in sorted(acc.items(), reverse=True):
+        rf = scan_roofline(d, k, kc, [(q, r)] * len(v), grouped, sum(v))
+        out.append({"queries": q, "rows": r, "launches": len(v), "avg_launch_ms": round(sum(v) / len(v), 4),
+                    "bound": rf["bound"], "frac": rf["frac"], "achieved": rf["achieved"], "unit": rf["unit"]})
+    return out
+
+
 def search_record(args, world, grouped, group_queries, kc, elapsed_s, launch_ms_total, launches, traffic,
-                  chunks=None):
+                  chunks=None, each_ms=None):
     """The headline JSON record of the search leg (rank 0).  ``chunks``: the row ranges of rank 0's
     group filter launches (search.group_chunks / ShardedFlatIP.group_chunks; rank 0 holds the largest
     shard)."""
@@ -382,6 +411,9 @@ def search_record(args, world, grouped, group_queries, kc, elapsed_s, launch_ms_
     rf = {"kernel": "%s<%d> (csrc/search.hip)" % (kname, d), **rf}
     if launches != len(shapes):
         rf["launches_counted"] = launches   # the profiler's count (differs only if a batch was redone)
+    ps = per_shape(d, k, kc, shapes, grouped, each_ms)
+    if ps is not None and len(ps) > 1:
+        rf["per_shape"] = ps   # rank 0's launches by shape (the line's avg_launch_ms mixes them)
     # PMC traffic (tools/pmc_traffic.py) of this configuration's dominant launch shape
     tb, tsrc = traffic
     rf["traffic"] = tb
@@ -506,21 +538,25 @@ def main():
             dist.barrier()
         t1 = time.perf_counter()
         lib.drt_profile_enable(_native.PROF_SCAN, 0)
-        tot_ms = _native.ctypes.c_double(0.0)
+        cap = 1 << 14
+        each = (_native.ctypes.c_double * cap)()
         cnt = _native.c_i64(0)
-        _native.check(lib.drt_profile_read(_native.PROF_SCAN, _native.ctypes.byref(tot_ms),
-                                           _native.ctypes.byref(cnt)), "drt_profile_read")
+        _native.check(lib.drt_profile_read_each(_native.PROF_SCAN, each, cap, _native.ctypes.byref(cnt)),
+                      "drt_profile_read_each")
+        each_ms = [float(each[j]) for j in range(min(cap, int(cnt.value)))]
         elapsed = torch.tensor([t1 - t0], dtype=torch.float64, device=dev)
-        scan_ms = torch.tensor([tot_ms.value / max(1, cnt.value)], dtype=torch.float64, device=dev)
+        scan_ms = torch.tensor([sum(each_ms) / max(1, cnt.value)], dtype=torch.float64, device=dev)
         if world > 1:
             if gloo:
                 elapsed, scan_ms = elapsed.cpu(), scan_ms.cpu()
             dist.all_reduce(elapsed, op=dist.ReduceOp.MAX)
             dist.all_reduce(scan_ms, op=dist.ReduceOp.MAX)
         counters = (local_index.resolved - res0, fallbacks() - fb0, index.order_uncertified - unc0)
+        timed.each_ms = each_ms   # this rank's launches, in issue order (per-shape averages in the record)
         return res, float(elapsed.item()), float(scan_ms.item()) * int(cnt.value), int(cnt.value), counters
 
     results, el, scan_ms_total, launches, (n_resolved, n_fallback, n_unc) = timed(args.warmup, nsteps)
+    each_ms = timed.each_ms
     grouped = index._use_groups()
     sub = None
     if world > 1 and grouped:
@@ -544,7 +580,8 @@ def main():
         chunks = srch.group_chunks(n_local) if world == 1 else index.group_chunks()
         shape = (srch.GROUP_QUERIES, max(b - a for a, b in chunks)) if grouped else None
         out = search_record(args, world, grouped, srch.GROUP_QUERIES, kernels.refine_width(k), el,
-                            scan_ms_total, launches, pmc_traffic(args, world, shape), chunks=chunks)
+                            scan_ms_total, launches, pmc_traffic(args, world, shape), chunks=chunks,
+                            each_ms=each_ms)
         if sub is not None:
             out["per_batch_qb%d" % qb] = sub
         out["order"] = ("canonical: exact-score re-rank of each query's near-tie window (fp64 sums of the bf16 "

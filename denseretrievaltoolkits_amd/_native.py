@@ -134,6 +134,7 @@ _SIGNATURES = [
     ("drt_transpose_f32", c_i32, [c_vp, c_i64, c_i64, c_vp, c_vp]),
     ("drt_profile_enable", c_i32, [c_i32, c_i32]),
     ("drt_profile_read", c_i32, [c_i32, c_vp, c_vp]),
+    ("drt_profile_read_each", c_i32, [c_i32, c_vp, c_i64, c_vp]),
 ]
 
 PROF_SCAN, PROF_SAMPLE, PROF_SELECT, PROF_MERGE, PROF_GEMM = range(5)

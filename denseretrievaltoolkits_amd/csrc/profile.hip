@@ -51,6 +51,26 @@ extern "C" int drt_profile_enable(int32_t family, int32_t enable) {
   return DRT_OK;
 }
 
+extern "C" int drt_profile_read_each(int32_t family, double* ms_each, int64_t cap, int64_t* count) {
+  if (family < 0 || family >= PROF_N || cap < 0 || (cap > 0 && !ms_each)) return DRT_EINVAL;
+  std::lock_guard<std::mutex> lk(g_mu);
+  int64_t n = 0;
+  for (auto& p : g_rec[family]) {
+    hipError_t e = hipEventSynchronize(p.b);
+    if (e != hipSuccess) return (int)e;
+    float ms = 0.f;
+    e = hipEventElapsedTime(&ms, p.a, p.b);
+    if (e != hipSuccess) return (int)e;
+    if (n < cap) ms_each[n] = ms;
+    ++n;
+    g_pool.push_back(p.a);
+    g_pool.push_back(p.b);
+  }
+  g_rec[family].clear();
+  if (count) *count = n;
+  return DRT_OK;
+}
+
 extern "C" int drt_profile_read(int32_t family, double* total_ms, int64_t* count) {
   if (family < 0 || family >= PROF_N) return DRT_EINVAL;
   std::lock_guard<std::mutex> lk(g_mu);

@@ -753,11 +753,7 @@ __global__ __launch_bounds__(512, 1) void ip_scan16r_kernel(ScanArgs a) {
 template <int D>
 struct Scan32Cfg {
   static constexpr int KS = D / 32;
-#ifdef DRT_SCAN32_RD
-  static constexpr int RD = KS % DRT_SCAN32_RD == 0 ? DRT_SCAN32_RD : 1;
-#else
   static constexpr int RD = KS % 2 == 0 ? 2 : 1;   // fragment roll depth (round 5: 2, 3, 4, 6 within noise)
-#endif
   static constexpr int TILE_BYTES = kT16 * D * 2;
   static constexpr int HIT_BYTES = kHitCap * 9;
   static constexpr int NB_RAW = (160 * 1024 - HIT_BYTES) / TILE_BYTES;
@@ -3286,14 +3282,6 @@ static int scan_grid_x(int64_t ntiles) {
   return (int)std::max<int64_t>(g, 1);
 }
 
-// Built with -DDRT_SCAN32_OFF (an A/B variant library, tools/build_variant.sh), grouped launches keep
-// ip_scan16r_kernel; results are identical either way.
-#ifdef DRT_SCAN32_OFF
-constexpr bool kScan32 = false;
-#else
-constexpr bool kScan32 = true;
-#endif
-
 template <int D>
 static int launch_scan_d(const ScanArgs& a, int mode, hipStream_t s) {
   if (a.nq == 0 || a.nrows == 0) return DRT_OK;
@@ -3331,7 +3319,7 @@ static int launch_scan_d(const ScanArgs& a, int mode, hipStream_t s) {
     } else {
       // non-temporal corpus loads for a single block; a group's blocks share each tile through L2, and a
       // group of more than 128 queries takes the 32-queries-per-wave kernel (256 per work-group)
-      if (kScan32 && D <= 768 && gy > 1) {   // (wider rows: the 32 queries' fragments spill)
+      if (D <= 768 && gy > 1) {   // (wider rows: the 32 queries' fragments spill)
         const unsigned gy32 = (unsigned)((a.nq + kQueriesPerWG32 - 1) / kQueriesPerWG32);
         int gx32 = scan_grid_x(ntiles);
         if (gy32 > 1 && ntiles >= 8) {

@@ -279,6 +279,12 @@ class RowAnswerMatcher:
         return hit
 
 
+# limits of drt_hit_metrics_i8 (csrc/match.hip kMetricMaxK / kMetricMaxB / kMetricMaxT)
+METRICS_MAX_K = 2048
+METRICS_MAX_B = 4096
+METRICS_MAX_T = 16
+
+
 class DeviceRowMatcher:
     """RowAnswerMatcher with the token slots resident in HBM: a query batch's k retrieved rows are
     gathered and compared on the GPU (the host only tokenises the batch's answers and any row not
@@ -366,12 +372,31 @@ class DeviceRowMatcher:
         if B == 0:
             return
         hit = self._enqueue_hits(rows, text_of, answers)
+        T = int(topk_dev.numel())
+        if k > METRICS_MAX_K or B > METRICS_MAX_B or T > METRICS_MAX_T:
+            # beyond the kernel's LDS-resident limits (k up to 32768 on the large-k search path, huge
+            # loader batches, many cut-offs): this batch's get_metrics on the host, added to the same sums
+            from .metrics import get_metrics
+            pos = np.zeros((B, k), dtype=np.int8) if hit is None else self._host_hits(hit)
+            topk = [int(x) for x in topk_dev.cpu().tolist()]
+            m = get_metrics(pos, topk)
+            vals = [m[f"Recall@{t}"] for t in topk] + [m[f"MRR@{t}"] for t in topk] + [m[f"NDCG@{t}"] for t in topk]
+            with torch.cuda.stream(self.stream):
+                acc.add_(torch.tensor(vals, dtype=torch.float64).to(self.device, non_blocking=False))
+            return
         with torch.cuda.stream(self.stream):
             if hit is None:
                 hit = torch.zeros((B, k), dtype=torch.int8, device=self.device)
             _native.check(_native.load().drt_hit_metrics_i8(hit.data_ptr(), B, k, topk_dev.data_ptr(),
                                                              int(topk_dev.numel()), acc.data_ptr(),
                                                              self.stream.cuda_stream), "drt_hit_metrics_i8")
+
+    def _host_hits(self, hit):
+        """The device hit matrix [B, k] read back (the matcher's stream drained)."""
+        import torch
+        with torch.cuda.stream(self.stream):
+            out = hit.cpu()
+        return out.numpy()
 
     def _enqueue_hits(self, rows, text_of, answers):
         """hit [B, k] int8 on the device (the matcher's stream), or None when no row has tokens."""

@@ -104,10 +104,20 @@ def _ip_topk_large(q, p, k, id_offset, out, status, stats):
             s, _, _ = ip_topk(q, p[a:b], m)   # certified fp32 scan scores
             tau = s[:, m - 1].clone() if tau is None else torch.minimum(tau, s[:, m - 1])
     scores, ids, st = drt.ip_topk_large(q, p, k, id_offset, stats, tau.contiguous())
-    nbad = int((st != 0).sum().item())
-    if nbad:
-        raise RuntimeError(f"ip_topk k={k}: {nbad} queries collected more than {_WIDE_CAP} rows within the "
-                           "fp32 error of their threshold (massive near-ties); no exact order was produced")
+    bad = torch.nonzero(st != 0).flatten()
+    if bad.numel():
+        # the range plan's threshold was too low for these queries (a corpus ordered or clustered by
+        # position: one range of weak rows drags the minimum far below the k-th score and more than
+        # _WIDE_CAP rows pass it).  Retry them at a threshold next to their own k-th score (_kth_bound)
+        qb = q.index_select(0, bad).contiguous()
+        s2, i2, st2 = drt.ip_topk_large(qb, p, k, id_offset, stats, _kth_bound(qb, p, k, stats))
+        scores.index_copy_(0, bad, s2)
+        ids.index_copy_(0, bad, i2)
+        st.index_copy_(0, bad, st2)
+        nbad = int((st2 != 0).sum().item())
+        if nbad:
+            raise RuntimeError(f"ip_topk k={k}: {nbad} queries have more than {_WIDE_CAP} rows within the fp32 "
+                               "error of their k-th score (massive near-ties); no exact order was produced")
     if out is not None:
         out[0].copy_(scores)
         out[1].copy_(ids)
@@ -116,6 +126,30 @@ def _ip_topk_large(q, p, k, id_offset, out, status, stats):
         status.copy_(st)
         st = status
     return scores, ids, st
+
+
+_KTH_ROWS = 1 << 20   # rows per dense block of _kth_bound
+
+
+def _kth_bound(q: torch.Tensor, p: torch.Tensor, k: int, stats: torch.Tensor) -> torch.Tensor:
+    """A threshold no larger than each query's EXACT k-th score and within two fp32 error bounds of it
+    (drt_ip_topk_large then collects only the near-tie window around the k-th score, whatever the row
+    order): the k-th largest of the queries' dense fp32 scores (MFMA GEMM, gemm_nt_f32, over row
+    blocks, running top-k values), lowered by a bound on any fp32 summation of the d exact bf16 x bf16
+    products -- 1.1 d u ||q|| max ||p||, above both the classic gamma_(d-1) bound and the scan's measured
+    MFMA-chain bound (10 u per 32-term step, csrc/search.hip "Error bound") -- so k rows' exact sums lie
+    above it.  Dense work for the (rare) queries that need it only."""
+    nq, d = q.shape
+    best = None
+    for a in range(0, p.shape[0], _KTH_ROWS):
+        g = gemm_nt_f32(q, p[a: a + _KTH_ROWS])
+        cand = g if best is None else torch.cat([best, g], dim=1)
+        best = torch.topk(cand, min(k, cand.shape[1]), dim=1, sorted=False).values
+        del g, cand
+    gk = best.min(dim=1).values if best.shape[1] >= k else torch.full((nq,), float("-inf"), device=q.device)
+    qn = q.float().pow(2).sum(1).sqrt()
+    eps = 1.1 * d * 2.0 ** -24 * qn * stats[0].clamp_min(0).sqrt()
+    return (gk - eps).contiguous()
 
 
 def resolve_failed(q, p, k, id_offset, scores, ids, status, n_failed: Optional[int] = None,

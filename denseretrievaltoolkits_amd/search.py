@@ -151,6 +151,28 @@ def _groups(batches, cap=None):
         yield grp
 
 
+def _reserve_group_memory(local, k: int, n_global: int, chunks=None):
+    """Size torch's caching allocator for a FULL group once per (index, k): the group's sample / filter
+    workspace (~0.85 GB at 2048 queries over a 10M-row shard) and its result lists are carved from one
+    segment allocated here, so the first full group after shorter ones (a short warm-up, a small first
+    batch set) does not hipMalloc inside the search.  (Round 6: the driver's 20-step bench met its first
+    2048-query group after a 640-query warm-up.)"""
+    key = (k, n_global, GROUP_QUERIES)
+    if getattr(local, "_group_reserved", None) == key or local.ntotal == 0:
+        return
+    kc = kernels.refine_width(k)
+    nq = GROUP_QUERIES
+    ws = int(_native.load().drt_ip_topk_dist_workspace(nq, local.ntotal, n_global, local.dp, kc))
+    nparts = max(1, len(chunks or [0]))
+    lists = nq * (kc + 1) * 8 * (nparts + 1)                  # packed lists (+ the chunked form's parts)
+    outs = nq * kc * (4 + 8 + 4) + nq * k * (4 + 8) * 2       # merge outputs, deltas, refined results
+    need = ws + lists + outs + (64 << 20)
+    with torch.cuda.device(local.device):
+        blk = torch.empty(need, dtype=torch.uint8, device=local.device)
+        del blk   # back to the cache as one free segment the group's allocations are split from
+    local._group_reserved = key
+
+
 def _gtau_enqueue_group(local, qs, k: int, n_global: int, offset: int, gather, to_host: bool = False,
                         stats=None, all_reduce_sum=None, id_shift: int = 0, chunks=None):
     """One group of query batches through the global-threshold protocol (see ShardedFlatIP):
@@ -400,6 +422,7 @@ class FlatIPIndex:
             return [self._enqueue(q, k, id_offset, None, to_host) for q in batches]
         out = []
         stats = self._stats_arg()
+        _reserve_group_memory(self, k, self.ntotal, group_chunks(self.ntotal))
         for g in _groups(list(batches)):
             gp = _GroupPend(_gtau_enqueue_group(self, [self._queries(q) for q in g], k, self.ntotal, 0,
                                                 lambda t: t.unsqueeze(0), to_host, stats=stats, id_shift=id_offset,
@@ -447,6 +470,7 @@ class FlatIPIndex:
 
         stats = self._stats_arg()
         chunks = group_chunks(self.ntotal)
+        _reserve_group_memory(self, k, self.ntotal, chunks)
         for res in _pipeline(groups, lambda j, g: _gtau_enqueue_group(self, g, k, self.ntotal, 0,
                                                                       lambda t: t.unsqueeze(0), to_host,
                                                                       stats=stats, id_shift=id_offset,
@@ -599,6 +623,8 @@ class ShardedFlatIP:
                 return res
 
             chunks = self.group_chunks()
+            if isinstance(self.local, FlatIPIndex):
+                _reserve_group_memory(self.local, k, self.ntotal, chunks)
             for res in _pipeline(groups, lambda j, g: _gtau_enqueue_group(
                     self.local, g, k, self.ntotal, self.offset, self._all_gather, to_host, stats=self.stats,
                     all_reduce_sum=lambda t: comm.all_reduce_sum_(t, self.group), chunks=chunks), fin):

@@ -408,7 +408,9 @@ class Trainer:
 
         # device metrics: the matches and get_metrics of every loader batch stay on the GPU (summed there,
         # read back once after the last batch) and the search's ids never leave the device -- unless the
-        # retrieve/ output file needs the documents on the host
+        # retrieve/ output file needs the documents on the host.  (A batch beyond the metrics kernel's limits
+        # -- k > 2048 on the large-k search path, > 4096 queries, > 16 cut-offs -- has its get_metrics taken
+        # on the host inside match_metrics, into the same sums.)
         dev_metrics = isinstance(matcher, DeviceRowMatcher) and not rdir
         if dev_metrics:
             macc = torch.zeros(3 * len(topk), dtype=torch.float64, device=self.device)

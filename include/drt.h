@@ -483,6 +483,9 @@ int drt_score_ce_bwd(const float* q, const float* p, const float* S, const float
  * their durations (ms) and the launch count, then clears the record.        */
 int drt_profile_enable(int32_t family, int32_t enable);
 int drt_profile_read(int32_t family, double* total_ms, int64_t* count);
+/* The same, launch by launch: the first min(cap, recorded) durations (ms) in launch order go to
+ * ms_each, *count = the number recorded; the record is cleared.                                 */
+int drt_profile_read_each(int32_t family, double* ms_each, int64_t cap, int64_t* count);
 
 #ifdef __cplusplus
 }

@@ -102,3 +102,37 @@ def test_world2_grouped_prices_the_shard_chunks():
     rf = r["roofline"]
     assert rf["launches"] == 4 and rf["launch_shapes"] == [(2048, 1_250_000)]
     assert "4 launch(es) over row chunks of the shard" in r["config"]["path"]
+
+
+@pytest.mark.parametrize("world", [2, 3, 8])
+def test_bench_corpus_union_of_shards_is_the_world1_corpus(world, monkeypatch):
+    """corpus rows are seeded by GLOBAL row block, so the W shards of the 1/2/4/8-GPU
+    runs concatenate to the one-GPU corpus (same rows searched at every N)."""
+    import torch
+    import bench
+    monkeypatch.setattr(bench, "CORPUS_BLOCK_ROWS", 1000)
+    n, d = 5321, 16
+    full, lo, hi = bench.gen_shard(n, 1, 0, d, torch.device("cpu"))
+    assert (lo, hi) == (0, n)
+    parts = [bench.gen_shard(n, world, r, d, torch.device("cpu")) for r in range(world)]
+    assert parts[0][1] == 0 and parts[-1][2] == n
+    assert all(parts[r][2] == parts[r + 1][1] for r in range(world - 1))
+    assert torch.equal(torch.cat([p[0] for p in parts]).view(torch.int16), full.view(torch.int16))
+
+
+def test_per_shape_roofline_of_a_20_step_run():
+    """The driver's --steps 20 runs a 2048-query group and a 512-query group: the record reports each
+    launch shape's own average and fraction beside the mixed average."""
+    import bench
+    from denseretrievaltoolkits_amd import search as srch
+    ch = srch.group_chunks(10_000_000)
+    shapes = bench.launch_shapes(20, 128, True, 2048, 10_000_000, ch)
+    each = [3.0 if q == 2048 else 0.8 for q, _ in shapes]
+    a = _args(10_000_000, 20)
+    r = bench.search_record(a, 1, True, 2048, KC, 20 * 1.7e-3, sum(each), len(each), (None, None), chunks=ch,
+                            each_ms=each)
+    ps = r["roofline"]["per_shape"]
+    assert [(p["queries"], p["rows"], p["launches"]) for p in ps] == [(2048, 1_250_000, 8), (512, 1_250_000, 8)]
+    assert ps[0]["avg_launch_ms"] == 3.0 and ps[1]["avg_launch_ms"] == 0.8
+    assert abs(ps[0]["frac"] - 2 * 2048 * 1_250_000 * 768 / 2.5e15 / 3.0e-3) < 1e-3
+    assert r["roofline"]["avg_launch_ms"] == round(sum(each) / 16, 4)

@@ -120,3 +120,24 @@ def test_flat_index_large_k_batches(dev):
     idx.exact_order = False
     s, i = idx.search_device(qd[:8], k)
     np.testing.assert_array_equal(i.cpu().numpy(), ei[:8])
+
+
+def test_large_k_corpus_ordered_by_relevance(dev):
+    """A corpus whose first third is relevant to the queries (passages grouped by article, sources
+    appended one after another): the range plan's minimum is dragged down by the weak ranges and every
+    row of the first range passes it (> 65,536 rows), so those queries are retried at a threshold next
+    to their own k-th score (kernels._kth_bound) -- the answer is still the fp64 oracle's."""
+    rng = np.random.default_rng(41)
+    n, d, k, nq = 200000, 768, 5000, 6
+    base = rng.standard_normal((1, d)).astype(np.float32)
+    q = gauss_bf16(rng, (nq, d)) * 0.25 + base
+    p = rng.standard_normal((n, d)).astype(np.float32)
+    p[: n // 3] += 0.5 * base           # rows [0, n / 3) score far above the rest
+    from oracle.search_oracle import bf16_round
+    q, p = bf16_round(q), bf16_round(p)
+    gs, gi, st = _large(dev, q, p, k)
+    es, ei = orc.ip_topk(q, p, k)
+    assert (st == 0).all()
+    assert (ei < n // 3).all()          # the setting: the whole top-k comes from the first range
+    np.testing.assert_array_equal(gi, ei)
+    _assert_scores(gs, es)

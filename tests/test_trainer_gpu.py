@@ -57,6 +57,10 @@ def _loaders(n_docs, n_q, L_p, L_q, bs):
     # BASELINE config C1's shape (1k passages / 32 queries, BERT-base) at k = 1000 = every row
     (12, 1000, 32, 1000, 128, 32, 128, True),
     (12, 1000, 32, 1000, 128, 32, 128, False),
+    # retrieve_num beyond the candidate-list kernels (the large-k search path) and beyond the device
+    # metrics kernel's k <= 2048: that batch's get_metrics runs on the host, into the same sums
+    (1, 5000, 24, 3000, 64, 16, 256, False),
+    (1, 5000, 24, 3000, 64, 16, 256, True),
 ])
 def test_evaluate_end_to_end_matches_oracle(dev, tmp_path, layers, n_docs, n_q, k, L_p, L_q, bs, files):
     import torch
