@@ -36,7 +36,15 @@ constexpr int kHitCap = 1024;       // LDS hit list entries per work-group
 // serialised in L2 (r02 A/B: see DESIGN.md §3).
 constexpr int kCntStride = 32;
 
-enum { SCAN_FILTER = 0, SCAN_DENSE = 1 };
+enum { SCAN_FILTER = 0, SCAN_DENSE = 1, SCAN_TOPR = 2 };
+// SCAN_TOPR (the grouped sample pass, round 6): instead of writing every sampled score, each lane keeps
+// the kTopRL best keys of its query over the rows it sees (its 4 rows of every tile of its work-group)
+// in registers and writes that list once; the union of a query's lists (4 per work-group column) holds
+// every sampled key that beats all but kTopRL - 1 of its list-mates, so its r-th best is the r-th best
+// sampled key unless more than kTopRL of the r best fell into one lane's share (then a slightly lower
+// threshold: more filter hits, never a wrong result -- the filter's counts certify).  Round 5 wrote a
+// [2048, 70.8k] u32 score matrix per group (580 MB) for kth_partial to read back.
+constexpr int kTopRL = 4;
 
 struct ScanArgs {
   const __bf16* Q;
@@ -389,6 +397,12 @@ __global__ __launch_bounds__(NW * 64, 1) void ip_scan16_kernel(ScanArgs a) {
 #pragma unroll
   for (int m = 0; m < 2; ++m) aoff[m] = r * 128 + (((4 * m + kq) ^ sw) << 4);
 
+  uint32_t topl[QB][MODE == SCAN_TOPR ? kTopRL : 1];
+#pragma unroll
+  for (int b = 0; b < QB; ++b)
+#pragma unroll
+    for (int i = 0; i < (MODE == SCAN_TOPR ? kTopRL : 1); ++i) topl[b][i] = 0xFFFFFFFFu;
+
   // The epilogue (filter / key stores) of tile it runs after the MFMAs of tile it + 1 are
   // issued (two accumulator sets, alternating): its VALU work and the wait for the last MFMA
   // result overlap the next tile's matrix work instead of stalling the wave at every tile.
@@ -457,6 +471,22 @@ __global__ __launch_bounds__(NW * 64, 1) void ip_scan16_kernel(ScanArgs a) {
           }
         }
       }
+    } else if (MODE == SCAN_TOPR) {
+      // bubble each of the lane's 4 keys through its sorted list (min / max, no indexing): the list
+      // keeps the kTopRL smallest keys (best scores) seen so far; padding rows insert nothing
+#pragma unroll
+      for (int b = 0; b < QB; ++b) {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          uint32_t x = rowbase + j < a.nrows ? desc_key(acc[b][j]) : 0xFFFFFFFFu;
+#pragma unroll
+          for (int i = 0; i < kTopRL; ++i) {
+            const uint32_t lo = x < topl[b][i] ? x : topl[b][i];
+            x = x < topl[b][i] ? topl[b][i] : x;
+            topl[b][i] = lo;
+          }
+        }
+      }
     } else {
 #pragma unroll
       for (int b = 0; b < QB; ++b) {
@@ -516,6 +546,15 @@ __global__ __launch_bounds__(NW * 64, 1) void ip_scan16_kernel(ScanArgs a) {
   if (my_tiles & 1) epilogue(accA, rbA);
   else epilogue(accB, rbB);
 
+  if (MODE == SCAN_TOPR) {   // list (work-group column x, row quad kq) of each of the lane's queries
+#pragma unroll
+    for (int b = 0; b < QB; ++b) {
+      if (!qok[b]) continue;
+      uint32_t* o = (uint32_t*)a.out + qg[b] * a.cap + ((int64_t)blockIdx.x * 4 + kq) * kTopRL;
+#pragma unroll
+      for (int i = 0; i < kTopRL; ++i) o[i] = topl[b][i];
+    }
+  }
   if (MODE == SCAN_FILTER) {
     lds_barrier();
     const uint32_t nf = *hit_n;
@@ -1631,18 +1670,18 @@ __global__ __launch_bounds__(kKthThreads) void kth_partial_kernel(const uint32_t
 // counters, so the fused distributed filter needs no separate memset launch).
 __global__ __launch_bounds__(kKthThreads) void kth_final_kernel(const uint32_t* part, int nlists, int r,
                                                                 int64_t lstride, int64_t qstride, float* tau,
-                                                                uint32_t* best, uint32_t* zero) {
+                                                                uint32_t* best, uint32_t* zero, int len) {
   __shared__ uint32_t buf[kKthChunk];
   const int64_t q = blockIdx.x;
   if (zero && threadIdx.x == 0) zero[q * kCntStride] = 0;
-  const int tot = nlists * r;
+  const int tot = nlists * len;   // nlists lists of len keys each (len = r: best-r lists)
   {
     uint32_t tmp[kKthChunk / kKthThreads];
 #pragma unroll
     for (int u = 0; u < kKthChunk / kKthThreads; ++u) {
       const int i = threadIdx.x + u * kKthThreads;
       const int ic = i < tot ? i : 0;
-      const uint32_t x = part[(int64_t)(ic / r) * lstride + q * qstride + (ic % r)];
+      const uint32_t x = part[(int64_t)(ic / len) * lstride + q * qstride + (ic % len)];
       tmp[u] = i < tot ? x : 0xFFFFFFFFu;
     }
 #pragma unroll
@@ -3282,23 +3321,29 @@ static int scan_grid_x(int64_t ntiles) {
   return (int)std::max<int64_t>(g, 1);
 }
 
-template <int D>
-static int launch_scan_d(const ScanArgs& a, int mode, hipStream_t s) {
-  if (a.nq == 0 || a.nrows == 0) return DRT_OK;
-  const unsigned gy = (unsigned)((a.nq + kQueriesPerWG - 1) / kQueriesPerWG);
-  const int64_t ntiles = (a.nrows + kT16 - 1) / kT16;
-  // Several 128-query blocks in one launch (a group of batches): gridDim.x = CUs / blocks, a multiple
-  // of 8, so work-groups (x, y) and (x, y') -- the same tiles for different query blocks -- sit on the
-  // same XCD (work-groups are dealt to XCDs round-robin by linear id) and run at the same time: a tile
-  // comes from HBM once and from that XCD's L2 for the other blocks.  (gridDim.x = CUs ran the blocks
-  // one after another, each streaming the whole shard from HBM.)
+// Grid of the 16-row scans (128 queries per work-group row): several 128-query blocks in one launch (a
+// group of batches) get gridDim.x = CUs / blocks, a multiple of 8, so work-groups (x, y) and (x, y') -- the
+// same tiles for different query blocks -- sit on the same XCD (work-groups are dealt to XCDs round-robin
+// by linear id) and run at the same time: a tile comes from HBM once and from that XCD's L2 for the other
+// blocks.  (gridDim.x = CUs ran the blocks one after another, each streaming the whole shard from HBM.)
+static dim3 scan16_grid(int64_t nq, int64_t nrows) {
+  const unsigned gy = (unsigned)((nq + kQueriesPerWG - 1) / kQueriesPerWG);
+  const int64_t ntiles = (nrows + kT16 - 1) / kT16;
   int gx = scan_grid_x(ntiles);
   if (gy > 1 && ntiles >= 8) {
     const int cus = scan_grid_x((int64_t)1 << 40);
     const int share = std::max(8, (cus / (int)gy) & ~7);
     gx = (int)std::min<int64_t>(ntiles, share);
   }
-  const dim3 grid(gx, gy);
+  return dim3(gx, gy);
+}
+
+template <int D>
+static int launch_scan_d(const ScanArgs& a, int mode, hipStream_t s) {
+  if (a.nq == 0 || a.nrows == 0) return DRT_OK;
+  const int64_t ntiles = (a.nrows + kT16 - 1) / kT16;
+  const dim3 grid = scan16_grid(a.nq, a.nrows);
+  const unsigned gy = grid.y;
   if (mode == SCAN_FILTER) {
     // 8 waves (2 per SIMD), 16 queries each; fragment reads of the next tile rolled into this
     // tile's MFMAs, non-temporal corpus loads, s_setprio 1 for waves 4-7 (r02 A/B, tools/scan_ab.py,
@@ -3334,6 +3379,8 @@ static int launch_scan_d(const ScanArgs& a, int mode, hipStream_t s) {
         hipLaunchKernelGGL((ip_scan16r_kernel<D, true>), grid, dim3(512), 0, s, a);
       }
     }
+  } else if (mode == SCAN_TOPR) {
+    hipLaunchKernelGGL((ip_scan16_kernel<D, SCAN_TOPR>), grid, dim3(512), 0, s, a);
   } else {
     hipLaunchKernelGGL((ip_scan16_kernel<D, SCAN_DENSE>), grid, dim3(512), 0, s, a);
   }
@@ -3539,7 +3586,7 @@ static int ip_topk_impl(const void* Q, int64_t nq, const void* P, int64_t n, int
                          (uint32_t*)(w + p.off_part));
       hipLaunchKernelGGL(kth_final_kernel, dim3((unsigned)nq), dim3(kKthThreads), 0, s,
                          (const uint32_t*)(w + p.off_part), (int)p.nchunk, (int)p.r, (int64_t)p.r,
-                         (int64_t)(p.nchunk * p.r), tau, (uint32_t*)nullptr, cnt);   // also zeroes the hit counters
+                         (int64_t)(p.nchunk * p.r), tau, (uint32_t*)nullptr, cnt, (int)p.r);   // also zeroes the hit counters
     }
     prof_end(pp, s);
     DRT_CHECK_HIP(hipGetLastError());
@@ -4056,6 +4103,21 @@ int drt_ip_topk_dist_sample(const void* Q, int64_t nq, const void* P, int64_t n_
   a.nrows = p.m;
   a.rstride = p.stride;
   a.out = w + p.off_sample;
+  // top-r sample pass (SCAN_TOPR): 4 lists of kTopRL keys per query and work-group column, their union's
+  // r-th best in one kth_final launch -- when the union fits kth_final's 4096 keys and the sample buffer
+  const int64_t nlists = 4 * (int64_t)scan16_grid(nq, p.m).x;
+  if (nlists * kTopRL <= kKthChunk && nlists * kTopRL <= align_up(p.m, 4)) {
+    a.cap = nlists * kTopRL;
+    DRT_CHECK_HIP(hipMemsetAsync(a.out, 0xFF, (size_t)nq * a.cap * 4, s));
+    int rc = launch_scan(a, d, SCAN_TOPR, s, PROF_SAMPLE);
+    if (rc) return rc;
+    const ProfPair pp = prof_begin(PROF_SELECT, s);
+    hipLaunchKernelGGL(kth_final_kernel, dim3((unsigned)nq), dim3(kKthThreads), 0, s, (const uint32_t*)a.out,
+                       (int)nlists, (int)r, (int64_t)kTopRL, (int64_t)a.cap, (float*)nullptr, best,
+                       (uint32_t*)nullptr, kTopRL);
+    prof_end(pp, s);
+    return hip_status(hipGetLastError());
+  }
   a.cap = align_up(p.m, 4);
   int rc = launch_scan(a, d, SCAN_DENSE, s, PROF_SAMPLE);
   if (rc) return rc;
@@ -4066,7 +4128,7 @@ int drt_ip_topk_dist_sample(const void* Q, int64_t nq, const void* P, int64_t n_
                      (uint32_t*)(w + p.off_part));
   hipLaunchKernelGGL(kth_final_kernel, dim3((unsigned)nq), dim3(kKthThreads), 0, s,
                      (const uint32_t*)(w + p.off_part), (int)p.nchunk, (int)r, (int64_t)r, (int64_t)(p.nchunk * r),
-                     (float*)nullptr, best, (uint32_t*)nullptr);
+                     (float*)nullptr, best, (uint32_t*)nullptr, (int)r);
   prof_end(pp, s);
   return hip_status(hipGetLastError());
 }
@@ -4077,7 +4139,8 @@ int drt_ip_topk_dist_tau(const uint32_t* lists, int64_t nq, int32_t nlists, int3
   if (nq == 0) return DRT_OK;
   DRT_REQUIRE(lists && tau);
   hipLaunchKernelGGL(kth_final_kernel, dim3((unsigned)nq), dim3(kKthThreads), 0, (hipStream_t)stream, lists,
-                     (int)nlists, (int)r, (int64_t)nq * r, (int64_t)r, tau, (uint32_t*)nullptr, (uint32_t*)nullptr);
+                     (int)nlists, (int)r, (int64_t)nq * r, (int64_t)r, tau, (uint32_t*)nullptr, (uint32_t*)nullptr,
+                     (int)r);
   return hip_status(hipGetLastError());
 }
 
@@ -4226,7 +4289,8 @@ int drt_ip_topk_dist_filter_lists_at(const void* Q, int64_t nq, const void* P, i
   uint32_t* cnt = (uint32_t*)(w + p.off_cnt);
   float* tau = tau_out ? tau_out : (float*)(w + p.off_tau);
   hipLaunchKernelGGL(kth_final_kernel, dim3((unsigned)nq), dim3(kKthThreads), 0, s, lists, (int)nlists, (int)r,
-                     lists_stride, (int64_t)r, tau, (uint32_t*)nullptr, n_local > 0 ? cnt : (uint32_t*)nullptr);
+                     lists_stride, (int64_t)r, tau, (uint32_t*)nullptr, n_local > 0 ? cnt : (uint32_t*)nullptr,
+                     (int)r);
   DRT_CHECK_HIP(hipGetLastError());
   SelectArgs sa{};
   sa.in = w + p.off_keys;

@@ -198,3 +198,44 @@ def test_dist_filter_chunks_equals_whole_shard(dev, nq, n, d, k, starts):
         kernels.dist_filter_chunks_into(qt, pt, n_global, k, off, tau, starts, chunked)
         torch.cuda.synchronize()
         assert torch.equal(chunked, whole), data
+
+
+@pytest.mark.parametrize("nq,n,d,data", [
+    (2048, 1_250_000, 768, "gauss"),   # a one-GPU group chunk / the W = 8 shard: the top-r sample pass
+    (512, 400_000, 768, "int"),        # heavy ties
+    (300, 200_000, 128, "gauss"),      # partial query blocks, narrow rows
+])
+def test_top_r_sample_pass_lower_bounds_the_rth_sampled_key(dev, nq, n, d, data):
+    """White-box (round 6): the grouped sample pass keeps per-lane lists of the best sampled keys
+    (SCAN_TOPR) instead of writing every sampled score.  The returned [nq, r] list must be sorted, made
+    of real sampled keys (each at least as far down the order as the exact r best: element-wise >= in
+    key order, so tau can only be lower -- never a wrong result, the filter's counts certify) and equal
+    to the exact best-r sampled keys for nearly every query."""
+    import torch
+    from denseretrievaltoolkits_amd import kernels
+    rng = np.random.default_rng(nq + n)
+    k = 1000
+    q = gauss_bf16(rng, (nq, d)) if data == "gauss" else int_bf16(rng, (nq, d), -4, 4)
+    qt = to_dev_bf16(q, dev)
+    if data == "gauss":
+        pt = torch.randn((n, d), generator=torch.Generator(device=dev).manual_seed(n), device=dev).to(torch.bfloat16)
+    else:
+        from helpers import device_int_corpus
+        pt = device_int_corpus(n, d, -4, 4, seed=n, device=dev)
+    n_global = 8 * n
+    got = kernels.dist_sample(qt, pt, n_global, k).cpu().numpy().view(np.uint32)
+    plan = orc.dist_plan(n, n_global, k)
+    r = plan["r"]
+    rows = torch.from_numpy(plan["rows"]).to(dev)
+    ps = pt[rows].double().cpu().numpy()   # the sampled rows; their exact scores, rounded to fp32
+    want = np.sort(orc.desc_key((q.astype(np.float64) @ ps.T).astype(np.float32)), axis=1)[:, :r]
+    assert got.shape == (nq, r)
+    assert (np.diff(got.astype(np.int64), axis=1) >= 0).all()
+    if data == "int":     # exact scores: the lists are comparable key for key
+        assert (got >= want).all()
+        assert (got == want).all(axis=1).mean() >= 0.99
+    else:                 # fp32 chains vs fp64-rounded sums: compare the thresholds' scores within 1e-3
+        gt = orc.desc_key_to_score(got[:, r - 1]).astype(np.float64)
+        wt = orc.desc_key_to_score(want[:, r - 1]).astype(np.float64)
+        assert (gt <= wt + 1e-3).all()
+        assert (np.abs(gt - wt) <= 1e-3).mean() >= 0.99

@@ -43,7 +43,7 @@ def main():
     print(json.dumps({"rows": a.rows, "queries": a.queries, "ms_per_launch": round(e0.elapsed_time(e1) / a.reps, 4),
                       "valid_per_query_mean": round(float(hits.mean()), 1),
                       # order-independent digest of the packed lists (variants must match bit for bit)
-                      "digest": int((packed.view(torch.int32).double() * torch.arange(1, 2 * packed.numel() + 1,
+                      "digest": int((packed.view(torch.int32).reshape(-1).double() * torch.arange(1, 2 * packed.numel() + 1,
                                      device=dev, dtype=torch.float64).remainder(1009)).sum().item())}), flush=True)
 
 
