@@ -67,6 +67,9 @@ _SIGNATURES = [
     ("drt_ip_topk_large_workspace", c_sz, [c_i32, c_i32]),
     ("drt_ip_topk_large", c_i32, [c_vp, c_i64, c_vp, c_i64, c_i32, c_i32, c_i64, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp,
                                   c_sz, c_vp]),
+    ("drt_ip_topk_large_keys", c_i32, [c_vp, c_i64, c_vp, c_i64, c_i32, c_i32, c_i64, c_vp, c_vp, c_vp, c_vp, c_vp,
+                                       c_vp, c_vp, c_sz, c_vp]),
+    ("drt_merge_exact", c_i32, [c_vp, c_vp, c_i64, c_i32, c_i32, c_vp, c_vp, c_vp]),
     ("drt_refine_delta_bf16", c_i32, [c_vp, c_i64, c_i32, c_vp, c_i64, c_i64, c_vp, c_vp, c_i32, c_i32, c_vp, c_vp,
                                       c_vp, c_vp, c_vp, c_vp]),
     ("drt_refine_delta_local_bf16", c_i32, [c_vp, c_i64, c_i32, c_vp, c_i64, c_i64, c_vp, c_vp, c_i32, c_i32, c_vp,

@@ -2744,6 +2744,8 @@ struct WideArgs {
   uint32_t* sel_n;
   uint64_t* bin_k;        // [*, k] the selected entries regrouped by bin (large_rank_kernel)
   uint32_t* bin_r;
+  uint64_t* out_keys;     // optional [*, k]: the exact order key of every output entry (~0: pad) -- what a
+                          // sharded index merges by (drt_merge_exact)
 };
 
 __device__ __forceinline__ int64_t wide_out_row(const WideArgs& w, int j) {
@@ -2991,15 +2993,25 @@ __global__ __launch_bounds__(kWideThreads) void large_select_kernel(WideArgs w) 
 }
 
 // One work-group per query: rank = the number of selected entries before an entry in (exact key, row)
-// order, counted within bins -- a histogram of the exact keys over kLargeBins equal ranges between the
-// set's min and max key (a monotone map: an entry's bin never exceeds a larger entry's), the bins'
-// exclusive prefix, the entries regrouped by bin, then each entry compared only with its own bin's.
-// Ties share a bin, so a set of many equal keys degrades towards the all-pairs count.
+// order, counted within bins -- a histogram of the exact SCORES (decoded from the keys) over kLargeBins
+// equal ranges between the set's max and min score (a monotone map: an entry's bin never exceeds a
+// larger key's), the bins' exclusive prefix, the entries regrouped by bin, then each entry compared only
+// with its own bin's.  Ties share a bin, so a set of many equal keys degrades towards the all-pairs count.
+// (Round 6: the bins were equal ranges of the raw 64-bit key; a set whose scores cross zero or span
+// several binades then crowded into a few bins -- the advisor's finding -- and the per-bin counts grew
+// towards k^2.)
 constexpr int kLargeBins = 4096;
 
-__device__ __forceinline__ int large_bin(uint64_t key, uint64_t kmin, double scale) {
-  const int b = (int)((double)(key - kmin) * scale);
-  return b < kLargeBins - 1 ? b : kLargeBins - 1;
+__device__ __forceinline__ double large_key_score(uint64_t key) {   // inverse of desc_key64
+  const uint64_t ord = ~key;
+  const uint64_t u = (ord >> 63) ? (ord & 0x7FFFFFFFFFFFFFFFull) : ~ord;
+  return __builtin_bit_cast(double, u);
+}
+
+__device__ __forceinline__ int large_bin(uint64_t key, double smax, double scale) {
+  const double x = (smax - large_key_score(key)) * scale;   // >= 0, non-decreasing in the key
+  const int b = x < (double)(kLargeBins - 1) ? (int)x : kLargeBins - 1;
+  return b > 0 ? b : 0;
 }
 
 __global__ __launch_bounds__(kLargeThreads) void large_rank_kernel(WideArgs w) {
@@ -3042,9 +3054,12 @@ __global__ __launch_bounds__(kLargeThreads) void large_rank_kernel(WideArgs w) {
     lo = red[0][q] < lo ? red[0][q] : lo;
     hi = red[1][q] > hi ? red[1][q] : hi;
   }
-  const double scale = m ? (double)kLargeBins / ((double)(hi - lo) + 1.0) : 0.0;
+  // lo / hi: the smallest / largest key = the best / worst score of the set
+  const double smax = m ? large_key_score(lo) : 0.0, smin = m ? large_key_score(hi) : 0.0;
+  const double range = smax - smin;
+  const double scale = range > 0.0 ? (double)kLargeBins / (range * (1.0 + 1e-12)) : 0.0;
   // histogram, exclusive prefix (4 bins per thread, wave scan, wave totals)
-  for (uint32_t i = tid; i < m; i += kLargeThreads) atomicAdd(&start[large_bin(sk[i], lo, scale)], 1u);
+  for (uint32_t i = tid; i < m; i += kLargeThreads) atomicAdd(&start[large_bin(sk[i], smax, scale)], 1u);
   __syncthreads();
   constexpr int kPer = kLargeBins / kLargeThreads;
   uint32_t c[kPer], tot = 0;
@@ -3073,7 +3088,7 @@ __global__ __launch_bounds__(kLargeThreads) void large_rank_kernel(WideArgs w) {
   // regroup by bin (positions within a bin are arbitrary: the counts below do not depend on them)
   for (uint32_t i = tid; i < m; i += kLargeThreads) {
     const uint64_t v = sk[i];
-    const uint32_t pos = atomicAdd(&cursor[large_bin(v, lo, scale)], 1u);
+    const uint32_t pos = atomicAdd(&cursor[large_bin(v, smax, scale)], 1u);
     bk[pos] = v;
     br[pos] = sr[i];
   }
@@ -3083,23 +3098,68 @@ __global__ __launch_bounds__(kLargeThreads) void large_rank_kernel(WideArgs w) {
   for (uint32_t i = tid; i < m; i += kLargeThreads) {
     const uint64_t ki = sk[i];
     const uint32_t ri = sr[i];
-    const int b = large_bin(ki, lo, scale);
+    const int b = large_bin(ki, smax, scale);
     const uint32_t b0 = start[b], b1 = cursor[b];   // cursor = end of the bin after the regroup
     uint32_t rank = b0;
     for (uint32_t t = b0; t < b1; ++t) {
       const uint64_t kt = bk[t];
       rank += (kt < ki || (kt == ki && br[t] < ri)) ? 1u : 0u;
     }
-    const uint64_t ord = ~ki;
-    const uint64_t u = (ord >> 63) ? (ord & 0x7FFFFFFFFFFFFFFFull) : ~ord;
-    os[rank] = (float)__builtin_bit_cast(double, u);
+    os[rank] = (float)large_key_score(ki);
     oi[rank] = (int64_t)ri + w.id_offset;
+    if (w.out_keys) w.out_keys[orow * w.k + rank] = ki;
   }
   for (int64_t i = (int64_t)m + tid; i < w.k; i += kLargeThreads) {
     os[i] = kPadScore;
     oi[i] = -1;
+    if (w.out_keys) w.out_keys[orow * w.k + i] = ~0ull;
   }
   if (tid == 0) w.status[orow] = 0;
+}
+
+// Merge of per-shard canonical lists by their EXACT order keys (a sharded index at k > 2048, round 6):
+// keys / ids [nparts][nq][k], every list sorted by (exact key asc = exact score desc, global id asc),
+// pads (~0, -1) last.  An entry's rank in the union = its index in its own list + the entries of every
+// other list before it (one binary search each); the first k ranks are written (out pre-filled with pads
+// by merge_exact_fill_kernel).  Global ids are unique, so the ranks of real entries are distinct.
+constexpr int kMergeExactThreads = 256;
+__global__ __launch_bounds__(kMergeExactThreads) void merge_exact_fill_kernel(int64_t n, float* os, int64_t* oi) {
+  for (int64_t i = (int64_t)blockIdx.x * kMergeExactThreads + threadIdx.x; i < n;
+       i += (int64_t)gridDim.x * kMergeExactThreads) {
+    os[i] = kPadScore;
+    oi[i] = -1;
+  }
+}
+
+__global__ __launch_bounds__(kMergeExactThreads) void merge_exact_kernel(const uint64_t* keys, const int64_t* ids,
+                                                                        int64_t nq, int nparts, int k, float* os,
+                                                                        int64_t* oi) {
+  const int64_t q = blockIdx.y;
+  const int64_t e = (int64_t)blockIdx.x * kMergeExactThreads + threadIdx.x;
+  if (e >= (int64_t)nparts * k) return;
+  const int l = (int)(e / k), i = (int)(e % k);
+  const int64_t base = ((int64_t)l * nq + q) * k;
+  const uint64_t K = keys[base + i];
+  if (K == ~0ull) return;
+  const int64_t I = ids[base + i];
+  int64_t rank = i;
+  for (int l2 = 0; l2 < nparts && rank < k; ++l2) {
+    if (l2 == l) continue;
+    const uint64_t* k2 = keys + ((int64_t)l2 * nq + q) * k;
+    const int64_t* i2 = ids + ((int64_t)l2 * nq + q) * k;
+    int lo = 0, hi = k;   // entries of list l2 before (K, I)
+    while (lo < hi) {
+      const int mid = (lo + hi) >> 1;
+      const uint64_t km = k2[mid];
+      if (km < K || (km == K && i2[mid] < I)) lo = mid + 1;
+      else hi = mid;
+    }
+    rank += lo;
+  }
+  if (rank < k) {
+    os[q * k + rank] = (float)large_key_score(K);
+    oi[q * k + rank] = I;
+  }
 }
 
 // Row statistics for the refine bound (layout above kStatsLen).  One wave per row: lane L holds the
@@ -3965,6 +4025,14 @@ size_t drt_ip_topk_large_workspace(int32_t d, int32_t k) {
 int drt_ip_topk_large(const void* Q, int64_t nq, const void* P, int64_t n, int32_t d, int32_t k, int64_t id_offset,
                       const float* stats, const float* tau, float* out_scores, int64_t* out_ids, int32_t* status,
                       void* ws, size_t ws_bytes, void* stream) {
+  return drt_ip_topk_large_keys(Q, nq, P, n, d, k, id_offset, stats, tau, out_scores, out_ids, nullptr, status, ws,
+                                ws_bytes, stream);
+}
+
+int drt_ip_topk_large_keys(const void* Q, int64_t nq, const void* P, int64_t n, int32_t d, int32_t k,
+                           int64_t id_offset, const float* stats, const float* tau, float* out_scores,
+                           int64_t* out_ids, uint64_t* out_keys, int32_t* status, void* ws, size_t ws_bytes,
+                           void* stream) {
   DRT_REQUIRE(nq >= 0 && n >= 0 && n < (int64_t)0xFFFFFFFFll && drt_ip_topk_large_workspace(d, k) > 0);
   if (nq == 0) return DRT_OK;
   DRT_REQUIRE(Q && (P || n == 0) && stats && tau && out_scores && out_ids && status && ws &&
@@ -4007,6 +4075,7 @@ int drt_ip_topk_large(const void* Q, int64_t nq, const void* P, int64_t n, int32
     w.sel_n = sel_n;
     w.bin_k = bin_k;
     w.bin_r = bin_r;
+    w.out_keys = out_keys;
     hipLaunchKernelGGL(wide_prep_kernel, dim3((unsigned)B), dim3(kRefThreads), 0, s, w);
     DRT_CHECK_HIP(hipGetLastError());
     if (n > 0) {
@@ -4048,6 +4117,22 @@ int drt_ip_topk_resolve_exact(const void* Q, int64_t nq, const void* P, int64_t 
   DRT_REQUIRE(stats != nullptr);
   return resolve_impl(Q, nq, P, n, d, k, id_offset, out_scores, out_ids, status, ws, ws_bytes, n_resolved, stats,
                       (hipStream_t)stream);
+}
+
+int drt_merge_exact(const uint64_t* keys, const int64_t* ids, int64_t nq, int32_t nparts, int32_t k,
+                    float* out_scores, int64_t* out_ids, void* stream) {
+  DRT_REQUIRE(nq >= 0 && nparts >= 1 && nparts <= 1024 && k >= 1 && k <= kLargeMaxK);
+  if (nq == 0) return DRT_OK;
+  DRT_REQUIRE(nq <= 65535 && keys && ids && out_scores && out_ids);
+  hipStream_t s = (hipStream_t)stream;
+  const int64_t n = nq * (int64_t)k;
+  hipLaunchKernelGGL(merge_exact_fill_kernel, dim3((unsigned)std::min<int64_t>((n + 255) / 256, 4096)),
+                     dim3(kMergeExactThreads), 0, s, n, out_scores, out_ids);
+  const int64_t ents = (int64_t)nparts * k;
+  hipLaunchKernelGGL(merge_exact_kernel, dim3((unsigned)((ents + kMergeExactThreads - 1) / kMergeExactThreads),
+                                              (unsigned)nq),
+                     dim3(kMergeExactThreads), 0, s, keys, ids, nq, (int)nparts, (int)k, out_scores, out_ids);
+  return hip_status(hipGetLastError());
 }
 
 int drt_topk_merge(const float* scores, const int64_t* ids, int64_t nq, int32_t nparts, int32_t k_in,

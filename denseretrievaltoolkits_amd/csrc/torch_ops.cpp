@@ -184,8 +184,9 @@ int64_t ip_topk_resolve_wide(const Tensor& q_, const Tensor& p_, int64_t k, int6
 
 // top-k for 2048 < k <= 32768 in the canonical order (drt_ip_topk_large): tau [nq] = a lower bound of each
 // query's k-th fp32 score; asynchronous, status 2 marks a query whose collected set overflowed
-std::tuple<Tensor, Tensor, Tensor> ip_topk_large(const Tensor& q_, const Tensor& p_, int64_t k, int64_t id_offset,
-                                                 const Tensor& stats, const Tensor& tau) {
+static std::tuple<Tensor, Tensor, Tensor, Tensor> ip_topk_large_impl(const Tensor& q_, const Tensor& p_, int64_t k,
+                                                                     int64_t id_offset, const Tensor& stats,
+                                                                     const Tensor& tau, bool want_keys) {
   need(q_, "q", at::kBFloat16, 2);
   need(p_, "p", at::kBFloat16, 2);
   need(tau, "tau", at::kFloat, 1);
@@ -201,13 +202,48 @@ std::tuple<Tensor, Tensor, Tensor> ip_topk_large(const Tensor& q_, const Tensor&
   Tensor scores = at::empty({nq, k}, q.options().dtype(at::kFloat));
   Tensor ids = at::empty({nq, k}, q.options().dtype(at::kLong));
   Tensor status = at::empty({nq}, q.options().dtype(at::kInt));
-  if (nq == 0) return {scores, ids, status};
+  Tensor keys = at::empty({want_keys ? nq : 0, k}, q.options().dtype(at::kLong));
+  if (nq == 0) return {scores, ids, status, keys};
   Tensor ws = workspace(q, wsb);
-  check_rc(drt_ip_topk_large(q.data_ptr(), nq, n ? p.data_ptr() : nullptr, n, (int32_t)d, (int32_t)k, id_offset, sp,
-                             tau.data_ptr<float>(), scores.data_ptr<float>(), ids.data_ptr<int64_t>(),
-                             status.data_ptr<int32_t>(), ws.data_ptr(), wsb, stream_of(q)),
-           "drt_ip_topk_large");
-  return {scores, ids, status};
+  check_rc(drt_ip_topk_large_keys(q.data_ptr(), nq, n ? p.data_ptr() : nullptr, n, (int32_t)d, (int32_t)k, id_offset,
+                                  sp, tau.data_ptr<float>(), scores.data_ptr<float>(), ids.data_ptr<int64_t>(),
+                                  want_keys ? (uint64_t*)keys.data_ptr<int64_t>() : nullptr,
+                                  status.data_ptr<int32_t>(), ws.data_ptr(), wsb, stream_of(q)),
+           "drt_ip_topk_large_keys");
+  return {scores, ids, status, keys};
+}
+
+std::tuple<Tensor, Tensor, Tensor> ip_topk_large(const Tensor& q, const Tensor& p, int64_t k, int64_t id_offset,
+                                                 const Tensor& stats, const Tensor& tau) {
+  auto r = ip_topk_large_impl(q, p, k, id_offset, stats, tau, false);
+  return {std::get<0>(r), std::get<1>(r), std::get<2>(r)};
+}
+
+// the same plus each entry's exact order key (u64 bits in int64; ~0 = pad): the per-shard step of a
+// sharded search at k > 2048
+std::tuple<Tensor, Tensor, Tensor, Tensor> ip_topk_large_keys(const Tensor& q, const Tensor& p, int64_t k,
+                                                              int64_t id_offset, const Tensor& stats,
+                                                              const Tensor& tau) {
+  return ip_topk_large_impl(q, p, k, id_offset, stats, tau, true);
+}
+
+// global top-k of per-shard canonical lists by exact order key (drt_merge_exact): keys / ids [nparts, nq, k]
+std::tuple<Tensor, Tensor> merge_exact(const Tensor& keys_, const Tensor& ids_, int64_t k) {
+  need(keys_, "keys", at::kLong, 3);
+  need(ids_, "ids", at::kLong, 3);
+  TORCH_CHECK_VALUE(keys_.sizes() == ids_.sizes() && keys_.device() == ids_.device(),
+                    "merge_exact: keys and ids differ in shape or device");
+  TORCH_CHECK_VALUE(keys_.size(2) == k, "merge_exact: lists of ", keys_.size(2), " entries, k = ", k);
+  const c10::DeviceGuard g(keys_.device());
+  const Tensor keys = keys_.contiguous(), ids = ids_.contiguous();
+  const int64_t nq = keys.size(1);
+  Tensor s = at::empty({nq, k}, keys.options().dtype(at::kFloat));
+  Tensor i = at::empty({nq, k}, keys.options().dtype(at::kLong));
+  check_rc(drt_merge_exact((const uint64_t*)keys.data_ptr<int64_t>(), ids.data_ptr<int64_t>(), nq,
+                           (int32_t)keys.size(0), (int32_t)k, s.data_ptr<float>(), i.data_ptr<int64_t>(),
+                           stream_of(keys)),
+           "drt_merge_exact");
+  return {s, i};
 }
 
 // row statistics of p (+ those of earlier rows in `prev`, appended rows)
@@ -615,6 +651,9 @@ TORCH_LIBRARY(drt, m) {
   m.def("ip_topk_resolve_wide(Tensor q, Tensor p, int k, int id_offset, Tensor(a!) scores, Tensor(b!) ids, "
         "Tensor(c!) status, Tensor stats) -> int");
   m.def("ip_topk_large(Tensor q, Tensor p, int k, int id_offset, Tensor stats, Tensor tau) -> (Tensor, Tensor, Tensor)");
+  m.def("ip_topk_large_keys(Tensor q, Tensor p, int k, int id_offset, Tensor stats, Tensor tau) -> "
+        "(Tensor, Tensor, Tensor, Tensor)");
+  m.def("merge_exact(Tensor keys, Tensor ids, int k) -> (Tensor, Tensor)");
   m.def("row_stats(Tensor p, Tensor? prev=None) -> Tensor");
   m.def("refine_delta(Tensor q, Tensor p, int row_offset, Tensor cand_scores, Tensor cand_ids, int k, Tensor stats, "
         "Tensor? tau, Tensor(a!) status, bool local=False) -> (Tensor, Tensor)");
@@ -649,6 +688,8 @@ TORCH_LIBRARY_IMPL(drt, CUDA, m) {   // the GPU dispatch key of torch-ROCm
   m.impl("ip_topk_resolve", &ip_topk_resolve);
   m.impl("ip_topk_resolve_wide", &ip_topk_resolve_wide);
   m.impl("ip_topk_large", &ip_topk_large);
+  m.impl("ip_topk_large_keys", &ip_topk_large_keys);
+  m.impl("merge_exact", &merge_exact);
   m.impl("row_stats", &row_stats);
   m.impl("refine_delta", &refine_delta);
   m.impl("refine_sort", &refine_sort);

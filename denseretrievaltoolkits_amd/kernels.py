@@ -82,7 +82,7 @@ def large_k_ranges(n: int, k: int):
     return m, [(n * j // c, n * (j + 1) // c) for j in range(c)]
 
 
-def _ip_topk_large(q, p, k, id_offset, out, status, stats):
+def _ip_topk_large(q, p, k, id_offset, out, status, stats, want_keys: bool = False):
     """k > MAX_K (faiss IndexFlatIP answers any k; DRT/arguments.py:195 retrieve_num is a free flag):
     a threshold no larger than each query's k-th fp32 score -- the minimum of the m-th scores of C
     disjoint row ranges, C = ceil(k / MAX_K), m = ceil(k / C), so at least C * m >= k rows reach it (every
@@ -103,17 +103,22 @@ def _ip_topk_large(q, p, k, id_offset, out, status, stats):
         for a, b in ranges[1]:
             s, _, _ = ip_topk(q, p[a:b], m)   # certified fp32 scan scores
             tau = s[:, m - 1].clone() if tau is None else torch.minimum(tau, s[:, m - 1])
-    scores, ids, st = drt.ip_topk_large(q, p, k, id_offset, stats, tau.contiguous())
+    if want_keys:
+        scores, ids, st, keys = drt.ip_topk_large_keys(q, p, k, id_offset, stats, tau.contiguous())
+    else:
+        (scores, ids, st), keys = drt.ip_topk_large(q, p, k, id_offset, stats, tau.contiguous()), None
     bad = torch.nonzero(st != 0).flatten()
     if bad.numel():
         # the range plan's threshold was too low for these queries (a corpus ordered or clustered by
         # position: one range of weak rows drags the minimum far below the k-th score and more than
         # _WIDE_CAP rows pass it).  Retry them at a threshold next to their own k-th score (_kth_bound)
         qb = q.index_select(0, bad).contiguous()
-        s2, i2, st2 = drt.ip_topk_large(qb, p, k, id_offset, stats, _kth_bound(qb, p, k, stats))
+        s2, i2, st2, k2 = drt.ip_topk_large_keys(qb, p, k, id_offset, stats, _kth_bound(qb, p, k, stats))
         scores.index_copy_(0, bad, s2)
         ids.index_copy_(0, bad, i2)
         st.index_copy_(0, bad, st2)
+        if keys is not None:
+            keys.index_copy_(0, bad, k2)
         nbad = int((st2 != 0).sum().item())
         if nbad:
             raise RuntimeError(f"ip_topk k={k}: {nbad} queries have more than {_WIDE_CAP} rows within the fp32 "
@@ -125,7 +130,35 @@ def _ip_topk_large(q, p, k, id_offset, out, status, stats):
     if status is not None:
         status.copy_(st)
         st = status
+    if want_keys:
+        return scores, ids, st, keys
     return scores, ids, st
+
+
+def ip_topk_exact_keys(q: torch.Tensor, p: torch.Tensor, k: int, id_offset: int = 0,
+                       stats: Optional[torch.Tensor] = None) -> Tuple[torch.Tensor, torch.Tensor]:
+    """The canonical top-k of shard ``p`` as (exact order keys, ids), both int64 [nq, k] (keys: u64 bits of
+    desc_key64(exact sum), ascending = exact score desc; ~0 / -1 for missing rows) -- the per-shard step of
+    a sharded search at k > 2048, merged across shards by ``merge_exact``.  Any 1 <= k <= 32768 (the
+    large-k path's machinery; synchronous)."""
+    drt = ops.load()
+    _require_device(q, p)
+    if k > MAX_K_LARGE or k < 1:
+        raise ValueError(f"unsupported k={k} (1 <= k <= {MAX_K_LARGE})")
+    if q.shape[0] == 0:
+        z = torch.empty((0, k), dtype=torch.int64, device=q.device)
+        return z, z.clone()
+    _, ids, _, keys = _ip_topk_large(q, p, k, id_offset, None, None, stats, want_keys=True)
+    return keys, ids
+
+
+def merge_exact(keys: torch.Tensor, ids: torch.Tensor, k: int) -> Tuple[torch.Tensor, torch.Tensor]:
+    """Global top-k of per-shard canonical lists [nparts, nq, k] (``ip_topk_exact_keys``, ids global) by
+    (exact score desc, id asc): (scores fp32 = exact sums rounded, ids int64) [nq, k]."""
+    _require_device(keys, ids)
+    if keys.dim() != 3 or keys.shape != ids.shape:
+        raise ValueError("merge_exact expects [nparts, nq, k] keys and ids")
+    return ops.load().merge_exact(keys, ids, k)
 
 
 _KTH_ROWS = 1 << 20   # rows per dense block of _kth_bound

@@ -10,6 +10,7 @@ formula of the fused score + cross-entropy op.
     torch.ops.drt.ip_topk_resolve(q, p, k, off, s, i, st, stats) -> n_resolved  (in place, synchronous)
     torch.ops.drt.row_stats / refine_delta / refine_sort  (canonical exact-score order, include/drt.h)
     torch.ops.drt.topk_merge(scores, ids, k_out)        -> (scores, ids)           utils.py:215-229
+    torch.ops.drt.ip_topk_large(_keys) / merge_exact    (k > 2048; sharded: merged by exact order keys)
     torch.ops.drt.dist_sample / dist_tau / dist_filter / dist_filter_chunks_into / dist_filter_lists / merge_packed
                                                                                             (sharded, §8e)
     torch.ops.drt.score_ce_fwd(q, p, stride, scale)     -> (loss, scores, lse)     biencoder.py:107-119
@@ -76,6 +77,17 @@ def _register_python_parts():
         nq = q.shape[0]
         return (q.new_empty((nq, k), dtype=torch.float32), q.new_empty((nq, k), dtype=torch.int64),
                 q.new_empty((nq,), dtype=torch.int32))
+
+    @lib.register_fake("drt::ip_topk_large_keys")
+    def _(q, p, k, id_offset, stats, tau):
+        nq = q.shape[0]
+        return (q.new_empty((nq, k), dtype=torch.float32), q.new_empty((nq, k), dtype=torch.int64),
+                q.new_empty((nq,), dtype=torch.int32), q.new_empty((nq, k), dtype=torch.int64))
+
+    @lib.register_fake("drt::merge_exact")
+    def _(keys, ids, k):
+        nq = keys.shape[1]
+        return keys.new_empty((nq, k), dtype=torch.float32), ids.new_empty((nq, k))
 
     @lib.register_fake("drt::row_stats")
     def _(p, prev=None):

@@ -132,6 +132,19 @@ size_t drt_ip_topk_large_workspace(int32_t d, int32_t k);
 int drt_ip_topk_large(const void* Q, int64_t nq, const void* P, int64_t n, int32_t d, int32_t k, int64_t id_offset,
                       const float* stats, const float* tau, float* out_scores, int64_t* out_ids, int32_t* status,
                       void* workspace, size_t workspace_bytes, void* stream);
+/* The same, also writing each output entry's EXACT order key (u64 [nq, k]: ascending = exact score desc;
+ * ~0 for pads) -- the per-shard step of a sharded search at k > 2048 (round 6), merged across shards by
+ * drt_merge_exact after an all-gather of (keys, global ids).                                            */
+int drt_ip_topk_large_keys(const void* Q, int64_t nq, const void* P, int64_t n, int32_t d, int32_t k,
+                           int64_t id_offset, const float* stats, const float* tau, float* out_scores,
+                           int64_t* out_ids, uint64_t* out_keys, int32_t* status, void* workspace,
+                           size_t workspace_bytes, void* stream);
+/* drt_merge_exact: the global top-k of nparts per-shard canonical lists ([nparts][nq][k] exact order keys
+ *   + global ids, each sorted by (key, id), pads (~0, -1) last) by (exact key, id) -- the reference's
+ *   partition merge (merge_retrieval_results_by_score, DRT/model/utils.py:215-229) on exact scores;
+ *   out_scores = the exact sums rounded to fp32, missing entries (-FLT_MAX, -1).  Asynchronous.          */
+int drt_merge_exact(const uint64_t* keys, const int64_t* ids, int64_t nq, int32_t nparts, int32_t k,
+                    float* out_scores, int64_t* out_ids, void* stream);
 int drt_refine_delta_bf16(const void* Q, int64_t nq, int32_t d, const void* P, int64_t n_local,
                           int64_t row_offset, const float* cand_s, const int64_t* cand_i, int32_t kc,
                           int32_t k, const float* stats, const float* tau, float* delta, int32_t* cnt,

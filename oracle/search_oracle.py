@@ -271,3 +271,44 @@ def merge_packed(parts, k, n_global):
     over = (parts[:, :, k] & np.uint64(1)).any(axis=0)
     status = (over | (pad[:, k - 1] & (n_global >= k))).astype(np.int32)
     return s.astype(np.float32), ids, status
+
+
+# ---------------------------------------------------------------------------
+# Sharded search at k > 2048 (csrc/search.hip drt_ip_topk_large_keys + drt_merge_exact, round 6): every
+# shard's canonical top-k carries each entry's EXACT order key; the lists are merged by (key, global id).
+# Like the protocol above this only restates the exchanged data; the tests check the end result against
+# the single-index ip_topk.
+# ---------------------------------------------------------------------------
+def desc_key64(scores: np.ndarray) -> np.ndarray:
+    """uint64 whose ascending order is descending fp64 score (search.hip desc_key64)."""
+    s = np.asarray(scores, dtype=np.float64) + 0.0
+    u = s.view(np.uint64)
+    neg = (u >> np.uint64(63)) != 0
+    ordk = np.where(neg, ~u, u | np.uint64(0x8000000000000000))
+    return ~ordk
+
+
+def exact_keys_topk(q, p_local, k, id_offset=0):
+    """(keys uint64 [nq, k], ids int64 [nq, k]) of a shard's canonical top-k; (~0, -1) pads."""
+    s, i = ip_topk(q, p_local, k, id_offset=id_offset, dtype=np.float64, out_dtype=np.float64)
+    keys = desc_key64(s)
+    keys[i < 0] = PAD_KEY64
+    return keys, i
+
+
+def merge_exact(keys, ids, k):
+    """Top-k of [nparts, nq, k] (key, id) lists by (key asc, id asc) -> (scores fp32, ids)."""
+    nparts, nq, _ = keys.shape
+    out_s = np.full((nq, k), PAD_SCORE, dtype=np.float32)
+    out_i = np.full((nq, k), PAD_ID, dtype=np.int64)
+    for r in range(nq):
+        kk = keys[:, r, :].reshape(-1)
+        ii = ids[:, r, :].reshape(-1)
+        real = kk != PAD_KEY64
+        kk, ii = kk[real], ii[real]
+        o = np.lexsort((ii, kk))[:k]
+        ordk = ~kk[o]
+        u = np.where((ordk >> np.uint64(63)) != 0, ordk & np.uint64(0x7FFFFFFFFFFFFFFF), ~ordk)
+        out_s[r, :len(o)] = u.view(np.float64).astype(np.float32)
+        out_i[r, :len(o)] = ii[o]
+    return out_s, out_i

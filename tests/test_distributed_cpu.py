@@ -33,6 +33,10 @@ class _OracleShard:
         s, i = orc.ip_topk(np.asarray(q, np.float32), self.rows, k, id_offset=id_offset)
         return torch.from_numpy(s), torch.from_numpy(i)
 
+    def search_exact_keys(self, q, k, id_offset=0):   # k > 2048: exact order keys (uint64 as int64)
+        keys, ids = orc.exact_keys_topk(np.asarray(q, np.float32), self.rows, k, id_offset=id_offset)
+        return torch.from_numpy(keys.view(np.int64)), torch.from_numpy(ids)
+
     # global-threshold protocol steps (uint32 / uint64 keys travel as int32 / int64 tensors)
     def dist_sample(self, q, n_global, k):
         return torch.from_numpy(orc.dist_sample(np.asarray(q, np.float32), self.rows, n_global, k).view(np.int32))
@@ -48,6 +52,11 @@ class _OracleShard:
 def _oracle_merge_packed(parts, k, n_global):
     s, i, st = orc.merge_packed(parts.numpy().view(np.uint64), k, n_global)
     return torch.from_numpy(s), torch.from_numpy(i), torch.from_numpy(st)
+
+
+def _oracle_merge_exact(keys, ids, k):
+    s, i = orc.merge_exact(keys.numpy().view(np.uint64), ids.numpy(), k)
+    return torch.from_numpy(s), torch.from_numpy(i)
 
 
 def _oracle_merge(s_all, i_all, k):
@@ -71,7 +80,7 @@ def _worker(rank, world, port, n, d, k, nq, out_q, protocol="global_tau", vals=3
     q = rng.integers(-vals, vals + 1, size=(nq, d)).astype(np.float32)
     lo, hi = orc.shard_bounds(n, world, rank)
     idx = ShardedFlatIP(d, local=_OracleShard(d), merge=_oracle_merge, merge_packed=_oracle_merge_packed,
-                        protocol=protocol)
+                        protocol=protocol, merge_exact=_oracle_merge_exact)
     idx.add_shard(p[lo:hi])
     assert idx.offset == lo and idx.ntotal == n
     s, i = idx.search_device(q, k)
@@ -108,6 +117,14 @@ def test_global_tau_sampled_corpus():
     """n_global > cap: the shards sample, agree on one tau, filter, certify; no fallback expected."""
     res = _run(2, 40000, k=20, nq=4, vals=8)
     assert all(r[2] == 0 for r in res), res
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_sharded_search_k_beyond_2048(world):
+    """k > 2048 across shards (round 6; the reference's retrieve_num is a free flag, faiss answers any k):
+    every shard's canonical top-k with exact order keys, all-gathered and merged by (exact key, id) ==
+    the single index's top-k, ties by id (integer rows: heavy ties at the k-th score)."""
+    _run(world, 9000, k=4096, nq=3, vals=2)
 
 
 def test_global_tau_uneven_and_empty_shards():

@@ -39,6 +39,7 @@ def _assert_scores(gs, es):
     (130, 90000, 256, 2049, True),     # k just past the list kernels, 2 query chunks of 128
     (3, 30000, 128, 4096, False),      # n <= 65536: every row collected
     (4, 150000, 64, 32768, False),     # k at its maximum (16 row ranges of 2048)
+    (3, 60000, 128, 32768, True),      # k > n / 2: the selected scores cross zero (rank bins on the score)
 ])
 def test_large_k_gaussian_bit_exact(dev, nq, n, d, k, stats):
     rng = np.random.default_rng(nq + n + d + k)
@@ -141,3 +142,43 @@ def test_large_k_corpus_ordered_by_relevance(dev):
     assert (ei < n // 3).all()          # the setting: the whole top-k comes from the first range
     np.testing.assert_array_equal(gi, ei)
     _assert_scores(gs, es)
+
+
+def test_exact_keys_and_merge_exact_vs_oracle(dev):
+    """The sharded k > 2048 pieces (round 6): kernels.ip_topk_exact_keys returns each shard's canonical
+    top-k with its exact order keys (integer rows: the fp64 sums are exact, so the keys equal the
+    oracle's bit for bit), and kernels.merge_exact merges [nparts, nq, k] lists by (key, global id) into
+    the single index's top-k."""
+    import torch
+    from denseretrievaltoolkits_amd import kernels
+    rng = np.random.default_rng(9)
+    q = int_bf16(rng, (4, 64), -3, 3)
+    p = int_bf16(rng, (50000, 64), -3, 3)
+    k, bounds = 2500, [(0, 16000), (16000, 16000), (16000, 50000)]   # an empty shard too
+    qt = to_dev_bf16(q, dev)
+    keys, ids = [], []
+    for a, b in bounds:
+        kk, ii = kernels.ip_topk_exact_keys(qt, to_dev_bf16(p[a:b], dev), k, id_offset=a)
+        ek, ei = orc.exact_keys_topk(q, p[a:b], k, id_offset=a)
+        np.testing.assert_array_equal(ii.cpu().numpy(), ei)
+        np.testing.assert_array_equal(kk.cpu().numpy().view(np.uint64), ek)
+        keys.append(kk)
+        ids.append(ii)
+    s, i = kernels.merge_exact(torch.stack(keys), torch.stack(ids), k)
+    es, ei = orc.ip_topk(q, p, k)
+    np.testing.assert_array_equal(i.cpu().numpy(), ei)
+    np.testing.assert_array_equal(s.cpu().numpy(), es)
+    # random sorted lists with ragged fills (pads last), ties across parts broken by id
+    nparts, nq = 5, 3
+    kr = orc.desc_key64(rng.integers(-3000, 3000, size=(nparts, nq, k)).astype(np.float64) / 8.0)
+    ir = rng.permutation(nparts * nq * k).reshape(nparts, nq, k).astype(np.int64)
+    for l in range(nparts):
+        for r in range(nq):
+            o = np.lexsort((ir[l, r], kr[l, r]))
+            kr[l, r], ir[l, r] = kr[l, r][o], ir[l, r][o]
+            c = int(rng.integers(0, k + 1))
+            kr[l, r, c:], ir[l, r, c:] = orc.PAD_KEY64, -1
+    s, i = kernels.merge_exact(torch.from_numpy(kr.view(np.int64)).to(dev), torch.from_numpy(ir).to(dev), k)
+    es, ei = orc.merge_exact(kr, ir, k)
+    np.testing.assert_array_equal(i.cpu().numpy(), ei)
+    np.testing.assert_array_equal(s.cpu().numpy(), es)

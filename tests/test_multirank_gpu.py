@@ -181,6 +181,40 @@ def test_sharded_search_multiprocess_gaussian_exact_order():
     assert all(v["global_tau"] == 0 and v["global_tau_batched"] == 0 for v in res.values()), res
 
 
+def _w_sharded_large_k(rank, world, dev, data):
+    """k > 2048 across ranks (round 6): each shard's canonical top-k with exact order keys, all-gathered
+    and merged by exact key on the HIP kernels -- ids == the fp64 single-index order."""
+    import torch
+    from helpers import gauss_bf16, int_bf16, to_dev_bf16
+    from oracle import search_oracle as orc
+    from denseretrievaltoolkits_amd.search import ShardedFlatIP
+    rng = np.random.default_rng(47)
+    if data == "gauss":
+        q = gauss_bf16(rng, (6, 768))
+        p = gauss_bf16(rng, (150001, 768))   # shards of 75k rows > 65,536: the range-plan threshold
+    else:
+        q = int_bf16(rng, (5, 128), -2, 2)
+        p = int_bf16(rng, (40000, 128), -2, 2)   # heavy exact ties, broken by global id
+    k = 4096
+    es, ei = orc.ip_topk(q, p, k)
+    lo, hi = orc.shard_bounds(p.shape[0], world, rank)
+    idx = ShardedFlatIP(p.shape[1], device=dev)
+    idx.add_shard(to_dev_bf16(p[lo:hi], dev))
+    s, i = idx.search_device(to_dev_bf16(q, dev), k)
+    torch.cuda.synchronize()
+    np.testing.assert_array_equal(i.cpu().numpy(), ei)
+    ulp = np.spacing(np.abs(es).astype(np.float32))
+    assert (np.abs(s.cpu().numpy().astype(np.float64) - es) <= ulp).all()
+    res = idx.search_batches([to_dev_bf16(q[:3], dev), to_dev_bf16(q[3:], dev)], k)
+    np.testing.assert_array_equal(torch.cat([r[1] for r in res]).cpu().numpy(), ei)
+    return True
+
+
+@pytest.mark.parametrize("data", ["gauss", "int"])
+def test_sharded_search_multiprocess_k_beyond_2048(data):
+    _spawn(_w_sharded_large_k, 2, data)
+
+
 def test_sharded_search_multiprocess_fallback():
     res = _spawn(_w_sharded, 2, "ties")
     # one batch of 9 queries; batched: batches of 5 + 4 in one group, both redone exactly

@@ -18,6 +18,9 @@ def main():
     ap.add_argument("--queries", type=int, default=2048)
     ap.add_argument("--k", type=int, default=1000)
     ap.add_argument("--reps", type=int, default=5)
+    ap.add_argument("--hits", type=int, default=512,
+                    help="hits per query the threshold admits in this chunk (512 = the product's ~4096 per query "
+                         "over a 10M corpus; 0 = none)")
     a = ap.parse_args()
     import torch
     from bench import gen_shard
@@ -27,8 +30,11 @@ def main():
     g = torch.Generator(device=dev).manual_seed(5678)
     q = torch.randn((a.queries, 768), generator=g, device=dev).to(torch.bfloat16)
     n_global = a.rows * 8   # a chunk of a 10M corpus: ~1/8 of a query's ~4096 hits land in it
-    tau = torch.cat([(q[b:b + 256].float() @ p.float().T).topk(512, dim=1).values[:, -1]
-                     for b in range(0, a.queries, 256)]).contiguous()
+    if a.hits > 0:
+        tau = torch.cat([(q[b:b + 256].float() @ p.float().T).topk(a.hits, dim=1).values[:, -1]
+                         for b in range(0, a.queries, 256)]).contiguous()
+    else:
+        tau = torch.full((a.queries,), float("inf"), device=dev)
     kc = kernels.refine_width(a.k)
     packed = torch.empty((a.queries, kc + 1), dtype=torch.int64, device=dev)
     kernels.dist_filter_into(q, p, n_global, kc, 0, tau, packed)
