@@ -444,7 +444,8 @@ def search_record(args, world, grouped, group_queries, kc, elapsed_s, launch_ms_
         "scaling": "strong",
         "vs_baseline": None,
         "dtype": "bf16",
-        "data": "synthetic: N(0,1) corpus and queries rounded to bf16, generated in HBM (seeded)",
+        "data": "synthetic: N(0,1) corpus and queries rounded to bf16, generated in HBM (seeded per global "
+                "1M-row block: the same corpus at every GPU count)",
         "config": {
             "workload": f"exact IP top-{k}, {args.n_corpus} x {d} bf16 corpus row-sharded over {world} GPU(s), "
                         f"loader batch {qb} queries" + (f", searched in groups of {group_queries}" if grouped else

@@ -52,6 +52,8 @@ _SIGNATURES = [
                                                  c_i32, c_i64, c_vp, c_vp, c_vp, c_sz, c_vp]),
     ("drt_topk_merge_packed", c_i32, [c_vp, c_i64, c_i32, c_i32, c_i64, c_vp, c_vp, c_vp, c_vp]),
     ("drt_topk_merge_packed_cert", c_i32, [c_vp, c_i64, c_i32, c_i32, c_i32, c_i64, c_vp, c_vp, c_vp, c_vp]),
+    ("drt_topk_merge_packed_capped", c_i32, [c_vp, c_i64, c_i32, c_i32, c_i32, c_i32, c_i64, c_vp, c_vp, c_vp,
+                                             c_vp]),
     ("drt_row_stats_bf16", c_i32, [c_vp, c_i64, c_i32, c_vp, c_i32, c_vp]),
     ("drt_refine_width", c_i32, [c_i32]),
     ("drt_ip_topk_exact_bf16", c_i32, [c_vp, c_i64, c_vp, c_i64, c_i32, c_i32, c_i64, c_vp, c_vp, c_vp, c_vp, c_vp,

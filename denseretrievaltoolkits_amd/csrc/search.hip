@@ -1486,7 +1486,10 @@ __global__ __launch_bounds__(kSelThreads) void select_kernel(SelectArgs a) {
     }
     if (tid == 0) {
       const uint64_t nval = (uint64_t)(kk_total < a.k ? kk_total : a.k);
-      op[a.k] = (nval << 32) | ((INPUT == SEL_KEYS64 && c_raw > a.cap) ? 1ull : 0ull);
+      // bit 0: overflow (more hits than the list buffer held); bit 1: truncated (more hits than the k
+      // entries written -- what a merge of capped exchange lists certifies against, round 6)
+      op[a.k] = (nval << 32) | ((INPUT == SEL_KEYS64 && c_raw > a.cap) ? 1ull : 0ull) |
+                (c_raw > (int64_t)a.k ? 2ull : 0ull);
     }
     return;
   }
@@ -2037,24 +2040,31 @@ __device__ __forceinline__ int packed_valid_count(const uint64_t* L, int k) {
 constexpr int kCntThreads = 1024;
 constexpr int kCntMaxParts = 8;
 constexpr int kCntMaxKeys = 16384;   // 128 KiB of LDS
+// lcap: entries per list (list stride lcap + 1); k: merged outputs.  lcap < k (capped exchange lists,
+// round 6): a list that was truncated (flag bit 1: its shard had more hits than it carries) certifies only
+// if its last entry ranks at or below the k-th merged place -- every entry it did not carry is worse.
 __global__ __launch_bounds__(kCntThreads) void merge_packed_count_kernel(const uint64_t* parts, int64_t nq,
                                                                          int nparts, int k, int64_t n_global,
                                                                          float* out_s, int64_t* out_i,
-                                                                         int32_t* status, int kcert) {
+                                                                         int32_t* status, int kcert, int lcap) {
   extern __shared__ __attribute__((aligned(16))) uint64_t P[];   // valid prefixes of all parts, concatenated
-  __shared__ int cnt[kCntMaxParts], off[kCntMaxParts + 1], flg[kCntMaxParts];
+  __shared__ int cnt[kCntMaxParts], off[kCntMaxParts + 1], flg[kCntMaxParts], trn[kCntMaxParts];
+  __shared__ int trunc_bad;
   const int tid = threadIdx.x;
   const int64_t q = blockIdx.x;
-  const int64_t ps = (int64_t)(k + 1);
+  const int64_t ps = (int64_t)(lcap + 1);
+  if (tid == 0) trunc_bad = 0;
   if (tid < kCntMaxParts) {
-    int c = 0, f = 0;
+    int c = 0, f = 0, t = 0;
     if (tid < nparts) {
       const uint64_t* L = parts + ((int64_t)tid * nq + q) * ps;
-      c = packed_valid_count(L, k);
-      f = (int)(L[k] & 1ull);
+      c = packed_valid_count(L, lcap);
+      f = (int)(L[lcap] & 1ull);
+      t = lcap < k && (L[lcap] & 2ull) != 0 && c == lcap;
     }
     cnt[tid] = c;
     flg[tid] = f;
+    trn[tid] = t;
   }
   __syncthreads();
   if (tid == 0) {
@@ -2119,6 +2129,9 @@ __global__ __launch_bounds__(kCntThreads) void merge_packed_count_kernel(const u
 #pragma unroll
     for (int l = 0; l < kCntMaxParts; ++l)
       rank += (base[l] - offs[l]) + ((len[l] == 1 && P[base[l]] < x) ? 1 : 0);
+    // a truncated list's last carried entry above the k-th merged place: entries it did not carry may
+    // belong to the top k -- not certified (the batch is redone exactly)
+    if (trn[me] && e == offs[me + 1] - 1 && rank < k - 1) trunc_bad = 1;
     if (rank < k) {
       out_s[q * k + rank] = desc_key_to_score((uint32_t)(x >> 32));
       out_i[q * k + rank] = (int64_t)(x & 0xFFFFFFFFull);
@@ -2128,8 +2141,9 @@ __global__ __launch_bounds__(kCntThreads) void merge_packed_count_kernel(const u
     out_s[q * k + i] = kPadScore;
     out_i[q * k + i] = -1;
   }
+  __syncthreads();
   if (status && tid == 0) {
-    int bad = 0;
+    int bad = trunc_bad;
     for (int l = 0; l < kCntMaxParts; ++l) bad |= flg[l];
     status[q] = (bad || (tot < kcert && n_global >= (int64_t)kcert)) ? 1 : 0;
   }
@@ -4419,6 +4433,30 @@ int drt_topk_merge_packed(const uint64_t* parts, int64_t nq, int32_t nparts, int
   return drt_topk_merge_packed_cert(parts, nq, nparts, k, k, n_global, out_scores, out_ids, status, stream);
 }
 
+// Capped exchange lists (round 6): parts [nparts][nq][lcap + 1] with lcap <= k entries each (a shard's top
+// lcap hits, flag bit 1 = it had more), merged into the top k; a truncated list whose last carried entry
+// ranks above the k-th merged place leaves its query uncertified.  The count merge only (2..8 parts).
+int drt_topk_merge_packed_capped(const uint64_t* parts, int64_t nq, int32_t nparts, int32_t lcap, int32_t k,
+                                 int32_t k_cert, int64_t n_global, float* out_scores, int64_t* out_ids,
+                                 int32_t* status, void* stream) {
+  DRT_REQUIRE(nq >= 0 && nparts >= 2 && nparts <= kCntMaxParts && k >= 1 && k <= kSelMaxK && lcap >= 1 &&
+              lcap <= k && (int64_t)nparts * lcap <= kCntMaxKeys && n_global >= 0 && k_cert >= 1 && k_cert <= k);
+  if (nq == 0) return DRT_OK;
+  DRT_REQUIRE(parts && out_scores && out_ids);
+  hipStream_t s = (hipStream_t)stream;
+  static bool attr_set = false;
+  if (!attr_set) {
+    DRT_CHECK_HIP(hipFuncSetAttribute((const void*)merge_packed_count_kernel,
+                                      hipFuncAttributeMaxDynamicSharedMemorySize, kCntMaxKeys * 8));
+    attr_set = true;
+  }
+  const ProfPair pp = prof_begin(PROF_MERGE, s);
+  hipLaunchKernelGGL(merge_packed_count_kernel, dim3((unsigned)nq), dim3(kCntThreads), (size_t)nparts * lcap * 8, s,
+                     parts, nq, (int)nparts, (int)k, n_global, out_scores, out_ids, status, (int)k_cert, (int)lcap);
+  prof_end(pp, s);
+  return hip_status(hipGetLastError());
+}
+
 int drt_topk_merge_packed_cert(const uint64_t* parts, int64_t nq, int32_t nparts, int32_t k, int32_t k_cert,
                                int64_t n_global, float* out_scores, int64_t* out_ids, int32_t* status,
                                void* stream) {
@@ -4445,7 +4483,7 @@ int drt_topk_merge_packed_cert(const uint64_t* parts, int64_t nq, int32_t nparts
       attr_set = true;
     }
     hipLaunchKernelGGL(merge_packed_count_kernel, dim3((unsigned)nq), dim3(kCntThreads), cnt_lds, s, parts, nq,
-                       (int)nparts, (int)k, n_global, out_scores, out_ids, status, (int)k_cert);
+                       (int)nparts, (int)k, n_global, out_scores, out_ids, status, (int)k_cert, (int)k);
   } else if (nparts > 1 && (p2 / 2) * kp <= kTreeMaxE * kTreeThreads && lds <= 128 * 1024) {
 #define DRT_TREE(KPV)                                                                                        \
   {                                                                                                          \

@@ -480,13 +480,22 @@ void dist_filter_lists_into(const Tensor& q_, const Tensor& p_, int64_t n_global
 
 std::tuple<Tensor, Tensor, Tensor> merge_packed(const Tensor& parts_, int64_t k, int64_t n_global, int64_t k_cert) {
   need(parts_, "parts", at::kLong, 3);
-  TORCH_CHECK_VALUE(parts_.size(2) == k + 1, "merge_packed expects [nparts, nq, k + 1]");
+  TORCH_CHECK_VALUE(parts_.size(2) >= 2 && parts_.size(2) <= k + 1,
+                    "merge_packed expects [nparts, nq, lcap + 1] lists with lcap <= k");
   const c10::DeviceGuard g(parts_.device());
   const Tensor parts = parts_.contiguous();
-  const int64_t nq = parts.size(1);
+  const int64_t nq = parts.size(1), lcap = parts.size(2) - 1;
   Tensor s = at::empty({nq, k}, parts.options().dtype(at::kFloat));
   Tensor i = at::empty({nq, k}, parts.options().dtype(at::kLong));
   Tensor st = at::empty({nq}, parts.options().dtype(at::kInt));
+  if (lcap < k) {   // capped exchange lists (drt_topk_merge_packed_capped)
+    check_rc(drt_topk_merge_packed_capped((const uint64_t*)parts.data_ptr<int64_t>(), nq, (int32_t)parts.size(0),
+                                          (int32_t)lcap, (int32_t)k, (int32_t)(k_cert > 0 ? k_cert : k), n_global,
+                                          s.data_ptr<float>(), i.data_ptr<int64_t>(), st.data_ptr<int32_t>(),
+                                          stream_of(parts)),
+             "drt_topk_merge_packed_capped");
+    return {s, i, st};
+  }
   check_rc(drt_topk_merge_packed_cert((const uint64_t*)parts.data_ptr<int64_t>(), nq, (int32_t)parts.size(0),
                                       (int32_t)k, (int32_t)(k_cert > 0 ? k_cert : k), n_global, s.data_ptr<float>(),
                                       i.data_ptr<int64_t>(), st.data_ptr<int32_t>(), stream_of(parts)),

@@ -315,12 +315,27 @@ def dist_filter_lists_into(q: torch.Tensor, p: torch.Tensor, n_global: int, k: i
 
 
 def merge_packed(parts: torch.Tensor, k: int, n_global: int, k_cert: int = -1):
-    """[nparts, nq, k + 1] packed lists -> (scores [nq,k], ids [nq,k], status [nq] int32; 0 = exact);
-    certified at ``k_cert`` <= k entries when given (the canonical-order stage merges wider lists)."""
+    """[nparts, nq, lcap + 1] packed lists -> (scores [nq,k], ids [nq,k], status [nq] int32; 0 = exact);
+    certified at ``k_cert`` <= k entries when given (the canonical-order stage merges wider lists).  Lists
+    of lcap < k entries are capped exchange lists (exchange_cap): 2-8 parts, a truncated list certified
+    only if its last entry ranks at or below the k-th merged place."""
     _require_device(parts)
-    if parts.dim() != 3 or parts.shape[2] != k + 1:
-        raise ValueError("merge_packed expects [nparts, nq, k + 1]")
+    if parts.dim() != 3 or not 2 <= parts.shape[2] <= k + 1:
+        raise ValueError("merge_packed expects [nparts, nq, lcap + 1] with lcap <= k")
     return ops.load().merge_packed(parts, k, n_global, k_cert)
+
+
+def exchange_cap(kc: int, nparts: int) -> int:
+    """Entries per shard list a W-way exchange carries (round 6): a shard holds ~kc / W of the
+    merged top-kc (Binomial(kc, 1 / W) for rows not ordered by relevance), so it sends its best
+    ceil(1.6 kc / W) + 64 packed keys (13 sigma above the mean at W = 8: 320 of 1256) instead of kc; a
+    query whose truncated list reaches into the merged top-kc is redone exactly (merge_packed's
+    certificate).  kc itself for one part, beyond the count merge's 8 parts, or when the cap saves little."""
+    if nparts <= 1 or nparts > 8:
+        return kc
+    cap = -(-16 * kc // (10 * nparts)) + 64
+    cap = -(-cap // 64) * 64
+    return kc if cap * 10 >= kc * 9 else cap
 
 
 def gemm_nt_f32(a: torch.Tensor, b: torch.Tensor, out: Optional[torch.Tensor] = None) -> torch.Tensor:

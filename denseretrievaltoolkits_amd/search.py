@@ -174,7 +174,7 @@ def _reserve_group_memory(local, k: int, n_global: int, chunks=None):
 
 
 def _gtau_enqueue_group(local, qs, k: int, n_global: int, offset: int, gather, to_host: bool = False,
-                        stats=None, all_reduce_sum=None, id_shift: int = 0, chunks=None):
+                        stats=None, all_reduce_sum=None, id_shift: int = 0, chunks=None, world: int = 1):
     """One group of query batches through the global-threshold protocol (see ShardedFlatIP):
     ONE sample launch for all of the group's queries, one exchange of the sample lists, one
     threshold launch, one filter scan (+ select) per batch writing its packed top-k into a group buffer,
@@ -194,12 +194,15 @@ def _gtau_enqueue_group(local, qs, k: int, n_global: int, offset: int, gather, t
     lists = gather(best).contiguous()                               # [world, Qg, r]
     tau = kernels.dist_tau(lists, k)                                # [Qg]: one launch for the group
     kc = kernels.refine_width(k) if stats is not None else k
+    # entries each rank's list carries through the exchange (round 6: W > 1 ranks send their best
+    # exchange_cap(kc, W) instead of kc; the merge certifies truncated lists, a failure is redone exactly)
+    lc = kernels.exchange_cap(kc, world) if world > 1 and getattr(local, "exchange_capped", True) else kc
     if chunks is not None and len(chunks) > 1 and qg.shape[1] <= 768:
         # long shard: one filter launch per row chunk (the group's query blocks stay in step over a
         # chunk, so its tiles are read from HBM once), all chunks' hits in one list, one select
-        packed = torch.empty((qg.shape[0], kc + 1), dtype=torch.int64, device=qg.device)
+        packed = torch.empty((qg.shape[0], lc + 1), dtype=torch.int64, device=qg.device)
         starts = [a for a, _ in chunks] + [chunks[-1][1]]
-        kernels.dist_filter_chunks_into(qg, local.rows, n_global, kc, offset, tau, starts, packed)
+        kernels.dist_filter_chunks_into(qg, local.rows, n_global, lc, offset, tau, starts, packed)
         s, i, st = kernels.merge_packed(gather(packed), kc, n_global, k_cert=k)
     elif chunks is not None and len(chunks) > 1:
         # (wider rows) one filter launch + select per chunk, every chunk's lists a part of the merge
@@ -209,10 +212,10 @@ def _gtau_enqueue_group(local, qs, k: int, n_global: int, offset: int, gather, t
         allp = gather(parts)
         s, i, st = kernels.merge_packed(allp.reshape(-1, qg.shape[0], kc + 1), kc, n_global, k_cert=k)
     else:
-        packed = torch.empty((qg.shape[0], kc + 1), dtype=torch.int64, device=qg.device)
+        packed = torch.empty((qg.shape[0], lc + 1), dtype=torch.int64, device=qg.device)
         # ONE filter launch for the whole group (grid: corpus tiles x 128-query blocks, the blocks of
         # a tile co-located per XCD) and one select over all of its queries
-        kernels.dist_filter_into(qg, local.rows, n_global, kc, offset, tau, packed)
+        kernels.dist_filter_into(qg, local.rows, n_global, lc, offset, tau, packed)
         s, i, st = kernels.merge_packed(gather(packed), kc, n_global, k_cert=k)
     if stats is not None:
         s, i = kernels.refine(qg, local.rows, offset, s, i, k, stats, tau, st, all_reduce_sum)
@@ -631,6 +634,11 @@ class ShardedFlatIP:
                 res, nredo, nunc = _gtau_finish_group(pend, redo)
                 self.fallbacks += nredo
                 self.order_uncertified += nunc
+                if nredo and getattr(self.local, "exchange_capped", True):
+                    # a capped list reached into the merged top-kc (rows ordered by relevance across the
+                    # shards?): every later group exchanges full lists (every rank merged the same
+                    # gathered data, so every rank takes this branch)
+                    self.local.exchange_capped = False
                 return res
 
             chunks = self.group_chunks()
@@ -638,7 +646,8 @@ class ShardedFlatIP:
                 _reserve_group_memory(self.local, k, self.ntotal, chunks)
             for res in _pipeline(groups, lambda j, g: _gtau_enqueue_group(
                     self.local, g, k, self.ntotal, self.offset, self._all_gather, to_host, stats=self.stats,
-                    all_reduce_sum=lambda t: comm.all_reduce_sum_(t, self.group), chunks=chunks), fin):
+                    all_reduce_sum=lambda t: comm.all_reduce_sum_(t, self.group), chunks=chunks,
+                    world=self.world), fin):
                 yield from res
             return
         for r in _pipeline(batches, lambda j, q: self._enqueue(q, k, to_host), self._finish):
@@ -695,7 +704,7 @@ class ShardedFlatIP:
                 qd = self.local._queries(q)
                 _, _, s, i, _, h, ev, _ = _gtau_enqueue_group(
                     self.local, [qd], k, self.ntotal, self.offset, self._all_gather, stats=self.stats,
-                    all_reduce_sum=lambda t: comm.all_reduce_sum_(t, self.group))
+                    all_reduce_sum=lambda t: comm.all_reduce_sum_(t, self.group), world=self.world)
                 return ("gtau", qd, k, s, i, h, ev)
             best = self.local.dist_sample(q, self.ntotal, k)                 # [nq, r] u32 keys
             lists = self._all_gather(best)                                   # [world, nq, r]
@@ -735,6 +744,8 @@ class ShardedFlatIP:
             self.fallbacks += 1
             if self.stats is not None:   # the per-shard redo merges by fp32 scores
                 self.order_uncertified += int(q.shape[0])
+            if isinstance(self.local, FlatIPIndex):   # full exchange lists from now on (see search_batches_iter)
+                self.local.exchange_capped = False
             pend = ("pshard", q, k) + self._per_shard_enqueue(q, k)
         _, q, k, ms, mi, h, ev, s, i, st = pend
         if _status_failed(h, ev) == 0:

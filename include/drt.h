@@ -243,6 +243,14 @@ int drt_topk_merge_packed(const uint64_t* parts, int64_t nq, int32_t nparts, int
 /* The same merge of lists of k entries certified at k_cert <= k (status 1 when fewer than k_cert
  * candidates exist overall or a shard overflowed): the canonical-order stage merges
  * drt_refine_width(k_cert) entries per shard.                                                  */
+/* Capped exchange lists (round 6): parts [nparts][nq][lcap + 1], lcap <= k, each a shard's best lcap
+ * packed keys (entry lcap = count << 32 | bit 0 overflow | bit 1 truncated: the shard had more hits than
+ * it carries), merged into the top k with the certificate of drt_topk_merge_packed_cert plus: a truncated
+ * list whose last entry ranks above the k-th merged place leaves its query uncertified (status 1).
+ * 2 <= nparts <= 8, nparts * lcap <= 16384.  What a W-rank exchange carries instead of k + 1 entries.   */
+int drt_topk_merge_packed_capped(const uint64_t* parts, int64_t nq, int32_t nparts, int32_t lcap, int32_t k,
+                                 int32_t k_cert, int64_t n_global, float* out_scores, int64_t* out_ids,
+                                 int32_t* status, void* stream);
 int drt_topk_merge_packed_cert(const uint64_t* parts, int64_t nq, int32_t nparts, int32_t k,
                                int32_t k_cert, int64_t n_global, float* out_scores, int64_t* out_ids,
                                int32_t* status, void* stream);

@@ -251,6 +251,8 @@ def dist_filter(q, p_local, n_global, k, id_offset, tau):
         sel = np.nonzero(s[i] >= tau[i])[0]
         if len(sel) > plan["cap"]:
             out[i, k] = 1
+        if len(sel) > k:   # truncated: more hits than the list carries (bit 1, round 6)
+            out[i, k] |= np.uint64(2)
         keys = (desc_key(s[i, sel]).astype(np.uint64) << np.uint64(32)) | (sel + id_offset).astype(np.uint64)
         keys = np.sort(keys)[:k]
         out[i, :len(keys)] = keys
@@ -258,19 +260,34 @@ def dist_filter(q, p_local, n_global, k, id_offset, tau):
     return out
 
 
-def merge_packed(parts, k, n_global):
-    """[nparts, nq, k + 1] packed lists -> (scores f32 [nq,k], ids i64 [nq,k], status i32 [nq])."""
+def merge_packed(parts, k, n_global, k_cert=None):
+    """[nparts, nq, lcap + 1] packed lists (lcap <= k) -> (scores f32 [nq,k], ids i64 [nq,k], status i32
+    [nq]).  Capped lists (lcap < k, round 6): a list flagged truncated (bit 1) whose last entry ranks above
+    the k-th merged place leaves its query uncertified."""
     parts = np.asarray(parts, dtype=np.uint64)
-    nparts, nq, _ = parts.shape
-    keys = np.sort(np.transpose(parts[:, :, :k], (1, 0, 2)).reshape(nq, -1), axis=1)[:, :k]
+    nparts, nq, w = parts.shape
+    lcap = w - 1
+    kc = k if k_cert is None else k_cert
+    allk = np.sort(np.transpose(parts[:, :, :lcap], (1, 0, 2)).reshape(nq, -1), axis=1)
+    keys = np.full((nq, k), PAD_KEY64, dtype=np.uint64)
+    keys[:, :min(k, allk.shape[1])] = allk[:, :k]
     pad = keys == PAD_KEY64
     s = desc_key_to_score((keys >> np.uint64(32)).astype(np.uint32)).copy()
     ids = (keys & np.uint64(0xFFFFFFFF)).astype(np.int64)
     s[pad] = PAD_SCORE
     ids[pad] = PAD_ID
-    over = (parts[:, :, k] & np.uint64(1)).any(axis=0)
-    status = (over | (pad[:, k - 1] & (n_global >= k))).astype(np.int32)
-    return s.astype(np.float32), ids, status
+    over = (parts[:, :, lcap] & np.uint64(1)).any(axis=0)
+    bad = over | (pad[:, kc - 1] & (n_global >= kc))
+    if lcap < k:
+        for qi in range(nq):
+            for l in range(nparts):
+                lst = parts[l, qi, :lcap]
+                cnt = int((lst != PAD_KEY64).sum())
+                if (parts[l, qi, lcap] & np.uint64(2)) and cnt == lcap:
+                    rank = int(np.searchsorted(allk[qi], lst[cnt - 1]))   # keys are unique
+                    if rank < k - 1:
+                        bad[qi] = True
+    return s.astype(np.float32), ids, bad.astype(np.int32)
 
 
 # ---------------------------------------------------------------------------

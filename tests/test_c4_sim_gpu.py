@@ -35,14 +35,16 @@ def _simulate(dev, pt, batches, k, group_queries, monkeypatch):
     stats[1] = st[:, 1].min()                  # ShardedFlatIP.sync_offsets' combination
     groups = list(srch._groups(batches, cap=group_queries))
     kc = kernels.refine_width(k)
+    lc = kernels.exchange_cap(kc, W)           # round 6: each rank sends its best lc of kc (W = 8: 320)
+    assert lc < kc
     exch = []                                  # the other ranks' exchanged data, per group
     for grp in groups:
         qg = torch.cat(grp)
         lists = torch.stack([loc.dist_sample(qg, N, k) for loc in locs]).contiguous()
         tau = kernels.dist_tau(lists, k)
-        parts = torch.empty((W, qg.shape[0], kc + 1), dtype=torch.int64, device=dev)
+        parts = torch.empty((W, qg.shape[0], lc + 1), dtype=torch.int64, device=dev)
         for r in range(W):
-            kernels.dist_filter_into(qg, locs[r].rows, N, kc, offs[r], tau, parts[r])
+            kernels.dist_filter_into(qg, locs[r].rows, N, lc, offs[r], tau, parts[r])
         exch.append((lists, parts))
     drt = ops.load()
     cur = {}
@@ -70,7 +72,7 @@ def _simulate(dev, pt, batches, k, group_queries, monkeypatch):
                 buf[R].copy_(t)
                 return buf
             pend = srch._gtau_enqueue_group(locs[R], grp, k, N, offs[R], gather, stats=stats,
-                                            all_reduce_sum=lambda t: t)
+                                            all_reduce_sum=lambda t: t, world=W)
 
             def redo(q):
                 raise AssertionError("a group the global-threshold protocol could not certify")

@@ -167,6 +167,38 @@ def test_merge_packed_vs_oracle(dev, nparts, nq, k, fill, count_word):
     np.testing.assert_array_equal(st.cpu().numpy(), est)
 
 
+@pytest.mark.parametrize("nparts,lcap,k,fill", [(8, 320, 1256, 0.15), (4, 576, 1256, 0.3), (2, 1088, 1256, 0.7),
+                                                 (3, 96, 200, 0.4)])
+def test_merge_packed_capped_vs_oracle(dev, nparts, lcap, k, fill):
+    """Capped exchange lists (round 6): each part carries its best lcap < k keys; a part flagged truncated
+    (bit 1) whose last key ranks above the k-th merged place must leave its query uncertified -- GPU ==
+    oracle on random lists built to hit both sides of that rule."""
+    import torch
+    from denseretrievaltoolkits_amd import kernels
+    rng = np.random.default_rng(nparts * 7 + lcap)
+    nq = 64
+    n_global = nparts * k * 4
+    parts = np.full((nparts, nq, lcap + 1), np.iinfo(np.uint64).max, dtype=np.uint64)
+    for q in range(nq):
+        ids = rng.permutation(n_global)[: nparts * lcap].astype(np.uint64)
+        # some queries skew one part's scores upward (its truncated tail reaches into the top k)
+        skew = rng.random() < 0.3
+        sc = rng.integers(0, 1 << 20, size=nparts * lcap).astype(np.uint64)
+        for l in range(nparts):
+            cnt = lcap if rng.random() < 0.5 else int(rng.binomial(lcap, fill))
+            ks = sc[l * lcap: l * lcap + cnt] // (np.uint64(8) if (skew and l == 0) else np.uint64(1))
+            keys = np.sort((ks << np.uint64(32)) | ids[l * lcap: l * lcap + cnt])
+            parts[l, q, :cnt] = keys
+            trunc = cnt == lcap and rng.random() < 0.8
+            parts[l, q, lcap] = (np.uint64(cnt) << np.uint64(32)) | (np.uint64(2) if trunc else np.uint64(0))
+    es, ei, est = orc.merge_packed(parts, k, n_global)
+    s, i, st = kernels.merge_packed(torch.from_numpy(parts.view(np.int64)).to(dev), k, n_global)
+    np.testing.assert_array_equal(i.cpu().numpy(), ei)
+    np.testing.assert_array_equal(s.cpu().numpy(), es)
+    np.testing.assert_array_equal(st.cpu().numpy(), est)
+    assert 0 < est.sum() < nq   # both outcomes exercised
+
+
 @pytest.mark.parametrize("nq,n,d,k,starts", [
     (300, 50011, 768, 1000, [0, 12000, 12000, 30001, 50011]),   # 32-query kernel, an empty chunk, ragged
     (128, 40000, 768, 100, [0, 16, 20000, 40000]),               # 16-query kernel, a one-tile chunk

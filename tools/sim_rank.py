@@ -51,24 +51,35 @@ def main():
     queries = [torch.randn((qb, a.dim), generator=g, device=dev).to(torch.bfloat16) for _ in range(a.batches)]
     groups = list(srch._groups(queries))
     kc = kernels.refine_width(k)
+    lc = kernels.exchange_cap(kc, W)   # entries per rank list through the exchange (round 6)
     # the other ranks' exchanged data, per group
     glists, gparts = [], []
     for grp in groups:
         qg = torch.cat(grp)
         lists = torch.stack([locs[r].dist_sample(qg, N, k) for r in range(W)]).contiguous()
         tau = kernels.dist_tau(lists, k)
-        parts = torch.empty((W, qg.shape[0], kc + 1), dtype=torch.int64, device=dev)
+        parts = torch.empty((W, qg.shape[0], lc + 1), dtype=torch.int64, device=dev)
         for r in range(W):
-            kernels.dist_filter_into(qg, locs[r].rows, N, kc, offs[r], tau, parts[r])
+            kernels.dist_filter_into(qg, locs[r].rows, N, lc, offs[r], tau, parts[r])
         glists.append(lists)
         gparts.append(parts)
     torch.cuda.synchronize()
     own, lo = locs[R], offs[R]
     out = {"world": W, "rank": R, "n_corpus": N, "rows_per_rank": int(own.ntotal), "qb": qb, "k": k,
-           "batches": a.batches, "group_queries": srch.GROUP_QUERIES, "kc": kc}
-    cnt = (gparts[0][:, :, kc] >> 32).float()   # valid entries per (part, query): rows >= tau, capped at kc
+           "batches": a.batches, "group_queries": srch.GROUP_QUERIES, "kc": kc, "exchange_list_entries": lc}
+    qg0 = sum(q.shape[0] for q in groups[0])
+    r_ = kernels.sample_rank(k)
+    # bytes each rank RECEIVES per group through the exchange (the other W - 1 ranks' data): sample lists
+    # [Qg, r] u32 + packed lists [Qg, lc + 1] u64 + the canonical stage's delta all-reduce [Qg, kc] f32
+    # (a ring all-reduce moves ~2 (W - 1) / W of it through each rank)
+    out["exchange_MB_received_per_rank_per_group"] = {
+        "sample_lists": round((W - 1) * qg0 * r_ * 4 / 1e6, 2),
+        "packed_lists": round((W - 1) * qg0 * (lc + 1) * 8 / 1e6, 2),
+        "packed_lists_uncapped": round((W - 1) * qg0 * (kc + 1) * 8 / 1e6, 2),
+        "delta_allreduce": round(2 * (W - 1) / W * qg0 * kc * 4 / 1e6, 2)}
+    cnt = (gparts[0][:, :, lc] >> 32).float()   # valid entries per (part, query): rows >= tau, capped at lc
     out["hits_per_part"] = {"mean": round(float(cnt.mean()), 1), "min": int(cnt.min()), "max": int(cnt.max()),
-                            "full_frac": round(float((cnt >= kc).float().mean()), 4)}
+                            "full_frac": round(float((cnt >= lc).float().mean()), 4)}
 
     filt = kernels.dist_filter_into
 
@@ -90,9 +101,11 @@ def main():
                 buf[R].copy_(t)
                 return buf
             pend.append(srch._gtau_enqueue_group(own, grp, k, N, lo, gather, stats=stats,
-                                                 all_reduce_sum=lambda t: t))
+                                                 all_reduce_sum=lambda t: t, world=W))
+        nredo = 0
         for p in pend:
-            srch._gtau_finish_group(p, lambda q: None)
+            nredo += srch._gtau_finish_group(p, lambda q: (q, q))[1]
+        run_all.redone = nredo
 
     for rep in range(a.reps):
         for var in a.variants.split(","):
@@ -105,7 +118,8 @@ def main():
             run_all()
             torch.cuda.synchronize()
             el = time.perf_counter() - t0
-            res = {"rep": rep, "variant": var, "ms_per_batch": round(el / a.batches * 1e3, 4),
+            res = {"rep": rep, "variant": var, "batches_uncertified": run_all.redone,
+                   "ms_per_batch": round(el / a.batches * 1e3, 4),
                    "qps_if_comm_free": round(a.batches * qb / el, 1)}
             for name, f in fams.items():
                 lib.drt_profile_enable(f, 0)
