@@ -225,6 +225,215 @@ __global__ __launch_bounds__(256) void splitk_reduce_kernel(const float* ws, int
   }
 }
 
+// ---------------------------------------------------------------------------
+// Large-tile exact-f32 GEMM (round 6, the score matrix and its backward at the C3 shape).
+// The 64 x 64 kernel above moves 1/16 B of operands per flop through VGPR staging and
+// ds_write_b32 between two barriers per K-step; at 512 x 4096 x 768 it runs at 0.53 of the
+// f32 MFMA rate.  Here a TM x TN block (TM = 128; TN = 64 forward, 96 backward) lands its
+// 32-deep K-steps global -> LDS with global_load_lds_dwordx4 in a STAGES-slot ring (no
+// staging registers, no LDS stores, one barrier per step) and each wave runs MT x NT
+// v_mfma_f32_32x32x2_f32 tiles.
+//   k-contiguous operand (q, p, dS as [m][n]): image [rows][8 x 16 B], chunk c of row r at
+//     position c ^ ((r >> 1) & 7); in a K-step lane (r, h) carries k = 16 h + s at MFMA s, so it
+//     reads its 16 k as 4 ds_read_b128 (conflict-free for every b128 lane group with this XOR).
+//   k-major operand (p / q as [k][d], dS^T): image [32 k][cols] fp32 as stored; lane (c, h)
+//     reads k row 16 h + s with one ds_read_b32 (32 consecutive floats per lane group).
+// The k order inside a step differs from the 64 x 64 kernel's (both are exact-f32 fmaf
+// chains; results agree to f32 rounding).  Blocks are remapped so that an XCD's blocks are
+// contiguous tiles sharing an operand panel (the wide operand is read into each L2 once).
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ void f32_glds16(const void* gsrc, uint32_t lds_addr) {
+  uint32_t keep;
+  asm volatile(
+      "s_mov_b32 %0, m0\n\t"
+      "s_mov_b32 m0, %2\n\t"
+      "s_nop 0\n\t"
+      "global_load_lds_dwordx4 %1, off\n\t"
+      "s_mov_b32 m0, %0"
+      : "=&s"(keep)
+      : "v"(gsrc), "s"(lds_addr)
+      : "memory");
+}
+
+__device__ __forceinline__ uint32_t f32_lds_addr(const void* p) {
+  return (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) char*)p;
+}
+
+struct F32Prob {
+  const float* A;   // KC: [m][lda] (row i, k) ; else [k][lda] (k, row i)
+  const float* B;   // KC: [n][ldb] ; else [k][ldb]
+  float* C;         // [m][ldc]; split z writes C + z * m * ldc
+  int64_t m, n, k, lda, ldb, ldc;
+  int64_t kchunk;   // k per split, multiple of 32
+  int tiles_m, tiles_n, splits;
+  int m_fast;       // block order inside the problem: 1 = m-tiles of one n-panel adjacent
+};
+
+// One operand's 32-deep K-step (ROWS rows of the output side) into its ring slot.  KC: 1 KiB
+// wave-instruction J = rows 8J .. 8J + 7 (rows past `rows` clamped: masked outputs); k-major:
+// J = floats [256 J, 256 J + 256) of the [32][ROWS] image (columns past `rows` clamped; `rows`
+// % 4 == 0 keeps every 16-B chunk whole).
+template <int ROWS, bool KC>
+__device__ __forceinline__ void f32_stage(const float* X, int64_t ld, int64_t r0, int64_t rows, int64_t k0,
+                                          uint32_t lds, int wave, int lane) {
+  constexpr int NI = ROWS / 8;
+  static_assert(NI % 4 == 0, "4 waves share the wave-instructions");
+#pragma unroll
+  for (int J0 = 0; J0 < NI; J0 += 4) {
+    const int J = J0 + wave;
+    const float* p;
+    if (KC) {
+      const int row = 8 * J + (lane >> 3);
+      int64_t gr = r0 + row;
+      gr = gr < rows ? gr : rows - 1;
+      const int chunk = (lane & 7) ^ ((4 * J + (lane >> 4)) & 7);
+      p = X + gr * ld + k0 + chunk * 4;
+    } else {
+      const int f = J * 256 + lane * 4;
+      const int kr = f / ROWS, col = f - kr * ROWS;
+      int64_t gc = r0 + col;
+      gc = gc < rows ? gc : rows - 4;
+      p = X + (k0 + kr) * ld + gc;
+    }
+    f32_glds16(p, __builtin_amdgcn_readfirstlane(lds + J * 1024));
+  }
+}
+
+// s_waitcnt vmcnt(PER * n): all but the n youngest K-steps (PER LDS-DMA per wave each) landed.
+template <int PER>
+__device__ __forceinline__ void f32_wait_steps(int n) {
+  if (n <= 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  else if (n == 1) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(PER) : "memory");
+  else asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * PER) : "memory");
+}
+
+template <int TM, int TN, int WM, int WN, bool A_KC, bool B_KC, int STAGES>
+struct F32Cfg {
+  static constexpr int kA = TM * 128, kB = TN * 128, kStage = kA + kB, kLds = STAGES * kStage;
+  static constexpr int kPer = kStage / 4096;            // LDS-DMA per wave per K-step
+  static constexpr int MT = TM / WM / 32, NT = TN / WN / 32;
+  static_assert(WM * WN == 4 && MT * WM * 32 == TM && NT * WN * 32 == TN, "4 waves of 32 x 32 tiles");
+  static_assert(STAGES >= 2 && STAGES <= 4, "ring depth");
+};
+
+template <int TM, int TN, int WM, int WN, bool A_KC, bool B_KC, int STAGES>
+__device__ __forceinline__ void f32x_block(const F32Prob& g, int64_t wg, char* smem) {
+  using Cfg = F32Cfg<TM, TN, WM, WN, A_KC, B_KC, STAGES>;
+  constexpr int MT = Cfg::MT, NT = Cfg::NT;
+  const int per_split = g.tiles_m * g.tiles_n;
+  const int z = (int)(wg / per_split);
+  const int t = (int)(wg - (int64_t)z * per_split);
+  const int tm = g.m_fast ? t % g.tiles_m : t / g.tiles_n;
+  const int tn = g.m_fast ? t / g.tiles_m : t % g.tiles_n;
+  const int tid = threadIdx.x;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int lane = tid & 63;
+  const int r = lane & 31, h = lane >> 5;
+  const int wm = wave / WN, wn = wave % WN;
+  const int64_t m0 = (int64_t)tm * TM, n0 = (int64_t)tn * TN;
+  const int64_t kb = (int64_t)z * g.kchunk;
+  const int64_t ke = kb + g.kchunk < g.k ? kb + g.kchunk : g.k;
+  const int nt = (int)((ke - kb) / 32);
+  const uint32_t lds0 = f32_lds_addr(smem);
+  auto stage = [&](int s, int slot) {
+    const uint32_t base = lds0 + slot * Cfg::kStage;
+    f32_stage<TM, A_KC>(g.A, g.lda, m0, g.m, kb + (int64_t)s * 32, base, wave, lane);
+    f32_stage<TN, B_KC>(g.B, g.ldb, n0, g.n, kb + (int64_t)s * 32, base + Cfg::kA, wave, lane);
+  };
+  f32x16 acc[MT][NT];
+#pragma unroll
+  for (int i = 0; i < MT; ++i)
+#pragma unroll
+    for (int j = 0; j < NT; ++j)
+#pragma unroll
+      for (int e = 0; e < 16; ++e) acc[i][j][e] = 0.0f;
+
+#pragma unroll
+  for (int s = 0; s < STAGES - 1; ++s)
+    if (s < nt) stage(s, s);
+  // per-lane read offsets: KC rows r of each 32-row tile (XOR (r >> 1) & 7), k-major column r, k row 16 h
+  const int swz = (r >> 1) & 7;
+  const int arow = wm * MT * 32 + r, brow = wn * NT * 32 + r;
+  for (int s = 0; s < nt; ++s) {
+    const int younger = nt - 1 - s < STAGES - 2 ? nt - 1 - s : STAGES - 2;
+    f32_wait_steps<Cfg::kPer>(younger);
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_sched_barrier(0);
+    if (s + STAGES - 1 < nt) stage(s + STAGES - 1, (s + STAGES - 1) % STAGES);
+    const char* As = smem + (s % STAGES) * Cfg::kStage;
+    const char* Bs = As + Cfg::kA;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      f32x4 av[MT], bv[NT];
+#pragma unroll
+      for (int i = 0; i < MT; ++i) {
+        if (A_KC) {
+          av[i] = *(const f32x4*)(As + (arow + i * 32) * 128 + (((4 * h + j) ^ swz) << 4));
+        } else {
+#pragma unroll
+          for (int e = 0; e < 4; ++e) av[i][e] = ((const float*)As)[(16 * h + 4 * j + e) * TM + arow + i * 32];
+        }
+      }
+#pragma unroll
+      for (int i = 0; i < NT; ++i) {
+        if (B_KC) {
+          bv[i] = *(const f32x4*)(Bs + (brow + i * 32) * 128 + (((4 * h + j) ^ swz) << 4));
+        } else {
+#pragma unroll
+          for (int e = 0; e < 4; ++e) bv[i][e] = ((const float*)Bs)[(16 * h + 4 * j + e) * TN + brow + i * 32];
+        }
+      }
+#pragma unroll
+      for (int e = 0; e < 4; ++e)
+#pragma unroll
+        for (int i = 0; i < MT; ++i)
+#pragma unroll
+          for (int jj = 0; jj < NT; ++jj)
+            acc[i][jj] = __builtin_amdgcn_mfma_f32_32x32x2f32(av[i][e], bv[jj][e], acc[i][jj], 0, 0, 0);
+    }
+    __builtin_amdgcn_sched_barrier(0);
+  }
+  float* Cz = g.C + (int64_t)z * g.m * g.ldc;
+#pragma unroll
+  for (int i = 0; i < MT; ++i)
+#pragma unroll
+    for (int jj = 0; jj < NT; ++jj)
+#pragma unroll
+      for (int e = 0; e < 16; ++e) {
+        const int64_t row = m0 + wm * MT * 32 + i * 32 + 8 * (e >> 2) + 4 * h + (e & 3);
+        const int64_t col = n0 + wn * NT * 32 + jj * 32 + r;
+        if (row < g.m && col < g.n) Cz[row * g.ldc + col] = acc[i][jj][e];
+      }
+}
+
+// XCD-contiguous block rank (blocks b, b + 8, ... run on XCD b % 8): an XCD's blocks are a
+// contiguous range of the problem's (split, tile) order.
+__device__ __forceinline__ int64_t f32_xcd_rank(int64_t bid, int64_t nwg) {
+  const int64_t xcd = bid & 7, q8 = nwg >> 3, r8 = nwg & 7;
+  return (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (bid >> 3);
+}
+
+// forward: S (or split partials) = q . p^T, both k-contiguous
+constexpr int kFwdTN = 64, kFwdStages = 4;
+using FwdCfg = F32Cfg<128, kFwdTN, 2, 2, true, true, kFwdStages>;
+__global__ __launch_bounds__(256) void score_fwd_gemm_kernel(F32Prob g) {
+  __shared__ __attribute__((aligned(16))) char smem[FwdCfg::kLds];
+  f32x_block<128, kFwdTN, 2, 2, true, true, kFwdStages>(g, f32_xcd_rank(blockIdx.x, gridDim.x), smem);
+}
+
+// backward, both GEMMs in one grid: problem 0 dq = dS . p (dS k-contiguous, p k-major),
+// problem 1 dp = dS^T . q (both k-major); blocks [0, nb0) are problem 0.
+constexpr int kBwdTN = 96, kBwdStages = 2;
+using Bwd0Cfg = F32Cfg<128, kBwdTN, 4, 1, true, false, kBwdStages>;
+using Bwd1Cfg = F32Cfg<128, kBwdTN, 4, 1, false, false, kBwdStages>;
+static_assert(Bwd0Cfg::kLds == Bwd1Cfg::kLds, "one LDS size");
+__global__ __launch_bounds__(256) void score_bwd_gemm_kernel(F32Prob g0, F32Prob g1, int64_t nb0) {
+  __shared__ __attribute__((aligned(16))) char smem[Bwd0Cfg::kLds];
+  const int64_t wg = f32_xcd_rank(blockIdx.x, gridDim.x);
+  if (wg < nb0) f32x_block<128, kBwdTN, 4, 1, true, false, kBwdStages>(g0, wg, smem);
+  else f32x_block<128, kBwdTN, 4, 1, false, false, kBwdStages>(g1, wg - nb0, smem);
+}
+
 __device__ __forceinline__ float warp_max(float v) {
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
@@ -420,13 +629,53 @@ static void split_plan(int64_t m, int64_t n, int64_t k, int64_t& kchunk, int64_t
   nz = k > 0 ? (k + kchunk - 1) / kchunk : 1;
 }
 
+static int64_t cdiv(int64_t a, int64_t b) { return (a + b - 1) / b; }
+
+// Large-tile path: every K range whole 32-deep steps (m, n, d multiples of 32), 16-B aligned rows.
+static bool large_f32_shape(int64_t m, int64_t n, int64_t d) { return m % 32 == 0 && n % 32 == 0 && d % 32 == 0; }
+static bool large_f32_ok(const float* q, const float* p, int64_t m, int64_t n, int64_t d) {
+  return large_f32_shape(m, n, d) && (uintptr_t)q % 16 == 0 && (uintptr_t)p % 16 == 0;
+}
+
+// forward: 128 x 64 tiles, K split until ~256 blocks (one per CU; >= 2 steps per split)
+static void fwd_plan_large(int64_t m, int64_t n, int64_t d, int64_t& kc, int64_t& z) {
+  const int64_t tiles = cdiv(m, 128) * cdiv(n, kFwdTN);
+  int64_t splits = cdiv(256, tiles);
+  if (splits > d / 64) splits = d / 64;
+  if (splits < 1) splits = 1;
+  kc = cdiv(cdiv(d, splits), 32) * 32;
+  z = cdiv(d, kc);
+}
+
+// backward: 128 x 96 tiles of dq [m][d] (K = n) and dp [n][d] (K = m), one K chunk for both so every
+// block carries the same work, sized for ~512 blocks (two per CU); a problem whose K fits one chunk
+// writes its output directly.
+static void bwd_plan_large(int64_t m, int64_t n, int64_t d, int64_t& kc0, int64_t& z0, int64_t& kc1, int64_t& z1) {
+  const int64_t tn = cdiv(d, kBwdTN);
+  const int64_t work = cdiv(m, 128) * tn * n + cdiv(n, 128) * tn * m;
+  int64_t kc = cdiv(cdiv(work, 512), 32) * 32;
+  if (kc < 128) kc = 128;
+  kc0 = kc < n ? kc : n;
+  z0 = cdiv(n, kc0);
+  kc1 = kc < m ? kc : m;
+  z1 = cdiv(m, kc1);
+}
+
 static size_t score_ce_ws_floats(int64_t m, int64_t n, int64_t d, size_t* fwd, size_t* bwd) {
   int64_t kc, z, kc0, z0, kc1, z1;
   split_plan(m, n, d, kc, z);
   split_plan(m, d, n, kc0, z0);
   split_plan(n, d, m, kc1, z1);
-  const size_t f = (size_t)z * m * n + (size_t)m;
-  const size_t b = (size_t)m * n + (size_t)z0 * m * d + (size_t)z1 * n * d;
+  size_t f = (size_t)z * m * n + (size_t)m;
+  size_t b = (size_t)m * n + (size_t)z0 * m * d + (size_t)z1 * n * d;
+  if (large_f32_shape(m, n, d)) {   // the large-tile plan may split differently: room for either
+    fwd_plan_large(m, n, d, kc, z);
+    bwd_plan_large(m, n, d, kc0, z0, kc1, z1);
+    const size_t fl = (z > 1 ? (size_t)z * m * n : 0) + (size_t)m;
+    const size_t bl = (size_t)m * n + (z0 > 1 ? (size_t)z0 * m * d : 0) + (z1 > 1 ? (size_t)z1 * n * d : 0);
+    f = f > fl ? f : fl;
+    b = b > bl ? b : bl;
+  }
   if (fwd) *fwd = f;
   if (bwd) *bwd = b;
   return f > b ? f : b;
@@ -438,15 +687,32 @@ size_t drt_score_ce_workspace(int64_t m, int64_t n, int32_t d) {
 }
 
 // S = q . p^T (exact f32), lse, loss = scale * mean_i (lse_i - S[i][i * target_stride]).
-// 3 launches: split-K GEMM -> per-row (split reduce + LSE + row loss) -> fixed-order mean.
+// 3 launches: GEMM (split-K partials or S itself) -> per-row (split reduce + LSE + row loss) ->
+// fixed-order mean.
 int drt_score_ce_fwd(const float* q, const float* p, int64_t m, int64_t n, int32_t d, int64_t target_stride,
                      float scale, float* S, float* lse, float* loss, void* ws, size_t ws_bytes, void* stream) {
   DRT_REQUIRE(m > 0 && n > 0 && d > 0 && target_stride >= 0 && (m - 1) * target_stride < n);
   DRT_REQUIRE(q && p && S && lse && loss && ws && ws_bytes >= drt_score_ce_workspace(m, n, d));
   hipStream_t s = (hipStream_t)stream;
   int64_t kc, z;
-  split_plan(m, n, d, kc, z);
   float* part = (float*)ws;
+  if (large_f32_ok(q, p, m, n, d)) {
+    fwd_plan_large(m, n, d, kc, z);
+    float* row_loss = part + (z > 1 ? (size_t)z * m * n : 0);
+    F32Prob g{q, p, z > 1 ? part : S, m, n, (int64_t)d, (int64_t)d, (int64_t)d, n, kc,
+              (int)cdiv(m, 128), (int)cdiv(n, kFwdTN), (int)z, 1};
+    const int64_t blocks = (int64_t)g.tiles_m * g.tiles_n * z;
+    hipLaunchKernelGGL(score_fwd_gemm_kernel, dim3((unsigned)blocks), dim3(256), 0, s, g);
+    if (z > 1)
+      hipLaunchKernelGGL(ce_fwd_reduce_kernel, dim3((unsigned)m), dim3(256), 0, s, (const float*)part, z, S, m, n,
+                         target_stride, lse, row_loss);
+    else
+      hipLaunchKernelGGL(ce_fwd_kernel, dim3((unsigned)m), dim3(256), 0, s, (const float*)S, m, n, target_stride,
+                         lse, row_loss);
+    hipLaunchKernelGGL(mean_kernel, dim3(1), dim3(256), 0, s, (const float*)row_loss, m, scale, loss);
+    return hip_status(hipGetLastError());
+  }
+  split_plan(m, n, d, kc, z);
   float* row_loss = part + (size_t)z * m * n;
   const bool vec = ((uintptr_t)q % 16 == 0) && ((uintptr_t)p % 16 == 0) && d % 4 == 0;
   dim3 grid((unsigned)((n + kGT - 1) / kGT), (unsigned)((m + kGT - 1) / kGT), (unsigned)z);
@@ -468,9 +734,30 @@ int drt_score_ce_bwd(const float* q, const float* p, const float* S, const float
   DRT_REQUIRE(m > 0 && n > 0 && d > 0 && target_stride >= 0 && (m - 1) * target_stride < n);
   DRT_REQUIRE(q && p && S && lse && dq && dp && ws && ws_bytes >= drt_score_ce_workspace(m, n, d));
   hipStream_t s = (hipStream_t)stream;
-  DualGemm g{};
   float* dS = (float*)ws;
   int64_t kc0, z0, kc1, z1;
+  if (large_f32_ok(q, p, m, n, d)) {
+    bwd_plan_large(m, n, d, kc0, z0, kc1, z1);
+    float* ws0 = dS + (size_t)m * n;
+    float* ws1 = ws0 + (z0 > 1 ? (size_t)z0 * m * d : 0);
+    const int tn = (int)cdiv(d, kBwdTN);
+    F32Prob g0{dS, p, z0 > 1 ? ws0 : dq, m, (int64_t)d, n, n, (int64_t)d, (int64_t)d, kc0,
+               (int)cdiv(m, 128), tn, (int)z0, 0};
+    F32Prob g1{dS, q, z1 > 1 ? ws1 : dp, n, (int64_t)d, m, n, (int64_t)d, (int64_t)d, kc1,
+               (int)cdiv(n, 128), tn, (int)z1, 0};
+    const int64_t nb0 = (int64_t)g0.tiles_m * tn * z0, nb1 = (int64_t)g1.tiles_m * tn * z1;
+    hipLaunchKernelGGL(ce_bwd_kernel, dim3((unsigned)m), dim3(256), 0, s, S, lse, m, n, target_stride, grad, scale,
+                       dS);
+    hipLaunchKernelGGL(score_bwd_gemm_kernel, dim3((unsigned)(nb0 + nb1)), dim3(256), 0, s, g0, g1, nb0);
+    const int64_t e0 = z0 > 1 ? m * d : 0, e1 = z1 > 1 ? n * d : 0;
+    if (e0 + e1 > 0) {
+      const int64_t rb = (e0 + e1 + 255) / 256 < 2048 ? (e0 + e1 + 255) / 256 : 2048;
+      hipLaunchKernelGGL(dual_reduce_kernel, dim3((unsigned)rb), dim3(256), 0, s, (const float*)ws0, z0, e0, dq,
+                         (const float*)ws1, z1, e1, dp);
+    }
+    return hip_status(hipGetLastError());
+  }
+  DualGemm g{};
   split_plan(m, d, n, kc0, z0);
   split_plan(n, d, m, kc1, z1);
   g.dS = dS; g.p = p; g.q = q;

@@ -328,12 +328,13 @@ def merge_packed(parts: torch.Tensor, k: int, n_global: int, k_cert: int = -1):
 def exchange_cap(kc: int, nparts: int) -> int:
     """Entries per shard list a W-way exchange carries (round 6): a shard holds ~kc / W of the
     merged top-kc (Binomial(kc, 1 / W) for rows not ordered by relevance), so it sends its best
-    ceil(1.6 kc / W) + 64 packed keys (13 sigma above the mean at W = 8: 320 of 1256) instead of kc; a
-    query whose truncated list reaches into the merged top-kc is redone exactly (merge_packed's
-    certificate).  kc itself for one part, beyond the count merge's 8 parts, or when the cap saves little."""
+    ceil(1.25 kc / W) + 32 packed keys, rounded up to 64 (8 sigma above the mean at W = 8: 256 of 1256;
+    11 sigma at W = 2: 832) instead of kc; a query whose truncated list reaches into the merged top-kc is
+    redone exactly (merge_packed's certificate) and the index then exchanges whole lists.  kc itself for
+    one part, beyond the count merge's 8 parts, or when the cap saves little."""
     if nparts <= 1 or nparts > 8:
         return kc
-    cap = -(-16 * kc // (10 * nparts)) + 64
+    cap = -(-5 * kc // (4 * nparts)) + 32
     cap = -(-cap // 64) * 64
     return kc if cap * 10 >= kc * 9 else cap
 

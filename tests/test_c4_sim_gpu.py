@@ -35,7 +35,7 @@ def _simulate(dev, pt, batches, k, group_queries, monkeypatch):
     stats[1] = st[:, 1].min()                  # ShardedFlatIP.sync_offsets' combination
     groups = list(srch._groups(batches, cap=group_queries))
     kc = kernels.refine_width(k)
-    lc = kernels.exchange_cap(kc, W)           # round 6: each rank sends its best lc of kc (W = 8: 320)
+    lc = kernels.exchange_cap(kc, W)           # round 6: each rank sends its best lc of kc (W = 8: 256)
     assert lc < kc
     exch = []                                  # the other ranks' exchanged data, per group
     for grp in groups:

@@ -167,7 +167,7 @@ def test_merge_packed_vs_oracle(dev, nparts, nq, k, fill, count_word):
     np.testing.assert_array_equal(st.cpu().numpy(), est)
 
 
-@pytest.mark.parametrize("nparts,lcap,k,fill", [(8, 320, 1256, 0.15), (4, 576, 1256, 0.3), (2, 1088, 1256, 0.7),
+@pytest.mark.parametrize("nparts,lcap,k,fill", [(8, 256, 1256, 0.15), (4, 448, 1256, 0.3), (2, 832, 1256, 0.7),
                                                  (3, 96, 200, 0.4)])
 def test_merge_packed_capped_vs_oracle(dev, nparts, lcap, k, fill):
     """Capped exchange lists (round 6): each part carries its best lcap < k keys; a part flagged truncated

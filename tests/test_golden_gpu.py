@@ -200,10 +200,14 @@ def test_gemm_f32_layouts_vs_fp64(dev, m, n, k, a_kc, b_kc):
 
 
 @pytest.mark.parametrize("m,n,d,stride", [(512, 1024, 768, 2), (512, 4096, 768, 8), (37, 111, 100, 3),
-                                          (8, 16, 768, 2), (1, 5, 64, 0)])
+                                          (8, 16, 768, 2), (1, 5, 64, 0), (96, 224, 160, 2), (160, 320, 96, 2),
+                                          (32, 64, 32, 1)])
 def test_fused_score_ce_bit_identical_to_unfused_kernels(dev, m, n, d, stride):
     """drt_score_ce_fwd / _bwd (2 host calls, 6 launches) == drt_gemm_f32 + drt_ce_fwd + drt_ce_bwd +
-    drt_gemm_f32 x 2 (the same fixed-order split-K sums) bit for bit, and torch fp32 autograd within 1e-5."""
+    drt_gemm_f32 x 2 (the same fixed-order split-K sums) bit for bit, and torch fp32 autograd within 1e-5.
+    Shapes with m, n, d multiples of 32 take the large-tile GEMMs (round 6: 128 x 64 / 128 x 96 tiles, another
+    k order and split inside each sum), so there the two agree to f32 rounding instead; the ragged cases here
+    (tiles cut by m, n and d) pin that path against fp64 like the others."""
     import torch
     from denseretrievaltoolkits_amd import _native
     from denseretrievaltoolkits_amd.score_ce import gemm_f32, score_ce
@@ -224,8 +228,14 @@ def test_fused_score_ce_bit_identical_to_unfused_kernels(dev, m, n, d, stride):
     _native.check(lib.drt_ce_bwd(S2.data_ptr(), lse.data_ptr(), m, n, stride, gg.data_ptr(), 1.5, dS.data_ptr(), s), "b")
     dq2 = gemm_f32(dS, p.detach(), True, False, m, d, n)
     dp2 = gemm_f32(dS, q.detach(), False, False, n, d, m)
-    assert torch.equal(S, S2) and torch.equal(loss.detach(), l2)
-    assert torch.equal(q.grad, dq2) and torch.equal(p.grad, dp2)
+    if m % 32 or n % 32 or d % 32:
+        assert torch.equal(S, S2) and torch.equal(loss.detach(), l2)
+        assert torch.equal(q.grad, dq2) and torch.equal(p.grad, dp2)
+    else:   # large-tile path: another summation order, f32 rounding apart
+        torch.testing.assert_close(S, S2, rtol=1e-5, atol=1e-4)
+        torch.testing.assert_close(loss.detach(), l2, rtol=1e-5, atol=1e-6)
+        for got, want in ((q.grad, dq2), (p.grad, dp2)):
+            torch.testing.assert_close(got, want, rtol=1e-4, atol=5e-5 * float(want.abs().max()))
     qt, pt = q.detach().double().requires_grad_(True), p.detach().double().requires_grad_(True)
     ref = 1.5 * torch.nn.functional.cross_entropy(qt @ pt.T, torch.arange(m, device=dev) * stride)
     (2.0 * ref).backward()
