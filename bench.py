@@ -413,6 +413,8 @@ def search_record(args, world, grouped, group_queries, kc, elapsed_s, launch_ms_
         rf["launches_counted"] = launches   # the profiler's count (differs only if a batch was redone)
     ps = per_shape(d, k, kc, shapes, grouped, each_ms)
     if ps is not None and len(ps) > 1:
+        for e in ps:   # PMC traffic of each shape where a record of that launch shape exists
+            e["traffic"], e["traffic_source"] = pmc_traffic(args, world, (e["queries"], e["rows"]) if grouped else None)
         rf["per_shape"] = ps   # rank 0's launches by shape (the line's avg_launch_ms mixes them)
     # PMC traffic (tools/pmc_traffic.py) of this configuration's dominant launch shape
     tb, tsrc = traffic
