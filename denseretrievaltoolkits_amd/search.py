@@ -173,8 +173,29 @@ def _reserve_group_memory(local, k: int, n_global: int, chunks=None):
     local._group_reserved = key
 
 
+class _SideChannel:
+    """The exchange side channel of a sharded index (round 6, SURVEY §5 "overlap the exchange for batch i
+    with the scan for batch i + 1"): a second HIP stream and a second communicator over the same ranks.
+    A group's packed all-gather, merge and canonical-order stage (its delta all-reduce included) run on
+    the side stream behind an event on the filter scan, while the next group's sample, sample-list
+    all-gather and filter scans run on the compute stream.  The second communicator matters: one RCCL
+    communicator runs its collectives in issue order on one internal stream, so the next group's
+    sample-list all-gather would queue behind this group's exchange and hold its scans back."""
+    __slots__ = ("stream", "group")
+
+    def __init__(self, stream, group):
+        self.stream, self.group = stream, group
+
+    def gather(self, t: torch.Tensor) -> torch.Tensor:
+        return comm.all_gather_stacked(t, self.group)
+
+    def all_reduce_sum(self, t: torch.Tensor) -> torch.Tensor:
+        return comm.all_reduce_sum_(t, self.group)
+
+
 def _gtau_enqueue_group(local, qs, k: int, n_global: int, offset: int, gather, to_host: bool = False,
-                        stats=None, all_reduce_sum=None, id_shift: int = 0, chunks=None, world: int = 1):
+                        stats=None, all_reduce_sum=None, id_shift: int = 0, chunks=None, world: int = 1,
+                        side: _SideChannel = None):
     """One group of query batches through the global-threshold protocol (see ShardedFlatIP):
     ONE sample launch for all of the group's queries, one exchange of the sample lists, one
     threshold launch, one filter scan (+ select) per batch writing its packed top-k into a group buffer,
@@ -187,7 +208,9 @@ def _gtau_enqueue_group(local, qs, k: int, n_global: int, offset: int, gather, t
     protocol itself runs on the index's own row numbers, packed in 32 bits).  ``chunks``: the filter runs as
     one launch per row range of this shard (group_chunks) and the chunks' hits are selected once
     (kernels.dist_filter_chunks_into; d > 768: each chunk's packed lists are a part of the merge, gathered
-    [world, chunks, ...] -- the same chunk count on every rank)."""
+    [world, chunks, ...] -- the same chunk count on every rank).  ``side`` (a _SideChannel): everything
+    after the filter scans -- exchange, merge, canonical stage, status staging -- goes on the side stream
+    and through its communicator, so the caller can enqueue the next group's scans behind it."""
     sizes = [q.shape[0] for q in qs]
     qg = qs[0] if len(qs) == 1 else torch.cat(qs)
     best = local.dist_sample(qg, n_global, k)                       # [Qg, r]
@@ -200,29 +223,45 @@ def _gtau_enqueue_group(local, qs, k: int, n_global: int, offset: int, gather, t
     if chunks is not None and len(chunks) > 1 and qg.shape[1] <= 768:
         # long shard: one filter launch per row chunk (the group's query blocks stay in step over a
         # chunk, so its tiles are read from HBM once), all chunks' hits in one list, one select
-        packed = torch.empty((qg.shape[0], lc + 1), dtype=torch.int64, device=qg.device)
+        lists = torch.empty((qg.shape[0], lc + 1), dtype=torch.int64, device=qg.device)
         starts = [a for a, _ in chunks] + [chunks[-1][1]]
-        kernels.dist_filter_chunks_into(qg, local.rows, n_global, lc, offset, tau, starts, packed)
-        s, i, st = kernels.merge_packed(gather(packed), kc, n_global, k_cert=k)
+        kernels.dist_filter_chunks_into(qg, local.rows, n_global, lc, offset, tau, starts, lists)
     elif chunks is not None and len(chunks) > 1:
         # (wider rows) one filter launch + select per chunk, every chunk's lists a part of the merge
-        parts = torch.empty((len(chunks), qg.shape[0], kc + 1), dtype=torch.int64, device=qg.device)
+        lists = torch.empty((len(chunks), qg.shape[0], kc + 1), dtype=torch.int64, device=qg.device)
         for c, (a, b) in enumerate(chunks):
-            kernels.dist_filter_into(qg, local.rows[a:b], n_global, kc, offset + a, tau, parts[c])
-        allp = gather(parts)
-        s, i, st = kernels.merge_packed(allp.reshape(-1, qg.shape[0], kc + 1), kc, n_global, k_cert=k)
+            kernels.dist_filter_into(qg, local.rows[a:b], n_global, kc, offset + a, tau, lists[c])
     else:
-        packed = torch.empty((qg.shape[0], lc + 1), dtype=torch.int64, device=qg.device)
+        lists = torch.empty((qg.shape[0], lc + 1), dtype=torch.int64, device=qg.device)
         # ONE filter launch for the whole group (grid: corpus tiles x 128-query blocks, the blocks of
         # a tile co-located per XCD) and one select over all of its queries
-        kernels.dist_filter_into(qg, local.rows, n_global, lc, offset, tau, packed)
-        s, i, st = kernels.merge_packed(gather(packed), kc, n_global, k_cert=k)
-    if stats is not None:
-        s, i = kernels.refine(qg, local.rows, offset, s, i, k, stats, tau, st, all_reduce_sum)
-    if id_shift:
-        i = torch.where(i >= 0, i + id_shift, i)
-    h, ev = _stage_status(st)
-    host = _HostResult(s, i) if to_host else None
+        kernels.dist_filter_into(qg, local.rows, n_global, lc, offset, tau, lists)
+
+    def exchange(gather, all_reduce_sum):
+        allp = gather(lists)
+        if lists.dim() == 3:
+            allp = allp.reshape(-1, qg.shape[0], kc + 1)
+        s, i, st = kernels.merge_packed(allp, kc, n_global, k_cert=k)
+        if stats is not None:
+            s, i = kernels.refine(qg, local.rows, offset, s, i, k, stats, tau, st, all_reduce_sum)
+        if id_shift:
+            i = torch.where(i >= 0, i + id_shift, i)
+        h, ev = _stage_status(st)
+        host = _HostResult(s, i) if to_host else None
+        return s, i, st, h, ev, host
+
+    if side is None:
+        return (qs, sizes) + exchange(gather, all_reduce_sum)
+    compute = torch.cuda.current_stream(qg.device)
+    scanned = torch.cuda.Event()
+    scanned.record(compute)
+    with torch.cuda.stream(side.stream):
+        side.stream.wait_event(scanned)
+        for t in (lists, qg, tau):   # compute-stream allocations the side stream still reads
+            t.record_stream(side.stream)
+        s, i, st, h, ev, host = exchange(side.gather, side.all_reduce_sum)
+    for t in (s, i, st):   # side-stream results the caller reads on its own stream
+        t.record_stream(compute)
     return qs, sizes, s, i, st, h, ev, host
 
 
@@ -572,6 +611,14 @@ class ShardedFlatIP:
         self.offset = 0      # global id of this shard's first row
         self.ntotal = 0      # rows over all shards
         self.stats = None    # GLOBAL row statistics (max over shards), set by sync_offsets
+        # grouped search: run each group's exchange + merge + canonical stage on a side stream and a
+        # second communicator, beside the next group's scans (_SideChannel).  Off by default: the
+        # group's filter launch keeps one 153-KiB-LDS, 512-VGPR work-group on EVERY CU for its whole
+        # duration, so RCCL's copy kernels only get CUs between scans either way, and the side kernels
+        # then hold the next scan's work-groups back ("overlapped exchange"); the 8-GPU
+        # node decides.  True: the side-stream form (tested identical on 2-3 ranks and through RCCL).
+        self.overlap_exchange = False
+        self._side_ch = None
 
     def add_shard(self, x) -> None:
         """Append rows to THIS rank's shard, then agree on the global id offsets (collective)."""
@@ -644,10 +691,11 @@ class ShardedFlatIP:
             chunks = self.group_chunks()
             if isinstance(self.local, FlatIPIndex):
                 _reserve_group_memory(self.local, k, self.ntotal, chunks)
+            side = self._side()
             for res in _pipeline(groups, lambda j, g: _gtau_enqueue_group(
                     self.local, g, k, self.ntotal, self.offset, self._all_gather, to_host, stats=self.stats,
                     all_reduce_sum=lambda t: comm.all_reduce_sum_(t, self.group), chunks=chunks,
-                    world=self.world), fin):
+                    world=self.world, side=side), fin):
                 yield from res
             return
         for r in _pipeline(batches, lambda j, q: self._enqueue(q, k, to_host), self._finish):
@@ -670,6 +718,21 @@ class ShardedFlatIP:
     def _all_gather(self, t: torch.Tensor) -> torch.Tensor:
         """[world, *t.shape] all-gather (RCCL on device; host-staged under gloo, comm.py)."""
         return comm.all_gather_stacked(t, self.group)
+
+    def _side(self):
+        """The exchange side channel (_SideChannel), created on first use -- every rank runs the same
+        searches, so every rank creates the second communicator at the same point.  None on a CPU shard,
+        for a sub-group index (a new communicator needs every rank of the job) or with overlap_exchange
+        off."""
+        if not (self.overlap_exchange and self._multi() and self.local.device.type == "cuda"):
+            return None
+        if self.group is not None and self.group != self.dist.group.WORLD:
+            return None
+        if self._side_ch is None:
+            xg = self.dist.new_group(ranks=list(range(self.dist.get_world_size())),
+                                     backend=self.dist.get_backend())
+            self._side_ch = _SideChannel(torch.cuda.Stream(self.local.device), xg)
+        return self._side_ch
 
     def _multi(self) -> bool:
         """Exchange through collectives: world > 1 (or the test-only world-1 forcing, comm.py)."""

@@ -154,6 +154,16 @@ def _w_sharded(rank, world, dev, case):
                 qd = to_dev_bf16(q, dev)
                 res = idx.search_batches([qd[a: a + 5] for a in range(0, q.shape[0], 5)], k)
                 torch.cuda.synchronize()
+                if proto == "global_tau":
+                    # round 6: the groups' exchange on a side stream + second communicator gives the same
+                    # answer as the default one-stream form
+                    idx.overlap_exchange = True
+                    res1 = idx.search_batches([qd[a: a + 5] for a in range(0, q.shape[0], 5)], k)
+                    torch.cuda.synchronize()
+                    idx.overlap_exchange = False
+                    assert idx._side_ch is not None
+                    for (s0, i0), (s1, i1) in zip(res, res1):
+                        assert torch.equal(i0, i1) and torch.equal(s0, s1)
             finally:
                 srch.GROUP_QUERIES, srch.GROUP_CHUNK_ROWS = saved
             np.testing.assert_array_equal(torch.cat([r[1] for r in res]).cpu().numpy(), ei)

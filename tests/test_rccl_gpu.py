@@ -68,6 +68,7 @@ def _worker(port, out_q):
         res = {}
         for proto in ("global_tau", "per_shard"):
             idx = ShardedFlatIP(768, device=dev, protocol=proto)
+            idx.overlap_exchange = True   # the side-stream exchange through its own RCCL communicator
             idx.add_shard(to_dev_bf16(p, dev))
             assert idx._multi() and idx.offset == 0 and idx.ntotal == p.shape[0]
             qd = to_dev_bf16(q, dev)
@@ -84,6 +85,8 @@ def _worker(port, out_q):
                 srch.GROUP_QUERIES = saved
             np.testing.assert_array_equal(torch.cat([r[1] for r in out]).cpu().numpy(), ei)
             np.testing.assert_array_equal(torch.cat([r[0] for r in out]).cpu().numpy(), es)
+            if proto == "global_tau":   # the groups' exchange ran on the side stream's own RCCL communicator
+                assert idx._side_ch is not None and idx._side_ch.group is not None
             res[proto] = idx.fallbacks
 
         # comm helpers on device tensors
