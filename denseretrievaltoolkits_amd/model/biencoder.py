@@ -117,11 +117,19 @@ class DRModel(nn.Module):
             p_reps = self.dist_gather_tensor(p_reps)
         n_passages = self.data_args.train_n_passages
         scale = float(self.world_size) if (self.training and x_dev) else 1.0
+        from ..score_ce import score_ce
         if q_reps.is_cuda:
-            from ..score_ce import score_ce
             loss, scores = score_ce(q_reps, p_reps, n_passages, scale)
+        elif torch.cuda.is_available():
+            # a tower on the CPU (the reference scores on any device, biencoder.py:107-116): the reps go to
+            # the GPU for the fused HIP op and the loss / scores come back; autograd carries the gradients
+            # across both copies to the CPU tower
+            dev = torch.device("cuda", torch.cuda.current_device())
+            loss, scores = score_ce(q_reps.to(dev), p_reps.to(dev), n_passages, scale)
+            loss, scores = loss.to(q_reps.device), scores.to(q_reps.device)
         else:
-            raise ValueError("DRModel.forward: the MI355X build computes the score matrix on the GPU only")
+            raise ValueError("DRModel.forward: the MI355X build computes the score matrix on the GPU only "
+                             "(no GPU visible)")
         return DROutput(loss=loss, scores=scores, q_reps=q_reps, p_reps=p_reps)
 
     # ------------------------------------------------------------------
