@@ -423,12 +423,23 @@ class FlatIPIndex:
         return s, i
 
     wide_resolved = 0   # queries put in the canonical order by the wide resolve (massive near-ties)
+    range_resolved = 0  # ... of them, windows wider than 65,536 rows (kernels.exact_by_ranges)
 
     def _wide(self, qd, k, off, s, i, st, stats, nwide=None) -> int:
         """Wide resolve (kernels.resolve_wide) of the queries with status 2; returns how many it resolved."""
         if stats is None or nwide == 0:
             return 0
         n = kernels.resolve_wide(qd, self.rows, k, off, s, i, st, stats, n_wide=nwide)
+        if n < (nwide if nwide is not None else n + 1):
+            # windows wider than the wide resolve's 65,536 rows (round 6): exact top-k range by range
+            left = torch.nonzero((st & 3) == 2).flatten()
+            if left.numel():
+                s2, i2 = kernels.exact_by_ranges(qd.index_select(0, left).contiguous(), self.rows, k, off, stats)
+                s.index_copy_(0, left, s2)
+                i.index_copy_(0, left, i2)
+                st.index_fill_(0, left, 0)
+                n += int(left.numel())
+                self.range_resolved += int(left.numel())
         self.wide_resolved += n
         return n
 

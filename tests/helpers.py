@@ -12,6 +12,26 @@ def gauss_bf16(rng, shape):
     return bf16_round(rng.standard_normal(shape).astype(np.float32))
 
 
+def massive_near_ties(n, d, seed=0, nq=2, special=40):
+    """(q [nq, d], p [n, d]) bf16-valued fp32 arrays whose n rows share one positive base row (scores
+    B ~ 360, fp32 spacing 2^-15) and differ only in a last element below 2^-16, which q's last element (1)
+    adds exactly: every exact score is B + t_r, all n inside one fp32 error bound of each other, so a
+    near-tie window holds every row (more than the 65,536 the wide resolve / large-k collection take when
+    n > 65536).  ``special`` random rows carry the largest tails j 2^-22 (j = 1..special, larger j on a
+    smaller id NOT guaranteed), the others random tails below 2^-24: the exact top-k differs from any
+    id or fp32 order."""
+    from oracle import search_oracle as orc
+    rng = np.random.default_rng(seed)
+    base = orc.bf16_round(rng.integers(1, 4, size=(1, d)).astype(np.float64) + 0.5)
+    p = np.repeat(base, n, axis=0)
+    p[:, -1] = orc.bf16_round(rng.random(n) * 2.0 ** -24)
+    rows = rng.choice(n, size=special, replace=False)
+    p[rows, -1] = np.arange(1, special + 1) * 2.0 ** -22
+    q = orc.bf16_round(rng.integers(1, 4, size=(nq, d)).astype(np.float64) + 0.25)
+    q[:, -1] = 1.0
+    return q.astype(np.float32), p.astype(np.float32)
+
+
 def to_dev_bf16(x, device):
     import torch
     from oracle.search_oracle import bf16_bits

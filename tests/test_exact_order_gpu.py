@@ -222,21 +222,20 @@ def test_exact_order_window_wider_than_list_resolved_wide(dev):
     assert (st.cpu().numpy() == 0).all()
 
 
-def test_exact_order_window_beyond_wide_cap_keeps_fp32_order(dev):
-    """More tied rows than the wide resolve can rank (65536 per query): status bit 1 stays and the
-    certified fp32 top-k is kept in the fp32 order (here ascending id, all scores equal), counted by
-    the index."""
+def test_exact_order_window_beyond_wide_cap(dev):
+    """More near-tied rows than the wide resolve can rank (65536 per query): round 6 takes the range-by-range
+    exact top-k (kernels.exact_by_ranges) for those queries -- ids and scores == the fp64 order, nothing left
+    in the fp32 order.  The rows differ only below the fp32 resolution of their scores (helpers.massive_near_ties)."""
+    from helpers import massive_near_ties
     from denseretrievaltoolkits_amd import search as srch
-    rng = np.random.default_rng(9)
-    n, d, k = 70000, 64, 10
-    row = orc.bf16_round(int_bf16(rng, (1, d), -3, 3) + 0.5)
-    p = np.repeat(row, n, axis=0)
-    q = orc.bf16_round(int_bf16(rng, (2, d), -3, 3) + 0.25)
+    q, p = massive_near_ties(70000, 64, seed=9)
+    k = 10
     idx = srch.FlatIPIndex.from_rows(to_dev_bf16(p, dev))
     s, i = idx.search(q, k)
-    es, ei = orc.ip_topk(q, p, k)
+    es, ei = orc.ip_topk(q, p, k, dtype=np.float64, out_dtype=np.float64)
     np.testing.assert_array_equal(i, ei)
-    assert idx.order_uncertified == 2 and idx.wide_resolved == 0
+    np.testing.assert_array_equal(s, es.astype(np.float32))
+    assert idx.order_uncertified == 0 and idx.wide_resolved == 2 and idx.range_resolved == 2
 
 
 def test_flat_index_exact_order_default_and_counter(dev):

@@ -83,12 +83,15 @@ def test_large_k_limits(dev):
     p = torch.zeros((10, 64), dtype=torch.bfloat16, device=dev)
     with pytest.raises(ValueError):
         kernels.ip_topk(q, p, 32769)
-    # 70,000 identical rows: every one within the error of the threshold -> more than the 65,536 a
-    # query may collect -> an error, never a silently wrong order
-    p = torch.ones((70000, 64), dtype=torch.bfloat16, device=dev)
-    q = torch.ones((1, 64), dtype=torch.bfloat16, device=dev)
-    with pytest.raises(RuntimeError, match="65536"):
-        kernels.ip_topk(q, p, 3000)
+    # 70,000 rows inside one fp32 error bound of each other: more than the 65,536 a query may collect ->
+    # round 6: the range-by-range exact top-k (kernels.exact_by_ranges) gives the fp64 order anyway
+    from helpers import massive_near_ties
+    qn, pn = massive_near_ties(70000, 64, seed=4)
+    s, i, st = kernels.ip_topk(torch.from_numpy(qn).to(dev).bfloat16(), torch.from_numpy(pn).to(dev).bfloat16(), 3000)
+    es, ei = orc.ip_topk(qn, pn, 3000, dtype=np.float64, out_dtype=np.float64)
+    np.testing.assert_array_equal(i.cpu().numpy(), ei)
+    np.testing.assert_array_equal(s.cpu().numpy(), es.astype(np.float32))
+    assert (st.cpu().numpy() == 0).all()
 
 
 def test_flat_index_large_k_batches(dev):
