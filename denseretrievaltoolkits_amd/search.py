@@ -684,8 +684,8 @@ class ShardedFlatIP:
             groups = [[self.local._queries(q) for q in g] for g in _groups(batches)]
 
             def redo(q):
-                if self.stats is not None:   # the per-shard redo merges by fp32 scores
-                    self.order_uncertified += int(q.shape[0])
+                if self.stats is not None:   # canonical order: exact keys per shard, merged by key (round 6)
+                    return self._search_large(q, k)
                 return self._finish(("pshard", q, k) + self._per_shard_enqueue(q, k))
 
             def fin(pend):
@@ -816,10 +816,12 @@ class ShardedFlatIP:
                 self.order_uncertified += _order_uncertified(h)
                 return s, i
             self.fallbacks += 1
-            if self.stats is not None:   # the per-shard redo merges by fp32 scores
-                self.order_uncertified += int(q.shape[0])
             if isinstance(self.local, FlatIPIndex):   # full exchange lists from now on (see search_batches_iter)
                 self.local.exchange_capped = False
+            if self.stats is not None:
+                # canonical order (round 6): every shard's exact top-k keys merged by key -- the redo stays
+                # in the fp64 order instead of merging the per-shard lists by fp32 scores
+                return self._search_large(q, k)
             pend = ("pshard", q, k) + self._per_shard_enqueue(q, k)
         _, q, k, ms, mi, h, ev, s, i, st = pend
         if _status_failed(h, ev) == 0:

@@ -172,6 +172,7 @@ def _w_sharded(rank, world, dev, case):
             if case != "gauss":
                 np.testing.assert_array_equal(torch.cat([r[0] for r in res]).cpu().numpy(), es)
         out[proto + "_batched"] = idx.fallbacks - fb0
+        out[proto + "_order_uncertified"] = idx.order_uncertified
     return out
 
 
@@ -229,8 +230,10 @@ def test_sharded_search_multiprocess_k_beyond_2048(data):
 
 def test_sharded_search_multiprocess_fallback():
     res = _spawn(_w_sharded, 2, "ties")
-    # one batch of 9 queries; batched: batches of 5 + 4 in one group, both redone exactly
+    # one batch of 9 queries; batched: batches of 5 + 4 in one group, both redone exactly -- round 6: the
+    # redo merges every shard's exact keys, so no query is left in the fp32 order
     assert all(v["global_tau"] == 1 and v["global_tau_batched"] == 2 for v in res.values()), res
+    assert all(v["global_tau_order_uncertified"] == 0 for v in res.values()), res
 
 
 # ---------------------------------------------------------------------------
