@@ -655,6 +655,10 @@ __device__ __forceinline__ void pp_epilogue(const GemmArgs& a, f32x4 (&acc)[8][4
 // slice in a private LDS region (row-per-lane 8-B pieces in, 16-B row-contiguous
 // pieces out, 16-B chunks XOR-swizzled by row), then writes whole 128-B (bf16) /
 // 256-B (fp32) row segments.  Needs a full tile in n; rows are masked.
+// bf16 outputs leave as non-temporal stores (round 6): every CU's 128 KiB tile per round is an
+// XCD's whole 4 MB L2, and plain stores evicted the X / W panels the next round's tiles re-read
+// (encode 38.6-39.0k -> 39.6-39.8k passages/s in three alternating rounds, FFN2 -8 %, FFN1 -3 %,
+// outputs bit-identical; profiles/r06v/).
 template <bool OUT_BF16, int EPI>
 __device__ __forceinline__ void pp_epilogue_lds(const GemmArgs& a, f32x4 (&acc)[8][4], int64_t m0, int64_t n0,
                                                 int grp, int wn, int fr, int fc, char* lds_wave, int lane) {
@@ -695,7 +699,7 @@ __device__ __forceinline__ void pp_epilogue_lds(const GemmArgs& a, f32x4 (&acc)[
         const int r = p * 8 + (lane >> 3);
         const bf16x8 v = *(const bf16x8*)(lds_wave + r * 128 + ((c ^ (r & 7)) << 4));
         const int64_t row = m0 + grp * 128 + r;
-        if (row < a.m) *(bf16x8*)(dst + row * a.ldc + colw + c * 8) = v;
+        if (row < a.m) __builtin_nontemporal_store(v, (bf16x8*)(dst + row * a.ldc + colw + c * 8));
       }
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     }
@@ -761,7 +765,7 @@ __device__ __forceinline__ void pp_epilogue_lds(const GemmArgs& a, f32x4 (&acc)[
             bf16x8 o;
 #pragma unroll
             for (int u = 0; u < 8; ++u) o[u] = (__bf16)v[u];
-            *(bf16x8*)((__bf16*)a.C + row * a.ldc + colw + c8 * 8) = o;
+            __builtin_nontemporal_store(o, (bf16x8*)((__bf16*)a.C + row * a.ldc + colw + c8 * 8));
             if (a.csum) {
 #pragma unroll
               for (int u = 0; u < 8; ++u) cs[u] += (float)o[u];
