@@ -260,8 +260,11 @@ void attention_fwd_kernel(AttnArgs a) {
       kv[u] = u32x4{0u, 0u, 0u, 0u};
       vv[u] = u32x4{0u, 0u, 0u, 0u};
       if (key < L) {
-        kv[u] = *(const u32x4*)(Kg + (int64_t)key * ld + c8 * 8);
-        vv[u] = *(const u32x4*)(Vg + (int64_t)key * ld + c8 * 8);
+        // non-temporal: K / V rows are read once per (sequence, head) -- kept out of L2 for the
+        // GEMM panels and the ctx rows the next projection reads (round 6: encode +0.4-0.8 % in three
+        // alternating rounds, profiles/r06y/)
+        kv[u] = __builtin_nontemporal_load((const u32x4*)(Kg + (int64_t)key * ld + c8 * 8));
+        vv[u] = __builtin_nontemporal_load((const u32x4*)(Vg + (int64_t)key * ld + c8 * 8));
       }
     }
 #pragma unroll
