@@ -151,21 +151,61 @@ __global__ __launch_bounds__(256) void layernorm_f32_kernel(const float* X, int6
 
 // Same LayerNorm over bf16 pre-LN sums (the encoder's default: the GEMM epilogue
 // adds bias + residual in fp32 and rounds once, halving the bytes of both sides).
+// Round 6: one round of work-groups, each wave normalising rows t, t + waves, ... with gamma / beta
+// held in registers (loaded once per wave instead of once per row: 2 x EPL / 4 16-B loads per row
+// were twice the row's own loads through the vector memory pipe) and the next row's loads issued
+// before the current row's reductions.  Same per-row arithmetic (ln_row_gb): bit-identical.
 template <int EPL>
 __global__ __launch_bounds__(256) void layernorm_bf16_kernel(const __bf16* X, int64_t M, int H, const float* gamma,
                                                              const float* beta, float eps, __bf16* out) {
   const int lane = threadIdx.x & 63;
-  const int64_t t = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
-  if (t >= M) return;
-  const __bf16* xr = X + t * H;
-  float x[EPL];
+  const int64_t t0 = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int64_t nw = (int64_t)gridDim.x * 4;
+  if (t0 >= M) return;
+  float g[EPL], b[EPL];
 #pragma unroll
   for (int e4 = 0; e4 < EPL / 4; ++e4) {
-    const bf16x4 a = *(const bf16x4*)(xr + e4 * 256 + lane * 4);
+    const f32x4 gv = *(const f32x4*)(gamma + e4 * 256 + lane * 4);
+    const f32x4 bv = *(const f32x4*)(beta + e4 * 256 + lane * 4);
 #pragma unroll
-    for (int u = 0; u < 4; ++u) x[e4 * 4 + u] = (float)a[u];
+    for (int u = 0; u < 4; ++u) {
+      g[e4 * 4 + u] = gv[u];
+      b[e4 * 4 + u] = bv[u];
+    }
   }
-  ln_row<EPL>(x, gamma, beta, eps, lane, H, out + t * H);
+  bf16x4 cur[EPL / 4];
+#pragma unroll
+  for (int e4 = 0; e4 < EPL / 4; ++e4) cur[e4] = *(const bf16x4*)(X + t0 * H + e4 * 256 + lane * 4);
+  for (int64_t t = t0; t < M; t += nw) {
+    const int64_t tn = t + nw;
+    bf16x4 nxt[EPL / 4];
+    if (tn < M) {
+#pragma unroll
+      for (int e4 = 0; e4 < EPL / 4; ++e4) nxt[e4] = *(const bf16x4*)(X + tn * H + e4 * 256 + lane * 4);
+    }
+    float x[EPL];
+#pragma unroll
+    for (int e4 = 0; e4 < EPL / 4; ++e4)
+#pragma unroll
+      for (int u = 0; u < 4; ++u) x[e4 * 4 + u] = (float)cur[e4][u];
+    ln_row_gb<EPL>(x, g, b, eps, lane, H, out + t * H);
+#pragma unroll
+    for (int e4 = 0; e4 < EPL / 4; ++e4) cur[e4] = nxt[e4];
+  }
+}
+
+// Work-groups of the row-looping LayerNorm: 8 per CU (32 waves), at most one per 4 rows.
+static unsigned ln_rows_grid(int64_t M) {
+  static int cus = 0;
+  if (cus == 0) {
+    int dev = 0, v = 0;
+    cus = (hipGetDevice(&dev) == hipSuccess &&
+           hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess && v > 0)
+              ? v
+              : 256;
+  }
+  const int64_t need = (M + 3) / 4, cap = (int64_t)cus * 8;
+  return (unsigned)(need < cap ? need : cap);
 }
 
 // ---------------------------------------------------------------------------
@@ -636,7 +676,7 @@ int drt_layernorm_bf16(const void* X, int64_t M, int32_t H, const float* gamma, 
   hipStream_t s = (hipStream_t)stream;
   const __bf16* x = (const __bf16*)X;
   __bf16* o = (__bf16*)out;
-  dim3 grid((unsigned)((M + 3) / 4));
+  dim3 grid(ln_rows_grid(M));
   switch (H / 64) {
     case 4: hipLaunchKernelGGL(layernorm_bf16_kernel<4>, grid, dim3(256), 0, s, x, M, H, gamma, beta, eps, o); break;
     case 8: hipLaunchKernelGGL(layernorm_bf16_kernel<8>, grid, dim3(256), 0, s, x, M, H, gamma, beta, eps, o); break;

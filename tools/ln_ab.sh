@@ -1,0 +1,8 @@
+set -u
+mkdir -p gpurun_out
+for r in 1 2; do
+  for v in prod lnold; do
+    if [ $v = prod ]; then L=denseretrievaltoolkits_amd/libdrt_hip.so; else L=denseretrievaltoolkits_amd/variants/libdrt_hip.$v.so; fi
+    DRT_LIB=$L timeout -k 10 200 python3 tools/ln_ab.py 2>>gpurun_out/ln_ab.err | grep '^{' | tee -a gpurun_out/ln_ab.txt || exit 1
+  done
+done
