@@ -129,7 +129,9 @@ def test_gemm_plans_vs_torch(dev, M, N, K, flags):
     torch.testing.assert_close(out.float(), ref, **tol)
 
 
-@pytest.mark.parametrize("M,H", [(1, 768), (1003, 768), (64, 256), (37, 1024)])
+# M > 8192 (a round of 2048 four-wave work-groups): waves normalise several rows each (grid-stride loop
+# with the next row prefetched; 20001 / 65537 leave a ragged last pass)
+@pytest.mark.parametrize("M,H", [(1, 768), (1003, 768), (64, 256), (37, 1024), (20001, 768), (65537, 512)])
 def test_layernorm_bf16_and_f32_inputs_vs_torch(dev, M, H):
     """drt_layernorm_bf16 (the encoder's default pre-LN sums) and drt_layernorm_f32_bf16 vs torch fp32 LN."""
     import torch
