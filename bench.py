@@ -283,6 +283,41 @@ def cpu_baseline(args, shard, queries, gpu_result):
     }
 
 
+def union_parity(args, queries, gpu_result, device, nq=8):
+    """N > 1 (rank 0, untimed, after the timed region): the first `nq` queries of the first timed batch
+    against the fp64 oracle over the UNION of the shards -- the n_corpus rows regenerated block by block
+    from the same per-block seeds every rank generated its shard from (gen_shard) -- so the sharded
+    protocol's merged top-k is checked at full size like the N = 1 line's cpu_baseline parity."""
+    import numpy as np
+    import torch
+    from oracle.search_oracle import ip_topk, merge_topk
+    q = queries[:nq].float().cpu().numpy()
+    n, d, B, chunk = args.n_corpus, queries.shape[1], CORPUS_BLOCK_ROWS, 262144
+    g = torch.Generator(device=device)
+    best_s = best_i = None
+    t0 = time.perf_counter()
+    for b in range(-(-n // B)):
+        a0, b0 = b * B, min(n, (b + 1) * B)
+        g.manual_seed(corpus_block_seed(b))
+        blk = torch.randn((b0 - a0, d), generator=g, device=device, dtype=torch.float32).to(torch.bfloat16)
+        for c in range(0, b0 - a0, chunk):
+            pc = blk[c: c + chunk].double().cpu().numpy()
+            cs, ci = ip_topk(q, pc, args.k, id_offset=a0 + c, chunk=pc.shape[0], dtype=np.float64,
+                             out_dtype=np.float64)
+            if best_s is None:
+                best_s, best_i = cs, ci
+            else:
+                best_s, best_i = merge_topk(np.stack([best_s, cs]), np.stack([best_i, ci]), args.k)
+        del blk
+    gs, gi = gpu_result
+    gs, gi = gs[:nq].cpu().numpy(), gi[:nq].cpu().numpy()
+    return {"queries": nq, "rows": n, "ids_equal_frac": round(float((gi == best_i).mean()), 6),
+            "n_mismatch": int((gi != best_i).sum()),
+            "max_abs_score_diff": float(np.abs(gs.astype(np.float64) - best_s).max()),
+            "check_s": round(time.perf_counter() - t0, 1),
+            "what": "merged sharded top-k vs oracle/search_oracle.ip_topk in fp64 over the union of the shards"}
+
+
 def encode_cpu_baseline(batch=32, L=128, min_seconds=10.0):
     """torch-CPU fp32 DRModel.encode (the reference's arithmetic: HF BertModel fp32 + [CLS]
     pooling through this build's DRModelForInference, which is pinned to the reference's
@@ -599,6 +634,8 @@ def main():
         out["global_tau_fallback_batches"] = int(n_fallback)
         if world == 1 and not args.no_cpu_baseline:
             out["cpu_baseline"] = cpu_baseline(args, shard, queries[args.warmup], results[0])
+        elif world > 1 and not args.no_cpu_baseline:
+            out["parity_union_fp64"] = union_parity(args, queries[args.warmup], results[0], dev)
     # the search leg's 15 GB corpus, index and results leave HBM before the model legs (the training
     # legs' torch baselines reserve ~140 GB)
     del shard, queries, results, index, local_index
