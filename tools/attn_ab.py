@@ -21,7 +21,10 @@ def main(reps=50):
     H = heads * dh
     res = {"lib": os.path.basename(os.environ.get("DRT_LIB", "product"))}
     g = torch.Generator(device=dev).manual_seed(1)
-    for (B, L, ragged) in ((256, 128, False), (256, 128, True), (128, 32, False), (64, 100, True)):
+    shapes = ((256, 128, False), (256, 128, True), (128, 32, False), (64, 100, True))
+    if os.environ.get("ATTN_SHAPES") == "rerank":
+        shapes = ((500, 160, False), (625, 128, False), (500, 160, True))
+    for (B, L, ragged) in shapes:
         qkv = (torch.randn((B * L, 3 * H), generator=g, device=dev) * 2).to(torch.bfloat16)
         mask = torch.ones((B, L), dtype=torch.int64, device=dev)
         if ragged:
